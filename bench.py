@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Benchmark: resolved transactions/s of the MI355X conflict-resolution engine.
+
+Workload (BASELINE.json configs[1], "C2"): a single-MI355X resolver with 5000-transaction commit
+batches, 5 read + 2 write conflict ranges per transaction, 16-byte uniform keys, over a
+5M-boundary MVCC history prefilled across a 5e6-version window.  A step is one
+ConflictBatch::detectConflicts pass (SkipList.cpp:844-890) over one batch, inputs already resident
+in HBM (uploaded before the timed region).
+
+N > 1 (torchrun, one rank per GPU): the key space is range-sharded across ranks like FDB's
+multi-resolver split (CommitProxyServer.actor.cpp:147-174).  Every rank builds the same global batch
+of N x 5000 transactions, keeps its routed sub-batch, resolves it on its GPU, and the verdicts are
+combined by an RCCL all-reduce MAX of conflict bytes (= proxy min over resolvers,
+CommitProxyServer.actor.cpp:772-777).  Weak scaling: per-GPU work is fixed.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--txns", type=int, default=5000)
+    ap.add_argument("--history", type=int, default=5_000_000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--gc-interval", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def shard_history(p, seed, rank, world, start_version):
+    """Prefill: p.history random 16-byte boundaries inside this rank's key range."""
+    from foundationdb_amd.workloads import c2_history
+
+    kb, ko, vers = c2_history(p, seed=seed * 1000 + rank, start_version=start_version)
+    if world > 1:
+        keys = kb.reshape(-1, 16).copy()
+        lo = (rank * 256) // world
+        hi = ((rank + 1) * 256) // world
+        keys[:, 0] = lo + (keys[:, 0].astype(np.int64) * (hi - lo) // 256).astype(np.uint8)
+        hi64 = keys[:, :8].copy().view(">u8").reshape(-1)
+        lo64 = keys[:, 8:].copy().view(">u8").reshape(-1)
+        order = np.lexsort((lo64, hi64))
+        keys = keys[order]
+        keep = np.ones(len(keys), bool)
+        keep[1:] = (keys[1:] != keys[:-1]).any(axis=1)
+        keys = keys[keep]
+        vers = vers[: len(keys)]
+        kb = keys.reshape(-1)
+        ko = np.arange(len(keys) + 1, dtype=np.int64) * 16
+    return kb, ko, vers
+
+
+def make_batches(args, p, n_batches, world, start_version):
+    """Global batches (identical on every rank) with their (now, newOldest)."""
+    from foundationdb_amd import workloads as W
+
+    rng = np.random.default_rng(args.seed)
+    zipf = W.ZipfGenerator(1_000_000, 0.99) if args.workload == "c3" else None
+    gp = W.C2Params(txns=args.txns * world, history=p.history)
+    out = []
+    now = start_version
+    for _ in range(n_batches):
+        now += p.version_step
+        pb = W.c3_batch(gp, rng, now, zipf) if zipf else W.c2_batch(gp, rng, now)
+        out.append((pb, now, now - p.window))
+    return out
+
+
+def cpu_baseline(args, p, kb, ko, vers, batches):
+    """Skip-list restatement of the reference (oracle/skiplist_baseline.cpp), single thread,
+    over a bounded sample of the same workload."""
+    from oracle import oracle
+
+    oracle.build()
+    sl = oracle.SkipListBaseline()
+    t0 = time.time()
+    sl.load_history(kb, ko, vers)
+    load_s = time.time() - t0
+    done_txn = 0
+    done_batches = 0
+    spent = 0.0
+    for pb, now, no in batches:
+        t = time.perf_counter()
+        sl.detect(pb, now, no)
+        spent += time.perf_counter() - t
+        done_txn += pb.n_txn
+        done_batches += 1
+        if spent >= args.cpu_seconds:
+            break
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": done_txn / spent if spent > 0 else None,
+        "unit": "txns/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{done_batches} C2 batches x {args.txns} txns on a {len(vers)}-boundary history "
+        f"({spent:.1f}s CPU, load {load_s:.1f}s), skip-list restatement oracle/skiplist_baseline.cpp, "
+        f"1 thread on {cpu}",
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    from foundationdb_amd import build as fbuild
+
+    fbuild.build()
+    from foundationdb_amd import conflict_set as C
+    from foundationdb_amd import workloads as W
+    from foundationdb_amd.sharding import KeyRangeSharding
+
+    p = W.C2Params(txns=args.txns, history=args.history)
+    start_version = 10_000_000
+    t0 = time.time()
+    kb, ko, vers = shard_history(p, args.seed, rank, world, start_version)
+    total = args.warmup + args.steps
+    gbatches = make_batches(args, p, total, world, start_version)
+    sharding = KeyRangeSharding.uniform(world) if world > 1 else None
+    routed = [sharding.route(pb)[rank] for pb, _, _ in gbatches] if sharding else None
+    log(f"[rank {rank}] generated history {len(vers)} + {total} batches in {time.time() - t0:.1f}s")
+
+    cs = C.ConflictSet(local)
+    cs.set_gc_interval(args.gc_interval)
+    cs.load_history(kb, ko, vers, 0)
+    mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
+    maxT = max(b.n_txn for b in mine)
+    maxR = max(b.n_reads for b in mine)
+    maxW = max(b.n_writes for b in mine)
+    cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, 64 * 1024 * 1024, maxT, maxR, maxW)
+    objs = []
+    for b in mine:
+        o = C.ConflictBatch(cs)
+        o.add_packed(b)
+        o.upload()
+        objs.append(o)
+    torch.cuda.synchronize()
+
+    def run(lo, hi, combine):
+        for i in range(lo, hi):
+            _, now, no = gbatches[i]
+            objs[i].detect_async(now, no)
+        for i in range(lo, hi):
+            v = objs[i].wait()
+            if combine:
+                T = gbatches[i][0].n_txn
+                c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to("cuda")
+                dist.all_reduce(c, op=dist.ReduceOp.MAX)
+
+    run(0, args.warmup, dist is not None)
+    torch.cuda.synchronize()
+    cs.reset_stats()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    run(args.warmup, total, dist is not None)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = cs.stats()
+    gtxn = sum(gbatches[i][0].n_txn for i in range(args.warmup, total))
+    granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(args.warmup, total))
+    hist_end = cs.history_size()
+
+    launches = max(1, st["merge_launches"])
+    avg_ms = st["ms_merge_kernel"] / launches
+    bytes_per_launch = st["merge_bytes"] / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                traffic = json.load(f).get("k_merge_copy_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "resolved txns/sec (conflict ranges checked/sec) per batch; HBM GB/s vs peak",
+        "value": gtxn / elapsed,
+        "unit": "txns/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/int64 (byte keys, int64 versions)",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{args.workload.upper()}: {args.txns}-txn batches per GPU, 5R+2W ranges/txn, 16-byte "
+            f"uniform keys, {args.history}-boundary MVCC history per GPU (5e6-version window)",
+            "global_batch_txns": args.txns * world,
+            "parallelism": f"key-range shards x{world}" if world > 1 else "single resolver",
+            "gc_interval": args.gc_interval,
+        },
+        "conflict_ranges_per_s": granges / elapsed,
+        "history_boundaries_end": hist_end,
+        "phase_ms_per_batch": {
+            k: st[k] / max(1, st["batches"])
+            for k in ("ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_gc", "ms_total")
+        },
+        "roofline": {
+            "kernel": "k_merge_copy (history rewrite)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "avg_launch_ms": avg_ms,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, p, kb, ko, vers, gbatches[args.warmup :])
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    for o in objs:
+        o.close()
+    cs.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+// dkey.h — normalized key record shared by host packing and the gfx950 kernels.
+//
+// A key (unsigned byte string, memcmp-then-length order: SkipList.cpp:53-60,
+// flow/Arena.h:692-697) is held as its first 16 bytes, zero-padded, read as two
+// big-endian u64 words (integer order == byte order), its full length, and —
+// only when it is longer than 16 bytes — the offset of bytes [16, len) in a
+// tail arena.  Exactness: if the padded prefixes tie and either
+// key is <= 16 bytes, the shorter key is a prefix of the longer, so comparing
+// lengths decides; only when both exceed 16 bytes are the tails compared.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define FDB_HD __host__ __device__ __forceinline__
+#else
+#define FDB_HD inline
+#endif
+
+struct __attribute__((aligned(8))) DKey {
+    uint64_t hi, lo;  // big-endian words of the zero-padded 16-byte prefix
+    uint32_t len;     // full key length in bytes
+    uint32_t tail;    // offset of bytes [16, len) in the owning tail arena (len > 16)
+};
+static_assert(sizeof(DKey) == 24, "DKey is 24 bytes");
+
+// Sort item: a batch endpoint with its key (KeyInfo, SkipList.cpp:77-87).
+// meta = range_id << 3 | is_end << 2 | class, class as extra_ordering
+// (SkipList.cpp:89-91): read-end 0 < write-end 1 < write-begin 2 < read-begin 3.
+struct __attribute__((aligned(16))) SortItem {
+    uint64_t hi, lo;
+    uint32_t len, tail;
+    uint32_t meta, pad;
+};
+static_assert(sizeof(SortItem) == 32, "SortItem is 32 bytes");
+
+enum PointClass : uint32_t { kReadEnd = 0, kWriteEnd = 1, kWriteBegin = 2, kReadBegin = 3 };
+
+FDB_HD uint32_t item_class(uint32_t meta) { return meta & 3u; }
+FDB_HD uint32_t item_range(uint32_t meta) { return meta >> 3; }
+FDB_HD uint32_t item_is_end(uint32_t meta) { return (meta >> 2) & 1u; }
+
+// Compare the bytes of two tails [16, min(la, lb)) then lengths.
+FDB_HD int tail_cmp(const uint8_t* ta, uint32_t la, const uint8_t* tb, uint32_t lb) {
+    uint32_t n = (la < lb ? la : lb) - 16u;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t a = ta[i], b = tb[i];
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return (la > lb) - (la < lb);
+}
+
+// Full key order.  arenaA / arenaB are the tail arenas the two keys index.
+FDB_HD int key_cmp(uint64_t ahi, uint64_t alo, uint32_t alen, uint32_t atail, const uint8_t* arenaA,
+                   uint64_t bhi, uint64_t blo, uint32_t blen, uint32_t btail, const uint8_t* arenaB) {
+    if (ahi != bhi) return ahi < bhi ? -1 : 1;
+    if (alo != blo) return alo < blo ? -1 : 1;
+    if (alen > 16u && blen > 16u) return tail_cmp(arenaA + atail, alen, arenaB + btail, blen);
+    return (alen > blen) - (alen < blen);
+}
+
+FDB_HD int dkey_cmp(const DKey& a, const uint8_t* arenaA, const DKey& b, const uint8_t* arenaB) {
+    return key_cmp(a.hi, a.lo, a.len, a.tail, arenaA, b.hi, b.lo, b.len, b.tail, arenaB);
+}
+
+// KeyInfo::operator< (SkipList.cpp:114-128): key, then class.
+FDB_HD bool item_less(const SortItem& a, const SortItem& b, const uint8_t* arena) {
+    int c = key_cmp(a.hi, a.lo, a.len, a.tail, arena, b.hi, b.lo, b.len, b.tail, arena);
+    if (c) return c < 0;
+    return item_class(a.meta) < item_class(b.meta);
+}
+
+// Host-side normalization of a key into a DKey (prefix words + length); the caller
+// appends bytes [16, len) to its tail arena and fills `tail`.
+inline void dkey_prefix(const uint8_t* p, uint32_t len, uint64_t* hi, uint64_t* lo) {
+    uint8_t buf[16] = {0};
+    for (uint32_t i = 0; i < len && i < 16; i++) buf[i] = p[i];
+    uint64_t h = 0, l = 0;
+    for (int i = 0; i < 8; i++) h = (h << 8) | buf[i];
+    for (int i = 8; i < 16; i++) l = (l << 8) | buf[i];
+    *hi = h;
+    *lo = l;
+}

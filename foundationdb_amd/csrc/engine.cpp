@@ -1,0 +1,866 @@
+// engine.cpp — host side of the MI355X conflict-resolution engine and its C-ABI
+// (include/fdb_conflict_set.h).
+//
+// Mirrors the reference ConflictSet / ConflictBatch lifecycle (fdbserver/SkipList.cpp:730-890):
+// addTransaction packs each transaction's conflict ranges into flat SoA buffers of normalized
+// key prefixes plus a tail arena; detectConflicts uploads the batch with one pinned H2D copy,
+// enqueues the kernel pipeline on the set's stream, and copies back one verdict byte per
+// transaction.  No CPU fallback exists: without a usable HIP device every entry point fails.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <vector>
+
+#include "../../include/fdb_conflict_set.h"
+#include "engine.h"
+
+using namespace fdbcs;
+
+#define HIPOK(expr)                                                                                   \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess) {                                                                       \
+            fprintf(stderr, "fdbcs: %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(_e), __FILE__, \
+                    __LINE__);                                                                        \
+            return FDBCS_E_DEVICE;                                                                    \
+        }                                                                                             \
+    } while (0)
+
+namespace {
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Grow-only device allocation.
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return FDBCS_OK;
+        size_t want = std::max(bytes, cap + cap / 2);
+        want = align_up(want < 256 ? 256 : want, 256);
+        if (p) HIPOK(hipFree(p));
+        p = nullptr;
+        cap = 0;
+        HIPOK(hipMalloc(&p, want));
+        cap = want;
+        return FDBCS_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// Grow-only pinned host allocation.
+struct HBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return FDBCS_OK;
+        size_t want = align_up(std::max(bytes, cap + cap / 2), 4096);
+        if (p) HIPOK(hipHostFree(p));
+        p = nullptr;
+        cap = 0;
+        HIPOK(hipHostMalloc(&p, want, hipHostMallocDefault));
+        cap = want;
+        return FDBCS_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+enum Phase {
+    kPhStart, kPhUpload, kPhCheck, kPhSort, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge, kPhGc, kPhEnd,
+    kPhCount
+};
+
+}  // namespace
+
+struct fdbcs_batch;
+
+struct fdbcs_conflict_set {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
+    int64_t header_version = 0;  // SkipList(Version) header (SkipList.cpp:398-404)
+    int64_t max_written = 0;     // highest version present in the history
+    int gc_interval = 1;
+    int batches_since_gc = 0;
+    int64_t gc_applied = 0;
+
+    // history: two buffer sets (ping-pong) + range-max levels + tail arena
+    DBuf hkey[2], hlt[2], hver[2];
+    DBuf lvl[kMaxLevels];  // lvl[0] unused (aliases hver[cur])
+    DBuf htail;  // tail arena shared by both buffer sets (append-only, offsets stable)
+    int cur = 0;
+    int64_t hist_cap = 0;  // elements per buffer set
+    int64_t n_ub = 0;      // upper bound of live boundaries (exact after a wait)
+    int64_t tail_ub = 0;
+    int64_t tail_cap = 0;
+    DBuf scal;  // Scalars
+    // workspace
+    DBuf ws[40];
+    int64_t ws_T = -1, ws_R = -1, ws_W = -1;
+    Work work{};
+    int64_t edge_cap = 0;
+
+    int inflight = 0;
+    fdbcs_stats stats{};
+};
+
+struct fdbcs_batch {
+    fdbcs_conflict_set* cs = nullptr;
+    int report_enabled = 0;
+    int state = 0;  // 0 adding, 1 uploaded, 2 submitted, 3 done
+    // host staging (pageable)
+    std::vector<int64_t> snap;
+    std::vector<uint8_t> flags;
+    std::vector<int32_t> roff{0}, woff{0};
+    std::vector<int32_t> rowner, wowner;
+    std::vector<DKey> rkeys, wkeys;
+    std::vector<uint8_t> tail;
+    // device copy
+    DBuf dev;
+    HBuf pin_in;
+    BatchDev bd{};
+    size_t tail_bytes = 0;
+    // results
+    HBuf pin_out;
+    DBuf dverdict;
+    uint8_t* h_verdict = nullptr;
+    Scalars* h_scal = nullptr;
+    uint8_t* h_rconf = nullptr;
+    uint8_t* h_hist = nullptr;
+    int32_t* h_first = nullptr;
+    hipEvent_t ev[kPhCount] = {};
+    bool events_made = false;
+    bool gc_ran = false;
+    bool any_report = false;
+    std::vector<int32_t> conf_off, conf_idx;
+    int32_t n_committed = 0, n_too_old = 0;
+
+    int32_t T() const { return (int32_t)snap.size(); }
+    int32_t R() const { return roff.back(); }
+    int32_t W() const { return woff.back(); }
+};
+
+namespace {
+
+void add_key(fdbcs_batch* b, std::vector<DKey>& out, const uint8_t* p, int32_t len) {
+    DKey k;
+    dkey_prefix(p, (uint32_t)len, &k.hi, &k.lo);
+    k.len = (uint32_t)len;
+    k.tail = 0;
+    if (len > 16) {
+        k.tail = (uint32_t)b->tail.size();
+        b->tail.insert(b->tail.end(), p + 16, p + len);
+    }
+    out.push_back(k);
+}
+
+int cmp_bytes(const uint8_t* a, int32_t al, const uint8_t* b, int32_t bl) {
+    int c = memcmp(a, b, (size_t)std::min(al, bl));
+    if (c) return c;
+    return (al > bl) - (al < bl);
+}
+
+// Workspace sized for (T, R, W); edge capacity grows with R.
+int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
+    if (T <= cs->ws_T && R <= cs->ws_R && W <= cs->ws_W) return FDBCS_OK;
+    T = std::max<int64_t>(T, std::max<int64_t>(cs->ws_T, 1024));
+    R = std::max<int64_t>(R, std::max<int64_t>(cs->ws_R, 4096));
+    W = std::max<int64_t>(W, std::max<int64_t>(cs->ws_W, 4096));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    const int64_t E = 2 * (R + W);
+    int64_t edge_cap = std::max<int64_t>(16 * R, 1 << 22);
+    if (const char* env = getenv("FDBCS_EDGE_CAP")) edge_cap = std::max<int64_t>(1, atoll(env));  // testing knob
+    Work& w = cs->work;
+    int i = 0;
+    auto take = [&](size_t bytes, void** ptr) -> int {
+        int rc = cs->ws[i].ensure(bytes + 64);
+        if (rc) return rc;
+        *ptr = cs->ws[i].p;
+        i++;
+        return FDBCS_OK;
+    };
+#define TAKE(field, bytes) \
+    if (int rc = take((bytes), (void**)&w.field)) return rc
+    TAKE(hist_conf, T);
+    TAKE(rconf, R);
+    TAKE(status, T);
+    TAKE(first_conf, 4 * T);
+    TAKE(items[0], sizeof(SortItem) * E);
+    TAKE(items[1], sizeof(SortItem) * E);
+    TAKE(pos, 4 * E);
+    TAKE(pmeta, 4 * E);
+    TAKE(cnt_pair, 8 * (E + 1));
+    TAKE(wbpos, 4 * W);
+    TAKE(rbpos, 4 * R);
+    TAKE(ecnt_a, 4 * R);
+    TAKE(ecnt_b, 4 * R);
+    TAKE(eoff, 4 * (R + 1));
+    TAKE(ecur, 4 * R);
+    TAKE(edges, 4 * edge_cap);
+    TAKE(eptr, 4 * T);
+    TAKE(cov, 4 * E);
+    TAKE(mcs_bits, 8 * (E / 64 + 2));
+    TAKE(seg_b, 4 * (W + 1));
+    TAKE(seg_e, 4 * (W + 1));
+    TAKE(seg_lo, 8 * (W + 1));
+    TAKE(seg_hi, 8 * (W + 1));
+    TAKE(seg_rem, 8 * (W + 1));
+    TAKE(seg_ins, 8 * (W + 1));
+    TAKE(seg_tlen, 8 * (W + 1));
+    TAKE(seg_endins, W + 1);
+    TAKE(seg_vend, 8 * (W + 1));
+    TAKE(verdict, T);
+#undef TAKE
+    w.edge_cap = edge_cap;
+    cs->edge_cap = edge_cap;
+    cs->ws_T = T;
+    cs->ws_R = R;
+    cs->ws_W = W;
+    return FDBCS_OK;
+}
+
+int ensure_tile_cnt(fdbcs_conflict_set* cs, int64_t n) {
+    const int64_t tiles = (n + kGcTile - 1) / kGcTile + 1;
+    int rc = cs->ws[39].ensure(8 * tiles);
+    if (rc) return rc;
+    cs->work.tile_cnt = (int64_t*)cs->ws[39].p;
+    return FDBCS_OK;
+}
+
+Hist hist_of(fdbcs_conflict_set* cs, int k) {
+    Hist h;
+    h.key = (ulonglong2*)cs->hkey[k].p;
+    h.lt = (uint2*)cs->hlt[k].p;
+    h.ver = (int64_t*)cs->hver[k].p;
+    return h;
+}
+
+MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
+    MaxLevels m;
+    m.lvl[0] = (int64_t*)cs->hver[k].p;
+    for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->lvl[L].p;
+    return m;
+}
+
+// Read the exact history size/tail usage back (synchronizes the stream).
+int sync_sizes(fdbcs_conflict_set* cs) {
+    Scalars s;
+    HIPOK(hipMemcpyAsync(&s, cs->scal.p, sizeof(s), hipMemcpyDeviceToHost, cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    cs->n_ub = s.n;
+    cs->tail_ub = s.tail_used;
+    return FDBCS_OK;
+}
+
+// History capacity for `need` boundaries (copies the live history when growing).
+int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
+    if (need <= cs->hist_cap && tail_need <= cs->tail_cap) return FDBCS_OK;
+    int rc = sync_sizes(cs);
+    if (rc) return rc;
+    const int64_t n = cs->n_ub;
+    const int64_t tail_used = cs->tail_ub;
+    int64_t cap = std::max<int64_t>(need, cs->hist_cap);
+    cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
+    int64_t tcap = std::max<int64_t>(tail_need, cs->tail_cap);
+    tcap = std::max<int64_t>(tcap + tcap / 2, 1 << 16);
+    for (int k = 0; k < 2; k++) {
+        DBuf nk, nl, nv;
+        if ((rc = nk.ensure(16 * cap)) || (rc = nl.ensure(8 * cap)) || (rc = nv.ensure(8 * cap))) return rc;
+        if (k == cs->cur) {
+            if (n) {
+                HIPOK(hipMemcpyAsync(nk.p, cs->hkey[k].p, 16 * n, hipMemcpyDeviceToDevice, cs->stream));
+                HIPOK(hipMemcpyAsync(nl.p, cs->hlt[k].p, 8 * n, hipMemcpyDeviceToDevice, cs->stream));
+                HIPOK(hipMemcpyAsync(nv.p, cs->hver[k].p, 8 * n, hipMemcpyDeviceToDevice, cs->stream));
+            }
+        }
+        HIPOK(hipStreamSynchronize(cs->stream));
+        cs->hkey[k].release();
+        cs->hlt[k].release();
+        cs->hver[k].release();
+        cs->hkey[k] = nk;
+        cs->hlt[k] = nl;
+        cs->hver[k] = nv;
+    }
+    if (tcap > cs->tail_cap) {
+        DBuf nt;
+        if ((rc = nt.ensure(tcap))) return rc;
+        if (tail_used) HIPOK(hipMemcpyAsync(nt.p, cs->htail.p, tail_used, hipMemcpyDeviceToDevice, cs->stream));
+        HIPOK(hipStreamSynchronize(cs->stream));
+        cs->htail.release();
+        cs->htail = nt;
+    }
+    int64_t m = cap;
+    for (int L = 1; L < kMaxLevels; L++) {
+        m = (m + kFan - 1) / kFan + 1;
+        cs->lvl[L].release();
+        if ((rc = cs->lvl[L].ensure(8 * m))) return rc;
+    }
+    cs->hist_cap = cap;
+    cs->tail_cap = tcap;
+    // rebuild the range-max levels for the live history
+    MaxLevels lv = levels_of(cs, cs->cur);
+    launch_blockmax(cs->stream, lv, &((Scalars*)cs->scal.p)->n, std::max<int64_t>(n, 1));
+    HIPOK(hipGetLastError());
+    HIPOK(hipStreamSynchronize(cs->stream));
+    return ensure_tile_cnt(cs, cap);
+}
+
+int ensure_events(fdbcs_batch* b) {
+    if (b->events_made) return FDBCS_OK;
+    for (int i = 0; i < kPhCount; i++) HIPOK(hipEventCreate(&b->ev[i]));
+    b->events_made = true;
+    return FDBCS_OK;
+}
+
+int do_upload(fdbcs_batch* b) {
+    fdbcs_conflict_set* cs = b->cs;
+    const size_t T = b->T(), R = b->R(), W = b->W();
+    // layout: snap | roff | woff | rowner | wowner | keys | flags | tail
+    size_t off = 0;
+    const size_t o_snap = off;
+    off = align_up(off + 8 * T, 64);
+    const size_t o_roff = off;
+    off = align_up(off + 4 * (T + 1), 64);
+    const size_t o_woff = off;
+    off = align_up(off + 4 * (T + 1), 64);
+    const size_t o_rown = off;
+    off = align_up(off + 4 * R, 64);
+    const size_t o_wown = off;
+    off = align_up(off + 4 * W, 64);
+    const size_t o_keys = off;
+    off = align_up(off + sizeof(DKey) * 2 * (R + W), 64);
+    const size_t o_flags = off;
+    off = align_up(off + T, 64);
+    const size_t o_tail = off;
+    off = align_up(off + b->tail.size() + 16, 64);
+    int rc;
+    if ((rc = b->pin_in.ensure(off)) || (rc = b->dev.ensure(off))) return rc;
+    char* h = (char*)b->pin_in.p;
+    memcpy(h + o_snap, b->snap.data(), 8 * T);
+    memcpy(h + o_roff, b->roff.data(), 4 * (T + 1));
+    memcpy(h + o_woff, b->woff.data(), 4 * (T + 1));
+    if (R) memcpy(h + o_rown, b->rowner.data(), 4 * R);
+    if (W) memcpy(h + o_wown, b->wowner.data(), 4 * W);
+    if (R) memcpy(h + o_keys, b->rkeys.data(), sizeof(DKey) * 2 * R);
+    if (W) memcpy(h + o_keys + sizeof(DKey) * 2 * R, b->wkeys.data(), sizeof(DKey) * 2 * W);
+    if (T) memcpy(h + o_flags, b->flags.data(), T);
+    if (!b->tail.empty()) memcpy(h + o_tail, b->tail.data(), b->tail.size());
+    HIPOK(hipMemcpyAsync(b->dev.p, h, off, hipMemcpyHostToDevice, cs->stream));
+    char* d = (char*)b->dev.p;
+    b->bd.T = (int32_t)T;
+    b->bd.R = (int32_t)R;
+    b->bd.W = (int32_t)W;
+    b->bd.snap = (int64_t*)(d + o_snap);
+    b->bd.roff = (int32_t*)(d + o_roff);
+    b->bd.woff = (int32_t*)(d + o_woff);
+    b->bd.rowner = (int32_t*)(d + o_rown);
+    b->bd.wowner = (int32_t*)(d + o_wown);
+    b->bd.keys = (DKey*)(d + o_keys);
+    b->bd.flags = (uint8_t*)(d + o_flags);
+    b->bd.tail = (uint8_t*)(d + o_tail);
+    b->tail_bytes = b->tail.size();
+    b->state = 1;
+    return FDBCS_OK;
+}
+
+double ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+    return (double)ms;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fdbcs_strerror(int s) {
+    switch (s) {
+        case FDBCS_OK: return "ok";
+        case FDBCS_E_INVALID: return "invalid argument";
+        case FDBCS_E_DEVICE: return "HIP device error";
+        case FDBCS_E_NOMEM: return "out of memory";
+        case FDBCS_E_VERSION: return "version below the history's newest version";
+        case FDBCS_E_STATE: return "call out of order";
+        case FDBCS_E_NODEVICE: return "no HIP device";
+        default: return "unknown status";
+    }
+}
+
+int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
+    if (!out) return FDBCS_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return FDBCS_E_NODEVICE;
+    if (device < 0 || device >= ndev) return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(device));
+    fdbcs_conflict_set* cs = new (std::nothrow) fdbcs_conflict_set();
+    if (!cs) return FDBCS_E_NOMEM;
+    cs->device = device;
+    if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete cs;
+        return FDBCS_E_DEVICE;
+    }
+    int rc = cs->scal.ensure(sizeof(Scalars));
+    if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
+    if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
+    if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
+    if (rc) {
+        fdbcs_destroy_conflict_set(cs);
+        return rc;
+    }
+    *out = cs;
+    return FDBCS_OK;
+}
+
+void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
+    if (!cs) return;
+    (void)hipSetDevice(cs->device);
+    if (cs->stream) (void)hipStreamSynchronize(cs->stream);
+    for (int k = 0; k < 2; k++) {
+        cs->hkey[k].release();
+        cs->hlt[k].release();
+        cs->hver[k].release();
+    }
+    cs->htail.release();
+    for (auto& l : cs->lvl) l.release();
+    for (auto& x : cs->ws) x.release();
+    cs->scal.release();
+    if (cs->stream) (void)hipStreamDestroy(cs->stream);
+    delete cs;
+}
+
+int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
+    if (!cs) return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(cs->device));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    HIPOK(hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    cs->header_version = version;
+    cs->max_written = version;
+    cs->n_ub = 0;
+    cs->tail_ub = 0;
+    return FDBCS_OK;
+}
+
+int fdbcs_set_oldest_version(fdbcs_conflict_set* cs, int64_t v) {
+    if (!cs) return FDBCS_E_INVALID;
+    if (v > cs->oldest) cs->oldest = v;
+    return FDBCS_OK;
+}
+
+int fdbcs_get_oldest_version(const fdbcs_conflict_set* cs, int64_t* out) {
+    if (!cs || !out) return FDBCS_E_INVALID;
+    *out = cs->oldest;
+    return FDBCS_OK;
+}
+
+int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes, int32_t max_txns,
+                  int32_t max_reads, int32_t max_writes) {
+    if (!cs || boundaries < 0 || tail_bytes < 0 || max_txns < 0 || max_reads < 0 || max_writes < 0)
+        return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(cs->device));
+    int rc = ensure_workspace(cs, max_txns, max_reads, max_writes);
+    if (rc) return rc;
+    return ensure_history(cs, std::max<int64_t>(boundaries, cs->hist_cap), std::max<int64_t>(tail_bytes, cs->tail_cap));
+}
+
+int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every) {
+    if (!cs || every < 1) return FDBCS_E_INVALID;
+    cs->gc_interval = every;
+    return FDBCS_OK;
+}
+
+int fdbcs_history_size(fdbcs_conflict_set* cs, int64_t* out) {
+    if (!cs || !out) return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(cs->device));
+    int rc = sync_sizes(cs);
+    if (rc) return rc;
+    *out = cs->n_ub;
+    return FDBCS_OK;
+}
+
+int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_bytes, const int64_t* key_offsets,
+                       const int64_t* versions, int64_t header_version) {
+    if (!cs || n < 0 || (n > 0 && (!key_bytes || !key_offsets || !versions))) return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(cs->device));
+    std::vector<ulonglong2> k(n);
+    std::vector<uint2> lt(n);
+    std::vector<uint8_t> tail;
+    int64_t maxv = header_version;
+    for (int64_t i = 0; i < n; i++) {
+        const uint8_t* p = key_bytes + key_offsets[i];
+        const int32_t len = (int32_t)(key_offsets[i + 1] - key_offsets[i]);
+        if (len < 0) return FDBCS_E_INVALID;
+        if (i > 0) {
+            const uint8_t* q = key_bytes + key_offsets[i - 1];
+            const int32_t ql = (int32_t)(key_offsets[i] - key_offsets[i - 1]);
+            if (cmp_bytes(q, ql, p, len) >= 0) return FDBCS_E_INVALID;  // strictly ascending
+        }
+        uint64_t hi, lo;
+        dkey_prefix(p, (uint32_t)len, &hi, &lo);
+        k[i] = make_ulonglong2(hi, lo);
+        uint32_t toff = 0;
+        if (len > 16) {
+            toff = (uint32_t)tail.size();
+            tail.insert(tail.end(), p + 16, p + len);
+        }
+        lt[i] = make_uint2((uint32_t)len, toff);
+        maxv = std::max(maxv, versions[i]);
+    }
+    int rc = ensure_history(cs, n + 1, (int64_t)tail.size() + 1);
+    if (rc) return rc;
+    if (n) {
+        HIPOK(hipMemcpyAsync(cs->hkey[cs->cur].p, k.data(), 16 * n, hipMemcpyHostToDevice, cs->stream));
+        HIPOK(hipMemcpyAsync(cs->hlt[cs->cur].p, lt.data(), 8 * n, hipMemcpyHostToDevice, cs->stream));
+        HIPOK(hipMemcpyAsync(cs->hver[cs->cur].p, versions, 8 * n, hipMemcpyHostToDevice, cs->stream));
+    }
+    if (!tail.empty())
+        HIPOK(hipMemcpyAsync(cs->htail.p, tail.data(), tail.size(), hipMemcpyHostToDevice, cs->stream));
+    Scalars s{};
+    s.n = n;
+    s.tail_used = (int64_t)tail.size();
+    HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
+    MaxLevels lv = levels_of(cs, cs->cur);
+    launch_blockmax(cs->stream, lv, &((Scalars*)cs->scal.p)->n, std::max<int64_t>(n, 1));
+    HIPOK(hipGetLastError());
+    HIPOK(hipStreamSynchronize(cs->stream));
+    cs->header_version = header_version;
+    cs->max_written = maxv;
+    cs->n_ub = n;
+    cs->tail_ub = (int64_t)tail.size();
+    return FDBCS_OK;
+}
+
+int fdbcs_get_stats(fdbcs_conflict_set* cs, fdbcs_stats* out) {
+    if (!cs || !out) return FDBCS_E_INVALID;
+    *out = cs->stats;
+    return FDBCS_OK;
+}
+
+int fdbcs_reset_stats(fdbcs_conflict_set* cs) {
+    if (!cs) return FDBCS_E_INVALID;
+    memset(&cs->stats, 0, sizeof(cs->stats));
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) {
+    if (!cs || !out) return FDBCS_E_INVALID;
+    fdbcs_batch* b = new (std::nothrow) fdbcs_batch();
+    if (!b) return FDBCS_E_NOMEM;
+    b->cs = cs;
+    b->report_enabled = report_keys ? 1 : 0;
+    *out = b;
+    return FDBCS_OK;
+}
+
+void fdbcs_batch_destroy(fdbcs_batch* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->cs->device);
+    if (b->state == 2) (void)hipStreamSynchronize(b->cs->stream);
+    if (b->events_made)
+        for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(b->ev[i]);
+    b->dev.release();
+    b->dverdict.release();
+    b->pin_in.release();
+    b->pin_out.release();
+    delete b;
+}
+
+int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int report_conflicting_keys, int32_t n_reads,
+                                const uint8_t* const* read_begin, const int32_t* read_begin_len,
+                                const uint8_t* const* read_end, const int32_t* read_end_len, int32_t n_writes,
+                                const uint8_t* const* write_begin, const int32_t* write_begin_len,
+                                const uint8_t* const* write_end, const int32_t* write_end_len) {
+    if (!b || n_reads < 0 || n_writes < 0) return FDBCS_E_INVALID;
+    if (b->state != 0) return FDBCS_E_STATE;
+    if ((n_reads && (!read_begin || !read_end || !read_begin_len || !read_end_len)) ||
+        (n_writes && (!write_begin || !write_end || !write_begin_len || !write_end_len)))
+        return FDBCS_E_INVALID;
+    // KeyRangeRef rejects begin > end (FDBTypes.h:288-291): validate before mutating anything.
+    for (int32_t i = 0; i < n_reads; i++)
+        if (read_begin_len[i] < 0 || read_end_len[i] < 0 ||
+            cmp_bytes(read_begin[i], read_begin_len[i], read_end[i], read_end_len[i]) > 0)
+            return FDBCS_E_INVALID;
+    for (int32_t i = 0; i < n_writes; i++)
+        if (write_begin_len[i] < 0 || write_end_len[i] < 0 ||
+            cmp_bytes(write_begin[i], write_begin_len[i], write_end[i], write_end_len[i]) > 0)
+            return FDBCS_E_INVALID;
+    const int32_t t = b->T();
+    uint8_t fl = (report_conflicting_keys && b->report_enabled) ? kFlagReport : 0;
+    const bool too_old = read_snapshot < b->cs->oldest && n_reads > 0;  // SkipList.cpp:770
+    if (too_old) fl |= kFlagTooOld;
+    b->snap.push_back(read_snapshot);
+    b->flags.push_back(fl);
+    if (!too_old) {
+        for (int32_t i = 0; i < n_reads; i++) {
+            add_key(b, b->rkeys, read_begin[i], read_begin_len[i]);
+            add_key(b, b->rkeys, read_end[i], read_end_len[i]);
+            b->rowner.push_back(t);
+        }
+        for (int32_t i = 0; i < n_writes; i++) {
+            add_key(b, b->wkeys, write_begin[i], write_begin_len[i]);
+            add_key(b, b->wkeys, write_end[i], write_end_len[i]);
+            b->wowner.push_back(t);
+        }
+    }
+    b->roff.push_back(b->roff.back() + (too_old ? 0 : n_reads));
+    b->woff.push_back(b->woff.back() + (too_old ? 0 : n_writes));
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
+    if (!b || !pb || pb->n_txn < 0) return FDBCS_E_INVALID;
+    if (b->state != 0) return FDBCS_E_STATE;
+    const int32_t T = pb->n_txn;
+    if (T == 0) return FDBCS_OK;
+    if (!pb->read_snapshot || !pb->read_offsets || !pb->write_offsets || !pb->key_offsets) return FDBCS_E_INVALID;
+    const int32_t R = pb->read_offsets[T];
+    const int64_t nk = 2 * ((int64_t)R + pb->write_offsets[T]);
+    if (nk && !pb->key_bytes) return FDBCS_E_INVALID;
+    // validate everything first (all-or-nothing)
+    for (int32_t t = 0; t < T; t++)
+        if (pb->read_offsets[t + 1] < pb->read_offsets[t] || pb->write_offsets[t + 1] < pb->write_offsets[t])
+            return FDBCS_E_INVALID;
+    for (int64_t k = 0; k < nk; k += 2) {
+        const int64_t a0 = pb->key_offsets[k], a1 = pb->key_offsets[k + 1], a2 = pb->key_offsets[k + 2];
+        if (a1 < a0 || a2 < a1) return FDBCS_E_INVALID;
+        if (cmp_bytes(pb->key_bytes + a0, (int32_t)(a1 - a0), pb->key_bytes + a1, (int32_t)(a2 - a1)) > 0)
+            return FDBCS_E_INVALID;
+    }
+    const int64_t oldest = b->cs->oldest;
+    b->snap.reserve(b->snap.size() + T);
+    for (int32_t t = 0; t < T; t++) {
+        const int32_t tt = b->T();
+        const int32_t r0 = pb->read_offsets[t], r1 = pb->read_offsets[t + 1];
+        const int32_t w0 = pb->write_offsets[t], w1 = pb->write_offsets[t + 1];
+        uint8_t fl = (pb->report_conflicting_keys && pb->report_conflicting_keys[t] && b->report_enabled)
+                         ? kFlagReport
+                         : 0;
+        const bool too_old = pb->read_snapshot[t] < oldest && r1 > r0;
+        if (too_old) fl |= kFlagTooOld;
+        b->snap.push_back(pb->read_snapshot[t]);
+        b->flags.push_back(fl);
+        if (!too_old) {
+            for (int32_t r = r0; r < r1; r++) {
+                for (int e = 0; e < 2; e++) {
+                    const int64_t k = 2 * (int64_t)r + e;
+                    add_key(b, b->rkeys, pb->key_bytes + pb->key_offsets[k],
+                            (int32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]));
+                }
+                b->rowner.push_back(tt);
+            }
+            for (int32_t w = w0; w < w1; w++) {
+                for (int e = 0; e < 2; e++) {
+                    const int64_t k = 2 * ((int64_t)R + w) + e;
+                    add_key(b, b->wkeys, pb->key_bytes + pb->key_offsets[k],
+                            (int32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]));
+                }
+                b->wowner.push_back(tt);
+            }
+        }
+        b->roff.push_back(b->roff.back() + (too_old ? 0 : r1 - r0));
+        b->woff.push_back(b->woff.back() + (too_old ? 0 : w1 - w0));
+    }
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_upload(fdbcs_batch* b) {
+    if (!b) return FDBCS_E_INVALID;
+    if (b->state != 0) return b->state == 1 ? FDBCS_OK : FDBCS_E_STATE;
+    HIPOK(hipSetDevice(b->cs->device));
+    return do_upload(b);
+}
+
+int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_version) {
+    if (!b) return FDBCS_E_INVALID;
+    if (b->state > 1) return FDBCS_E_STATE;
+    fdbcs_conflict_set* cs = b->cs;
+    HIPOK(hipSetDevice(cs->device));
+    if (now < cs->max_written) return FDBCS_E_VERSION;
+    if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
+    const int64_t T = b->T(), R = b->R(), W = b->W();
+    int rc;
+    if ((rc = ensure_workspace(cs, T, R, W))) return rc;
+    if ((rc = ensure_history(cs, cs->n_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail.size() + 1))) return rc;
+    if ((rc = ensure_events(b))) return rc;
+    // results staging: verdict | scalars | rconf | hist | first_conf
+    const size_t o_sc = align_up(T + 1, 64);
+    const size_t o_rc = align_up(o_sc + sizeof(Scalars), 64);
+    const size_t o_hc = align_up(o_rc + R + 1, 64);
+    const size_t o_fc = align_up(o_hc + T + 1, 64);
+    const size_t out_bytes = o_fc + 4 * (T + 1);
+    if ((rc = b->pin_out.ensure(out_bytes))) return rc;
+    char* ho = (char*)b->pin_out.p;
+    b->h_verdict = (uint8_t*)ho;
+    b->h_scal = (Scalars*)(ho + o_sc);
+    b->h_rconf = (uint8_t*)(ho + o_rc);
+    b->h_hist = (uint8_t*)(ho + o_hc);
+    b->h_first = (int32_t*)(ho + o_fc);
+    if ((rc = b->dverdict.ensure(T + 1))) return rc;
+
+    hipStream_t s = cs->stream;
+    HIPOK(hipEventRecord(b->ev[kPhStart], s));
+    if (b->state == 0 && (rc = do_upload(b))) return rc;
+    HIPOK(hipEventRecord(b->ev[kPhUpload], s));
+    const BatchDev& bd = b->bd;
+    Work& w = cs->work;
+    Scalars* sc = (Scalars*)cs->scal.p;
+    const int src = cs->cur;
+    Hist hs = hist_of(cs, src), hd = hist_of(cs, src ^ 1);
+    MaxLevels lv = levels_of(cs, src);
+
+    if (T) HIPOK(hipMemsetAsync(w.hist_conf, 0, T, s));
+    launch_check_reads(s, bd, hs, lv, (const uint8_t*)cs->htail.p, sc, cs->header_version, w);
+    HIPOK(hipEventRecord(b->ev[kPhCheck], s));
+    int sorted = 0;
+    launch_sort_points(s, bd, w, &sorted);
+    HIPOK(hipEventRecord(b->ev[kPhSort], s));
+    launch_positions(s, bd, w, sorted);
+    launch_edges(s, bd, w, sc);
+    launch_resolve(s, bd, w, sc);
+    HIPOK(hipEventRecord(b->ev[kPhIntra], s));
+    launch_combine(s, bd, w, sc);
+    HIPOK(hipEventRecord(b->ev[kPhCombine], s));
+    launch_merge(s, bd, w, hs, hd, (uint8_t*)cs->htail.p, sc, now, cs->header_version, cs->n_ub + 1,
+                 b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
+    HIPOK(hipEventRecord(b->ev[kPhMerge], s));
+    int final_buf = src ^ 1;
+    const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
+    // removeBefore (SkipList.cpp:880-889) on every gc_interval-th batch whose oldest version moved
+    bool gc = false;
+    if (new_oldest > cs->gc_applied && ++cs->batches_since_gc >= cs->gc_interval) gc = true;
+    if (gc) {
+        launch_gc(s, w, hd, hs, sc, new_oldest, cs->header_version, cs->n_ub + 2 * W + 1);
+        final_buf = src;
+        cs->batches_since_gc = 0;
+        cs->gc_applied = new_oldest;
+    }
+    b->gc_ran = gc;
+    MaxLevels lf = levels_of(cs, final_buf);
+    launch_blockmax(s, lf, gc ? &sc->n_gc : &sc->n_next, cs->n_ub + 2 * W + 1);
+    HIPOK(hipEventRecord(b->ev[kPhGc], s));
+    launch_finalize(s, bd, w, sc, gc ? 1 : 0);
+    HIPOK(hipGetLastError());
+    // results back
+    if (T) HIPOK(hipMemcpyAsync(b->h_verdict, w.verdict, T, hipMemcpyDeviceToHost, s));
+    if (T) HIPOK(hipMemcpyAsync(b->dverdict.p, w.verdict, T, hipMemcpyDeviceToDevice, s));
+    HIPOK(hipMemcpyAsync(b->h_scal, sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
+    b->any_report = false;
+    for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
+    if (b->any_report) {
+        if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(b->h_first, w.first_conf, 4 * T, hipMemcpyDeviceToHost, s));
+    }
+    HIPOK(hipEventRecord(b->ev[kPhEnd], s));
+    cs->cur = final_buf;
+    cs->oldest = new_oldest;  // SkipList.cpp:880-882
+    if (W) cs->max_written = std::max(cs->max_written, now);
+    cs->n_ub += 2 * W;
+    cs->tail_ub += (int64_t)b->tail.size();
+    cs->inflight++;
+    b->state = 2;
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, int32_t* n_too_old) {
+    if (!b) return FDBCS_E_INVALID;
+    fdbcs_conflict_set* cs = b->cs;
+    if (b->state == 2) {
+        HIPOK(hipSetDevice(cs->device));
+        HIPOK(hipEventSynchronize(b->ev[kPhEnd]));
+        const int32_t T = b->T();
+        int32_t nc = 0, nt = 0;
+        for (int32_t t = 0; t < T; t++) {
+            nc += b->h_verdict[t] == FDBCS_TRANSACTION_COMMITTED;
+            nt += b->h_verdict[t] == FDBCS_TRANSACTION_TOO_OLD;
+        }
+        b->n_committed = nc;
+        b->n_too_old = nt;
+        // conflictingKeyRangeMap: every conflicting read for history conflicts (SkipList.cpp:641-645),
+        // the first for intra-batch conflicts (SkipList.cpp:821-828).
+        b->conf_off.assign(T + 1, 0);
+        b->conf_idx.clear();
+        if (b->any_report) {
+            for (int32_t t = 0; t < T; t++) {
+                if ((b->flags[t] & kFlagReport) && b->h_verdict[t] == FDBCS_TRANSACTION_CONFLICT) {
+                    if (b->h_hist[t]) {
+                        for (int32_t r = b->roff[t]; r < b->roff[t + 1]; r++)
+                            if (b->h_rconf[r]) b->conf_idx.push_back(r - b->roff[t]);
+                    } else if (b->h_first[t] != INT_MAX) {
+                        b->conf_idx.push_back(b->h_first[t]);
+                    }
+                }
+                b->conf_off[t + 1] = (int32_t)b->conf_idx.size();
+            }
+        }
+        // stats
+        fdbcs_stats& st = cs->stats;
+        st.batches++;
+        st.transactions += T;
+        st.read_ranges += b->R();
+        st.write_ranges += b->W();
+        st.ms_upload += ev_ms(b->ev[kPhStart], b->ev[kPhUpload]);
+        st.ms_check_read += ev_ms(b->ev[kPhUpload], b->ev[kPhCheck]);
+        st.ms_sort += ev_ms(b->ev[kPhCheck], b->ev[kPhSort]);
+        st.ms_intra += ev_ms(b->ev[kPhSort], b->ev[kPhIntra]);
+        st.ms_combine += ev_ms(b->ev[kPhIntra], b->ev[kPhCombine]);
+        st.ms_merge += ev_ms(b->ev[kPhCombine], b->ev[kPhMerge]);
+        st.ms_gc += ev_ms(b->ev[kPhMerge], b->ev[kPhGc]);
+        st.ms_total += ev_ms(b->ev[kPhUpload], b->ev[kPhEnd]);
+        // dominant kernel: history rewrite reads every old boundary (32 B) and writes the kept ones
+        st.ms_merge_kernel += ev_ms(b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
+        st.merge_launches += 1;
+        st.merge_bytes += 32 * (2 * b->h_scal->n_before - b->h_scal->rem_total);
+        cs->inflight--;
+        if (cs->inflight == 0) {
+            cs->n_ub = b->h_scal->n;
+            cs->tail_ub = b->h_scal->tail_used;
+        }
+        b->state = 3;
+    }
+    if (b->state != 3) return FDBCS_E_STATE;
+    if (verdicts && b->T()) memcpy(verdicts, b->h_verdict, b->T());
+    if (n_committed) *n_committed = b->n_committed;
+    if (n_too_old) *n_too_old = b->n_too_old;
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_detect_conflicts(fdbcs_batch* b, int64_t now, int64_t new_oldest_version, uint8_t* verdicts,
+                                 int32_t* n_committed, int32_t* n_too_old) {
+    int rc = fdbcs_batch_detect_async(b, now, new_oldest_version);
+    if (rc) return rc;
+    return fdbcs_batch_wait(b, verdicts, n_committed, n_too_old);
+}
+
+int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out, int32_t cap, int32_t* n_out) {
+    if (!b || !n_out) return FDBCS_E_INVALID;
+    if (b->state != 3) return FDBCS_E_STATE;
+    if (txn < 0 || txn >= b->T()) return FDBCS_E_INVALID;
+    const int32_t a = b->conf_off[txn], e = b->conf_off[txn + 1];
+    *n_out = e - a;
+    if (idx_out)
+        for (int32_t i = a; i < e && i - a < cap; i++) idx_out[i - a] = b->conf_idx[i];
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr) {
+    if (!b || !dptr) return FDBCS_E_INVALID;
+    if (b->state < 2) return FDBCS_E_STATE;
+    *dptr = b->dverdict.p;
+    return FDBCS_OK;
+}
+
+}  // extern "C"

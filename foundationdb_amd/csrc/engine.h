@@ -1,0 +1,117 @@
+// engine.h — internal interface between the host engine (engine.cpp) and the
+// gfx950 kernels (kernels.hip).  Not part of the public C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dkey.h"
+
+namespace fdbcs {
+
+constexpr int kBlock = 256;        // default workgroup: 4 waves of 64
+constexpr int kWG = 1024;          // single-workgroup kernels (scans, resolution)
+constexpr int kSortTile = 2048;    // endpoints per LDS sort tile (256 threads x 8)
+constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
+constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)
+constexpr int kGcTile = 4096;      // history elements per GC / merge tile
+constexpr int kMaxTxnLds = 65536;  // transactions whose status fits the resolver's LDS
+
+// Transaction status during batch-order resolution.
+enum : uint8_t { kUndecided = 0, kAborted = 1, kCommitted = 2 };
+// Per-transaction input flags.
+enum : uint8_t { kFlagTooOld = 1, kFlagReport = 2 };
+
+// One history buffer set (structure of arrays; boundary i covers [key_i, key_{i+1})).
+struct Hist {
+    ulonglong2* key;  // (hi, lo) prefix words
+    uint2* lt;        // (len, tail offset)
+    int64_t* ver;     // segment version
+};
+
+// Range-max hierarchy over the current history's versions.
+struct MaxLevels {
+    int64_t* lvl[kMaxLevels];  // lvl[0] == current Hist::ver
+};
+
+// Device-side scalars of a conflict set (one allocation).
+struct Scalars {
+    int64_t n;             // live boundaries in the current history
+    int64_t n_next;        // after this batch's merge
+    int64_t n_gc;          // after GC
+    int64_t tail_used;     // bytes used in the history tail arena
+    int64_t tail_next;
+    int32_t n_segments;    // union segments of committed writes
+    int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
+    int64_t n_edges;
+    int32_t rounds;        // resolution rounds used
+    int32_t pad;
+    int64_t n_before;      // history size at the start of the merge
+    int64_t rem_total;     // boundaries removed by union segments
+};
+
+// Device copy of one batch's packed input (tooOld transactions carry no ranges,
+// as in addTransaction, SkipList.cpp:770-790).
+struct BatchDev {
+    int32_t T, R, W;
+    int64_t* snap;       // [T]
+    uint8_t* flags;      // [T]
+    int32_t* roff;       // [T+1]
+    int32_t* woff;       // [T+1]
+    int32_t* rowner;     // [R]
+    int32_t* wowner;     // [W]
+    DKey* keys;          // [2(R+W)]
+    uint8_t* tail;       // key bytes beyond 16
+};
+
+// Per-set scratch, sized for the largest batch seen.
+struct Work {
+    uint8_t* hist_conf;    // [T]
+    uint8_t* rconf;        // [R]
+    uint8_t* status;       // [T]
+    int32_t* first_conf;   // [T]
+    SortItem* items[2];    // [E]
+    int32_t* pos;          // [2(R+W)] sorted position of each endpoint
+    uint32_t* pmeta;       // [E] meta of the item at each position
+    int64_t* cnt_pair;     // [E+1] packed exclusive counts: write-begins << 32 | read-begins
+    int32_t* wbpos;        // [W] positions of write-begins in order
+    int32_t* rbpos;        // [R] positions of read-begins in order
+    int32_t* ecnt_a;       // [R]
+    int32_t* ecnt_b;       // [R]
+    int32_t* eoff;         // [R+1]
+    int32_t* ecur;         // [R]
+    int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
+    int64_t edge_cap;
+    int32_t* eptr;         // [T] resume pointer per transaction
+    int32_t* cov;          // [E]
+    uint64_t* mcs_bits;    // [E/64+1] sequential-fallback MiniConflictSet
+    // union segments (<= W)
+    int32_t* seg_b;        // position of segment begin
+    int32_t* seg_e;        // position of segment end
+    int64_t* seg_lo;
+    int64_t* seg_hi;
+    int64_t* seg_rem;      // -> exclusive prefix after scan
+    int64_t* seg_ins;
+    int64_t* seg_tlen;
+    uint8_t* seg_endins;
+    int64_t* seg_vend;
+    int64_t* tile_cnt;     // GC tiles
+    uint8_t* verdict;      // [T]
+};
+
+// ---- launchers (kernels.hip); all enqueue on `s` and never synchronize.
+void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const MaxLevels& m, const uint8_t* htail,
+                        const Scalars* sc, int64_t header_version, const Work& w);
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer);
+void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
+void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
+void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
+void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
+                  Scalars* sc, int64_t now, int64_t header_version, int64_t grid_hint_n, hipEvent_t copy_begin,
+                  hipEvent_t copy_end);
+void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
+               int64_t header_version, int64_t grid_hint_n);
+void launch_blockmax(hipStream_t s, const MaxLevels& m, const int64_t* n_ptr, int64_t grid_hint_n);
+void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran);
+
+}  // namespace fdbcs

@@ -1,0 +1,902 @@
+// kernels.hip — gfx950 (CDNA4) kernels of the MVCC conflict-resolution engine.
+//
+// The reference resolves a batch on one CPU thread with a versioned skip list
+// (fdbserver/SkipList.cpp:844-890).  Here the history is a sorted boundary array
+// in HBM (structure of arrays) with a 64-ary range-max hierarchy, and every phase
+// of ConflictBatch::detectConflicts is a data-parallel kernel:
+//
+//   D.CheckRead        k_check_reads      per read range: two searches + range max
+//   D.Sort             k_sort_tile / k_merge_pass   merge sort of endpoints by (key, class)
+//   D.CheckIntraBatch  k_positions, k_edges_*, k_resolve   candidate edges + batch-order rounds
+//   D.Combine          k_combine          coverage scan over sorted endpoints
+//   D.MergeWrite       k_seg_search, k_merge_copy, k_merge_insert, k_blockmax
+//   D.RemoveBefore     k_gc_count / k_gc_scatter
+//
+// Memory-bound integer/byte work: no MFMA anywhere (BASELINE.json north_star).
+#include <hip/hip_runtime.h>
+#include <limits.h>
+
+#include "engine.h"
+
+namespace fdbcs {
+
+// ------------------------------------------------------------------ helpers
+
+__device__ __forceinline__ int hist_cmp(const Hist& h, int64_t i, const uint8_t* htail, const DKey& q,
+                                        const uint8_t* qtail) {
+    ulonglong2 k = h.key[i];
+    if (k.x != q.hi) return k.x < q.hi ? -1 : 1;
+    if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
+    uint2 lt = h.lt[i];
+    if (lt.x > 16u && q.len > 16u) return tail_cmp(htail + lt.y, lt.x, qtail + q.tail, q.len);
+    return (lt.x > q.len) - (lt.x < q.len);
+}
+
+// First index in [lo, hi) whose boundary key is >= q (std::lower_bound).
+__device__ __forceinline__ int64_t hist_lower_bound(const Hist& h, int64_t lo, int64_t hi, const uint8_t* htail,
+                                                    const DKey& q, const uint8_t* qtail) {
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (hist_cmp(h, mid, htail, q, qtail) < 0)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
+__device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
+    int64_t best = LLONG_MIN;
+    for (int L = 0; L < kMaxLevels; L++) {
+        const int64_t* a = m.lvl[L];
+        if (hi - lo <= 2 * kFan || L == kMaxLevels - 1) {
+            for (int64_t i = lo; i < hi; i++) {
+                int64_t v = a[i];
+                best = v > best ? v : best;
+                if (best > snap) return best;
+            }
+            return best;
+        }
+        int64_t lo2 = (lo + kFan - 1) / kFan, hi2 = hi / kFan;
+        for (int64_t i = lo; i < lo2 * kFan; i++) {
+            int64_t v = a[i];
+            best = v > best ? v : best;
+        }
+        for (int64_t i = hi2 * kFan; i < hi; i++) {
+            int64_t v = a[i];
+            best = v > best ? v : best;
+        }
+        if (best > snap) return best;
+        lo = lo2;
+        hi = hi2;
+    }
+    return best;
+}
+
+// Exclusive block-wide sum over all threads of the block (blockDim multiple of 64).
+template <typename T>
+__device__ __forceinline__ T block_excl_sum(T v, T* sh, T* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        T y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        T s = lane < nw ? sh[lane] : T(0);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            T y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane < nw) sh[lane] = s;
+    }
+    __syncthreads();
+    T before = wid ? sh[wid - 1] : T(0);
+    *total = sh[nw - 1];
+    __syncthreads();
+    return before + x - v;
+}
+
+// Single-workgroup exclusive scan of n elements given by load(i); store(i, prefix).
+// Returns the total.  Each thread owns 4 consecutive elements per 4*blockDim chunk.
+template <typename T, typename Load, typename Store>
+__device__ T wg_scan(int64_t n, Load load, Store store, T* sh) {
+    T carry = 0;
+    const int64_t chunk = 4 * (int64_t)blockDim.x;
+    for (int64_t base = 0; base < n; base += chunk) {
+        int64_t i0 = base + 4 * (int64_t)threadIdx.x;
+        T v[4];
+        T s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            v[k] = (i0 + k < n) ? load(i0 + k) : T(0);
+            s += v[k];
+        }
+        T tot;
+        T run = carry + block_excl_sum<T>(s, sh, &tot);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (i0 + k < n) store(i0 + k, run);
+            run += v[k];
+        }
+        carry += tot;
+    }
+    return carry;
+}
+
+// ------------------------------------------------------------------ D.CheckRead
+
+// One thread per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the
+// step-function rule of SURVEY A.2).
+__global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Hist h, MaxLevels m, const uint8_t* htail,
+                                                        const Scalars* sc, int64_t hdr, uint8_t* hist_conf,
+                                                        uint8_t* rconf) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= b.R) return;
+    const int64_t n = sc->n;
+    const int t = b.rowner[r];
+    const int64_t snap = b.snap[t];
+    const DKey kb = b.keys[2 * r], ke = b.keys[2 * r + 1];
+    bool conf;
+    const int64_t lb = hist_lower_bound(h, 0, n, htail, kb, b.tail);
+    if (dkey_cmp(kb, b.tail, ke, b.tail) == 0) {
+        // degenerate [b, b): greatest boundary < b (fingers never diverge, SkipList.cpp:650-666)
+        const int64_t v = lb > 0 ? h.ver[lb - 1] : hdr;
+        conf = v > snap;
+    } else {
+        const int64_t ub = lb + ((lb < n && hist_cmp(h, lb, htail, kb, b.tail) == 0) ? 1 : 0);
+        const int64_t j = hist_lower_bound(h, ub, n, htail, ke, b.tail);
+        // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
+        if (ub == 0) {
+            conf = hdr > snap || range_max(m, 0, j, snap) > snap;
+        } else {
+            conf = range_max(m, ub - 1, j, snap) > snap;
+        }
+    }
+    rconf[r] = conf ? 1 : 0;
+    if (conf) hist_conf[t] = 1;
+}
+
+void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const MaxLevels& m, const uint8_t* htail,
+                        const Scalars* sc, int64_t header_version, const Work& w) {
+    if (b.R == 0) return;
+    hipLaunchKernelGGL(k_check_reads, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, h, m, htail, sc,
+                       header_version, w.hist_conf, w.rconf);
+}
+
+// ------------------------------------------------------------------ D.Sort
+
+__global__ __launch_bounds__(kBlock) void k_make_items(BatchDev b, SortItem* items) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;  // range id: reads then writes
+    if (g >= b.R + b.W) return;
+    const bool is_read = g < b.R;
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const DKey k = b.keys[2 * g + e];
+        // extra_ordering (SkipList.cpp:89-91): begin*2 + (write ^ begin)
+        const uint32_t cls = is_read ? (e ? kReadEnd : kReadBegin) : (e ? kWriteEnd : kWriteBegin);
+        SortItem it;
+        it.hi = k.hi;
+        it.lo = k.lo;
+        it.len = k.len;
+        it.tail = k.tail;
+        it.meta = ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
+        it.pad = 0;
+        items[2 * g + e] = it;
+    }
+}
+
+// Merge-path split + 8-way serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties):
+// writes outputs [d, d+count) of the merged sequence to out[0, count).
+__device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
+                                       SortItem (&out)[8], int count, const uint8_t* arena) {
+    int lo = d - lenB > 0 ? d - lenB : 0;
+    int hi = d < lenA ? d : lenA;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (!item_less(B[d - mid - 1], A[mid], arena))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    int i = lo, j = d - lo;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (k < count) {
+            bool takeA = (j >= lenB) || (i < lenA && !item_less(B[j], A[i], arena));
+            out[k] = takeA ? A[i] : B[j];
+            i += takeA ? 1 : 0;
+            j += takeA ? 0 : 1;
+        }
+    }
+}
+
+// Sort one tile of kSortTile endpoints in LDS (runs 1,2,4,... merged by merge path).
+__global__ __launch_bounds__(kBlock) void k_sort_tile(const SortItem* in, SortItem* out, int n,
+                                                      const uint8_t* arena) {
+    __shared__ SortItem sh[kSortTile];
+    const int base = blockIdx.x * kSortTile;
+    const int cnt = min(kSortTile, n - base);
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = in[base + i];
+    __syncthreads();
+    const int o = threadIdx.x * 8;
+    const int mine = max(0, min(8, cnt - o));
+    SortItem r[8];
+    for (int w = 1; w < cnt; w <<= 1) {
+        const int pb = (o / (2 * w)) * (2 * w);
+        const int lenA = max(0, min(w, cnt - pb));
+        const int lenB = max(0, min(w, cnt - pb - w));
+        if (mine > 0) merge8(sh + pb, lenA, sh + pb + w, lenB, o - pb, r, mine, arena);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k < mine) sh[o + k] = r[k];
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) out[base + i] = sh[i];
+}
+
+// Merge sorted runs of length w pairwise into runs of 2w; one output tile per workgroup.
+__global__ __launch_bounds__(kBlock) void k_merge_pass(const SortItem* in, SortItem* out, int n, int w,
+                                                       const uint8_t* arena) {
+    __shared__ SortItem sh[kSortTile];
+    __shared__ int split[2];
+    const int o0 = blockIdx.x * kSortTile;
+    if (o0 >= n) return;
+    const int pb = (o0 / (2 * w)) * (2 * w);
+    const int lenA = max(0, min(w, n - pb));
+    const int lenB = max(0, min(w, n - pb - w));
+    const SortItem* A = in + pb;
+    const SortItem* B = A + w;
+    const int d0 = o0 - pb;
+    const int d1 = min(d0 + kSortTile, lenA + lenB);
+    if (threadIdx.x < 2) {
+        const int d = threadIdx.x ? d1 : d0;
+        int lo = d - lenB > 0 ? d - lenB : 0;
+        int hi = d < lenA ? d : lenA;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (!item_less(B[d - mid - 1], A[mid], arena))
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        split[threadIdx.x] = lo;
+    }
+    __syncthreads();
+    const int i0 = split[0], i1 = split[1];
+    const int j0 = d0 - i0, j1 = d1 - i1;
+    const int na = i1 - i0, nb = j1 - j0;
+    for (int i = threadIdx.x; i < na; i += blockDim.x) sh[i] = A[i0 + i];
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) sh[na + i] = B[j0 + i];
+    __syncthreads();
+    const int o = threadIdx.x * 8;
+    const int mine = max(0, min(8, (d1 - d0) - o));
+    if (mine > 0) {
+        SortItem r[8];
+        merge8(sh, na, sh + na, nb, o, r, mine, arena);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (k < mine) out[o0 + o + k] = r[k];
+    }
+}
+
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer) {
+    const int E = 2 * (b.R + b.W);
+    *result_buffer = 0;
+    if (E == 0) return;
+    hipLaunchKernelGGL(k_make_items, dim3((b.R + b.W + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w.items[1]);
+    const int tiles = (E + kSortTile - 1) / kSortTile;
+    hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kBlock), 0, s, w.items[1], w.items[0], E, b.tail);
+    int cur = 0;
+    for (int run = kSortTile; run < E; run *= 2) {
+        hipLaunchKernelGGL(k_merge_pass, dim3(tiles), dim3(kBlock), 0, s, w.items[cur], w.items[cur ^ 1], E, run,
+                           b.tail);
+        cur ^= 1;
+    }
+    *result_buffer = cur;
+}
+
+// ------------------------------------------------------------------ positions
+
+__global__ __launch_bounds__(kBlock) void k_positions(const SortItem* sorted, int E, int32_t* pos, uint32_t* pmeta) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    const uint32_t meta = sorted[p].meta;
+    pmeta[p] = meta;
+    pos[2 * item_range(meta) + item_is_end(meta)] = p;  // KeyInfo::pIndex (SkipList.cpp:814)
+}
+
+// Exclusive counts of write-begins (high word) and read-begins (low word) before each position,
+// plus the compacted position lists of each kind.
+__global__ __launch_bounds__(kWG) void k_begin_lists(const uint32_t* pmeta, int E, int64_t* cnt_pair,
+                                                     int32_t* wbpos, int32_t* rbpos) {
+    __shared__ int64_t sh[16];
+    auto flag = [&](int64_t p) -> int64_t {
+        const uint32_t c = item_class(pmeta[p]);
+        return (c == kWriteBegin ? (int64_t(1) << 32) : 0) | (c == kReadBegin ? 1 : 0);
+    };
+    int64_t tot = wg_scan<int64_t>(
+        E, flag, [&](int64_t p, int64_t pre) { cnt_pair[p] = pre; }, sh);
+    if (threadIdx.x == 0) cnt_pair[E] = tot;
+    __syncthreads();
+    for (int p = threadIdx.x; p < E; p += blockDim.x) {
+        const uint32_t c = item_class(pmeta[p]);
+        if (c == kWriteBegin) wbpos[cnt_pair[p] >> 32] = p;
+        if (c == kReadBegin) rbpos[cnt_pair[p] & 0xffffffffll] = p;
+    }
+}
+
+void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
+    const int E = 2 * (b.R + b.W);
+    if (E == 0) return;
+    hipLaunchKernelGGL(k_positions, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf], E,
+                       w.pos, w.pmeta);
+    hipLaunchKernelGGL(k_begin_lists, dim3(1), dim3(kWG), 0, s, w.pmeta, E, w.cnt_pair, w.wbpos, w.rbpos);
+}
+
+// ------------------------------------------------------------------ D.CheckIntraBatch: candidate edges
+//
+// Read r of txn t and write w of txn t' < t overlap iff (index space, SkipList.cpp:812-834)
+// wb < re and rb < we with both intervals non-empty.  Either w begins inside (rb, re)
+// (found from the read) or r begins inside (wb, we) (found from the write).  Each such
+// pair is one candidate edge t' -> t: t aborts iff some candidate writer commits.
+
+template <bool FILL>
+__global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scalars* sc) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= b.R + b.W) return;
+    if (FILL && sc->edge_overflow) return;
+    const int R = b.R;
+    if (g < R) {
+        const int r = g;
+        const int t = b.rowner[r];
+        if (w.hist_conf[t]) {
+            if (!FILL) w.ecnt_a[r] = 0;
+            return;
+        }
+        const int rb = w.pos[2 * r], re = w.pos[2 * r + 1];
+        int cnt = 0;
+        if (rb < re) {
+            const int k0 = (int)(w.cnt_pair[rb] >> 32), k1 = (int)(w.cnt_pair[re] >> 32);
+            int out = FILL ? w.eoff[r] : 0;
+            for (int k = k0; k < k1; k++) {
+                const int p = w.wbpos[k];
+                const int wr = (int)item_range(w.pmeta[p]) - R;
+                const int tw = b.wowner[wr];
+                if (tw < t && !w.hist_conf[tw] && w.pos[2 * (R + wr)] < w.pos[2 * (R + wr) + 1]) {
+                    if (FILL) w.edges[out + cnt] = tw;
+                    cnt++;
+                }
+            }
+        }
+        if (!FILL) w.ecnt_a[r] = cnt;
+    } else {
+        const int wr = g - R;
+        const int tw = b.wowner[wr];
+        if (w.hist_conf[tw]) return;
+        const int wb = w.pos[2 * g], we = w.pos[2 * g + 1];
+        if (wb >= we) return;
+        const int k0 = (int)(w.cnt_pair[wb] & 0xffffffffll), k1 = (int)(w.cnt_pair[we] & 0xffffffffll);
+        for (int k = k0; k < k1; k++) {
+            const int p = w.rbpos[k];
+            const int r = (int)item_range(w.pmeta[p]);
+            const int t = b.rowner[r];
+            if (tw < t && !w.hist_conf[t] && w.pos[2 * r] < w.pos[2 * r + 1]) {
+                if (FILL) {
+                    const int slot = atomicAdd(&w.ecur[r], 1);
+                    w.edges[w.eoff[r] + w.ecnt_a[r] + slot] = tw;
+                } else {
+                    atomicAdd(&w.ecnt_b[r], 1);
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWG) void k_edge_offsets(BatchDev b, Work w, Scalars* sc) {
+    __shared__ int64_t sh[16];
+    int64_t tot = wg_scan<int64_t>(
+        b.R, [&](int64_t r) -> int64_t { return (int64_t)w.ecnt_a[r] + w.ecnt_b[r]; },
+        [&](int64_t r, int64_t pre) { w.eoff[r] = (int32_t)(pre < INT_MAX ? pre : INT_MAX); }, sh);
+    if (threadIdx.x == 0) {
+        w.eoff[b.R] = (int32_t)(tot < INT_MAX ? tot : INT_MAX);
+        sc->n_edges = tot;
+        sc->edge_overflow = tot > w.edge_cap ? 1 : 0;
+    }
+}
+
+void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
+    const int G = b.R + b.W;
+    if (b.R) {
+        (void)hipMemsetAsync(w.ecnt_b, 0, sizeof(int32_t) * b.R, s);
+        (void)hipMemsetAsync(w.ecur, 0, sizeof(int32_t) * b.R, s);
+    }
+    if (G) hipLaunchKernelGGL(k_edges<false>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
+    hipLaunchKernelGGL(k_edge_offsets, dim3(1), dim3(kWG), 0, s, b, w, sc);
+    if (G) hipLaunchKernelGGL(k_edges<true>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
+}
+
+// ------------------------------------------------------------------ D.CheckIntraBatch: resolution
+//
+// Batch order (SkipList.cpp:817-833): commit(t) = !hist(t) && !tooOld(t) && no earlier committed
+// candidate writer.  Rounds in one workgroup: an undecided t commits once every candidate writer
+// is aborted and aborts as soon as one commits; the lowest undecided t always decides, so the
+// rounds terminate.  If the candidate edges overflowed, the workgroup replays MiniConflictSet
+// sequentially over point indices instead (exact, slower).
+
+__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, Scalars* sc) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t st[];
+    __shared__ int s_more;
+    const int T = b.T;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        st[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
+        w.first_conf[t] = INT_MAX;
+    }
+    __syncthreads();
+    int rounds = 0;
+    if (!sc->edge_overflow) {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) w.eptr[t] = w.eoff[b.roff[t]];
+        volatile uint8_t* vst = st;
+        for (;;) {
+            if (threadIdx.x == 0) s_more = 0;
+            __syncthreads();
+            int more = 0;
+            for (int t = threadIdx.x; t < T; t += blockDim.x) {
+                if (vst[t] != kUndecided) continue;
+                int p = w.eptr[t];
+                const int end = w.eoff[b.roff[t + 1]];
+                uint8_t res = kUndecided;
+                while (p < end) {
+                    const uint8_t sp = vst[w.edges[p]];
+                    if (sp == kAborted) {
+                        p++;
+                        continue;
+                    }
+                    if (sp == kCommitted) res = kAborted;
+                    break;
+                }
+                if (p == end) res = kCommitted;
+                w.eptr[t] = p;
+                if (res != kUndecided)
+                    vst[t] = res;
+                else
+                    more = 1;
+            }
+            if (more) s_more = 1;
+            __syncthreads();
+            rounds++;
+            if (!s_more) break;
+            __syncthreads();
+        }
+    } else {
+        // Sequential MiniConflictSet replay (SkipList.cpp:797-834) over E point indices.
+        for (int t = 0; t < T; t++) {
+            if (st[t] != kUndecided) continue;  // uniform: st read after a barrier
+            int conflict_at = INT_MAX;
+            for (int r = b.roff[t]; r < b.roff[t + 1]; r++) {
+                const int a = w.pos[2 * r], e = w.pos[2 * r + 1];
+                int hit = 0;
+                if (a < e) {
+                    for (int word = (a >> 6) + threadIdx.x; word <= ((e - 1) >> 6); word += blockDim.x) {
+                        uint64_t m = ((volatile uint64_t*)w.mcs_bits)[word];
+                        const int lo = word << 6;
+                        if (a > lo) m &= ~0ull << (a - lo);
+                        if (e < lo + 64) m &= (e - lo >= 64) ? ~0ull : ((1ull << (e - lo)) - 1);
+                        if (m) hit = 1;
+                    }
+                }
+                if (__syncthreads_or(hit)) {
+                    conflict_at = r - b.roff[t];
+                    break;
+                }
+            }
+            if (conflict_at == INT_MAX) {
+                for (int x = b.woff[t]; x < b.woff[t + 1]; x++) {
+                    const int g = b.R + x;
+                    const int a = w.pos[2 * g], e = w.pos[2 * g + 1];
+                    if (a < e) {
+                        for (int word = (a >> 6) + threadIdx.x; word <= ((e - 1) >> 6); word += blockDim.x) {
+                            uint64_t m = ~0ull;
+                            const int lo = word << 6;
+                            if (a > lo) m &= ~0ull << (a - lo);
+                            if (e < lo + 64) m &= (e - lo >= 64) ? ~0ull : ((1ull << (e - lo)) - 1);
+                            atomicOr((unsigned long long*)&w.mcs_bits[word], (unsigned long long)m);
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            if (threadIdx.x == 0) {
+                st[t] = conflict_at == INT_MAX ? kCommitted : kAborted;
+                if (conflict_at != INT_MAX) w.first_conf[t] = conflict_at;
+            }
+            __syncthreads();
+        }
+        rounds = -1;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x) w.status[t] = st[t];
+    if (threadIdx.x == 0) sc->rounds = rounds;
+}
+
+// First conflicting read index of intra-batch aborts that report conflicting keys
+// (SkipList.cpp:821-828).
+__global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w, const Scalars* sc) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= b.R || sc->edge_overflow) return;
+    const int t = b.rowner[r];
+    if (!(b.flags[t] & kFlagReport) || w.hist_conf[t] || w.status[t] != kAborted) return;
+    for (int p = w.eoff[r]; p < w.eoff[r + 1]; p++) {
+        if (w.status[w.edges[p]] == kCommitted) {
+            atomicMin(&w.first_conf[t], r - b.roff[t]);
+            return;
+        }
+    }
+}
+
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
+    if (b.T == 0) return;
+    const int E = 2 * (b.R + b.W);
+    (void)hipMemsetAsync(w.mcs_bits, 0, sizeof(uint64_t) * (E / 64 + 1), s);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxTxnLds);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWG), (size_t)b.T, s, b, w, sc);
+    if (b.R) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
+}
+
+// ------------------------------------------------------------------ D.Combine
+//
+// combineWriteConflictRanges (SkipList.cpp:926-939): coverage of committed non-empty writes over
+// sorted positions; each maximal covered run is one union segment [key(begin), key(end)).
+
+__global__ __launch_bounds__(kWG) void k_combine(BatchDev b, Work w, Scalars* sc) {
+    __shared__ int32_t sh[16];
+    const int E = 2 * (b.R + b.W);
+    const int R = b.R;
+    auto delta = [&](int64_t p) -> int32_t {
+        const uint32_t meta = w.pmeta[p];
+        const uint32_t c = item_class(meta);
+        if (c != kWriteBegin && c != kWriteEnd) return 0;
+        const int g = (int)item_range(meta);
+        if (w.status[b.wowner[g - R]] != kCommitted) return 0;
+        if (w.pos[2 * g] >= w.pos[2 * g + 1]) return 0;
+        return c == kWriteBegin ? 1 : -1;
+    };
+    // inclusive coverage = exclusive prefix + own delta
+    wg_scan<int32_t>(
+        E, delta, [&](int64_t p, int32_t pre) { w.cov[p] = pre + delta(p); }, sh);
+    __syncthreads();
+    auto sflag = [&](int64_t p) -> int32_t { return (w.cov[p] > 0 && (p == 0 || w.cov[p - 1] == 0)) ? 1 : 0; };
+    int32_t U = wg_scan<int32_t>(
+        E, sflag,
+        [&](int64_t p, int32_t pre) {
+            const int32_t c = w.cov[p];
+            const int32_t prev = p ? w.cov[p - 1] : 0;
+            if (c > 0 && prev == 0) w.seg_b[pre] = (int32_t)p;
+            if (c == 0 && prev > 0) w.seg_e[pre - 1] = (int32_t)p;
+        },
+        sh);
+    if (threadIdx.x == 0) sc->n_segments = U;
+}
+
+void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
+    hipLaunchKernelGGL(k_combine, dim3(1), dim3(kWG), 0, s, b, w, sc);
+}
+
+// ------------------------------------------------------------------ D.MergeWrite
+//
+// mergeWriteConflictRanges (SkipList.cpp:899-924, 414-424): for each union segment [B, E):
+// boundaries in [B, E) are removed, B is written at `now`, and E keeps the version it had
+// (SkipList.cpp:419) unless a boundary at E already exists or the next segment starts at E.
+
+__device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w, int pos, int end) {
+    const int g = (int)item_range(w.pmeta[pos]);
+    return b.keys[2 * g + end];
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, const uint8_t* htail,
+                                                       const Scalars* sc, int64_t hdr) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int U = sc->n_segments;
+    if (s >= U) return;
+    const int64_t n = sc->n;
+    const DKey kb = seg_key(b, w, w.seg_b[s], 0);
+    const DKey ke = seg_key(b, w, w.seg_e[s], 1);
+    const int64_t lo = hist_lower_bound(h, 0, n, htail, kb, b.tail);
+    const int64_t hi = hist_lower_bound(h, lo, n, htail, ke, b.tail);
+    const bool exact = hi < n && hist_cmp(h, hi, htail, ke, b.tail) == 0;
+    const bool glue = s + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[s + 1], 0), b.tail, ke, b.tail) == 0;
+    const bool endins = !exact && !glue;
+    w.seg_lo[s] = lo;
+    w.seg_hi[s] = hi;
+    w.seg_rem[s] = hi - lo;
+    w.seg_ins[s] = endins ? 2 : 1;
+    w.seg_endins[s] = endins ? 1 : 0;
+    w.seg_vend[s] = hi > 0 ? h.ver[hi - 1] : hdr;
+    w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
+}
+
+__global__ __launch_bounds__(kWG) void k_seg_scan(Work w, Scalars* sc) {
+    __shared__ int64_t sh[16];
+    const int U = sc->n_segments;
+    int64_t rem = wg_scan<int64_t>(
+        U, [&](int64_t s) { return w.seg_rem[s]; }, [&](int64_t s, int64_t p) { w.seg_rem[s] = p; }, sh);
+    int64_t ins = wg_scan<int64_t>(
+        U, [&](int64_t s) { return w.seg_ins[s]; }, [&](int64_t s, int64_t p) { w.seg_ins[s] = p; }, sh);
+    int64_t tl = wg_scan<int64_t>(
+        U, [&](int64_t s) { return w.seg_tlen[s]; }, [&](int64_t s, int64_t p) { w.seg_tlen[s] = p; }, sh);
+    if (threadIdx.x == 0) {
+        // sentinel entries at U: totals, used by the copy kernel for elements after every segment
+        w.seg_rem[U] = rem;
+        w.seg_ins[U] = ins;
+        w.seg_tlen[U] = tl;
+        sc->n_before = sc->n;
+        sc->rem_total = rem;
+        sc->n_next = sc->n - rem + ins;
+        sc->tail_next = sc->tail_used + tl;
+    }
+}
+
+constexpr int kSegLds = 1024;
+
+// Copy surviving old boundaries to their new positions.  Per tile, the segments that can affect
+// it are staged in LDS; element i is removed iff lo_j <= i < hi_j for the last segment j with
+// lo_j <= i, else it moves to i - rem_before + ins_before.
+__global__ __launch_bounds__(kBlock) void k_merge_copy(Work w, Hist src, Hist dst, const Scalars* sc) {
+    __shared__ int64_t s_lo[kSegLds + 1], s_hi[kSegLds + 1], s_shift[kSegLds + 1];
+    __shared__ int s_j0, s_cnt;
+    const int64_t n = sc->n;
+    const int U = sc->n_segments;
+    for (int64_t i0 = (int64_t)blockIdx.x * kGcTile; i0 < n; i0 += (int64_t)gridDim.x * kGcTile) {
+        const int64_t i1 = min(n, i0 + kGcTile);
+        if (threadIdx.x == 0) {
+            // ja = #segments with lo <= i0, jb = #segments with lo <= i1-1
+            int lo = 0, hi = U;
+            while (lo < hi) {
+                int mid = (lo + hi) >> 1;
+                if (w.seg_lo[mid] <= i0) lo = mid + 1; else hi = mid;
+            }
+            const int ja = lo;
+            hi = U;
+            while (lo < hi) {
+                int mid = (lo + hi) >> 1;
+                if (w.seg_lo[mid] <= i1 - 1) lo = mid + 1; else hi = mid;
+            }
+            s_j0 = ja;
+            s_cnt = lo - ja;  // segments starting inside the tile
+        }
+        __syncthreads();
+        const int ja = s_j0, cnt = s_cnt;
+        if (cnt <= kSegLds) {
+            // slot k <-> segment ja-1+k for k in [0, cnt]; slot holds lo/hi of that segment and the
+            // shift applying to elements after it (= shift of segment index ja+k as prefix)
+            for (int k = threadIdx.x; k <= cnt; k += blockDim.x) {
+                const int j = ja - 1 + k;
+                s_lo[k] = j >= 0 ? w.seg_lo[j] : LLONG_MIN;
+                s_hi[k] = j >= 0 ? w.seg_hi[j] : LLONG_MIN;
+                s_shift[k] = w.seg_ins[j + 1] - w.seg_rem[j + 1];  // exclusive prefixes at j+1
+            }
+        }
+        __syncthreads();
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+            int64_t seg_lo_v, seg_hi_v, shift;
+            if (cnt <= kSegLds) {
+                int lo = 0, hi = cnt;  // last slot k with s_lo[k] <= i (slot 0 always qualifies)
+                while (lo < hi) {
+                    int mid = (lo + hi + 1) >> 1;
+                    if (s_lo[mid] <= i) lo = mid; else hi = mid - 1;
+                }
+                seg_lo_v = s_lo[lo];
+                seg_hi_v = s_hi[lo];
+                shift = s_shift[lo];
+            } else {
+                int lo = 0, hi = U;
+                while (lo < hi) {
+                    int mid = (lo + hi) >> 1;
+                    if (w.seg_lo[mid] <= i) lo = mid + 1; else hi = mid;
+                }
+                const int j = lo - 1;
+                seg_lo_v = j >= 0 ? w.seg_lo[j] : LLONG_MIN;
+                seg_hi_v = j >= 0 ? w.seg_hi[j] : LLONG_MIN;
+                shift = w.seg_ins[j + 1] - w.seg_rem[j + 1];
+            }
+            if (i >= seg_lo_v && i < seg_hi_v) continue;  // inside a written span
+            const int64_t o = i + shift;
+            dst.key[o] = src.key[i];
+            dst.lt[o] = src.lt[i];
+            dst.ver[o] = src.ver[i];
+        }
+        __syncthreads();
+    }
+}
+
+// Write each segment's new boundaries: B at `now`, E (when needed) at its previous version.
+__global__ __launch_bounds__(kBlock) void k_merge_insert(BatchDev b, Work w, Hist dst, uint8_t* htail,
+                                                         const Scalars* sc, int64_t now) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int U = sc->n_segments;
+    if (s >= U) return;
+    const int64_t o = w.seg_lo[s] - w.seg_rem[s] + w.seg_ins[s];
+    int64_t toff = sc->tail_used + w.seg_tlen[s];
+    const DKey kb = seg_key(b, w, w.seg_b[s], 0);
+    uint32_t tb = 0;
+    if (kb.len > 16) {
+        tb = (uint32_t)toff;
+        for (uint32_t k = 0; k < kb.len - 16; k++) htail[toff + k] = b.tail[kb.tail + k];
+        toff += kb.len - 16;
+    }
+    dst.key[o] = make_ulonglong2(kb.hi, kb.lo);
+    dst.lt[o] = make_uint2(kb.len, tb);
+    dst.ver[o] = now;
+    if (w.seg_endins[s]) {
+        const DKey ke = seg_key(b, w, w.seg_e[s], 1);
+        uint32_t te = 0;
+        if (ke.len > 16) {
+            te = (uint32_t)toff;
+            for (uint32_t k = 0; k < ke.len - 16; k++) htail[toff + k] = b.tail[ke.tail + k];
+        }
+        dst.key[o + 1] = make_ulonglong2(ke.hi, ke.lo);
+        dst.lt[o + 1] = make_uint2(ke.len, te);
+        dst.ver[o + 1] = w.seg_vend[s];
+    }
+}
+
+void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
+                  Scalars* sc, int64_t now, int64_t header_version, int64_t grid_hint_n, hipEvent_t copy_begin,
+                  hipEvent_t copy_end) {
+    const int Wn = b.W > 0 ? b.W : 1;
+    hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
+                       header_version);
+    hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(kWG), 0, s, w, sc);
+    if (copy_begin) (void)hipEventRecord(copy_begin, s);
+    int64_t tiles = (grid_hint_n + kGcTile - 1) / kGcTile;
+    if (tiles < 1) tiles = 1;
+    if (tiles > 8192) tiles = 8192;
+    hipLaunchKernelGGL(k_merge_copy, dim3((unsigned)tiles), dim3(kBlock), 0, s, w, src, dst, sc);
+    if (copy_end) (void)hipEventRecord(copy_end, s);
+    hipLaunchKernelGGL(k_merge_insert, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, dst, htail, sc,
+                       now);
+}
+
+// ------------------------------------------------------------------ D.RemoveBefore
+//
+// removeBefore (SkipList.cpp:542-571) over the whole history: boundary i is dropped when its
+// version and its predecessor's are both below oldestVersion (verdict-neutral).
+
+__device__ __forceinline__ bool gc_keep(const Hist& h, int64_t i, int64_t v, int64_t hdr) {
+    const int64_t pv = i ? h.ver[i - 1] : hdr;
+    return h.ver[i] >= v || pv >= v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gc_count(Hist h, const Scalars* sc, int64_t v, int64_t hdr,
+                                                     int64_t* tile_cnt) {
+    __shared__ int64_t sh[4];
+    const int64_t n = sc->n_next;
+    const int64_t i0 = (int64_t)blockIdx.x * kGcTile;
+    int64_t c = 0;
+    if (i0 < n) {
+        for (int64_t i = i0 + threadIdx.x; i < min(n, i0 + kGcTile); i += blockDim.x) c += gc_keep(h, i, v, hdr);
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ __launch_bounds__(kWG) void k_gc_spine(int64_t* tile_cnt, int tiles, Scalars* sc) {
+    __shared__ int64_t sh[16];
+    int64_t tot = wg_scan<int64_t>(
+        tiles, [&](int64_t k) { return tile_cnt[k]; }, [&](int64_t k, int64_t p) { tile_cnt[k] = p; }, sh);
+    if (threadIdx.x == 0) sc->n_gc = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gc_scatter(Hist src, Hist dst, const Scalars* sc, int64_t v,
+                                                       int64_t hdr, const int64_t* tile_off) {
+    __shared__ int64_t sh[16];
+    const int64_t n = sc->n_next;
+    const int64_t i0 = (int64_t)blockIdx.x * kGcTile;
+    if (i0 >= n) return;
+    constexpr int kPer = kGcTile / kBlock;  // contiguous elements per thread
+    const int64_t a = i0 + (int64_t)threadIdx.x * kPer;
+    uint32_t keepmask = 0;
+    int64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int64_t i = a + k;
+        if (i < n && gc_keep(src, i, v, hdr)) {
+            keepmask |= 1u << k;
+            c++;
+        }
+    }
+    int64_t tot;
+    int64_t o = tile_off[blockIdx.x] + block_excl_sum<int64_t>(c, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        if (keepmask >> k & 1) {
+            const int64_t i = a + k;
+            dst.key[o] = src.key[i];
+            dst.lt[o] = src.lt[i];
+            dst.ver[o] = src.ver[i];
+            o++;
+        }
+    }
+}
+
+void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
+               int64_t header_version, int64_t grid_hint_n) {
+    int64_t tiles = (grid_hint_n + kGcTile - 1) / kGcTile;
+    if (tiles < 1) tiles = 1;
+    hipLaunchKernelGGL(k_gc_count, dim3((unsigned)tiles), dim3(kBlock), 0, s, src, sc, oldest, header_version,
+                       w.tile_cnt);
+    hipLaunchKernelGGL(k_gc_spine, dim3(1), dim3(kWG), 0, s, w.tile_cnt, (int)tiles, sc);
+    hipLaunchKernelGGL(k_gc_scatter, dim3((unsigned)tiles), dim3(kBlock), 0, s, src, dst, sc, oldest,
+                       header_version, w.tile_cnt);
+}
+
+// ------------------------------------------------------------------ range-max hierarchy
+
+__global__ __launch_bounds__(kBlock) void k_blockmax(const int64_t* in, int64_t* out, const int64_t* n_ptr,
+                                                     int level_shift) {
+    // level L: n_L = ceil(n / 64^L); one wave per 64-element block of level L-1
+    int64_t n = *n_ptr;
+    for (int k = 0; k < level_shift; k++) n = (n + kFan - 1) / kFan;
+    const int64_t nout = (n + kFan - 1) / kFan;
+    const int lane = threadIdx.x & 63;
+    for (int64_t blk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; blk < nout;
+         blk += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t i = blk * kFan + lane;
+        int64_t v = i < n ? in[i] : LLONG_MIN;
+        for (int o = 32; o > 0; o >>= 1) {
+            int64_t y = __shfl_xor(v, o, 64);
+            v = y > v ? y : v;
+        }
+        if (lane == 0) out[blk] = v;
+    }
+}
+
+void launch_blockmax(hipStream_t s, const MaxLevels& m, const int64_t* n_ptr, int64_t grid_hint_n) {
+    int64_t n = grid_hint_n;
+    for (int L = 1; L < kMaxLevels; L++) {
+        const int64_t blocks = (n + kFan - 1) / kFan;  // output elements = waves
+        int64_t grid = (blocks * 64 + kBlock - 1) / kBlock;
+        if (grid < 1) grid = 1;
+        if (grid > 16384) grid = 16384;
+        hipLaunchKernelGGL(k_blockmax, dim3((unsigned)grid), dim3(kBlock), 0, s, m.lvl[L - 1], m.lvl[L], n_ptr,
+                           L - 1);
+        n = blocks;
+    }
+}
+
+// ------------------------------------------------------------------ verdicts
+
+__global__ __launch_bounds__(kBlock) void k_finalize(BatchDev b, Work w, Scalars* sc, int gc_ran) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < b.T) {
+        uint8_t v;
+        if (b.flags[t] & kFlagTooOld)
+            v = 1;  // TransactionTooOld (ConflictSet.h:42)
+        else
+            v = w.status[t] == kCommitted ? 2 : 0;
+        w.verdict[t] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        sc->n = gc_ran ? sc->n_gc : sc->n_next;
+        sc->tail_used = sc->tail_next;
+    }
+}
+
+void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran) {
+    const int T = b.T > 0 ? b.T : 1;
+    hipLaunchKernelGGL(k_finalize, dim3((T + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc, gc_ran);
+}
+
+}  // namespace fdbcs

@@ -1,0 +1,167 @@
+/*
+ * fdb_conflict_set.h — C-ABI of the MI355X-native MVCC conflict-resolution engine.
+ *
+ * Drop-in boundary for the FoundationDB resolver hot path.  Each entry point
+ * replaces one member of the reference interface `fdbserver/ConflictSet.h`
+ * (implemented by `fdbserver/SkipList.cpp`); the citation on every
+ * declaration names the reference line it stands in for.  Plain C types only:
+ * pointers, sizes, int64 versions.  No entry point throws; every fallible call
+ * returns an `int` status (FDBCS_OK == 0, negative on error).
+ *
+ * Semantics are those of the reference:
+ *   - keys are unsigned byte strings, compared memcmp-then-length
+ *     (SkipList.cpp:53-60, flow/Arena.h:692-697);
+ *   - a transaction is TooOld iff read_snapshot < oldestVersion and it has at
+ *     least one read range (SkipList.cpp:770);
+ *   - history conflict: some read range [b,e) overlaps history written at a
+ *     version > read_snapshot (SkipList.cpp:619-706);
+ *   - intra-batch conflict: in batch order, a read range overlaps a write range
+ *     of an earlier committed transaction of the same batch (SkipList.cpp:812-834);
+ *   - committed write ranges are recorded at version `now` (SkipList.cpp:899-939);
+ *   - verdict bytes use the reference enum: 0 = TransactionConflict,
+ *     1 = TransactionTooOld, 2 = TransactionCommitted (ConflictSet.h:40-44).
+ *
+ * Threading: like the reference (single flow thread, Resolver.actor.cpp:179-194)
+ * a conflict set handle is not thread-safe; one handle per GPU.
+ * Precondition the reference relies on implicitly (Resolver orders batches by
+ * version, Resolver.actor.cpp:139-150): `now` never decreases below a version
+ * already written; violating it returns FDBCS_E_VERSION.
+ */
+#ifndef FDB_CONFLICT_SET_H
+#define FDB_CONFLICT_SET_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes. */
+#define FDBCS_OK 0
+#define FDBCS_E_INVALID (-1)   /* bad argument: NULL handle, inverted range (KeyRangeRef throws inverted_range, FDBTypes.h:288-291), ... */
+#define FDBCS_E_DEVICE (-2)    /* HIP runtime error */
+#define FDBCS_E_NOMEM (-3)     /* host or device allocation failed / capacity exceeded */
+#define FDBCS_E_VERSION (-4)   /* `now` below a version already present in the history */
+#define FDBCS_E_STATE (-5)     /* call out of order (e.g. add after detect) */
+#define FDBCS_E_NODEVICE (-6)  /* no HIP device / extension unusable: the product never falls back to the CPU */
+
+/* Verdict bytes: ConflictBatch::TransactionCommitResult (ConflictSet.h:40-44). */
+#define FDBCS_TRANSACTION_CONFLICT 0
+#define FDBCS_TRANSACTION_TOO_OLD 1
+#define FDBCS_TRANSACTION_COMMITTED 2
+
+typedef struct fdbcs_conflict_set fdbcs_conflict_set; /* ConflictSet (SkipList.cpp:730-737) */
+typedef struct fdbcs_batch fdbcs_batch;               /* ConflictBatch (ConflictSet.h:35-69) */
+
+/*
+ * Packed, structure-of-arrays form of a commit batch: the CommitTransactionRef
+ * fields the conflict set reads (CommitTransaction.h:184-188), flattened.
+ * R = read_offsets[n_txn], W = write_offsets[n_txn].
+ * Key k occupies key_bytes[key_offsets[k] .. key_offsets[k+1]).
+ * Read range r (0 <= r < R): begin key 2r, end key 2r+1.
+ * Write range w (0 <= w < W): begin key 2(R+w), end key 2(R+w)+1.
+ * Ranges of transaction t: reads [read_offsets[t], read_offsets[t+1]),
+ * writes [write_offsets[t], write_offsets[t+1]), in the transaction's order
+ * (that order defines indexInTx for conflicting-key reports, SkipList.cpp:781).
+ */
+typedef struct fdbcs_packed_batch {
+    int32_t n_txn;
+    const int64_t* read_snapshot;           /* [n_txn] CommitTransactionRef::read_snapshot */
+    const uint8_t* report_conflicting_keys; /* [n_txn] or NULL (= all false) */
+    const int32_t* read_offsets;            /* [n_txn+1] */
+    const int32_t* write_offsets;           /* [n_txn+1] */
+    const uint8_t* key_bytes;               /* key arena */
+    const int64_t* key_offsets;             /* [2*(R+W)+1] */
+} fdbcs_packed_batch;
+
+/* Per-phase device time (HIP events on the engine's stream), accumulated
+ * since the last reset.  Phase names mirror the reference PerfDoubleCounters
+ * D.CheckRead / D.Sort / D.CheckIntraBatch / D.Combine / D.MergeWrite /
+ * D.RemoveBefore (SkipList.cpp:49-51). */
+typedef struct fdbcs_stats {
+    int64_t batches;
+    int64_t transactions;
+    int64_t read_ranges;
+    int64_t write_ranges;
+    double ms_upload;       /* H2D of packed batches */
+    double ms_check_read;   /* history check (search + range max) */
+    double ms_sort;         /* endpoint sort */
+    double ms_intra;        /* intra-batch candidate edges + batch-order resolution */
+    double ms_combine;      /* union of committed writes */
+    double ms_merge;        /* merge into history + range-max rebuild */
+    double ms_gc;           /* removeBefore equivalent */
+    double ms_total;        /* whole detect pipeline, device time */
+    int64_t merge_bytes;    /* algorithmic bytes moved by the merge kernels */
+    int64_t merge_launches;
+    double ms_merge_kernel; /* device time of the dominant history-rewrite kernel alone */
+} fdbcs_stats;
+
+/* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
+int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out);
+/* clearConflictSet(cs, v) — SkipList.cpp:742-744: history reset to all-v, oldestVersion kept. */
+int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version);
+/* destroyConflictSet(cs) — SkipList.cpp:745-747. */
+void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs);
+
+/* Raise-only oldestVersion (the effect of SkipList.cpp:880-882 without GC);
+ * affects the next batch's TooOld test (SkipList.cpp:770). */
+int fdbcs_set_oldest_version(fdbcs_conflict_set* cs, int64_t version);
+int fdbcs_get_oldest_version(const fdbcs_conflict_set* cs, int64_t* out);
+/* Live boundaries in the device history (SkipList::count, SkipList.cpp:386-394, up to GC laziness). */
+int fdbcs_history_size(fdbcs_conflict_set* cs, int64_t* out);
+/* Bulk-load a history: boundaries sorted strictly ascending, boundary i holds
+ * version versions[i] for keys in [key_i, key_{i+1}); keys below the first
+ * boundary read `header_version`.  Used by benchmarks to prefill an MVCC window. */
+int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_bytes,
+                       const int64_t* key_offsets, const int64_t* versions, int64_t header_version);
+int fdbcs_get_stats(fdbcs_conflict_set* cs, fdbcs_stats* out);
+int fdbcs_reset_stats(fdbcs_conflict_set* cs);
+/* Pre-size device capacity (history boundaries, history tail bytes, and the largest batch
+ * shape) so later batches never reallocate; sizes are upper bounds, 0 keeps the current. */
+int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes, int32_t max_txns,
+                  int32_t max_reads, int32_t max_writes);
+/* Garbage-collection cadence: GC runs on every `every`-th batch whose
+ * newOldestVersion advanced (default 1).  GC is verdict-neutral. */
+int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every);
+
+/* ConflictBatch(cs, conflictingKeyRangeMap, arena) — SkipList.cpp:749-752.
+ * report_keys != 0 enables conflictingKeyRangeMap collection for transactions
+ * that set report_conflicting_keys. */
+int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out);
+void fdbcs_batch_destroy(fdbcs_batch* b);
+/* ConflictBatch::addTransaction(tr) — SkipList.cpp:763-794.  Keys are copied. */
+int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int report_conflicting_keys,
+                                int32_t n_reads, const uint8_t* const* read_begin,
+                                const int32_t* read_begin_len, const uint8_t* const* read_end,
+                                const int32_t* read_end_len, int32_t n_writes,
+                                const uint8_t* const* write_begin, const int32_t* write_begin_len,
+                                const uint8_t* const* write_end, const int32_t* write_end_len);
+/* addTransaction for every transaction of a packed batch, in order. */
+int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb);
+/* Stage the batch in HBM now (async H2D on the engine stream).  Optional:
+ * detect uploads implicitly.  Lets callers keep PCIe out of a timed region. */
+int fdbcs_batch_upload(fdbcs_batch* b);
+/* ConflictBatch::detectConflicts(now, newOldestVersion, nonConflicting, tooOld)
+ * — SkipList.cpp:844-890.  verdicts[t] receives 0/1/2 per transaction
+ * (Resolver.actor.cpp:196-204 encoding); counts are optional (NULL). */
+int fdbcs_batch_detect_conflicts(fdbcs_batch* b, int64_t now, int64_t new_oldest_version,
+                                 uint8_t* verdicts, int32_t* n_committed, int32_t* n_too_old);
+/* Asynchronous form: enqueue the pipeline, return immediately; the verdicts of
+ * the batch are fetched with fdbcs_batch_wait.  Batches must be waited in
+ * submission order before the set is used for anything else. */
+int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_version);
+int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, int32_t* n_too_old);
+/* conflictingKeyRangeMap[txn] (SkipList.cpp:641-645, 822-825): read-range
+ * indices (indexInTx) that conflicted, ascending.  Valid after detect. */
+int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out, int32_t cap,
+                                  int32_t* n_out);
+/* Device pointer to the batch's per-transaction verdict bytes (valid after
+ * detect until the batch is destroyed) for on-device combine (RCCL). */
+int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr);
+
+const char* fdbcs_strerror(int status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FDB_CONFLICT_SET_H */

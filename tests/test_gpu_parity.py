@@ -1,0 +1,221 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle, bit-exact verdicts and
+conflicting-key reports, on the reference's known answers, frozen fixtures, live random batches,
+the BASELINE configurations (reduced where the oracle must keep up) and size-independent
+properties at full size."""
+import os
+
+import numpy as np
+import pytest
+
+from foundationdb_amd import workloads as W
+from foundationdb_amd.packing import CommitTransaction, KeyRange, PackedBatch
+from tests.helpers import EngineDriver, load_json, nonempty, random_fixture_sequences, scenario_batches
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def oracle_mod():
+    from oracle import oracle
+
+    oracle.build()
+    return oracle
+
+
+def run_pair(engine, oracle_mod, seq, gc_interval=1, clear=None, check_conf=True, ref="oracle"):
+    e = EngineDriver(engine, gc_interval=gc_interval)
+    o = oracle_mod.OracleConflictSet() if ref == "oracle" else oracle_mod.SkipListBaseline()
+    if clear is not None:
+        e.clear(clear)
+        o.clear(clear)
+    for i, (pb, now, no) in enumerate(seq):
+        ve, ce = e.detect(pb, now, no)
+        vo, co = o.detect(pb, now, no)
+        assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10], ve[ve != vo][:10], vo[ve != vo][:10])
+        if check_conf:
+            assert ce == nonempty(co), i
+    return e, o
+
+
+def test_kat_scenarios(engine):
+    for scn in load_json("kat_scenarios.json"):
+        e = EngineDriver(engine)
+        for i, (pb, now, no, expect, conf) in enumerate(scenario_batches(scn)):
+            if scn.get("clear_before") == i:
+                e.clear(scn["clear_version"])
+            v, c = e.detect(pb, now, no)
+            assert v.tolist() == expect, (scn["name"], i, v.tolist(), expect)
+            if conf:
+                assert c == conf, (scn["name"], c, conf)
+
+
+def test_frozen_random_fixtures(engine):
+    for s, seq in random_fixture_sequences():
+        e = EngineDriver(engine)
+        for pb, now, no, verdict, conf in seq:
+            v, c = e.detect(pb, now, no)
+            assert (v == verdict).all(), s
+            assert c == conf, s
+
+
+@pytest.mark.parametrize("alphabet,max_len", [(2, 2), (3, 3), (4, 5), (256, 2), (3, 24), (2, 40)])
+def test_random_vs_oracle(engine, oracle_mod, alphabet, max_len):
+    rng = np.random.default_rng(alphabet * 100 + max_len)
+    for trial in range(12):
+        seq = []
+        now = 10
+        for _ in range(6):
+            pb = W.random_small_batch(rng, int(rng.integers(1, 120)), alphabet=alphabet, max_len=max_len, now=now,
+                                      staleness=15, max_reads=4, max_writes=3)
+            seq.append((pb, now, now - int(rng.integers(0, 12))))
+            now += int(rng.integers(1, 6))
+        run_pair(engine, oracle_mod, seq, gc_interval=1 + trial % 3, clear=(5 if trial % 5 == 0 else None))
+
+
+def test_shared_long_prefixes(engine, oracle_mod):
+    """Tuple-like keys sharing > 16-byte prefixes exercise the tail comparison everywhere."""
+    rng = np.random.default_rng(99)
+    prefix = b"\x01subspace\x00\x02users\x00"
+    seq = []
+    now = 10
+    for _ in range(8):
+        txns = []
+        for _ in range(80):
+            def key():
+                return prefix + bytes(rng.integers(0, 3, size=int(rng.integers(0, 4))).astype(np.uint8))
+
+            def rr():
+                a, b = key(), key()
+                return KeyRange(min(a, b), max(a, b))
+
+            txns.append(CommitTransaction([rr() for _ in range(int(rng.integers(0, 3)))],
+                                          [rr() for _ in range(int(rng.integers(0, 3)))],
+                                          now - int(rng.integers(0, 10)), bool(rng.random() < 0.5)))
+        seq.append((PackedBatch.from_transactions(txns), now, now - 8))
+        now += 3
+    run_pair(engine, oracle_mod, seq)
+
+
+def test_c1_skiplisttest(engine, oracle_mod):
+    seq = list(W.c1_batches(25, seed=7))
+    e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
+    # GC is eager in both (interval 1, full): same step function size
+    assert e.cs.history_size() == o.history_size()
+
+
+def test_c2_reduced(engine, oracle_mod):
+    p = W.C2Params(txns=2000, history=200_000)
+    kb, ko, vers = W.c2_history(p, seed=1, start_version=10_000_000)
+    e = EngineDriver(engine, gc_interval=4)
+    o = oracle_mod.SkipListBaseline()
+    e.load_history(kb, ko, vers)
+    o.load_history(kb, ko, vers)
+    rng = np.random.default_rng(2)
+    now = 10_000_000
+    for i in range(10):
+        now += p.version_step
+        pb = W.c2_batch(p, rng, now)
+        ve, _ = e.detect(pb, now, now - p.window)
+        vo, _ = o.detect(pb, now, now - p.window)
+        assert (ve == vo).all(), i
+
+
+def test_c3_zipf_heavy_contention(engine, oracle_mod):
+    p = W.C2Params(txns=3000)
+    z = W.ZipfGenerator(1_000_000, 0.99)
+    rng = np.random.default_rng(3)
+    seq = []
+    now = 1000
+    for _ in range(6):
+        now += 1000
+        seq.append((W.c3_batch(p, rng, now, z), now, now - 100_000))
+    e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
+
+
+def test_async_pipelined_batches_match_sync(engine):
+    rng = np.random.default_rng(4)
+    batches = []
+    now = 10
+    for _ in range(8):
+        batches.append((W.random_small_batch(rng, 200, alphabet=4, max_len=4, now=now, staleness=10), now, now - 5))
+        now += 2
+    sync = EngineDriver(engine)
+    want = [sync.detect(pb, n, no)[0] for pb, n, no in batches]
+    cs = engine.ConflictSet(0)
+    objs = []
+    for pb, n, no in batches:
+        b = engine.ConflictBatch(cs)
+        b.add_packed(pb)
+        b.upload()
+        b.detect_async(n, no)
+        objs.append(b)
+    for b, w in zip(objs, want):
+        assert (b.wait() == w).all()
+
+
+def test_gc_interval_is_verdict_neutral(engine):
+    rng = np.random.default_rng(6)
+    seq = []
+    now = 10
+    for _ in range(12):
+        seq.append((W.random_small_batch(rng, 150, alphabet=3, max_len=4, now=now, staleness=9), now, now - 4))
+        now += 3
+    a, b = EngineDriver(engine, gc_interval=1), EngineDriver(engine, gc_interval=1000)
+    for pb, n, no in seq:
+        assert (a.detect(pb, n, no)[0] == b.detect(pb, n, no)[0]).all()
+    assert a.cs.history_size() <= b.cs.history_size()
+
+
+def test_edge_cases(engine):
+    e = EngineDriver(engine)
+    empty = PackedBatch.from_transactions([])
+    v, _ = e.detect(empty, 5, 0)
+    assert v.size == 0
+    # transactions with no ranges commit; version going backwards is refused
+    pb = PackedBatch.from_transactions([CommitTransaction(), CommitTransaction(write_conflict_ranges=[KeyRange(b"a", b"b")])])
+    v, _ = e.detect(pb, 10, 0)
+    assert v.tolist() == [2, 2]
+    with pytest.raises(engine.FdbcsError) as ex:
+        e.detect(pb, 9, 0)
+    assert ex.value.status == engine.FDBCS_E_VERSION
+
+
+def test_sequential_fallback_matches(engine, oracle_mod, monkeypatch):
+    """Force the candidate-edge overflow path (sequential MiniConflictSet replay on the GPU)."""
+    monkeypatch.setenv("FDBCS_EDGE_CAP", "8")
+    rng = np.random.default_rng(8)
+    seq = []
+    now = 10
+    for _ in range(4):
+        seq.append((W.random_small_batch(rng, 100, alphabet=2, max_len=3, now=now, staleness=10, report_frac=1.0),
+                    now, now - 3))
+        now += 2
+    run_pair(engine, oracle_mod, seq)
+
+
+def test_full_size_c2_properties(engine, oracle_mod):
+    """BASELINE config C2 at full size (5M-boundary history, 5000 txns x 5R+2W): determinism
+    (two engines, identical verdicts), parity with the skip-list restatement on the first
+    batches, and history growth bounded by 2 boundaries per committed write."""
+    p = W.C2Params()
+    kb, ko, vers = W.c2_history(p, seed=1, start_version=10_000_000)
+    a, b = EngineDriver(engine, gc_interval=8), EngineDriver(engine, gc_interval=1)
+    a.load_history(kb, ko, vers)
+    b.load_history(kb, ko, vers)
+    o = oracle_mod.SkipListBaseline()
+    o.load_history(kb, ko, vers)
+    rng = np.random.default_rng(12)
+    now = 10_000_000
+    n0 = a.cs.history_size()
+    assert n0 == len(vers)
+    committed_writes = 0
+    for i in range(4):
+        now += p.version_step
+        pb = W.c2_batch(p, rng, now)
+        va, _ = a.detect(pb, now, now - p.window)
+        vb, _ = b.detect(pb, now, now - p.window)
+        assert (va == vb).all()
+        vo, _ = o.detect(pb, now, now - p.window)
+        assert (va == vo).all(), i
+        committed_writes += int((va == 2).sum()) * p.writes
+    assert a.cs.history_size() <= n0 + 2 * committed_writes
