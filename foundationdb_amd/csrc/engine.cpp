@@ -113,6 +113,7 @@ struct fdbcs_conflict_set {
     int64_t edge_cap = 0;
 
     int inflight = 0;
+    bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
     fdbcs_stats stats{};
 };
 
@@ -408,6 +409,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     fdbcs_conflict_set* cs = new (std::nothrow) fdbcs_conflict_set();
     if (!cs) return FDBCS_E_NOMEM;
     cs->device = device;
+    if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
     if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) {
         delete cs;
         return FDBCS_E_DEVICE;
@@ -567,8 +569,11 @@ int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) 
 
 void fdbcs_batch_destroy(fdbcs_batch* b) {
     if (!b) return;
-    (void)hipSetDevice(b->cs->device);
-    if (b->state == 2) (void)hipStreamSynchronize(b->cs->stream);
+    if (b->state == 2) {  // still in flight: its set (which must outlive it) owns the stream
+        (void)hipSetDevice(b->cs->device);
+        (void)hipStreamSynchronize(b->cs->stream);
+        b->cs->inflight--;
+    }
     if (b->events_made)
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(b->ev[i]);
     b->dev.release();
@@ -722,12 +727,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     MaxLevels lv = levels_of(cs, src);
 
     if (T) HIPOK(hipMemsetAsync(w.hist_conf, 0, T, s));
+    if (cs->validate) HIPOK(hipMemsetAsync(&sc->debug_error, 0, sizeof(int32_t), s));
     launch_check_reads(s, bd, hs, lv, (const uint8_t*)cs->htail.p, sc, cs->header_version, w);
     HIPOK(hipEventRecord(b->ev[kPhCheck], s));
     int sorted = 0;
     launch_sort_points(s, bd, w, &sorted);
     HIPOK(hipEventRecord(b->ev[kPhSort], s));
     launch_positions(s, bd, w, sorted);
+    if (cs->validate) launch_validate_sort(s, bd, w, sorted, sc);
     launch_edges(s, bd, w, sc);
     launch_resolve(s, bd, w, sc);
     HIPOK(hipEventRecord(b->ev[kPhIntra], s));
@@ -781,6 +788,12 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
     if (b->state == 2) {
         HIPOK(hipSetDevice(cs->device));
         HIPOK(hipEventSynchronize(b->ev[kPhEnd]));
+        if (b->h_scal->debug_error) {
+            fprintf(stderr, "fdbcs: device invariant check failed (debug_error=%d)\n", b->h_scal->debug_error);
+            cs->inflight--;
+            b->state = 3;
+            return FDBCS_E_DEVICE;
+        }
         const int32_t T = b->T();
         int32_t nc = 0, nt = 0;
         for (int32_t t = 0; t < T; t++) {

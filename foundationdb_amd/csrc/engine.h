@@ -14,7 +14,8 @@ constexpr int kSortTile = 2048;    // endpoints per LDS sort tile (256 threads x
 constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
 constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)
 constexpr int kGcTile = 4096;      // history elements per GC / merge tile
-constexpr int kMaxTxnLds = 65536;  // transactions whose status fits the resolver's LDS
+constexpr int kMaxTxnLds = 49152;  // transactions whose status bytes fit the resolver's LDS (> the
+                                   // reference's 32768-transaction batch cap, fdbserver/Knobs.cpp:370)
 
 // Transaction status during batch-order resolution.
 enum : uint8_t { kUndecided = 0, kAborted = 1, kCommitted = 2 };
@@ -44,7 +45,7 @@ struct Scalars {
     int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
     int64_t n_edges;
     int32_t rounds;        // resolution rounds used
-    int32_t pad;
+    int32_t debug_error;   // FDBCS_VALIDATE: invariant violated
     int64_t n_before;      // history size at the start of the merge
     int64_t rem_total;     // boundaries removed by union segments
 };
@@ -103,6 +104,7 @@ void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const M
                         const Scalars* sc, int64_t header_version, const Work& w);
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
+void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);

@@ -216,7 +216,18 @@ __device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortIt
     }
 }
 
-// Sort one tile of kSortTile endpoints in LDS (runs 1,2,4,... merged by merge path).
+// Compare-exchange of two register items (constant indices keep them in VGPRs).
+__device__ __forceinline__ void cex(SortItem& a, SortItem& b, bool active, const uint8_t* arena) {
+    if (active && item_less(b, a, arena)) {
+        SortItem t = a;
+        a = b;
+        b = t;
+    }
+}
+
+// Sort one tile of kSortTile endpoints: each thread sorts its 8 items with Batcher's odd-even
+// merge network (19 comparators, items past `mine` stay put), then runs of 8, 16, ... are merged
+// in LDS by merge path (each thread's 8 outputs always fall inside one pair of runs).
 __global__ __launch_bounds__(kBlock) void k_sort_tile(const SortItem* in, SortItem* out, int n,
                                                       const uint8_t* arena) {
     __shared__ SortItem sh[kSortTile];
@@ -227,7 +238,22 @@ __global__ __launch_bounds__(kBlock) void k_sort_tile(const SortItem* in, SortIt
     const int o = threadIdx.x * 8;
     const int mine = max(0, min(8, cnt - o));
     SortItem r[8];
-    for (int w = 1; w < cnt; w <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (k < mine) r[k] = sh[o + k];
+#define CEX(i, j) cex(r[i], r[j], (j) < mine, arena)
+    CEX(0, 1); CEX(2, 3); CEX(4, 5); CEX(6, 7);
+    CEX(0, 2); CEX(1, 3); CEX(4, 6); CEX(5, 7);
+    CEX(1, 2); CEX(5, 6);
+    CEX(0, 4); CEX(1, 5); CEX(2, 6); CEX(3, 7);
+    CEX(2, 4); CEX(3, 5);
+    CEX(1, 2); CEX(3, 4); CEX(5, 6);
+#undef CEX
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (k < mine) sh[o + k] = r[k];
+    __syncthreads();
+    for (int w = 8; w < cnt; w <<= 1) {
         const int pb = (o / (2 * w)) * (2 * w);
         const int lenA = max(0, min(w, cnt - pb));
         const int lenB = max(0, min(w, cnt - pb - w));
@@ -309,7 +335,20 @@ __global__ __launch_bounds__(kBlock) void k_positions(const SortItem* sorted, in
     if (p >= E) return;
     const uint32_t meta = sorted[p].meta;
     pmeta[p] = meta;
-    pos[2 * item_range(meta) + item_is_end(meta)] = p;  // KeyInfo::pIndex (SkipList.cpp:814)
+    const uint32_t slot = 2 * item_range(meta) + item_is_end(meta);
+    if (slot < (uint32_t)E) pos[slot] = p;  // KeyInfo::pIndex (SkipList.cpp:814)
+}
+
+// FDBCS_VALIDATE=1: check the endpoint order and that positions invert the permutation.
+__global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted, const int32_t* pos,
+                                                          const uint32_t* pmeta, int E, const uint8_t* arena,
+                                                          Scalars* sc) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= E) return;
+    bool bad = p > 0 && item_less(sorted[p], sorted[p - 1], arena);
+    const int q = pos[p];  // slot p -> position
+    bad |= q < 0 || q >= E || (2 * item_range(pmeta[q]) + item_is_end(pmeta[q])) != (uint32_t)p;
+    if (bad) atomicOr(&sc->debug_error, 1);
 }
 
 // Exclusive counts of write-begins (high word) and read-begins (low word) before each position,
@@ -338,6 +377,13 @@ void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorte
     hipLaunchKernelGGL(k_positions, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf], E,
                        w.pos, w.pmeta);
     hipLaunchKernelGGL(k_begin_lists, dim3(1), dim3(kWG), 0, s, w.pmeta, E, w.cnt_pair, w.wbpos, w.rbpos);
+}
+
+void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc) {
+    const int E = 2 * (b.R + b.W);
+    if (E == 0) return;
+    hipLaunchKernelGGL(k_validate_sort, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf],
+                       w.pos, w.pmeta, E, b.tail, sc);
 }
 
 // ------------------------------------------------------------------ D.CheckIntraBatch: candidate edges
@@ -544,11 +590,6 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc
     if (b.T == 0) return;
     const int E = 2 * (b.R + b.W);
     (void)hipMemsetAsync(w.mcs_bits, 0, sizeof(uint64_t) * (E / 64 + 1), s);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxTxnLds);
-        attr_set = true;
-    }
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWG), (size_t)b.T, s, b, w, sc);
     if (b.R) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
 }

@@ -63,6 +63,9 @@ class KeyRangeSharding:
 
     def _shard_span(self, pb: PackedBatch, kb: np.ndarray, ke: np.ndarray):
         """(g0, g1) per range: rangeContaining(begin) .. last shard whose start < end."""
+        if self.G == 1:
+            z = np.zeros(len(kb), np.int64)
+            return z, z
         if self._byte_splits is not None:
             fb = self._first_bytes(pb, kb)
             fe = self._first_bytes(pb, ke)

@@ -25,6 +25,7 @@ def engine():
     """The HIP engine; GPU tests only.  Builds in-tree if needed and fails loudly without a device."""
     from foundationdb_amd import build, conflict_set
 
+    os.environ.setdefault("FDBCS_VALIDATE", "1")  # device-side sort/permutation invariant checks
     build.build()
     conflict_set.load_library()
     return conflict_set

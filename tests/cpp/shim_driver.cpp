@@ -1,0 +1,60 @@
+// Drives the reference-shaped C++ API (include/conflict_set_shim.hpp) with stand-in
+// CommitTransactionRef/KeyRangeRef types, the way Resolver.actor.cpp:179-194 does.
+// Prints one verdict digit per transaction per batch.
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "conflict_set_shim.hpp"
+
+struct Ref {  // StringRef-like
+    std::string s;
+    const uint8_t* begin() const { return (const uint8_t*)s.data(); }
+    int size() const { return (int)s.size(); }
+};
+struct Range {
+    Ref begin, end;
+};
+struct Txn {
+    std::vector<Range> read_conflict_ranges, write_conflict_ranges;
+    int64_t read_snapshot = 0;
+    bool report_conflicting_keys = false;
+};
+
+int main() {
+    ConflictSet* cs = newConflictSet();
+    // batch 1: T0 writes [k, k\0); T1 reads it (intra-batch conflict); T2 reads [a, b)
+    {
+        std::map<int, std::vector<int>> ckr;
+        ConflictBatch batch(cs, &ckr);
+        Txn t0, t1, t2;
+        t0.write_conflict_ranges.push_back({{"k"}, {std::string("k\0", 2)}});
+        t1.read_conflict_ranges.push_back({{"k"}, {std::string("k\0", 2)}});
+        t1.report_conflicting_keys = true;
+        t2.read_conflict_ranges.push_back({{"a"}, {"b"}});
+        batch.addTransaction(t0);
+        batch.addTransaction(t1);
+        batch.addTransaction(t2);
+        std::vector<int> ok, tooOld;
+        batch.detectConflicts(10, 0, ok, &tooOld);
+        printf("b1 commit=%zu tooold=%zu report1=%zu\n", ok.size(), tooOld.size(), ckr[1].size());
+    }
+    // batch 2: snapshot 5 reads of k see version 10 -> conflict; snapshot 10 commits
+    {
+        ConflictBatch batch(cs);
+        Txn a, b;
+        a.read_conflict_ranges.push_back({{"k"}, {"l"}});
+        a.read_snapshot = 5;
+        b.read_conflict_ranges.push_back({{"k"}, {"l"}});
+        b.read_snapshot = 10;
+        batch.addTransaction(a);
+        batch.addTransaction(b);
+        std::vector<int> ok;
+        batch.detectConflicts(20, 0, ok);
+        printf("b2 commit=%zu first=%d\n", ok.size(), ok.empty() ? -1 : ok[0]);
+    }
+    destroyConflictSet(cs);
+    return 0;
+}

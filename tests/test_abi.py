@@ -78,3 +78,21 @@ def test_product_never_imports_oracle():
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in txt and "from oracle" not in txt, f
                 assert "liboracle" not in txt and "skiplist_baseline" not in txt, f
+
+
+def build_shim_driver(out_path):
+    from foundationdb_amd import build
+
+    build.build()
+    src = os.path.join(ROOT, "tests", "cpp", "shim_driver.cpp")
+    subprocess.check_call(
+        ["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"), src, "-L",
+         os.path.join(ROOT, "foundationdb_amd"), "-lfdbcs", f"-Wl,-rpath,{os.path.join(ROOT, 'foundationdb_amd')}",
+         "-o", out_path]
+    )
+    return out_path
+
+
+def test_reference_shaped_cpp_shim_compiles_and_links(tmp_path):
+    """include/conflict_set_shim.hpp restores the ConflictSet.h signatures over the C-ABI."""
+    assert os.path.exists(build_shim_driver(str(tmp_path / "shim_driver")))

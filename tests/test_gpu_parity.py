@@ -219,3 +219,15 @@ def test_full_size_c2_properties(engine, oracle_mod):
         assert (va == vo).all(), i
         committed_writes += int((va == 2).sum()) * p.writes
     assert a.cs.history_size() <= n0 + 2 * committed_writes
+
+
+def test_cpp_shim_driver(tmp_path):
+    """The reference-shaped C++ API (conflict_set_shim.hpp) end to end on the GPU."""
+    import subprocess
+
+    from tests.test_abi import build_shim_driver
+
+    exe = build_shim_driver(str(tmp_path / "shim_driver"))
+    out = subprocess.check_output([exe], text=True, timeout=120)
+    assert "b1 commit=2 tooold=0 report1=1" in out, out
+    assert "b2 commit=1 first=1" in out, out
