@@ -15,6 +15,8 @@ step() {  # name, timeout, command...
 }
 step tests 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
 tail -30 gpurun_out/gpu_tests.log >&2
+if [ "${REQUIRE_PASS:-1}" = "1" ] && ! grep -q " passed" gpurun_out/gpu_tests.log; then echo "no passing tests; stop" >&2; exit 1; fi
+if [ "${REQUIRE_PASS:-1}" = "1" ] && grep -q " failed" gpurun_out/gpu_tests.log; then echo "tests failed; skipping bench" >&2; exit 1; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 tail -5 gpurun_out/smoke.log >&2
 step bench 600 python bench.py ${BENCH_ARGS:---steps 30 --warmup 3} > gpurun_out/bench.json 2> gpurun_out/bench.err
