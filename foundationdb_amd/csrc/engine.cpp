@@ -173,6 +173,18 @@ int cmp_bytes(const uint8_t* a, int32_t al, const uint8_t* b, int32_t bl) {
     return (al > bl) - (al < bl);
 }
 
+// Scan arena for the current workspace shape and history capacity (zeroed per batch by k_prepare).
+int ensure_scan_arena(fdbcs_conflict_set* cs) {
+    if (cs->ws_T < 0 || cs->hist_cap <= 0) return FDBCS_OK;
+    const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap);
+    int rc = cs->ws[39].ensure(8 * words + 64);
+    if (rc) return rc;
+    cs->work.scan_arena = (uint64_t*)cs->ws[39].p;
+    carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap);
+    for (int k = 0; k < kNumScans; k++) cs->work.scan[k].error = &((Scalars*)cs->scal.p)->debug_error;
+    return FDBCS_OK;
+}
+
 // Workspace sized for (T, R, W); edge capacity grows with R.
 int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     if (T <= cs->ws_T && R <= cs->ws_R && W <= cs->ws_W) return FDBCS_OK;
@@ -202,7 +214,9 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(items[1], sizeof(SortItem) * E);
     TAKE(pos, 4 * E);
     TAKE(pmeta, 4 * E);
-    TAKE(cnt_pair, 8 * (E + 1));
+    TAKE(cwb, 4 * (E + 1));
+    TAKE(crb, 4 * (E + 1));
+    TAKE(segflag, E + 1);
     TAKE(wbpos, 4 * W);
     TAKE(rbpos, 4 * R);
     TAKE(ecnt_a, 4 * R);
@@ -229,16 +243,9 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     cs->ws_T = T;
     cs->ws_R = R;
     cs->ws_W = W;
-    return FDBCS_OK;
+    return ensure_scan_arena(cs);
 }
 
-int ensure_tile_cnt(fdbcs_conflict_set* cs, int64_t n) {
-    const int64_t tiles = (n + kGcTile - 1) / kGcTile + 1;
-    int rc = cs->ws[39].ensure(8 * tiles);
-    if (rc) return rc;
-    cs->work.tile_cnt = (int64_t*)cs->ws[39].p;
-    return FDBCS_OK;
-}
 
 Hist hist_of(fdbcs_conflict_set* cs, int k) {
     Hist h;
@@ -315,7 +322,7 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
     launch_blockmax(cs->stream, lv, &((Scalars*)cs->scal.p)->n, std::max<int64_t>(n, 1));
     HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(cs->stream));
-    return ensure_tile_cnt(cs, cap);
+    return ensure_scan_arena(cs);
 }
 
 int ensure_events(fdbcs_batch* b) {
@@ -726,8 +733,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     Hist hs = hist_of(cs, src), hd = hist_of(cs, src ^ 1);
     MaxLevels lv = levels_of(cs, src);
 
-    if (T) HIPOK(hipMemsetAsync(w.hist_conf, 0, T, s));
-    if (cs->validate) HIPOK(hipMemsetAsync(&sc->debug_error, 0, sizeof(int32_t), s));
+    launch_prepare(s, bd, w, sc);
     launch_check_reads(s, bd, hs, lv, (const uint8_t*)cs->htail.p, sc, cs->header_version, w);
     HIPOK(hipEventRecord(b->ev[kPhCheck], s));
     int sorted = 0;
@@ -758,11 +764,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     MaxLevels lf = levels_of(cs, final_buf);
     launch_blockmax(s, lf, gc ? &sc->n_gc : &sc->n_next, cs->n_ub + 2 * W + 1);
     HIPOK(hipEventRecord(b->ev[kPhGc], s));
-    launch_finalize(s, bd, w, sc, gc ? 1 : 0);
+    launch_finalize(s, bd, w, sc, gc ? 1 : 0, (uint8_t*)b->dverdict.p);
     HIPOK(hipGetLastError());
     // results back
-    if (T) HIPOK(hipMemcpyAsync(b->h_verdict, w.verdict, T, hipMemcpyDeviceToHost, s));
-    if (T) HIPOK(hipMemcpyAsync(b->dverdict.p, w.verdict, T, hipMemcpyDeviceToDevice, s));
+    if (T) HIPOK(hipMemcpyAsync(b->h_verdict, b->dverdict.p, T, hipMemcpyDeviceToHost, s));
     HIPOK(hipMemcpyAsync(b->h_scal, sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
     b->any_report = false;
     for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "dkey.h"
+#include "scan.h"
 
 namespace fdbcs {
 
@@ -41,14 +42,18 @@ struct Scalars {
     int64_t n_gc;          // after GC
     int64_t tail_used;     // bytes used in the history tail arena
     int64_t tail_next;
-    int32_t n_segments;    // union segments of committed writes
-    int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
-    int64_t n_edges;
-    int32_t rounds;        // resolution rounds used
-    int32_t debug_error;   // FDBCS_VALIDATE: invariant violated
+    int64_t n_segments;    // union segments of committed writes
+    int64_t n_edges;       // candidate edges
     int64_t n_before;      // history size at the start of the merge
     int64_t rem_total;     // boundaries removed by union segments
+    int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
+    int32_t rounds;        // resolution rounds used
+    int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
+    int32_t pad;
 };
+
+// Scans of one batch (each owns a slice of the per-batch zeroed scan arena).
+enum ScanKind { kScanPos, kScanEdges, kScanCov, kScanSeg, kScanSegSum, kScanGc, kNumScans };
 
 // Device copy of one batch's packed input (tooOld transactions carry no ranges,
 // as in addTransaction, SkipList.cpp:770-790).
@@ -73,7 +78,9 @@ struct Work {
     SortItem* items[2];    // [E]
     int32_t* pos;          // [2(R+W)] sorted position of each endpoint
     uint32_t* pmeta;       // [E] meta of the item at each position
-    int64_t* cnt_pair;     // [E+1] packed exclusive counts: write-begins << 32 | read-begins
+    int32_t* cwb;          // [E+1] write-begins before each position
+    int32_t* crb;          // [E+1] read-begins before each position
+    uint8_t* segflag;      // [E] bit0: union segment starts here, bit1: one ends here
     int32_t* wbpos;        // [W] positions of write-begins in order
     int32_t* rbpos;        // [R] positions of read-begins in order
     int32_t* ecnt_a;       // [R]
@@ -95,13 +102,16 @@ struct Work {
     int64_t* seg_tlen;
     uint8_t* seg_endins;
     int64_t* seg_vend;
-    int64_t* tile_cnt;     // GC tiles
     uint8_t* verdict;      // [T]
+    ScanState scan[kNumScans];
+    uint64_t* scan_arena;  // zeroed by k_prepare each batch
+    int64_t scan_words;
 };
 
 // ---- launchers (kernels.hip); all enqueue on `s` and never synchronize.
 void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const MaxLevels& m, const uint8_t* htail,
                         const Scalars* sc, int64_t header_version, const Work& w);
+void launch_prepare(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc);
@@ -113,7 +123,9 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   hipEvent_t copy_end);
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
                int64_t header_version, int64_t grid_hint_n);
+int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap);
+void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap);
 void launch_blockmax(hipStream_t s, const MaxLevels& m, const int64_t* n_ptr, int64_t grid_hint_n);
-void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran);
+void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran, uint8_t* verdict_out);
 
 }  // namespace fdbcs

@@ -171,24 +171,44 @@ void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const M
 
 // ------------------------------------------------------------------ D.Sort
 
-__global__ __launch_bounds__(kBlock) void k_make_items(BatchDev b, SortItem* items) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;  // range id: reads then writes
-    if (g >= b.R + b.W) return;
-    const bool is_read = g < b.R;
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-        const DKey k = b.keys[2 * g + e];
-        // extra_ordering (SkipList.cpp:89-91): begin*2 + (write ^ begin)
-        const uint32_t cls = is_read ? (e ? kReadEnd : kReadBegin) : (e ? kWriteEnd : kWriteBegin);
-        SortItem it;
-        it.hi = k.hi;
-        it.lo = k.lo;
-        it.len = k.len;
-        it.tail = k.tail;
-        it.meta = ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
-        it.pad = 0;
-        items[2 * g + e] = it;
+// First kernel of a batch: zero the per-batch scratch (transaction conflict flags, edge counters,
+// the scan arena) and emit the endpoint items (KeyInfo, SkipList.cpp:779-789) for the sort.
+__global__ __launch_bounds__(kBlock) void k_prepare(BatchDev b, Work w, Scalars* sc) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid == 0) sc->debug_error = 0;
+    for (int64_t i = tid; i < w.scan_words; i += stride) w.scan_arena[i] = 0;
+    for (int64_t i = tid; i < b.T; i += stride) w.hist_conf[i] = 0;
+    for (int64_t i = tid; i < b.R; i += stride) {
+        w.ecnt_b[i] = 0;
+        w.ecur[i] = 0;
     }
+    for (int64_t g = tid; g < b.R + b.W; g += stride) {
+        const bool is_read = g < b.R;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const DKey k = b.keys[2 * g + e];
+            // extra_ordering (SkipList.cpp:89-91): begin*2 + (write ^ begin)
+            const uint32_t cls = is_read ? (e ? kReadEnd : kReadBegin) : (e ? kWriteEnd : kWriteBegin);
+            SortItem it;
+            it.hi = k.hi;
+            it.lo = k.lo;
+            it.len = k.len;
+            it.tail = k.tail;
+            it.meta = ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
+            it.pad = 0;
+            w.items[1][2 * g + e] = it;
+        }
+    }
+}
+
+void launch_prepare(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
+    int64_t n = b.R + b.W;
+    n = n > b.T ? n : b.T;
+    n = n > w.scan_words ? n : w.scan_words;
+    int64_t grid = (n + kBlock - 1) / kBlock;
+    grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
+    hipLaunchKernelGGL(k_prepare, dim3((unsigned)grid), dim3(kBlock), 0, s, b, w, sc);
 }
 
 // Merge-path split + 8-way serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties):
@@ -213,6 +233,27 @@ __device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortIt
             i += takeA ? 1 : 0;
             j += takeA ? 0 : 1;
         }
+    }
+}
+
+// As merge8, writing the outputs straight to dst[0, count).
+__device__ __forceinline__ void merge8_to(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
+                                          SortItem* dst, int count, const uint8_t* arena) {
+    int lo = d - lenB > 0 ? d - lenB : 0;
+    int hi = d < lenA ? d : lenA;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (!item_less(B[d - mid - 1], A[mid], arena))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    int i = lo, j = d - lo;
+    for (int k = 0; k < count; k++) {
+        const bool takeA = (j >= lenB) || (i < lenA && !item_less(B[j], A[i], arena));
+        dst[k] = takeA ? A[i] : B[j];
+        i += takeA ? 1 : 0;
+        j += takeA ? 0 : 1;
     }
 }
 
@@ -303,20 +344,13 @@ __global__ __launch_bounds__(kBlock) void k_merge_pass(const SortItem* in, SortI
     __syncthreads();
     const int o = threadIdx.x * 8;
     const int mine = max(0, min(8, (d1 - d0) - o));
-    if (mine > 0) {
-        SortItem r[8];
-        merge8(sh, na, sh + na, nb, o, r, mine, arena);
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (k < mine) out[o0 + o + k] = r[k];
-    }
+    if (mine > 0) merge8_to(sh, na, sh + na, nb, o, out + o0 + o, mine, arena);
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
-    hipLaunchKernelGGL(k_make_items, dim3((b.R + b.W + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w.items[1]);
     const int tiles = (E + kSortTile - 1) / kSortTile;
     hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kBlock), 0, s, w.items[1], w.items[0], E, b.tail);
     int cur = 0;
@@ -330,14 +364,35 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* re
 
 // ------------------------------------------------------------------ positions
 
-__global__ __launch_bounds__(kBlock) void k_positions(const SortItem* sorted, int E, int32_t* pos, uint32_t* pmeta) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= E) return;
-    const uint32_t meta = sorted[p].meta;
-    pmeta[p] = meta;
-    const uint32_t slot = 2 * item_range(meta) + item_is_end(meta);
-    if (slot < (uint32_t)E) pos[slot] = p;  // KeyInfo::pIndex (SkipList.cpp:814)
-}
+// Positions (KeyInfo::pIndex, SkipList.cpp:814) and, in the same scan, the number of write-begins
+// and read-begins before every position with the compacted position list of each kind.
+struct PosScan {
+    const SortItem* sorted;
+    int32_t* pos;
+    uint32_t* pmeta;
+    int32_t *cwb, *crb, *wbpos, *rbpos;
+    int32_t E;
+    __device__ void load(int64_t p, uint32_t (&v)[2]) const {
+        const uint32_t meta = sorted[p].meta;
+        pmeta[p] = meta;
+        const uint32_t slot = 2 * item_range(meta) + item_is_end(meta);
+        if (slot < (uint32_t)E) pos[slot] = (int32_t)p;
+        const uint32_t c = item_class(meta);
+        v[0] = c == kWriteBegin;
+        v[1] = c == kReadBegin;
+    }
+    __device__ void store(int64_t p, const uint32_t (&ex)[2]) const {
+        cwb[p] = (int32_t)ex[0];
+        crb[p] = (int32_t)ex[1];
+        const uint32_t c = item_class(pmeta[p]);
+        if (c == kWriteBegin) wbpos[ex[0]] = (int32_t)p;
+        if (c == kReadBegin) rbpos[ex[1]] = (int32_t)p;
+    }
+    __device__ void finish(const uint32_t (&tot)[2]) const {
+        cwb[E] = (int32_t)tot[0];
+        crb[E] = (int32_t)tot[1];
+    }
+};
 
 // FDBCS_VALIDATE=1: check the endpoint order and that positions invert the permutation.
 __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted, const int32_t* pos,
@@ -351,32 +406,11 @@ __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted
     if (bad) atomicOr(&sc->debug_error, 1);
 }
 
-// Exclusive counts of write-begins (high word) and read-begins (low word) before each position,
-// plus the compacted position lists of each kind.
-__global__ __launch_bounds__(kWG) void k_begin_lists(const uint32_t* pmeta, int E, int64_t* cnt_pair,
-                                                     int32_t* wbpos, int32_t* rbpos) {
-    __shared__ int64_t sh[16];
-    auto flag = [&](int64_t p) -> int64_t {
-        const uint32_t c = item_class(pmeta[p]);
-        return (c == kWriteBegin ? (int64_t(1) << 32) : 0) | (c == kReadBegin ? 1 : 0);
-    };
-    int64_t tot = wg_scan<int64_t>(
-        E, flag, [&](int64_t p, int64_t pre) { cnt_pair[p] = pre; }, sh);
-    if (threadIdx.x == 0) cnt_pair[E] = tot;
-    __syncthreads();
-    for (int p = threadIdx.x; p < E; p += blockDim.x) {
-        const uint32_t c = item_class(pmeta[p]);
-        if (c == kWriteBegin) wbpos[cnt_pair[p] >> 32] = p;
-        if (c == kReadBegin) rbpos[cnt_pair[p] & 0xffffffffll] = p;
-    }
-}
-
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
     const int E = 2 * (b.R + b.W);
     if (E == 0) return;
-    hipLaunchKernelGGL(k_positions, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf], E,
-                       w.pos, w.pmeta);
-    hipLaunchKernelGGL(k_begin_lists, dim3(1), dim3(kWG), 0, s, w.pmeta, E, w.cnt_pair, w.wbpos, w.rbpos);
+    PosScan f{w.items[sorted_buf], w.pos, w.pmeta, w.cwb, w.crb, w.wbpos, w.rbpos, E};
+    launch_scan<2>(s, f, nullptr, E, w.scan[kScanPos]);
 }
 
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc) {
@@ -409,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scal
         const int rb = w.pos[2 * r], re = w.pos[2 * r + 1];
         int cnt = 0;
         if (rb < re) {
-            const int k0 = (int)(w.cnt_pair[rb] >> 32), k1 = (int)(w.cnt_pair[re] >> 32);
+            const int k0 = w.cwb[rb], k1 = w.cwb[re];
             int out = FILL ? w.eoff[r] : 0;
             for (int k = k0; k < k1; k++) {
                 const int p = w.wbpos[k];
@@ -428,7 +462,7 @@ __global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scal
         if (w.hist_conf[tw]) return;
         const int wb = w.pos[2 * g], we = w.pos[2 * g + 1];
         if (wb >= we) return;
-        const int k0 = (int)(w.cnt_pair[wb] & 0xffffffffll), k1 = (int)(w.cnt_pair[we] & 0xffffffffll);
+        const int k0 = w.crb[wb], k1 = w.crb[we];
         for (int k = k0; k < k1; k++) {
             const int p = w.rbpos[k];
             const int r = (int)item_range(w.pmeta[p]);
@@ -445,26 +479,27 @@ __global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scal
     }
 }
 
-__global__ __launch_bounds__(kWG) void k_edge_offsets(BatchDev b, Work w, Scalars* sc) {
-    __shared__ int64_t sh[16];
-    int64_t tot = wg_scan<int64_t>(
-        b.R, [&](int64_t r) -> int64_t { return (int64_t)w.ecnt_a[r] + w.ecnt_b[r]; },
-        [&](int64_t r, int64_t pre) { w.eoff[r] = (int32_t)(pre < INT_MAX ? pre : INT_MAX); }, sh);
-    if (threadIdx.x == 0) {
-        w.eoff[b.R] = (int32_t)(tot < INT_MAX ? tot : INT_MAX);
-        sc->n_edges = tot;
-        sc->edge_overflow = tot > w.edge_cap ? 1 : 0;
+// Edge offsets per read range: exclusive scan of the two candidate counts.
+struct EdgeOffsetScan {
+    const int32_t *a, *b;
+    int32_t* eoff;
+    int32_t R;
+    int64_t cap;
+    Scalars* sc;
+    __device__ void load(int64_t r, uint32_t (&v)[1]) const { v[0] = (uint32_t)(a[r] + b[r]); }
+    __device__ void store(int64_t r, const uint32_t (&ex)[1]) const { eoff[r] = (int32_t)ex[0]; }
+    __device__ void finish(const uint32_t (&tot)[1]) const {
+        eoff[R] = (int32_t)tot[0];
+        sc->n_edges = tot[0];
+        sc->edge_overflow = (int64_t)tot[0] > cap || tot[0] > 0x7fffffffu ? 1 : 0;
     }
-}
+};
 
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
     const int G = b.R + b.W;
-    if (b.R) {
-        (void)hipMemsetAsync(w.ecnt_b, 0, sizeof(int32_t) * b.R, s);
-        (void)hipMemsetAsync(w.ecur, 0, sizeof(int32_t) * b.R, s);
-    }
     if (G) hipLaunchKernelGGL(k_edges<false>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
-    hipLaunchKernelGGL(k_edge_offsets, dim3(1), dim3(kWG), 0, s, b, w, sc);
+    EdgeOffsetScan f{w.ecnt_a, w.ecnt_b, w.eoff, b.R, w.edge_cap, sc};
+    launch_scan<1>(s, f, nullptr, b.R, w.scan[kScanEdges]);
     if (G) hipLaunchKernelGGL(k_edges<true>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
 }
 
@@ -522,6 +557,9 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, Scalars* sc
         }
     } else {
         // Sequential MiniConflictSet replay (SkipList.cpp:797-834) over E point indices.
+        const int E = 2 * (b.R + b.W);
+        for (int i = threadIdx.x; i <= E / 64; i += blockDim.x) w.mcs_bits[i] = 0;
+        __syncthreads();
         for (int t = 0; t < T; t++) {
             if (st[t] != kUndecided) continue;  // uniform: st read after a barrier
             int conflict_at = INT_MAX;
@@ -588,8 +626,6 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w, con
 
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
     if (b.T == 0) return;
-    const int E = 2 * (b.R + b.W);
-    (void)hipMemsetAsync(w.mcs_bits, 0, sizeof(uint64_t) * (E / 64 + 1), s);
     hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWG), (size_t)b.T, s, b, w, sc);
     if (b.R) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
 }
@@ -599,38 +635,54 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc
 // combineWriteConflictRanges (SkipList.cpp:926-939): coverage of committed non-empty writes over
 // sorted positions; each maximal covered run is one union segment [key(begin), key(end)).
 
-__global__ __launch_bounds__(kWG) void k_combine(BatchDev b, Work w, Scalars* sc) {
-    __shared__ int32_t sh[16];
-    const int E = 2 * (b.R + b.W);
-    const int R = b.R;
-    auto delta = [&](int64_t p) -> int32_t {
-        const uint32_t meta = w.pmeta[p];
+struct Delta {
+    const uint32_t* pmeta;
+    const int32_t* pos;
+    const uint8_t* status;
+    const int32_t* wowner;
+    int32_t R;
+    // +1 at the begin and -1 at the end of every committed, non-empty write range
+    __device__ int32_t operator()(int64_t p) const {
+        const uint32_t meta = pmeta[p];
         const uint32_t c = item_class(meta);
         if (c != kWriteBegin && c != kWriteEnd) return 0;
         const int g = (int)item_range(meta);
-        if (w.status[b.wowner[g - R]] != kCommitted) return 0;
-        if (w.pos[2 * g] >= w.pos[2 * g + 1]) return 0;
+        if (status[wowner[g - R]] != kCommitted) return 0;
+        if (pos[2 * g] >= pos[2 * g + 1]) return 0;
         return c == kWriteBegin ? 1 : -1;
-    };
-    // inclusive coverage = exclusive prefix + own delta
-    wg_scan<int32_t>(
-        E, delta, [&](int64_t p, int32_t pre) { w.cov[p] = pre + delta(p); }, sh);
-    __syncthreads();
-    auto sflag = [&](int64_t p) -> int32_t { return (w.cov[p] > 0 && (p == 0 || w.cov[p - 1] == 0)) ? 1 : 0; };
-    int32_t U = wg_scan<int32_t>(
-        E, sflag,
-        [&](int64_t p, int32_t pre) {
-            const int32_t c = w.cov[p];
-            const int32_t prev = p ? w.cov[p - 1] : 0;
-            if (c > 0 && prev == 0) w.seg_b[pre] = (int32_t)p;
-            if (c == 0 && prev > 0) w.seg_e[pre - 1] = (int32_t)p;
-        },
-        sh);
-    if (threadIdx.x == 0) sc->n_segments = U;
-}
+    }
+};
+
+// Coverage before each position; a segment starts where coverage leaves 0 and ends where it returns.
+struct CoverScan {
+    Delta d;
+    uint8_t* segflag;
+    __device__ void load(int64_t p, uint32_t (&v)[1]) const { v[0] = (uint32_t)d(p); }
+    __device__ void store(int64_t p, const uint32_t (&ex)[1]) const {
+        const int32_t before = (int32_t)ex[0], dp = d(p);
+        segflag[p] = (uint8_t)((dp == 1 && before == 0 ? 1 : 0) | (dp == -1 && before == 1 ? 2 : 0));
+    }
+    __device__ void finish(const uint32_t (&)[1]) const {}
+};
+
+struct SegmentScan {
+    const uint8_t* segflag;
+    int32_t *seg_b, *seg_e;
+    Scalars* sc;
+    __device__ void load(int64_t p, uint32_t (&v)[1]) const { v[0] = segflag[p] & 1u; }
+    __device__ void store(int64_t p, const uint32_t (&ex)[1]) const {
+        const uint8_t f = segflag[p];
+        if (f & 1) seg_b[ex[0]] = (int32_t)p;
+        if (f & 2) seg_e[ex[0] - 1] = (int32_t)p;
+    }
+    __device__ void finish(const uint32_t (&tot)[1]) const { sc->n_segments = tot[0]; }
+};
 
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
-    hipLaunchKernelGGL(k_combine, dim3(1), dim3(kWG), 0, s, b, w, sc);
+    const int E = 2 * (b.R + b.W);
+    Delta d{w.pmeta, w.pos, w.status, b.wowner, b.R};
+    launch_scan<1>(s, CoverScan{d, w.segflag}, nullptr, E, w.scan[kScanCov]);
+    launch_scan<1>(s, SegmentScan{w.segflag, w.seg_b, w.seg_e, sc}, nullptr, E, w.scan[kScanSeg]);
 }
 
 // ------------------------------------------------------------------ D.MergeWrite
@@ -666,26 +718,32 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
 }
 
-__global__ __launch_bounds__(kWG) void k_seg_scan(Work w, Scalars* sc) {
-    __shared__ int64_t sh[16];
-    const int U = sc->n_segments;
-    int64_t rem = wg_scan<int64_t>(
-        U, [&](int64_t s) { return w.seg_rem[s]; }, [&](int64_t s, int64_t p) { w.seg_rem[s] = p; }, sh);
-    int64_t ins = wg_scan<int64_t>(
-        U, [&](int64_t s) { return w.seg_ins[s]; }, [&](int64_t s, int64_t p) { w.seg_ins[s] = p; }, sh);
-    int64_t tl = wg_scan<int64_t>(
-        U, [&](int64_t s) { return w.seg_tlen[s]; }, [&](int64_t s, int64_t p) { w.seg_tlen[s] = p; }, sh);
-    if (threadIdx.x == 0) {
-        // sentinel entries at U: totals, used by the copy kernel for elements after every segment
-        w.seg_rem[U] = rem;
-        w.seg_ins[U] = ins;
-        w.seg_tlen[U] = tl;
-        sc->n_before = sc->n;
-        sc->rem_total = rem;
-        sc->n_next = sc->n - rem + ins;
-        sc->tail_next = sc->tail_used + tl;
+// Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per segment.
+struct SegSumScan {
+    int64_t *rem, *ins, *tlen;
+    Scalars* sc;
+    __device__ void load(int64_t j, uint32_t (&v)[3]) const {
+        v[0] = (uint32_t)rem[j];
+        v[1] = (uint32_t)ins[j];
+        v[2] = (uint32_t)tlen[j];
     }
-}
+    __device__ void store(int64_t j, const uint32_t (&ex)[3]) const {
+        rem[j] = ex[0];
+        ins[j] = ex[1];
+        tlen[j] = ex[2];
+    }
+    __device__ void finish(const uint32_t (&tot)[3]) const {
+        const int64_t U = sc->n_segments;
+        // sentinel entries at U: totals, used by the copy kernel for elements after every segment
+        rem[U] = tot[0];
+        ins[U] = tot[1];
+        tlen[U] = tot[2];
+        sc->n_before = sc->n;
+        sc->rem_total = tot[0];
+        sc->n_next = sc->n - (int64_t)tot[0] + (int64_t)tot[1];
+        sc->tail_next = sc->tail_used + (int64_t)tot[2];
+    }
+};
 
 constexpr int kSegLds = 1024;
 
@@ -797,7 +855,8 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     const int Wn = b.W > 0 ? b.W : 1;
     hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
                        header_version);
-    hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(kWG), 0, s, w, sc);
+    launch_scan<3>(s, SegSumScan{w.seg_rem, w.seg_ins, w.seg_tlen, sc}, &sc->n_segments, (int64_t)b.W + 1,
+                   w.scan[kScanSegSum]);
     if (copy_begin) (void)hipEventRecord(copy_begin, s);
     int64_t tiles = (grid_hint_n + kGcTile - 1) / kGcTile;
     if (tiles < 1) tiles = 1;
@@ -818,69 +877,46 @@ __device__ __forceinline__ bool gc_keep(const Hist& h, int64_t i, int64_t v, int
     return h.ver[i] >= v || pv >= v;
 }
 
-__global__ __launch_bounds__(kBlock) void k_gc_count(Hist h, const Scalars* sc, int64_t v, int64_t hdr,
-                                                     int64_t* tile_cnt) {
-    __shared__ int64_t sh[4];
-    const int64_t n = sc->n_next;
-    const int64_t i0 = (int64_t)blockIdx.x * kGcTile;
-    int64_t c = 0;
-    if (i0 < n) {
-        for (int64_t i = i0 + threadIdx.x; i < min(n, i0 + kGcTile); i += blockDim.x) c += gc_keep(h, i, v, hdr);
+struct GcScan {
+    Hist src, dst;
+    int64_t v, hdr;
+    Scalars* sc;
+    __device__ void load(int64_t i, uint32_t (&x)[1]) const { x[0] = gc_keep(src, i, v, hdr) ? 1u : 0u; }
+    __device__ void store(int64_t i, const uint32_t (&ex)[1]) const {
+        if (!gc_keep(src, i, v, hdr)) return;
+        const int64_t o = ex[0];
+        dst.key[o] = src.key[i];
+        dst.lt[o] = src.lt[i];
+        dst.ver[o] = src.ver[i];
     }
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
-}
-
-__global__ __launch_bounds__(kWG) void k_gc_spine(int64_t* tile_cnt, int tiles, Scalars* sc) {
-    __shared__ int64_t sh[16];
-    int64_t tot = wg_scan<int64_t>(
-        tiles, [&](int64_t k) { return tile_cnt[k]; }, [&](int64_t k, int64_t p) { tile_cnt[k] = p; }, sh);
-    if (threadIdx.x == 0) sc->n_gc = tot;
-}
-
-__global__ __launch_bounds__(kBlock) void k_gc_scatter(Hist src, Hist dst, const Scalars* sc, int64_t v,
-                                                       int64_t hdr, const int64_t* tile_off) {
-    __shared__ int64_t sh[16];
-    const int64_t n = sc->n_next;
-    const int64_t i0 = (int64_t)blockIdx.x * kGcTile;
-    if (i0 >= n) return;
-    constexpr int kPer = kGcTile / kBlock;  // contiguous elements per thread
-    const int64_t a = i0 + (int64_t)threadIdx.x * kPer;
-    uint32_t keepmask = 0;
-    int64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        const int64_t i = a + k;
-        if (i < n && gc_keep(src, i, v, hdr)) {
-            keepmask |= 1u << k;
-            c++;
-        }
-    }
-    int64_t tot;
-    int64_t o = tile_off[blockIdx.x] + block_excl_sum<int64_t>(c, sh, &tot);
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-        if (keepmask >> k & 1) {
-            const int64_t i = a + k;
-            dst.key[o] = src.key[i];
-            dst.lt[o] = src.lt[i];
-            dst.ver[o] = src.ver[i];
-            o++;
-        }
-    }
-}
+    __device__ void finish(const uint32_t (&tot)[1]) const { sc->n_gc = tot[0]; }
+};
 
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
                int64_t header_version, int64_t grid_hint_n) {
-    int64_t tiles = (grid_hint_n + kGcTile - 1) / kGcTile;
-    if (tiles < 1) tiles = 1;
-    hipLaunchKernelGGL(k_gc_count, dim3((unsigned)tiles), dim3(kBlock), 0, s, src, sc, oldest, header_version,
-                       w.tile_cnt);
-    hipLaunchKernelGGL(k_gc_spine, dim3(1), dim3(kWG), 0, s, w.tile_cnt, (int)tiles, sc);
-    hipLaunchKernelGGL(k_gc_scatter, dim3((unsigned)tiles), dim3(kBlock), 0, s, src, dst, sc, oldest,
-                       header_version, w.tile_cnt);
+    launch_scan<1>(s, GcScan{src, dst, oldest, header_version, sc}, &sc->n_next, grid_hint_n, w.scan[kScanGc]);
+}
+
+int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap) {
+    (void)T;
+    const int64_t E = 2 * (R + W);
+    return kNumScans + scan_granules(E, 2) + scan_granules(R, 1) + 2 * scan_granules(E, 1) +
+           scan_granules(W + 1, 3) + scan_granules(hist_cap, 1);
+}
+
+void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap) {
+    (void)T;
+    const int64_t E = 2 * (R + W);
+    uint64_t* a = w.scan_arena;
+    const int64_t gran[kNumScans] = {scan_granules(E, 2), scan_granules(R, 1), scan_granules(E, 1),
+                                     scan_granules(E, 1), scan_granules(W + 1, 3), scan_granules(hist_cap, 1)};
+    uint64_t* g = a + kNumScans;
+    for (int k = 0; k < kNumScans; k++) {
+        w.scan[k].counter = (int*)(a + k);
+        w.scan[k].granules = g;
+        g += gran[k];
+    }
+    w.scan_words = g - a;
 }
 
 // ------------------------------------------------------------------ range-max hierarchy
@@ -919,7 +955,8 @@ void launch_blockmax(hipStream_t s, const MaxLevels& m, const int64_t* n_ptr, in
 
 // ------------------------------------------------------------------ verdicts
 
-__global__ __launch_bounds__(kBlock) void k_finalize(BatchDev b, Work w, Scalars* sc, int gc_ran) {
+__global__ __launch_bounds__(kBlock) void k_finalize(BatchDev b, Work w, Scalars* sc, int gc_ran,
+                                                     uint8_t* verdict_out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < b.T) {
         uint8_t v;
@@ -927,7 +964,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchDev b, Work w, Scalars
             v = 1;  // TransactionTooOld (ConflictSet.h:42)
         else
             v = w.status[t] == kCommitted ? 2 : 0;
-        w.verdict[t] = v;
+        verdict_out[t] = v;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         sc->n = gc_ran ? sc->n_gc : sc->n_next;
@@ -935,9 +972,10 @@ __global__ __launch_bounds__(kBlock) void k_finalize(BatchDev b, Work w, Scalars
     }
 }
 
-void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran) {
+void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran, uint8_t* verdict_out) {
     const int T = b.T > 0 ? b.T : 1;
-    hipLaunchKernelGGL(k_finalize, dim3((T + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc, gc_ran);
+    hipLaunchKernelGGL(k_finalize, dim3((T + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc, gc_ran,
+                       verdict_out);
 }
 
 }  // namespace fdbcs

@@ -1,0 +1,179 @@
+// scan.h — single-pass device-wide exclusive scan with decoupled look-back (gfx950).
+//
+// One workgroup per 4096-element tile; tiles take ids from an atomic counter in launch order so a
+// tile only ever waits on tiles that are already running (no deadlock whatever the dispatch order).
+// Each tile publishes, per scanned component, an 8-byte granule {status << 32 | value} with an
+// agent-scope atomic store: status 1 = tile aggregate, 2 = inclusive prefix.  Look-back reads the
+// granules with agent-scope atomic loads (they bypass the per-CU L1), so the data is the flag and
+// no fence is needed (MI355X_MICROARCH.md, inter-workgroup visibility, granule form R2).
+//
+// The element function object F supplies
+//   __device__ void load(int64_t i, uint32_t (&v)[K]);             // visit i, produce K counts
+//   __device__ void store(int64_t i, const uint32_t (&excl)[K]);   // exclusive prefixes of i
+//   __device__ void finish(const uint32_t (&total)[K]);            // once, by the last tile
+// Both visits of an element run on the same thread.  Sums are modulo 2^32, so +/-1 deltas work.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fdbcs {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanPer = 16;
+constexpr int kScanTile = kScanThreads * kScanPer;  // 4096
+constexpr int kScanPad = kScanTile + kScanTile / 16;
+
+__device__ __forceinline__ int scan_slot(int e) { return e + (e >> 4); }  // one pad word per 16
+
+__device__ __forceinline__ void granule_store(uint64_t* g, uint32_t status, uint32_t value) {
+    __hip_atomic_store(g, ((uint64_t)status << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t granule_load(const uint64_t* g) {
+    return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Scan state for one launch: K granules per tile + the tile counter + an error word, zeroed
+// before the launch (one hipMemsetAsync covers every scan of a batch).
+struct ScanState {
+    uint64_t* granules;  // [tiles * K]
+    int* counter;
+    int* error;          // set if a look-back spin exceeded its bound
+};
+
+template <int K, class F>
+__global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr, int64_t n_host, ScanState st) {
+    __shared__ uint32_t sv[K][kScanPad];
+    __shared__ uint32_t swave[K][kScanThreads / 64];
+    __shared__ uint32_t sbase[K];
+    __shared__ int s_tile;
+    const int64_t n = n_ptr ? *n_ptr : n_host;
+    if (threadIdx.x == 0) s_tile = atomicAdd(st.counter, 1);
+    __syncthreads();
+    const int tile = s_tile;
+    const int64_t base = (int64_t)tile * kScanTile;
+    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+    if (tile >= ntiles) return;  // spare tile of a device-sized launch: nobody waits on it
+
+    // phase 1: coalesced visits
+#pragma unroll 4
+    for (int k = 0; k < kScanPer; k++) {
+        const int e = k * kScanThreads + threadIdx.x;
+        const int64_t i = base + e;
+        uint32_t v[K];
+#pragma unroll
+        for (int c = 0; c < K; c++) v[c] = 0;
+        if (i < n) f.load(i, v);
+#pragma unroll
+        for (int c = 0; c < K; c++) sv[c][scan_slot(e)] = v[c];
+    }
+    __syncthreads();
+    // phase 2: each thread scans its 16 consecutive elements
+    uint32_t tsum[K];
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < kScanPer; j++) {
+            const int slot = scan_slot(threadIdx.x * kScanPer + j);
+            const uint32_t x = sv[c][slot];
+            sv[c][slot] = s;
+            s += x;
+        }
+        tsum[c] = s;
+    }
+    // block scan of thread sums
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t texcl[K];
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        uint32_t x = tsum[c];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        texcl[c] = x - tsum[c];
+        if (lane == 63) swave[c][wid] = x;
+    }
+    __syncthreads();
+    uint32_t btot[K];
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int q = 0; q < kScanThreads / 64; q++) {
+            if (q < wid) before += swave[c][q];
+            all += swave[c][q];
+        }
+        texcl[c] += before;
+        btot[c] = all;
+    }
+    // phase 3: look-back, one thread per component
+    if (threadIdx.x < K) {
+        const int c = threadIdx.x;
+        uint64_t* g = st.granules;
+        uint32_t prefix = 0;
+        if (tile == 0) {
+            granule_store(&g[c], 2, btot[c]);
+        } else {
+            granule_store(&g[(int64_t)tile * K + c], 1, btot[c]);
+            int64_t j = tile - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const uint64_t x = granule_load(&g[j * K + c]);
+                const uint32_t status = (uint32_t)(x >> 32);
+                if (status == 0) {
+                    if (++spins > (1u << 26)) {  // bounded: never hang the GPU
+                        atomicOr(st.error, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                prefix += (uint32_t)x;
+                if (status == 2) break;
+                j--;
+            }
+            granule_store(&g[(int64_t)tile * K + c], 2, prefix + btot[c]);
+        }
+        sbase[c] = prefix;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        const uint32_t add = sbase[c] + texcl[c];
+#pragma unroll
+        for (int j = 0; j < kScanPer; j++) sv[c][scan_slot(threadIdx.x * kScanPer + j)] += add;
+    }
+    __syncthreads();
+    // phase 4: coalesced stores
+#pragma unroll 4
+    for (int k = 0; k < kScanPer; k++) {
+        const int e = k * kScanThreads + threadIdx.x;
+        const int64_t i = base + e;
+        if (i < n) {
+            uint32_t ex[K];
+#pragma unroll
+            for (int c = 0; c < K; c++) ex[c] = sv[c][scan_slot(e)];
+            f.store(i, ex);
+        }
+    }
+    if (tile == ntiles - 1 && threadIdx.x == 0) {
+        uint32_t tot[K];
+#pragma unroll
+        for (int c = 0; c < K; c++) tot[c] = sbase[c] + btot[c];
+        f.finish(tot);
+    }
+}
+
+// Granules needed for a scan of up to n elements with K components.
+inline int64_t scan_granules(int64_t n, int K) { return ((n > 0 ? n : 1) + kScanTile - 1) / kScanTile * K; }
+
+template <int K, class F>
+void launch_scan(hipStream_t s, const F& f, const int64_t* n_dev, int64_t n_max, ScanState st) {
+    int64_t tiles = (n_max + kScanTile - 1) / kScanTile;
+    if (tiles < 1) tiles = 1;
+    hipLaunchKernelGGL((k_scan<K, F>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f, n_dev, n_max, st);
+}
+
+}  // namespace fdbcs
