@@ -11,7 +11,8 @@ namespace fdbcs {
 
 constexpr int kBlock = 256;        // default workgroup: 4 waves of 64
 constexpr int kWG = 1024;          // single-workgroup kernels (scans, resolution)
-constexpr int kSortTile = 2048;    // endpoints per LDS sort tile (256 threads x 8)
+constexpr int kSortThreads = 512;  // sort workgroups: 8 waves, 8 endpoints per thread
+constexpr int kSortTile = 4096;    // endpoints per LDS sort tile (128 KiB of LDS)
 constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
 constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)
 constexpr int kGcTile = 4096;      // history elements per GC / merge tile

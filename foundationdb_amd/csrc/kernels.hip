@@ -269,7 +269,7 @@ __device__ __forceinline__ void cex(SortItem& a, SortItem& b, bool active, const
 // Sort one tile of kSortTile endpoints: each thread sorts its 8 items with Batcher's odd-even
 // merge network (19 comparators, items past `mine` stay put), then runs of 8, 16, ... are merged
 // in LDS by merge path (each thread's 8 outputs always fall inside one pair of runs).
-__global__ __launch_bounds__(kBlock) void k_sort_tile(const SortItem* in, SortItem* out, int n,
+__global__ __launch_bounds__(kSortThreads) void k_sort_tile(const SortItem* in, SortItem* out, int n,
                                                       const uint8_t* arena) {
     __shared__ SortItem sh[kSortTile];
     const int base = blockIdx.x * kSortTile;
@@ -308,8 +308,39 @@ __global__ __launch_bounds__(kBlock) void k_sort_tile(const SortItem* in, SortIt
     for (int i = threadIdx.x; i < cnt; i += blockDim.x) out[base + i] = sh[i];
 }
 
+// Merge-path split over global memory by one wave: smallest i in [lo, hi) with B[d-i-1] < A[i]
+// (else hi), narrowing 64-fold per round instead of halving, so a 128k-element split costs
+// three dependent loads instead of seventeen.
+__device__ __forceinline__ int wave_merge_split(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
+                                                const uint8_t* arena) {
+    const int lane = threadIdx.x & 63;
+    int lo = d - lenB > 0 ? d - lenB : 0;
+    int hi = d < lenA ? d : lenA;
+    while (lo < hi) {
+        const int span = hi - lo;
+        const int step = (span + 63) / 64;
+        const int i = lo + lane * step;
+        const bool pred = i < hi && item_less(B[d - i - 1], A[i], arena);
+        const uint64_t mask = __ballot(pred);
+        // lanes with i >= hi are treated as true (the answer is at most hi)
+        const int nvalid = (span + step - 1) / step;
+        const uint64_t beyond = nvalid >= 64 ? 0ull : (~0ull << nvalid);
+        const uint64_t m = mask | beyond;
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __ffsll((long long)m) - 1;  // first lane whose probe is at/after the split
+        const int nhi = lo + f * step;
+        const int nlo = f > 0 ? lo + (f - 1) * step + 1 : lo;
+        lo = nlo;
+        hi = nhi < hi ? nhi : hi;
+    }
+    return lo;
+}
+
 // Merge sorted runs of length w pairwise into runs of 2w; one output tile per workgroup.
-__global__ __launch_bounds__(kBlock) void k_merge_pass(const SortItem* in, SortItem* out, int n, int w,
+__global__ __launch_bounds__(kSortThreads) void k_merge_pass(const SortItem* in, SortItem* out, int n, int w,
                                                        const uint8_t* arena) {
     __shared__ SortItem sh[kSortTile];
     __shared__ int split[2];
@@ -322,18 +353,10 @@ __global__ __launch_bounds__(kBlock) void k_merge_pass(const SortItem* in, SortI
     const SortItem* B = A + w;
     const int d0 = o0 - pb;
     const int d1 = min(d0 + kSortTile, lenA + lenB);
-    if (threadIdx.x < 2) {
-        const int d = threadIdx.x ? d1 : d0;
-        int lo = d - lenB > 0 ? d - lenB : 0;
-        int hi = d < lenA ? d : lenA;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (!item_less(B[d - mid - 1], A[mid], arena))
-                lo = mid + 1;
-            else
-                hi = mid;
-        }
-        split[threadIdx.x] = lo;
+    const int wave = threadIdx.x >> 6;
+    if (wave < 2) {
+        const int sp = wave_merge_split(A, lenA, B, lenB, wave ? d1 : d0, arena);
+        if ((threadIdx.x & 63) == 0) split[wave] = sp;
     }
     __syncthreads();
     const int i0 = split[0], i1 = split[1];
@@ -352,11 +375,11 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* re
     *result_buffer = 0;
     if (E == 0) return;
     const int tiles = (E + kSortTile - 1) / kSortTile;
-    hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kBlock), 0, s, w.items[1], w.items[0], E, b.tail);
+    hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kSortThreads), 0, s, w.items[1], w.items[0], E, b.tail);
     int cur = 0;
     for (int run = kSortTile; run < E; run *= 2) {
-        hipLaunchKernelGGL(k_merge_pass, dim3(tiles), dim3(kBlock), 0, s, w.items[cur], w.items[cur ^ 1], E, run,
-                           b.tail);
+        hipLaunchKernelGGL(k_merge_pass, dim3(tiles), dim3(kSortThreads), 0, s, w.items[cur], w.items[cur ^ 1], E,
+                           run, b.tail);
         cur ^= 1;
     }
     *result_buffer = cur;
@@ -786,33 +809,59 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Work w, Hist src, Hist ds
             }
         }
         __syncthreads();
-        for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-            int64_t seg_lo_v, seg_hi_v, shift;
-            if (cnt <= kSegLds) {
-                int lo = 0, hi = cnt;  // last slot k with s_lo[k] <= i (slot 0 always qualifies)
-                while (lo < hi) {
-                    int mid = (lo + hi + 1) >> 1;
-                    if (s_lo[mid] <= i) lo = mid; else hi = mid - 1;
+        if (cnt <= kSegLds) {
+            // 8 elements per thread per chunk: resolve every destination first (branch-free binary
+            // lifting over the staged segments), then issue all loads, then all stores, so each
+            // thread keeps 8 independent HBM requests in flight.
+            constexpr int kPer = 8;
+            for (int64_t c0 = i0; c0 < i1; c0 += kPer * kBlock) {
+                int64_t dsto[kPer];
+#pragma unroll
+                for (int k = 0; k < kPer; k++) {
+                    const int64_t i = c0 + k * kBlock + threadIdx.x;
+                    int sl = 0;  // last slot with s_lo <= i (slot 0 always qualifies)
+#pragma unroll
+                    for (int step = kSegLds; step > 0; step >>= 1) {
+                        const int mid = sl + step;
+                        if (mid <= cnt && s_lo[mid] <= i) sl = mid;
+                    }
+                    const bool keep = i < i1 && !(i >= s_lo[sl] && i < s_hi[sl]);  // else inside a written span
+                    dsto[k] = keep ? i + s_shift[sl] : -1;
                 }
-                seg_lo_v = s_lo[lo];
-                seg_hi_v = s_hi[lo];
-                shift = s_shift[lo];
-            } else {
+                uint64_t khi[kPer], klo[kPer], lt[kPer], vv[kPer];
+#pragma unroll
+                for (int k = 0; k < kPer; k++) {
+                    const int64_t i = c0 + k * kBlock + threadIdx.x;
+                    const int64_t j = dsto[k] >= 0 ? i : i0;  // always-valid address, loads stay unconditional
+                    const ulonglong2 kv = src.key[j];
+                    khi[k] = kv.x;
+                    klo[k] = kv.y;
+                    lt[k] = reinterpret_cast<const uint64_t*>(src.lt)[j];
+                    vv[k] = (uint64_t)src.ver[j];
+                }
+#pragma unroll
+                for (int k = 0; k < kPer; k++) {
+                    if (dsto[k] >= 0) {
+                        dst.key[dsto[k]] = make_ulonglong2(khi[k], klo[k]);
+                        reinterpret_cast<uint64_t*>(dst.lt)[dsto[k]] = lt[k];
+                        dst.ver[dsto[k]] = (int64_t)vv[k];
+                    }
+                }
+            }
+        } else {
+            for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
                 int lo = 0, hi = U;
                 while (lo < hi) {
                     int mid = (lo + hi) >> 1;
                     if (w.seg_lo[mid] <= i) lo = mid + 1; else hi = mid;
                 }
                 const int j = lo - 1;
-                seg_lo_v = j >= 0 ? w.seg_lo[j] : LLONG_MIN;
-                seg_hi_v = j >= 0 ? w.seg_hi[j] : LLONG_MIN;
-                shift = w.seg_ins[j + 1] - w.seg_rem[j + 1];
+                if (j >= 0 && i >= w.seg_lo[j] && i < w.seg_hi[j]) continue;
+                const int64_t o = i + w.seg_ins[j + 1] - w.seg_rem[j + 1];
+                dst.key[o] = src.key[i];
+                dst.lt[o] = src.lt[i];
+                dst.ver[o] = src.ver[i];
             }
-            if (i >= seg_lo_v && i < seg_hi_v) continue;  // inside a written span
-            const int64_t o = i + shift;
-            dst.key[o] = src.key[i];
-            dst.lt[o] = src.lt[i];
-            dst.ver[o] = src.ver[i];
         }
         __syncthreads();
     }

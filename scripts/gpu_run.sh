@@ -22,3 +22,7 @@ tail -5 gpurun_out/smoke.log >&2
 step bench 600 python bench.py ${BENCH_ARGS:---steps 30 --warmup 3} > gpurun_out/bench.json 2> gpurun_out/bench.err
 cat gpurun_out/bench.json >&2
 tail -5 gpurun_out/bench.err >&2
+if [ "${PROFILE:-0}" = "1" ]; then
+  step profile 600 bash scripts/gpu_profile.sh
+  python3 scripts/prof_summary.py gpurun_out/prof/run_kernel_stats.csv >&2 || true
+fi
