@@ -181,6 +181,7 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     if (rc) return rc;
     cs->work.scan_arena = (uint64_t*)cs->ws[39].p;
     carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap);
+    HIPOK(hipMemsetAsync(cs->work.scan_arena, 0, 8 * cs->work.scan_words, cs->stream));
     for (int k = 0; k < kNumScans; k++) cs->work.scan[k].error = &((Scalars*)cs->scal.p)->debug_error;
     return FDBCS_OK;
 }
@@ -239,10 +240,16 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(verdict, T);
 #undef TAKE
     w.edge_cap = edge_cap;
+    w.cap_T = T;
+    w.cap_R = R;
     cs->edge_cap = edge_cap;
     cs->ws_T = T;
     cs->ws_R = R;
     cs->ws_W = W;
+    // the epilogue of every batch re-zeroes these for the next one; start them zeroed
+    HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
+    HIPOK(hipMemsetAsync(w.ecnt_b, 0, 4 * R, cs->stream));
+    HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
     return ensure_scan_arena(cs);
 }
 
@@ -319,7 +326,9 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
     cs->tail_cap = tcap;
     // rebuild the range-max levels for the live history
     MaxLevels lv = levels_of(cs, cs->cur);
-    launch_blockmax(cs->stream, lv, &((Scalars*)cs->scal.p)->n, std::max<int64_t>(n, 1));
+    cs->work.lvl3 = (int64_t*)cs->lvl[3].p;
+    cs->work.lvl3_n = m;
+    launch_rangemax(cs->stream, lv, (Scalars*)cs->scal.p, m, std::max<int64_t>(n, 1));
     HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(cs->stream));
     return ensure_scan_arena(cs);
@@ -542,7 +551,7 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     s.tail_used = (int64_t)tail.size();
     HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
     MaxLevels lv = levels_of(cs, cs->cur);
-    launch_blockmax(cs->stream, lv, &((Scalars*)cs->scal.p)->n, std::max<int64_t>(n, 1));
+    launch_rangemax(cs->stream, lv, (Scalars*)cs->scal.p, cs->work.lvl3_n, std::max<int64_t>(n, 1));
     HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
@@ -707,8 +716,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
     if ((rc = ensure_history(cs, cs->n_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail.size() + 1))) return rc;
     if ((rc = ensure_events(b))) return rc;
-    // results staging: verdict | scalars | rconf | hist | first_conf
-    const size_t o_sc = align_up(T + 1, 64);
+    // results staging: verdicts + scalars (one D2H) | rconf | hist | first_conf
+    const size_t o_sc = (size_t)verdict_scalars_offset(T);
     const size_t o_rc = align_up(o_sc + sizeof(Scalars), 64);
     const size_t o_hc = align_up(o_rc + R + 1, 64);
     const size_t o_fc = align_up(o_hc + T + 1, 64);
@@ -720,7 +729,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     b->h_rconf = (uint8_t*)(ho + o_rc);
     b->h_hist = (uint8_t*)(ho + o_hc);
     b->h_first = (int32_t*)(ho + o_fc);
-    if ((rc = b->dverdict.ensure(T + 1))) return rc;
+    if ((rc = b->dverdict.ensure(o_sc + sizeof(Scalars)))) return rc;
+    b->any_report = false;
+    for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
 
     hipStream_t s = cs->stream;
     HIPOK(hipEventRecord(b->ev[kPhStart], s));
@@ -733,7 +744,6 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     Hist hs = hist_of(cs, src), hd = hist_of(cs, src ^ 1);
     MaxLevels lv = levels_of(cs, src);
 
-    launch_prepare(s, bd, w, sc);
     launch_check_reads(s, bd, hs, lv, (const uint8_t*)cs->htail.p, sc, cs->header_version, w);
     HIPOK(hipEventRecord(b->ev[kPhCheck], s));
     int sorted = 0;
@@ -742,7 +752,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_positions(s, bd, w, sorted);
     if (cs->validate) launch_validate_sort(s, bd, w, sorted, sc);
     launch_edges(s, bd, w, sc);
-    launch_resolve(s, bd, w, sc);
+    launch_resolve(s, bd, w, sc, b->any_report);
+    if (b->any_report) {  // before the epilogue re-zeroes hist_conf
+        if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(b->h_first, w.first_conf, 4 * T, hipMemcpyDeviceToHost, s));
+    }
     HIPOK(hipEventRecord(b->ev[kPhIntra], s));
     launch_combine(s, bd, w, sc);
     HIPOK(hipEventRecord(b->ev[kPhCombine], s));
@@ -762,20 +777,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     b->gc_ran = gc;
     MaxLevels lf = levels_of(cs, final_buf);
-    launch_blockmax(s, lf, gc ? &sc->n_gc : &sc->n_next, cs->n_ub + 2 * W + 1);
+    launch_epilogue(s, bd, w, lf, sc, gc ? 1 : 0, (uint8_t*)b->dverdict.p, cs->n_ub + 2 * W + 1);
     HIPOK(hipEventRecord(b->ev[kPhGc], s));
-    launch_finalize(s, bd, w, sc, gc ? 1 : 0, (uint8_t*)b->dverdict.p);
     HIPOK(hipGetLastError());
-    // results back
-    if (T) HIPOK(hipMemcpyAsync(b->h_verdict, b->dverdict.p, T, hipMemcpyDeviceToHost, s));
-    HIPOK(hipMemcpyAsync(b->h_scal, sc, sizeof(Scalars), hipMemcpyDeviceToHost, s));
-    b->any_report = false;
-    for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
-    if (b->any_report) {
-        if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(b->h_first, w.first_conf, 4 * T, hipMemcpyDeviceToHost, s));
-    }
+    // results back: verdicts and the scalars right behind them, one copy
+    HIPOK(hipMemcpyAsync(b->pin_out.p, b->dverdict.p, o_sc + sizeof(Scalars), hipMemcpyDeviceToHost, s));
     HIPOK(hipEventRecord(b->ev[kPhEnd], s));
     cs->cur = final_buf;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882

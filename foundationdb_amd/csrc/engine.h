@@ -105,19 +105,24 @@ struct Work {
     int64_t* seg_vend;
     uint8_t* verdict;      // [T]
     ScanState scan[kNumScans];
-    uint64_t* scan_arena;  // zeroed by k_prepare each batch
+    uint64_t* scan_arena;  // zeroed by the previous batch's epilogue (and at allocation)
     int64_t scan_words;
+    int64_t cap_T, cap_R;  // workspace capacity (what the epilogue zeroes)
+    int64_t* lvl3;         // top range-max level, reset by k_seg_search for the epilogue
+    int64_t lvl3_n;
 };
+
+// Byte offset of the Scalars copy that follows the verdicts in a batch's result buffer.
+__host__ __device__ inline int64_t verdict_scalars_offset(int64_t T) { return (T + 64) / 64 * 64; }
 
 // ---- launchers (kernels.hip); all enqueue on `s` and never synchronize.
 void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const MaxLevels& m, const uint8_t* htail,
                         const Scalars* sc, int64_t header_version, const Work& w);
-void launch_prepare(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, bool report);
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
                   Scalars* sc, int64_t now, int64_t header_version, int64_t grid_hint_n, hipEvent_t copy_begin,
@@ -126,7 +131,8 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, S
                int64_t header_version, int64_t grid_hint_n);
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap);
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap);
-void launch_blockmax(hipStream_t s, const MaxLevels& m, const int64_t* n_ptr, int64_t grid_hint_n);
-void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran, uint8_t* verdict_out);
+void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, int64_t lvl3_n, int64_t grid_hint_n);
+void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc, int gc_ran,
+                     uint8_t* verdict_out, int64_t grid_hint_n);
 
 }  // namespace fdbcs

@@ -171,44 +171,20 @@ void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const M
 
 // ------------------------------------------------------------------ D.Sort
 
-// First kernel of a batch: zero the per-batch scratch (transaction conflict flags, edge counters,
-// the scan arena) and emit the endpoint items (KeyInfo, SkipList.cpp:779-789) for the sort.
-__global__ __launch_bounds__(kBlock) void k_prepare(BatchDev b, Work w, Scalars* sc) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid == 0) sc->debug_error = 0;
-    for (int64_t i = tid; i < w.scan_words; i += stride) w.scan_arena[i] = 0;
-    for (int64_t i = tid; i < b.T; i += stride) w.hist_conf[i] = 0;
-    for (int64_t i = tid; i < b.R; i += stride) {
-        w.ecnt_b[i] = 0;
-        w.ecur[i] = 0;
-    }
-    for (int64_t g = tid; g < b.R + b.W; g += stride) {
-        const bool is_read = g < b.R;
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const DKey k = b.keys[2 * g + e];
-            // extra_ordering (SkipList.cpp:89-91): begin*2 + (write ^ begin)
-            const uint32_t cls = is_read ? (e ? kReadEnd : kReadBegin) : (e ? kWriteEnd : kWriteBegin);
-            SortItem it;
-            it.hi = k.hi;
-            it.lo = k.lo;
-            it.len = k.len;
-            it.tail = k.tail;
-            it.meta = ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
-            it.pad = 0;
-            w.items[1][2 * g + e] = it;
-        }
-    }
-}
-
-void launch_prepare(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
-    int64_t n = b.R + b.W;
-    n = n > b.T ? n : b.T;
-    n = n > w.scan_words ? n : w.scan_words;
-    int64_t grid = (n + kBlock - 1) / kBlock;
-    grid = grid < 1 ? 1 : (grid > 2048 ? 2048 : grid);
-    hipLaunchKernelGGL(k_prepare, dim3((unsigned)grid), dim3(kBlock), 0, s, b, w, sc);
+// Endpoint item p of the batch (KeyInfo, SkipList.cpp:77-87): range g = p / 2, end = p & 1.
+__device__ __forceinline__ SortItem make_item(const BatchDev& b, int p) {
+    const int g = p >> 1, e = p & 1;
+    const DKey k = b.keys[p];
+    // extra_ordering (SkipList.cpp:89-91): begin*2 + (write ^ begin)
+    const uint32_t cls = g < b.R ? (e ? kReadEnd : kReadBegin) : (e ? kWriteEnd : kWriteBegin);
+    SortItem it;
+    it.hi = k.hi;
+    it.lo = k.lo;
+    it.len = k.len;
+    it.tail = k.tail;
+    it.meta = ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
+    it.pad = 0;
+    return it;
 }
 
 // Merge-path split + 8-way serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties):
@@ -269,12 +245,11 @@ __device__ __forceinline__ void cex(SortItem& a, SortItem& b, bool active, const
 // Sort one tile of kSortTile endpoints: each thread sorts its 8 items with Batcher's odd-even
 // merge network (19 comparators, items past `mine` stay put), then runs of 8, 16, ... are merged
 // in LDS by merge path (each thread's 8 outputs always fall inside one pair of runs).
-__global__ __launch_bounds__(kSortThreads) void k_sort_tile(const SortItem* in, SortItem* out, int n,
-                                                      const uint8_t* arena) {
+__global__ __launch_bounds__(kSortThreads) void k_sort_tile(BatchDev b, SortItem* out, int n, const uint8_t* arena) {
     __shared__ SortItem sh[kSortTile];
     const int base = blockIdx.x * kSortTile;
     const int cnt = min(kSortTile, n - base);
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = in[base + i];
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = make_item(b, base + i);
     __syncthreads();
     const int o = threadIdx.x * 8;
     const int mine = max(0, min(8, cnt - o));
@@ -375,7 +350,7 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* re
     *result_buffer = 0;
     if (E == 0) return;
     const int tiles = (E + kSortTile - 1) / kSortTile;
-    hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kSortThreads), 0, s, w.items[1], w.items[0], E, b.tail);
+    hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kSortThreads), 0, s, b, w.items[0], E, b.tail);
     int cur = 0;
     for (int run = kSortTile; run < E; run *= 2) {
         hipLaunchKernelGGL(k_merge_pass, dim3(tiles), dim3(kSortThreads), 0, s, w.items[cur], w.items[cur ^ 1], E,
@@ -538,6 +513,17 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, Scalars* sc
     extern __shared__ __attribute__((aligned(16))) uint8_t st[];
     __shared__ int s_more;
     const int T = b.T;
+    if (sc->n_edges == 0 && !sc->edge_overflow) {
+        // no candidate writer anywhere: every admitted transaction without a history conflict
+        // commits (SkipList.cpp:817-833 with an empty MiniConflictSet); all workgroups share the work
+        for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
+            w.status[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
+            w.first_conf[t] = INT_MAX;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) sc->rounds = 0;
+        return;
+    }
+    if (blockIdx.x != 0) return;  // batch-order rounds run in one workgroup
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         st[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
         w.first_conf[t] = INT_MAX;
@@ -647,10 +633,10 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w, con
     }
 }
 
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, bool report) {
     if (b.T == 0) return;
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(kWG), (size_t)b.T, s, b, w, sc);
-    if (b.R) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
+    hipLaunchKernelGGL(k_resolve, dim3((b.T + kWG - 1) / kWG), dim3(kWG), (size_t)b.T, s, b, w, sc);
+    if (b.R && report) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
 }
 
 // ------------------------------------------------------------------ D.Combine
@@ -720,8 +706,11 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
 }
 
 __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, const uint8_t* htail,
-                                                       const Scalars* sc, int64_t hdr) {
+                                                       const Scalars* sc, int64_t hdr, int64_t* lvl3, int64_t lvl3_n) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    // the history check of this batch is done with the old hierarchy: reset its top level for the
+    // epilogue's atomicMax build
+    for (int64_t i = s; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
     const int U = sc->n_segments;
     if (s >= U) return;
     const int64_t n = sc->n;
@@ -773,13 +762,35 @@ constexpr int kSegLds = 1024;
 // Copy surviving old boundaries to their new positions.  Per tile, the segments that can affect
 // it are staged in LDS; element i is removed iff lo_j <= i < hi_j for the last segment j with
 // lo_j <= i, else it moves to i - rem_before + ins_before.
-__global__ __launch_bounds__(kBlock) void k_merge_copy(Work w, Hist src, Hist dst, const Scalars* sc) {
+__device__ __forceinline__ void write_insert(const BatchDev& b, const Work& w, Hist dst, uint8_t* htail,
+                                             const Scalars* sc, int64_t now, int s);
+
+__global__ __launch_bounds__(kBlock) void k_merge_copy(BatchDev b, Work w, Hist src, Hist dst, uint8_t* htail,
+                                                       const Scalars* sc, int64_t now) {
     __shared__ int64_t s_lo[kSegLds + 1], s_hi[kSegLds + 1], s_shift[kSegLds + 1];
     __shared__ int s_j0, s_cnt;
     const int64_t n = sc->n;
     const int U = sc->n_segments;
-    for (int64_t i0 = (int64_t)blockIdx.x * kGcTile; i0 < n; i0 += (int64_t)gridDim.x * kGcTile) {
+    __shared__ int s_ins0, s_ins1;
+    // tiles cover positions [0, n]: position n only owns the inserts of segments past every boundary
+    for (int64_t i0 = (int64_t)blockIdx.x * kGcTile; i0 <= n; i0 += (int64_t)gridDim.x * kGcTile) {
         const int64_t i1 = min(n, i0 + kGcTile);
+        if (threadIdx.x == 1) {
+            // segments whose B lands in this tile: lo in [i0, i0 + tile), or lo == n for the last tile
+            const int64_t hi_pos = (i0 + kGcTile > n) ? n + 1 : i0 + kGcTile;
+            int lo = 0, hi = U;
+            while (lo < hi) {
+                int mid = (lo + hi) >> 1;
+                if (w.seg_lo[mid] < i0) lo = mid + 1; else hi = mid;
+            }
+            s_ins0 = lo;
+            hi = U;
+            while (lo < hi) {
+                int mid = (lo + hi) >> 1;
+                if (w.seg_lo[mid] < hi_pos) lo = mid + 1; else hi = mid;
+            }
+            s_ins1 = lo;
+        }
         if (threadIdx.x == 0) {
             // ja = #segments with lo <= i0, jb = #segments with lo <= i1-1
             int lo = 0, hi = U;
@@ -863,16 +874,14 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Work w, Hist src, Hist ds
                 dst.ver[o] = src.ver[i];
             }
         }
+        for (int sg = s_ins0 + threadIdx.x; sg < s_ins1; sg += blockDim.x) write_insert(b, w, dst, htail, sc, now, sg);
         __syncthreads();
     }
 }
 
-// Write each segment's new boundaries: B at `now`, E (when needed) at its previous version.
-__global__ __launch_bounds__(kBlock) void k_merge_insert(BatchDev b, Work w, Hist dst, uint8_t* htail,
-                                                         const Scalars* sc, int64_t now) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    const int U = sc->n_segments;
-    if (s >= U) return;
+// Write segment s's new boundaries: B at `now`, E (when needed) at its previous version.
+__device__ __forceinline__ void write_insert(const BatchDev& b, const Work& w, Hist dst, uint8_t* htail,
+                                             const Scalars* sc, int64_t now, int s) {
     const int64_t o = w.seg_lo[s] - w.seg_rem[s] + w.seg_ins[s];
     int64_t toff = sc->tail_used + w.seg_tlen[s];
     const DKey kb = seg_key(b, w, w.seg_b[s], 0);
@@ -903,17 +912,15 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   hipEvent_t copy_end) {
     const int Wn = b.W > 0 ? b.W : 1;
     hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
-                       header_version);
+                       header_version, w.lvl3, w.lvl3_n);
     launch_scan<3>(s, SegSumScan{w.seg_rem, w.seg_ins, w.seg_tlen, sc}, &sc->n_segments, (int64_t)b.W + 1,
                    w.scan[kScanSegSum]);
     if (copy_begin) (void)hipEventRecord(copy_begin, s);
-    int64_t tiles = (grid_hint_n + kGcTile - 1) / kGcTile;
+    int64_t tiles = (grid_hint_n + 1 + kGcTile - 1) / kGcTile;
     if (tiles < 1) tiles = 1;
     if (tiles > 8192) tiles = 8192;
-    hipLaunchKernelGGL(k_merge_copy, dim3((unsigned)tiles), dim3(kBlock), 0, s, w, src, dst, sc);
+    hipLaunchKernelGGL(k_merge_copy, dim3((unsigned)tiles), dim3(kBlock), 0, s, b, w, src, dst, htail, sc, now);
     if (copy_end) (void)hipEventRecord(copy_end, s);
-    hipLaunchKernelGGL(k_merge_insert, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, dst, htail, sc,
-                       now);
 }
 
 // ------------------------------------------------------------------ D.RemoveBefore
@@ -968,63 +975,123 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap) {
     w.scan_words = g - a;
 }
 
-// ------------------------------------------------------------------ range-max hierarchy
+// ------------------------------------------------------------------ range-max hierarchy + epilogue
+//
+// One workgroup per 4096 boundaries: each wave reduces 16 blocks of 64 versions to level 1, wave 0
+// reduces the 64 level-1 values to level 2, and level 3 is built by atomicMax (reset beforehand).
+// With a batch attached the same launch writes the verdicts, publishes the scalars next to them for
+// the single D2H copy, and zeroes the scratch the next batch expects zeroed.
 
-__global__ __launch_bounds__(kBlock) void k_blockmax(const int64_t* in, int64_t* out, const int64_t* n_ptr,
-                                                     int level_shift) {
-    // level L: n_L = ceil(n / 64^L); one wave per 64-element block of level L-1
-    int64_t n = *n_ptr;
-    for (int k = 0; k < level_shift; k++) n = (n + kFan - 1) / kFan;
-    const int64_t nout = (n + kFan - 1) / kFan;
-    const int lane = threadIdx.x & 63;
-    for (int64_t blk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; blk < nout;
-         blk += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        const int64_t i = blk * kFan + lane;
-        int64_t v = i < n ? in[i] : LLONG_MIN;
-        for (int o = 32; o > 0; o >>= 1) {
-            int64_t y = __shfl_xor(v, o, 64);
-            v = y > v ? y : v;
+struct Epilogue {
+    const uint8_t* flags;
+    const uint8_t* status;
+    uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T)
+    int32_t T;
+    int gc_ran;
+    uint8_t* zero8;  // hist_conf
+    int64_t zero8_n;
+    int32_t* zero32a;  // ecnt_b
+    int32_t* zero32b;  // ecur
+    int64_t zero32_n;
+    uint64_t* zero64;  // scan arena
+    int64_t zero64_n;
+};
+
+__global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, int use_gc_n, Epilogue ep) {
+    __shared__ int64_t l1[kFan];
+    const int64_t n0 = use_gc_n == 2 ? sc->n : (use_gc_n ? sc->n_gc : sc->n_next);
+    const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t b2 = blockIdx.x; b2 < n2; b2 += gridDim.x) {
+#pragma unroll 4
+        for (int q = 0; q < kFan / 4; q++) {
+            const int64_t b1 = b2 * kFan + wid * (kFan / 4) + q;
+            const int64_t i = b1 * kFan + lane;
+            int64_t v = i < n0 ? m.lvl[0][i] : LLONG_MIN;
+            for (int o = 32; o > 0; o >>= 1) {
+                const int64_t y = __shfl_xor(v, o, 64);
+                v = y > v ? y : v;
+            }
+            if (lane == 0) {
+                if (b1 < n1) m.lvl[1][b1] = v;
+                l1[wid * (kFan / 4) + q] = v;
+            }
         }
-        if (lane == 0) out[blk] = v;
+        __syncthreads();
+        if (wid == 0) {
+            int64_t v = l1[lane];
+            for (int o = 32; o > 0; o >>= 1) {
+                const int64_t y = __shfl_xor(v, o, 64);
+                v = y > v ? y : v;
+            }
+            if (lane == 0) {
+                m.lvl[2][b2] = v;
+                atomicMax((long long*)&m.lvl[3][b2 / kFan], (long long)v);
+            }
+        }
+        __syncthreads();
     }
-}
-
-void launch_blockmax(hipStream_t s, const MaxLevels& m, const int64_t* n_ptr, int64_t grid_hint_n) {
-    int64_t n = grid_hint_n;
-    for (int L = 1; L < kMaxLevels; L++) {
-        const int64_t blocks = (n + kFan - 1) / kFan;  // output elements = waves
-        int64_t grid = (blocks * 64 + kBlock - 1) / kBlock;
-        if (grid < 1) grid = 1;
-        if (grid > 16384) grid = 16384;
-        hipLaunchKernelGGL(k_blockmax, dim3((unsigned)grid), dim3(kBlock), 0, s, m.lvl[L - 1], m.lvl[L], n_ptr,
-                           L - 1);
-        n = blocks;
-    }
-}
-
-// ------------------------------------------------------------------ verdicts
-
-__global__ __launch_bounds__(kBlock) void k_finalize(BatchDev b, Work w, Scalars* sc, int gc_ran,
-                                                     uint8_t* verdict_out) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < b.T) {
+    if (!ep.verdict_out) return;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = tid; t < ep.T; t += stride) {
         uint8_t v;
-        if (b.flags[t] & kFlagTooOld)
+        if (ep.flags[t] & kFlagTooOld)
             v = 1;  // TransactionTooOld (ConflictSet.h:42)
         else
-            v = w.status[t] == kCommitted ? 2 : 0;
-        verdict_out[t] = v;
+            v = ep.status[t] == kCommitted ? 2 : 0;
+        ep.verdict_out[t] = v;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        sc->n = gc_ran ? sc->n_gc : sc->n_next;
+    if (tid == 0) {
+        sc->n = use_gc_n ? sc->n_gc : sc->n_next;
         sc->tail_used = sc->tail_next;
+        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = *sc;
+        sc->debug_error = 0;
     }
+    for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
+    for (int64_t i = tid; i < ep.zero32_n; i += stride) {
+        ep.zero32a[i] = 0;
+        ep.zero32b[i] = 0;
+    }
+    for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
 }
 
-void launch_finalize(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, int gc_ran, uint8_t* verdict_out) {
-    const int T = b.T > 0 ? b.T : 1;
-    hipLaunchKernelGGL(k_finalize, dim3((T + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc, gc_ran,
-                       verdict_out);
+__global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lvl3[i] = LLONG_MIN;
+}
+
+static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
+    int64_t g = (hint_n + (int64_t)kFan * kFan - 1) / ((int64_t)kFan * kFan);
+    const int64_t ge = (extra + kBlock - 1) / kBlock;
+    g = g > ge ? g : ge;
+    g = g < 1 ? 1 : g;
+    return g > 4096 ? 4096 : g;
+}
+
+void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, int64_t lvl3_n, int64_t grid_hint_n) {
+    hipLaunchKernelGGL(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
+    Epilogue ep{};
+    hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, 2, ep);
+}
+
+void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc, int gc_ran,
+                     uint8_t* verdict_out, int64_t grid_hint_n) {
+    Epilogue ep;
+    ep.flags = b.flags;
+    ep.status = w.status;
+    ep.verdict_out = verdict_out;
+    ep.T = b.T;
+    ep.gc_ran = gc_ran;
+    ep.zero8 = w.hist_conf;
+    ep.zero8_n = w.cap_T;
+    ep.zero32a = w.ecnt_b;
+    ep.zero32b = w.ecur;
+    ep.zero32_n = w.cap_R;
+    ep.zero64 = w.scan_arena;
+    ep.zero64_n = w.scan_words;
+    int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
+    extra = extra > b.T ? extra : b.T;
+    hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
+                       gc_ran ? 1 : 0, ep);
 }
 
 }  // namespace fdbcs

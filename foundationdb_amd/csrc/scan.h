@@ -1,6 +1,6 @@
 // scan.h — single-pass device-wide exclusive scan with decoupled look-back (gfx950).
 //
-// One workgroup per 4096-element tile; tiles take ids from an atomic counter in launch order so a
+// One workgroup per 1024-element tile; tiles take ids from an atomic counter in launch order so a
 // tile only ever waits on tiles that are already running (no deadlock whatever the dispatch order).
 // Each tile publishes, per scanned component, an 8-byte granule {status << 32 | value} with an
 // agent-scope atomic store: status 1 = tile aggregate, 2 = inclusive prefix.  Look-back reads the
@@ -19,11 +19,11 @@
 namespace fdbcs {
 
 constexpr int kScanThreads = 256;
-constexpr int kScanPer = 16;
-constexpr int kScanTile = kScanThreads * kScanPer;  // 4096
-constexpr int kScanPad = kScanTile + kScanTile / 16;
+constexpr int kScanPer = 4;
+constexpr int kScanTile = kScanThreads * kScanPer;  // 1024: many workgroups even for small scans
+constexpr int kScanPad = kScanTile + kScanTile / 4;
 
-__device__ __forceinline__ int scan_slot(int e) { return e + (e >> 4); }  // one pad word per 16
+__device__ __forceinline__ int scan_slot(int e) { return e + (e >> 2); }  // one pad word per thread run
 
 __device__ __forceinline__ void granule_store(uint64_t* g, uint32_t status, uint32_t value) {
     __hip_atomic_store(g, ((uint64_t)status << 32) | value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr
     if (tile >= ntiles) return;  // spare tile of a device-sized launch: nobody waits on it
 
     // phase 1: coalesced visits
-#pragma unroll 4
+#pragma unroll
     for (int k = 0; k < kScanPer; k++) {
         const int e = k * kScanThreads + threadIdx.x;
         const int64_t i = base + e;
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr
     }
     __syncthreads();
     // phase 4: coalesced stores
-#pragma unroll 4
+#pragma unroll
     for (int k = 0; k < kScanPer; k++) {
         const int e = k * kScanThreads + threadIdx.x;
         const int64_t i = base + e;
