@@ -213,6 +213,11 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(first_conf, 4 * T);
     TAKE(items[0], sizeof(SortItem) * E);
     TAKE(items[1], sizeof(SortItem) * E);
+    TAKE(splitters, sizeof(SortItem) * 1024);
+    TAKE(bucket, 2 * E);
+    TAKE(bcount, 4 * 1024);
+    TAKE(bcursor, 4 * 1024);
+    TAKE(boff, 4 * 1028);
     TAKE(pos, 4 * E);
     TAKE(pmeta, 4 * E);
     TAKE(cwb, 4 * (E + 1));
@@ -250,6 +255,8 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
     HIPOK(hipMemsetAsync(w.ecnt_b, 0, 4 * R, cs->stream));
     HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
+    HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 1024, cs->stream));
+    HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 1024, cs->stream));
     return ensure_scan_arena(cs);
 }
 

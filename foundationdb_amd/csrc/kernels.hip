@@ -6,7 +6,7 @@
 // of ConflictBatch::detectConflicts is a data-parallel kernel:
 //
 //   D.CheckRead        k_check_reads      per read range: two searches + range max
-//   D.Sort             k_sort_tile / k_merge_pass   merge sort of endpoints by (key, class)
+//   D.Sort             k_sample, k_bucket_count/scatter/sort   sample sort of endpoints by (key, class)
 //   D.CheckIntraBatch  k_positions, k_edges_*, k_resolve   candidate edges + batch-order rounds
 //   D.Combine          k_combine          coverage scan over sorted endpoints
 //   D.MergeWrite       k_seg_search, k_merge_copy, k_merge_insert, k_blockmax
@@ -187,6 +187,22 @@ __device__ __forceinline__ SortItem make_item(const BatchDev& b, int p) {
     return it;
 }
 
+// Total order used by the sort: KeyInfo::operator< (key, then class; SkipList.cpp:114-128) with the
+// endpoint id as a final tie-break.  Endpoints equal in (key, class) are interchangeable for every
+// later use, so the tie-break changes nothing observable; it makes every item distinct,
+// which keeps sample-sort buckets balanced even when one hot key repeats thousands of times.
+__device__ __forceinline__ bool item_less_total(const SortItem& a, const SortItem& b, const uint8_t* arena) {
+    if (a.hi != b.hi) return a.hi < b.hi;
+    if (a.lo != b.lo) return a.lo < b.lo;
+    if (a.len != b.len || a.len > 16u) {
+        const int c = key_cmp(a.hi, a.lo, a.len, a.tail, arena, b.hi, b.lo, b.len, b.tail, arena);
+        if (c) return c < 0;
+    }
+    const uint32_t ca = item_class(a.meta), cb = item_class(b.meta);
+    if (ca != cb) return ca < cb;
+    return a.meta < b.meta;
+}
+
 // Merge-path split + 8-way serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties):
 // writes outputs [d, d+count) of the merged sequence to out[0, count).
 __device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
@@ -195,7 +211,7 @@ __device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortIt
     int hi = d < lenA ? d : lenA;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (!item_less(B[d - mid - 1], A[mid], arena))
+        if (!item_less_total(B[d - mid - 1], A[mid], arena))
             lo = mid + 1;
         else
             hi = mid;
@@ -204,7 +220,7 @@ __device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortIt
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         if (k < count) {
-            bool takeA = (j >= lenB) || (i < lenA && !item_less(B[j], A[i], arena));
+            bool takeA = (j >= lenB) || (i < lenA && !item_less_total(B[j], A[i], arena));
             out[k] = takeA ? A[i] : B[j];
             i += takeA ? 1 : 0;
             j += takeA ? 0 : 1;
@@ -219,14 +235,14 @@ __device__ __forceinline__ void merge8_to(const SortItem* A, int lenA, const Sor
     int hi = d < lenA ? d : lenA;
     while (lo < hi) {
         int mid = (lo + hi) >> 1;
-        if (!item_less(B[d - mid - 1], A[mid], arena))
+        if (!item_less_total(B[d - mid - 1], A[mid], arena))
             lo = mid + 1;
         else
             hi = mid;
     }
     int i = lo, j = d - lo;
     for (int k = 0; k < count; k++) {
-        const bool takeA = (j >= lenB) || (i < lenA && !item_less(B[j], A[i], arena));
+        const bool takeA = (j >= lenB) || (i < lenA && !item_less_total(B[j], A[i], arena));
         dst[k] = takeA ? A[i] : B[j];
         i += takeA ? 1 : 0;
         j += takeA ? 0 : 1;
@@ -235,22 +251,16 @@ __device__ __forceinline__ void merge8_to(const SortItem* A, int lenA, const Sor
 
 // Compare-exchange of two register items (constant indices keep them in VGPRs).
 __device__ __forceinline__ void cex(SortItem& a, SortItem& b, bool active, const uint8_t* arena) {
-    if (active && item_less(b, a, arena)) {
+    if (active && item_less_total(b, a, arena)) {
         SortItem t = a;
         a = b;
         b = t;
     }
 }
 
-// Sort one tile of kSortTile endpoints: each thread sorts its 8 items with Batcher's odd-even
-// merge network (19 comparators, items past `mine` stay put), then runs of 8, 16, ... are merged
-// in LDS by merge path (each thread's 8 outputs always fall inside one pair of runs).
-__global__ __launch_bounds__(kSortThreads) void k_sort_tile(BatchDev b, SortItem* out, int n, const uint8_t* arena) {
-    __shared__ SortItem sh[kSortTile];
-    const int base = blockIdx.x * kSortTile;
-    const int cnt = min(kSortTile, n - base);
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = make_item(b, base + i);
-    __syncthreads();
+// Sort sh[0, cnt) (cnt <= 8 * blockDim.x) in LDS: each thread sorts its 8 items with Batcher's
+// odd-even merge network (19 comparators), then runs of 8, 16, ... are merged by merge path.
+__device__ void lds_merge_sort(SortItem* sh, int cnt, const uint8_t* arena) {
     const int o = threadIdx.x * 8;
     const int mine = max(0, min(8, cnt - o));
     SortItem r[8];
@@ -280,84 +290,208 @@ __global__ __launch_bounds__(kSortThreads) void k_sort_tile(BatchDev b, SortItem
             if (k < mine) sh[o + k] = r[k];
         __syncthreads();
     }
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) out[base + i] = sh[i];
 }
 
-// Merge-path split over global memory by one wave: smallest i in [lo, hi) with B[d-i-1] < A[i]
-// (else hi), narrowing 64-fold per round instead of halving, so a 128k-element split costs
-// three dependent loads instead of seventeen.
-__device__ __forceinline__ int wave_merge_split(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
-                                                const uint8_t* arena) {
-    const int lane = threadIdx.x & 63;
-    int lo = d - lenB > 0 ? d - lenB : 0;
-    int hi = d < lenA ? d : lenA;
+// Rank sort of sh[0, cnt) into dst (global): every thread ranks its items against all cnt items,
+// read as LDS broadcasts.  O(cnt^2 / threads); used for small buckets.
+template <int PER>
+__device__ void lds_rank_sort_to(const SortItem* sh, int cnt, SortItem* dst, const uint8_t* arena) {
+    SortItem mine[PER];
+    int rank[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = threadIdx.x + k * blockDim.x;
+        if (i < cnt) mine[k] = sh[i];
+        rank[k] = 0;
+    }
+    for (int j = 0; j < cnt; j++) {
+        const SortItem y = sh[j];
+#pragma unroll
+        for (int k = 0; k < PER; k++) rank[k] += item_less_total(y, mine[k], arena) ? 1 : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        const int i = threadIdx.x + k * blockDim.x;
+        if (i < cnt) dst[rank[k]] = mine[k];
+    }
+}
+
+// ---- sample sort of the batch endpoints (D.Sort, SkipList.cpp:161-208)
+//
+// 1. k_sample: one workgroup rank-sorts S evenly spaced endpoints and keeps nb-1 splitters.
+// 2. k_bucket_count: each endpoint's bucket = number of splitters <= it; per-bucket counts.
+// 3. k_bucket_scatter: bucket offsets (prefix of the counts, recomputed per workgroup) and scatter.
+// 4. k_bucket_sort: one workgroup per bucket sorts it in LDS (rank sort, merge sort, or a
+//    workgroup-local merge over global memory for oversized buckets).
+constexpr int kSample = 2048;
+constexpr int kMaxBuckets = 1024;
+
+__global__ __launch_bounds__(kWG) void k_sample(BatchDev b, SortItem* splitters, int nb, const uint8_t* arena) {
+    __shared__ SortItem sh[kSample];  // 64 KiB
+    const int E = 2 * (b.R + b.W);
+    const int S = E < kSample ? E : kSample;
+    for (int i = threadIdx.x; i < S; i += blockDim.x) sh[i] = make_item(b, (int)(((int64_t)i * E) / S));
+    __syncthreads();
+    // rank-sort the sample in place: ranks into registers, barrier, then write
+    SortItem mine[2];
+    int rank[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int i = threadIdx.x + k * blockDim.x;
+        if (i < S) mine[k] = sh[i];
+    }
+    for (int j = 0; j < S; j++) {
+        const SortItem y = sh[j];
+#pragma unroll
+        for (int k = 0; k < 2; k++) rank[k] += item_less_total(y, mine[k], arena) ? 1 : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int i = threadIdx.x + k * blockDim.x;
+        if (i < S) sh[rank[k]] = mine[k];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x + 1; k < nb; k += blockDim.x) splitters[k - 1] = sh[(int)(((int64_t)k * S) / nb)];
+}
+
+__device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl, int nsplit, const uint8_t* arena) {
+    int lo = 0, hi = nsplit;  // number of splitters <= it (items are distinct: < suffices)
     while (lo < hi) {
-        const int span = hi - lo;
-        const int step = (span + 63) / 64;
-        const int i = lo + lane * step;
-        const bool pred = i < hi && item_less(B[d - i - 1], A[i], arena);
-        const uint64_t mask = __ballot(pred);
-        // lanes with i >= hi are treated as true (the answer is at most hi)
-        const int nvalid = (span + step - 1) / step;
-        const uint64_t beyond = nvalid >= 64 ? 0ull : (~0ull << nvalid);
-        const uint64_t m = mask | beyond;
-        if (m == 0) {
-            lo = lo + 63 * step + 1;
-            continue;
-        }
-        const int f = __ffsll((long long)m) - 1;  // first lane whose probe is at/after the split
-        const int nhi = lo + f * step;
-        const int nlo = f > 0 ? lo + (f - 1) * step + 1 : lo;
-        lo = nlo;
-        hi = nhi < hi ? nhi : hi;
+        const int mid = (lo + hi) >> 1;
+        if (!item_less_total(it, spl[mid], arena))
+            lo = mid + 1;
+        else
+            hi = mid;
     }
     return lo;
 }
 
-// Merge sorted runs of length w pairwise into runs of 2w; one output tile per workgroup.
-__global__ __launch_bounds__(kSortThreads) void k_merge_pass(const SortItem* in, SortItem* out, int n, int w,
-                                                       const uint8_t* arena) {
-    __shared__ SortItem sh[kSortTile];
-    __shared__ int split[2];
-    const int o0 = blockIdx.x * kSortTile;
-    if (o0 >= n) return;
-    const int pb = (o0 / (2 * w)) * (2 * w);
-    const int lenA = max(0, min(w, n - pb));
-    const int lenB = max(0, min(w, n - pb - w));
-    const SortItem* A = in + pb;
-    const SortItem* B = A + w;
-    const int d0 = o0 - pb;
-    const int d1 = min(d0 + kSortTile, lenA + lenB);
-    const int wave = threadIdx.x >> 6;
-    if (wave < 2) {
-        const int sp = wave_merge_split(A, lenA, B, lenB, wave ? d1 : d0, arena);
-        if ((threadIdx.x & 63) == 0) split[wave] = sp;
+__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const SortItem* splitters, int nb,
+                                                         uint16_t* bucket, int32_t* bcount, const uint8_t* arena) {
+    __shared__ SortItem spl[kMaxBuckets - 1];
+    __shared__ int hist[kMaxBuckets];
+    for (int i = threadIdx.x; i < nb - 1; i += blockDim.x) spl[i] = splitters[i];
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const int E = 2 * (b.R + b.W);
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < E) {
+        const int k = bucket_of(make_item(b, p), spl, nb - 1, arena);
+        bucket[p] = (uint16_t)k;
+        atomicAdd(&hist[k], 1);
     }
     __syncthreads();
-    const int i0 = split[0], i1 = split[1];
-    const int j0 = d0 - i0, j1 = d1 - i1;
-    const int na = i1 - i0, nb = j1 - j0;
-    for (int i = threadIdx.x; i < na; i += blockDim.x) sh[i] = A[i0 + i];
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) sh[na + i] = B[j0 + i];
+    for (int i = threadIdx.x; i < nb; i += blockDim.x)
+        if (hist[i]) atomicAdd(&bcount[i], hist[i]);
+}
+
+__device__ __forceinline__ void bucket_prefix(const int32_t* bcount, int nb, int* off) {
+    // off[k] = sum of bcount[0..k); blockDim.x threads, nb <= 4 * blockDim.x
+    __shared__ int part[kBlock];
+    const int per = (nb + blockDim.x - 1) / blockDim.x;
+    const int a = threadIdx.x * per;
+    int sum = 0;
+    for (int k = a; k < a + per && k < nb; k++) sum += bcount[k];
+    part[threadIdx.x] = sum;
     __syncthreads();
-    const int o = threadIdx.x * 8;
-    const int mine = max(0, min(8, (d1 - d0) - o));
-    if (mine > 0) merge8_to(sh, na, sh + na, nb, o, out + o0 + o, mine, arena);
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int q = 0; q < (int)blockDim.x; q++) {
+            const int x = part[q];
+            part[q] = run;
+            run += x;
+        }
+    }
+    __syncthreads();
+    int run = part[threadIdx.x];
+    for (int k = a; k < a + per && k < nb; k++) {
+        off[k] = run;
+        run += bcount[k];
+    }
+    if (threadIdx.x == blockDim.x - 1) off[nb] = run;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uint16_t* bucket, const int32_t* bcount,
+                                                           int32_t* bcursor, int32_t* boff_out, int nb, SortItem* out) {
+    __shared__ int off[kMaxBuckets + 1];
+    bucket_prefix(bcount, nb, off);
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k <= nb; k += blockDim.x) boff_out[k] = off[k];
+    const int E = 2 * (b.R + b.W);
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < E) {
+        const int k = bucket[p];
+        out[off[k] + atomicAdd(&bcursor[k], 1)] = make_item(b, p);
+    }
+}
+
+// Sort one bucket; data in a[off, off+m), scratch in tmp (same offsets).  Result in a.
+__global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
+                                                              const uint8_t* arena) {
+    __shared__ SortItem sh[kSortTile];  // 128 KiB
+    const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
+    if (m <= 1) return;
+    if (m <= kSortTile) {
+        for (int i = threadIdx.x; i < m; i += blockDim.x) sh[i] = a[off + i];
+        __syncthreads();
+        if (m <= 2 * kSortThreads) {
+            lds_rank_sort_to<2>(sh, m, a + off, arena);
+        } else {
+            lds_merge_sort(sh, m, arena);
+            for (int i = threadIdx.x; i < m; i += blockDim.x) a[off + i] = sh[i];
+        }
+        return;
+    }
+    // oversized bucket (skewed sample): sort tiles in LDS, then merge pairs through global memory
+    for (int c = 0; c < m; c += kSortTile) {
+        const int cnt = min(kSortTile, m - c);
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = a[off + c + i];
+        __syncthreads();
+        lds_merge_sort(sh, cnt, arena);
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) a[off + c + i] = sh[i];
+        __syncthreads();
+    }
+    SortItem* src = a + off;
+    SortItem* dst = tmp + off;
+    for (int w = kSortTile; w < m; w *= 2) {
+        for (int o0 = 0; o0 < m; o0 += 8 * blockDim.x) {
+            const int o = o0 + threadIdx.x * 8;
+            if (o < m) {
+                const int pb = (o / (2 * w)) * (2 * w);
+                const int lenA = max(0, min(w, m - pb));
+                const int lenB = max(0, min(w, m - pb - w));
+                merge8_to(src + pb, lenA, src + pb + w, lenB, o - pb, dst + o, min(8, m - o), arena);
+            }
+        }
+        __syncthreads();
+        SortItem* t = src;
+        src = dst;
+        dst = t;
+    }
+    if (src != a + off) {
+        for (int i = threadIdx.x; i < m; i += blockDim.x) a[off + i] = src[i];
+    }
+}
+
+int sort_buckets(int E) {
+    int nb = (E + 399) / 400;
+    nb = nb < 1 ? 1 : nb;
+    return nb > kMaxBuckets ? kMaxBuckets : nb;
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
-    const int tiles = (E + kSortTile - 1) / kSortTile;
-    hipLaunchKernelGGL(k_sort_tile, dim3(tiles), dim3(kSortThreads), 0, s, b, w.items[0], E, b.tail);
-    int cur = 0;
-    for (int run = kSortTile; run < E; run *= 2) {
-        hipLaunchKernelGGL(k_merge_pass, dim3(tiles), dim3(kSortThreads), 0, s, w.items[cur], w.items[cur ^ 1], E,
-                           run, b.tail);
-        cur ^= 1;
-    }
-    *result_buffer = cur;
+    const int nb = sort_buckets(E);
+    if (nb > 1) hipLaunchKernelGGL(k_sample, dim3(1), dim3(kWG), 0, s, b, w.splitters, nb, b.tail);
+    const int grid = (E + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.splitters, nb, w.bucket, w.bcount, b.tail);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
+                       w.items[0]);
+    hipLaunchKernelGGL(k_bucket_sort, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
 }
 
 // ------------------------------------------------------------------ positions
@@ -398,7 +532,7 @@ __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted
                                                           Scalars* sc) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= E) return;
-    bool bad = p > 0 && item_less(sorted[p], sorted[p - 1], arena);
+    bool bad = p > 0 && !item_less_total(sorted[p - 1], sorted[p], arena);
     const int q = pos[p];  // slot p -> position
     bad |= q < 0 || q >= E || (2 * item_range(pmeta[q]) + item_is_end(pmeta[q])) != (uint32_t)p;
     if (bad) atomicOr(&sc->debug_error, 1);
@@ -995,6 +1129,8 @@ struct Epilogue {
     int64_t zero32_n;
     uint64_t* zero64;  // scan arena
     int64_t zero64_n;
+    int32_t* zero_bc;  // sample-sort bucket counts and cursors
+    int32_t* zero_bk;
 };
 
 __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, int use_gc_n, Epilogue ep) {
@@ -1053,6 +1189,10 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, i
         ep.zero32b[i] = 0;
     }
     for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
+    for (int64_t i = tid; i < 1024; i += stride) {
+        ep.zero_bc[i] = 0;
+        ep.zero_bk[i] = 0;
+    }
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
@@ -1088,6 +1228,8 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.zero32_n = w.cap_R;
     ep.zero64 = w.scan_arena;
     ep.zero64_n = w.scan_words;
+    ep.zero_bc = w.bcount;
+    ep.zero_bk = w.bcursor;
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
     hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
