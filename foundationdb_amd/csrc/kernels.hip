@@ -191,16 +191,29 @@ __device__ __forceinline__ SortItem make_item(const BatchDev& b, int p) {
 // endpoint id as a final tie-break.  Endpoints equal in (key, class) are interchangeable for every
 // later use, so the tie-break changes nothing observable; it makes every item distinct,
 // which keeps sample-sort buckets balanced even when one hot key repeats thousands of times.
-__device__ __forceinline__ bool item_less_total(const SortItem& a, const SortItem& b, const uint8_t* arena) {
-    if (a.hi != b.hi) return a.hi < b.hi;
-    if (a.lo != b.lo) return a.lo < b.lo;
-    if (a.len != b.len || a.len > 16u) {
-        const int c = key_cmp(a.hi, a.lo, a.len, a.tail, arena, b.hi, b.lo, b.len, b.tail, arena);
-        if (c) return c < 0;
-    }
-    const uint32_t ca = item_class(a.meta), cb = item_class(b.meta);
+__device__ __noinline__ bool item_less_tail(uint32_t alen, uint32_t atail, uint32_t ameta, uint32_t blen,
+                                            uint32_t btail, uint32_t bmeta, const uint8_t* arena) {
+    const int c = tail_cmp(arena + atail, alen, arena + btail, blen);
+    if (c) return c < 0;
+    const uint32_t ca = item_class(ameta), cb = item_class(bmeta);
     if (ca != cb) return ca < cb;
-    return a.meta < b.meta;
+    return ameta < bmeta;
+}
+
+// Packed tie-break word: capped length (17 stands for "longer than the prefix"), class, id.
+__device__ __forceinline__ uint64_t item_aux(const SortItem& a) {
+    const uint64_t l = a.len > 16u ? 17u : a.len;
+    return (l << 40) | ((uint64_t)item_class(a.meta) << 32) | a.meta;
+}
+
+// Branch-free on the common path; the tail comparison (both keys longer than 16 bytes with
+// equal prefixes) is out of line.
+__device__ __forceinline__ bool item_less_total(const SortItem& a, const SortItem& b, const uint8_t* arena) {
+    const bool hi_eq = a.hi == b.hi, lo_eq = a.lo == b.lo;
+    if (hi_eq && lo_eq && a.len > 16u && b.len > 16u)
+        return item_less_tail(a.len, a.tail, a.meta, b.len, b.tail, b.meta, arena);
+    const bool aux_lt = item_aux(a) < item_aux(b);
+    return (a.hi < b.hi) | (hi_eq & ((a.lo < b.lo) | (lo_eq & aux_lt)));
 }
 
 // Merge-path split + 8-way serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties):
@@ -304,6 +317,7 @@ __device__ void lds_rank_sort_to(const SortItem* sh, int cnt, SortItem* dst, con
         if (i < cnt) mine[k] = sh[i];
         rank[k] = 0;
     }
+#pragma unroll 8
     for (int j = 0; j < cnt; j++) {
         const SortItem y = sh[j];
 #pragma unroll
@@ -323,34 +337,28 @@ __device__ void lds_rank_sort_to(const SortItem* sh, int cnt, SortItem* dst, con
 // 3. k_bucket_scatter: bucket offsets (prefix of the counts, recomputed per workgroup) and scatter.
 // 4. k_bucket_sort: one workgroup per bucket sorts it in LDS (rank sort, merge sort, or a
 //    workgroup-local merge over global memory for oversized buckets).
-constexpr int kSample = 2048;
+constexpr int kSample = 1024;
 constexpr int kMaxBuckets = 1024;
 
 __global__ __launch_bounds__(kWG) void k_sample(BatchDev b, SortItem* splitters, int nb, const uint8_t* arena) {
-    __shared__ SortItem sh[kSample];  // 64 KiB
+    __shared__ SortItem sh[kSample];  // 32 KiB
     const int E = 2 * (b.R + b.W);
     const int S = E < kSample ? E : kSample;
-    for (int i = threadIdx.x; i < S; i += blockDim.x) sh[i] = make_item(b, (int)(((int64_t)i * E) / S));
-    __syncthreads();
-    // rank-sort the sample in place: ranks into registers, barrier, then write
-    SortItem mine[2];
-    int rank[2] = {0, 0};
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int i = threadIdx.x + k * blockDim.x;
-        if (i < S) mine[k] = sh[i];
+    const int i = threadIdx.x;
+    SortItem mine;
+    if (i < S) {
+        mine = make_item(b, (int)(((int64_t)i * E) / S));
+        sh[i] = mine;
     }
+    __syncthreads();
+    int rank = 0;
+#pragma unroll 8
     for (int j = 0; j < S; j++) {
         const SortItem y = sh[j];
-#pragma unroll
-        for (int k = 0; k < 2; k++) rank[k] += item_less_total(y, mine[k], arena) ? 1 : 0;
+        rank += item_less_total(y, mine, arena) ? 1 : 0;
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int i = threadIdx.x + k * blockDim.x;
-        if (i < S) sh[rank[k]] = mine[k];
-    }
+    if (i < S) sh[rank] = mine;
     __syncthreads();
     for (int k = threadIdx.x + 1; k < nb; k += blockDim.x) splitters[k - 1] = sh[(int)(((int64_t)k * S) / nb)];
 }
@@ -386,45 +394,62 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const SortI
         if (hist[i]) atomicAdd(&bcount[i], hist[i]);
 }
 
+// off[k] = sum of bcount[0..k) for k <= nb (nb <= 4 * kBlock), by one block.
 __device__ __forceinline__ void bucket_prefix(const int32_t* bcount, int nb, int* off) {
-    // off[k] = sum of bcount[0..k); blockDim.x threads, nb <= 4 * blockDim.x
-    __shared__ int part[kBlock];
-    const int per = (nb + blockDim.x - 1) / blockDim.x;
+    __shared__ int wsum[kBlock / 64];
+    const int per = 4;
     const int a = threadIdx.x * per;
+    int v[per];
     int sum = 0;
-    for (int k = a; k < a + per && k < nb; k++) sum += bcount[k];
-    part[threadIdx.x] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int q = 0; q < (int)blockDim.x; q++) {
-            const int x = part[q];
-            part[q] = run;
-            run += x;
-        }
+#pragma unroll
+    for (int k = 0; k < per; k++) {
+        v[k] = a + k < nb ? bcount[a + k] : 0;
+        sum += v[k];
     }
-    __syncthreads();
-    int run = part[threadIdx.x];
-    for (int k = a; k < a + per && k < nb; k++) {
-        off[k] = run;
-        run += bcount[k];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    if (threadIdx.x == blockDim.x - 1) off[nb] = run;
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int before = 0;
+    for (int q = 0; q < wid; q++) before += wsum[q];
+    int run = before + x - sum;
+#pragma unroll
+    for (int k = 0; k < per; k++) {
+        if (a + k <= nb) off[a + k] = run;
+        run += v[k];
+    }
     __syncthreads();
 }
 
 __global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uint16_t* bucket, const int32_t* bcount,
                                                            int32_t* bcursor, int32_t* boff_out, int nb, SortItem* out) {
     __shared__ int off[kMaxBuckets + 1];
+    __shared__ int local[kMaxBuckets];
     bucket_prefix(bcount, nb, off);
     if (blockIdx.x == 0)
         for (int k = threadIdx.x; k <= nb; k += blockDim.x) boff_out[k] = off[k];
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) local[k] = 0;
+    __syncthreads();
     const int E = 2 * (b.R + b.W);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    int k = -1, slot = 0;
     if (p < E) {
-        const int k = bucket[p];
-        out[off[k] + atomicAdd(&bcursor[k], 1)] = make_item(b, p);
+        k = bucket[p];
+        slot = atomicAdd(&local[k], 1);  // order inside a bucket is irrelevant: it is sorted next
     }
+    __syncthreads();
+    // one global reservation per (workgroup, bucket)
+    for (int q = threadIdx.x; q < nb; q += blockDim.x) {
+        const int c = local[q];
+        local[q] = c ? atomicAdd(&bcursor[q], c) : 0;
+    }
+    __syncthreads();
+    if (p < E) out[off[k] + local[k] + slot] = make_item(b, p);
 }
 
 // Sort one bucket; data in a[off, off+m), scratch in tmp (same offsets).  Result in a.
