@@ -180,6 +180,8 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     int rc = cs->ws[39].ensure(8 * words + 64);
     if (rc) return rc;
     cs->work.scan_arena = (uint64_t*)cs->ws[39].p;
+    if ((rc = cs->ws[38].ensure(4 * (cs->hist_cap / kGcTile + 4)))) return rc;
+    cs->work.tile_first = (int32_t*)cs->ws[38].p;
     carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap);
     HIPOK(hipMemsetAsync(cs->work.scan_arena, 0, 8 * cs->work.scan_words, cs->stream));
     for (int k = 0; k < kNumScans; k++) cs->work.scan[k].error = &((Scalars*)cs->scal.p)->debug_error;

@@ -113,6 +113,7 @@ struct Work {
     uint64_t* scan_arena;  // zeroed by the previous batch's epilogue (and at allocation)
     int64_t scan_words;
     int64_t cap_T, cap_R;  // workspace capacity (what the epilogue zeroes)
+    int32_t* tile_first;   // [hist_cap / kGcTile + 3] first segment of each merge-copy tile
     int64_t* lvl3;         // top range-max level, reset by k_seg_search for the epilogue
     int64_t lvl3_n;
 };

@@ -305,61 +305,23 @@ __device__ void lds_merge_sort(SortItem* sh, int cnt, const uint8_t* arena) {
     }
 }
 
-// Rank sort of sh[0, cnt) into dst (global): every thread ranks its items against all cnt items,
-// read as LDS broadcasts.  O(cnt^2 / threads); used for small buckets.
-template <int PER>
-__device__ void lds_rank_sort_to(const SortItem* sh, int cnt, SortItem* dst, const uint8_t* arena) {
-    SortItem mine[PER];
-    int rank[PER];
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int i = threadIdx.x + k * blockDim.x;
-        if (i < cnt) mine[k] = sh[i];
-        rank[k] = 0;
-    }
-#pragma unroll 8
-    for (int j = 0; j < cnt; j++) {
-        const SortItem y = sh[j];
-#pragma unroll
-        for (int k = 0; k < PER; k++) rank[k] += item_less_total(y, mine[k], arena) ? 1 : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < PER; k++) {
-        const int i = threadIdx.x + k * blockDim.x;
-        if (i < cnt) dst[rank[k]] = mine[k];
-    }
-}
-
 // ---- sample sort of the batch endpoints (D.Sort, SkipList.cpp:161-208)
 //
-// 1. k_sample: one workgroup rank-sorts S evenly spaced endpoints and keeps nb-1 splitters.
+// 1. k_sample: one workgroup merge-sorts S evenly spaced endpoints and keeps nb-1 splitters.
 // 2. k_bucket_count: each endpoint's bucket = number of splitters <= it; per-bucket counts.
 // 3. k_bucket_scatter: bucket offsets (prefix of the counts, recomputed per workgroup) and scatter.
-// 4. k_bucket_sort: one workgroup per bucket sorts it in LDS (rank sort, merge sort, or a
-//    workgroup-local merge over global memory for oversized buckets).
+// 4. k_bucket_sort: one workgroup per bucket merge-sorts it in LDS (oversized buckets: LDS tiles
+//    then a workgroup-local merge over global memory).
 constexpr int kSample = 1024;
 constexpr int kMaxBuckets = 1024;
 
-__global__ __launch_bounds__(kWG) void k_sample(BatchDev b, SortItem* splitters, int nb, const uint8_t* arena) {
+__global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SortItem* splitters, int nb, const uint8_t* arena) {
     __shared__ SortItem sh[kSample];  // 32 KiB
     const int E = 2 * (b.R + b.W);
     const int S = E < kSample ? E : kSample;
-    const int i = threadIdx.x;
-    SortItem mine;
-    if (i < S) {
-        mine = make_item(b, (int)(((int64_t)i * E) / S));
-        sh[i] = mine;
-    }
+    for (int i = threadIdx.x; i < S; i += blockDim.x) sh[i] = make_item(b, (int)(((int64_t)i * E) / S));
     __syncthreads();
-    int rank = 0;
-#pragma unroll 8
-    for (int j = 0; j < S; j++) {
-        const SortItem y = sh[j];
-        rank += item_less_total(y, mine, arena) ? 1 : 0;
-    }
-    __syncthreads();
-    if (i < S) sh[rank] = mine;
-    __syncthreads();
+    lds_merge_sort(sh, S, arena);  // 8 items per thread: S <= 8 * kBlock
     for (int k = threadIdx.x + 1; k < nb; k += blockDim.x) splitters[k - 1] = sh[(int)(((int64_t)k * S) / nb)];
 }
 
@@ -461,12 +423,8 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
     if (m <= kSortTile) {
         for (int i = threadIdx.x; i < m; i += blockDim.x) sh[i] = a[off + i];
         __syncthreads();
-        if (m <= 2 * kSortThreads) {
-            lds_rank_sort_to<2>(sh, m, a + off, arena);
-        } else {
-            lds_merge_sort(sh, m, arena);
-            for (int i = threadIdx.x; i < m; i += blockDim.x) a[off + i] = sh[i];
-        }
+        lds_merge_sort(sh, m, arena);
+        for (int i = threadIdx.x; i < m; i += blockDim.x) a[off + i] = sh[i];
         return;
     }
     // oversized bucket (skewed sample): sort tiles in LDS, then merge pairs through global memory
@@ -511,7 +469,7 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* re
     *result_buffer = 0;
     if (E == 0) return;
     const int nb = sort_buckets(E);
-    if (nb > 1) hipLaunchKernelGGL(k_sample, dim3(1), dim3(kWG), 0, s, b, w.splitters, nb, b.tail);
+    if (nb > 1) hipLaunchKernelGGL(k_sample, dim3(1), dim3(kBlock), 0, s, b, w.splitters, nb, b.tail);
     const int grid = (E + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.splitters, nb, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
@@ -889,9 +847,13 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
 }
 
-// Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per segment.
+// Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per segment; in the
+// same pass, tile_first[t] = first segment whose lo lies in copy tile t or later, so each copy tile
+// knows its segments without searching.
 struct SegSumScan {
     int64_t *rem, *ins, *tlen;
+    const int64_t* lo;
+    int32_t* tile_first;
     Scalars* sc;
     __device__ void load(int64_t j, uint32_t (&v)[3]) const {
         v[0] = (uint32_t)rem[j];
@@ -902,6 +864,8 @@ struct SegSumScan {
         rem[j] = ex[0];
         ins[j] = ex[1];
         tlen[j] = ex[2];
+        const int64_t t0 = j > 0 ? lo[j - 1] / kGcTile + 1 : 0;
+        for (int64_t t = t0; t <= lo[j] / kGcTile; t++) tile_first[t] = (int32_t)j;
     }
     __device__ void finish(const uint32_t (&tot)[3]) const {
         const int64_t U = sc->n_segments;
@@ -909,6 +873,8 @@ struct SegSumScan {
         rem[U] = tot[0];
         ins[U] = tot[1];
         tlen[U] = tot[2];
+        const int64_t t0 = U > 0 ? lo[U - 1] / kGcTile + 1 : 0;
+        for (int64_t t = t0; t <= sc->n / kGcTile + 1; t++) tile_first[t] = (int32_t)U;
         sc->n_before = sc->n;
         sc->rem_total = tot[0];
         sc->n_next = sc->n - (int64_t)tot[0] + (int64_t)tot[1];
@@ -934,37 +900,12 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(BatchDev b, Work w, Hist 
     // tiles cover positions [0, n]: position n only owns the inserts of segments past every boundary
     for (int64_t i0 = (int64_t)blockIdx.x * kGcTile; i0 <= n; i0 += (int64_t)gridDim.x * kGcTile) {
         const int64_t i1 = min(n, i0 + kGcTile);
-        if (threadIdx.x == 1) {
-            // segments whose B lands in this tile: lo in [i0, i0 + tile), or lo == n for the last tile
-            const int64_t hi_pos = (i0 + kGcTile > n) ? n + 1 : i0 + kGcTile;
-            int lo = 0, hi = U;
-            while (lo < hi) {
-                int mid = (lo + hi) >> 1;
-                if (w.seg_lo[mid] < i0) lo = mid + 1; else hi = mid;
-            }
-            s_ins0 = lo;
-            hi = U;
-            while (lo < hi) {
-                int mid = (lo + hi) >> 1;
-                if (w.seg_lo[mid] < hi_pos) lo = mid + 1; else hi = mid;
-            }
-            s_ins1 = lo;
-        }
         if (threadIdx.x == 0) {
-            // ja = #segments with lo <= i0, jb = #segments with lo <= i1-1
-            int lo = 0, hi = U;
-            while (lo < hi) {
-                int mid = (lo + hi) >> 1;
-                if (w.seg_lo[mid] <= i0) lo = mid + 1; else hi = mid;
-            }
-            const int ja = lo;
-            hi = U;
-            while (lo < hi) {
-                int mid = (lo + hi) >> 1;
-                if (w.seg_lo[mid] <= i1 - 1) lo = mid + 1; else hi = mid;
-            }
-            s_j0 = ja;
-            s_cnt = lo - ja;  // segments starting inside the tile
+            const int64_t t = i0 / kGcTile;
+            s_ins0 = w.tile_first[t];
+            s_ins1 = w.tile_first[t + 1];
+            s_j0 = s_ins0;  // slots: segment ja-1 (last with lo < i0), then the tile's own segments
+            s_cnt = s_ins1 - s_ins0;
         }
         __syncthreads();
         const int ja = s_j0, cnt = s_cnt;
@@ -1072,8 +1013,8 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     const int Wn = b.W > 0 ? b.W : 1;
     hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
                        header_version, w.lvl3, w.lvl3_n);
-    launch_scan<3>(s, SegSumScan{w.seg_rem, w.seg_ins, w.seg_tlen, sc}, &sc->n_segments, (int64_t)b.W + 1,
-                   w.scan[kScanSegSum]);
+    launch_scan<3>(s, SegSumScan{w.seg_rem, w.seg_ins, w.seg_tlen, w.seg_lo, w.tile_first, sc}, &sc->n_segments,
+                   (int64_t)b.W + 1, w.scan[kScanSegSum]);
     if (copy_begin) (void)hipEventRecord(copy_begin, s);
     int64_t tiles = (grid_hint_n + 1 + kGcTile - 1) / kGcTile;
     if (tiles < 1) tiles = 1;
