@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for the verdict all-reduce (nccl = RCCL over xGMI)")
     return ap.parse_args()
 
 
@@ -139,11 +141,14 @@ def main():
     import torch
 
     dist = None
+    ndev = max(1, torch.cuda.device_count())
+    device = local % ndev  # one rank per GPU; more ranks than GPUs only for rehearsals (gloo)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.backend)
+    cdev = "cuda" if args.backend == "nccl" else "cpu"
     from foundationdb_amd import build as fbuild
 
     fbuild.build()
@@ -161,7 +166,7 @@ def main():
     routed = [sharding.route(pb)[rank] for pb, _, _ in gbatches] if sharding else None
     log(f"[rank {rank}] generated history {len(vers)} + {total} batches in {time.time() - t0:.1f}s")
 
-    cs = C.ConflictSet(local)
+    cs = C.ConflictSet(device)
     cs.set_gc_interval(args.gc_interval)
     cs.load_history(kb, ko, vers, 0)
     mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
@@ -185,7 +190,7 @@ def main():
             v = objs[i].wait()
             if combine:
                 T = gbatches[i][0].n_txn
-                c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to("cuda")
+                c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
                 dist.all_reduce(c, op=dist.ReduceOp.MAX)
 
     run(0, args.warmup, dist is not None)
@@ -202,7 +207,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = cs.stats()

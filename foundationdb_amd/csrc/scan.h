@@ -108,35 +108,43 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr
         texcl[c] += before;
         btot[c] = all;
     }
-    // phase 3: look-back, one thread per component
-    if (threadIdx.x < K) {
-        const int c = threadIdx.x;
-        uint64_t* g = st.granules;
-        uint32_t prefix = 0;
-        if (tile == 0) {
-            granule_store(&g[c], 2, btot[c]);
-        } else {
-            granule_store(&g[(int64_t)tile * K + c], 1, btot[c]);
-            int64_t j = tile - 1;
+    // phase 3: look-back by wave 0, 64 predecessor tiles per probe (tile -1 reads as an inclusive 0)
+    if (wid == 0) {
+#pragma unroll
+        for (int c = 0; c < K; c++) {
+            uint64_t* g = st.granules;
+            if (lane == 0) granule_store(&g[(int64_t)tile * K + c], tile == 0 ? 2 : 1, btot[c]);
+            uint32_t prefix = 0;
+            int64_t jhi = (int64_t)tile - 1;
             uint32_t spins = 0;
-            for (;;) {
-                const uint64_t x = granule_load(&g[j * K + c]);
+            while (jhi >= 0) {
+                const int64_t j = jhi - lane;
+                const uint64_t x = j >= 0 ? granule_load(&g[j * K + c]) : (2ull << 32);
                 const uint32_t status = (uint32_t)(x >> 32);
-                if (status == 0) {
-                    if (++spins > (1u << 26)) {  // bounded: never hang the GPU
-                        atomicOr(st.error, 1);
+                const uint64_t incl = __ballot(status == 2);
+                const uint64_t zero = __ballot(status == 0);
+                const int first = incl ? __ffsll((long long)incl) - 1 : 63;
+                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+                if (zero & upto) {  // a tile in the window has not published yet
+                    if (++spins > (1u << 24)) {  // bounded: never hang the GPU
+                        if (lane == 0) atomicOr(st.error, 2);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                prefix += (uint32_t)x;
-                if (status == 2) break;
-                j--;
+                uint32_t v = (lane <= first) ? (uint32_t)x : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                prefix += v;
+                if (incl) break;
+                jhi -= 64;
             }
-            granule_store(&g[(int64_t)tile * K + c], 2, prefix + btot[c]);
+            if (lane == 0) {
+                if (tile > 0) granule_store(&g[(int64_t)tile * K + c], 2, prefix + btot[c]);
+                sbase[c] = prefix;
+            }
         }
-        sbase[c] = prefix;
     }
     __syncthreads();
 #pragma unroll

@@ -231,3 +231,24 @@ def test_cpp_shim_driver(tmp_path):
     out = subprocess.check_output([exe], text=True, timeout=120)
     assert "b1 commit=2 tooold=0 report1=1" in out, out
     assert "b2 commit=1 first=1" in out, out
+
+
+def test_sharded_engines_match_sharded_oracles(engine, oracle_mod):
+    """Two key-range shards (two engine handles) fed by the proxy routing, combined by min, equal
+    two oracles fed the same way (CommitProxyServer.actor.cpp:118-187, 764-780)."""
+    from foundationdb_amd.sharding import KeyRangeSharding
+
+    sh = KeyRangeSharding.uniform(2)
+    engines = [EngineDriver(engine) for _ in range(2)]
+    oracles = [oracle_mod.OracleConflictSet() for _ in range(2)]
+    rng = np.random.default_rng(21)
+    now = 10
+    for _ in range(8):
+        pb = W.random_small_batch(rng, 300, alphabet=256, max_len=3, now=now, staleness=10)
+        parts = sh.route(pb)
+        ve = [engines[g].detect(parts[g].batch, now, now - 5)[0] for g in range(2)]
+        vo = [oracles[g].detect(parts[g].batch, now, now - 5)[0] for g in range(2)]
+        for g in range(2):
+            assert (ve[g] == vo[g]).all()
+        assert (KeyRangeSharding.combine(pb.n_txn, parts, ve) == KeyRangeSharding.combine(pb.n_txn, parts, vo)).all()
+        now += 3
