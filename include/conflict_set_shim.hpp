@@ -15,6 +15,7 @@
 
 #include <stdint.h>
 
+#include <functional>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -53,8 +54,9 @@ inline void destroyConflictSet(ConflictSet* cs) {  // SkipList.cpp:745-747
     delete cs;
 }
 
-// ConflictingKeyRangeMap: std::map<int, VectorRef<int>> in FDB (with an Arena); any map whose
-// mapped type supports push_back(int) works here.
+// ConflictingKeyRangeMap: std::map<int, VectorRef<int>> in FDB, filled with push_back(arena, i)
+// (SkipList.cpp:782-784, 822-825) when the three-argument constructor receives the Arena; with
+// the two-argument constructor any map whose mapped type supports push_back(int) works.
 template <class ConflictingKeyRangeMap = std::map<int, std::vector<int>>>
 struct ConflictBatchT {
     enum TransactionCommitResult {  // ConflictSet.h:40-44
@@ -66,6 +68,14 @@ struct ConflictBatchT {
     explicit ConflictBatchT(ConflictSet* cs, ConflictingKeyRangeMap* conflictingKeyRangeMap = nullptr)
       : cs(cs), map(conflictingKeyRangeMap) {
         fdbcs_shim::check(fdbcs_batch_new(cs->h, map != nullptr, &b), "ConflictBatch");
+        append = [](typename ConflictingKeyRangeMap::mapped_type& e, int i) { e.push_back(i); };
+    }
+    // ConflictBatch(cs, conflictingKeyRangeMap, resolveBatchReplyArena) — SkipList.cpp:749-752.
+    template <class Arena>
+    ConflictBatchT(ConflictSet* cs, ConflictingKeyRangeMap* conflictingKeyRangeMap, Arena* arena)
+      : cs(cs), map(conflictingKeyRangeMap) {
+        fdbcs_shim::check(fdbcs_batch_new(cs->h, map != nullptr, &b), "ConflictBatch");
+        append = [arena](typename ConflictingKeyRangeMap::mapped_type& e, int i) { e.push_back(*arena, i); };
     }
     ~ConflictBatchT() { fdbcs_batch_destroy(b); }
     ConflictBatchT(const ConflictBatchT&) = delete;
@@ -115,7 +125,7 @@ struct ConflictBatchT {
                 fdbcs_shim::check(fdbcs_batch_conflicting_reads(b, t, nullptr, 0, &n), "conflictingReads");
                 idx.resize(n > 0 ? n : 1);
                 fdbcs_shim::check(fdbcs_batch_conflicting_reads(b, t, idx.data(), n, &n), "conflictingReads");
-                for (int32_t i = 0; i < n; i++) entry.push_back(idx[i]);
+                for (int32_t i = 0; i < n; i++) append(entry, idx[i]);
             }
         }
     }
@@ -129,6 +139,7 @@ private:
     ConflictSet* cs;
     ConflictingKeyRangeMap* map;
     fdbcs_batch* b = nullptr;
+    std::function<void(typename ConflictingKeyRangeMap::mapped_type&, int)> append;
     std::vector<bool> report;
     std::vector<uint8_t> verdicts;
 };

@@ -17,6 +17,17 @@ struct Ref {  // StringRef-like
 struct Range {
     Ref begin, end;
 };
+struct Arena {  // flow Arena stand-in: counts allocations made through it
+    int pushes = 0;
+};
+struct IntVectorRef {  // VectorRef<int> stand-in: push_back(arena, v) like flow/Arena.h
+    std::vector<int> v;
+    void push_back(Arena& a, int x) {
+        a.pushes++;
+        v.push_back(x);
+    }
+    size_t size() const { return v.size(); }
+};
 struct Txn {
     std::vector<Range> read_conflict_ranges, write_conflict_ranges;
     int64_t read_snapshot = 0;
@@ -54,6 +65,22 @@ int main() {
         std::vector<int> ok;
         batch.detectConflicts(20, 0, ok);
         printf("b2 commit=%zu first=%d\n", ok.size(), ok.empty() ? -1 : ok[0]);
+    }
+    // batch 3: the Resolver's three-argument form with an Arena-backed map (Resolver.actor.cpp:179)
+    {
+        std::map<int, IntVectorRef> ckr;
+        Arena arena;
+        ConflictBatchT<std::map<int, IntVectorRef>> batch(cs, &ckr, &arena);
+        Txn a;
+        a.read_conflict_ranges.push_back({{"a"}, {"b"}});
+        a.read_conflict_ranges.push_back({{"k"}, {"l"}});
+        a.read_snapshot = 5;
+        a.report_conflicting_keys = true;
+        batch.addTransaction(a);
+        std::vector<int> ok;
+        batch.detectConflicts(30, 0, ok);
+        printf("b3 commit=%zu report0=%zu idx=%d arena=%d\n", ok.size(), ckr[0].size(),
+               ckr[0].size() ? ckr[0].v[0] : -1, arena.pushes);
     }
     destroyConflictSet(cs);
     return 0;
