@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--txns", type=int, default=5000)
     ap.add_argument("--history", type=int, default=5_000_000)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--gc-interval", type=int, default=8)
+    ap.add_argument("--gc-interval", type=int, default=0,
+                    help="force a compaction (+GC) at least every N batches; 0 = when the delta tier is full")
+    ap.add_argument("--delta-limit", type=int, default=0, help="delta-tier bound; 0 = automatic (~base/16)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
@@ -168,6 +170,7 @@ def main():
 
     cs = C.ConflictSet(device)
     cs.set_gc_interval(args.gc_interval)
+    cs.set_delta_limit(args.delta_limit)
     cs.load_history(kb, ko, vers, 0)
     mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
     maxT = max(b.n_txn for b in mine)
@@ -215,18 +218,30 @@ def main():
     granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(args.warmup, total))
     hist_end = cs.history_size()
 
-    launches = max(1, st["merge_launches"])
-    avg_ms = st["ms_merge_kernel"] / launches
-    bytes_per_launch = st["merge_bytes"] / launches
+    # Dominant kernel: of the two copy kernels (delta merge every batch, compaction of the base every
+    # ~16 batches) the one with the larger total device time; both are HBM-bound rewrites of a
+    # sorted boundary array reading 32 B per old boundary and writing 32 B per kept one.
+    kernels = {
+        "merge": ("k_merge_copy<BatchIns> (delta-tier merge)", st["ms_merge_kernel"], st["merge_launches"],
+                  st["merge_bytes"]),
+        "compact": ("k_merge_copy<CompactIns> (base-tier compaction)", st["ms_compact_kernel"], st["compactions"],
+                    st["compact_bytes"]),
+    }
+    dom = max(kernels, key=lambda k: kernels[k][1])
+    kname, kms, klaunch, kbytes = kernels[dom]
+    launches = max(1, klaunch)
+    avg_ms = kms / launches
+    bytes_per_launch = kbytes / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
-                traffic = json.load(f).get("k_merge_copy_bytes_per_launch")
+                traffic = json.load(f).get(f"{dom}_bytes_per_launch")
         except Exception:
             traffic = None
+    other = kernels["compact" if dom == "merge" else "merge"]
 
     out = {
         "metric": "resolved txns/sec (conflict ranges checked/sec) per batch; HBM GB/s vs peak",
@@ -247,15 +262,25 @@ def main():
             "global_batch_txns": args.txns * world,
             "parallelism": f"key-range shards x{world}" if world > 1 else "single resolver",
             "gc_interval": args.gc_interval,
+            "delta_limit": args.delta_limit or "auto",
         },
         "conflict_ranges_per_s": granges / elapsed,
         "history_boundaries_end": hist_end,
         "phase_ms_per_batch": {
             k: st[k] / max(1, st["batches"])
-            for k in ("ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_gc", "ms_total")
+            for k in ("ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_compact", "ms_gc",
+                      "ms_epilogue", "ms_total")
+        },
+        "compactions": st["compactions"],
+        "other_copy_kernel": {
+            "kernel": other[0],
+            "launches": other[2],
+            "avg_launch_ms": other[1] / max(1, other[2]),
+            "achieved_GBps": (other[3] / max(1, other[2])) / (other[1] / max(1, other[2]) * 1e-3) / 1e9
+            if other[1] > 0 else None,
         },
         "roofline": {
-            "kernel": "k_merge_copy (history rewrite)",
+            "kernel": kname,
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,

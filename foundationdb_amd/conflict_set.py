@@ -63,6 +63,11 @@ class Stats(ctypes.Structure):
         ("merge_bytes", ctypes.c_int64),
         ("merge_launches", ctypes.c_int64),
         ("ms_merge_kernel", ctypes.c_double),
+        ("compactions", ctypes.c_int64),
+        ("ms_compact", ctypes.c_double),
+        ("compact_bytes", ctypes.c_int64),
+        ("ms_compact_kernel", ctypes.c_double),
+        ("ms_epilogue", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -83,6 +88,7 @@ SIGNATURES = {
     "fdbcs_get_stats": (ctypes.c_int, [_VP, ctypes.POINTER(Stats)]),
     "fdbcs_reset_stats": (ctypes.c_int, [_VP]),
     "fdbcs_set_gc_interval": (ctypes.c_int, [_VP, _I32]),
+    "fdbcs_set_delta_limit": (ctypes.c_int, [_VP, _I64]),
     "fdbcs_reserve": (ctypes.c_int, [_VP, _I64, _I64, _I32, _I32, _I32]),
     "fdbcs_batch_new": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(_VP)]),
     "fdbcs_batch_destroy": (None, [_VP]),
@@ -177,7 +183,12 @@ class ConflictSet:
         _check(load_library().fdbcs_set_oldest_version(self._h, v), "setOldestVersion")
 
     def set_gc_interval(self, every: int) -> None:
+        """Compaction (with GC) at least every `every` batches; 0 = only when the delta is full."""
         _check(load_library().fdbcs_set_gc_interval(self._h, every), "setGcInterval")
+
+    def set_delta_limit(self, boundaries: int) -> None:
+        """Delta-tier bound that triggers a compaction; 0 = automatic (~1/16 of the base)."""
+        _check(load_library().fdbcs_set_delta_limit(self._h, boundaries), "setDeltaLimit")
 
     def reserve(self, boundaries: int, tail_bytes: int = 0, max_txns: int = 0, max_reads: int = 0,
                 max_writes: int = 0) -> None:

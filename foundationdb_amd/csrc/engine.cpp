@@ -78,8 +78,8 @@ struct HBuf {
 };
 
 enum Phase {
-    kPhStart, kPhUpload, kPhCheck, kPhSort, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge, kPhGc, kPhEnd,
-    kPhCount
+    kPhStart, kPhUpload, kPhCheck, kPhSort, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge,
+    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhCount
 };
 
 }  // namespace
@@ -92,17 +92,27 @@ struct fdbcs_conflict_set {
     int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
     int64_t header_version = 0;  // SkipList(Version) header (SkipList.cpp:398-404)
     int64_t max_written = 0;     // highest version present in the history
-    int gc_interval = 1;
-    int batches_since_gc = 0;
+    int gc_interval = 0;          // compaction (and GC) at least every this many batches; 0: by size only
+    int batches_since_compact = 0;
     int64_t gc_applied = 0;
+    int64_t delta_limit = 0;      // compaction once the delta may exceed this; 0: automatic
 
-    // history: two buffer sets (ping-pong) + range-max levels + tail arena
+    // base tier: two buffer sets (ping-pong) + range-max levels
     DBuf hkey[2], hlt[2], hver[2];
     DBuf lvl[kMaxLevels];  // lvl[0] unused (aliases hver[cur])
-    DBuf htail;  // tail arena shared by both buffer sets (append-only, offsets stable)
     int cur = 0;
     int64_t hist_cap = 0;  // elements per buffer set
-    int64_t n_ub = 0;      // upper bound of live boundaries (exact after a wait)
+    int64_t n_ub = 0;      // upper bound of live base boundaries (exact after a wait)
+    int64_t lvl3_n = 0;
+    // delta tier: the same layout, small
+    DBuf dkey[2], dlt[2], dver[2];
+    DBuf dlvl[kMaxLevels];
+    int dcur = 0;
+    int64_t delta_cap = 0;
+    int64_t nd_ub = 0;
+    int64_t dlvl3_n = 0;
+    DBuf cws[6];  // compaction arrays (per delta boundary)
+    DBuf htail;   // tail arena shared by every buffer set (append-only, offsets stable)
     int64_t tail_ub = 0;
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
@@ -144,6 +154,7 @@ struct fdbcs_batch {
     hipEvent_t ev[kPhCount] = {};
     bool events_made = false;
     bool gc_ran = false;
+    bool compacted = false;
     bool any_report = false;
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
@@ -176,13 +187,14 @@ int cmp_bytes(const uint8_t* a, int32_t al, const uint8_t* b, int32_t bl) {
 // Scan arena for the current workspace shape and history capacity (zeroed per batch by k_prepare).
 int ensure_scan_arena(fdbcs_conflict_set* cs) {
     if (cs->ws_T < 0 || cs->hist_cap <= 0) return FDBCS_OK;
-    const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap);
+    if (cs->delta_cap <= 0) return FDBCS_OK;
+    const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
     int rc = cs->ws[39].ensure(8 * words + 64);
     if (rc) return rc;
     cs->work.scan_arena = (uint64_t*)cs->ws[39].p;
-    if ((rc = cs->ws[38].ensure(4 * (cs->hist_cap / kGcTile + 4)))) return rc;
+    if ((rc = cs->ws[38].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / kGcTile + 4)))) return rc;
     cs->work.tile_first = (int32_t*)cs->ws[38].p;
-    carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap);
+    carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
     HIPOK(hipMemsetAsync(cs->work.scan_arena, 0, 8 * cs->work.scan_words, cs->stream));
     for (int k = 0; k < kNumScans; k++) cs->work.scan[k].error = &((Scalars*)cs->scal.p)->debug_error;
     return FDBCS_OK;
@@ -262,6 +274,13 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     return ensure_scan_arena(cs);
 }
 
+// Automatic delta bound: about 1/16 of the base, so a batch's merge touches a small tier and a
+// compaction (a full rewrite of the base) is amortised over many batches.
+int64_t delta_limit_for(const fdbcs_conflict_set* cs, int64_t n_base) {
+    if (cs->delta_limit > 0) return cs->delta_limit;
+    return std::max<int64_t>(1 << 16, n_base / 16);
+}
+
 
 Hist hist_of(fdbcs_conflict_set* cs, int k) {
     Hist h;
@@ -278,67 +297,120 @@ MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     return m;
 }
 
+Hist delta_of(fdbcs_conflict_set* cs, int k) {
+    Hist h;
+    h.key = (ulonglong2*)cs->dkey[k].p;
+    h.lt = (uint2*)cs->dlt[k].p;
+    h.ver = (int64_t*)cs->dver[k].p;
+    return h;
+}
+
+MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
+    MaxLevels m;
+    m.lvl[0] = (int64_t*)cs->dver[k].p;
+    for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->dlvl[L].p;
+    return m;
+}
+
 // Read the exact history size/tail usage back (synchronizes the stream).
 int sync_sizes(fdbcs_conflict_set* cs) {
     Scalars s;
     HIPOK(hipMemcpyAsync(&s, cs->scal.p, sizeof(s), hipMemcpyDeviceToHost, cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->n_ub = s.n;
+    cs->nd_ub = s.nd;
     cs->tail_ub = s.tail_used;
     return FDBCS_OK;
 }
 
-// History capacity for `need` boundaries (copies the live history when growing).
+// Range-max hierarchy buffers for `cap` elements; returns the top level's length.
+int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n) {
+    int64_t m = cap;
+    for (int L = 1; L < kMaxLevels; L++) {
+        m = (m + kFan - 1) / kFan + 1;
+        lv[L].release();
+        if (int rc = lv[L].ensure(8 * m)) return rc;
+    }
+    *top_n = m;
+    return FDBCS_OK;
+}
+
+// Grow one ping-pong buffer set pair to `cap` elements, keeping the live `n` of set `live`.
+int grow_sets(fdbcs_conflict_set* cs, DBuf* key, DBuf* lt, DBuf* ver, int live, int64_t n, int64_t cap) {
+    int rc;
+    for (int k = 0; k < 2; k++) {
+        DBuf nk, nl, nv;
+        if ((rc = nk.ensure(16 * cap)) || (rc = nl.ensure(8 * cap)) || (rc = nv.ensure(8 * cap))) return rc;
+        if (k == live && n) {
+            HIPOK(hipMemcpyAsync(nk.p, key[k].p, 16 * n, hipMemcpyDeviceToDevice, cs->stream));
+            HIPOK(hipMemcpyAsync(nl.p, lt[k].p, 8 * n, hipMemcpyDeviceToDevice, cs->stream));
+            HIPOK(hipMemcpyAsync(nv.p, ver[k].p, 8 * n, hipMemcpyDeviceToDevice, cs->stream));
+        }
+        HIPOK(hipStreamSynchronize(cs->stream));
+        key[k].release();
+        lt[k].release();
+        ver[k].release();
+        key[k] = nk;
+        lt[k] = nl;
+        ver[k] = nv;
+    }
+    return FDBCS_OK;
+}
+
+// Delta-tier capacity for `need` boundaries (plus the compaction arrays sized to match).
+int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
+    if (need <= cs->delta_cap) return FDBCS_OK;
+    int rc = sync_sizes(cs);
+    if (rc) return rc;
+    int64_t cap = std::max<int64_t>(need, cs->delta_cap);
+    cap = std::max<int64_t>(cap + cap / 2, 1 << 14);
+    if ((rc = grow_sets(cs, cs->dkey, cs->dlt, cs->dver, cs->dcur, cs->nd_ub, cap))) return rc;
+    Work& w = cs->work;
+    int64_t** c64[5] = {&w.c_lo, &w.c_hi, &w.c_rem, &w.c_ins, &w.c_val};
+    for (int k = 0; k < 5; k++) {
+        cs->cws[k].release();
+        if ((rc = cs->cws[k].ensure(8 * (cap + 2)))) return rc;
+        *c64[k] = (int64_t*)cs->cws[k].p;
+    }
+    cs->cws[5].release();
+    if ((rc = cs->cws[5].ensure(cap + 2))) return rc;
+    w.c_exact = (uint8_t*)cs->cws[5].p;
+    if ((rc = alloc_levels(cs->dlvl, cap, &cs->dlvl3_n))) return rc;
+    cs->delta_cap = cap;
+    launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->nd,
+                    cs->dlvl3_n, std::max<int64_t>(cs->nd_ub, 1));
+    HIPOK(hipGetLastError());
+    HIPOK(hipStreamSynchronize(cs->stream));
+    return ensure_scan_arena(cs);
+}
+
+// Base-tier capacity for `need` boundaries (copies the live history when growing).
 int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
     if (need <= cs->hist_cap && tail_need <= cs->tail_cap) return FDBCS_OK;
     int rc = sync_sizes(cs);
     if (rc) return rc;
-    const int64_t n = cs->n_ub;
     const int64_t tail_used = cs->tail_ub;
-    int64_t cap = std::max<int64_t>(need, cs->hist_cap);
-    cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
-    int64_t tcap = std::max<int64_t>(tail_need, cs->tail_cap);
-    tcap = std::max<int64_t>(tcap + tcap / 2, 1 << 16);
-    for (int k = 0; k < 2; k++) {
-        DBuf nk, nl, nv;
-        if ((rc = nk.ensure(16 * cap)) || (rc = nl.ensure(8 * cap)) || (rc = nv.ensure(8 * cap))) return rc;
-        if (k == cs->cur) {
-            if (n) {
-                HIPOK(hipMemcpyAsync(nk.p, cs->hkey[k].p, 16 * n, hipMemcpyDeviceToDevice, cs->stream));
-                HIPOK(hipMemcpyAsync(nl.p, cs->hlt[k].p, 8 * n, hipMemcpyDeviceToDevice, cs->stream));
-                HIPOK(hipMemcpyAsync(nv.p, cs->hver[k].p, 8 * n, hipMemcpyDeviceToDevice, cs->stream));
-            }
-        }
-        HIPOK(hipStreamSynchronize(cs->stream));
-        cs->hkey[k].release();
-        cs->hlt[k].release();
-        cs->hver[k].release();
-        cs->hkey[k] = nk;
-        cs->hlt[k] = nl;
-        cs->hver[k] = nv;
+    if (need > cs->hist_cap) {
+        int64_t cap = std::max<int64_t>(need, cs->hist_cap);
+        cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
+        if ((rc = grow_sets(cs, cs->hkey, cs->hlt, cs->hver, cs->cur, cs->n_ub, cap))) return rc;
+        if ((rc = alloc_levels(cs->lvl, cap, &cs->lvl3_n))) return rc;
+        cs->hist_cap = cap;
+        launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n,
+                        cs->lvl3_n, std::max<int64_t>(cs->n_ub, 1));
+        HIPOK(hipGetLastError());
     }
-    if (tcap > cs->tail_cap) {
+    if (tail_need > cs->tail_cap) {
+        int64_t tcap = std::max<int64_t>(tail_need, cs->tail_cap);
+        tcap = std::max<int64_t>(tcap + tcap / 2, 1 << 16);
         DBuf nt;
         if ((rc = nt.ensure(tcap))) return rc;
         if (tail_used) HIPOK(hipMemcpyAsync(nt.p, cs->htail.p, tail_used, hipMemcpyDeviceToDevice, cs->stream));
         HIPOK(hipStreamSynchronize(cs->stream));
         cs->htail.release();
         cs->htail = nt;
+        cs->tail_cap = tcap;
     }
-    int64_t m = cap;
-    for (int L = 1; L < kMaxLevels; L++) {
-        m = (m + kFan - 1) / kFan + 1;
-        cs->lvl[L].release();
-        if ((rc = cs->lvl[L].ensure(8 * m))) return rc;
-    }
-    cs->hist_cap = cap;
-    cs->tail_cap = tcap;
-    // rebuild the range-max levels for the live history
-    MaxLevels lv = levels_of(cs, cs->cur);
-    cs->work.lvl3 = (int64_t*)cs->lvl[3].p;
-    cs->work.lvl3_n = m;
-    launch_rangemax(cs->stream, lv, (Scalars*)cs->scal.p, m, std::max<int64_t>(n, 1));
-    HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(cs->stream));
     return ensure_scan_arena(cs);
 }
@@ -442,6 +514,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
+    if (!rc) rc = ensure_delta(cs, 1 << 14);
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
     if (rc) {
         fdbcs_destroy_conflict_set(cs);
@@ -459,9 +532,14 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         cs->hkey[k].release();
         cs->hlt[k].release();
         cs->hver[k].release();
+        cs->dkey[k].release();
+        cs->dlt[k].release();
+        cs->dver[k].release();
     }
     cs->htail.release();
     for (auto& l : cs->lvl) l.release();
+    for (auto& l : cs->dlvl) l.release();
+    for (auto& x : cs->cws) x.release();
     for (auto& x : cs->ws) x.release();
     cs->scal.release();
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
@@ -477,6 +555,7 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     cs->header_version = version;
     cs->max_written = version;
     cs->n_ub = 0;
+    cs->nd_ub = 0;
     cs->tail_ub = 0;
     return FDBCS_OK;
 }
@@ -500,12 +579,21 @@ int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes
     HIPOK(hipSetDevice(cs->device));
     int rc = ensure_workspace(cs, max_txns, max_reads, max_writes);
     if (rc) return rc;
-    return ensure_history(cs, std::max<int64_t>(boundaries, cs->hist_cap), std::max<int64_t>(tail_bytes, cs->tail_cap));
+    const int64_t dneed = delta_limit_for(cs, boundaries) + 2 * (int64_t)max_writes + 2;
+    if ((rc = ensure_delta(cs, dneed))) return rc;
+    return ensure_history(cs, std::max<int64_t>(boundaries + dneed, cs->hist_cap),
+                          std::max<int64_t>(tail_bytes, cs->tail_cap));
 }
 
 int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every) {
-    if (!cs || every < 1) return FDBCS_E_INVALID;
+    if (!cs || every < 0) return FDBCS_E_INVALID;
     cs->gc_interval = every;
+    return FDBCS_OK;
+}
+
+int fdbcs_set_delta_limit(fdbcs_conflict_set* cs, int64_t boundaries) {
+    if (!cs || boundaries < 0) return FDBCS_E_INVALID;
+    cs->delta_limit = boundaries;
     return FDBCS_OK;
 }
 
@@ -514,7 +602,7 @@ int fdbcs_history_size(fdbcs_conflict_set* cs, int64_t* out) {
     HIPOK(hipSetDevice(cs->device));
     int rc = sync_sizes(cs);
     if (rc) return rc;
-    *out = cs->n_ub;
+    *out = cs->n_ub + cs->nd_ub;
     return FDBCS_OK;
 }
 
@@ -559,13 +647,14 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     s.n = n;
     s.tail_used = (int64_t)tail.size();
     HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
-    MaxLevels lv = levels_of(cs, cs->cur);
-    launch_rangemax(cs->stream, lv, (Scalars*)cs->scal.p, cs->work.lvl3_n, std::max<int64_t>(n, 1));
+    launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n, cs->lvl3_n,
+                    std::max<int64_t>(n, 1));
     HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
     cs->max_written = maxv;
     cs->n_ub = n;
+    cs->nd_ub = 0;
     cs->tail_ub = (int64_t)tail.size();
     return FDBCS_OK;
 }
@@ -723,7 +812,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const int64_t T = b->T(), R = b->R(), W = b->W();
     int rc;
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
-    if ((rc = ensure_history(cs, cs->n_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail.size() + 1))) return rc;
+    if ((rc = ensure_delta(cs, cs->nd_ub + 2 * W + 1))) return rc;
+    if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail.size() + 1)))
+        return rc;
     if ((rc = ensure_events(b))) return rc;
     // results staging: verdicts + scalars (one D2H) | rconf | hist | first_conf
     const size_t o_sc = (size_t)verdict_scalars_offset(T);
@@ -749,11 +840,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const BatchDev& bd = b->bd;
     Work& w = cs->work;
     Scalars* sc = (Scalars*)cs->scal.p;
-    const int src = cs->cur;
-    Hist hs = hist_of(cs, src), hd = hist_of(cs, src ^ 1);
-    MaxLevels lv = levels_of(cs, src);
+    const int bsrc = cs->cur, dsrc = cs->dcur;
+    const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
+    const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->nd, kHole};
+    uint8_t* htail = (uint8_t*)cs->htail.p;
 
-    launch_check_reads(s, bd, hs, lv, (const uint8_t*)cs->htail.p, sc, cs->header_version, w);
+    launch_check_reads(s, bd, base, delta, htail, w);
     HIPOK(hipEventRecord(b->ev[kPhCheck], s));
     int sorted = 0;
     launch_sort_points(s, bd, w, &sorted);
@@ -770,32 +862,57 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     HIPOK(hipEventRecord(b->ev[kPhIntra], s));
     launch_combine(s, bd, w, sc);
     HIPOK(hipEventRecord(b->ev[kPhCombine], s));
-    launch_merge(s, bd, w, hs, hd, (uint8_t*)cs->htail.p, sc, now, cs->header_version, cs->n_ub + 1,
-                 b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
+    // D.MergeWrite into the delta tier
+    launch_merge(s, bd, w, delta.h, delta_of(cs, dsrc ^ 1), htail, sc, now, (int64_t*)cs->dlvl[3].p,
+                 cs->dlvl3_n, cs->nd_ub + 1, b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
     HIPOK(hipEventRecord(b->ev[kPhMerge], s));
-    int final_buf = src ^ 1;
+    const int dnew = dsrc ^ 1;
+    const int64_t nd_after = cs->nd_ub + 2 * W;
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
-    // removeBefore (SkipList.cpp:880-889) on every gc_interval-th batch whose oldest version moved
+    // Compaction when the delta may outgrow its bound (or on the forced cadence); removeBefore
+    // (SkipList.cpp:880-889) runs with it whenever the oldest version moved.
+    bool compact = nd_after > delta_limit_for(cs, cs->n_ub);
+    if (cs->gc_interval > 0 && ++cs->batches_since_compact >= cs->gc_interval) compact = true;
     bool gc = false;
-    if (new_oldest > cs->gc_applied && ++cs->batches_since_gc >= cs->gc_interval) gc = true;
+    int final_base = bsrc;
+    const int64_t base_hint = cs->n_ub + nd_after + 1;
+    if (compact) {
+        launch_compact(s, w, base.h, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc, cs->header_version,
+                       (int64_t*)cs->lvl[3].p, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, b->ev[kPhCompBegin],
+                       b->ev[kPhCompEnd]);
+        final_base = bsrc ^ 1;
+        cs->batches_since_compact = 0;
+        gc = new_oldest > cs->gc_applied;
+    } else {
+        HIPOK(hipEventRecord(b->ev[kPhCompEnd], s));
+    }
+    HIPOK(hipEventRecord(b->ev[kPhCompact], s));
     if (gc) {
-        launch_gc(s, w, hd, hs, sc, new_oldest, cs->header_version, cs->n_ub + 2 * W + 1);
-        final_buf = src;
-        cs->batches_since_gc = 0;
+        launch_gc(s, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), sc, new_oldest, cs->header_version,
+                  base_hint);
+        final_base ^= 1;
         cs->gc_applied = new_oldest;
     }
-    b->gc_ran = gc;
-    MaxLevels lf = levels_of(cs, final_buf);
-    launch_epilogue(s, bd, w, lf, sc, gc ? 1 : 0, (uint8_t*)b->dverdict.p, cs->n_ub + 2 * W + 1);
     HIPOK(hipEventRecord(b->ev[kPhGc], s));
+    b->gc_ran = gc;
+    b->compacted = compact;
+    launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
+                    gc ? 1 : 0, (uint8_t*)b->dverdict.p, compact ? base_hint : nd_after + 1);
+    HIPOK(hipEventRecord(b->ev[kPhEpilogue], s));
     HIPOK(hipGetLastError());
     // results back: verdicts and the scalars right behind them, one copy
     HIPOK(hipMemcpyAsync(b->pin_out.p, b->dverdict.p, o_sc + sizeof(Scalars), hipMemcpyDeviceToHost, s));
     HIPOK(hipEventRecord(b->ev[kPhEnd], s));
-    cs->cur = final_buf;
+    cs->cur = final_base;
+    cs->dcur = dnew;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
     if (W) cs->max_written = std::max(cs->max_written, now);
-    cs->n_ub += 2 * W;
+    if (compact) {
+        cs->n_ub += nd_after;
+        cs->nd_ub = 0;
+    } else {
+        cs->nd_ub = nd_after;
+    }
     cs->tail_ub += (int64_t)b->tail.size();
     cs->inflight++;
     b->state = 2;
@@ -851,15 +968,23 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         st.ms_intra += ev_ms(b->ev[kPhSort], b->ev[kPhIntra]);
         st.ms_combine += ev_ms(b->ev[kPhIntra], b->ev[kPhCombine]);
         st.ms_merge += ev_ms(b->ev[kPhCombine], b->ev[kPhMerge]);
-        st.ms_gc += ev_ms(b->ev[kPhMerge], b->ev[kPhGc]);
+        st.ms_compact += ev_ms(b->ev[kPhMerge], b->ev[kPhCompact]);
+        st.ms_gc += ev_ms(b->ev[kPhCompact], b->ev[kPhGc]);
+        st.ms_epilogue += ev_ms(b->ev[kPhGc], b->ev[kPhEpilogue]);
         st.ms_total += ev_ms(b->ev[kPhUpload], b->ev[kPhEnd]);
-        // dominant kernel: history rewrite reads every old boundary (32 B) and writes the kept ones
+        // copy kernels: each reads every old boundary of its tier (32 B) and writes the kept ones
         st.ms_merge_kernel += ev_ms(b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
         st.merge_launches += 1;
-        st.merge_bytes += 32 * (2 * b->h_scal->n_before - b->h_scal->rem_total);
+        st.merge_bytes += 32 * (2 * b->h_scal->d_before - b->h_scal->d_rem);
+        if (b->compacted) {
+            st.compactions += 1;
+            st.ms_compact_kernel += ev_ms(b->ev[kPhCompBegin], b->ev[kPhCompEnd]);
+            st.compact_bytes += 32 * (2 * b->h_scal->c_before - b->h_scal->c_rem);
+        }
         cs->inflight--;
         if (cs->inflight == 0) {
             cs->n_ub = b->h_scal->n;
+            cs->nd_ub = b->h_scal->nd;
             cs->tail_ub = b->h_scal->tail_used;
         }
         b->state = 3;

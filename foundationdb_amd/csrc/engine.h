@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <limits.h>
 
 #include "dkey.h"
 #include "scan.h"
@@ -36,25 +37,49 @@ struct MaxLevels {
     int64_t* lvl[kMaxLevels];  // lvl[0] == current Hist::ver
 };
 
-// Device-side scalars of a conflict set (one allocation).
+// Device-side scalars of a conflict set (one allocation).  The history has two tiers: the base
+// (sorted boundaries, rewritten only by compaction) and the delta (this window's merges, versions
+// or kHole where the base shows through).
 struct Scalars {
-    int64_t n;             // live boundaries in the current history
-    int64_t n_next;        // after this batch's merge
-    int64_t n_gc;          // after GC
+    int64_t n;             // base boundaries
+    int64_t nd;            // delta boundaries
+    int64_t n_next;        // base after this batch's compaction
+    int64_t nd_next;       // delta after this batch's merge
+    int64_t n_gc;          // base after GC
     int64_t tail_used;     // bytes used in the history tail arena
     int64_t tail_next;
     int64_t n_segments;    // union segments of committed writes
     int64_t n_edges;       // candidate edges
-    int64_t n_before;      // history size at the start of the merge
-    int64_t rem_total;     // boundaries removed by union segments
+    int64_t d_before;      // delta size at the start of the merge
+    int64_t d_rem;         // delta boundaries removed by union segments
+    int64_t c_before;      // base size at the start of a compaction
+    int64_t c_rem;         // base boundaries removed (overwritten) by the compaction
     int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
     int32_t pad;
 };
 
+// Delta-tier version meaning "not written in this window: the base tier's version applies".
+constexpr int64_t kHole = INT64_MIN;
+
+// Where a merge reads its source size and reports its result.
+struct TierIO {
+    const int64_t* n_in;   // source boundaries
+    int64_t* n_out;        // boundaries after the merge
+    int64_t* before;       // copy of *n_in (stats)
+    int64_t* removed;      // boundaries removed (stats)
+};
+
+// Segments applied to a sorted boundary array by k_merge_copy: segment s removes [lo_s, hi_s) and
+// inserts ins_s boundaries at lo_s.  rem/ins hold counts, then exclusive prefixes (sentinel at U).
+struct Segs {
+    int64_t *lo, *hi, *rem, *ins;
+    int32_t* tile_first;   // first segment whose lo lies in copy tile t or later
+};
+
 // Scans of one batch (each owns a slice of the per-batch zeroed scan arena).
-enum ScanKind { kScanPos, kScanEdges, kScanCov, kScanSeg, kScanSegSum, kScanGc, kNumScans };
+enum ScanKind { kScanPos, kScanEdges, kScanCov, kScanSeg, kScanSegSum, kScanCompact, kScanGc, kNumScans };
 
 // Device copy of one batch's packed input (tooOld transactions carry no ranges,
 // as in addTransaction, SkipList.cpp:770-790).
@@ -113,32 +138,49 @@ struct Work {
     uint64_t* scan_arena;  // zeroed by the previous batch's epilogue (and at allocation)
     int64_t scan_words;
     int64_t cap_T, cap_R;  // workspace capacity (what the epilogue zeroes)
-    int32_t* tile_first;   // [hist_cap / kGcTile + 3] first segment of each merge-copy tile
-    int64_t* lvl3;         // top range-max level, reset by k_seg_search for the epilogue
-    int64_t lvl3_n;
+    int32_t* tile_first;   // [max(hist_cap, delta_cap) / kGcTile + 4] first segment of each copy tile
+    // compaction: one entry per delta boundary (sized by the delta capacity)
+    int64_t *c_lo, *c_hi, *c_rem, *c_ins, *c_val;
+    uint8_t* c_exact;
 };
 
 // Byte offset of the Scalars copy that follows the verdicts in a batch's result buffer.
 __host__ __device__ inline int64_t verdict_scalars_offset(int64_t T) { return (T + 64) / 64 * 64; }
 
 // ---- launchers (kernels.hip); all enqueue on `s` and never synchronize.
-void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const MaxLevels& m, const uint8_t* htail,
-                        const Scalars* sc, int64_t header_version, const Work& w);
+// A history tier as the read check sees it.
+struct Tier {
+    Hist h;
+    MaxLevels m;
+    const int64_t* n;  // device size
+    int64_t hdr;       // version below the first boundary (kHole for the delta)
+};
+void launch_check_reads(hipStream_t s, const BatchDev& b, const Tier& base, const Tier& delta, const uint8_t* htail,
+                        const Work& w);
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, bool report);
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
+// Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
-                  Scalars* sc, int64_t now, int64_t header_version, int64_t grid_hint_n, hipEvent_t copy_begin,
+                  Scalars* sc, int64_t now, int64_t* lvl3, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin,
                   hipEvent_t copy_end);
+// Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
+void launch_compact(hipStream_t s, const Work& w, const Hist& base, const Hist& delta, const Hist& dst,
+                    const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t* lvl3, int64_t lvl3_n,
+                    int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end);
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
                int64_t header_version, int64_t grid_hint_n);
-int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap);
-void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap);
-void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, int64_t lvl3_n, int64_t grid_hint_n);
-void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc, int gc_ran,
-                     uint8_t* verdict_out, int64_t grid_hint_n);
+int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
+void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
+// Range-max levels of a tier whose size is *n (lvl[3] reset first).
+void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
+                     int64_t grid_hint_n);
+// Verdicts, scalar roll-over, scratch zeroing and the range-max levels of the tier that changed
+// (the base after a compaction, else the delta).
+void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
+                     int compacted, int gc_ran, uint8_t* verdict_out, int64_t grid_hint_n);
 
 }  // namespace fdbcs

@@ -131,42 +131,46 @@ __device__ T wg_scan(int64_t n, Load load, Store store, T* sh) {
 
 // ------------------------------------------------------------------ D.CheckRead
 
-// One thread per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the
-// step-function rule of SURVEY A.2).
-__global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Hist h, MaxLevels m, const uint8_t* htail,
-                                                        const Scalars* sc, int64_t hdr, uint8_t* hist_conf,
-                                                        uint8_t* rconf) {
+// Does some segment of one tier meeting the read [kb, ke) hold a version > snap?  Degenerate
+// [b, b) reads look at the greatest boundary < b (fingers never diverge, SkipList.cpp:650-666).
+__device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m, int64_t n, int64_t hdr,
+                                              const uint8_t* htail, const DKey& kb, const DKey& ke,
+                                              const uint8_t* qtail, bool degenerate, int64_t snap) {
+    const int64_t lb = hist_lower_bound(h, 0, n, htail, kb, qtail);
+    if (degenerate) return (lb > 0 ? h.ver[lb - 1] : hdr) > snap;
+    const int64_t ub = lb + ((lb < n && hist_cmp(h, lb, htail, kb, qtail) == 0) ? 1 : 0);
+    const int64_t j = hist_lower_bound(h, ub, n, htail, ke, qtail);
+    // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
+    if (ub == 0) return hdr > snap || range_max(m, 0, j, snap) > snap;
+    return range_max(m, ub - 1, j, snap) > snap;
+}
+
+// One thread per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
+// of SURVEY A.2).  The history is the base tier overlaid by the delta tier; every delta version is
+// >= the base versions it covers (versions only grow), so the max over the overlay equals the max
+// of the two tiers' maxima, and holes (kHole) never conflict.
+__global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Tier base, Tier delta, const uint8_t* htail,
+                                                        uint8_t* hist_conf, uint8_t* rconf) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= b.R) return;
-    const int64_t n = sc->n;
     const int t = b.rowner[r];
     const int64_t snap = b.snap[t];
     const DKey kb = b.keys[2 * r], ke = b.keys[2 * r + 1];
-    bool conf;
-    const int64_t lb = hist_lower_bound(h, 0, n, htail, kb, b.tail);
-    if (dkey_cmp(kb, b.tail, ke, b.tail) == 0) {
-        // degenerate [b, b): greatest boundary < b (fingers never diverge, SkipList.cpp:650-666)
-        const int64_t v = lb > 0 ? h.ver[lb - 1] : hdr;
-        conf = v > snap;
-    } else {
-        const int64_t ub = lb + ((lb < n && hist_cmp(h, lb, htail, kb, b.tail) == 0) ? 1 : 0);
-        const int64_t j = hist_lower_bound(h, ub, n, htail, ke, b.tail);
-        // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
-        if (ub == 0) {
-            conf = hdr > snap || range_max(m, 0, j, snap) > snap;
-        } else {
-            conf = range_max(m, ub - 1, j, snap) > snap;
-        }
+    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+    bool conf = tier_conflict(base.h, base.m, *base.n, base.hdr, htail, kb, ke, b.tail, degenerate, snap);
+    if (!conf) {
+        const int64_t nd = *delta.n;
+        if (nd > 0) conf = tier_conflict(delta.h, delta.m, nd, kHole, htail, kb, ke, b.tail, degenerate, snap);
     }
     rconf[r] = conf ? 1 : 0;
     if (conf) hist_conf[t] = 1;
 }
 
-void launch_check_reads(hipStream_t s, const BatchDev& b, const Hist& h, const MaxLevels& m, const uint8_t* htail,
-                        const Scalars* sc, int64_t header_version, const Work& w) {
+void launch_check_reads(hipStream_t s, const BatchDev& b, const Tier& base, const Tier& delta, const uint8_t* htail,
+                        const Work& w) {
     if (b.R == 0) return;
-    hipLaunchKernelGGL(k_check_reads, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, h, m, htail, sc,
-                       header_version, w.hist_conf, w.rconf);
+    hipLaunchKernelGGL(k_check_reads, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, base, delta, htail,
+                       w.hist_conf, w.rconf);
 }
 
 // ------------------------------------------------------------------ D.Sort
@@ -816,6 +820,8 @@ void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc
 // mergeWriteConflictRanges (SkipList.cpp:899-924, 414-424): for each union segment [B, E):
 // boundaries in [B, E) are removed, B is written at `now`, and E keeps the version it had
 // (SkipList.cpp:419) unless a boundary at E already exists or the next segment starts at E.
+// The batch merges into the delta tier, whose header is kHole: an E that inherits kHole lets the
+// base tier show through from E on, exactly as the reference's E keeps the old version.
 
 __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w, int pos, int end) {
     const int g = (int)item_range(w.pmeta[pos]);
@@ -823,14 +829,15 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
 }
 
 __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, const uint8_t* htail,
-                                                       const Scalars* sc, int64_t hdr, int64_t* lvl3, int64_t lvl3_n) {
+                                                       const Scalars* sc, const int64_t* n_in, int64_t* lvl3,
+                                                       int64_t lvl3_n) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     // the history check of this batch is done with the old hierarchy: reset its top level for the
     // epilogue's atomicMax build
     for (int64_t i = s; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
     const int U = sc->n_segments;
     if (s >= U) return;
-    const int64_t n = sc->n;
+    const int64_t n = *n_in;
     const DKey kb = seg_key(b, w, w.seg_b[s], 0);
     const DKey ke = seg_key(b, w, w.seg_e[s], 1);
     const int64_t lo = hist_lower_bound(h, 0, n, htail, kb, b.tail);
@@ -843,67 +850,73 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     w.seg_rem[s] = hi - lo;
     w.seg_ins[s] = endins ? 2 : 1;
     w.seg_endins[s] = endins ? 1 : 0;
-    w.seg_vend[s] = hi > 0 ? h.ver[hi - 1] : hdr;
+    w.seg_vend[s] = hi > 0 ? h.ver[hi - 1] : kHole;
     w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
 }
 
-// Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per segment; in the
-// same pass, tile_first[t] = first segment whose lo lies in copy tile t or later, so each copy tile
-// knows its segments without searching.
+// tile_first[t] = first segment whose lo lies in copy tile t or later (segment j's share).
+__device__ __forceinline__ void fill_tile_first(int32_t* tile_first, const int64_t* lo, int64_t j) {
+    const int64_t t0 = j > 0 ? lo[j - 1] / kGcTile + 1 : 0;
+    for (int64_t t = t0; t <= lo[j] / kGcTile; t++) tile_first[t] = (int32_t)j;
+}
+__device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const int64_t* lo, int64_t U, int64_t n) {
+    const int64_t t0 = U > 0 ? lo[U - 1] / kGcTile + 1 : 0;
+    for (int64_t t = t0; t <= n / kGcTile + 1; t++) tile_first[t] = (int32_t)U;
+}
+
+// Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per union segment,
+// plus tile_first for the copy.
 struct SegSumScan {
-    int64_t *rem, *ins, *tlen;
-    const int64_t* lo;
-    int32_t* tile_first;
+    Segs g;
+    int64_t* tlen;
+    TierIO io;
     Scalars* sc;
     __device__ void load(int64_t j, uint32_t (&v)[3]) const {
-        v[0] = (uint32_t)rem[j];
-        v[1] = (uint32_t)ins[j];
+        v[0] = (uint32_t)g.rem[j];
+        v[1] = (uint32_t)g.ins[j];
         v[2] = (uint32_t)tlen[j];
     }
     __device__ void store(int64_t j, const uint32_t (&ex)[3]) const {
-        rem[j] = ex[0];
-        ins[j] = ex[1];
+        g.rem[j] = ex[0];
+        g.ins[j] = ex[1];
         tlen[j] = ex[2];
-        const int64_t t0 = j > 0 ? lo[j - 1] / kGcTile + 1 : 0;
-        for (int64_t t = t0; t <= lo[j] / kGcTile; t++) tile_first[t] = (int32_t)j;
+        fill_tile_first(g.tile_first, g.lo, j);
     }
     __device__ void finish(const uint32_t (&tot)[3]) const {
-        const int64_t U = sc->n_segments;
+        const int64_t U = sc->n_segments, n = *io.n_in;
         // sentinel entries at U: totals, used by the copy kernel for elements after every segment
-        rem[U] = tot[0];
-        ins[U] = tot[1];
+        g.rem[U] = tot[0];
+        g.ins[U] = tot[1];
         tlen[U] = tot[2];
-        const int64_t t0 = U > 0 ? lo[U - 1] / kGcTile + 1 : 0;
-        for (int64_t t = t0; t <= sc->n / kGcTile + 1; t++) tile_first[t] = (int32_t)U;
-        sc->n_before = sc->n;
-        sc->rem_total = tot[0];
-        sc->n_next = sc->n - (int64_t)tot[0] + (int64_t)tot[1];
+        fill_tile_first_tail(g.tile_first, g.lo, U, n);
+        *io.before = n;
+        *io.removed = tot[0];
+        *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
         sc->tail_next = sc->tail_used + (int64_t)tot[2];
     }
 };
 
 constexpr int kSegLds = 1024;
 
-// Copy surviving old boundaries to their new positions.  Per tile, the segments that can affect
-// it are staged in LDS; element i is removed iff lo_j <= i < hi_j for the last segment j with
-// lo_j <= i, else it moves to i - rem_before + ins_before.
-__device__ __forceinline__ void write_insert(const BatchDev& b, const Work& w, Hist dst, uint8_t* htail,
-                                             const Scalars* sc, int64_t now, int s);
-
-__global__ __launch_bounds__(kBlock) void k_merge_copy(BatchDev b, Work w, Hist src, Hist dst, uint8_t* htail,
-                                                       const Scalars* sc, int64_t now) {
+// Copy surviving old boundaries to their new positions and write each segment's inserts.  Per
+// tile, the segments that can affect it are staged in LDS; element i is removed iff
+// lo_j <= i < hi_j for the last segment j with lo_j <= i, else it moves to i - rem_before +
+// ins_before.  `Ins` writes segment s's new boundaries starting at output position o.
+template <class Ins>
+__global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist dst, const int64_t* n_in,
+                                                       const int64_t* U_ptr, Ins ins) {
     __shared__ int64_t s_lo[kSegLds + 1], s_hi[kSegLds + 1], s_shift[kSegLds + 1];
     __shared__ int s_j0, s_cnt;
-    const int64_t n = sc->n;
-    const int U = sc->n_segments;
+    const int64_t n = *n_in;
+    const int64_t U = *U_ptr;
     __shared__ int s_ins0, s_ins1;
     // tiles cover positions [0, n]: position n only owns the inserts of segments past every boundary
     for (int64_t i0 = (int64_t)blockIdx.x * kGcTile; i0 <= n; i0 += (int64_t)gridDim.x * kGcTile) {
         const int64_t i1 = min(n, i0 + kGcTile);
         if (threadIdx.x == 0) {
             const int64_t t = i0 / kGcTile;
-            s_ins0 = w.tile_first[t];
-            s_ins1 = w.tile_first[t + 1];
+            s_ins0 = g.tile_first[t];
+            s_ins1 = g.tile_first[t + 1];
             s_j0 = s_ins0;  // slots: segment ja-1 (last with lo < i0), then the tile's own segments
             s_cnt = s_ins1 - s_ins0;
         }
@@ -914,9 +927,9 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(BatchDev b, Work w, Hist 
             // shift applying to elements after it (= shift of segment index ja+k as prefix)
             for (int k = threadIdx.x; k <= cnt; k += blockDim.x) {
                 const int j = ja - 1 + k;
-                s_lo[k] = j >= 0 ? w.seg_lo[j] : LLONG_MIN;
-                s_hi[k] = j >= 0 ? w.seg_hi[j] : LLONG_MIN;
-                s_shift[k] = w.seg_ins[j + 1] - w.seg_rem[j + 1];  // exclusive prefixes at j+1
+                s_lo[k] = j >= 0 ? g.lo[j] : LLONG_MIN;
+                s_hi[k] = j >= 0 ? g.hi[j] : LLONG_MIN;
+                s_shift[k] = g.ins[j + 1] - g.rem[j + 1];  // exclusive prefixes at j+1
             }
         }
         __syncthreads();
@@ -961,65 +974,177 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(BatchDev b, Work w, Hist 
             }
         } else {
             for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-                int lo = 0, hi = U;
+                int64_t lo = 0, hi = U;
                 while (lo < hi) {
-                    int mid = (lo + hi) >> 1;
-                    if (w.seg_lo[mid] <= i) lo = mid + 1; else hi = mid;
+                    int64_t mid = (lo + hi) >> 1;
+                    if (g.lo[mid] <= i) lo = mid + 1; else hi = mid;
                 }
-                const int j = lo - 1;
-                if (j >= 0 && i >= w.seg_lo[j] && i < w.seg_hi[j]) continue;
-                const int64_t o = i + w.seg_ins[j + 1] - w.seg_rem[j + 1];
+                const int64_t j = lo - 1;
+                if (j >= 0 && i >= g.lo[j] && i < g.hi[j]) continue;
+                const int64_t o = i + g.ins[j + 1] - g.rem[j + 1];
                 dst.key[o] = src.key[i];
                 dst.lt[o] = src.lt[i];
                 dst.ver[o] = src.ver[i];
             }
         }
-        for (int sg = s_ins0 + threadIdx.x; sg < s_ins1; sg += blockDim.x) write_insert(b, w, dst, htail, sc, now, sg);
+        for (int sg = s_ins0 + threadIdx.x; sg < s_ins1; sg += blockDim.x)
+            ins(sg, dst, g.lo[sg] - g.rem[sg] + g.ins[sg]);
         __syncthreads();
     }
 }
 
-// Write segment s's new boundaries: B at `now`, E (when needed) at its previous version.
-__device__ __forceinline__ void write_insert(const BatchDev& b, const Work& w, Hist dst, uint8_t* htail,
-                                             const Scalars* sc, int64_t now, int s) {
-    const int64_t o = w.seg_lo[s] - w.seg_rem[s] + w.seg_ins[s];
-    int64_t toff = sc->tail_used + w.seg_tlen[s];
-    const DKey kb = seg_key(b, w, w.seg_b[s], 0);
-    uint32_t tb = 0;
-    if (kb.len > 16) {
-        tb = (uint32_t)toff;
-        for (uint32_t k = 0; k < kb.len - 16; k++) htail[toff + k] = b.tail[kb.tail + k];
-        toff += kb.len - 16;
+// Inserts of a union segment: B at `now`, E (when needed) at the version it had.
+struct BatchIns {
+    BatchDev b;
+    const uint32_t* pmeta;
+    const int32_t *seg_b, *seg_e;
+    const int64_t *tlen, *vend;
+    const uint8_t* endins;
+    uint8_t* htail;
+    const Scalars* sc;
+    int64_t now;
+    __device__ const DKey& key(int pos, int end) const {
+        return b.keys[2 * (int)item_range(pmeta[pos]) + end];
     }
-    dst.key[o] = make_ulonglong2(kb.hi, kb.lo);
-    dst.lt[o] = make_uint2(kb.len, tb);
-    dst.ver[o] = now;
-    if (w.seg_endins[s]) {
-        const DKey ke = seg_key(b, w, w.seg_e[s], 1);
-        uint32_t te = 0;
-        if (ke.len > 16) {
-            te = (uint32_t)toff;
-            for (uint32_t k = 0; k < ke.len - 16; k++) htail[toff + k] = b.tail[ke.tail + k];
+    __device__ void operator()(int s, Hist dst, int64_t o) const {
+        int64_t toff = sc->tail_used + tlen[s];
+        const DKey kb = key(seg_b[s], 0);
+        uint32_t tb = 0;
+        if (kb.len > 16) {
+            tb = (uint32_t)toff;
+            for (uint32_t k = 0; k < kb.len - 16; k++) htail[toff + k] = b.tail[kb.tail + k];
+            toff += kb.len - 16;
         }
-        dst.key[o + 1] = make_ulonglong2(ke.hi, ke.lo);
-        dst.lt[o + 1] = make_uint2(ke.len, te);
-        dst.ver[o + 1] = w.seg_vend[s];
+        dst.key[o] = make_ulonglong2(kb.hi, kb.lo);
+        dst.lt[o] = make_uint2(kb.len, tb);
+        dst.ver[o] = now;
+        if (endins[s]) {
+            const DKey ke = key(seg_e[s], 1);
+            uint32_t te = 0;
+            if (ke.len > 16) {
+                te = (uint32_t)toff;
+                for (uint32_t k = 0; k < ke.len - 16; k++) htail[toff + k] = b.tail[ke.tail + k];
+            }
+            dst.key[o + 1] = make_ulonglong2(ke.hi, ke.lo);
+            dst.lt[o + 1] = make_uint2(ke.len, te);
+            dst.ver[o + 1] = vend[s];
+        }
     }
-}
+};
 
-void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
-                  Scalars* sc, int64_t now, int64_t header_version, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end) {
-    const int Wn = b.W > 0 ? b.W : 1;
-    hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
-                       header_version, w.lvl3, w.lvl3_n);
-    launch_scan<3>(s, SegSumScan{w.seg_rem, w.seg_ins, w.seg_tlen, w.seg_lo, w.tile_first, sc}, &sc->n_segments,
-                   (int64_t)b.W + 1, w.scan[kScanSegSum]);
-    if (copy_begin) (void)hipEventRecord(copy_begin, s);
+static Segs batch_segs(const Work& w) { return Segs{w.seg_lo, w.seg_hi, w.seg_rem, w.seg_ins, w.tile_first}; }
+
+static unsigned copy_tiles(int64_t grid_hint_n) {
     int64_t tiles = (grid_hint_n + 1 + kGcTile - 1) / kGcTile;
     if (tiles < 1) tiles = 1;
     if (tiles > 8192) tiles = 8192;
-    hipLaunchKernelGGL(k_merge_copy, dim3((unsigned)tiles), dim3(kBlock), 0, s, b, w, src, dst, htail, sc, now);
+    return (unsigned)tiles;
+}
+
+void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
+                  Scalars* sc, int64_t now, int64_t* lvl3, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin,
+                  hipEvent_t copy_end) {
+    const int Wn = b.W > 0 ? b.W : 1;
+    hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
+                       &sc->nd, lvl3, lvl3_n);
+    const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
+    launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
+                   w.scan[kScanSegSum]);
+    if (copy_begin) (void)hipEventRecord(copy_begin, s);
+    BatchIns ins{b, w.pmeta, w.seg_b, w.seg_e, w.seg_tlen, w.seg_vend, w.seg_endins, htail, sc, now};
+    hipLaunchKernelGGL(k_merge_copy<BatchIns>, dim3(copy_tiles(grid_hint_n)), dim3(kBlock), 0, s, batch_segs(w), src,
+                       dst, &sc->nd, &sc->n_segments, ins);
+    if (copy_end) (void)hipEventRecord(copy_end, s);
+}
+
+// ------------------------------------------------------------------ compaction
+//
+// Overlay the delta tier onto the base: delta boundary j with a version overwrites the base over
+// [d_j, d_{j+1}) (base boundaries there are removed, d_j is inserted); a kHole boundary j is the E
+// of an earlier merge and becomes a real boundary carrying the base version at d_j, unless the
+// base already has a boundary at d_j.  The result is the boundary set the reference would hold.
+
+__global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, Hist delta, const uint8_t* htail,
+                                                           const int64_t* nb_ptr, const int64_t* nd_ptr, int64_t hdr,
+                                                           Work w, int64_t* lvl3, int64_t lvl3_n) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = j; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    const int64_t nd = *nd_ptr;
+    if (j >= nd) return;
+    const int64_t nb = *nb_ptr;
+    const ulonglong2 k = delta.key[j];
+    const uint2 lt = delta.lt[j];
+    DKey q;
+    q.hi = k.x;
+    q.lo = k.y;
+    q.len = lt.x;
+    q.tail = lt.y;
+    const int64_t lo = hist_lower_bound(base, 0, nb, htail, q, htail);
+    const bool exact = lo < nb && hist_cmp(base, lo, htail, q, htail) == 0;
+    const int64_t dv = delta.ver[j];
+    w.c_lo[j] = lo;
+    w.c_exact[j] = exact ? 1 : 0;
+    w.c_val[j] = dv != kHole ? dv : (lo > 0 ? base.ver[lo - 1] : hdr);
+}
+
+// Per delta boundary: removed range [lo_j, hi_j) (hi_j = lo_{j+1} for a written segment, empty for
+// a hole) and 0/1 inserts, as exclusive prefixes.
+struct CompactSumScan {
+    Segs g;
+    const int64_t* dver;
+    const uint8_t* exact;
+    TierIO io;
+    const int64_t* nd_ptr;
+    __device__ int64_t hi_of(int64_t j) const {
+        if (dver[j] == kHole) return g.lo[j];
+        return j + 1 < *nd_ptr ? g.lo[j + 1] : *io.n_in;
+    }
+    __device__ void load(int64_t j, uint32_t (&v)[2]) const {
+        v[0] = (uint32_t)(hi_of(j) - g.lo[j]);
+        v[1] = (dver[j] != kHole || !exact[j]) ? 1u : 0u;
+    }
+    __device__ void store(int64_t j, const uint32_t (&ex)[2]) const {
+        g.hi[j] = hi_of(j);
+        g.rem[j] = ex[0];
+        g.ins[j] = ex[1];
+        fill_tile_first(g.tile_first, g.lo, j);
+    }
+    __device__ void finish(const uint32_t (&tot)[2]) const {
+        const int64_t U = *nd_ptr, n = *io.n_in;
+        g.rem[U] = tot[0];
+        g.ins[U] = tot[1];
+        fill_tile_first_tail(g.tile_first, g.lo, U, n);
+        *io.before = n;
+        *io.removed = tot[0];
+        *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
+    }
+};
+
+struct CompactIns {
+    Hist delta;
+    const int64_t *val, *ins;
+    __device__ void operator()(int s, Hist dst, int64_t o) const {
+        if (ins[s + 1] == ins[s]) return;  // hole over an existing base boundary
+        dst.key[o] = delta.key[s];
+        dst.lt[o] = delta.lt[s];
+        dst.ver[o] = val[s];
+    }
+};
+
+void launch_compact(hipStream_t s, const Work& w, const Hist& base, const Hist& delta, const Hist& dst,
+                    const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t* lvl3, int64_t lvl3_n,
+                    int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end) {
+    int64_t blocks = (delta_hint_n + kBlock - 1) / kBlock;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, delta, htail, &sc->n,
+                       &sc->nd_next, header_version, w, lvl3, lvl3_n);
+    const Segs g{w.c_lo, w.c_hi, w.c_rem, w.c_ins, w.tile_first};
+    const TierIO io{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem};
+    launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
+                   w.scan[kScanCompact]);
+    if (copy_begin) (void)hipEventRecord(copy_begin, s);
+    hipLaunchKernelGGL(k_merge_copy<CompactIns>, dim3(copy_tiles(grid_hint_n)), dim3(kBlock), 0, s, g, base, dst,
+                       &sc->n, &sc->nd_next, CompactIns{delta, w.c_val, w.c_ins});
     if (copy_end) (void)hipEventRecord(copy_end, s);
 }
 
@@ -1053,19 +1178,21 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, S
     launch_scan<1>(s, GcScan{src, dst, oldest, header_version, sc}, &sc->n_next, grid_hint_n, w.scan[kScanGc]);
 }
 
-int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap) {
+int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
     const int64_t E = 2 * (R + W);
     return kNumScans + scan_granules(E, 2) + scan_granules(R, 1) + 2 * scan_granules(E, 1) +
-           scan_granules(W + 1, 3) + scan_granules(hist_cap, 1);
+           scan_granules(W + 1, 3) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 1);
 }
 
-void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap) {
+void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
     const int64_t E = 2 * (R + W);
     uint64_t* a = w.scan_arena;
-    const int64_t gran[kNumScans] = {scan_granules(E, 2), scan_granules(R, 1), scan_granules(E, 1),
-                                     scan_granules(E, 1), scan_granules(W + 1, 3), scan_granules(hist_cap, 1)};
+    const int64_t gran[kNumScans] = {scan_granules(E, 2),     scan_granules(R, 1),
+                                     scan_granules(E, 1),     scan_granules(E, 1),
+                                     scan_granules(W + 1, 3), scan_granules(delta_cap + 1, 2),
+                                     scan_granules(hist_cap, 1)};
     uint64_t* g = a + kNumScans;
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);
@@ -1087,7 +1214,7 @@ struct Epilogue {
     const uint8_t* status;
     uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T)
     int32_t T;
-    int gc_ran;
+    int compacted, gc_ran;
     uint8_t* zero8;  // hist_conf
     int64_t zero8_n;
     int32_t* zero32a;  // ecnt_b
@@ -1099,9 +1226,18 @@ struct Epilogue {
     int32_t* zero_bk;
 };
 
-__global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, int use_gc_n, Epilogue ep) {
+// Range-max levels over lvl[0][0, n0) (lvl[3] reset beforehand); with a batch attached, also the
+// verdicts and the scalar roll-over.  n0 comes from `n_levels` or, for a batch, from the tier
+// that changed.
+__global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, const int64_t* n_levels, Epilogue ep) {
     __shared__ int64_t l1[kFan];
-    const int64_t n0 = use_gc_n == 2 ? sc->n : (use_gc_n ? sc->n_gc : sc->n_next);
+    int64_t n0;
+    if (n_levels)
+        n0 = *n_levels;
+    else if (ep.compacted)
+        n0 = ep.gc_ran ? sc->n_gc : sc->n_next;
+    else
+        n0 = sc->nd_next;
     const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int64_t b2 = blockIdx.x; b2 < n2; b2 += gridDim.x) {
@@ -1144,7 +1280,12 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, i
         ep.verdict_out[t] = v;
     }
     if (tid == 0) {
-        sc->n = use_gc_n ? sc->n_gc : sc->n_next;
+        if (ep.compacted) {
+            sc->n = ep.gc_ran ? sc->n_gc : sc->n_next;
+            sc->nd = 0;
+        } else {
+            sc->nd = sc->nd_next;
+        }
         sc->tail_used = sc->tail_next;
         *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = *sc;
         sc->debug_error = 0;
@@ -1173,19 +1314,21 @@ static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
     return g > 4096 ? 4096 : g;
 }
 
-void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, int64_t lvl3_n, int64_t grid_hint_n) {
+void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
+                     int64_t grid_hint_n) {
     hipLaunchKernelGGL(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
     Epilogue ep{};
-    hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, 2, ep);
+    hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, n, ep);
 }
 
-void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc, int gc_ran,
-                     uint8_t* verdict_out, int64_t grid_hint_n) {
+void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
+                     int compacted, int gc_ran, uint8_t* verdict_out, int64_t grid_hint_n) {
     Epilogue ep;
     ep.flags = b.flags;
     ep.status = w.status;
     ep.verdict_out = verdict_out;
     ep.T = b.T;
+    ep.compacted = compacted;
     ep.gc_ran = gc_ran;
     ep.zero8 = w.hist_conf;
     ep.zero8_n = w.cap_T;
@@ -1199,7 +1342,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
     hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
-                       gc_ran ? 1 : 0, ep);
+                       (const int64_t*)nullptr, ep);
 }
 
 }  // namespace fdbcs

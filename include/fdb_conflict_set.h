@@ -84,16 +84,21 @@ typedef struct fdbcs_stats {
     int64_t read_ranges;
     int64_t write_ranges;
     double ms_upload;       /* H2D of packed batches */
-    double ms_check_read;   /* history check (search + range max) */
+    double ms_check_read;   /* history check (search + range max over both tiers) */
     double ms_sort;         /* endpoint sort */
     double ms_intra;        /* intra-batch candidate edges + batch-order resolution */
     double ms_combine;      /* union of committed writes */
-    double ms_merge;        /* merge into history + range-max rebuild */
-    double ms_gc;           /* removeBefore equivalent */
+    double ms_merge;        /* merge into the delta tier */
+    double ms_gc;           /* removeBefore equivalent (runs with compactions) */
     double ms_total;        /* whole detect pipeline, device time */
-    int64_t merge_bytes;    /* algorithmic bytes moved by the merge kernels */
+    int64_t merge_bytes;    /* algorithmic bytes moved by the delta-merge copy kernel */
     int64_t merge_launches;
-    double ms_merge_kernel; /* device time of the dominant history-rewrite kernel alone */
+    double ms_merge_kernel; /* device time of the delta-merge copy kernel alone */
+    int64_t compactions;    /* delta tier folded into the base tier */
+    double ms_compact;      /* compaction phase (search + scan + copy) */
+    int64_t compact_bytes;  /* algorithmic bytes moved by the compaction copy kernel */
+    double ms_compact_kernel; /* device time of the compaction copy kernel alone */
+    double ms_epilogue;     /* range-max rebuild + verdicts */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
@@ -107,7 +112,8 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs);
  * affects the next batch's TooOld test (SkipList.cpp:770). */
 int fdbcs_set_oldest_version(fdbcs_conflict_set* cs, int64_t version);
 int fdbcs_get_oldest_version(const fdbcs_conflict_set* cs, int64_t* out);
-/* Live boundaries in the device history (SkipList::count, SkipList.cpp:386-394, up to GC laziness). */
+/* Boundaries held on the device, both tiers (SkipList::count, SkipList.cpp:386-394; equal to the
+ * reference's count right after a compaction with GC, an upper bound otherwise). */
 int fdbcs_history_size(fdbcs_conflict_set* cs, int64_t* out);
 /* Bulk-load a history: boundaries sorted strictly ascending, boundary i holds
  * version versions[i] for keys in [key_i, key_{i+1}); keys below the first
@@ -120,9 +126,14 @@ int fdbcs_reset_stats(fdbcs_conflict_set* cs);
  * shape) so later batches never reallocate; sizes are upper bounds, 0 keeps the current. */
 int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes, int32_t max_txns,
                   int32_t max_reads, int32_t max_writes);
-/* Garbage-collection cadence: GC runs on every `every`-th batch whose
- * newOldestVersion advanced (default 1).  GC is verdict-neutral. */
+/* The history is two-tiered: every batch merges into a small delta tier; a
+ * compaction folds the delta into the base tier, and removeBefore (GC) runs
+ * with it when the oldest version moved.  Compaction happens when the delta may
+ * exceed its limit (set_delta_limit; 0 = automatic, ~1/16 of the base) and, if
+ * `every` > 0, at least every `every` batches (default 0).  Both knobs are
+ * verdict-neutral: they only trade memory for speed. */
 int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every);
+int fdbcs_set_delta_limit(fdbcs_conflict_set* cs, int64_t boundaries);
 
 /* ConflictBatch(cs, conflictingKeyRangeMap, arena) — SkipList.cpp:749-752.
  * report_keys != 0 enables conflictingKeyRangeMap collection for transactions

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc/$c -o run -- \
-    python3 bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/pmc/$c.json 2> gpurun_out/pmc/$c.err
+    python3 bench.py --steps ${STEPS:-40} --warmup 2 --no-cpu-baseline > gpurun_out/pmc/$c.json 2> gpurun_out/pmc/$c.err
   rc=$?
   echo "pmc $c rc=$rc" >&2
   [ $rc -ne 0 ] && exit $rc

@@ -1,8 +1,10 @@
-"""Per-launch HBM bytes of the history-rewrite kernel from rocprofv3 --pmc CSVs.
+"""Per-launch HBM bytes of the two history copy kernels from rocprofv3 --pmc CSVs.
 
-FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half the bytes of a wide
-(16 B/lane) coalesced streaming read (MI355X_MICROARCH.md, HBM); k_merge_copy reads 16-B keys and
-8-B length/version words, so both the raw and the x2-corrected fetch figures are reported.
+k_merge_copy<BatchIns> merges a batch into the delta tier; k_merge_copy<CompactIns> folds the delta
+into the base tier.  FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
+the bytes of a wide (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md, HBM); the copy
+reads 16-B keys and 8-B length/version words, so both the raw and the x2-corrected fetch figures
+are reported.
 """
 import csv
 import glob
@@ -10,19 +12,25 @@ import json
 import os
 import sys
 
+KERNELS = {"merge": "BatchIns", "compact": "CompactIns"}
+
 root = sys.argv[1]
 out = {}
-for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    files = glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True)
-    vals = []
-    for f in files:
-        for r in csv.DictReader(open(f)):
-            if "k_merge_copy" in r.get("Kernel_Name", "") and r.get("Counter_Name") == c:
-                vals.append(float(r["Counter_Value"]))
-    out[c + "_kib_per_launch"] = sum(vals) / len(vals) if vals else None
-    out[c + "_launches"] = len(vals)
-f, w = out.get("FETCH_SIZE_kib_per_launch"), out.get("WRITE_SIZE_kib_per_launch")
-if f is not None and w is not None:
-    out["k_merge_copy_bytes_per_launch_raw"] = (f + w) * 1024
-    out["k_merge_copy_bytes_per_launch"] = (2 * f + w) * 1024  # gfx950 FETCH_SIZE half-count correction
+for key, tag in KERNELS.items():
+    per = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        files = glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True)
+        vals = []
+        for f in files:
+            for r in csv.DictReader(open(f)):
+                name = r.get("Kernel_Name", "")
+                if "k_merge_copy" in name and tag in name and r.get("Counter_Name") == c:
+                    vals.append(float(r["Counter_Value"]))
+        per[c] = sum(vals) / len(vals) if vals else None
+        out[f"{key}_{c}_kib_per_launch"] = per[c]
+        out[f"{key}_{c}_launches"] = len(vals)
+    f, w = per["FETCH_SIZE"], per["WRITE_SIZE"]
+    if f is not None and w is not None:
+        out[f"{key}_bytes_per_launch_raw"] = (f + w) * 1024
+        out[f"{key}_bytes_per_launch"] = (2 * f + w) * 1024  # gfx950 FETCH_SIZE half-count correction
 print(json.dumps(out, indent=1))

@@ -51,10 +51,11 @@ def random_fixture_sequences():
 class EngineDriver:
     """Runs packed batches through the HIP engine's Python mirror of ConflictBatch."""
 
-    def __init__(self, cs_module, device=0, gc_interval=1):
+    def __init__(self, cs_module, device=0, gc_interval=1, delta_limit=0):
         self.C = cs_module
         self.cs = cs_module.ConflictSet(device)
         self.cs.set_gc_interval(gc_interval)
+        self.cs.set_delta_limit(delta_limit)
 
     def clear(self, v):
         self.cs.clear(v)

@@ -22,8 +22,8 @@ def oracle_mod():
     return oracle
 
 
-def run_pair(engine, oracle_mod, seq, gc_interval=1, clear=None, check_conf=True, ref="oracle"):
-    e = EngineDriver(engine, gc_interval=gc_interval)
+def run_pair(engine, oracle_mod, seq, gc_interval=1, clear=None, check_conf=True, ref="oracle", delta_limit=0):
+    e = EngineDriver(engine, gc_interval=gc_interval, delta_limit=delta_limit)
     o = oracle_mod.OracleConflictSet() if ref == "oracle" else oracle_mod.SkipListBaseline()
     if clear is not None:
         e.clear(clear)
@@ -69,7 +69,41 @@ def test_random_vs_oracle(engine, oracle_mod, alphabet, max_len):
                                       staleness=15, max_reads=4, max_writes=3)
             seq.append((pb, now, now - int(rng.integers(0, 12))))
             now += int(rng.integers(1, 6))
-        run_pair(engine, oracle_mod, seq, gc_interval=1 + trial % 3, clear=(5 if trial % 5 == 0 else None))
+        # trials alternate: compaction every 1-3 batches, size-triggered compaction with a tiny delta
+        # bound, and a delta tier that is never compacted
+        gc, dl = [(1, 0), (2, 0), (3, 0), (0, 7), (0, 40), (0, 0)][trial % 6]
+        run_pair(engine, oracle_mod, seq, gc_interval=gc, delta_limit=dl, clear=(5 if trial % 5 == 0 else None))
+
+
+@pytest.mark.parametrize("gc_interval,delta_limit", [(1, 0), (0, 0), (0, 25), (4, 0)])
+def test_delta_tier_configurations(engine, oracle_mod, gc_interval, delta_limit):
+    """The two-tier history (delta merges, compaction, GC at compaction) is verdict- and
+    report-exact whatever the compaction cadence: long sequences over tiny alphabets make
+    delta boundaries overwrite, nest in and touch base boundaries."""
+    rng = np.random.default_rng(1000 + 10 * gc_interval + delta_limit)
+    seq = []
+    now = 10
+    for _ in range(30):
+        pb = W.random_small_batch(rng, int(rng.integers(1, 60)), alphabet=3, max_len=3, now=now, staleness=12,
+                                  max_reads=3, max_writes=3, report_frac=0.5)
+        seq.append((pb, now, now - int(rng.integers(0, 10))))
+        now += int(rng.integers(1, 4))
+    run_pair(engine, oracle_mod, seq, gc_interval=gc_interval, delta_limit=delta_limit)
+
+
+def test_delta_tier_history_size_after_compaction(engine, oracle_mod):
+    """After a compaction with GC the device holds exactly the reference's boundary count (skip-list
+    restatement running removeBefore on the same batches), although the batches in between lived
+    in the delta tier."""
+    seq = list(W.c1_batches(12, seed=11))
+    e = EngineDriver(engine, gc_interval=4)
+    o = oracle_mod.SkipListBaseline()
+    for i, (pb, now, no) in enumerate(seq):
+        ve, _ = e.detect(pb, now, no)
+        vo, _ = o.detect(pb, now, no, gc=(i + 1) % 4 == 0)
+        assert (ve == vo).all(), i
+        if (i + 1) % 4 == 0:
+            assert e.cs.history_size() == o.history_size(), i
 
 
 def test_shared_long_prefixes(engine, oracle_mod):
@@ -94,6 +128,7 @@ def test_shared_long_prefixes(engine, oracle_mod):
         seq.append((PackedBatch.from_transactions(txns), now, now - 8))
         now += 3
     run_pair(engine, oracle_mod, seq)
+    run_pair(engine, oracle_mod, seq, gc_interval=0, delta_limit=30)
 
 
 def test_c1_skiplisttest(engine, oracle_mod):
@@ -106,7 +141,7 @@ def test_c1_skiplisttest(engine, oracle_mod):
 def test_c2_reduced(engine, oracle_mod):
     p = W.C2Params(txns=2000, history=200_000)
     kb, ko, vers = W.c2_history(p, seed=1, start_version=10_000_000)
-    e = EngineDriver(engine, gc_interval=4)
+    e = EngineDriver(engine, gc_interval=0, delta_limit=30_000)
     o = oracle_mod.SkipListBaseline()
     e.load_history(kb, ko, vers)
     o.load_history(kb, ko, vers)
@@ -199,7 +234,7 @@ def test_full_size_c2_properties(engine, oracle_mod):
     batches, and history growth bounded by 2 boundaries per committed write."""
     p = W.C2Params()
     kb, ko, vers = W.c2_history(p, seed=1, start_version=10_000_000)
-    a, b = EngineDriver(engine, gc_interval=8), EngineDriver(engine, gc_interval=1)
+    a, b = EngineDriver(engine, gc_interval=0), EngineDriver(engine, gc_interval=1)
     a.load_history(kb, ko, vers)
     b.load_history(kb, ko, vers)
     o = oracle_mod.SkipListBaseline()
