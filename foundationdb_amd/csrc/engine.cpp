@@ -192,7 +192,7 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     int rc = cs->ws[39].ensure(8 * words + 64);
     if (rc) return rc;
     cs->work.scan_arena = (uint64_t*)cs->ws[39].p;
-    if ((rc = cs->ws[38].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / kGcTile + 4)))) return rc;
+    if ((rc = cs->ws[38].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 1024 + 8)))) return rc;  // per copy tile
     cs->work.tile_first = (int32_t*)cs->ws[38].p;
     carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
     HIPOK(hipMemsetAsync(cs->work.scan_arena, 0, 8 * cs->work.scan_words, cs->stream));
@@ -227,11 +227,12 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(first_conf, 4 * T);
     TAKE(items[0], sizeof(SortItem) * E);
     TAKE(items[1], sizeof(SortItem) * E);
-    TAKE(splitters, sizeof(SortItem) * 1024);
+    TAKE(splitters, sizeof(SortItem) * 2048);
     TAKE(bucket, 2 * E);
-    TAKE(bcount, 4 * 1024);
-    TAKE(bcursor, 4 * 1024);
-    TAKE(boff, 4 * 1028);
+    TAKE(bcount, 4 * 2048);
+    TAKE(bcursor, 4 * 2048);
+    TAKE(boff, 4 * 2052);
+    TAKE(srank, 4 * (8192 + 64));
     TAKE(pos, 4 * E);
     TAKE(pmeta, 4 * E);
     TAKE(cwb, 4 * (E + 1));
@@ -269,8 +270,9 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
     HIPOK(hipMemsetAsync(w.ecnt_b, 0, 4 * R, cs->stream));
     HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
-    HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 1024, cs->stream));
-    HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 1024, cs->stream));
+    HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 2048, cs->stream));
+    HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 2048, cs->stream));
+    HIPOK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), cs->stream));
     return ensure_scan_arena(cs);
 }
 

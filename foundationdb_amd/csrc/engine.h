@@ -102,11 +102,12 @@ struct Work {
     uint8_t* status;       // [T]
     int32_t* first_conf;   // [T]
     SortItem* items[2];    // [E] sorted endpoints / bucket-sort scratch
-    SortItem* splitters;   // [1023] sample-sort splitters
+    SortItem* splitters;   // [2047] sample-sort splitters
     uint16_t* bucket;      // [E] bucket of each endpoint
-    int32_t* bcount;       // [1024] endpoints per bucket (zeroed per batch)
-    int32_t* bcursor;      // [1024] scatter cursors (zeroed per batch)
-    int32_t* boff;         // [1025] bucket offsets
+    int32_t* bcount;       // [2048] endpoints per bucket (zeroed per batch)
+    int32_t* bcursor;      // [2048] scatter cursors (zeroed per batch)
+    int32_t* boff;         // [2049] bucket offsets
+    int32_t* srank;        // [8192 + 64] sample ranks, then the done counter (zeroed per batch)
     int32_t* pos;          // [2(R+W)] sorted position of each endpoint
     uint32_t* pmeta;       // [E] meta of the item at each position
     int32_t* cwb;          // [E+1] write-begins before each position

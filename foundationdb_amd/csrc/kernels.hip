@@ -311,22 +311,48 @@ __device__ void lds_merge_sort(SortItem* sh, int cnt, const uint8_t* arena) {
 
 // ---- sample sort of the batch endpoints (D.Sort, SkipList.cpp:161-208)
 //
-// 1. k_sample: one workgroup merge-sorts S evenly spaced endpoints and keeps nb-1 splitters.
+// 1. k_sample_rank: S evenly spaced endpoints are ranked against each other (each workgroup
+//    compares every sample with a 64-sample slice and adds partial ranks); the last workgroup to
+//    finish writes the nb-1 splitters (the samples of rank k*S/nb) straight from the ranks.
 // 2. k_bucket_count: each endpoint's bucket = number of splitters <= it; per-bucket counts.
 // 3. k_bucket_scatter: bucket offsets (prefix of the counts, recomputed per workgroup) and scatter.
-// 4. k_bucket_sort: one workgroup per bucket merge-sorts it in LDS (oversized buckets: LDS tiles
-//    then a workgroup-local merge over global memory).
-constexpr int kSample = 1024;
-constexpr int kMaxBuckets = 1024;
+// 4. k_bucket_sort: one workgroup per bucket (~256 endpoints) ranks its items in LDS and writes
+//    each to its final slot; oversized buckets rank 1024-item chunks, then merge through memory.
+constexpr int kMaxBuckets = 2048;
+constexpr int kMaxSample = 8192;
+constexpr int kSampleSlice = 64;
+constexpr int kRankTile = 1024;
+constexpr int kBucketTarget = 256;
 
-__global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SortItem* splitters, int nb, const uint8_t* arena) {
-    __shared__ SortItem sh[kSample];  // 32 KiB
+__device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((int64_t)i * E) / S); }
+
+__global__ __launch_bounds__(kBlock) void k_sample_rank(BatchDev b, int S, int nb, int32_t* srank, SortItem* splitters,
+                                                        const uint8_t* arena) {
+    __shared__ SortItem sl[kSampleSlice];
+    __shared__ int s_last;
     const int E = 2 * (b.R + b.W);
-    const int S = E < kSample ? E : kSample;
-    for (int i = threadIdx.x; i < S; i += blockDim.x) sh[i] = make_item(b, (int)(((int64_t)i * E) / S));
+    const int j0 = blockIdx.x * kSampleSlice;
+    const int cj = min(kSampleSlice, S - j0);
+    for (int t = threadIdx.x; t < cj; t += blockDim.x) sl[t] = make_item(b, sample_pos(j0 + t, E, S));
     __syncthreads();
-    lds_merge_sort(sh, S, arena);  // 8 items per thread: S <= 8 * kBlock
-    for (int k = threadIdx.x + 1; k < nb; k += blockDim.x) splitters[k - 1] = sh[(int)(((int64_t)k * S) / nb)];
+    for (int i = threadIdx.x; i < S; i += blockDim.x) {
+        const SortItem mine = make_item(b, sample_pos(i, E, S));
+        int c = 0;
+        for (int j = 0; j < cj; j++) c += item_less_total(sl[j], mine, arena) ? 1 : 0;
+        if (c) atomicAdd(&srank[i], c);
+    }
+    // the last workgroup to finish sees every partial rank and writes the splitters
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&srank[kMaxSample], 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (int i = threadIdx.x; i < S; i += blockDim.x) {
+        const int r = __hip_atomic_load(&srank[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int k = (int)(((int64_t)r * nb + S - 1) / S);  // the splitter index whose rank would be r
+        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) splitters[k - 1] = make_item(b, sample_pos(i, E, S));
+    }
 }
 
 __device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl, int nsplit, const uint8_t* arena) {
@@ -360,10 +386,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const SortI
         if (hist[i]) atomicAdd(&bcount[i], hist[i]);
 }
 
-// off[k] = sum of bcount[0..k) for k <= nb (nb <= 4 * kBlock), by one block.
+// off[k] = sum of bcount[0..k) for k <= nb (nb <= kMaxBuckets), by one block.
 __device__ __forceinline__ void bucket_prefix(const int32_t* bcount, int nb, int* off) {
     __shared__ int wsum[kBlock / 64];
-    const int per = 4;
+    constexpr int per = (kMaxBuckets + kBlock) / kBlock;  // covers nb + 1 entries
     const int a = threadIdx.x * per;
     int v[per];
     int sum = 0;
@@ -418,31 +444,43 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uin
     if (p < E) out[off[k] + local[k] + slot] = make_item(b, p);
 }
 
-// Sort one bucket; data in a[off, off+m), scratch in tmp (same offsets).  Result in a.
-__global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
-                                                              const uint8_t* arena) {
-    __shared__ SortItem sh[kSortTile];  // 128 KiB
+// Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets).  Items are distinct under
+// item_less_total, so an item's rank (items less than it) is its slot.
+__global__ __launch_bounds__(kBlock) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
+                                                        const uint8_t* arena) {
+    __shared__ SortItem sh[kRankTile];  // 32 KiB
+    constexpr int kPer = kRankTile / kBlock;
     const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
     if (m <= 1) return;
-    if (m <= kSortTile) {
-        for (int i = threadIdx.x; i < m; i += blockDim.x) sh[i] = a[off + i];
-        __syncthreads();
-        lds_merge_sort(sh, m, arena);
-        for (int i = threadIdx.x; i < m; i += blockDim.x) a[off + i] = sh[i];
-        return;
-    }
-    // oversized bucket (skewed sample): sort tiles in LDS, then merge pairs through global memory
-    for (int c = 0; c < m; c += kSortTile) {
-        const int cnt = min(kSortTile, m - c);
+    for (int c = 0; c < m; c += kRankTile) {
+        const int cnt = min(kRankTile, m - c);
         for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = a[off + c + i];
         __syncthreads();
-        lds_merge_sort(sh, cnt, arena);
-        for (int i = threadIdx.x; i < cnt; i += blockDim.x) a[off + c + i] = sh[i];
+        const int nk = (cnt - (int)threadIdx.x + kBlock - 1) / kBlock;  // items this thread ranks
+        SortItem mine[kPer];
+        int rk[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            rk[k] = 0;
+            if (k < nk) mine[k] = sh[threadIdx.x + k * kBlock];
+        }
+        for (int j = 0; j < cnt; j++) {
+            const SortItem x = sh[j];
+#pragma unroll
+            for (int k = 0; k < kPer; k++)
+                if (k < nk) rk[k] += item_less_total(x, mine[k], arena) ? 1 : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kPer; k++)
+            if (k < nk) a[off + c + rk[k]] = mine[k];
         __syncthreads();
     }
+    if (m <= kRankTile) return;
+    // oversized bucket (skewed sample): merge the sorted chunks pairwise through global memory
     SortItem* src = a + off;
     SortItem* dst = tmp + off;
-    for (int w = kSortTile; w < m; w *= 2) {
+    for (int w = kRankTile; w < m; w *= 2) {
         for (int o0 = 0; o0 < m; o0 += 8 * blockDim.x) {
             const int o = o0 + threadIdx.x * 8;
             if (o < m) {
@@ -452,6 +490,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 merge8_to(src + pb, lenA, src + pb + w, lenB, o - pb, dst + o, min(8, m - o), arena);
             }
         }
+        __threadfence_block();
         __syncthreads();
         SortItem* t = src;
         src = dst;
@@ -463,7 +502,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
 }
 
 int sort_buckets(int E) {
-    int nb = (E + 399) / 400;
+    int nb = (E + kBucketTarget - 1) / kBucketTarget;
     nb = nb < 1 ? 1 : nb;
     return nb > kMaxBuckets ? kMaxBuckets : nb;
 }
@@ -473,12 +512,18 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* re
     *result_buffer = 0;
     if (E == 0) return;
     const int nb = sort_buckets(E);
-    if (nb > 1) hipLaunchKernelGGL(k_sample, dim3(1), dim3(kBlock), 0, s, b, w.splitters, nb, b.tail);
+    if (nb > 1) {
+        int S = 4 * nb;
+        S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
+        S = S > E ? E : S;
+        hipLaunchKernelGGL(k_sample_rank, dim3((S + kSampleSlice - 1) / kSampleSlice), dim3(kBlock), 0, s, b, S, nb,
+                           w.srank, w.splitters, b.tail);
+    }
     const int grid = (E + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.splitters, nb, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
-    hipLaunchKernelGGL(k_bucket_sort, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    hipLaunchKernelGGL(k_bucket_sort, dim3(nb), dim3(kBlock), 0, s, w.items[0], w.items[1], w.boff, b.tail);
 }
 
 // ------------------------------------------------------------------ positions
@@ -854,14 +899,18 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
 }
 
+constexpr int kDeltaTile = 1024;  // copy tile of the (small) delta tier: enough workgroups to fill the chip
+constexpr int kBaseTile = 4096;   // copy tile of the base tier during compaction
+
 // tile_first[t] = first segment whose lo lies in copy tile t or later (segment j's share).
-__device__ __forceinline__ void fill_tile_first(int32_t* tile_first, const int64_t* lo, int64_t j) {
-    const int64_t t0 = j > 0 ? lo[j - 1] / kGcTile + 1 : 0;
-    for (int64_t t = t0; t <= lo[j] / kGcTile; t++) tile_first[t] = (int32_t)j;
+__device__ __forceinline__ void fill_tile_first(int32_t* tile_first, const int64_t* lo, int64_t j, int tile) {
+    const int64_t t0 = j > 0 ? lo[j - 1] / tile + 1 : 0;
+    for (int64_t t = t0; t <= lo[j] / tile; t++) tile_first[t] = (int32_t)j;
 }
-__device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const int64_t* lo, int64_t U, int64_t n) {
-    const int64_t t0 = U > 0 ? lo[U - 1] / kGcTile + 1 : 0;
-    for (int64_t t = t0; t <= n / kGcTile + 1; t++) tile_first[t] = (int32_t)U;
+__device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const int64_t* lo, int64_t U, int64_t n,
+                                                     int tile) {
+    const int64_t t0 = U > 0 ? lo[U - 1] / tile + 1 : 0;
+    for (int64_t t = t0; t <= n / tile + 1; t++) tile_first[t] = (int32_t)U;
 }
 
 // Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per union segment,
@@ -880,7 +929,7 @@ struct SegSumScan {
         g.rem[j] = ex[0];
         g.ins[j] = ex[1];
         tlen[j] = ex[2];
-        fill_tile_first(g.tile_first, g.lo, j);
+        fill_tile_first(g.tile_first, g.lo, j, kDeltaTile);
     }
     __device__ void finish(const uint32_t (&tot)[3]) const {
         const int64_t U = sc->n_segments, n = *io.n_in;
@@ -888,7 +937,7 @@ struct SegSumScan {
         g.rem[U] = tot[0];
         g.ins[U] = tot[1];
         tlen[U] = tot[2];
-        fill_tile_first_tail(g.tile_first, g.lo, U, n);
+        fill_tile_first_tail(g.tile_first, g.lo, U, n, kDeltaTile);
         *io.before = n;
         *io.removed = tot[0];
         *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
@@ -902,7 +951,7 @@ constexpr int kSegLds = 1024;
 // tile, the segments that can affect it are staged in LDS; element i is removed iff
 // lo_j <= i < hi_j for the last segment j with lo_j <= i, else it moves to i - rem_before +
 // ins_before.  `Ins` writes segment s's new boundaries starting at output position o.
-template <class Ins>
+template <class Ins, int TILE>
 __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist dst, const int64_t* n_in,
                                                        const int64_t* U_ptr, Ins ins) {
     __shared__ int64_t s_lo[kSegLds + 1], s_hi[kSegLds + 1], s_shift[kSegLds + 1];
@@ -911,10 +960,10 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
     const int64_t U = *U_ptr;
     __shared__ int s_ins0, s_ins1;
     // tiles cover positions [0, n]: position n only owns the inserts of segments past every boundary
-    for (int64_t i0 = (int64_t)blockIdx.x * kGcTile; i0 <= n; i0 += (int64_t)gridDim.x * kGcTile) {
-        const int64_t i1 = min(n, i0 + kGcTile);
+    for (int64_t i0 = (int64_t)blockIdx.x * TILE; i0 <= n; i0 += (int64_t)gridDim.x * TILE) {
+        const int64_t i1 = min(n, i0 + TILE);
         if (threadIdx.x == 0) {
-            const int64_t t = i0 / kGcTile;
+            const int64_t t = i0 / TILE;
             s_ins0 = g.tile_first[t];
             s_ins1 = g.tile_first[t + 1];
             s_j0 = s_ins0;  // slots: segment ja-1 (last with lo < i0), then the tile's own segments
@@ -937,7 +986,7 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
             // 8 elements per thread per chunk: resolve every destination first (branch-free binary
             // lifting over the staged segments), then issue all loads, then all stores, so each
             // thread keeps 8 independent HBM requests in flight.
-            constexpr int kPer = 8;
+            constexpr int kPer = TILE / kBlock < 8 ? TILE / kBlock : 8;
             for (int64_t c0 = i0; c0 < i1; c0 += kPer * kBlock) {
                 int64_t dsto[kPer];
 #pragma unroll
@@ -1034,8 +1083,8 @@ struct BatchIns {
 
 static Segs batch_segs(const Work& w) { return Segs{w.seg_lo, w.seg_hi, w.seg_rem, w.seg_ins, w.tile_first}; }
 
-static unsigned copy_tiles(int64_t grid_hint_n) {
-    int64_t tiles = (grid_hint_n + 1 + kGcTile - 1) / kGcTile;
+static unsigned copy_tiles(int64_t grid_hint_n, int tile) {
+    int64_t tiles = (grid_hint_n + 1 + tile - 1) / tile;
     if (tiles < 1) tiles = 1;
     if (tiles > 8192) tiles = 8192;
     return (unsigned)tiles;
@@ -1052,7 +1101,8 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                    w.scan[kScanSegSum]);
     if (copy_begin) (void)hipEventRecord(copy_begin, s);
     BatchIns ins{b, w.pmeta, w.seg_b, w.seg_e, w.seg_tlen, w.seg_vend, w.seg_endins, htail, sc, now};
-    hipLaunchKernelGGL(k_merge_copy<BatchIns>, dim3(copy_tiles(grid_hint_n)), dim3(kBlock), 0, s, batch_segs(w), src,
+    hipLaunchKernelGGL((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile)), dim3(kBlock), 0,
+                       s, batch_segs(w), src,
                        dst, &sc->nd, &sc->n_segments, ins);
     if (copy_end) (void)hipEventRecord(copy_end, s);
 }
@@ -1107,13 +1157,13 @@ struct CompactSumScan {
         g.hi[j] = hi_of(j);
         g.rem[j] = ex[0];
         g.ins[j] = ex[1];
-        fill_tile_first(g.tile_first, g.lo, j);
+        fill_tile_first(g.tile_first, g.lo, j, kBaseTile);
     }
     __device__ void finish(const uint32_t (&tot)[2]) const {
         const int64_t U = *nd_ptr, n = *io.n_in;
         g.rem[U] = tot[0];
         g.ins[U] = tot[1];
-        fill_tile_first_tail(g.tile_first, g.lo, U, n);
+        fill_tile_first_tail(g.tile_first, g.lo, U, n, kBaseTile);
         *io.before = n;
         *io.removed = tot[0];
         *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
@@ -1143,7 +1193,8 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const Hist& 
     launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
                    w.scan[kScanCompact]);
     if (copy_begin) (void)hipEventRecord(copy_begin, s);
-    hipLaunchKernelGGL(k_merge_copy<CompactIns>, dim3(copy_tiles(grid_hint_n)), dim3(kBlock), 0, s, g, base, dst,
+    hipLaunchKernelGGL((k_merge_copy<CompactIns, kBaseTile>), dim3(copy_tiles(grid_hint_n, kBaseTile)), dim3(kBlock), 0,
+                       s, g, base, dst,
                        &sc->n, &sc->nd_next, CompactIns{delta, w.c_val, w.c_ins});
     if (copy_end) (void)hipEventRecord(copy_end, s);
 }
@@ -1222,8 +1273,9 @@ struct Epilogue {
     int64_t zero32_n;
     uint64_t* zero64;  // scan arena
     int64_t zero64_n;
-    int32_t* zero_bc;  // sample-sort bucket counts and cursors
+    int32_t* zero_bc;  // sample-sort bucket counts and cursors [kMaxBuckets]
     int32_t* zero_bk;
+    int32_t* zero_rank;  // sample ranks + done counter [kMaxSample + 64]
 };
 
 // Range-max levels over lvl[0][0, n0) (lvl[3] reset beforehand); with a batch attached, also the
@@ -1296,10 +1348,11 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         ep.zero32b[i] = 0;
     }
     for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
-    for (int64_t i = tid; i < 1024; i += stride) {
+    for (int64_t i = tid; i < kMaxBuckets; i += stride) {
         ep.zero_bc[i] = 0;
         ep.zero_bk[i] = 0;
     }
+    for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
@@ -1339,6 +1392,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.zero64_n = w.scan_words;
     ep.zero_bc = w.bcount;
     ep.zero_bk = w.bcursor;
+    ep.zero_rank = w.srank;
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
     hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
