@@ -124,6 +124,7 @@ struct fdbcs_conflict_set {
 
     int inflight = 0;
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
+    int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket (testing knob; 0 = default)
     fdbcs_stats stats{};
 };
 
@@ -509,6 +510,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (!cs) return FDBCS_E_NOMEM;
     cs->device = device;
     if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
+    if (const char* v = getenv("FDBCS_SORT_BUCKET")) cs->bucket_target = atoi(v);
     if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) {
         delete cs;
         return FDBCS_E_DEVICE;
@@ -850,7 +852,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_check_reads(s, bd, base, delta, htail, w);
     HIPOK(hipEventRecord(b->ev[kPhCheck], s));
     int sorted = 0;
-    launch_sort_points(s, bd, w, &sorted);
+    launch_sort_points(s, bd, w, cs->bucket_target, &sorted);
     HIPOK(hipEventRecord(b->ev[kPhSort], s));
     launch_positions(s, bd, w, sorted);
     if (cs->validate) launch_validate_sort(s, bd, w, sorted, sc);

@@ -158,7 +158,8 @@ struct Tier {
 };
 void launch_check_reads(hipStream_t s, const BatchDev& b, const Tier& base, const Tier& delta, const uint8_t* htail,
                         const Work& w);
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer);
+// bucket_target: endpoints per sample-sort bucket (0 = default 256; tests force oversized buckets).
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);

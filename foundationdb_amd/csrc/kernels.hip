@@ -220,32 +220,8 @@ __device__ __forceinline__ bool item_less_total(const SortItem& a, const SortIte
     return (a.hi < b.hi) | (hi_eq & ((a.lo < b.lo) | (lo_eq & aux_lt)));
 }
 
-// Merge-path split + 8-way serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties):
-// writes outputs [d, d+count) of the merged sequence to out[0, count).
-__device__ __forceinline__ void merge8(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
-                                       SortItem (&out)[8], int count, const uint8_t* arena) {
-    int lo = d - lenB > 0 ? d - lenB : 0;
-    int hi = d < lenA ? d : lenA;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (!item_less_total(B[d - mid - 1], A[mid], arena))
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    int i = lo, j = d - lo;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        if (k < count) {
-            bool takeA = (j >= lenB) || (i < lenA && !item_less_total(B[j], A[i], arena));
-            out[k] = takeA ? A[i] : B[j];
-            i += takeA ? 1 : 0;
-            j += takeA ? 0 : 1;
-        }
-    }
-}
-
-// As merge8, writing the outputs straight to dst[0, count).
+// Merge-path split + serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties): writes
+// outputs [d, d+count) of the merged sequence to dst[0, count).
 __device__ __forceinline__ void merge8_to(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
                                           SortItem* dst, int count, const uint8_t* arena) {
     int lo = d - lenB > 0 ? d - lenB : 0;
@@ -266,47 +242,41 @@ __device__ __forceinline__ void merge8_to(const SortItem* A, int lenA, const Sor
     }
 }
 
-// Compare-exchange of two register items (constant indices keep them in VGPRs).
-__device__ __forceinline__ void cex(SortItem& a, SortItem& b, bool active, const uint8_t* arena) {
-    if (active && item_less_total(b, a, arena)) {
-        SortItem t = a;
-        a = b;
-        b = t;
+// Rank counting: rk[k] += number of items of sh[0, cnt) ordered before mine[k].  Branch-free on
+// the 16-byte prefix and the (length, class, id) tie-break word, 8 LDS reads in flight; a
+// comparison that needs the bytes beyond the prefix (both keys longer than 16 bytes, equal
+// prefixes) only raises `tail`, and the caller recounts that item exactly.
+template <int P>
+__device__ __forceinline__ void rank_count(const SortItem* sh, int cnt, const SortItem (&mine)[P], int (&rk)[P],
+                                           bool& tail) {
+    uint64_t maux[P];
+#pragma unroll
+    for (int k = 0; k < P; k++) maux[k] = item_aux(mine[k]);
+    auto one = [&](const SortItem& x) {
+        const uint64_t xa = item_aux(x);
+#pragma unroll
+        for (int k = 0; k < P; k++) {
+            const bool heq = x.hi == mine[k].hi, leq = x.lo == mine[k].lo;
+            rk[k] += ((x.hi < mine[k].hi) | (heq & ((x.lo < mine[k].lo) | (leq & (xa < maux[k]))))) ? 1 : 0;
+            tail |= heq & leq & (x.len > 16u) & (mine[k].len > 16u) & (x.meta != mine[k].meta);
+        }
+    };
+    int j = 0;
+    for (; j + 8 <= cnt; j += 8) {
+        SortItem x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) x[u] = sh[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) one(x[u]);
     }
+    for (; j < cnt; j++) one(sh[j]);
 }
 
-// Sort sh[0, cnt) (cnt <= 8 * blockDim.x) in LDS: each thread sorts its 8 items with Batcher's
-// odd-even merge network (19 comparators), then runs of 8, 16, ... are merged by merge path.
-__device__ void lds_merge_sort(SortItem* sh, int cnt, const uint8_t* arena) {
-    const int o = threadIdx.x * 8;
-    const int mine = max(0, min(8, cnt - o));
-    SortItem r[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-        if (k < mine) r[k] = sh[o + k];
-#define CEX(i, j) cex(r[i], r[j], (j) < mine, arena)
-    CEX(0, 1); CEX(2, 3); CEX(4, 5); CEX(6, 7);
-    CEX(0, 2); CEX(1, 3); CEX(4, 6); CEX(5, 7);
-    CEX(1, 2); CEX(5, 6);
-    CEX(0, 4); CEX(1, 5); CEX(2, 6); CEX(3, 7);
-    CEX(2, 4); CEX(3, 5);
-    CEX(1, 2); CEX(3, 4); CEX(5, 6);
-#undef CEX
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-        if (k < mine) sh[o + k] = r[k];
-    __syncthreads();
-    for (int w = 8; w < cnt; w <<= 1) {
-        const int pb = (o / (2 * w)) * (2 * w);
-        const int lenA = max(0, min(w, cnt - pb));
-        const int lenB = max(0, min(w, cnt - pb - w));
-        if (mine > 0) merge8(sh + pb, lenA, sh + pb + w, lenB, o - pb, r, mine, arena);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (k < mine) sh[o + k] = r[k];
-        __syncthreads();
-    }
+// Exact rank of one item (tail comparisons included): the slow path of rank_count.
+__device__ __noinline__ int rank_exact(const SortItem* sh, int cnt, SortItem mine, const uint8_t* arena) {
+    int r = 0;
+    for (int j = 0; j < cnt; j++) r += item_less_total(sh[j], mine, arena) ? 1 : 0;
+    return r;
 }
 
 // ---- sample sort of the batch endpoints (D.Sort, SkipList.cpp:161-208)
@@ -336,10 +306,12 @@ __global__ __launch_bounds__(kBlock) void k_sample_rank(BatchDev b, int S, int n
     for (int t = threadIdx.x; t < cj; t += blockDim.x) sl[t] = make_item(b, sample_pos(j0 + t, E, S));
     __syncthreads();
     for (int i = threadIdx.x; i < S; i += blockDim.x) {
-        const SortItem mine = make_item(b, sample_pos(i, E, S));
-        int c = 0;
-        for (int j = 0; j < cj; j++) c += item_less_total(sl[j], mine, arena) ? 1 : 0;
-        if (c) atomicAdd(&srank[i], c);
+        SortItem mine[1] = {make_item(b, sample_pos(i, E, S))};
+        int c[1] = {0};
+        bool tail = false;
+        rank_count<1>(sl, cj, mine, c, tail);
+        if (tail) c[0] = rank_exact(sl, cj, mine[0], arena);
+        if (c[0]) atomicAdd(&srank[i], c[0]);
     }
     // the last workgroup to finish sees every partial rank and writes the splitters
     __threadfence();
@@ -456,24 +428,35 @@ __global__ __launch_bounds__(kBlock) void k_bucket_sort(SortItem* a, SortItem* t
         const int cnt = min(kRankTile, m - c);
         for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = a[off + c + i];
         __syncthreads();
-        const int nk = (cnt - (int)threadIdx.x + kBlock - 1) / kBlock;  // items this thread ranks
-        SortItem mine[kPer];
-        int rk[kPer];
+        if (cnt <= kBlock) {  // the common bucket: one item per thread
+            if ((int)threadIdx.x < cnt) {
+                SortItem mine[1] = {sh[threadIdx.x]};
+                int rk[1] = {0};
+                bool tail = false;
+                rank_count<1>(sh, cnt, mine, rk, tail);
+                if (tail) rk[0] = rank_exact(sh, cnt, mine[0], arena);
+                a[off + c + rk[0]] = mine[0];
+            }
+        } else {
+            SortItem mine[kPer];
+            int rk[kPer];
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            rk[k] = 0;
-            if (k < nk) mine[k] = sh[threadIdx.x + k * kBlock];
+            for (int k = 0; k < kPer; k++) {
+                rk[k] = 0;
+                const int i = threadIdx.x + k * kBlock;
+                mine[k] = sh[i < cnt ? i : cnt - 1];
+            }
+            bool tail = false;
+            rank_count<kPer>(sh, cnt, mine, rk, tail);
+#pragma unroll
+            for (int k = 0; k < kPer; k++) {
+                const int i = threadIdx.x + k * kBlock;
+                if (i < cnt) {
+                    const int r = tail ? rank_exact(sh, cnt, mine[k], arena) : rk[k];
+                    a[off + c + r] = mine[k];
+                }
+            }
         }
-        for (int j = 0; j < cnt; j++) {
-            const SortItem x = sh[j];
-#pragma unroll
-            for (int k = 0; k < kPer; k++)
-                if (k < nk) rk[k] += item_less_total(x, mine[k], arena) ? 1 : 0;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kPer; k++)
-            if (k < nk) a[off + c + rk[k]] = mine[k];
         __syncthreads();
     }
     if (m <= kRankTile) return;
@@ -501,17 +484,18 @@ __global__ __launch_bounds__(kBlock) void k_bucket_sort(SortItem* a, SortItem* t
     }
 }
 
-int sort_buckets(int E) {
-    int nb = (E + kBucketTarget - 1) / kBucketTarget;
+int sort_buckets(int E, int target) {
+    if (target <= 0) target = kBucketTarget;
+    int nb = (E + target - 1) / target;
     nb = nb < 1 ? 1 : nb;
     return nb > kMaxBuckets ? kMaxBuckets : nb;
 }
 
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int* result_buffer) {
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int* result_buffer) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
-    const int nb = sort_buckets(E);
+    const int nb = sort_buckets(E, bucket_target);
     if (nb > 1) {
         int S = 4 * nb;
         S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);

@@ -215,6 +215,36 @@ def test_edge_cases(engine):
     assert ex.value.status == engine.FDBCS_E_VERSION
 
 
+@pytest.mark.parametrize("bucket", ["3000", "40"])
+def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket):
+    """Oversized sort buckets (chunked rank sort + merges through memory) and tiny ones, with keys
+    longer than the 16-byte prefix, give the same verdicts and reports."""
+    monkeypatch.setenv("FDBCS_SORT_BUCKET", bucket)
+    rng = np.random.default_rng(31)
+    seq = []
+    now = 10
+    for i in range(4):
+        pb = W.random_small_batch(rng, 700, alphabet=3, max_len=4, now=now, staleness=10, report_frac=0.5)
+        if i % 2:  # every key behind a shared 17-byte prefix: prefix ties resolved by the tail bytes
+            pb = prefixed(pb, b"\x02tenant\x00orders\x00\x15\x01")
+        seq.append((pb, now, now - 3))
+        now += 2
+    run_pair(engine, oracle_mod, seq)
+
+
+def prefixed(pb, prefix):
+    """The same batch with `prefix` prepended to every key (order and overlaps unchanged)."""
+    lens = np.diff(pb.key_offsets)
+    parts = [np.frombuffer(prefix, np.uint8)]
+    out = []
+    for k in range(len(lens)):
+        out.append(parts[0])
+        out.append(pb.key_bytes[pb.key_offsets[k] : pb.key_offsets[k + 1]])
+    kb = np.concatenate(out) if out else np.zeros(0, np.uint8)
+    ko = np.concatenate([[0], np.cumsum(lens + len(prefix))]).astype(np.int64)
+    return PackedBatch(pb.read_snapshot, pb.report, pb.read_offsets, pb.write_offsets, kb, ko)
+
+
 def test_sequential_fallback_matches(engine, oracle_mod, monkeypatch):
     """Force the candidate-edge overflow path (sequential MiniConflictSet replay on the GPU)."""
     monkeypatch.setenv("FDBCS_EDGE_CAP", "8")
