@@ -291,7 +291,6 @@ __device__ __noinline__ int rank_exact(const SortItem* sh, int cnt, SortItem min
 constexpr int kMaxBuckets = 2048;
 constexpr int kMaxSample = 8192;
 constexpr int kSampleSlice = 64;
-constexpr int kRankTile = 1024;
 constexpr int kBucketTarget = 256;
 
 __device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((int64_t)i * E) / S); }
@@ -301,11 +300,13 @@ __global__ __launch_bounds__(kBlock) void k_sample_rank(BatchDev b, int S, int n
     __shared__ SortItem sl[kSampleSlice];
     __shared__ int s_last;
     const int E = 2 * (b.R + b.W);
+    // workgroup (x, y): samples [y*256, y*256+256) against the slice [x*64, x*64+64)
     const int j0 = blockIdx.x * kSampleSlice;
     const int cj = min(kSampleSlice, S - j0);
     for (int t = threadIdx.x; t < cj; t += blockDim.x) sl[t] = make_item(b, sample_pos(j0 + t, E, S));
     __syncthreads();
-    for (int i = threadIdx.x; i < S; i += blockDim.x) {
+    const int i = blockIdx.y * blockDim.x + threadIdx.x;
+    if (i < S) {
         SortItem mine[1] = {make_item(b, sample_pos(i, E, S))};
         int c[1] = {0};
         bool tail = false;
@@ -316,14 +317,14 @@ __global__ __launch_bounds__(kBlock) void k_sample_rank(BatchDev b, int S, int n
     // the last workgroup to finish sees every partial rank and writes the splitters
     __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&srank[kMaxSample], 1) == (int)gridDim.x - 1;
+    if (threadIdx.x == 0) s_last = atomicAdd(&srank[kMaxSample], 1) == (int)(gridDim.x * gridDim.y) - 1;
     __syncthreads();
     if (!s_last) return;
     __threadfence();
-    for (int i = threadIdx.x; i < S; i += blockDim.x) {
-        const int r = __hip_atomic_load(&srank[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = threadIdx.x; q < S; q += blockDim.x) {
+        const int r = __hip_atomic_load(&srank[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int k = (int)(((int64_t)r * nb + S - 1) / S);  // the splitter index whose rank would be r
-        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) splitters[k - 1] = make_item(b, sample_pos(i, E, S));
+        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) splitters[k - 1] = make_item(b, sample_pos(q, E, S));
     }
 }
 
@@ -416,54 +417,62 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uin
     if (p < E) out[off[k] + local[k] + slot] = make_item(b, p);
 }
 
-// Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets).  Items are distinct under
-// item_less_total, so an item's rank (items less than it) is its slot.
-__global__ __launch_bounds__(kBlock) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
-                                                        const uint8_t* arena) {
-    __shared__ SortItem sh[kRankTile];  // 32 KiB
-    constexpr int kPer = kRankTile / kBlock;
+// Sentinel-aware order for the bitonic network: padding items (pad = 1) sort after every item.
+__device__ __forceinline__ bool lt_pad(const SortItem& x, const SortItem& y, const uint8_t* arena) {
+    if (x.pad | y.pad) return y.pad && !x.pad;
+    return item_less_total(x, y, arena);
+}
+
+// Bitonic sort of sh[0, L) (L a power of two, L/2 <= blockDim.x) in LDS.
+__device__ void lds_bitonic(SortItem* sh, int L, const uint8_t* arena) {
+    for (int k = 2; k <= L; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const int t = threadIdx.x;
+            if (t < (L >> 1)) {
+                const int i = 2 * t - (t & (j - 1)), p = i + j;
+                const SortItem x = sh[i], y = sh[p];
+                const bool up = (i & k) == 0;
+                if (up ? lt_pad(y, x, arena) : lt_pad(x, y, arena)) {
+                    sh[i] = y;
+                    sh[p] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+constexpr int kBitonicMax = 2 * kSortThreads;  // endpoints sorted in one pass by one workgroup
+
+// Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic in LDS, padded to a
+// power of two; oversized buckets (skewed sample) sort kBitonicMax chunks, then merge through memory.
+__global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
+                                                              const uint8_t* arena) {
+    __shared__ SortItem sh[kBitonicMax];  // 32 KiB
     const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
     if (m <= 1) return;
-    for (int c = 0; c < m; c += kRankTile) {
-        const int cnt = min(kRankTile, m - c);
-        for (int i = threadIdx.x; i < cnt; i += blockDim.x) sh[i] = a[off + c + i];
-        __syncthreads();
-        if (cnt <= kBlock) {  // the common bucket: one item per thread
-            if ((int)threadIdx.x < cnt) {
-                SortItem mine[1] = {sh[threadIdx.x]};
-                int rk[1] = {0};
-                bool tail = false;
-                rank_count<1>(sh, cnt, mine, rk, tail);
-                if (tail) rk[0] = rank_exact(sh, cnt, mine[0], arena);
-                a[off + c + rk[0]] = mine[0];
-            }
-        } else {
-            SortItem mine[kPer];
-            int rk[kPer];
-#pragma unroll
-            for (int k = 0; k < kPer; k++) {
-                rk[k] = 0;
-                const int i = threadIdx.x + k * kBlock;
-                mine[k] = sh[i < cnt ? i : cnt - 1];
-            }
-            bool tail = false;
-            rank_count<kPer>(sh, cnt, mine, rk, tail);
-#pragma unroll
-            for (int k = 0; k < kPer; k++) {
-                const int i = threadIdx.x + k * kBlock;
-                if (i < cnt) {
-                    const int r = tail ? rank_exact(sh, cnt, mine[k], arena) : rk[k];
-                    a[off + c + r] = mine[k];
-                }
+    for (int c = 0; c < m; c += kBitonicMax) {
+        const int cnt = min(kBitonicMax, m - c);
+        int L = 2;
+        while (L < cnt) L <<= 1;
+        for (int i = threadIdx.x; i < L; i += blockDim.x) {
+            if (i < cnt) {
+                sh[i] = a[off + c + i];
+            } else {
+                SortItem z{};
+                z.pad = 1;
+                sh[i] = z;
             }
         }
         __syncthreads();
+        lds_bitonic(sh, L, arena);
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) a[off + c + i] = sh[i];
+        __syncthreads();
     }
-    if (m <= kRankTile) return;
-    // oversized bucket (skewed sample): merge the sorted chunks pairwise through global memory
+    if (m <= kBitonicMax) return;
     SortItem* src = a + off;
     SortItem* dst = tmp + off;
-    for (int w = kRankTile; w < m; w *= 2) {
+    for (int w = kBitonicMax; w < m; w *= 2) {
         for (int o0 = 0; o0 < m; o0 += 8 * blockDim.x) {
             const int o = o0 + threadIdx.x * 8;
             if (o < m) {
@@ -500,14 +509,14 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
         int S = 4 * nb;
         S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
         S = S > E ? E : S;
-        hipLaunchKernelGGL(k_sample_rank, dim3((S + kSampleSlice - 1) / kSampleSlice), dim3(kBlock), 0, s, b, S, nb,
-                           w.srank, w.splitters, b.tail);
+        hipLaunchKernelGGL(k_sample_rank, dim3((S + kSampleSlice - 1) / kSampleSlice, (S + kBlock - 1) / kBlock),
+                           dim3(kBlock), 0, s, b, S, nb, w.srank, w.splitters, b.tail);
     }
     const int grid = (E + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.splitters, nb, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
-    hipLaunchKernelGGL(k_bucket_sort, dim3(nb), dim3(kBlock), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    hipLaunchKernelGGL(k_bucket_sort, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
 }
 
 // ------------------------------------------------------------------ positions
