@@ -79,7 +79,7 @@ struct HBuf {
 
 enum Phase {
     kPhStart, kPhUpload, kPhCheck, kPhSort, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge,
-    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhCount
+    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhFork, kPhCheckBegin, kPhCount
 };
 
 }  // namespace
@@ -89,6 +89,7 @@ struct fdbcs_batch;
 struct fdbcs_conflict_set {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;  // the read check runs here, concurrently with the endpoint sort
     int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
     int64_t header_version = 0;  // SkipList(Version) header (SkipList.cpp:398-404)
     int64_t max_written = 0;     // highest version present in the history
@@ -515,6 +516,11 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
         delete cs;
         return FDBCS_E_DEVICE;
     }
+    if (hipStreamCreateWithFlags(&cs->side, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipStreamDestroy(cs->stream);
+        delete cs;
+        return FDBCS_E_DEVICE;
+    }
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
@@ -546,7 +552,9 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     for (auto& x : cs->cws) x.release();
     for (auto& x : cs->ws) x.release();
     cs->scal.release();
+    if (cs->side) (void)hipStreamSynchronize(cs->side);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
+    if (cs->side) (void)hipStreamDestroy(cs->side);
     delete cs;
 }
 
@@ -849,13 +857,19 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->nd, kHole};
     uint8_t* htail = (uint8_t*)cs->htail.p;
 
-    launch_check_reads(s, bd, base, delta, htail, w);
-    HIPOK(hipEventRecord(b->ev[kPhCheck], s));
+    // D.CheckRead on the side stream, overlapping D.Sort and the position scan (independent work;
+    // both are latency-bound and leave most of the chip idle); joined before the first consumer.
+    HIPOK(hipEventRecord(b->ev[kPhFork], s));
+    HIPOK(hipStreamWaitEvent(cs->side, b->ev[kPhFork], 0));
+    HIPOK(hipEventRecord(b->ev[kPhCheckBegin], cs->side));
+    launch_check_reads(cs->side, bd, base, delta, htail, w);
+    HIPOK(hipEventRecord(b->ev[kPhCheck], cs->side));
     int sorted = 0;
     launch_sort_points(s, bd, w, cs->bucket_target, &sorted);
     HIPOK(hipEventRecord(b->ev[kPhSort], s));
     launch_positions(s, bd, w, sorted);
     if (cs->validate) launch_validate_sort(s, bd, w, sorted, sc);
+    HIPOK(hipStreamWaitEvent(s, b->ev[kPhCheck], 0));
     launch_edges(s, bd, w, sc);
     launch_resolve(s, bd, w, sc, b->any_report);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf
@@ -967,8 +981,8 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         st.read_ranges += b->R();
         st.write_ranges += b->W();
         st.ms_upload += ev_ms(b->ev[kPhStart], b->ev[kPhUpload]);
-        st.ms_check_read += ev_ms(b->ev[kPhUpload], b->ev[kPhCheck]);
-        st.ms_sort += ev_ms(b->ev[kPhCheck], b->ev[kPhSort]);
+        st.ms_check_read += ev_ms(b->ev[kPhCheckBegin], b->ev[kPhCheck]);  // concurrent with the sort
+        st.ms_sort += ev_ms(b->ev[kPhUpload], b->ev[kPhSort]);
         st.ms_intra += ev_ms(b->ev[kPhSort], b->ev[kPhIntra]);
         st.ms_combine += ev_ms(b->ev[kPhIntra], b->ev[kPhCombine]);
         st.ms_merge += ev_ms(b->ev[kPhCombine], b->ev[kPhMerge]);

@@ -45,6 +45,49 @@ __device__ __forceinline__ int64_t hist_lower_bound(const Hist& h, int64_t lo, i
     return lo;
 }
 
+// Q independent std::lower_bound searches advanced in lockstep: each round issues every active
+// probe load before comparing, so a thread keeps Q requests in flight and the critical path is one
+// search deep.  eq[i]: key[lo[i]] == q[i] (the last probe that lowered hi hit the key itself).
+template <int Q>
+__device__ __forceinline__ void multi_lower_bound(const Hist (&h)[Q], int64_t (&lo)[Q], int64_t (&hi)[Q],
+                                                  bool (&eq)[Q], const uint8_t* htail, const DKey (&q)[Q],
+                                                  const uint8_t* qtail) {
+#pragma unroll
+    for (int i = 0; i < Q; i++) eq[i] = false;
+    for (;;) {
+        bool any = false;
+        int64_t mid[Q];
+        ulonglong2 k[Q];
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            mid[i] = (lo[i] + hi[i]) >> 1;
+            if (lo[i] < hi[i]) {
+                k[i] = h[i].key[mid[i]];
+                any = true;
+            }
+        }
+        if (!any) break;
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            if (lo[i] < hi[i]) {
+                int c;
+                if (k[i].x != q[i].hi)
+                    c = k[i].x < q[i].hi ? -1 : 1;
+                else if (k[i].y != q[i].lo)
+                    c = k[i].y < q[i].lo ? -1 : 1;
+                else
+                    c = hist_cmp(h[i], mid[i], htail, q[i], qtail);  // equal prefixes: length / tail
+                if (c < 0) {
+                    lo[i] = mid[i] + 1;
+                } else {
+                    hi[i] = mid[i];
+                    eq[i] = c == 0;
+                }
+            }
+        }
+    }
+}
+
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
 __device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
     int64_t best = LLONG_MIN;
@@ -131,15 +174,13 @@ __device__ T wg_scan(int64_t n, Load load, Store store, T* sh) {
 
 // ------------------------------------------------------------------ D.CheckRead
 
-// Does some segment of one tier meeting the read [kb, ke) hold a version > snap?  Degenerate
-// [b, b) reads look at the greatest boundary < b (fingers never diverge, SkipList.cpp:650-666).
-__device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m, int64_t n, int64_t hdr,
-                                              const uint8_t* htail, const DKey& kb, const DKey& ke,
-                                              const uint8_t* qtail, bool degenerate, int64_t snap) {
-    const int64_t lb = hist_lower_bound(h, 0, n, htail, kb, qtail);
+// Does some segment of one tier meeting the read [kb, ke) hold a version > snap?  lb / lb_eq locate
+// kb, j = lower_bound(ke).  Degenerate [b, b) reads look at the greatest boundary < b (fingers
+// never diverge, SkipList.cpp:650-666).
+__device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m, int64_t hdr, int64_t lb, bool lb_eq,
+                                              int64_t j, bool degenerate, int64_t snap) {
     if (degenerate) return (lb > 0 ? h.ver[lb - 1] : hdr) > snap;
-    const int64_t ub = lb + ((lb < n && hist_cmp(h, lb, htail, kb, qtail) == 0) ? 1 : 0);
-    const int64_t j = hist_lower_bound(h, ub, n, htail, ke, qtail);
+    const int64_t ub = lb + (lb_eq ? 1 : 0);
     // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
     if (ub == 0) return hdr > snap || range_max(m, 0, j, snap) > snap;
     return range_max(m, ub - 1, j, snap) > snap;
@@ -148,7 +189,8 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
 // One thread per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
 // of SURVEY A.2).  The history is the base tier overlaid by the delta tier; every delta version is
 // >= the base versions it covers (versions only grow), so the max over the overlay equals the max
-// of the two tiers' maxima, and holes (kHole) never conflict.
+// of the two tiers' maxima, and holes (kHole) never conflict.  The four searches (begin and end
+// key in both tiers) run in lockstep.
 __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Tier base, Tier delta, const uint8_t* htail,
                                                         uint8_t* hist_conf, uint8_t* rconf) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -157,11 +199,15 @@ __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Tier base, T
     const int64_t snap = b.snap[t];
     const DKey kb = b.keys[2 * r], ke = b.keys[2 * r + 1];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    bool conf = tier_conflict(base.h, base.m, *base.n, base.hdr, htail, kb, ke, b.tail, degenerate, snap);
-    if (!conf) {
-        const int64_t nd = *delta.n;
-        if (nd > 0) conf = tier_conflict(delta.h, delta.m, nd, kHole, htail, kb, ke, b.tail, degenerate, snap);
-    }
+    const int64_t nb = *base.n, nd = *delta.n;
+    const Hist h[4] = {base.h, base.h, delta.h, delta.h};
+    const DKey q[4] = {kb, ke, kb, ke};
+    int64_t lo[4] = {0, 0, 0, 0};
+    int64_t hi[4] = {nb, degenerate ? 0 : nb, nd, degenerate ? 0 : nd};
+    bool eq[4];
+    multi_lower_bound<4>(h, lo, hi, eq, htail, q, b.tail);
+    bool conf = tier_conflict(base.h, base.m, base.hdr, lo[0], eq[0], lo[1], degenerate, snap);
+    if (!conf && nd > 0) conf = tier_conflict(delta.h, delta.m, kHole, lo[2], eq[2], lo[3], degenerate, snap);
     rconf[r] = conf ? 1 : 0;
     if (conf) hist_conf[t] = 1;
 }
@@ -878,9 +924,13 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     const int64_t n = *n_in;
     const DKey kb = seg_key(b, w, w.seg_b[s], 0);
     const DKey ke = seg_key(b, w, w.seg_e[s], 1);
-    const int64_t lo = hist_lower_bound(h, 0, n, htail, kb, b.tail);
-    const int64_t hi = hist_lower_bound(h, lo, n, htail, ke, b.tail);
-    const bool exact = hi < n && hist_cmp(h, hi, htail, ke, b.tail) == 0;
+    const Hist hh[2] = {h, h};
+    const DKey q[2] = {kb, ke};
+    int64_t l[2] = {0, 0}, u[2] = {n, n};
+    bool eq[2];
+    multi_lower_bound<2>(hh, l, u, eq, htail, q, b.tail);
+    const int64_t lo = l[0], hi = l[1];
+    const bool exact = eq[1];
     const bool glue = s + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[s + 1], 0), b.tail, ke, b.tail) == 0;
     const bool endins = !exact && !glue;
     w.seg_lo[s] = lo;
@@ -1122,8 +1172,13 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, Hist delta
     q.lo = k.y;
     q.len = lt.x;
     q.tail = lt.y;
-    const int64_t lo = hist_lower_bound(base, 0, nb, htail, q, htail);
-    const bool exact = lo < nb && hist_cmp(base, lo, htail, q, htail) == 0;
+    const Hist hh[1] = {base};
+    const DKey qq[1] = {q};
+    int64_t l[1] = {0}, u[1] = {nb};
+    bool eq[1];
+    multi_lower_bound<1>(hh, l, u, eq, htail, qq, htail);
+    const int64_t lo = l[0];
+    const bool exact = eq[0];
     const int64_t dv = delta.ver[j];
     w.c_lo[j] = lo;
     w.c_exact[j] = exact ? 1 : 0;

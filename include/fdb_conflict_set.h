@@ -84,7 +84,7 @@ typedef struct fdbcs_stats {
     int64_t read_ranges;
     int64_t write_ranges;
     double ms_upload;       /* H2D of packed batches */
-    double ms_check_read;   /* history check (search + range max over both tiers) */
+    double ms_check_read;   /* history check (search + range max over both tiers; overlaps the sort) */
     double ms_sort;         /* endpoint sort */
     double ms_intra;        /* intra-batch candidate edges + batch-order resolution */
     double ms_combine;      /* union of committed writes */
