@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--gc-interval", type=int, default=0,
                     help="force a compaction (+GC) at least every N batches; 0 = when the delta tier is full")
     ap.add_argument("--delta-limit", type=int, default=0, help="delta-tier bound; 0 = automatic (~base/16)")
+    ap.add_argument("--timing", type=int, default=1, choices=[0, 1],
+                    help="events in the timed region: 0 none, 1 around the copy kernels (roofline)")
+    ap.add_argument("--breakdown-steps", type=int, default=16,
+                    help="extra batches after the timed region with every phase timed (diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
@@ -163,14 +167,16 @@ def main():
     t0 = time.time()
     kb, ko, vers = shard_history(p, args.seed, rank, world, start_version)
     total = args.warmup + args.steps
-    gbatches = make_batches(args, p, total, world, start_version)
+    n_all = total + args.breakdown_steps
+    gbatches = make_batches(args, p, n_all, world, start_version)
     sharding = KeyRangeSharding.uniform(world) if world > 1 else None
     routed = [sharding.route(pb)[rank] for pb, _, _ in gbatches] if sharding else None
-    log(f"[rank {rank}] generated history {len(vers)} + {total} batches in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] generated history {len(vers)} + {n_all} batches in {time.time() - t0:.1f}s")
 
     cs = C.ConflictSet(device)
     cs.set_gc_interval(args.gc_interval)
     cs.set_delta_limit(args.delta_limit)
+    cs.set_timing(args.timing)
     cs.load_history(kb, ko, vers, 0)
     mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
     maxT = max(b.n_txn for b in mine)
@@ -214,6 +220,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = cs.stats()
+    # diagnostic phase split: extra batches with every phase timed (each event costs queue time,
+    # so these are outside the timed region)
+    phase = None
+    if args.breakdown_steps > 0:
+        cs.set_timing(2)
+        cs.reset_stats()
+        run(total, n_all, dist is not None)
+        torch.cuda.synchronize()
+        sb = cs.stats()
+        phase = {
+            k: sb[k] / max(1, sb["batches"])
+            for k in ("ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_compact", "ms_gc",
+                      "ms_epilogue", "ms_total")
+        }
+        phase["batches"] = sb["batches"]
+        phase["compactions"] = sb["compactions"]
     gtxn = sum(gbatches[i][0].n_txn for i in range(args.warmup, total))
     granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(args.warmup, total))
     hist_end = cs.history_size()
@@ -266,11 +288,7 @@ def main():
         },
         "conflict_ranges_per_s": granges / elapsed,
         "history_boundaries_end": hist_end,
-        "phase_ms_per_batch": {
-            k: st[k] / max(1, st["batches"])
-            for k in ("ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_compact", "ms_gc",
-                      "ms_epilogue", "ms_total")
-        },
+        "phase_ms_per_batch": phase,
         "compactions": st["compactions"],
         "other_copy_kernel": {
             "kernel": other[0],

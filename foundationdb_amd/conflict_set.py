@@ -89,6 +89,7 @@ SIGNATURES = {
     "fdbcs_reset_stats": (ctypes.c_int, [_VP]),
     "fdbcs_set_gc_interval": (ctypes.c_int, [_VP, _I32]),
     "fdbcs_set_delta_limit": (ctypes.c_int, [_VP, _I64]),
+    "fdbcs_set_timing": (ctypes.c_int, [_VP, _I32]),
     "fdbcs_reserve": (ctypes.c_int, [_VP, _I64, _I64, _I32, _I32, _I32]),
     "fdbcs_batch_new": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.POINTER(_VP)]),
     "fdbcs_batch_destroy": (None, [_VP]),
@@ -185,6 +186,10 @@ class ConflictSet:
     def set_gc_interval(self, every: int) -> None:
         """Compaction (with GC) at least every `every` batches; 0 = only when the delta is full."""
         _check(load_library().fdbcs_set_gc_interval(self._h, every), "setGcInterval")
+
+    def set_timing(self, level: int) -> None:
+        """Device timing: 0 none, 1 copy kernels (roofline), 2 every phase (stats())."""
+        _check(load_library().fdbcs_set_timing(self._h, level), "setTiming")
 
     def set_delta_limit(self, boundaries: int) -> None:
         """Delta-tier bound that triggers a compaction; 0 = automatic (~1/16 of the base)."""

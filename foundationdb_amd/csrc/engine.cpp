@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <vector>
 
@@ -56,30 +57,32 @@ struct DBuf {
     }
 };
 
-// Grow-only pinned host allocation.
+// Grow-only pinned host allocation; `mapped` buffers are fine-grained and written by kernels directly.
 struct HBuf {
     void* p = nullptr;
+    void* dp = nullptr;  // device view (mapped buffers)
     size_t cap = 0;
-    int ensure(size_t bytes) {
+    int ensure(size_t bytes, bool mapped = false) {
         if (bytes <= cap) return FDBCS_OK;
         size_t want = align_up(std::max(bytes, cap + cap / 2), 4096);
         if (p) HIPOK(hipHostFree(p));
-        p = nullptr;
+        p = dp = nullptr;
         cap = 0;
-        HIPOK(hipHostMalloc(&p, want, hipHostMallocDefault));
+        HIPOK(hipHostMalloc(&p, want, mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault));
+        if (mapped) HIPOK(hipHostGetDevicePointer(&dp, p, 0));
         cap = want;
         return FDBCS_OK;
     }
     void release() {
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dp = nullptr;
         cap = 0;
     }
 };
 
 enum Phase {
     kPhStart, kPhUpload, kPhCheck, kPhSort, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge,
-    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhFork, kPhCheckBegin, kPhCount
+    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhCount
 };
 
 }  // namespace
@@ -89,7 +92,8 @@ struct fdbcs_batch;
 struct fdbcs_conflict_set {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;  // the read check runs here, concurrently with the endpoint sort
+    int timing = 0;       // 0: no events; 1: the copy kernels; 2: every phase (fdbcs_set_timing)
+    uint32_t seq = 0;     // batches submitted (completion flag values)
     int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
     int64_t header_version = 0;  // SkipList(Version) header (SkipList.cpp:398-404)
     int64_t max_written = 0;     // highest version present in the history
@@ -157,6 +161,9 @@ struct fdbcs_batch {
     bool events_made = false;
     bool gc_ran = false;
     bool compacted = false;
+    uint32_t seq = 0;
+    volatile uint32_t* h_flag = nullptr;
+    uint32_t recorded = 0;  // phases whose events were recorded (bit per Phase)
     bool any_report = false;
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
@@ -260,6 +267,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(seg_endins, W + 1);
     TAKE(seg_vend, 8 * (W + 1));
     TAKE(verdict, T);
+    TAKE(epi_done, 64);
 #undef TAKE
     w.edge_cap = edge_cap;
     w.cap_T = T;
@@ -275,6 +283,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), cs->stream));
+    HIPOK(hipMemsetAsync(w.epi_done, 0, 64, cs->stream));
     return ensure_scan_arena(cs);
 }
 
@@ -516,11 +525,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
         delete cs;
         return FDBCS_E_DEVICE;
     }
-    if (hipStreamCreateWithFlags(&cs->side, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipStreamDestroy(cs->stream);
-        delete cs;
-        return FDBCS_E_DEVICE;
-    }
+
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
@@ -552,9 +557,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     for (auto& x : cs->cws) x.release();
     for (auto& x : cs->ws) x.release();
     cs->scal.release();
-    if (cs->side) (void)hipStreamSynchronize(cs->side);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
-    if (cs->side) (void)hipStreamDestroy(cs->side);
     delete cs;
 }
 
@@ -600,6 +603,12 @@ int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes
 int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every) {
     if (!cs || every < 0) return FDBCS_E_INVALID;
     cs->gc_interval = every;
+    return FDBCS_OK;
+}
+
+int fdbcs_set_timing(fdbcs_conflict_set* cs, int32_t level) {
+    if (!cs || level < 0 || level > 2) return FDBCS_E_INVALID;
+    cs->timing = level;
     return FDBCS_OK;
 }
 
@@ -828,27 +837,45 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail.size() + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
-    // results staging: verdicts + scalars (one D2H) | rconf | hist | first_conf
+    // results (host-mapped, written by the epilogue): verdicts | scalars | completion flag, then the
+    // report copies rconf | hist | first_conf
     const size_t o_sc = (size_t)verdict_scalars_offset(T);
-    const size_t o_rc = align_up(o_sc + sizeof(Scalars), 64);
+    const size_t o_fl = align_up(o_sc + sizeof(Scalars), 64);
+    const size_t o_rc = o_fl + 64;
     const size_t o_hc = align_up(o_rc + R + 1, 64);
     const size_t o_fc = align_up(o_hc + T + 1, 64);
     const size_t out_bytes = o_fc + 4 * (T + 1);
-    if ((rc = b->pin_out.ensure(out_bytes))) return rc;
+    if ((rc = b->pin_out.ensure(out_bytes, true))) return rc;
     char* ho = (char*)b->pin_out.p;
     b->h_verdict = (uint8_t*)ho;
     b->h_scal = (Scalars*)(ho + o_sc);
+    b->h_flag = (volatile uint32_t*)(ho + o_fl);
     b->h_rconf = (uint8_t*)(ho + o_rc);
     b->h_hist = (uint8_t*)(ho + o_hc);
     b->h_first = (int32_t*)(ho + o_fc);
-    if ((rc = b->dverdict.ensure(o_sc + sizeof(Scalars)))) return rc;
+    if ((rc = b->dverdict.ensure(T + 64))) return rc;
     b->any_report = false;
     for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
+    b->seq = ++cs->seq;
+    if (b->seq == 0) b->seq = ++cs->seq;  // 0 means "not done"
+    *b->h_flag = 0;
+    b->recorded = 0;
 
     hipStream_t s = cs->stream;
-    HIPOK(hipEventRecord(b->ev[kPhStart], s));
+    const int timing = cs->timing;
+    // phase events: level 2 records every phase, level 1 only the copy kernels (roofline)
+    auto rec = [&](int ph, int level) -> hipEvent_t {
+        if (timing < level) return nullptr;
+        b->recorded |= 1u << ph;
+        return b->ev[ph];
+    };
+    auto mark = [&](int ph) -> int {
+        if (hipEvent_t e = rec(ph, 2)) HIPOK(hipEventRecord(e, s));
+        return FDBCS_OK;
+    };
+    if ((rc = mark(kPhStart))) return rc;
     if (b->state == 0 && (rc = do_upload(b))) return rc;
-    HIPOK(hipEventRecord(b->ev[kPhUpload], s));
+    if ((rc = mark(kPhUpload))) return rc;
     const BatchDev& bd = b->bd;
     Work& w = cs->work;
     Scalars* sc = (Scalars*)cs->scal.p;
@@ -857,19 +884,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->nd, kHole};
     uint8_t* htail = (uint8_t*)cs->htail.p;
 
-    // D.CheckRead on the side stream, overlapping D.Sort and the position scan (independent work;
-    // both are latency-bound and leave most of the chip idle); joined before the first consumer.
-    HIPOK(hipEventRecord(b->ev[kPhFork], s));
-    HIPOK(hipStreamWaitEvent(cs->side, b->ev[kPhFork], 0));
-    HIPOK(hipEventRecord(b->ev[kPhCheckBegin], cs->side));
-    launch_check_reads(cs->side, bd, base, delta, htail, w);
-    HIPOK(hipEventRecord(b->ev[kPhCheck], cs->side));
+    // D.CheckRead rides in the same launch as the sort's sample ranking (independent workgroups)
+    launch_sample_check(s, bd, w, base, delta, htail, cs->bucket_target);
+    if ((rc = mark(kPhCheck))) return rc;
     int sorted = 0;
     launch_sort_points(s, bd, w, cs->bucket_target, &sorted);
-    HIPOK(hipEventRecord(b->ev[kPhSort], s));
+    if ((rc = mark(kPhSort))) return rc;
     launch_positions(s, bd, w, sorted);
     if (cs->validate) launch_validate_sort(s, bd, w, sorted, sc);
-    HIPOK(hipStreamWaitEvent(s, b->ev[kPhCheck], 0));
     launch_edges(s, bd, w, sc);
     launch_resolve(s, bd, w, sc, b->any_report);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf
@@ -877,13 +899,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
         HIPOK(hipMemcpyAsync(b->h_first, w.first_conf, 4 * T, hipMemcpyDeviceToHost, s));
     }
-    HIPOK(hipEventRecord(b->ev[kPhIntra], s));
+    if ((rc = mark(kPhIntra))) return rc;
     launch_combine(s, bd, w, sc);
-    HIPOK(hipEventRecord(b->ev[kPhCombine], s));
+    if ((rc = mark(kPhCombine))) return rc;
     // D.MergeWrite into the delta tier
-    launch_merge(s, bd, w, delta.h, delta_of(cs, dsrc ^ 1), htail, sc, now, (int64_t*)cs->dlvl[3].p,
-                 cs->dlvl3_n, cs->nd_ub + 1, b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
-    HIPOK(hipEventRecord(b->ev[kPhMerge], s));
+    launch_merge(s, bd, w, delta.h, delta_of(cs, dsrc ^ 1), htail, sc, now, (int64_t*)cs->dlvl[3].p, cs->dlvl3_n,
+                 cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1));
+    if ((rc = mark(kPhMerge))) return rc;
     const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
@@ -896,31 +918,29 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const int64_t base_hint = cs->n_ub + nd_after + 1;
     if (compact) {
         launch_compact(s, w, base.h, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc, cs->header_version,
-                       (int64_t*)cs->lvl[3].p, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, b->ev[kPhCompBegin],
-                       b->ev[kPhCompEnd]);
+                       (int64_t*)cs->lvl[3].p, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
+                       rec(kPhCompEnd, 1));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
         gc = new_oldest > cs->gc_applied;
-    } else {
-        HIPOK(hipEventRecord(b->ev[kPhCompEnd], s));
     }
-    HIPOK(hipEventRecord(b->ev[kPhCompact], s));
+    if ((rc = mark(kPhCompact))) return rc;
     if (gc) {
         launch_gc(s, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), sc, new_oldest, cs->header_version,
                   base_hint);
         final_base ^= 1;
         cs->gc_applied = new_oldest;
     }
-    HIPOK(hipEventRecord(b->ev[kPhGc], s));
+    if ((rc = mark(kPhGc))) return rc;
     b->gc_ran = gc;
     b->compacted = compact;
+    char* hd = (char*)b->pin_out.dp;
     launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
-                    gc ? 1 : 0, (uint8_t*)b->dverdict.p, compact ? base_hint : nd_after + 1);
-    HIPOK(hipEventRecord(b->ev[kPhEpilogue], s));
+                    gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)b->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
+                    compact ? base_hint : nd_after + 1);
+    if ((rc = mark(kPhEpilogue))) return rc;
     HIPOK(hipGetLastError());
-    // results back: verdicts and the scalars right behind them, one copy
-    HIPOK(hipMemcpyAsync(b->pin_out.p, b->dverdict.p, o_sc + sizeof(Scalars), hipMemcpyDeviceToHost, s));
-    HIPOK(hipEventRecord(b->ev[kPhEnd], s));
+    if ((rc = mark(kPhEnd))) return rc;
     cs->cur = final_base;
     cs->dcur = dnew;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
@@ -942,7 +962,21 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
     fdbcs_conflict_set* cs = b->cs;
     if (b->state == 2) {
         HIPOK(hipSetDevice(cs->device));
-        HIPOK(hipEventSynchronize(b->ev[kPhEnd]));
+        // the epilogue's last workgroup publishes b->seq; poll it (checking the stream for errors)
+        for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
+            if ((spin & 1023) == 1023) {
+                const hipError_t e = hipStreamQuery(cs->stream);
+                if (e != hipSuccess && e != hipErrorNotReady) {
+                    fprintf(stderr, "fdbcs: stream error while waiting: %s\n", hipGetErrorString(e));
+                    return FDBCS_E_DEVICE;
+                }
+                if (e == hipSuccess && *b->h_flag != b->seq) {
+                    fprintf(stderr, "fdbcs: stream idle but batch %u not completed\n", b->seq);
+                    return FDBCS_E_DEVICE;
+                }
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
         if (b->h_scal->debug_error) {
             fprintf(stderr, "fdbcs: device invariant check failed (debug_error=%d)\n", b->h_scal->debug_error);
             cs->inflight--;
@@ -980,23 +1014,32 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         st.transactions += T;
         st.read_ranges += b->R();
         st.write_ranges += b->W();
-        st.ms_upload += ev_ms(b->ev[kPhStart], b->ev[kPhUpload]);
-        st.ms_check_read += ev_ms(b->ev[kPhCheckBegin], b->ev[kPhCheck]);  // concurrent with the sort
-        st.ms_sort += ev_ms(b->ev[kPhUpload], b->ev[kPhSort]);
-        st.ms_intra += ev_ms(b->ev[kPhSort], b->ev[kPhIntra]);
-        st.ms_combine += ev_ms(b->ev[kPhIntra], b->ev[kPhCombine]);
-        st.ms_merge += ev_ms(b->ev[kPhCombine], b->ev[kPhMerge]);
-        st.ms_compact += ev_ms(b->ev[kPhMerge], b->ev[kPhCompact]);
-        st.ms_gc += ev_ms(b->ev[kPhCompact], b->ev[kPhGc]);
-        st.ms_epilogue += ev_ms(b->ev[kPhGc], b->ev[kPhEpilogue]);
-        st.ms_total += ev_ms(b->ev[kPhUpload], b->ev[kPhEnd]);
+        // timing events may trail the completion flag: wait for the last one recorded
+        for (int e : {(int)kPhEnd, (int)kPhCompEnd, (int)kPhCopyEnd})
+            if ((b->recorded >> e) & 1u) {
+                HIPOK(hipEventSynchronize(b->ev[e]));
+                break;
+            }
+        auto ph = [&](int a, int z) {
+            return ((b->recorded >> a) & (b->recorded >> z) & 1u) ? ev_ms(b->ev[a], b->ev[z]) : 0.0;
+        };
+        st.ms_upload += ph(kPhStart, kPhUpload);
+        st.ms_check_read += ph(kPhUpload, kPhCheck);  // includes the sort's sample ranking (same launch)
+        st.ms_sort += ph(kPhCheck, kPhSort);
+        st.ms_intra += ph(kPhSort, kPhIntra);
+        st.ms_combine += ph(kPhIntra, kPhCombine);
+        st.ms_merge += ph(kPhCombine, kPhMerge);
+        st.ms_compact += ph(kPhMerge, kPhCompact);
+        st.ms_gc += ph(kPhCompact, kPhGc);
+        st.ms_epilogue += ph(kPhGc, kPhEpilogue);
+        st.ms_total += ph(kPhUpload, kPhEnd);
         // copy kernels: each reads every old boundary of its tier (32 B) and writes the kept ones
-        st.ms_merge_kernel += ev_ms(b->ev[kPhCopyBegin], b->ev[kPhCopyEnd]);
+        st.ms_merge_kernel += ph(kPhCopyBegin, kPhCopyEnd);
         st.merge_launches += 1;
         st.merge_bytes += 32 * (2 * b->h_scal->d_before - b->h_scal->d_rem);
         if (b->compacted) {
             st.compactions += 1;
-            st.ms_compact_kernel += ev_ms(b->ev[kPhCompBegin], b->ev[kPhCompEnd]);
+            st.ms_compact_kernel += ph(kPhCompBegin, kPhCompEnd);
             st.compact_bytes += 32 * (2 * b->h_scal->c_before - b->h_scal->c_rem);
         }
         cs->inflight--;

@@ -143,6 +143,7 @@ struct Work {
     // compaction: one entry per delta boundary (sized by the delta capacity)
     int64_t *c_lo, *c_hi, *c_rem, *c_ins, *c_val;
     uint8_t* c_exact;
+    int32_t* epi_done;     // epilogue workgroups finished (self-resetting)
 };
 
 // Byte offset of the Scalars copy that follows the verdicts in a batch's result buffer.
@@ -156,8 +157,9 @@ struct Tier {
     const int64_t* n;  // device size
     int64_t hdr;       // version below the first boundary (kHole for the delta)
 };
-void launch_check_reads(hipStream_t s, const BatchDev& b, const Tier& base, const Tier& delta, const uint8_t* htail,
-                        const Work& w);
+// Sample ranking for the sort's splitters and D.CheckRead in one launch (independent roles).
+void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
+                         const uint8_t* htail, int bucket_target);
 // bucket_target: endpoints per sample-sort bucket (0 = default 256; tests force oversized buckets).
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
@@ -182,7 +184,9 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
                      int64_t grid_hint_n);
 // Verdicts, scalar roll-over, scratch zeroing and the range-max levels of the tier that changed
 // (the base after a compaction, else the delta).
+// verdict_out / flag are host-mapped: the host waits for *flag == seq instead of an event.
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
-                     int compacted, int gc_ran, uint8_t* verdict_out, int64_t grid_hint_n);
+                     int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
+                     uint32_t seq, int64_t grid_hint_n);
 
 }  // namespace fdbcs

@@ -191,10 +191,8 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
 // >= the base versions it covers (versions only grow), so the max over the overlay equals the max
 // of the two tiers' maxima, and holes (kHole) never conflict.  The four searches (begin and end
 // key in both tiers) run in lockstep.
-__global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Tier base, Tier delta, const uint8_t* htail,
-                                                        uint8_t* hist_conf, uint8_t* rconf) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= b.R) return;
+__device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, const Tier& delta,
+                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int r) {
     const int t = b.rowner[r];
     const int64_t snap = b.snap[t];
     const DKey kb = b.keys[2 * r], ke = b.keys[2 * r + 1];
@@ -210,13 +208,6 @@ __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, Tier base, T
     if (!conf && nd > 0) conf = tier_conflict(delta.h, delta.m, kHole, lo[2], eq[2], lo[3], degenerate, snap);
     rconf[r] = conf ? 1 : 0;
     if (conf) hist_conf[t] = 1;
-}
-
-void launch_check_reads(hipStream_t s, const BatchDev& b, const Tier& base, const Tier& delta, const uint8_t* htail,
-                        const Work& w) {
-    if (b.R == 0) return;
-    hipLaunchKernelGGL(k_check_reads, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, base, delta, htail,
-                       w.hist_conf, w.rconf);
 }
 
 // ------------------------------------------------------------------ D.Sort
@@ -341,36 +332,54 @@ constexpr int kBucketTarget = 256;
 
 __device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((int64_t)i * E) / S); }
 
-__global__ __launch_bounds__(kBlock) void k_sample_rank(BatchDev b, int S, int nb, int32_t* srank, SortItem* splitters,
-                                                        const uint8_t* arena) {
+// One launch, two independent roles (no stream fork/join needed for the overlap):
+//  * workgroups [0, n_sample_wg): sample ranking -- workgroup (x, y) ranks samples
+//    [y*256, y*256+256) against the slice [x*64, x*64+64); partial ranks are added atomically and the
+//    last of these workgroups writes the nb-1 splitters (the samples of rank k*S/nb);
+//  * workgroups after them: D.CheckRead, one thread per read range.
+struct SampleCheck {
+    int S, nb, n_sample_wg, n_slice;
+    int32_t* srank;  // [S] partial ranks, [kMaxSample] done counter
+    SortItem* splitters;
+    Tier base, delta;
+    const uint8_t* htail;
+    uint8_t *hist_conf, *rconf;
+};
+
+__global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck c) {
     __shared__ SortItem sl[kSampleSlice];
     __shared__ int s_last;
-    const int E = 2 * (b.R + b.W);
-    // workgroup (x, y): samples [y*256, y*256+256) against the slice [x*64, x*64+64)
-    const int j0 = blockIdx.x * kSampleSlice;
+    if ((int)blockIdx.x >= c.n_sample_wg) {
+        const int r = (blockIdx.x - c.n_sample_wg) * blockDim.x + threadIdx.x;
+        if (r < b.R) check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, r);
+        return;
+    }
+    const int E = 2 * (b.R + b.W), S = c.S, nb = c.nb;
+    const int x = blockIdx.x % c.n_slice, y = blockIdx.x / c.n_slice;
+    const int j0 = x * kSampleSlice;
     const int cj = min(kSampleSlice, S - j0);
     for (int t = threadIdx.x; t < cj; t += blockDim.x) sl[t] = make_item(b, sample_pos(j0 + t, E, S));
     __syncthreads();
-    const int i = blockIdx.y * blockDim.x + threadIdx.x;
+    const int i = y * blockDim.x + threadIdx.x;
     if (i < S) {
         SortItem mine[1] = {make_item(b, sample_pos(i, E, S))};
-        int c[1] = {0};
+        int cnt[1] = {0};
         bool tail = false;
-        rank_count<1>(sl, cj, mine, c, tail);
-        if (tail) c[0] = rank_exact(sl, cj, mine[0], arena);
-        if (c[0]) atomicAdd(&srank[i], c[0]);
+        rank_count<1>(sl, cj, mine, cnt, tail);
+        if (tail) cnt[0] = rank_exact(sl, cj, mine[0], b.tail);
+        if (cnt[0]) atomicAdd(&c.srank[i], cnt[0]);
     }
-    // the last workgroup to finish sees every partial rank and writes the splitters
+    // the last sampling workgroup to finish sees every partial rank and writes the splitters
     __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&srank[kMaxSample], 1) == (int)(gridDim.x * gridDim.y) - 1;
+    if (threadIdx.x == 0) s_last = atomicAdd(&c.srank[kMaxSample], 1) == c.n_sample_wg - 1;
     __syncthreads();
     if (!s_last) return;
     __threadfence();
     for (int q = threadIdx.x; q < S; q += blockDim.x) {
-        const int r = __hip_atomic_load(&srank[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int r = __hip_atomic_load(&c.srank[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int k = (int)(((int64_t)r * nb + S - 1) / S);  // the splitter index whose rank would be r
-        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) splitters[k - 1] = make_item(b, sample_pos(q, E, S));
+        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) c.splitters[k - 1] = make_item(b, sample_pos(q, E, S));
     }
 }
 
@@ -546,18 +555,36 @@ int sort_buckets(int E, int target) {
     return nb > kMaxBuckets ? kMaxBuckets : nb;
 }
 
+void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
+                         const uint8_t* htail, int bucket_target) {
+    const int E = 2 * (b.R + b.W);
+    const int nb = E ? sort_buckets(E, bucket_target) : 1;
+    SampleCheck c{};
+    if (nb > 1) {
+        int S = 4 * nb;
+        S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
+        S = S > E ? E : S;
+        c.S = S;
+        c.nb = nb;
+        c.n_slice = (S + kSampleSlice - 1) / kSampleSlice;
+        c.n_sample_wg = c.n_slice * ((S + kBlock - 1) / kBlock);
+    }
+    c.srank = w.srank;
+    c.splitters = w.splitters;
+    c.base = base;
+    c.delta = delta;
+    c.htail = htail;
+    c.hist_conf = w.hist_conf;
+    c.rconf = w.rconf;
+    const int grid = c.n_sample_wg + (b.R + kBlock - 1) / kBlock;
+    if (grid > 0) hipLaunchKernelGGL(k_sample_check, dim3(grid), dim3(kBlock), 0, s, b, c);
+}
+
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int* result_buffer) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
     const int nb = sort_buckets(E, bucket_target);
-    if (nb > 1) {
-        int S = 4 * nb;
-        S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
-        S = S > E ? E : S;
-        hipLaunchKernelGGL(k_sample_rank, dim3((S + kSampleSlice - 1) / kSampleSlice, (S + kBlock - 1) / kBlock),
-                           dim3(kBlock), 0, s, b, S, nb, w.srank, w.splitters, b.tail);
-    }
     const int grid = (E + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.splitters, nb, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
@@ -1311,7 +1338,11 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
 struct Epilogue {
     const uint8_t* flags;
     const uint8_t* status;
-    uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T)
+    uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T) (host-mapped)
+    uint8_t* verdict_dev;  // [T] device copy of the verdicts (on-device combine)
+    int32_t* done;         // workgroups finished (reset by the last)
+    uint32_t* flag;        // host-mapped completion word, set to `seq` last
+    uint32_t seq;
     int32_t T;
     int compacted, gc_ran;
     uint8_t* zero8;  // hist_conf
@@ -1378,6 +1409,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         else
             v = ep.status[t] == kCommitted ? 2 : 0;
         ep.verdict_out[t] = v;
+        ep.verdict_dev[t] = v;
     }
     if (tid == 0) {
         if (ep.compacted) {
@@ -1401,6 +1433,14 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         ep.zero_bk[i] = 0;
     }
     for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
+    // completion: the last workgroup publishes the batch's sequence number to the host
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(ep.done, 1) == (int)gridDim.x - 1) {
+        *ep.done = 0;
+        __threadfence_system();
+        __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
@@ -1423,8 +1463,13 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 }
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
-                     int compacted, int gc_ran, uint8_t* verdict_out, int64_t grid_hint_n) {
+                     int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
+                     uint32_t seq, int64_t grid_hint_n) {
     Epilogue ep;
+    ep.verdict_dev = verdict_dev;
+    ep.done = w.epi_done;
+    ep.flag = flag;
+    ep.seq = seq;
     ep.flags = b.flags;
     ep.status = w.status;
     ep.verdict_out = verdict_out;

@@ -74,7 +74,7 @@ typedef struct fdbcs_packed_batch {
     const int64_t* key_offsets;             /* [2*(R+W)+1] */
 } fdbcs_packed_batch;
 
-/* Per-phase device time (HIP events on the engine's stream), accumulated
+/* Per-phase device time (HIP events on the engine's stream, see fdbcs_set_timing), accumulated
  * since the last reset.  Phase names mirror the reference PerfDoubleCounters
  * D.CheckRead / D.Sort / D.CheckIntraBatch / D.Combine / D.MergeWrite /
  * D.RemoveBefore (SkipList.cpp:49-51). */
@@ -134,6 +134,10 @@ int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes
  * verdict-neutral: they only trade memory for speed. */
 int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every);
 int fdbcs_set_delta_limit(fdbcs_conflict_set* cs, int64_t boundaries);
+/* Device timing of the pipeline (HIP events; each recorded event costs a few microseconds of
+ * queue time, so production runs keep them off): 0 = none (default), 1 = the two history copy
+ * kernels only (fills ms_merge_kernel / ms_compact_kernel), 2 = every phase of fdbcs_stats. */
+int fdbcs_set_timing(fdbcs_conflict_set* cs, int32_t level);
 
 /* ConflictBatch(cs, conflictingKeyRangeMap, arena) — SkipList.cpp:749-752.
  * report_keys != 0 enables conflictingKeyRangeMap collection for transactions
