@@ -104,7 +104,7 @@ struct fdbcs_conflict_set {
 
     // base tier: two buffer sets (ping-pong) + range-max levels
     DBuf hkey[2], hlt[2], hver[2];
-    DBuf lvl[kMaxLevels];  // lvl[0] unused (aliases hver[cur])
+    DBuf lvl[kMaxLevels];  // lvl[0]: sampled key index (the level-0 versions are hver[cur])
     int cur = 0;
     int64_t hist_cap = 0;  // elements per buffer set
     int64_t n_ub = 0;      // upper bound of live base boundaries (exact after a wait)
@@ -267,7 +267,6 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(seg_endins, W + 1);
     TAKE(seg_vend, 8 * (W + 1));
     TAKE(verdict, T);
-    TAKE(epi_done, 64);
 #undef TAKE
     w.edge_cap = edge_cap;
     w.cap_T = T;
@@ -283,7 +282,6 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), cs->stream));
-    HIPOK(hipMemsetAsync(w.epi_done, 0, 64, cs->stream));
     return ensure_scan_arena(cs);
 }
 
@@ -307,6 +305,8 @@ MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     MaxLevels m;
     m.lvl[0] = (int64_t*)cs->hver[k].p;
     for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->lvl[L].p;
+    m.keys = (const ulonglong2*)cs->hkey[k].p;
+    m.skey = (ulonglong2*)cs->lvl[0].p;
     return m;
 }
 
@@ -322,6 +322,8 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     MaxLevels m;
     m.lvl[0] = (int64_t*)cs->dver[k].p;
     for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->dlvl[L].p;
+    m.keys = (const ulonglong2*)cs->dkey[k].p;
+    m.skey = (ulonglong2*)cs->dlvl[0].p;
     return m;
 }
 
@@ -336,8 +338,11 @@ int sync_sizes(fdbcs_conflict_set* cs) {
     return FDBCS_OK;
 }
 
-// Range-max hierarchy buffers for `cap` elements; returns the top level's length.
+// Range-max hierarchy buffers (and the sampled key index in lv[0]) for `cap` elements; returns the
+// top level's length.
 int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n) {
+    lv[0].release();
+    if (int rc = lv[0].ensure(16 * (cap / kFan + 2))) return rc;
     int64_t m = cap;
     for (int L = 1; L < kMaxLevels; L++) {
         m = (m + kFan - 1) / kFan + 1;
@@ -903,8 +908,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_combine(s, bd, w, sc);
     if ((rc = mark(kPhCombine))) return rc;
     // D.MergeWrite into the delta tier
-    launch_merge(s, bd, w, delta.h, delta_of(cs, dsrc ^ 1), htail, sc, now, (int64_t*)cs->dlvl[3].p, cs->dlvl3_n,
-                 cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1));
+    launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
+                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1));
     if ((rc = mark(kPhMerge))) return rc;
     const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
@@ -917,8 +922,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     int final_base = bsrc;
     const int64_t base_hint = cs->n_ub + nd_after + 1;
     if (compact) {
-        launch_compact(s, w, base.h, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc, cs->header_version,
-                       (int64_t*)cs->lvl[3].p, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
+        launch_compact(s, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
+                       cs->header_version, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
                        rec(kPhCompEnd, 1));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;

@@ -33,8 +33,13 @@ struct Hist {
 };
 
 // Range-max hierarchy over the current history's versions.
+// Range-max hierarchy over a tier's versions, and its sampled key index: skey[j] = prefix of
+// boundary 64*j, so a search narrows to one 64-boundary block through a small (cache-resident)
+// array before touching the boundary keys.
 struct MaxLevels {
     int64_t* lvl[kMaxLevels];  // lvl[0] == current Hist::ver
+    const ulonglong2* keys;    // the tier's keys (source of the samples)
+    ulonglong2* skey;          // [ceil(n / 64)]
 };
 
 // Device-side scalars of a conflict set (one allocation).  The history has two tiers: the base
@@ -143,7 +148,6 @@ struct Work {
     // compaction: one entry per delta boundary (sized by the delta capacity)
     int64_t *c_lo, *c_hi, *c_rem, *c_ins, *c_val;
     uint8_t* c_exact;
-    int32_t* epi_done;     // epilogue workgroups finished (self-resetting)
 };
 
 // Byte offset of the Scalars copy that follows the verdicts in a batch's result buffer.
@@ -168,12 +172,14 @@ void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, bool report);
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
-void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
-                  Scalars* sc, int64_t now, int64_t* lvl3, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end);
+// `srcm` are the source tier's levels: its key index is searched, its top level reset for the
+// epilogue's rebuild.
+void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
+                  const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
+                  hipEvent_t copy_begin, hipEvent_t copy_end);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
-void launch_compact(hipStream_t s, const Work& w, const Hist& base, const Hist& delta, const Hist& dst,
-                    const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t* lvl3, int64_t lvl3_n,
+void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
+                    const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end);
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
                int64_t header_version, int64_t grid_hint_n);

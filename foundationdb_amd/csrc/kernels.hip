@@ -88,6 +88,56 @@ __device__ __forceinline__ void multi_lower_bound(const Hist (&h)[Q], int64_t (&
     }
 }
 
+// Narrow Q searches through the tiers' sampled key indexes (skey[j] = prefix of boundary 64*j,
+// ns = ceil(n / 64) samples): with a = #samples whose prefix is < q's and b = #samples whose prefix
+// is <= q's, lower_bound(q) lies in [64(a-1)+1, min(n, 64b)] -- one 64-boundary block unless
+// several samples share q's 16-byte prefix.  Queries with lo >= hi are left alone.
+template <int Q>
+__device__ __forceinline__ void multi_narrow(const MaxLevels (&m)[Q], const int64_t (&n)[Q], const DKey (&q)[Q],
+                                             int64_t (&lo)[Q], int64_t (&hi)[Q]) {
+    int64_t l[Q], h[Q], ns[Q];
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+        ns[i] = (n[i] + kFan - 1) / kFan;
+        l[i] = 0;
+        h[i] = lo[i] < hi[i] ? ns[i] : 0;
+    }
+    for (;;) {
+        bool any = false;
+        int64_t mid[Q];
+        ulonglong2 k[Q];
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            mid[i] = (l[i] + h[i]) >> 1;
+            if (l[i] < h[i]) {
+                k[i] = m[i].skey[mid[i]];
+                any = true;
+            }
+        }
+        if (!any) break;
+#pragma unroll
+        for (int i = 0; i < Q; i++) {
+            if (l[i] < h[i]) {
+                const bool less = k[i].x < q[i].hi || (k[i].x == q[i].hi && k[i].y < q[i].lo);
+                if (less)
+                    l[i] = mid[i] + 1;
+                else
+                    h[i] = mid[i];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < Q; i++) {
+        if (lo[i] < hi[i]) {
+            const int64_t a = l[i];
+            int64_t b = a;
+            while (b < ns[i] && m[i].skey[b].x == q[i].hi && m[i].skey[b].y == q[i].lo) b++;  // shared prefixes
+            lo[i] = a > 0 ? kFan * (a - 1) + 1 : 0;
+            hi[i] = min(n[i], kFan * b);
+        }
+    }
+}
+
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
 __device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
     int64_t best = LLONG_MIN;
@@ -199,10 +249,13 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
     const int64_t nb = *base.n, nd = *delta.n;
     const Hist h[4] = {base.h, base.h, delta.h, delta.h};
+    const MaxLevels m[4] = {base.m, base.m, delta.m, delta.m};
+    const int64_t n[4] = {nb, nb, nd, nd};
     const DKey q[4] = {kb, ke, kb, ke};
     int64_t lo[4] = {0, 0, 0, 0};
     int64_t hi[4] = {nb, degenerate ? 0 : nb, nd, degenerate ? 0 : nd};
     bool eq[4];
+    multi_narrow<4>(m, n, q, lo, hi);
     multi_lower_bound<4>(h, lo, hi, eq, htail, q, b.tail);
     bool conf = tier_conflict(base.h, base.m, base.hdr, lo[0], eq[0], lo[1], degenerate, snap);
     if (!conf && nd > 0) conf = tier_conflict(delta.h, delta.m, kHole, lo[2], eq[2], lo[3], degenerate, snap);
@@ -939,9 +992,9 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
     return b.keys[2 * g + end];
 }
 
-__global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, const uint8_t* htail,
-                                                       const Scalars* sc, const int64_t* n_in, int64_t* lvl3,
-                                                       int64_t lvl3_n) {
+__global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, MaxLevels hm,
+                                                       const uint8_t* htail, const Scalars* sc, const int64_t* n_in,
+                                                       int64_t* lvl3, int64_t lvl3_n) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     // the history check of this batch is done with the old hierarchy: reset its top level for the
     // epilogue's atomicMax build
@@ -952,9 +1005,12 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     const DKey kb = seg_key(b, w, w.seg_b[s], 0);
     const DKey ke = seg_key(b, w, w.seg_e[s], 1);
     const Hist hh[2] = {h, h};
+    const MaxLevels mm[2] = {hm, hm};
+    const int64_t nn[2] = {n, n};
     const DKey q[2] = {kb, ke};
     int64_t l[2] = {0, 0}, u[2] = {n, n};
     bool eq[2];
+    multi_narrow<2>(mm, nn, q, l, u);
     multi_lower_bound<2>(hh, l, u, eq, htail, q, b.tail);
     const int64_t lo = l[0], hi = l[1];
     const bool exact = eq[1];
@@ -1160,12 +1216,12 @@ static unsigned copy_tiles(int64_t grid_hint_n, int tile) {
     return (unsigned)tiles;
 }
 
-void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const Hist& dst, uint8_t* htail,
-                  Scalars* sc, int64_t now, int64_t* lvl3, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end) {
+void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
+                  const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
+                  hipEvent_t copy_begin, hipEvent_t copy_end) {
     const int Wn = b.W > 0 ? b.W : 1;
-    hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, htail, sc,
-                       &sc->nd, lvl3, lvl3_n);
+    hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm, htail, sc,
+                       &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
                    w.scan[kScanSegSum]);
@@ -1184,9 +1240,10 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
 // of an earlier merge and becomes a real boundary carrying the base version at d_j, unless the
 // base already has a boundary at d_j.  The result is the boundary set the reference would hold.
 
-__global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, Hist delta, const uint8_t* htail,
-                                                           const int64_t* nb_ptr, const int64_t* nd_ptr, int64_t hdr,
-                                                           Work w, int64_t* lvl3, int64_t lvl3_n) {
+__global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels basem, Hist delta,
+                                                           const uint8_t* htail, const int64_t* nb_ptr,
+                                                           const int64_t* nd_ptr, int64_t hdr, Work w, int64_t* lvl3,
+                                                           int64_t lvl3_n) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = j; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
     const int64_t nd = *nd_ptr;
@@ -1200,9 +1257,12 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, Hist delta
     q.len = lt.x;
     q.tail = lt.y;
     const Hist hh[1] = {base};
+    const MaxLevels mm[1] = {basem};
+    const int64_t nn[1] = {nb};
     const DKey qq[1] = {q};
     int64_t l[1] = {0}, u[1] = {nb};
     bool eq[1];
+    multi_narrow<1>(mm, nn, qq, l, u);
     multi_lower_bound<1>(hh, l, u, eq, htail, qq, htail);
     const int64_t lo = l[0];
     const bool exact = eq[0];
@@ -1256,13 +1316,13 @@ struct CompactIns {
     }
 };
 
-void launch_compact(hipStream_t s, const Work& w, const Hist& base, const Hist& delta, const Hist& dst,
-                    const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t* lvl3, int64_t lvl3_n,
+void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
+                    const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end) {
     int64_t blocks = (delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, delta, htail, &sc->n,
-                       &sc->nd_next, header_version, w, lvl3, lvl3_n);
+    hipLaunchKernelGGL(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
+                       &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n);
     const Segs g{w.c_lo, w.c_hi, w.c_rem, w.c_ins, w.tile_first};
     const TierIO io{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem};
     launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
@@ -1340,7 +1400,6 @@ struct Epilogue {
     const uint8_t* status;
     uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T) (host-mapped)
     uint8_t* verdict_dev;  // [T] device copy of the verdicts (on-device combine)
-    int32_t* done;         // workgroups finished (reset by the last)
     uint32_t* flag;        // host-mapped completion word, set to `seq` last
     uint32_t seq;
     int32_t T;
@@ -1382,7 +1441,10 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
                 v = y > v ? y : v;
             }
             if (lane == 0) {
-                if (b1 < n1) m.lvl[1][b1] = v;
+                if (b1 < n1) {
+                    m.lvl[1][b1] = v;
+                    m.skey[b1] = m.keys[b1 * kFan];  // sampled key index
+                }
                 l1[wid * (kFan / 4) + q] = v;
             }
         }
@@ -1402,26 +1464,11 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     }
     if (!ep.verdict_out) return;
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t = tid; t < ep.T; t += stride) {
-        uint8_t v;
-        if (ep.flags[t] & kFlagTooOld)
-            v = 1;  // TransactionTooOld (ConflictSet.h:42)
-        else
-            v = ep.status[t] == kCommitted ? 2 : 0;
-        ep.verdict_out[t] = v;
-        ep.verdict_dev[t] = v;
-    }
-    if (tid == 0) {
-        if (ep.compacted) {
-            sc->n = ep.gc_ran ? sc->n_gc : sc->n_next;
-            sc->nd = 0;
-        } else {
-            sc->nd = sc->nd_next;
-        }
-        sc->tail_used = sc->tail_next;
-        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = *sc;
-        sc->debug_error = 0;
-    }
+    auto verdict = [&](int64_t t) -> uint8_t {
+        if (ep.flags[t] & kFlagTooOld) return 1;  // TransactionTooOld (ConflictSet.h:42)
+        return ep.status[t] == kCommitted ? 2 : 0;
+    };
+    for (int64_t t = tid; t < ep.T; t += stride) ep.verdict_dev[t] = verdict(t);
     for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
     for (int64_t i = tid; i < ep.zero32_n; i += stride) {
         ep.zero32a[i] = 0;
@@ -1433,14 +1480,37 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         ep.zero_bk[i] = 0;
     }
     for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
-    // completion: the last workgroup publishes the batch's sequence number to the host
+    if (blockIdx.x != 0) return;
+    // Workgroup 0 writes what the host reads (host-mapped, 16 verdicts per store), then publishes
+    // the batch's sequence number; everything else this launch writes is read only by later
+    // kernels on the same stream.
+    for (int64_t q = threadIdx.x; q * 16 < ep.T; q += blockDim.x) {
+        uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int64_t t = q * 16 + k;
+            if (t < ep.T) wv[k >> 2] |= (uint32_t)verdict(t) << (8 * (k & 3));
+        }
+        if (q * 16 + 16 <= ep.T) {
+            *reinterpret_cast<uint4*>(ep.verdict_out + q * 16) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        } else {
+            for (int k = 0; q * 16 + k < ep.T; k++) ep.verdict_out[q * 16 + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (ep.compacted) {
+            sc->n = ep.gc_ran ? sc->n_gc : sc->n_next;
+            sc->nd = 0;
+        } else {
+            sc->nd = sc->nd_next;
+        }
+        sc->tail_used = sc->tail_next;
+        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = *sc;
+        sc->debug_error = 0;
+    }
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(ep.done, 1) == (int)gridDim.x - 1) {
-        *ep.done = 0;
-        __threadfence_system();
-        __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (threadIdx.x == 0) __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
@@ -1467,7 +1537,6 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
                      uint32_t seq, int64_t grid_hint_n) {
     Epilogue ep;
     ep.verdict_dev = verdict_dev;
-    ep.done = w.epi_done;
     ep.flag = flag;
     ep.seq = seq;
     ep.flags = b.flags;
