@@ -130,6 +130,8 @@ struct fdbcs_conflict_set {
     int inflight = 0;
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
     int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket (testing knob; 0 = default)
+    bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
+    DBuf trace_buf;
     fdbcs_stats stats{};
 };
 
@@ -301,12 +303,26 @@ Hist hist_of(fdbcs_conflict_set* cs, int k) {
     return h;
 }
 
+// Search-tree levels laid out back to back in one allocation sized for `cap` boundaries.
+void carve_index(MaxLevels& m, ulonglong2* base, int64_t cap) {
+    for (int L = 0; L < kIdxLevels; L++) {
+        m.skey[L] = base;
+        base += idx_level_cap(cap, L);
+    }
+}
+
+int64_t index_bytes(int64_t cap) {
+    int64_t n = 0;
+    for (int L = 0; L < kIdxLevels; L++) n += idx_level_cap(cap, L);
+    return 16 * n;
+}
+
 MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     MaxLevels m;
     m.lvl[0] = (int64_t*)cs->hver[k].p;
     for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->lvl[L].p;
     m.keys = (const ulonglong2*)cs->hkey[k].p;
-    m.skey = (ulonglong2*)cs->lvl[0].p;
+    carve_index(m, (ulonglong2*)cs->lvl[0].p, cs->hist_cap);
     return m;
 }
 
@@ -323,7 +339,7 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     m.lvl[0] = (int64_t*)cs->dver[k].p;
     for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->dlvl[L].p;
     m.keys = (const ulonglong2*)cs->dkey[k].p;
-    m.skey = (ulonglong2*)cs->dlvl[0].p;
+    carve_index(m, (ulonglong2*)cs->dlvl[0].p, cs->delta_cap);
     return m;
 }
 
@@ -342,7 +358,7 @@ int sync_sizes(fdbcs_conflict_set* cs) {
 // top level's length.
 int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n) {
     lv[0].release();
-    if (int rc = lv[0].ensure(16 * (cap / kFan + 2))) return rc;
+    if (int rc = lv[0].ensure(index_bytes(cap))) return rc;
     int64_t m = cap;
     for (int L = 1; L < kMaxLevels; L++) {
         m = (m + kFan - 1) / kFan + 1;
@@ -526,6 +542,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     cs->device = device;
     if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
     if (const char* v = getenv("FDBCS_SORT_BUCKET")) cs->bucket_target = atoi(v);
+    if (const char* v = getenv("FDBCS_TRACE")) cs->trace = v[0] == '1';
     if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) {
         delete cs;
         return FDBCS_E_DEVICE;
@@ -536,6 +553,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
     if (!rc) rc = ensure_delta(cs, 1 << 14);
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
+    if (!rc && cs->trace) rc = cs->trace_buf.ensure(8 * kTrSlots);
     if (rc) {
         fdbcs_destroy_conflict_set(cs);
         return rc;
@@ -562,6 +580,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     for (auto& x : cs->cws) x.release();
     for (auto& x : cs->ws) x.release();
     cs->scal.release();
+    cs->trace_buf.release();
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -889,6 +908,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->nd, kHole};
     uint8_t* htail = (uint8_t*)cs->htail.p;
 
+    w.trace = cs->trace ? (unsigned long long*)cs->trace_buf.p : nullptr;
+    if (w.trace) {
+        unsigned long long init[kTrSlots];
+        for (int i = 0; i < kTrSlots; i++)
+            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin) ? ~0ull : 0ull;
+        HIPOK(hipMemcpyAsync(w.trace, init, sizeof(init), hipMemcpyHostToDevice, s));  // staged before return
+        HIPOK(hipStreamSynchronize(s));
+    }
     // D.CheckRead rides in the same launch as the sort's sample ranking (independent workgroups)
     launch_sample_check(s, bd, w, base, delta, htail, cs->bucket_target);
     if ((rc = mark(kPhCheck))) return rc;
@@ -982,6 +1009,19 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        if (cs->trace && cs->inflight == 1) {
+            HIPOK(hipStreamSynchronize(cs->stream));
+            unsigned long long tr[kTrSlots];
+            HIPOK(hipMemcpy(tr, cs->trace_buf.p, sizeof(tr), hipMemcpyDeviceToHost));
+            auto us = [&](int a, int z) { return (double)((long long)(tr[z] - tr[a])) / 100.0; };  // 100 MHz
+            fprintf(stderr,
+                    "fdbcs trace: sample %.2f us, check %.2f us (check starts %+.2f us after sample); epilogue "
+                    "levels %.2f, zero %.2f, host %.2f, fence %.2f us\n",
+                    us(kTrSampleBegin, kTrSampleEnd), us(kTrCheckBegin, kTrCheckEnd), us(kTrSampleBegin, kTrCheckBegin),
+                    us(kTrEpiBegin, kTrEpiLevels), us(kTrEpiLevels, kTrEpiZero), us(kTrEpiZero, kTrEpiHost),
+                    us(kTrEpiHost, kTrEpiFence));
+
+        }
         if (b->h_scal->debug_error) {
             fprintf(stderr, "fdbcs: device invariant check failed (debug_error=%d)\n", b->h_scal->debug_error);
             cs->inflight--;

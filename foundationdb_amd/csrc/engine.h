@@ -33,14 +33,20 @@ struct Hist {
 };
 
 // Range-max hierarchy over the current history's versions.
-// Range-max hierarchy over a tier's versions, and its sampled key index: skey[j] = prefix of
-// boundary 64*j, so a search narrows to one 64-boundary block through a small (cache-resident)
-// array before touching the boundary keys.
+// Range-max hierarchy over a tier's versions, and its static 16-ary search tree over sampled key
+// prefixes: skey[L][j] = prefix of boundary 64 * 16^L * j, so skey[L][j] == skey[L-1][16 j].  A
+// search descends the tree one 16-wide parallel probe per level and lands in one 64-boundary block.
+constexpr int kIdxLevels = 6;  // enough for 16 * 64 * 16^5 boundaries under a 16-entry top level
 struct MaxLevels {
-    int64_t* lvl[kMaxLevels];  // lvl[0] == current Hist::ver
-    const ulonglong2* keys;    // the tier's keys (source of the samples)
-    ulonglong2* skey;          // [ceil(n / 64)]
+    int64_t* lvl[kMaxLevels];       // lvl[0] == current Hist::ver
+    const ulonglong2* keys;         // the tier's keys (source of the samples)
+    ulonglong2* skey[kIdxLevels];   // [ceil(n / (64 * 16^L))]
 };
+__host__ __device__ inline int64_t idx_level_cap(int64_t cap, int L) {
+    int64_t d = 64;
+    for (int i = 0; i < L; i++) d *= 16;
+    return cap / d + 2;
+}
 
 // Device-side scalars of a conflict set (one allocation).  The history has two tiers: the base
 // (sorted boundaries, rewritten only by compaction) and the delta (this window's merges, versions
@@ -148,7 +154,21 @@ struct Work {
     // compaction: one entry per delta boundary (sized by the delta capacity)
     int64_t *c_lo, *c_hi, *c_rem, *c_ins, *c_val;
     uint8_t* c_exact;
+    unsigned long long* trace;  // [kTrSlots] or null
 };
+
+// FDBCS_TRACE: device timestamps (wall_clock64 ticks) of kernel sections, for tuning.
+enum TraceSlot {
+    kTrSampleBegin, kTrSampleEnd, kTrCheckBegin, kTrCheckEnd,
+    kTrEpiBegin, kTrEpiLevels, kTrEpiZero, kTrEpiHost, kTrEpiFence, kTrEpiEnd,
+    kTrSlots
+};
+__device__ __forceinline__ void trace_min(unsigned long long* tr, int slot) {
+    if (tr) atomicMin(&tr[slot], (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void trace_max(unsigned long long* tr, int slot) {
+    if (tr) atomicMax(&tr[slot], (unsigned long long)wall_clock64());
+}
 
 // Byte offset of the Scalars copy that follows the verdicts in a batch's result buffer.
 __host__ __device__ inline int64_t verdict_scalars_offset(int64_t T) { return (T + 64) / 64 * 64; }

@@ -88,54 +88,121 @@ __device__ __forceinline__ void multi_lower_bound(const Hist (&h)[Q], int64_t (&
     }
 }
 
-// Narrow Q searches through the tiers' sampled key indexes (skey[j] = prefix of boundary 64*j,
-// ns = ceil(n / 64) samples): with a = #samples whose prefix is < q's and b = #samples whose prefix
-// is <= q's, lower_bound(q) lies in [64(a-1)+1, min(n, 64b)] -- one 64-boundary block unless
-// several samples share q's 16-byte prefix.  Queries with lo >= hi are left alone.
-template <int Q>
-__device__ __forceinline__ void multi_narrow(const MaxLevels (&m)[Q], const int64_t (&n)[Q], const DKey (&q)[Q],
-                                             int64_t (&lo)[Q], int64_t (&hi)[Q]) {
-    int64_t l[Q], h[Q], ns[Q];
+__device__ __forceinline__ bool prefix_less(const ulonglong2& k, const DKey& q) {
+    return k.x < q.hi || (k.x == q.hi && k.y < q.lo);
+}
+
+// Number of leading entries of a[base, base+cnt) (cnt <= 16, sorted) whose prefix is < q's: the
+// 16 loads are issued together.
+__device__ __forceinline__ int count16(const ulonglong2* a, int64_t base, int cnt, const DKey& q) {
+    ulonglong2 k[16];
 #pragma unroll
-    for (int i = 0; i < Q; i++) {
-        ns[i] = (n[i] + kFan - 1) / kFan;
-        l[i] = 0;
-        h[i] = lo[i] < hi[i] ? ns[i] : 0;
+    for (int i = 0; i < 16; i++)
+        if (i < cnt) k[i] = a[base + i];
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) c += (i < cnt && prefix_less(k[i], q)) ? 1 : 0;
+    return c;
+}
+
+// Full key comparison of boundary i with q, given its prefix already loaded.
+__device__ __forceinline__ int probe_cmp(const Hist& h, int64_t i, const ulonglong2& k, const uint8_t* htail,
+                                         const DKey& q, const uint8_t* qtail) {
+    if (k.x != q.hi) return k.x < q.hi ? -1 : 1;
+    if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
+    return hist_cmp(h, i, htail, q, qtail);  // equal prefixes: length / tail
+}
+
+// std::lower_bound of q over the n boundaries of a tier, through its search tree: one 16-wide
+// probe per tree level down to a 64-boundary block, then two probes inside the block (about 6
+// dependent rounds instead of ~23 for a plain binary search over millions of boundaries).
+// eq: the boundary at the result equals q.
+__device__ __forceinline__ int64_t tree_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
+                                                    const uint8_t* htail, const uint8_t* qtail, bool& eq) {
+    eq = false;
+    if (n <= 0) return 0;
+    int64_t sz[kIdxLevels];
+    sz[0] = (n + kFan - 1) / kFan;
+#pragma unroll
+    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + 15) / 16;
+    int top = 0;
+    while (top + 1 < kIdxLevels && sz[top] > 16) top++;
+    // c = number of entries of level `top` whose prefix is < q
+    int64_t c = 0;
+    for (int64_t j0 = 0; j0 < sz[top]; j0 += 16) {
+        const int cnt = (int)min((int64_t)16, sz[top] - j0);
+        const int k = count16(m.skey[top], j0, cnt, q);
+        c += k;
+        if (k < cnt) break;
     }
-    for (;;) {
-        bool any = false;
-        int64_t mid[Q];
-        ulonglong2 k[Q];
-#pragma unroll
-        for (int i = 0; i < Q; i++) {
-            mid[i] = (l[i] + h[i]) >> 1;
-            if (l[i] < h[i]) {
-                k[i] = m[i].skey[mid[i]];
-                any = true;
+    for (int L = top; L > 0; L--) {
+        if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
+        // entries of level L-1 below q: [0, c') with c' in [16(c-1)+1, 16c]
+        const int64_t base = 16 * (c - 1) + 1;
+        const int64_t end = min(16 * c, sz[L - 1]);
+        c = base + count16(m.skey[L - 1], base, (int)(end - base), q);
+    }
+    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
+    int64_t b = c;
+    while (b < sz[0] && m.skey[0][b].x == q.hi && m.skey[0][b].y == q.lo) b++;
+    int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
+    int64_t hi = min(n, kFan * b);
+    if (hi - lo > kFan) {  // long run of shared prefixes: plain binary search
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            const int r = hist_cmp(h, mid, htail, q, qtail);
+            if (r < 0) {
+                lo = mid + 1;
+            } else {
+                hi = mid;
+                eq = r == 0;
             }
         }
-        if (!any) break;
+        return lo;
+    }
+    // lower_bound in [lo, hi], hi - lo <= 64: probes at lo+4i+3, then the 3 left in one quad
+    ulonglong2 k1[16];
 #pragma unroll
-        for (int i = 0; i < Q; i++) {
-            if (l[i] < h[i]) {
-                const bool less = k[i].x < q[i].hi || (k[i].x == q[i].hi && k[i].y < q[i].lo);
-                if (less)
-                    l[i] = mid[i] + 1;
-                else
-                    h[i] = mid[i];
+    for (int i = 0; i < 16; i++) {
+        const int64_t p = lo + 4 * i + 3;
+        if (p < hi) k1[i] = h.key[p];
+    }
+    int c1 = 0;
+    bool eq1 = false;  // the probe that stopped the count hit q itself
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int64_t p = lo + 4 * i + 3;
+        if (p < hi && c1 == i) {
+            const int r = probe_cmp(h, p, k1[i], htail, q, qtail);
+            if (r < 0)
+                c1++;
+            else
+                eq1 = r == 0;
+        }
+    }
+    const int64_t q0 = lo + 4 * c1;  // lower_bound in [q0, min(hi, q0 + 3)]
+    ulonglong2 k2[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+        if (q0 + i < hi) k2[i] = h.key[q0 + i];
+    int c2 = 0;
+    bool eq2 = false, stopped = false;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        if (q0 + i < hi && !stopped) {
+            const int r = probe_cmp(h, q0 + i, k2[i], htail, q, qtail);
+            if (r < 0) {
+                c2++;
+            } else {
+                stopped = true;
+                eq2 = r == 0;
             }
         }
     }
-#pragma unroll
-    for (int i = 0; i < Q; i++) {
-        if (lo[i] < hi[i]) {
-            const int64_t a = l[i];
-            int64_t b = a;
-            while (b < ns[i] && m[i].skey[b].x == q[i].hi && m[i].skey[b].y == q[i].lo) b++;  // shared prefixes
-            lo[i] = a > 0 ? kFan * (a - 1) + 1 : 0;
-            hi[i] = min(n[i], kFan * b);
-        }
-    }
+    const int64_t lb = q0 + c2;
+    // the boundary at lb was probed in the quad (stopped) or is the round-1 probe lo+4c1+3
+    eq = stopped ? eq2 : (c2 == 3 && lb < hi ? eq1 : false);
+    return lb;
 }
 
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
@@ -236,31 +303,40 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
     return range_max(m, ub - 1, j, snap) > snap;
 }
 
-// One thread per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
-// of SURVEY A.2).  The history is the base tier overlaid by the delta tier; every delta version is
-// >= the base versions it covers (versions only grow), so the max over the overlay equals the max
-// of the two tiers' maxima, and holes (kHole) never conflict.  The four searches (begin and end
-// key in both tiers) run in lockstep.
+// Four lanes per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
+// of SURVEY A.2): lane roles 0/1 locate the begin/end key in the base tier, 2/3 in the delta tier,
+// all concurrently.  The history is the base tier overlaid by the delta tier; every delta version
+// is >= the base versions it covers (versions only grow), so the max over the overlay equals the
+// max of the two tiers' maxima, and holes (kHole) never conflict.  slot = 4 * r + role; every lane
+// of the wave calls this (shuffles).
 __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, const Tier& delta,
-                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int r) {
-    const int t = b.rowner[r];
-    const int64_t snap = b.snap[t];
-    const DKey kb = b.keys[2 * r], ke = b.keys[2 * r + 1];
+                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int64_t slot) {
+    const int role = (int)(slot & 3);
+    const int r = (int)(slot >> 2);
+    const bool live = r < b.R;
+    const int rr = live ? r : 0;
+    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    const int64_t nb = *base.n, nd = *delta.n;
-    const Hist h[4] = {base.h, base.h, delta.h, delta.h};
-    const MaxLevels m[4] = {base.m, base.m, delta.m, delta.m};
-    const int64_t n[4] = {nb, nb, nd, nd};
-    const DKey q[4] = {kb, ke, kb, ke};
-    int64_t lo[4] = {0, 0, 0, 0};
-    int64_t hi[4] = {nb, degenerate ? 0 : nb, nd, degenerate ? 0 : nd};
-    bool eq[4];
-    multi_narrow<4>(m, n, q, lo, hi);
-    multi_lower_bound<4>(h, lo, hi, eq, htail, q, b.tail);
-    bool conf = tier_conflict(base.h, base.m, base.hdr, lo[0], eq[0], lo[1], degenerate, snap);
-    if (!conf && nd > 0) conf = tier_conflict(delta.h, delta.m, kHole, lo[2], eq[2], lo[3], degenerate, snap);
-    rconf[r] = conf ? 1 : 0;
-    if (conf) hist_conf[t] = 1;
+    const Tier& tier = role < 2 ? base : delta;
+    const int64_t n = *tier.n;
+    int64_t lb = 0;
+    bool eq = false;
+    if (live && !((role & 1) && degenerate))
+        lb = tree_lower_bound(tier.h, tier.m, n, (role & 1) ? ke : kb, htail, b.tail, eq);
+    // roles 0 and 2 take the end key's position from their neighbour
+    const int lane = threadIdx.x & 63;
+    const int64_t j = __shfl(lb, lane + 1, 64);
+    bool conf = false;
+    if (live && !(role & 1) && (role == 0 || n > 0)) {
+        const int64_t snap = b.snap[b.rowner[rr]];
+        conf = tier_conflict(tier.h, tier.m, role == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
+    }
+    const int dconf = __shfl((int)conf, lane + 2, 64);
+    if (live && role == 0) {
+        conf = conf || dconf;
+        rconf[r] = conf ? 1 : 0;
+        if (conf) hist_conf[b.rowner[r]] = 1;
+    }
 }
 
 // ------------------------------------------------------------------ D.Sort
@@ -397,16 +473,21 @@ struct SampleCheck {
     Tier base, delta;
     const uint8_t* htail;
     uint8_t *hist_conf, *rconf;
+    unsigned long long* trace;
 };
 
 __global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck c) {
     __shared__ SortItem sl[kSampleSlice];
     __shared__ int s_last;
     if ((int)blockIdx.x >= c.n_sample_wg) {
-        const int r = (blockIdx.x - c.n_sample_wg) * blockDim.x + threadIdx.x;
-        if (r < b.R) check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, r);
+        if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
+        const int64_t slot = (int64_t)(blockIdx.x - c.n_sample_wg) * blockDim.x + threadIdx.x;
+        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
+        __syncthreads();
+        if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
         return;
     }
+    if (threadIdx.x == 0) trace_min(c.trace, kTrSampleBegin);
     const int E = 2 * (b.R + b.W), S = c.S, nb = c.nb;
     const int x = blockIdx.x % c.n_slice, y = blockIdx.x / c.n_slice;
     const int j0 = x * kSampleSlice;
@@ -434,6 +515,8 @@ __global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck
         const int k = (int)(((int64_t)r * nb + S - 1) / S);  // the splitter index whose rank would be r
         if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) c.splitters[k - 1] = make_item(b, sample_pos(q, E, S));
     }
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(c.trace, kTrSampleEnd);
 }
 
 __device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl, int nsplit, const uint8_t* arena) {
@@ -629,7 +712,8 @@ void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const 
     c.htail = htail;
     c.hist_conf = w.hist_conf;
     c.rconf = w.rconf;
-    const int grid = c.n_sample_wg + (b.R + kBlock - 1) / kBlock;
+    c.trace = w.trace;
+    const int grid = c.n_sample_wg + (4 * b.R + kBlock - 1) / kBlock;
     if (grid > 0) hipLaunchKernelGGL(k_sample_check, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
@@ -995,25 +1079,28 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
 __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, MaxLevels hm,
                                                        const uint8_t* htail, const Scalars* sc, const int64_t* n_in,
                                                        int64_t* lvl3, int64_t lvl3_n) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // the history check of this batch is done with the old hierarchy: reset its top level for the
     // epilogue's atomicMax build
-    for (int64_t i = s; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    // two lanes per union segment: lane role 0 locates B, role 1 locates E
     const int U = sc->n_segments;
-    if (s >= U) return;
+    const int s = (int)(gt >> 1), role = (int)(gt & 1);
+    const bool live = s < U;
     const int64_t n = *n_in;
-    const DKey kb = seg_key(b, w, w.seg_b[s], 0);
-    const DKey ke = seg_key(b, w, w.seg_e[s], 1);
-    const Hist hh[2] = {h, h};
-    const MaxLevels mm[2] = {hm, hm};
-    const int64_t nn[2] = {n, n};
-    const DKey q[2] = {kb, ke};
-    int64_t l[2] = {0, 0}, u[2] = {n, n};
-    bool eq[2];
-    multi_narrow<2>(mm, nn, q, l, u);
-    multi_lower_bound<2>(hh, l, u, eq, htail, q, b.tail);
-    const int64_t lo = l[0], hi = l[1];
-    const bool exact = eq[1];
+    int64_t pos = 0;
+    bool eq = false;
+    DKey kb{}, ke{};
+    if (live) {
+        kb = seg_key(b, w, w.seg_b[s], 0);
+        ke = seg_key(b, w, w.seg_e[s], 1);
+        pos = tree_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+    }
+    const int lane = threadIdx.x & 63;
+    const int64_t hi = __shfl(pos, lane + 1, 64);
+    const int exact = __shfl((int)eq, lane + 1, 64);
+    if (!live || role) return;
+    const int64_t lo = pos;
     const bool glue = s + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[s + 1], 0), b.tail, ke, b.tail) == 0;
     const bool endins = !exact && !glue;
     w.seg_lo[s] = lo;
@@ -1220,7 +1307,7 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
                   hipEvent_t copy_begin, hipEvent_t copy_end) {
     const int Wn = b.W > 0 ? b.W : 1;
-    hipLaunchKernelGGL(k_seg_search, dim3((Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm, htail, sc,
+    hipLaunchKernelGGL(k_seg_search, dim3((2 * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm, htail, sc,
                        &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
@@ -1256,16 +1343,8 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     q.lo = k.y;
     q.len = lt.x;
     q.tail = lt.y;
-    const Hist hh[1] = {base};
-    const MaxLevels mm[1] = {basem};
-    const int64_t nn[1] = {nb};
-    const DKey qq[1] = {q};
-    int64_t l[1] = {0}, u[1] = {nb};
-    bool eq[1];
-    multi_narrow<1>(mm, nn, qq, l, u);
-    multi_lower_bound<1>(hh, l, u, eq, htail, qq, htail);
-    const int64_t lo = l[0];
-    const bool exact = eq[0];
+    bool exact;
+    const int64_t lo = tree_lower_bound(base, basem, nb, q, htail, htail, exact);
     const int64_t dv = delta.ver[j];
     w.c_lo[j] = lo;
     w.c_exact[j] = exact ? 1 : 0;
@@ -1402,6 +1481,7 @@ struct Epilogue {
     uint8_t* verdict_dev;  // [T] device copy of the verdicts (on-device combine)
     uint32_t* flag;        // host-mapped completion word, set to `seq` last
     uint32_t seq;
+    unsigned long long* trace;
     int32_t T;
     int compacted, gc_ran;
     uint8_t* zero8;  // hist_conf
@@ -1421,6 +1501,7 @@ struct Epilogue {
 // that changed.
 __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, const int64_t* n_levels, Epilogue ep) {
     __shared__ int64_t l1[kFan];
+    if (threadIdx.x == 0) trace_min(ep.trace, kTrEpiBegin);
     int64_t n0;
     if (n_levels)
         n0 = *n_levels;
@@ -1431,22 +1512,40 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int64_t b2 = blockIdx.x; b2 < n2; b2 += gridDim.x) {
-#pragma unroll 4
+        // each wave reduces 16 blocks of 64 versions: all 16 loads first, then the reductions
+        const int64_t b1_0 = b2 * kFan + wid * (kFan / 4);
+        int64_t v[kFan / 4];
+#pragma unroll
         for (int q = 0; q < kFan / 4; q++) {
-            const int64_t b1 = b2 * kFan + wid * (kFan / 4) + q;
-            const int64_t i = b1 * kFan + lane;
-            int64_t v = i < n0 ? m.lvl[0][i] : LLONG_MIN;
+            const int64_t i = (b1_0 + q) * kFan + lane;
+            v[q] = i < n0 ? m.lvl[0][i] : LLONG_MIN;
+        }
+        const int64_t b1l = b1_0 + lane;  // lane q < 16 owns block b1_0 + q
+        ulonglong2 sk = make_ulonglong2(0, 0);
+        if (lane < kFan / 4 && b1l < n1) sk = m.keys[b1l * kFan];  // sampled key of the block
+        int64_t mine = LLONG_MIN;
+#pragma unroll
+        for (int q = 0; q < kFan / 4; q++) {
+            int64_t x = v[q];
+#pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
-                const int64_t y = __shfl_xor(v, o, 64);
-                v = y > v ? y : v;
+                const int64_t y = __shfl_xor(x, o, 64);
+                x = y > x ? y : x;
             }
-            if (lane == 0) {
-                if (b1 < n1) {
-                    m.lvl[1][b1] = v;
-                    m.skey[b1] = m.keys[b1 * kFan];  // sampled key index
+            if (lane == q) mine = x;
+        }
+        if (lane < kFan / 4) {
+            if (b1l < n1) {
+                m.lvl[1][b1l] = mine;
+                m.skey[0][b1l] = sk;
+                // search-tree levels above: block b1l is entry b1l / 16^L of level L when divisible
+                int64_t d = b1l;
+                for (int L = 1; L < kIdxLevels && (d & 15) == 0; L++) {
+                    d >>= 4;
+                    m.skey[L][d] = sk;
                 }
-                l1[wid * (kFan / 4) + q] = v;
             }
+            l1[wid * (kFan / 4) + lane] = mine;
         }
         __syncthreads();
         if (wid == 0) {
@@ -1463,6 +1562,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         __syncthreads();
     }
     if (!ep.verdict_out) return;
+    if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiLevels);
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
     auto verdict = [&](int64_t t) -> uint8_t {
         if (ep.flags[t] & kFlagTooOld) return 1;  // TransactionTooOld (ConflictSet.h:42)
@@ -1480,6 +1580,8 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         ep.zero_bk[i] = 0;
     }
     for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiZero);
     if (blockIdx.x != 0) return;
     // Workgroup 0 writes what the host reads (host-mapped, 16 verdicts per store), then publishes
     // the batch's sequence number; everything else this launch writes is read only by later
@@ -1508,9 +1610,14 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = *sc;
         sc->debug_error = 0;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiHost);
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+        trace_max(ep.trace, kTrEpiFence);
+        __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
@@ -1529,6 +1636,7 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
                      int64_t grid_hint_n) {
     hipLaunchKernelGGL(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
     Epilogue ep{};
+    ep.trace = nullptr;
     hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, n, ep);
 }
 
@@ -1539,6 +1647,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.verdict_dev = verdict_dev;
     ep.flag = flag;
     ep.seq = seq;
+    ep.trace = w.trace;
     ep.flags = b.flags;
     ep.status = w.status;
     ep.verdict_out = verdict_out;
