@@ -1021,6 +1021,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                     us(kTrEpiBegin, kTrEpiLevels), us(kTrEpiLevels, kTrEpiZero), us(kTrEpiZero, kTrEpiHost),
                     us(kTrEpiHost, kTrEpiFence));
 
+
         }
         if (b->h_scal->debug_error) {
             fprintf(stderr, "fdbcs: device invariant check failed (debug_error=%d)\n", b->h_scal->debug_error);

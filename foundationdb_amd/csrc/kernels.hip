@@ -205,6 +205,91 @@ __device__ __forceinline__ int64_t tree_lower_bound(const Hist& h, const MaxLeve
     return lb;
 }
 
+// ---- cooperative search: 16 lanes per query, one 16-entry tree node per level
+//
+// Each lane of an aligned 16-lane group loads one entry of the node, so a level costs one
+// coalesced 256-byte access instead of sixteen scattered ones.  All 16 lanes call with the same
+// query and get the same result.  gmask(): the group's 16 bits of a wave ballot.
+__device__ __forceinline__ uint32_t gmask(bool pred) {
+    const uint64_t m = __ballot(pred);
+    return (uint32_t)(m >> (threadIdx.x & 48)) & 0xFFFFu;
+}
+
+__device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
+                                                     const uint8_t* htail, const uint8_t* qtail, bool& eq) {
+    const int gl = threadIdx.x & 15;
+    eq = false;
+    if (n <= 0) return 0;
+    int64_t sz[kIdxLevels];
+    sz[0] = (n + kFan - 1) / kFan;
+#pragma unroll
+    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + 15) / 16;
+    int top = 0;
+    while (top + 1 < kIdxLevels && sz[top] > 16) top++;
+    // c = number of entries of level `top` whose prefix is < q
+    int64_t c = 0;
+    for (int64_t j0 = 0; j0 < sz[top]; j0 += 16) {
+        const bool v = j0 + gl < sz[top];
+        const uint32_t less = gmask(v && prefix_less(m.skey[top][v ? j0 + gl : 0], q));
+        const int k = __popc(less);
+        c += k;
+        if (k < 16) break;
+    }
+    for (int L = top; L > 0; L--) {
+        if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
+        // entries of level L-1 below q: [0, c') with c' in [16(c-1)+1, 16c]
+        const int64_t base = 16 * (c - 1) + 1;
+        const int64_t end = min(16 * c, sz[L - 1]);
+        const bool v = base + gl < end;
+        c = base + __popc(gmask(v && prefix_less(m.skey[L - 1][v ? base + gl : 0], q)));
+    }
+    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
+    int64_t b = c;
+    for (;;) {
+        const bool v = b + gl < sz[0];
+        const ulonglong2 k = m.skey[0][v ? b + gl : 0];
+        const uint32_t same = gmask(v && k.x == q.hi && k.y == q.lo);
+        const int run = __ffs(~same) - 1;  // leading lanes equal to q's prefix
+        b += run;
+        if (run < 16) break;
+    }
+    int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
+    int64_t hi = min(n, kFan * b);
+    if (hi - lo > kFan) {  // long run of shared prefixes: binary search, every lane alike
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            const int r = hist_cmp(h, mid, htail, q, qtail);
+            if (r < 0) {
+                lo = mid + 1;
+            } else {
+                hi = mid;
+                eq = r == 0;
+            }
+        }
+        return lo;
+    }
+    // lower_bound in [lo, hi], hi - lo <= 64: lane j probes lo+4j+3, then lanes 0..2 the quad left
+    const int64_t p1 = lo + 4 * gl + 3;
+    int r1 = 1;
+    if (p1 < hi) r1 = probe_cmp(h, p1, h.key[p1], htail, q, qtail);
+    const int c1 = __popc(gmask(p1 < hi && r1 < 0));
+    const int q0l = c1 < 16 ? c1 : 15;
+    const bool eq1 = __shfl(r1, (threadIdx.x & 48) + q0l, 64) == 0;  // probe lo+4c1+3 (if it exists)
+    const int64_t q0 = lo + 4 * c1;
+    const int64_t p2 = q0 + gl;
+    int r2 = 1;
+    if (gl < 3 && p2 < hi) r2 = probe_cmp(h, p2, h.key[p2], htail, q, qtail);
+    const int c2 = __popc(gmask(gl < 3 && p2 < hi && r2 < 0));
+    const int64_t lb = q0 + c2;
+    if (lb < hi) {
+        if (c2 < 3)
+            eq = __shfl(r2, (threadIdx.x & 48) + c2, 64) == 0;
+        else
+            eq = eq1;  // lb = lo + 4c1 + 3: the round-1 probe of lane c1
+    }
+    return lb;
+}
+
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
 __device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
     int64_t best = LLONG_MIN;
@@ -303,36 +388,33 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
     return range_max(m, ub - 1, j, snap) > snap;
 }
 
-// Four lanes per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
-// of SURVEY A.2): lane roles 0/1 locate the begin/end key in the base tier, 2/3 in the delta tier,
-// all concurrently.  The history is the base tier overlaid by the delta tier; every delta version
-// is >= the base versions it covers (versions only grow), so the max over the overlay equals the
-// max of the two tiers' maxima, and holes (kHole) never conflict.  slot = 4 * r + role; every lane
-// of the wave calls this (shuffles).
+// One wave per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
+// of SURVEY A.2): lane groups 0/1 locate the begin/end key in the base tier, groups 2/3 in the
+// delta tier, all concurrently.  The history is the base tier overlaid by the delta tier; every
+// delta version is >= the base versions it covers (versions only grow), so the max over the
+// overlay equals the max of the two tiers' maxima, and holes (kHole) never conflict.  Every lane
+// of the wave calls this with the wave's read index (shuffles and ballots).
 __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, const Tier& delta,
-                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int64_t slot) {
-    const int role = (int)(slot & 3);
-    const int r = (int)(slot >> 2);
+                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int r) {
+    const int lane = threadIdx.x & 63;
+    const int grp = lane >> 4;
     const bool live = r < b.R;
     const int rr = live ? r : 0;
     const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    const Tier& tier = role < 2 ? base : delta;
+    const Tier& tier = grp < 2 ? base : delta;
     const int64_t n = *tier.n;
     int64_t lb = 0;
     bool eq = false;
-    if (live && !((role & 1) && degenerate))
-        lb = tree_lower_bound(tier.h, tier.m, n, (role & 1) ? ke : kb, htail, b.tail, eq);
-    // roles 0 and 2 take the end key's position from their neighbour
-    const int lane = threadIdx.x & 63;
-    const int64_t j = __shfl(lb, lane + 1, 64);
+    if (live && !((grp & 1) && degenerate)) lb = group_lower_bound(tier.h, tier.m, n, (grp & 1) ? ke : kb, htail, b.tail, eq);
+    const int64_t j = __shfl(lb, lane + 16, 64);  // groups 0 and 2 take the end key's position
     bool conf = false;
-    if (live && !(role & 1) && (role == 0 || n > 0)) {
+    if (live && (lane == 0 || (lane == 32 && n > 0))) {
         const int64_t snap = b.snap[b.rowner[rr]];
-        conf = tier_conflict(tier.h, tier.m, role == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
+        conf = tier_conflict(tier.h, tier.m, lane == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
     }
-    const int dconf = __shfl((int)conf, lane + 2, 64);
-    if (live && role == 0) {
+    const int dconf = __shfl((int)conf, 32, 64);
+    if (live && lane == 0) {
         conf = conf || dconf;
         rconf[r] = conf ? 1 : 0;
         if (conf) hist_conf[b.rowner[r]] = 1;
@@ -481,8 +563,8 @@ __global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck
     __shared__ int s_last;
     if ((int)blockIdx.x >= c.n_sample_wg) {
         if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
-        const int64_t slot = (int64_t)(blockIdx.x - c.n_sample_wg) * blockDim.x + threadIdx.x;
-        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
+        const int r = (blockIdx.x - c.n_sample_wg) * (blockDim.x / 64) + (threadIdx.x >> 6);  // one wave per read
+        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, r);
         __syncthreads();
         if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
         return;
@@ -713,7 +795,7 @@ void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const 
     c.hist_conf = w.hist_conf;
     c.rconf = w.rconf;
     c.trace = w.trace;
-    const int grid = c.n_sample_wg + (4 * b.R + kBlock - 1) / kBlock;
+    const int grid = c.n_sample_wg + (b.R + kBlock / 64 - 1) / (kBlock / 64);
     if (grid > 0) hipLaunchKernelGGL(k_sample_check, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
@@ -1083,9 +1165,9 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     // the history check of this batch is done with the old hierarchy: reset its top level for the
     // epilogue's atomicMax build
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
-    // two lanes per union segment: lane role 0 locates B, role 1 locates E
+    // 32 lanes per union segment: lane group 0 locates B, group 1 locates E (cooperative search)
     const int U = sc->n_segments;
-    const int s = (int)(gt >> 1), role = (int)(gt & 1);
+    const int s = (int)(gt >> 5), role = (int)((gt >> 4) & 1);
     const bool live = s < U;
     const int64_t n = *n_in;
     int64_t pos = 0;
@@ -1094,12 +1176,12 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     if (live) {
         kb = seg_key(b, w, w.seg_b[s], 0);
         ke = seg_key(b, w, w.seg_e[s], 1);
-        pos = tree_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        pos = group_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
     }
     const int lane = threadIdx.x & 63;
-    const int64_t hi = __shfl(pos, lane + 1, 64);
-    const int exact = __shfl((int)eq, lane + 1, 64);
-    if (!live || role) return;
+    const int64_t hi = __shfl(pos, lane + 16, 64);
+    const int exact = __shfl((int)eq, lane + 16, 64);
+    if (!live || (gt & 31) != 0) return;
     const int64_t lo = pos;
     const bool glue = s + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[s + 1], 0), b.tail, ke, b.tail) == 0;
     const bool endins = !exact && !glue;
@@ -1307,7 +1389,7 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
                   hipEvent_t copy_begin, hipEvent_t copy_end) {
     const int Wn = b.W > 0 ? b.W : 1;
-    hipLaunchKernelGGL(k_seg_search, dim3((2 * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm, htail, sc,
+    hipLaunchKernelGGL(k_seg_search, dim3((32 * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm, htail, sc,
                        &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
@@ -1331,10 +1413,11 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
                                                            const uint8_t* htail, const int64_t* nb_ptr,
                                                            const int64_t* nd_ptr, int64_t hdr, Work w, int64_t* lvl3,
                                                            int64_t lvl3_n) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int64_t i = j; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    const int64_t j = gt >> 4;  // 16 lanes per delta boundary (cooperative search)
     const int64_t nd = *nd_ptr;
-    if (j >= nd) return;
+    if (j >= nd) return;  // whole groups leave together
     const int64_t nb = *nb_ptr;
     const ulonglong2 k = delta.key[j];
     const uint2 lt = delta.lt[j];
@@ -1344,7 +1427,8 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     q.len = lt.x;
     q.tail = lt.y;
     bool exact;
-    const int64_t lo = tree_lower_bound(base, basem, nb, q, htail, htail, exact);
+    const int64_t lo = group_lower_bound(base, basem, nb, q, htail, htail, exact);
+    if ((gt & 15) != 0) return;
     const int64_t dv = delta.ver[j];
     w.c_lo[j] = lo;
     w.c_exact[j] = exact ? 1 : 0;
@@ -1398,7 +1482,7 @@ struct CompactIns {
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end) {
-    int64_t blocks = (delta_hint_n + kBlock - 1) / kBlock;
+    int64_t blocks = (16 * delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
                        &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n);
