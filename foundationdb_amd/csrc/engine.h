@@ -33,18 +33,20 @@ struct Hist {
 };
 
 // Range-max hierarchy over the current history's versions.
-// Range-max hierarchy over a tier's versions, and its static 16-ary search tree over sampled key
-// prefixes: skey[L][j] = prefix of boundary 64 * 16^L * j, so skey[L][j] == skey[L-1][16 j].  A
-// search descends the tree one 16-wide parallel probe per level and lands in one 64-boundary block.
-constexpr int kIdxLevels = 6;  // enough for 16 * 64 * 16^5 boundaries under a 16-entry top level
+// Range-max hierarchy over a tier's versions, and its static kArity-ary search tree over sampled
+// key prefixes: skey[L][j] = prefix of boundary 64 * A^L * j, so skey[L][j] == skey[L-1][A j].  A
+// lookup descends the tree with kArity cooperating lanes, one node (one 128-byte line at A = 8) per
+// level, and lands in one 64-boundary block.
+constexpr int kArity = 8;
+constexpr int kIdxLevels = 12;  // A^11 * 64 * A boundaries under an A-entry top level
 struct MaxLevels {
     int64_t* lvl[kMaxLevels];       // lvl[0] == current Hist::ver
     const ulonglong2* keys;         // the tier's keys (source of the samples)
-    ulonglong2* skey[kIdxLevels];   // [ceil(n / (64 * 16^L))]
+    ulonglong2* skey[kIdxLevels];   // [ceil(n / (64 * A^L))]
 };
 __host__ __device__ inline int64_t idx_level_cap(int64_t cap, int L) {
     int64_t d = 64;
-    for (int i = 0; i < L; i++) d *= 16;
+    for (int i = 0; i < L && d <= cap; i++) d *= kArity;
     return cap / d + 2;
 }
 

@@ -205,89 +205,96 @@ __device__ __forceinline__ int64_t tree_lower_bound(const Hist& h, const MaxLeve
     return lb;
 }
 
-// ---- cooperative search: 16 lanes per query, one 16-entry tree node per level
+// ---- cooperative search: kArity lanes per query, one kArity-entry tree node per level
 //
-// Each lane of an aligned 16-lane group loads one entry of the node, so a level costs one
-// coalesced 256-byte access instead of sixteen scattered ones.  All 16 lanes call with the same
-// query and get the same result.  gmask(): the group's 16 bits of a wave ballot.
+// Each lane of an aligned kArity-lane group loads one entry of the node, so a level is one
+// coalesced kArity*16-byte access (one 128-byte line at kArity 8).  All lanes of a group call with
+// the same query and get the same result.  gmask(): the group's bits of a wave ballot.
 __device__ __forceinline__ uint32_t gmask(bool pred) {
     const uint64_t m = __ballot(pred);
-    return (uint32_t)(m >> (threadIdx.x & 48)) & 0xFFFFu;
+    return (uint32_t)(m >> (threadIdx.x & 63 & ~(kArity - 1))) & ((1u << kArity) - 1u);
 }
 
 __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
                                                      const uint8_t* htail, const uint8_t* qtail, bool& eq) {
-    const int gl = threadIdx.x & 15;
+    const int gl = threadIdx.x & (kArity - 1);
+    const int g0 = threadIdx.x & 63 & ~(kArity - 1);  // first lane of the group
     eq = false;
     if (n <= 0) return 0;
     int64_t sz[kIdxLevels];
     sz[0] = (n + kFan - 1) / kFan;
 #pragma unroll
-    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + 15) / 16;
+    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + kArity - 1) / kArity;
     int top = 0;
-    while (top + 1 < kIdxLevels && sz[top] > 16) top++;
-    // c = number of entries of level `top` whose prefix is < q
+    while (top + 1 < kIdxLevels && sz[top] > kArity) top++;
+    // c = number of entries of level `top` whose prefix is < q.  When level 0 is probed, also learn
+    // whether the first sample not below q shares q's prefix (`bknown`: it does not).
+    auto prefix_eq = [&](const ulonglong2& k) { return k.x == q.hi && k.y == q.lo; };
     int64_t c = 0;
-    for (int64_t j0 = 0; j0 < sz[top]; j0 += 16) {
+    bool bknown = false;
+    for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
         const bool v = j0 + gl < sz[top];
-        const uint32_t less = gmask(v && prefix_less(m.skey[top][v ? j0 + gl : 0], q));
-        const int k = __popc(less);
+        const ulonglong2 e = m.skey[top][v ? j0 + gl : 0];
+        const int k = __popc(gmask(v && prefix_less(e, q)));
+        if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
         c += k;
-        if (k < 16) break;
+        if (k < kArity) break;
     }
     for (int L = top; L > 0; L--) {
         if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
-        // entries of level L-1 below q: [0, c') with c' in [16(c-1)+1, 16c]
-        const int64_t base = 16 * (c - 1) + 1;
-        const int64_t end = min(16 * c, sz[L - 1]);
+        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, Ac]
+        const int64_t base = (int64_t)kArity * (c - 1) + 1;
+        const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
         const bool v = base + gl < end;
-        c = base + __popc(gmask(v && prefix_less(m.skey[L - 1][v ? base + gl : 0], q)));
+        const ulonglong2 e = m.skey[L - 1][v ? base + gl : 0];
+        const int k = __popc(gmask(v && prefix_less(e, q)));
+        if (L == 1 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+        c = base + k;
     }
     // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
     int64_t b = c;
-    for (;;) {
+    for (; !bknown;) {
         const bool v = b + gl < sz[0];
         const ulonglong2 k = m.skey[0][v ? b + gl : 0];
         const uint32_t same = gmask(v && k.x == q.hi && k.y == q.lo);
         const int run = __ffs(~same) - 1;  // leading lanes equal to q's prefix
         b += run;
-        if (run < 16) break;
+        if (run < kArity) break;
     }
     int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
-    int64_t hi = min(n, kFan * b);
+    const int64_t hi = min(n, kFan * b);
     if (hi - lo > kFan) {  // long run of shared prefixes: binary search, every lane alike
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
+        int64_t l = lo, u = hi;
+        while (l < u) {
+            const int64_t mid = (l + u) >> 1;
             const int r = hist_cmp(h, mid, htail, q, qtail);
             if (r < 0) {
-                lo = mid + 1;
+                l = mid + 1;
             } else {
-                hi = mid;
+                u = mid;
                 eq = r == 0;
             }
         }
-        return lo;
+        return l;
     }
-    // lower_bound in [lo, hi], hi - lo <= 64: lane j probes lo+4j+3, then lanes 0..2 the quad left
-    const int64_t p1 = lo + 4 * gl + 3;
-    int r1 = 1;
-    if (p1 < hi) r1 = probe_cmp(h, p1, h.key[p1], htail, q, qtail);
-    const int c1 = __popc(gmask(p1 < hi && r1 < 0));
-    const int q0l = c1 < 16 ? c1 : 15;
-    const bool eq1 = __shfl(r1, (threadIdx.x & 48) + q0l, 64) == 0;  // probe lo+4c1+3 (if it exists)
-    const int64_t q0 = lo + 4 * c1;
-    const int64_t p2 = q0 + gl;
-    int r2 = 1;
-    if (gl < 3 && p2 < hi) r2 = probe_cmp(h, p2, h.key[p2], htail, q, qtail);
-    const int c2 = __popc(gmask(gl < 3 && p2 < hi && r2 < 0));
-    const int64_t lb = q0 + c2;
-    if (lb < hi) {
-        if (c2 < 3)
-            eq = __shfl(r2, (threadIdx.x & 48) + c2, 64) == 0;
-        else
-            eq = eq1;  // lb = lo + 4c1 + 3: the round-1 probe of lane c1
+    // lower_bound in [lo, lo + span], span <= 64: rounds of kArity probes at a shrinking stride
+    int64_t span = hi - lo;
+    bool eq_cand = false;  // cmp == 0 at the last probe that stopped a count (the answer, if < hi)
+    for (int64_t stride = kFan / kArity; span > 0; stride = stride > kArity ? stride / kArity : 1) {
+        const int64_t p = lo + stride * (gl + 1) - 1;
+        const bool v = stride * (gl + 1) <= span && p < hi;
+        int r = 1;
+        if (v) r = probe_cmp(h, p, h.key[p], htail, q, qtail);
+        const uint32_t valid = gmask(v);
+        const int cnt = __popc(gmask(v && r < 0));
+        const int stop = __shfl(r, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
+        if (cnt < __popc(valid)) eq_cand = stop == 0;  // lane cnt probed a key >= q
+        lo += stride * cnt;
+        span = cnt < __popc(valid) ? stride - 1 : span - stride * cnt;
+        if (stride == 1) break;
     }
-    return lb;
+    if (lo < hi) eq = eq_cand;
+    return lo;
 }
 
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
@@ -388,33 +395,39 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
     return range_max(m, ub - 1, j, snap) > snap;
 }
 
-// One wave per read range (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule
-// of SURVEY A.2): lane groups 0/1 locate the begin/end key in the base tier, groups 2/3 in the
-// delta tier, all concurrently.  The history is the base tier overlaid by the delta tier; every
-// delta version is >= the base versions it covers (versions only grow), so the max over the
-// overlay equals the max of the two tiers' maxima, and holes (kHole) never conflict.  Every lane
-// of the wave calls this with the wave's read index (shuffles and ballots).
+// kArity lanes per lookup, four lookups per read range (SkipList.cpp:426-458 + CheckMax :619-706,
+// as the step-function rule of SURVEY A.2): lane groups 0/1 of a read locate its begin/end key in
+// the base tier, groups 2/3 in the delta tier, all concurrently.  The history is the base tier
+// overlaid by the delta tier; every delta version is >= the base versions it covers (versions only
+// grow), so the max over the overlay equals the max of the two tiers' maxima, and holes (kHole)
+// never conflict.  Every lane of the wave calls this (shuffles and ballots).
+constexpr int kReadLanes = 4 * kArity;
+
 __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, const Tier& delta,
-                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int r) {
+                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int64_t slot) {
     const int lane = threadIdx.x & 63;
-    const int grp = lane >> 4;
+    const int r = (int)(slot / kReadLanes);
+    const int grp = (lane / kArity) & 3;
+    const int lead = lane & ~(kReadLanes - 1);  // first lane of this read
     const bool live = r < b.R;
     const int rr = live ? r : 0;
     const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
     const Tier& tier = grp < 2 ? base : delta;
     const int64_t n = *tier.n;
+    const int64_t snap = b.snap[b.rowner[rr]];  // issued before the search
     int64_t lb = 0;
     bool eq = false;
-    if (live && !((grp & 1) && degenerate)) lb = group_lower_bound(tier.h, tier.m, n, (grp & 1) ? ke : kb, htail, b.tail, eq);
-    const int64_t j = __shfl(lb, lane + 16, 64);  // groups 0 and 2 take the end key's position
+    if (live && !((grp & 1) && degenerate))
+        lb = group_lower_bound(tier.h, tier.m, n, (grp & 1) ? ke : kb, htail, b.tail, eq);
+    const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // groups 0 and 2 take the end key's position
+    const bool leader = lane == lead || lane == lead + 2 * kArity;
     bool conf = false;
-    if (live && (lane == 0 || (lane == 32 && n > 0))) {
-        const int64_t snap = b.snap[b.rowner[rr]];
-        conf = tier_conflict(tier.h, tier.m, lane == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
+    if (live && leader && (grp == 0 || n > 0)) {
+        conf = tier_conflict(tier.h, tier.m, grp == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
     }
-    const int dconf = __shfl((int)conf, 32, 64);
-    if (live && lane == 0) {
+    const int dconf = __shfl((int)conf, lead + 2 * kArity, 64);
+    if (live && lane == lead) {
         conf = conf || dconf;
         rconf[r] = conf ? 1 : 0;
         if (conf) hist_conf[b.rowner[r]] = 1;
@@ -563,8 +576,8 @@ __global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck
     __shared__ int s_last;
     if ((int)blockIdx.x >= c.n_sample_wg) {
         if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
-        const int r = (blockIdx.x - c.n_sample_wg) * (blockDim.x / 64) + (threadIdx.x >> 6);  // one wave per read
-        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, r);
+        const int64_t slot = (int64_t)(blockIdx.x - c.n_sample_wg) * blockDim.x + threadIdx.x;
+        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
         __syncthreads();
         if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
         return;
@@ -795,7 +808,7 @@ void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const 
     c.hist_conf = w.hist_conf;
     c.rconf = w.rconf;
     c.trace = w.trace;
-    const int grid = c.n_sample_wg + (b.R + kBlock / 64 - 1) / (kBlock / 64);
+    const int grid = c.n_sample_wg + (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
     if (grid > 0) hipLaunchKernelGGL(k_sample_check, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
@@ -1165,9 +1178,9 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     // the history check of this batch is done with the old hierarchy: reset its top level for the
     // epilogue's atomicMax build
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
-    // 32 lanes per union segment: lane group 0 locates B, group 1 locates E (cooperative search)
+    // 2*kArity lanes per union segment: lane group 0 locates B, group 1 locates E (cooperative search)
     const int U = sc->n_segments;
-    const int s = (int)(gt >> 5), role = (int)((gt >> 4) & 1);
+    const int s = (int)(gt / (2 * kArity)), role = (int)((gt / kArity) & 1);
     const bool live = s < U;
     const int64_t n = *n_in;
     int64_t pos = 0;
@@ -1179,9 +1192,9 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
         pos = group_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
     }
     const int lane = threadIdx.x & 63;
-    const int64_t hi = __shfl(pos, lane + 16, 64);
-    const int exact = __shfl((int)eq, lane + 16, 64);
-    if (!live || (gt & 31) != 0) return;
+    const int64_t hi = __shfl(pos, (lane + kArity) & 63, 64);
+    const int exact = __shfl((int)eq, (lane + kArity) & 63, 64);
+    if (!live || (gt % (2 * kArity)) != 0) return;
     const int64_t lo = pos;
     const bool glue = s + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[s + 1], 0), b.tail, ke, b.tail) == 0;
     const bool endins = !exact && !glue;
@@ -1389,7 +1402,8 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
                   hipEvent_t copy_begin, hipEvent_t copy_end) {
     const int Wn = b.W > 0 ? b.W : 1;
-    hipLaunchKernelGGL(k_seg_search, dim3((32 * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm, htail, sc,
+    hipLaunchKernelGGL(k_seg_search, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
+                       htail, sc,
                        &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
@@ -1415,7 +1429,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
                                                            int64_t lvl3_n) {
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
-    const int64_t j = gt >> 4;  // 16 lanes per delta boundary (cooperative search)
+    const int64_t j = gt / kArity;  // kArity lanes per delta boundary (cooperative search)
     const int64_t nd = *nd_ptr;
     if (j >= nd) return;  // whole groups leave together
     const int64_t nb = *nb_ptr;
@@ -1428,7 +1442,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     q.tail = lt.y;
     bool exact;
     const int64_t lo = group_lower_bound(base, basem, nb, q, htail, htail, exact);
-    if ((gt & 15) != 0) return;
+    if ((gt % kArity) != 0) return;
     const int64_t dv = delta.ver[j];
     w.c_lo[j] = lo;
     w.c_exact[j] = exact ? 1 : 0;
@@ -1482,7 +1496,7 @@ struct CompactIns {
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end) {
-    int64_t blocks = (16 * delta_hint_n + kBlock - 1) / kBlock;
+    int64_t blocks = (kArity * delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
                        &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n);
@@ -1622,10 +1636,10 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
             if (b1l < n1) {
                 m.lvl[1][b1l] = mine;
                 m.skey[0][b1l] = sk;
-                // search-tree levels above: block b1l is entry b1l / 16^L of level L when divisible
+                // search-tree levels above: block b1l is entry b1l / A^L of level L when divisible
                 int64_t d = b1l;
-                for (int L = 1; L < kIdxLevels && (d & 15) == 0; L++) {
-                    d >>= 4;
+                for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
+                    d /= kArity;
                     m.skey[L][d] = sk;
                 }
             }
