@@ -456,7 +456,7 @@ __device__ __forceinline__ SortItem make_item(const BatchDev& b, int p) {
 // endpoint id as a final tie-break.  Endpoints equal in (key, class) are interchangeable for every
 // later use, so the tie-break changes nothing observable; it makes every item distinct,
 // which keeps sample-sort buckets balanced even when one hot key repeats thousands of times.
-__device__ __noinline__ bool item_less_tail(uint32_t alen, uint32_t atail, uint32_t ameta, uint32_t blen,
+__device__ __forceinline__ bool item_less_tail(uint32_t alen, uint32_t atail, uint32_t ameta, uint32_t blen,
                                             uint32_t btail, uint32_t bmeta, const uint8_t* arena) {
     const int c = tail_cmp(arena + atail, alen, arena + btail, blen);
     if (c) return c < 0;
@@ -709,50 +709,59 @@ __device__ __forceinline__ bool lt_pad(const SortItem& x, const SortItem& y, con
     return item_less_total(x, y, arena);
 }
 
-// Bitonic sort of sh[0, L) (L a power of two, L/2 <= blockDim.x) in LDS.
-__device__ void lds_bitonic(SortItem* sh, int L, const uint8_t* arena) {
+__device__ __forceinline__ SortItem shfl_xor_item(const SortItem& x, int j) {
+    SortItem y;
+    y.hi = __shfl_xor(x.hi, j, 64);
+    y.lo = __shfl_xor(x.lo, j, 64);
+    y.len = __shfl_xor(x.len, j, 64);
+    y.tail = __shfl_xor(x.tail, j, 64);
+    y.meta = __shfl_xor(x.meta, j, 64);
+    y.pad = __shfl_xor(x.pad, j, 64);
+    return y;
+}
+
+// Bitonic network over the workgroup, one item per thread (x = element threadIdx.x; L a power of
+// two <= blockDim.x; threads >= L hold padding).  Partners closer than a wave exchange through
+// cross-lane shuffles, farther ones through LDS.
+__device__ void reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* arena) {
+    const int t = threadIdx.x;
     for (int k = 2; k <= L; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            const int t = threadIdx.x;
-            if (t < (L >> 1)) {
-                const int i = 2 * t - (t & (j - 1)), p = i + j;
-                const SortItem x = sh[i], y = sh[p];
-                const bool up = (i & k) == 0;
-                if (up ? lt_pad(y, x, arena) : lt_pad(x, y, arena)) {
-                    sh[i] = y;
-                    sh[p] = x;
-                }
+            SortItem y;
+            if (j >= 64) {
+                sh[t] = x;
+                __syncthreads();
+                y = sh[t ^ j];
+                __syncthreads();
+            } else {
+                y = shfl_xor_item(x, j);
             }
-            __syncthreads();
+            const bool up = (t & k) == 0, lower = (t & j) == 0;
+            // ascending runs keep the smaller item at the lower position
+            if (lower == up ? lt_pad(y, x, arena) : lt_pad(x, y, arena)) x = y;
         }
     }
 }
 
-constexpr int kBitonicMax = 2 * kSortThreads;  // endpoints sorted in one pass by one workgroup
+constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by one workgroup
 
-// Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic in LDS, padded to a
+// Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic network padded to a
 // power of two; oversized buckets (skewed sample) sort kBitonicMax chunks, then merge through memory.
 __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
                                                               const uint8_t* arena) {
-    __shared__ SortItem sh[kBitonicMax];  // 32 KiB
+    __shared__ SortItem sh[kBitonicMax];  // 32 KiB exchange buffer
     const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
     if (m <= 1) return;
+    const int t = threadIdx.x;
     for (int c = 0; c < m; c += kBitonicMax) {
         const int cnt = min(kBitonicMax, m - c);
         int L = 2;
         while (L < cnt) L <<= 1;
-        for (int i = threadIdx.x; i < L; i += blockDim.x) {
-            if (i < cnt) {
-                sh[i] = a[off + c + i];
-            } else {
-                SortItem z{};
-                z.pad = 1;
-                sh[i] = z;
-            }
-        }
-        __syncthreads();
-        lds_bitonic(sh, L, arena);
-        for (int i = threadIdx.x; i < cnt; i += blockDim.x) a[off + c + i] = sh[i];
+        SortItem x{};
+        x.pad = 1;
+        if (t < cnt) x = a[off + c + t];
+        reg_bitonic(x, sh, L, arena);
+        if (t < cnt) a[off + c + t] = x;
         __syncthreads();
     }
     if (m <= kBitonicMax) return;
