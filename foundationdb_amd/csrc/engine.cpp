@@ -1014,6 +1014,21 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             unsigned long long tr[kTrSlots];
             HIPOK(hipMemcpy(tr, cs->trace_buf.p, sizeof(tr), hipMemcpyDeviceToHost));
             auto us = [&](int a, int z) { return (double)((long long)(tr[z] - tr[a])) / 100.0; };  // 100 MHz
+            {
+                const int E = 2 * (b->R() + b->W());
+                int nb = (E + 127) / 128;
+                nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+                std::vector<int32_t> bo(nb + 1);
+                HIPOK(hipMemcpy(bo.data(), cs->work.boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
+                int mx = 0, over = 0;
+                for (int k = 0; k < nb; k++) {
+                    const int sz = bo[k + 1] - bo[k];
+                    mx = std::max(mx, sz);
+                    over += sz > 512;
+                }
+                fprintf(stderr, "fdbcs trace: %d buckets for %d endpoints, largest %d, over 512: %d\n", nb, E, mx,
+                        over);
+            }
             fprintf(stderr,
                     "fdbcs trace: sample %.2f us, check %.2f us (check starts %+.2f us after sample); epilogue "
                     "levels %.2f, zero %.2f, host %.2f, fence %.2f us\n",

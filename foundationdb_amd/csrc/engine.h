@@ -12,7 +12,7 @@ namespace fdbcs {
 
 constexpr int kBlock = 256;        // default workgroup: 4 waves of 64
 constexpr int kWG = 1024;          // single-workgroup kernels (scans, resolution)
-constexpr int kSortThreads = 1024; // bucket-sort workgroups: 16 waves, one endpoint per thread
+constexpr int kSortThreads = 512;  // bucket-sort workgroups: 8 waves, one endpoint per thread
 constexpr int kSortTile = 4096;    // endpoints per LDS sort tile (128 KiB of LDS)
 constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
 constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)

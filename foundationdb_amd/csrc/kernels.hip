@@ -552,7 +552,7 @@ __device__ __noinline__ int rank_exact(const SortItem* sh, int cnt, SortItem min
 constexpr int kMaxBuckets = 2048;
 constexpr int kMaxSample = 8192;
 constexpr int kSampleSlice = 64;
-constexpr int kBucketTarget = 256;
+constexpr int kBucketTarget = 128;
 
 __device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((int64_t)i * E) / S); }
 
@@ -721,26 +721,42 @@ __device__ __forceinline__ SortItem shfl_xor_item(const SortItem& x, int j) {
 }
 
 // Bitonic network over the workgroup, one item per thread (x = element threadIdx.x; L a power of
-// two <= blockDim.x; threads >= L hold padding).  Partners closer than a wave exchange through
-// cross-lane shuffles, farther ones through LDS.
-__device__ void reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* arena) {
+// two <= blockDim.x; threads >= L sit out).  Partners closer than a wave exchange through
+// cross-lane shuffles, farther ones through LDS.  EXACT = false compares (prefix, tie-break word)
+// branch-free and only flags comparisons that would need the bytes beyond the prefix; the caller
+// reruns with EXACT = true when any lane flagged one.
+template <bool EXACT>
+__device__ bool reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* arena) {
     const int t = threadIdx.x;
+    const bool active = t < L;
+    bool tie = false;
     for (int k = 2; k <= L; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             SortItem y;
             if (j >= 64) {
-                sh[t] = x;
+                if (active) sh[t] = x;
                 __syncthreads();
-                y = sh[t ^ j];
+                if (active) y = sh[t ^ j];
                 __syncthreads();
             } else {
                 y = shfl_xor_item(x, j);
             }
-            const bool up = (t & k) == 0, lower = (t & j) == 0;
+            if (!active) continue;
             // ascending runs keep the smaller item at the lower position
-            if (lower == up ? lt_pad(y, x, arena) : lt_pad(x, y, arena)) x = y;
+            const bool want_smaller = ((t & j) == 0) == ((t & k) == 0);
+            bool y_less;
+            if (EXACT) {
+                y_less = lt_pad(y, x, arena);
+            } else {
+                const uint64_t ax = x.pad ? ~0ull : item_aux(x), ay = y.pad ? ~0ull : item_aux(y);
+                const bool heq = y.hi == x.hi, leq = y.lo == x.lo;
+                y_less = (y.hi < x.hi) | (heq & ((y.lo < x.lo) | (leq & (ay < ax))));
+                tie |= heq & leq & (x.len > 16u) & (y.len > 16u) & !(x.pad | y.pad);
+            }
+            if (want_smaller == y_less) x = y;
         }
     }
+    return tie;
 }
 
 constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by one workgroup
@@ -749,7 +765,7 @@ constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by on
 // power of two; oversized buckets (skewed sample) sort kBitonicMax chunks, then merge through memory.
 __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
                                                               const uint8_t* arena) {
-    __shared__ SortItem sh[kBitonicMax];  // 32 KiB exchange buffer
+    __shared__ SortItem sh[kBitonicMax];  // exchange buffer
     const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
     if (m <= 1) return;
     const int t = threadIdx.x;
@@ -757,10 +773,16 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
         const int cnt = min(kBitonicMax, m - c);
         int L = 2;
         while (L < cnt) L <<= 1;
-        SortItem x{};
-        x.pad = 1;
-        if (t < cnt) x = a[off + c + t];
-        reg_bitonic(x, sh, L, arena);
+        SortItem x0{};
+        x0.hi = x0.lo = ~0ull;  // padding sorts after every endpoint
+        x0.pad = 1;
+        if (t < cnt) x0 = a[off + c + t];
+        SortItem x = x0;
+        const bool tie = reg_bitonic<false>(x, sh, L, arena);
+        if (__syncthreads_or(tie)) {  // long keys sharing a 16-byte prefix: exact network
+            x = x0;
+            reg_bitonic<true>(x, sh, L, arena);
+        }
         if (t < cnt) a[off + c + t] = x;
         __syncthreads();
     }
