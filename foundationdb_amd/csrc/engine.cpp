@@ -81,7 +81,7 @@ struct HBuf {
 };
 
 enum Phase {
-    kPhStart, kPhUpload, kPhCheck, kPhSort, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge,
+    kPhStart, kPhUpload, kPhSort, kPhEdges, kPhCheck, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge,
     kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhCount
 };
 
@@ -91,7 +91,12 @@ struct fdbcs_batch;
 
 struct fdbcs_conflict_set {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // stage B: everything that reads or writes the history, in batch order
+    hipStream_t astream = nullptr;  // stage A: each batch's history-independent sort and candidate edges
+    hipEvent_t ev_a[2] = {};        // stage A of the batch using workspace k is done
+    hipEvent_t ev_b[2] = {};        // stage B (epilogue) of the batch using workspace k is done
+    bool wused[2] = {false, false};
+    int wpar = 0;                   // workspace of the next batch
     int timing = 0;       // 0: no events; 1: the copy kernels; 2: every phase (fdbcs_set_timing)
     uint32_t seq = 0;     // batches submitted (completion flag values)
     int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
@@ -121,16 +126,18 @@ struct fdbcs_conflict_set {
     int64_t tail_ub = 0;
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
-    // workspace
-    DBuf ws[40];
+    // two batch workspaces (alternating batches)
+    DBuf ws[2][41];
     int64_t ws_T = -1, ws_R = -1, ws_W = -1;
-    Work work{};
+    Work work[2]{};
     int64_t edge_cap = 0;
 
     int inflight = 0;
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
     int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket (testing knob; 0 = default)
     bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
+    bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
+    int sort_alg = 0;       // FDBCS_SORT_ALG: per-bucket sort (0 rank count, 1 bitonic network)
     DBuf trace_buf;
     fdbcs_stats stats{};
 };
@@ -161,6 +168,7 @@ struct fdbcs_batch {
     int32_t* h_first = nullptr;
     hipEvent_t ev[kPhCount] = {};
     bool events_made = false;
+    hipEvent_t ev_up = nullptr;  // upload done (recorded on stage A's stream)
     bool gc_ran = false;
     bool compacted = false;
     uint32_t seq = 0;
@@ -200,14 +208,25 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     if (cs->ws_T < 0 || cs->hist_cap <= 0) return FDBCS_OK;
     if (cs->delta_cap <= 0) return FDBCS_OK;
     const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
-    int rc = cs->ws[39].ensure(8 * words + 64);
-    if (rc) return rc;
-    cs->work.scan_arena = (uint64_t*)cs->ws[39].p;
-    if ((rc = cs->ws[38].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 1024 + 8)))) return rc;  // per copy tile
-    cs->work.tile_first = (int32_t*)cs->ws[38].p;
-    carve_scans(cs->work, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
-    HIPOK(hipMemsetAsync(cs->work.scan_arena, 0, 8 * cs->work.scan_words, cs->stream));
-    for (int k = 0; k < kNumScans; k++) cs->work.scan[k].error = &((Scalars*)cs->scal.p)->debug_error;
+    for (int k = 0; k < 2; k++) {
+        Work& w = cs->work[k];
+        int rc = cs->ws[k][39].ensure(8 * words + 64);
+        if (rc) return rc;
+        w.scan_arena = (uint64_t*)cs->ws[k][39].p;
+        if ((rc = cs->ws[k][38].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 1024 + 8)))) return rc;
+        w.tile_first = (int32_t*)cs->ws[k][38].p;
+        carve_scans(w, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
+        HIPOK(hipMemsetAsync(w.scan_arena, 0, 8 * w.scan_words, cs->stream));
+        for (int q = 0; q < kNumScans; q++) w.scan[q].error = &w.bsc->debug_error;
+    }
+    HIPOK(hipStreamSynchronize(cs->stream));
+    return FDBCS_OK;
+}
+
+// Both streams idle (before reallocating anything either stage uses).
+int sync_all(fdbcs_conflict_set* cs) {
+    HIPOK(hipStreamSynchronize(cs->astream));
+    HIPOK(hipStreamSynchronize(cs->stream));
     return FDBCS_OK;
 }
 
@@ -217,16 +236,17 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     T = std::max<int64_t>(T, std::max<int64_t>(cs->ws_T, 1024));
     R = std::max<int64_t>(R, std::max<int64_t>(cs->ws_R, 4096));
     W = std::max<int64_t>(W, std::max<int64_t>(cs->ws_W, 4096));
-    HIPOK(hipStreamSynchronize(cs->stream));
+    if (int rc = sync_all(cs)) return rc;
     const int64_t E = 2 * (R + W);
     int64_t edge_cap = std::max<int64_t>(16 * R, 1 << 22);
     if (const char* env = getenv("FDBCS_EDGE_CAP")) edge_cap = std::max<int64_t>(1, atoll(env));  // testing knob
-    Work& w = cs->work;
+    for (int k = 0; k < 2; k++) {
+    Work& w = cs->work[k];
     int i = 0;
     auto take = [&](size_t bytes, void** ptr) -> int {
-        int rc = cs->ws[i].ensure(bytes + 64);
+        int rc = cs->ws[k][i].ensure(bytes + 64);
         if (rc) return rc;
-        *ptr = cs->ws[i].p;
+        *ptr = cs->ws[k][i].p;
         i++;
         return FDBCS_OK;
     };
@@ -269,21 +289,30 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(seg_endins, W + 1);
     TAKE(seg_vend, 8 * (W + 1));
     TAKE(verdict, T);
+    TAKE(bsc, sizeof(BatchScalars));
 #undef TAKE
     w.edge_cap = edge_cap;
     w.cap_T = T;
     w.cap_R = R;
-    cs->edge_cap = edge_cap;
-    cs->ws_T = T;
-    cs->ws_R = R;
-    cs->ws_W = W;
-    // the epilogue of every batch re-zeroes these for the next one; start them zeroed
+    // the epilogue of every batch re-zeroes these for the batch after next; start them zeroed
     HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
     HIPOK(hipMemsetAsync(w.ecnt_b, 0, 4 * R, cs->stream));
     HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
     HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), cs->stream));
+    HIPOK(hipMemsetAsync(w.bsc, 0, sizeof(BatchScalars), cs->stream));
+    // compaction arrays are shared (stage B only)
+    if (k == 1) {
+        Work& w0 = cs->work[0];
+        w.c_lo = w0.c_lo, w.c_hi = w0.c_hi, w.c_rem = w0.c_rem, w.c_ins = w0.c_ins, w.c_val = w0.c_val;
+        w.c_exact = w0.c_exact;
+    }
+    }
+    cs->edge_cap = edge_cap;
+    cs->ws_T = T;
+    cs->ws_R = R;
+    cs->ws_W = W;
     return ensure_scan_arena(cs);
 }
 
@@ -399,16 +428,17 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
     int64_t cap = std::max<int64_t>(need, cs->delta_cap);
     cap = std::max<int64_t>(cap + cap / 2, 1 << 14);
     if ((rc = grow_sets(cs, cs->dkey, cs->dlt, cs->dver, cs->dcur, cs->nd_ub, cap))) return rc;
-    Work& w = cs->work;
-    int64_t** c64[5] = {&w.c_lo, &w.c_hi, &w.c_rem, &w.c_ins, &w.c_val};
     for (int k = 0; k < 5; k++) {
         cs->cws[k].release();
         if ((rc = cs->cws[k].ensure(8 * (cap + 2)))) return rc;
-        *c64[k] = (int64_t*)cs->cws[k].p;
     }
     cs->cws[5].release();
     if ((rc = cs->cws[5].ensure(cap + 2))) return rc;
-    w.c_exact = (uint8_t*)cs->cws[5].p;
+    for (Work& w : cs->work) {  // compaction runs on stage B only: both workspaces share the arrays
+        int64_t** c64[5] = {&w.c_lo, &w.c_hi, &w.c_rem, &w.c_ins, &w.c_val};
+        for (int k = 0; k < 5; k++) *c64[k] = (int64_t*)cs->cws[k].p;
+        w.c_exact = (uint8_t*)cs->cws[5].p;
+    }
     if ((rc = alloc_levels(cs->dlvl, cap, &cs->dlvl3_n))) return rc;
     cs->delta_cap = cap;
     launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->nd,
@@ -489,7 +519,10 @@ int do_upload(fdbcs_batch* b) {
     if (W) memcpy(h + o_keys + sizeof(DKey) * 2 * R, b->wkeys.data(), sizeof(DKey) * 2 * W);
     if (T) memcpy(h + o_flags, b->flags.data(), T);
     if (!b->tail.empty()) memcpy(h + o_tail, b->tail.data(), b->tail.size());
-    HIPOK(hipMemcpyAsync(b->dev.p, h, off, hipMemcpyHostToDevice, cs->stream));
+    // on stage A's stream (its kernels read the batch first); stage B waits for ev_up
+    if (!b->ev_up) HIPOK(hipEventCreateWithFlags(&b->ev_up, hipEventDisableTiming));
+    HIPOK(hipMemcpyAsync(b->dev.p, h, off, hipMemcpyHostToDevice, cs->astream));
+    HIPOK(hipEventRecord(b->ev_up, cs->astream));
     char* d = (char*)b->dev.p;
     b->bd.T = (int32_t)T;
     b->bd.R = (int32_t)R;
@@ -543,8 +576,15 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
     if (const char* v = getenv("FDBCS_SORT_BUCKET")) cs->bucket_target = atoi(v);
     if (const char* v = getenv("FDBCS_TRACE")) cs->trace = v[0] == '1';
-    if (hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete cs;
+    if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
+    if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
+    bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < 2 && ok; k++)
+        ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&cs->ev_b[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        fdbcs_destroy_conflict_set(cs);
         return FDBCS_E_DEVICE;
     }
 
@@ -565,6 +605,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
 void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (!cs) return;
     (void)hipSetDevice(cs->device);
+    if (cs->astream) (void)hipStreamSynchronize(cs->astream);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
     for (int k = 0; k < 2; k++) {
         cs->hkey[k].release();
@@ -578,9 +619,15 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     for (auto& l : cs->lvl) l.release();
     for (auto& l : cs->dlvl) l.release();
     for (auto& x : cs->cws) x.release();
-    for (auto& x : cs->ws) x.release();
+    for (auto& set : cs->ws)
+        for (auto& x : set) x.release();
     cs->scal.release();
     cs->trace_buf.release();
+    for (int k = 0; k < 2; k++) {
+        if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
+        if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
+    }
+    if (cs->astream) (void)hipStreamDestroy(cs->astream);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -588,7 +635,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
 int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     if (!cs) return FDBCS_E_INVALID;
     HIPOK(hipSetDevice(cs->device));
-    HIPOK(hipStreamSynchronize(cs->stream));
+    if (int rc = sync_all(cs)) return rc;
     HIPOK(hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = version;
@@ -730,11 +777,16 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
     if (!b) return;
     if (b->state == 2) {  // still in flight: its set (which must outlive it) owns the stream
         (void)hipSetDevice(b->cs->device);
+        (void)hipStreamSynchronize(b->cs->astream);
         (void)hipStreamSynchronize(b->cs->stream);
         b->cs->inflight--;
+    } else if (b->state == 1) {  // uploaded, never submitted: the copy may still be in flight
+        (void)hipSetDevice(b->cs->device);
+        (void)hipStreamSynchronize(b->cs->astream);
     }
     if (b->events_made)
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(b->ev[i]);
+    if (b->ev_up) (void)hipEventDestroy(b->ev_up);
     b->dev.release();
     b->dverdict.release();
     b->pin_in.release();
@@ -887,6 +939,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
 
     hipStream_t s = cs->stream;
     const int timing = cs->timing;
+    // Stage A (sort, positions, candidate edges) depends only on this batch: it runs on its own
+    // stream and overlaps stage B of the previous batch.  Phase timing (level 2) runs both stages on
+    // one stream so the phases are measured one after another.
+    hipStream_t sa = (timing >= 2 || cs->serial) ? s : cs->astream;
+    const int wp = cs->wpar;
+    cs->wpar ^= 1;
+    Work& w = cs->work[wp];
     // phase events: level 2 records every phase, level 1 only the copy kernels (roofline)
     auto rec = [&](int ph, int level) -> hipEvent_t {
         if (timing < level) return nullptr;
@@ -898,10 +957,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         return FDBCS_OK;
     };
     if ((rc = mark(kPhStart))) return rc;
+    // workspace wp was last used by the batch before the previous one: its epilogue re-zeroed it
+    if (cs->wused[wp] && sa != s) HIPOK(hipStreamWaitEvent(sa, cs->ev_b[wp], 0));
+    cs->wused[wp] = true;
     if (b->state == 0 && (rc = do_upload(b))) return rc;
+    if (sa == s || hipEventQuery(b->ev_up) != hipSuccess) HIPOK(hipStreamWaitEvent(s, b->ev_up, 0));
     if ((rc = mark(kPhUpload))) return rc;
     const BatchDev& bd = b->bd;
-    Work& w = cs->work;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
@@ -910,22 +972,28 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
 
     w.trace = cs->trace ? (unsigned long long*)cs->trace_buf.p : nullptr;
     if (w.trace) {
+        HIPOK(hipStreamSynchronize(cs->astream));
+        HIPOK(hipStreamSynchronize(s));
         unsigned long long init[kTrSlots];
         for (int i = 0; i < kTrSlots; i++)
             init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin) ? ~0ull : 0ull;
-        HIPOK(hipMemcpyAsync(w.trace, init, sizeof(init), hipMemcpyHostToDevice, s));  // staged before return
-        HIPOK(hipStreamSynchronize(s));
+        HIPOK(hipMemcpy(w.trace, init, sizeof(init), hipMemcpyHostToDevice));
     }
-    // D.CheckRead rides in the same launch as the sort's sample ranking (independent workgroups)
-    launch_sample_check(s, bd, w, base, delta, htail, cs->bucket_target);
-    if ((rc = mark(kPhCheck))) return rc;
+    // ---- stage A: D.Sort and the candidate edges of D.CheckIntraBatch
+    launch_sample(sa, bd, w, cs->bucket_target);
     int sorted = 0;
-    launch_sort_points(s, bd, w, cs->bucket_target, &sorted);
+    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sort_alg, &sorted);
     if ((rc = mark(kPhSort))) return rc;
-    launch_positions(s, bd, w, sorted);
-    if (cs->validate) launch_validate_sort(s, bd, w, sorted, sc);
-    launch_edges(s, bd, w, sc);
-    launch_resolve(s, bd, w, sc, b->any_report);
+    launch_positions(sa, bd, w, sorted);
+    if (cs->validate) launch_validate_sort(sa, bd, w, sorted);
+    launch_edges(sa, bd, w);
+    if (sa != s) HIPOK(hipEventRecord(cs->ev_a[wp], sa));
+    if ((rc = mark(kPhEdges))) return rc;
+    // ---- stage B: D.CheckRead against the history the previous batch left, then batch order
+    launch_check(s, bd, w, base, delta, htail);
+    if ((rc = mark(kPhCheck))) return rc;
+    if (sa != s) HIPOK(hipStreamWaitEvent(s, cs->ev_a[wp], 0));
+    launch_resolve(s, bd, w, b->any_report);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf
         if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
         HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
@@ -970,6 +1038,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
                     gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)b->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1);
+    if (sa != s) HIPOK(hipEventRecord(cs->ev_b[wp], s));
     if ((rc = mark(kPhEpilogue))) return rc;
     HIPOK(hipGetLastError());
     if ((rc = mark(kPhEnd))) return rc;
@@ -997,7 +1066,8 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         // the epilogue's last workgroup publishes b->seq; poll it (checking the stream for errors)
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
             if ((spin & 1023) == 1023) {
-                const hipError_t e = hipStreamQuery(cs->stream);
+                hipError_t e = hipStreamQuery(cs->astream);
+                if (e == hipSuccess || e == hipErrorNotReady) e = hipStreamQuery(cs->stream);
                 if (e != hipSuccess && e != hipErrorNotReady) {
                     fprintf(stderr, "fdbcs: stream error while waiting: %s\n", hipGetErrorString(e));
                     return FDBCS_E_DEVICE;
@@ -1010,7 +1080,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         if (cs->trace && cs->inflight == 1) {
-            HIPOK(hipStreamSynchronize(cs->stream));
+            if (int rc = sync_all(cs)) return rc;
             unsigned long long tr[kTrSlots];
             HIPOK(hipMemcpy(tr, cs->trace_buf.p, sizeof(tr), hipMemcpyDeviceToHost));
             auto us = [&](int a, int z) { return (double)((long long)(tr[z] - tr[a])) / 100.0; };  // 100 MHz
@@ -1019,7 +1089,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                 int nb = (E + 127) / 128;
                 nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
                 std::vector<int32_t> bo(nb + 1);
-                HIPOK(hipMemcpy(bo.data(), cs->work.boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
+                HIPOK(hipMemcpy(bo.data(), cs->work[cs->wpar ^ 1].boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
                 int mx = 0, over = 0;
                 for (int k = 0; k < nb; k++) {
                     const int sz = bo[k + 1] - bo[k];
@@ -1085,9 +1155,9 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             return ((b->recorded >> a) & (b->recorded >> z) & 1u) ? ev_ms(b->ev[a], b->ev[z]) : 0.0;
         };
         st.ms_upload += ph(kPhStart, kPhUpload);
-        st.ms_check_read += ph(kPhUpload, kPhCheck);  // includes the sort's sample ranking (same launch)
-        st.ms_sort += ph(kPhCheck, kPhSort);
-        st.ms_intra += ph(kPhSort, kPhIntra);
+        st.ms_sort += ph(kPhUpload, kPhSort);
+        st.ms_intra += ph(kPhSort, kPhEdges) + ph(kPhCheck, kPhIntra);
+        st.ms_check_read += ph(kPhEdges, kPhCheck);
         st.ms_combine += ph(kPhIntra, kPhCombine);
         st.ms_merge += ph(kPhCombine, kPhMerge);
         st.ms_compact += ph(kPhMerge, kPhCompact);

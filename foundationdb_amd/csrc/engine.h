@@ -62,11 +62,18 @@ struct Scalars {
     int64_t tail_used;     // bytes used in the history tail arena
     int64_t tail_next;
     int64_t n_segments;    // union segments of committed writes
-    int64_t n_edges;       // candidate edges
     int64_t d_before;      // delta size at the start of the merge
     int64_t d_rem;         // delta boundaries removed by union segments
     int64_t c_before;      // base size at the start of a compaction
     int64_t c_rem;         // base boundaries removed (overwritten) by the compaction
+    int32_t debug_error;   // copied from the batch's BatchScalars by the epilogue (host view only)
+    int32_t pad;
+};
+
+// Device scalars of one batch workspace (two workspaces alternate, so batch i+1's history-
+// independent stage can run while batch i finishes).
+struct BatchScalars {
+    int64_t n_edges;       // candidate edges
     int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
@@ -148,6 +155,7 @@ struct Work {
     uint8_t* seg_endins;
     int64_t* seg_vend;
     uint8_t* verdict;      // [T]
+    BatchScalars* bsc;
     ScanState scan[kNumScans];
     uint64_t* scan_arena;  // zeroed by the previous batch's epilogue (and at allocation)
     int64_t scan_words;
@@ -183,15 +191,23 @@ struct Tier {
     const int64_t* n;  // device size
     int64_t hdr;       // version below the first boundary (kHole for the delta)
 };
-// Sample ranking for the sort's splitters and D.CheckRead in one launch (independent roles).
-void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                         const uint8_t* htail, int bucket_target);
+// Per batch, two stages on two streams:
+//   A (history-independent): launch_sample, launch_sort_points, launch_positions, launch_edges;
+//   B (reads/writes the history, in batch order): launch_check, launch_resolve, launch_combine,
+//     launch_merge, launch_compact/gc, launch_epilogue.
+// Sample ranking for the sort's splitters.
+void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target);
+// D.CheckRead against the history the previous batch left.
+void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
+                  const uint8_t* htail);
 // bucket_target: endpoints per sample-sort bucket (0 = default 256; tests force oversized buckets).
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int* result_buffer);
+// alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int alg,
+                        int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
-void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc);
-void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, bool report);
+void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
+void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report);
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 // `srcm` are the source tier's levels: its key index is searched, its top level reset for the

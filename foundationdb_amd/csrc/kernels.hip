@@ -542,10 +542,10 @@ __device__ __noinline__ int rank_exact(const SortItem* sh, int cnt, SortItem min
 
 // ---- sample sort of the batch endpoints (D.Sort, SkipList.cpp:161-208)
 //
-// 1. k_sample_rank: S evenly spaced endpoints are ranked against each other (each workgroup
-//    compares every sample with a 64-sample slice and adds partial ranks); the last workgroup to
-//    finish writes the nb-1 splitters (the samples of rank k*S/nb) straight from the ranks.
-// 2. k_bucket_count: each endpoint's bucket = number of splitters <= it; per-bucket counts.
+// 1. k_sample: S evenly spaced endpoints are ranked against each other (each workgroup compares
+//    every sample with a 64-sample slice and adds partial ranks).
+// 2. k_bucket_count: every workgroup picks the nb-1 splitters (the samples of rank k*S/nb) straight
+//    from the ranks into LDS; each endpoint's bucket = number of splitters <= it; per-bucket counts.
 // 3. k_bucket_scatter: bucket offsets (prefix of the counts, recomputed per workgroup) and scatter.
 // 4. k_bucket_sort: one workgroup per bucket (~256 endpoints) ranks its items in LDS and writes
 //    each to its final slot; oversized buckets rank 1024-item chunks, then merge through memory.
@@ -556,34 +556,18 @@ constexpr int kBucketTarget = 128;
 
 __device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((int64_t)i * E) / S); }
 
-// One launch, two independent roles (no stream fork/join needed for the overlap):
-//  * workgroups [0, n_sample_wg): sample ranking -- workgroup (x, y) ranks samples
-//    [y*256, y*256+256) against the slice [x*64, x*64+64); partial ranks are added atomically and the
-//    last of these workgroups writes the nb-1 splitters (the samples of rank k*S/nb);
-//  * workgroups after them: D.CheckRead, one thread per read range.
-struct SampleCheck {
-    int S, nb, n_sample_wg, n_slice;
-    int32_t* srank;  // [S] partial ranks, [kMaxSample] done counter
-    SortItem* splitters;
-    Tier base, delta;
-    const uint8_t* htail;
-    uint8_t *hist_conf, *rconf;
+// Sample ranking (stage A, history-independent): workgroup (x, y) ranks samples [y*256, y*256+256)
+// against the slice [x*64, x*64+64); partial ranks are added atomically.
+struct SampleRank {
+    int S, n_slice;
+    int32_t* srank;  // [S] ranks (zeroed by the previous epilogue on this workspace)
     unsigned long long* trace;
 };
 
-__global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck c) {
+__global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
     __shared__ SortItem sl[kSampleSlice];
-    __shared__ int s_last;
-    if ((int)blockIdx.x >= c.n_sample_wg) {
-        if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
-        const int64_t slot = (int64_t)(blockIdx.x - c.n_sample_wg) * blockDim.x + threadIdx.x;
-        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
-        __syncthreads();
-        if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
-        return;
-    }
     if (threadIdx.x == 0) trace_min(c.trace, kTrSampleBegin);
-    const int E = 2 * (b.R + b.W), S = c.S, nb = c.nb;
+    const int E = 2 * (b.R + b.W), S = c.S;
     const int x = blockIdx.x % c.n_slice, y = blockIdx.x / c.n_slice;
     const int j0 = x * kSampleSlice;
     const int cj = min(kSampleSlice, S - j0);
@@ -598,20 +582,32 @@ __global__ __launch_bounds__(kBlock) void k_sample_check(BatchDev b, SampleCheck
         if (tail) cnt[0] = rank_exact(sl, cj, mine[0], b.tail);
         if (cnt[0]) atomicAdd(&c.srank[i], cnt[0]);
     }
-    // the last sampling workgroup to finish sees every partial rank and writes the splitters
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&c.srank[kMaxSample], 1) == c.n_sample_wg - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    for (int q = threadIdx.x; q < S; q += blockDim.x) {
-        const int r = __hip_atomic_load(&c.srank[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int k = (int)(((int64_t)r * nb + S - 1) / S);  // the splitter index whose rank would be r
-        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) c.splitters[k - 1] = make_item(b, sample_pos(q, E, S));
-    }
-    __syncthreads();
     if (threadIdx.x == 0) trace_max(c.trace, kTrSampleEnd);
+}
+
+// Number of samples for nb buckets (about 8 per bucket: the largest of ~550 buckets stays well
+// under the one-pass bitonic size).
+__host__ __device__ inline int sample_count(int E, int nb) {
+    int S = 8 * nb;
+    S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
+    return S > E ? E : S;
+}
+
+// D.CheckRead (stage B: reads the history as the previous batch left it), kReadLanes lanes per
+// read range.
+struct CheckReads {
+    Tier base, delta;
+    const uint8_t* htail;
+    uint8_t *hist_conf, *rconf;
+    unsigned long long* trace;
+};
+
+__global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c) {
+    if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
 
 __device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl, int nsplit, const uint8_t* arena) {
@@ -626,14 +622,20 @@ __device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl
     return lo;
 }
 
-__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const SortItem* splitters, int nb,
+__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32_t* srank, int nb,
                                                          uint16_t* bucket, int32_t* bcount, const uint8_t* arena) {
     __shared__ SortItem spl[kMaxBuckets - 1];
     __shared__ int hist[kMaxBuckets];
-    for (int i = threadIdx.x; i < nb - 1; i += blockDim.x) spl[i] = splitters[i];
+    const int E = 2 * (b.R + b.W);
+    const int S = sample_count(E, nb);
+    // splitter k-1 is the sample of rank k*S/nb (ranks are distinct: items are totally ordered)
+    for (int q = threadIdx.x; q < S; q += blockDim.x) {
+        const int r = srank[q];
+        const int k = (int)(((int64_t)r * nb + S - 1) / S);
+        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) spl[k - 1] = make_item(b, sample_pos(q, E, S));
+    }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    const int E = 2 * (b.R + b.W);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p < E) {
         const int k = bucket_of(make_item(b, p), spl, nb - 1, arena);
@@ -763,12 +765,29 @@ constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by on
 
 // Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic network padded to a
 // power of two; oversized buckets (skewed sample) sort kBitonicMax chunks, then merge through memory.
+template <int ALG>
 __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
                                                               const uint8_t* arena) {
     __shared__ SortItem sh[kBitonicMax];  // exchange buffer
     const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
     if (m <= 1) return;
     const int t = threadIdx.x;
+    if (ALG == 0 && m <= kBitonicMax) {
+        // rank count: every item counts the items ordered before it (one pass over the bucket in
+        // LDS, broadcast reads, no barriers) and goes straight to its slot
+        SortItem x{};
+        if (t < m) sh[t] = x = a[off + t];
+        __syncthreads();
+        if (t < m) {
+            SortItem mine[1] = {x};
+            int rk[1] = {0};
+            bool tail = false;
+            rank_count<1>(sh, m, mine, rk, tail);
+            if (tail) rk[0] = rank_exact(sh, m, x, arena);
+            a[off + rk[0]] = x;
+        }
+        return;
+    }
     for (int c = 0; c < m; c += kBitonicMax) {
         const int cnt = min(kBitonicMax, m - c);
         int L = 2;
@@ -817,42 +836,41 @@ int sort_buckets(int E, int target) {
     return nb > kMaxBuckets ? kMaxBuckets : nb;
 }
 
-void launch_sample_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                         const uint8_t* htail, int bucket_target) {
+void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target) {
     const int E = 2 * (b.R + b.W);
     const int nb = E ? sort_buckets(E, bucket_target) : 1;
-    SampleCheck c{};
-    if (nb > 1) {
-        int S = 4 * nb;
-        S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
-        S = S > E ? E : S;
-        c.S = S;
-        c.nb = nb;
-        c.n_slice = (S + kSampleSlice - 1) / kSampleSlice;
-        c.n_sample_wg = c.n_slice * ((S + kBlock - 1) / kBlock);
-    }
+    if (nb <= 1) return;
+    SampleRank c{};
+    c.S = sample_count(E, nb);
+    c.n_slice = (c.S + kSampleSlice - 1) / kSampleSlice;
     c.srank = w.srank;
-    c.splitters = w.splitters;
-    c.base = base;
-    c.delta = delta;
-    c.htail = htail;
-    c.hist_conf = w.hist_conf;
-    c.rconf = w.rconf;
     c.trace = w.trace;
-    const int grid = c.n_sample_wg + (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
-    if (grid > 0) hipLaunchKernelGGL(k_sample_check, dim3(grid), dim3(kBlock), 0, s, b, c);
+    const int grid = c.n_slice * ((c.S + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_sample, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int* result_buffer) {
+void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
+                  const uint8_t* htail) {
+    if (b.R == 0) return;
+    CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
+    const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
+}
+
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int alg,
+                        int* result_buffer) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
     const int nb = sort_buckets(E, bucket_target);
     const int grid = (E + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.splitters, nb, w.bucket, w.bcount, b.tail);
+    hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
-    hipLaunchKernelGGL(k_bucket_sort, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    if (alg == 1)
+        hipLaunchKernelGGL(k_bucket_sort<1>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    else
+        hipLaunchKernelGGL(k_bucket_sort<0>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
 }
 
 // ------------------------------------------------------------------ positions
@@ -890,7 +908,7 @@ struct PosScan {
 // FDBCS_VALIDATE=1: check the endpoint order and that positions invert the permutation.
 __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted, const int32_t* pos,
                                                           const uint32_t* pmeta, int E, const uint8_t* arena,
-                                                          Scalars* sc) {
+                                                          BatchScalars* sc) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= E) return;
     bool bad = p > 0 && !item_less_total(sorted[p - 1], sorted[p], arena);
@@ -906,7 +924,8 @@ void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorte
     launch_scan<2>(s, f, nullptr, E, w.scan[kScanPos]);
 }
 
-void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf, Scalars* sc) {
+void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
+    BatchScalars* sc = w.bsc;
     const int E = 2 * (b.R + b.W);
     if (E == 0) return;
     hipLaunchKernelGGL(k_validate_sort, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf],
@@ -921,18 +940,14 @@ void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int s
 // pair is one candidate edge t' -> t: t aborts iff some candidate writer commits.
 
 template <bool FILL>
-__global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scalars* sc) {
+__global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= b.R + b.W) return;
-    if (FILL && sc->edge_overflow) return;
+    if (FILL && w.bsc->edge_overflow) return;
     const int R = b.R;
     if (g < R) {
         const int r = g;
         const int t = b.rowner[r];
-        if (w.hist_conf[t]) {
-            if (!FILL) w.ecnt_a[r] = 0;
-            return;
-        }
         const int rb = w.pos[2 * r], re = w.pos[2 * r + 1];
         int cnt = 0;
         if (rb < re) {
@@ -942,7 +957,7 @@ __global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scal
                 const int p = w.wbpos[k];
                 const int wr = (int)item_range(w.pmeta[p]) - R;
                 const int tw = b.wowner[wr];
-                if (tw < t && !w.hist_conf[tw] && w.pos[2 * (R + wr)] < w.pos[2 * (R + wr) + 1]) {
+                if (tw < t && w.pos[2 * (R + wr)] < w.pos[2 * (R + wr) + 1]) {
                     if (FILL) w.edges[out + cnt] = tw;
                     cnt++;
                 }
@@ -952,7 +967,6 @@ __global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scal
     } else {
         const int wr = g - R;
         const int tw = b.wowner[wr];
-        if (w.hist_conf[tw]) return;
         const int wb = w.pos[2 * g], we = w.pos[2 * g + 1];
         if (wb >= we) return;
         const int k0 = w.crb[wb], k1 = w.crb[we];
@@ -960,7 +974,7 @@ __global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w, const Scal
             const int p = w.rbpos[k];
             const int r = (int)item_range(w.pmeta[p]);
             const int t = b.rowner[r];
-            if (tw < t && !w.hist_conf[t] && w.pos[2 * r] < w.pos[2 * r + 1]) {
+            if (tw < t && w.pos[2 * r] < w.pos[2 * r + 1]) {
                 if (FILL) {
                     const int slot = atomicAdd(&w.ecur[r], 1);
                     w.edges[w.eoff[r] + w.ecnt_a[r] + slot] = tw;
@@ -978,7 +992,7 @@ struct EdgeOffsetScan {
     int32_t* eoff;
     int32_t R;
     int64_t cap;
-    Scalars* sc;
+    BatchScalars* sc;
     __device__ void load(int64_t r, uint32_t (&v)[1]) const { v[0] = (uint32_t)(a[r] + b[r]); }
     __device__ void store(int64_t r, const uint32_t (&ex)[1]) const { eoff[r] = (int32_t)ex[0]; }
     __device__ void finish(const uint32_t (&tot)[1]) const {
@@ -988,12 +1002,12 @@ struct EdgeOffsetScan {
     }
 };
 
-void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
+void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    if (G) hipLaunchKernelGGL(k_edges<false>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
-    EdgeOffsetScan f{w.ecnt_a, w.ecnt_b, w.eoff, b.R, w.edge_cap, sc};
+    if (G) hipLaunchKernelGGL(k_edges<false>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
+    EdgeOffsetScan f{w.ecnt_a, w.ecnt_b, w.eoff, b.R, w.edge_cap, w.bsc};
     launch_scan<1>(s, f, nullptr, b.R, w.scan[kScanEdges]);
-    if (G) hipLaunchKernelGGL(k_edges<true>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
+    if (G) hipLaunchKernelGGL(k_edges<true>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
 // ------------------------------------------------------------------ D.CheckIntraBatch: resolution
@@ -1004,7 +1018,8 @@ void launch_edges(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) 
 // rounds terminate.  If the candidate edges overflowed, the workgroup replays MiniConflictSet
 // sequentially over point indices instead (exact, slower).
 
-__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, Scalars* sc) {
+__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
+    BatchScalars* sc = w.bsc;
     extern __shared__ __attribute__((aligned(16))) uint8_t st[];
     __shared__ int s_more;
     const int T = b.T;
@@ -1115,7 +1130,8 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, Scalars* sc
 
 // First conflicting read index of intra-batch aborts that report conflicting keys
 // (SkipList.cpp:821-828).
-__global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w, const Scalars* sc) {
+__global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
+    const BatchScalars* sc = w.bsc;
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= b.R || sc->edge_overflow) return;
     const int t = b.rowner[r];
@@ -1128,10 +1144,10 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w, con
     }
 }
 
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc, bool report) {
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report) {
     if (b.T == 0) return;
-    hipLaunchKernelGGL(k_resolve, dim3((b.T + kWG - 1) / kWG), dim3(kWG), (size_t)b.T, s, b, w, sc);
-    if (b.R && report) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, sc);
+    hipLaunchKernelGGL(k_resolve, dim3((b.T + kWG - 1) / kWG), dim3(kWG), (size_t)b.T, s, b, w);
+    if (b.R && report) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
 // ------------------------------------------------------------------ D.Combine
@@ -1623,6 +1639,7 @@ struct Epilogue {
     int32_t* zero_bc;  // sample-sort bucket counts and cursors [kMaxBuckets]
     int32_t* zero_bk;
     int32_t* zero_rank;  // sample ranks + done counter [kMaxSample + 64]
+    BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
 };
 
 // Range-max levels over lvl[0][0, n0) (lvl[3] reset beforehand); with a batch attached, also the
@@ -1736,8 +1753,10 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
             sc->nd = sc->nd_next;
         }
         sc->tail_used = sc->tail_next;
-        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = *sc;
-        sc->debug_error = 0;
+        Scalars out = *sc;
+        out.debug_error = ep.bsc->debug_error;
+        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;
+        ep.bsc->debug_error = 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiHost);
@@ -1793,6 +1812,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.zero_bc = w.bcount;
     ep.zero_bk = w.bcursor;
     ep.zero_rank = w.srank;
+    ep.bsc = w.bsc;
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
     hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
