@@ -35,7 +35,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     objs = []
     hipcc = _hipcc()
-    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+              "-mllvm", "-disable-promote-alloca-to-lds"]
     for src in SOURCES:
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
         cmd = [hipcc, *common, "-c", os.path.join(CSRC, src), "-o", obj]

@@ -773,18 +773,41 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
     if (m <= 1) return;
     const int t = threadIdx.x;
     if (ALG == 0 && m <= kBitonicMax) {
-        // rank count: every item counts the items ordered before it (one pass over the bucket in
-        // LDS, broadcast reads, no barriers) and goes straight to its slot
+        // Rank count on the high key word: rank = #items whose hi word is smaller, exact whenever no
+        // other item of the bucket shares my hi word (distinct keys: the common case).  Items that
+        // share it add the exact comparisons against exactly those items (hot keys, long prefixes).
+        // Two items per LDS read, two VALU ops per comparison.
+        __shared__ __attribute__((aligned(16))) uint64_t shi[kBitonicMax];
         SortItem x{};
-        if (t < m) sh[t] = x = a[off + t];
+        if (t < m) {
+            sh[t] = x = a[off + t];
+            shi[t] = x.hi;
+        }
         __syncthreads();
         if (t < m) {
-            SortItem mine[1] = {x};
-            int rk[1] = {0};
-            bool tail = false;
-            rank_count<1>(sh, m, mine, rk, tail);
-            if (tail) rk[0] = rank_exact(sh, m, x, arena);
-            a[off + rk[0]] = x;
+            int lt = 0, eq = 0;
+            const uint64_t mh = x.hi;
+            int j = 0;
+            for (; j + 8 <= m; j += 8) {
+                ulonglong2 p[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    lt += (p[u].x < mh) + (p[u].y < mh);
+                    eq += (p[u].x == mh) + (p[u].y == mh);
+                }
+            }
+            for (; j < m; j++) {
+                const uint64_t h = shi[j];
+                lt += h < mh;
+                eq += h == mh;
+            }
+            if (eq > 1) {  // another item shares my hi word: order those exactly
+                for (int q = 0; q < m; q++)
+                    if (shi[q] == mh && q != t && item_less_total(sh[q], x, arena)) lt++;
+            }
+            a[off + lt] = x;
         }
         return;
     }

@@ -20,14 +20,61 @@ using namespace fdbcs;
         }                                                                            \
     } while (0)
 
+__device__ unsigned long long g_wgtime[4096][2];
+__device__ unsigned long long g_wgclk[4096][2];
 __global__ void k_empty() {}
+// LDS loop calibration: cycles per iteration of a compare-count loop over LDS, per wave
+template <int MODE>
+__global__ void k_ldsloop(unsigned long long* out, int iters) {
+    __shared__ uint64_t sh[256];
+    __shared__ uint32_t sw[256];
+    const int t = threadIdx.x;
+    sh[t] = (uint64_t)t * 0x9E3779B97F4A7C15ull;
+    sw[t] = t;
+    __syncthreads();
+    const uint64_t mh = sh[(t * 7) & 255];
+    const uint32_t mw = sw[(t * 7) & 255];
+    int r = 0;
+    const unsigned long long c0 = clock64();
+    if (MODE == 0) {  // broadcast reads, one dependent chain
+        for (int j = 0; j < iters; j++) r += sh[j & 255] < mh;
+    } else if (MODE == 1) {  // broadcast reads, 3 fields like the rank compare
+        for (int j = 0; j < iters; j++) {
+            const uint64_t h = sh[j & 255], l = sh[(j + 1) & 255];
+            const uint32_t w = sw[j & 255];
+            r += (h < mh) | ((h == mh) & ((l < mh) | ((l == mh) & (w < mw))));
+        }
+    } else {  // 8 loads in flight
+        for (int j = 0; j < iters; j += 8) {
+            uint64_t h[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) h[u] = sh[(j + u) & 255];
+#pragma unroll
+            for (int u = 0; u < 8; u++) r += h[u] < mh;
+        }
+    }
+    const unsigned long long c1 = clock64();
+    if (t == 0) out[blockIdx.x] = c1 - c0;
+    if (r == 12345) out[1000] = r;
+}
+// shader clock vs the 100 MHz wall clock over a busy loop
+__global__ void k_clock(unsigned long long* out, int iters) {
+    const unsigned long long c0 = clock64(), w0 = wall_clock64();
+    float x = threadIdx.x;
+    for (int i = 0; i < iters; i++) x = x * 1.0001f + 0.5f;
+    const unsigned long long c1 = clock64(), w1 = wall_clock64();
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        out[0] = c1 - c0;
+        out[1] = w1 - w0;
+        out[2] = (unsigned long long)x;
+    }
+}
 __global__ void k_copy_items(const SortItem* a, SortItem* b, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) b[i] = a[i];
 }
 
 // probe: one workgroup per bucket, load -> LDS -> (optional rank count) -> store
-__device__ unsigned long long g_wgtime[4096][2];
 template <int NT, int MODE>
 __global__ __launch_bounds__(NT) void k_probe_bucket(SortItem* a, const int32_t* boff, const uint8_t* arena,
                                                      SortItem* out = nullptr) {
@@ -59,6 +106,194 @@ __global__ __launch_bounds__(NT) void k_probe_bucket(SortItem* a, const int32_t*
     if (threadIdx.x == 0) g_wgtime[blockIdx.x][1] = wall_clock64();
 }
 
+// bitonic network alone, NT threads per bucket workgroup (buckets larger than NT skipped)
+template <int NT, int MODE>
+__global__ __launch_bounds__(NT) void k_bitonic_probe(SortItem* a, const int32_t* boff, const uint8_t* arena) {
+    __shared__ SortItem sh[NT];
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][0] = wall_clock64();
+    const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
+    const int t = threadIdx.x;
+    if (m > 1 && m <= NT) {
+        int L = 2;
+        while (L < m) L <<= 1;
+        SortItem x{};
+        x.hi = x.lo = ~0ull;
+        x.pad = 1;
+        if (t < m) x = a[off + t];
+        if (MODE == 0) reg_bitonic<false>(x, sh, L, arena);
+        if (t < m) a[off + t] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][1] = wall_clock64();
+}
+
+// rank sort over SoA LDS copies of (hi, lo, tie word); exact when no two items of the bucket share
+// (hi, lo) with both longer than 16 bytes (the probe ignores that case)
+__device__ __forceinline__ uint32_t tie_word(const SortItem& x) {
+    const uint32_t l = x.len > 16u ? 17u : x.len;
+    const uint32_t p = 2u * item_range(x.meta) + item_is_end(x.meta);
+    return (l << 27) | (item_class(x.meta) << 25) | p;
+}
+template <int NT, int MODE>
+__global__ __launch_bounds__(NT) void k_rank_probe(const SortItem* a, SortItem* out, const int32_t* boff) {
+    __shared__ uint64_t shi[NT], slo[NT];
+    __shared__ uint32_t stw[NT];
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][0] = wall_clock64();
+    const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
+    const int t = threadIdx.x;
+    if (m > 1 && m <= NT) {
+        SortItem x{};
+        uint32_t tw = 0;
+        if (t < m) {
+            x = a[off + t];
+            tw = tie_word(x);
+            shi[t] = x.hi;
+            slo[t] = x.lo;
+            stw[t] = tw;
+        }
+        __syncthreads();
+        if (t < m) {
+            int r = 0;
+            if (MODE == 0) {
+                for (int j = 0; j < m; j++) {
+                    const uint64_t h = shi[j], l = slo[j];
+                    const uint32_t w = stw[j];
+                    r += (h < x.hi) | ((h == x.hi) & ((l < x.lo) | ((l == x.lo) & (w < tw))));
+                }
+            } else {  // hi word decides; ties in hi fall back per pair
+                for (int j = 0; j < m; j++) {
+                    const uint64_t h = shi[j];
+                    int lt = h < x.hi;
+                    if (h == x.hi) {
+                        const uint64_t l = slo[j];
+                        lt = (l < x.lo) | ((l == x.lo) & (stw[j] < tw));
+                    }
+                    r += lt;
+                }
+            }
+            out[off + r] = x;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][1] = wall_clock64();
+}
+
+// rank sort, register-blocked: each wave pulls a 64-item chunk of the bucket into its lanes and
+// every lane compares its own item with the chunk's items one lane at a time (readlane -> SGPR)
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int q) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, q);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), q);
+    return ((uint64_t)hi << 32) | lo;
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rank_reg(const SortItem* a, SortItem* out, const int32_t* boff) {
+    __shared__ uint64_t shi[NT], slo[NT];
+    __shared__ uint32_t stw[NT];
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][0] = wall_clock64();
+    if (threadIdx.x == 0) g_wgclk[blockIdx.x][0] = clock64();
+    const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
+    const int t = threadIdx.x, lane = t & 63;
+    if (m > 1 && m <= NT) {
+        SortItem x{};
+        uint32_t tw = 0;
+        if (t < m) {
+            x = a[off + t];
+            tw = tie_word(x);
+            shi[t] = x.hi;
+            slo[t] = x.lo;
+            stw[t] = tw;
+        }
+        __syncthreads();
+        if ((t & ~63) < m) {  // wave has items
+            int r = 0;
+            for (int c = 0; c < m; c += 64) {
+                const int j = c + lane;
+                const uint64_t hv = j < m ? shi[j] : ~0ull, lv = j < m ? slo[j] : ~0ull;
+                const uint32_t wv = j < m ? stw[j] : ~0u;
+                const int cnt = m - c < 64 ? m - c : 64;
+                for (int q = 0; q < cnt; q++) {
+                    const uint64_t H = rl64(hv, q), L = rl64(lv, q);
+                    const uint32_t Wd = __builtin_amdgcn_readlane(wv, q);
+                    r += (H < x.hi) | ((H == x.hi) & ((L < x.lo) | ((L == x.lo) & (Wd < tw))));
+                }
+            }
+            if (t < m) out[off + r] = x;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) g_wgclk[blockIdx.x][1] = clock64();
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][1] = wall_clock64();
+}
+
+// rank sort with the comparisons of each item split over G = NT / m threads (LDS partial ranks)
+template <int NT, int U>
+__global__ __launch_bounds__(NT) void k_rank_split(const SortItem* a, SortItem* out, const int32_t* boff) {
+    __shared__ uint64_t shi[NT], slo[NT];
+    __shared__ uint32_t stw[NT];
+    __shared__ int srk[NT];
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][0] = wall_clock64();
+    const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
+    const int t = threadIdx.x;
+    if (m > 1 && m <= NT) {
+        SortItem x{};
+        if (t < m) {
+            x = a[off + t];
+            shi[t] = x.hi;
+            slo[t] = x.lo;
+            stw[t] = tie_word(x);
+            srk[t] = 0;
+        }
+        __syncthreads();
+        const int G = NT / m;
+        const int i = t % m, g = t / m;
+        if (g < G) {
+            const uint64_t mh = shi[i], ml = slo[i];
+            const uint32_t mw = stw[i];
+            int r[U] = {};
+            int j = g;
+            for (; j + (U - 1) * G < m; j += U * G) {
+                uint64_t h[U], l[U];
+                uint32_t w[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    h[u] = shi[j + u * G];
+                    l[u] = slo[j + u * G];
+                    w[u] = stw[j + u * G];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    r[u] += (h[u] < mh) | ((h[u] == mh) & ((l[u] < ml) | ((l[u] == ml) & (w[u] < mw))));
+            }
+            for (; j < m; j += G) {
+                const uint64_t h = shi[j], l = slo[j];
+                const uint32_t w = stw[j];
+                r[0] += (h < mh) | ((h == mh) & ((l < ml) | ((l == ml) & (w < mw))));
+            }
+            int tot = 0;
+#pragma unroll
+            for (int u = 0; u < U; u++) tot += r[u];
+            if (tot) atomicAdd(&srk[i], tot);
+        }
+        __syncthreads();
+        if (t < m) out[off + srk[t]] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) g_wgtime[blockIdx.x][1] = wall_clock64();
+}
+
+void wg_report(const char* what, int nb) {
+    static unsigned long long t[4096][2];
+    CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wgtime), sizeof(t)));
+    unsigned long long t0 = ~0ull, t1 = 0, sum = 0, mx = 0;
+    for (int i = 0; i < nb; i++) {
+        t0 = std::min(t0, t[i][0]);
+        t1 = std::max(t1, t[i][1]);
+        sum += t[i][1] - t[i][0];
+        mx = std::max(mx, t[i][1] - t[i][0]);
+    }
+    printf("  %s WG times (10 ns ticks): span %llu, avg WG %.1f, max WG %llu\n", what, t1 - t0, (double)sum / nb, mx);
+}
+
 // morphs of the bucket probe toward the chunk copy
 template <int V>
 __global__ __launch_bounds__(512) void k_morph(SortItem* a, const int32_t* boff, const uint8_t* arena, SortItem* out) {
@@ -68,6 +303,15 @@ __global__ __launch_bounds__(512) void k_morph(SortItem* a, const int32_t* boff,
     if (V == 1 && (m <= 1 || m > 512)) return;
     SortItem x;
     if (V == 2) x = SortItem{};
+    if (V == 3) {
+        SortItem y{};
+        if (t < m) y = a[off + t];
+        if (t < m) sh[t] = y;
+        __syncthreads();
+        if (t < m) y = sh[t];
+        if (t < m) out[off + t] = y;
+        return;
+    }
     if (t < m) sh[t] = x = a[off + t];
     __syncthreads();
     if (t < m) out[off + t] = x;
@@ -160,6 +404,29 @@ int main(int argc, char** argv) {
         CK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), s));
     };
     printf("E=%d nb=%d\n", E, nb);
+    {
+        unsigned long long* d = (unsigned long long*)dmalloc(64);
+        for (int g : {1, 256, 1024}) {
+            hipLaunchKernelGGL(k_clock, g, 256, 0, s, d, 200000);
+            CK(hipStreamSynchronize(s));
+            unsigned long long h[3];
+            CK(hipMemcpy(h, d, 24, hipMemcpyDeviceToHost));
+            printf("clock (%d WGs): %llu shader cycles in %llu wall ticks -> %.0f MHz\n", g, h[0], h[1], 100.0 * h[0] / h[1]);
+        }
+    }
+    {
+        unsigned long long* d = (unsigned long long*)dmalloc(8 * 1024);
+        for (int mode = 0; mode < 3; mode++)
+            for (int wgs : {1, 256, 1024}) {
+                if (mode == 0) hipLaunchKernelGGL(k_ldsloop<0>, wgs, 256, 0, s, d, 1024);
+                if (mode == 1) hipLaunchKernelGGL(k_ldsloop<1>, wgs, 256, 0, s, d, 1024);
+                if (mode == 2) hipLaunchKernelGGL(k_ldsloop<2>, wgs, 256, 0, s, d, 1024);
+                CK(hipStreamSynchronize(s));
+                unsigned long long h;
+                CK(hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost));
+                printf("ldsloop mode %d, %4d WGs x 256: %.1f cycles per iteration\n", mode, wgs, h / 1024.0);
+            }
+    }
     printf("empty 1 WG:            %7.2f us\n", time_us(reps, [&] { hipLaunchKernelGGL(k_empty, 1, 64, 0, s); }, s));
     printf("empty 547x512:         %7.2f us\n", time_us(reps, [&] { hipLaunchKernelGGL(k_empty, 547, 512, 0, s); }, s));
     printf("empty 4096x256:        %7.2f us\n", time_us(reps, [&] { hipLaunchKernelGGL(k_empty, 4096, 256, 0, s); }, s));
@@ -209,11 +476,12 @@ int main(int argc, char** argv) {
     printf("k_bucket_sort<bitonic>:%7.2f us\n", t_sort1 / reps * 1000);
     printf("chunk V4 (32KB LDS):   %7.2f us\n", time_us(reps, [&] {
         hipLaunchKernelGGL((k_probe_chunk<4>), nb, 512, 0, s, w.items[1], w.items[0], w.boff, 128); }, s));
-    for (int v = 0; v < 3; v++)
+    for (int v = 0; v < 4; v++)
         printf("morph V%d:              %7.2f us\n", v, time_us(reps, [&] {
             if (v == 0) hipLaunchKernelGGL((k_morph<0>), nb, 512, 0, s, w.items[1], w.boff, b.tail, w.items[0]);
             if (v == 1) hipLaunchKernelGGL((k_morph<1>), nb, 512, 0, s, w.items[1], w.boff, b.tail, w.items[0]);
-            if (v == 2) hipLaunchKernelGGL((k_morph<2>), nb, 512, 0, s, w.items[1], w.boff, b.tail, w.items[0]); }, s));
+            if (v == 2) hipLaunchKernelGGL((k_morph<2>), nb, 512, 0, s, w.items[1], w.boff, b.tail, w.items[0]);
+            if (v == 3) hipLaunchKernelGGL((k_morph<3>), nb, 512, 0, s, w.items[1], w.boff, b.tail, w.items[0]); }, s));
     for (int pass = 0; pass < 2; pass++) {
     printf("chunk V1 (fixed 128):  %7.2f us\n", time_us(reps, [&] {
         hipLaunchKernelGGL((k_probe_chunk<1>), nb, 512, 0, s, w.items[1], w.items[0], w.boff, 128); }, s));
@@ -244,6 +512,46 @@ int main(int argc, char** argv) {
         printf("probe WG times (100MHz ticks): span %llu, avg WG %.1f, max WG %llu\n", t1 - t0, (double)sum / nb, mx);
         for (int i = 0; i < nb; i += 61) printf("  wg %d start %llu dur %llu\n", i, t[i][0] - t0, t[i][1] - t[i][0]);
     }
+    printf("bitonic probe 512:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_bitonic_probe<512, 0>), nb, 512, 0, s, w.items[1], w.boff, b.tail); }, s));
+    wg_report("bitonic 512", nb);
+    printf("bitonic probe 256:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_bitonic_probe<256, 0>), nb, 256, 0, s, w.items[1], w.boff, b.tail); }, s));
+    wg_report("bitonic 256", nb);
+    printf("no-sort probe 256:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_bitonic_probe<256, 1>), nb, 256, 0, s, w.items[1], w.boff, b.tail); }, s));
+    wg_report("no-sort 256", nb);
+    printf("rank SoA 256 full:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_probe<256, 0>), nb, 256, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank full", nb);
+    printf("rank SoA 256 hi-first: %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_probe<256, 1>), nb, 256, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank hi-first", nb);
+    printf("rank reg 256:          %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_reg<256>), nb, 256, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank reg 256", nb);
+    {
+        static unsigned long long c[4096][2], t[4096][2];
+        CK(hipMemcpyFromSymbol(c, HIP_SYMBOL(g_wgclk), sizeof(c)));
+        CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wgtime), sizeof(t)));
+        double cs = 0, ts = 0;
+        for (int i = 0; i < nb; i++) { cs += c[i][1] - c[i][0]; ts += t[i][1] - t[i][0]; }
+        printf("  rank reg: WG shader cycles / wall ticks -> %.0f MHz\n", 100.0 * cs / ts);
+    }
+    printf("rank reg 512:          %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_reg<512>), nb, 512, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank reg 512", nb);
+    printf("rank split 256 U4:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_split<256, 4>), nb, 256, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank split 256 U4", nb);
+    printf("rank split 512 U4:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_split<512, 4>), nb, 512, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank split 512 U4", nb);
+    printf("rank split 1024 U2:    %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_split<1024, 2>), nb, 1024, 0, s, w.items[1], w.items[0], w.boff); }, s));
+    wg_report("rank split 1024 U2", nb);
+    printf("rank SoA 512 full:     %7.2f us\n", time_us(reps, [&] {
+        hipLaunchKernelGGL((k_rank_probe<512, 0>), nb, 512, 0, s, w.items[1], w.items[0], w.boff); }, s));
     printf("probe 512 load/store:  %7.2f us\n", time_us(reps, [&] {
         hipLaunchKernelGGL((k_probe_bucket<512, 0>), nb, 512, 0, s, w.items[1], w.boff, b.tail); }, s));
     printf("probe 512 rank_count:  %7.2f us\n", time_us(reps, [&] {
