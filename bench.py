@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--txns", type=int, default=5000)
-    ap.add_argument("--history", type=int, default=5_000_000)
+    ap.add_argument("--history", type=int, default=0,
+                    help="history boundaries per GPU; 0 = the workload's (5M for c2/c3, 50M for c4)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--gc-interval", type=int, default=0,
                     help="force a compaction (+GC) at least every N batches; 0 = when the delta tier is full")
@@ -49,7 +50,7 @@ def parse():
                     help="extra batches after the timed region with every phase timed (diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the verdict all-reduce (nccl = RCCL over xGMI)")
     return ap.parse_args()
@@ -59,10 +60,32 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def shard_history(p, seed, rank, world, start_version):
-    """Prefill: p.history random 16-byte boundaries inside this rank's key range."""
-    from foundationdb_amd.workloads import c2_history
+def workload_params(args):
+    from foundationdb_amd import workloads as W
 
+    if args.workload == "c4":
+        return W.C4Params(txns=args.txns, history=args.history or 50_000_000)
+    return W.C2Params(txns=args.txns, history=args.history or 5_000_000)
+
+
+def sharding_for(args, p, world):
+    from foundationdb_amd import workloads as W
+    from foundationdb_amd.sharding import KeyRangeSharding
+
+    if world == 1:
+        return None
+    if args.workload == "c4":  # every key shares the subspace: split by user
+        return KeyRangeSharding([W.c4_user_split(p, g * p.users // world) for g in range(1, world)])
+    return KeyRangeSharding.uniform(world)
+
+
+def shard_history(args, p, seed, rank, world, start_version):
+    """Prefill: p.history boundaries inside this rank's key range."""
+    from foundationdb_amd.workloads import c2_history, c4_history
+
+    if args.workload == "c4":
+        users = (rank * p.users // world, (rank + 1) * p.users // world)
+        return c4_history(p, seed=seed * 1000 + rank, start_version=start_version, users=users)
     kb, ko, vers = c2_history(p, seed=seed * 1000 + rank, start_version=start_version)
     if world > 1:
         keys = kb.reshape(-1, 16).copy()
@@ -86,14 +109,19 @@ def make_batches(args, p, n_batches, world, start_version):
     """Global batches (identical on every rank) with their (now, newOldest)."""
     from foundationdb_amd import workloads as W
 
+    import dataclasses
+
     rng = np.random.default_rng(args.seed)
     zipf = W.ZipfGenerator(1_000_000, 0.99) if args.workload == "c3" else None
-    gp = W.C2Params(txns=args.txns * world, history=p.history)
+    gp = dataclasses.replace(p, txns=args.txns * world)
     out = []
     now = start_version
     for _ in range(n_batches):
         now += p.version_step
-        pb = W.c3_batch(gp, rng, now, zipf) if zipf else W.c2_batch(gp, rng, now)
+        if args.workload == "c4":
+            pb = W.c4_batch(gp, rng, now)
+        else:
+            pb = W.c3_batch(gp, rng, now, zipf) if zipf else W.c2_batch(gp, rng, now)
         out.append((pb, now, now - p.window))
     return out
 
@@ -133,7 +161,7 @@ def cpu_baseline(args, p, kb, ko, vers, batches):
         "unit": "txns/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{done_batches} C2 batches x {args.txns} txns on a {len(vers)}-boundary history "
+        "sample": f"{done_batches} {args.workload.upper()} batches x {args.txns} txns on a {len(vers)}-boundary history "
         f"({spent:.1f}s CPU, load {load_s:.1f}s), skip-list restatement oracle/skiplist_baseline.cpp, "
         f"1 thread on {cpu}",
     }
@@ -162,14 +190,14 @@ def main():
     from foundationdb_amd import workloads as W
     from foundationdb_amd.sharding import KeyRangeSharding
 
-    p = W.C2Params(txns=args.txns, history=args.history)
+    p = workload_params(args)
     start_version = 10_000_000
     t0 = time.time()
-    kb, ko, vers = shard_history(p, args.seed, rank, world, start_version)
+    kb, ko, vers = shard_history(args, p, args.seed, rank, world, start_version)
     total = args.warmup + args.steps
     n_all = total + args.breakdown_steps
     gbatches = make_batches(args, p, n_all, world, start_version)
-    sharding = KeyRangeSharding.uniform(world) if world > 1 else None
+    sharding = sharding_for(args, p, world)
     routed = [sharding.route(pb)[rank] for pb, _, _ in gbatches] if sharding else None
     log(f"[rank {rank}] generated history {len(vers)} + {n_all} batches in {time.time() - t0:.1f}s")
 
@@ -182,7 +210,11 @@ def main():
     maxT = max(b.n_txn for b in mine)
     maxR = max(b.n_reads for b in mine)
     maxW = max(b.n_writes for b in mine)
-    cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, 64 * 1024 * 1024, maxT, maxR, maxW)
+    def tail_bytes(ko):
+        return int(np.maximum(np.diff(ko) - 16, 0).sum())
+
+    tail_total = tail_bytes(ko) + sum(tail_bytes(b.key_offsets) for b in mine) + (1 << 20)
+    cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, tail_total, maxT, maxR, maxW)
     objs = []
     for b in mine:
         o = C.ConflictBatch(cs)
@@ -279,8 +311,11 @@ def main():
         "dtype": "u8/int64 (byte keys, int64 versions)",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.workload.upper()}: {args.txns}-txn batches per GPU, 5R+2W ranges/txn, 16-byte "
-            f"uniform keys, {args.history}-boundary MVCC history per GPU (5e6-version window)",
+            "workload": f"{args.workload.upper()}: {args.txns}-txn batches per GPU, 5R+2W ranges/txn, "
+            + {"c2": "16-byte uniform keys", "c3": "YCSB Zipf(0.99) hot keys over 1M Mako-style 16-byte keys",
+               "c4": "tuple keys (subspace, user string, int) up to 100 B, 1 wide Tuple.range() read per txn"}[
+                args.workload]
+            + f", {p.history}-boundary MVCC history per GPU (5e6-version window)",
             "global_batch_txns": args.txns * world,
             "parallelism": f"key-range shards x{world}" if world > 1 else "single resolver",
             "gc_interval": args.gc_interval,

@@ -35,6 +35,9 @@ namespace {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+constexpr int64_t kTailLimit = (int64_t)1 << 32;    // tail offsets are uint32 (engine.h Hist::lt)
+constexpr int64_t kTailReclaim = (int64_t)1 << 31;  // force the GC repack past half of that
+
 // Grow-only device allocation.
 struct DBuf {
     void* p = nullptr;
@@ -122,7 +125,8 @@ struct fdbcs_conflict_set {
     int64_t nd_ub = 0;
     int64_t dlvl3_n = 0;
     DBuf cws[6];  // compaction arrays (per delta boundary)
-    DBuf htail;   // tail arena shared by every buffer set (append-only, offsets stable)
+    DBuf htail[2];  // tail arenas (bytes [16, len) of long keys): append-only between GCs; each GC
+    int tcur = 0;   // repacks the live tails into the other one, reclaiming the rest
     int64_t tail_ub = 0;
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
@@ -467,12 +471,15 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
     if (tail_need > cs->tail_cap) {
         int64_t tcap = std::max<int64_t>(tail_need, cs->tail_cap);
         tcap = std::max<int64_t>(tcap + tcap / 2, 1 << 16);
-        DBuf nt;
-        if ((rc = nt.ensure(tcap))) return rc;
-        if (tail_used) HIPOK(hipMemcpyAsync(nt.p, cs->htail.p, tail_used, hipMemcpyDeviceToDevice, cs->stream));
+        DBuf nt, spare;
+        if ((rc = nt.ensure(tcap)) || (rc = spare.ensure(tcap))) return rc;
+        if (tail_used)
+            HIPOK(hipMemcpyAsync(nt.p, cs->htail[cs->tcur].p, tail_used, hipMemcpyDeviceToDevice, cs->stream));
         HIPOK(hipStreamSynchronize(cs->stream));
-        cs->htail.release();
-        cs->htail = nt;
+        cs->htail[cs->tcur].release();
+        cs->htail[cs->tcur ^ 1].release();
+        cs->htail[cs->tcur] = nt;
+        cs->htail[cs->tcur ^ 1] = spare;
         cs->tail_cap = tcap;
     }
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -615,7 +622,8 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         cs->dlt[k].release();
         cs->dver[k].release();
     }
-    cs->htail.release();
+    cs->htail[0].release();
+    cs->htail[1].release();
     for (auto& l : cs->lvl) l.release();
     for (auto& l : cs->dlvl) l.release();
     for (auto& x : cs->cws) x.release();
@@ -734,7 +742,7 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
         HIPOK(hipMemcpyAsync(cs->hver[cs->cur].p, versions, 8 * n, hipMemcpyHostToDevice, cs->stream));
     }
     if (!tail.empty())
-        HIPOK(hipMemcpyAsync(cs->htail.p, tail.data(), tail.size(), hipMemcpyHostToDevice, cs->stream));
+        HIPOK(hipMemcpyAsync(cs->htail[cs->tcur].p, tail.data(), tail.size(), hipMemcpyHostToDevice, cs->stream));
     Scalars s{};
     s.n = n;
     s.tail_used = (int64_t)tail.size();
@@ -906,6 +914,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     HIPOK(hipSetDevice(cs->device));
     if (now < cs->max_written) return FDBCS_E_VERSION;
     if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
+    // tail offsets are 32-bit: refuse a batch that could overflow the arena (GC repacks it long before)
+    if (cs->tail_ub + (int64_t)b->tail.size() + 1 >= kTailLimit) return FDBCS_E_NOMEM;
     const int64_t T = b->T(), R = b->R(), W = b->W();
     int rc;
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
@@ -968,7 +978,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const int bsrc = cs->cur, dsrc = cs->dcur;
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->nd, kHole};
-    uint8_t* htail = (uint8_t*)cs->htail.p;
+    uint8_t* htail = (uint8_t*)cs->htail[cs->tcur].p;
 
     w.trace = cs->trace ? (unsigned long long*)cs->trace_buf.p : nullptr;
     if (w.trace) {
@@ -1013,6 +1023,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // (SkipList.cpp:880-889) runs with it whenever the oldest version moved.
     bool compact = nd_after > delta_limit_for(cs, cs->n_ub);
     if (cs->gc_interval > 0 && ++cs->batches_since_compact >= cs->gc_interval) compact = true;
+    if (cs->tail_ub > kTailReclaim) compact = true;
     bool gc = false;
     int final_base = bsrc;
     const int64_t base_hint = cs->n_ub + nd_after + 1;
@@ -1022,12 +1033,16 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
                        rec(kPhCompEnd, 1));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
-        gc = new_oldest > cs->gc_applied;
+        // removeBefore when the oldest version moved; also whenever the tail arena is half full, for
+        // the repack that reclaims the tails of removed boundaries
+        gc = new_oldest > cs->gc_applied || cs->tail_ub > kTailReclaim;
     }
     if ((rc = mark(kPhCompact))) return rc;
     if (gc) {
-        launch_gc(s, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), sc, new_oldest, cs->header_version,
+        launch_gc(s, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), htail,
+                  (uint8_t*)cs->htail[cs->tcur ^ 1].p, sc, std::max(new_oldest, cs->gc_applied), cs->header_version,
                   base_hint);
+        cs->tcur ^= 1;
         final_base ^= 1;
         cs->gc_applied = new_oldest;
     }

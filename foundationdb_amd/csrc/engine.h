@@ -60,7 +60,8 @@ struct Scalars {
     int64_t nd_next;       // delta after this batch's merge
     int64_t n_gc;          // base after GC
     int64_t tail_used;     // bytes used in the history tail arena
-    int64_t tail_next;
+    int64_t tail_next;     // after this batch's merge appended its new boundaries' tails
+    int64_t tail_gc;       // after GC repacked the live tails into the other arena
     int64_t n_segments;    // union segments of committed writes
     int64_t d_before;      // delta size at the start of the merge
     int64_t d_rem;         // delta boundaries removed by union segments
@@ -219,8 +220,10 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end);
-void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
-               int64_t header_version, int64_t grid_hint_n);
+// removeBefore over the whole base (src -> dst); the live tails are repacked from arena tsrc into
+// the empty arena tdst (reclaiming the bytes of removed and overwritten boundaries).
+void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
+               Scalars* sc, int64_t oldest, int64_t header_version, int64_t grid_hint_n);
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 // Range-max levels of a tier whose size is *n (lvl[3] reset first).

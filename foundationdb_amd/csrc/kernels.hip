@@ -1593,29 +1593,48 @@ __device__ __forceinline__ bool gc_keep(const Hist& h, int64_t i, int64_t v, int
 
 struct GcScan {
     Hist src, dst;
+    const uint8_t* tsrc;
+    uint8_t* tdst;
     int64_t v, hdr;
     Scalars* sc;
-    __device__ void load(int64_t i, uint32_t (&x)[1]) const { x[0] = gc_keep(src, i, v, hdr) ? 1u : 0u; }
-    __device__ void store(int64_t i, const uint32_t (&ex)[1]) const {
+    // [0] kept boundaries, [1] tail bytes of the kept boundaries (their offsets in the new arena)
+    __device__ void load(int64_t i, uint32_t (&x)[2]) const {
+        const bool keep = gc_keep(src, i, v, hdr);
+        const uint32_t len = src.lt[i].x;
+        x[0] = keep ? 1u : 0u;
+        x[1] = keep && len > 16u ? len - 16u : 0u;
+    }
+    __device__ void store(int64_t i, const uint32_t (&ex)[2]) const {
         if (!gc_keep(src, i, v, hdr)) return;
         const int64_t o = ex[0];
+        uint2 lt = src.lt[i];
+        if (lt.x > 16u) {
+            const uint8_t* a = tsrc + lt.y;
+            uint8_t* d = tdst + ex[1];
+            for (uint32_t k = 0; k < lt.x - 16u; k++) d[k] = a[k];
+            lt.y = ex[1];
+        }
         dst.key[o] = src.key[i];
-        dst.lt[o] = src.lt[i];
+        dst.lt[o] = lt;
         dst.ver[o] = src.ver[i];
     }
-    __device__ void finish(const uint32_t (&tot)[1]) const { sc->n_gc = tot[0]; }
+    __device__ void finish(const uint32_t (&tot)[2]) const {
+        sc->n_gc = tot[0];
+        sc->tail_gc = tot[1];
+    }
 };
 
-void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, Scalars* sc, int64_t oldest,
-               int64_t header_version, int64_t grid_hint_n) {
-    launch_scan<1>(s, GcScan{src, dst, oldest, header_version, sc}, &sc->n_next, grid_hint_n, w.scan[kScanGc]);
+void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
+               Scalars* sc, int64_t oldest, int64_t header_version, int64_t grid_hint_n) {
+    launch_scan<2>(s, GcScan{src, dst, tsrc, tdst, oldest, header_version, sc}, &sc->n_next, grid_hint_n,
+                   w.scan[kScanGc]);
 }
 
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
     const int64_t E = 2 * (R + W);
     return kNumScans + scan_granules(E, 2) + scan_granules(R, 1) + 2 * scan_granules(E, 1) +
-           scan_granules(W + 1, 3) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 1);
+           scan_granules(W + 1, 3) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 2);
 }
 
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
@@ -1625,7 +1644,7 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     const int64_t gran[kNumScans] = {scan_granules(E, 2),     scan_granules(R, 1),
                                      scan_granules(E, 1),     scan_granules(E, 1),
                                      scan_granules(W + 1, 3), scan_granules(delta_cap + 1, 2),
-                                     scan_granules(hist_cap, 1)};
+                                     scan_granules(hist_cap, 2)};
     uint64_t* g = a + kNumScans;
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);
@@ -1775,7 +1794,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         } else {
             sc->nd = sc->nd_next;
         }
-        sc->tail_used = sc->tail_next;
+        sc->tail_used = ep.gc_ran ? sc->tail_gc : sc->tail_next;
         Scalars out = *sc;
         out.debug_error = ep.bsc->debug_error;
         *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;

@@ -240,6 +240,144 @@ def tuple_range(prefix: bytes) -> Tuple[bytes, bytes]:
     return prefix + b"\x00", prefix + b"\xff"
 
 
+@dataclass
+class C4Params:
+    """Tuple-key workload (BASELINE.json configs[3]).
+
+    Keys are ``subspace + pack((str user, int item))``: a 2-byte directory-layer style subspace
+    (the tuple encoding of a small int, as the directory layer's allocator hands out), the user
+    string ``"user" + 8 digits + filler`` (filler 0..max_filler bytes of 'x', fixed per user, so
+    keys run up to ~100 B) and a positive int item.  The first 16 bytes distinguish users, so
+    every comparison between keys of one user goes to the tail bytes (SURVEY §7 hard parts).
+    Each transaction reads one whole user (``Tuple.range()`` of the user prefix, a wide read)
+    plus ``point_reads`` single keys, and writes ``writes`` single keys."""
+
+    txns: int = 5000
+    point_reads: int = 4
+    writes: int = 2
+    users: int = 1_000_000
+    items: int = 50_000
+    history: int = 50_000_000  # boundaries (two per prefilled key: k and k + b"\0")
+    max_filler: int = 70
+    version_step: int = 1000
+    window: int = 5_000_000
+    staleness: int = 100_000
+    subspace: bytes = b"\x15\x2a"  # tuple-encoded int 42
+
+    @property
+    def reads(self) -> int:
+        return 1 + self.point_reads
+
+
+C4_WIDTH = 112  # row width of the key matrices (longest key is < 100 bytes)
+
+
+def c4_filler_len(p: C4Params, user: np.ndarray) -> np.ndarray:
+    """Per-user filler length: a fixed hash of the user id (Knuth multiplicative)."""
+    h = (np.asarray(user, np.uint64) * np.uint64(2654435761)) & np.uint64(0xFFFFFFFF)
+    return (h % np.uint64(p.max_filler + 1)).astype(np.int64)
+
+
+def c4_user_string(p: C4Params, user: int) -> str:
+    return f"user{user:08d}" + "x" * int(c4_filler_len(p, np.array([user]))[0])
+
+
+def c4_user_split(p: C4Params, user: int) -> bytes:
+    """A key below every key of `user` and above every key of smaller users (shard split point)."""
+    return p.subspace + b"\x02" + f"user{user:08d}".encode()
+
+
+def c4_keys(p: C4Params, user: np.ndarray, item: np.ndarray, kind: np.ndarray):
+    """Key matrix (n, C4_WIDTH) and lengths, one row per (user, item, kind):
+    0 = pack(user, item);  1 = pack(user, item) + b"\\0" (keyAfter);
+    2 = Tuple.range(user).begin = prefix(user) + b"\\0";  3 = Tuple.range(user).end = prefix(user) + b"\\xff".
+    Items must lie in [1, 65536) (one or two magnitude bytes)."""
+    user = np.asarray(user, np.int64)
+    item = np.asarray(item, np.int64)
+    kind = np.asarray(kind, np.int64)
+    n = len(user)
+    sub = np.frombuffer(p.subspace, np.uint8)
+    S = len(sub)
+    mat = np.zeros((n, C4_WIDTH), np.uint8)
+    mat[:, :S] = sub
+    mat[:, S] = 0x02  # string type code (Tuple.cpp:72-117)
+    mat[:, S + 1 : S + 5] = np.frombuffer(b"user", np.uint8)
+    v = user.copy()
+    for d in range(7, -1, -1):
+        mat[:, S + 5 + d] = ord("0") + (v % 10)
+        v //= 10
+    f0 = S + 13  # filler start
+    L = c4_filler_len(p, user)
+    cols = np.arange(C4_WIDTH)[None, :]
+    mat[(cols >= f0) & (cols < (f0 + L)[:, None])] = ord("x")
+    rows = np.arange(n)
+    pe = f0 + L  # string terminator; prefix(user) = bytes [0, pe]
+    mat[rows, pe] = 0x00
+    nb = np.where(item >= 256, 2, 1)
+    length = np.empty(n, np.int64)
+    wide = kind >= 2
+    mat[rows[wide], pe[wide] + 1] = np.where(kind[wide] == 2, 0x00, 0xFF)
+    length[wide] = pe[wide] + 2
+    pt = ~wide
+    r, q, it, nbp = rows[pt], pe[pt], item[pt], nb[pt]
+    mat[r, q + 1] = 0x14 + nbp  # positive int code (Tuple.cpp:72-117)
+    two = nbp == 2
+    mat[r[two], q[two] + 2] = (it[two] >> 8).astype(np.uint8)
+    mat[r[two], q[two] + 3] = (it[two] & 0xFF).astype(np.uint8)
+    mat[r[~two], q[~two] + 2] = it[~two].astype(np.uint8)
+    klen = q + 2 + nbp
+    suf = kind[pt] == 1
+    mat[r[suf], klen[suf]] = 0x00  # keyAfter(k) = k + b"\0"
+    length[pt] = klen + suf
+    return mat, length
+
+
+def c4_history(p: C4Params, seed: int, start_version: int, users: Tuple[int, int] | None = None,
+               chunk: int = 1_000_000):
+    """Prefilled history of about p.history boundaries: random distinct (user, item) keys (users
+    in [users[0], users[1]) when given), each a boundary k and its keyAfter k + b"\\0", with versions
+    spread over the window (the step function single-key writes leave).  Sorted by construction:
+    tuple order is (user, item) because the user digits are fixed width and positive ints encode
+    order-preservingly (Tuple.cpp:72-117).  Returns (key_bytes, key_offsets, versions)."""
+    rng = np.random.default_rng(seed + 4000037)
+    u0, u1 = users if users is not None else (0, p.users)
+    span = p.items - 1
+    code = np.unique(rng.integers(u0 * span, u1 * span, size=p.history // 2, dtype=np.int64))
+    user = code // span
+    item = code % span + 1
+    n = 2 * len(code)
+    lens = np.empty(n, np.int64)
+    parts = []
+    for a in range(0, len(code), chunk):
+        m = len(code[a : a + chunk])
+        mat, ln = c4_keys(p, np.repeat(user[a : a + chunk], 2), np.repeat(item[a : a + chunk], 2),
+                          np.tile(np.array([0, 1], np.int64), m))
+        lens[2 * a : 2 * a + 2 * m] = ln
+        parts.append(mat[np.arange(C4_WIDTH)[None, :] < ln[:, None]])
+    kb = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    ko = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=ko[1:])
+    vers = rng.integers(max(0, start_version - p.window), start_version, size=n, dtype=np.int64)
+    return kb, ko, vers
+
+
+def c4_batch(p: C4Params, rng: np.random.Generator, now: int) -> PackedBatch:
+    """One C4 batch: per transaction one wide read of a user, p.point_reads point reads and
+    p.writes point writes, the point ranges single-key [k, k + b"\\0") (FDBTypes.h:499-505)."""
+    T, nr, nw = p.txns, p.reads, p.writes
+    R, W = T * nr, T * nw
+    user = rng.integers(0, p.users, size=R + W)
+    item = rng.integers(1, p.items, size=R + W)
+    wide = np.zeros(R + W, bool)
+    wide[0:R:nr] = True  # each transaction's first read covers the whole user
+    kind = np.tile(np.array([0, 1], np.int64), R + W) + 2 * np.repeat(wide, 2)
+    mat, lens = c4_keys(p, np.repeat(user, 2), np.repeat(item, 2), kind)
+    snap = now - rng.integers(0, p.staleness, size=T)
+    return PackedBatch.from_key_matrix(
+        snap, np.arange(T + 1, dtype=np.int32) * nr, np.arange(T + 1, dtype=np.int32) * nw, mat, lens
+    )
+
+
 # --------------------------------------------------------------------------- tests
 def random_small_batch(
     rng: np.random.Generator,

@@ -1,0 +1,63 @@
+"""CPU tests of the C4 generator (BASELINE.json configs[3]): tuple-encoded keys restated from
+fdbclient/Tuple.cpp:72-117 / 240-255, a history sorted by construction, and oracle vs skip-list
+restatement parity on a reduced C4 run with GC every batch."""
+import numpy as np
+
+from foundationdb_amd import workloads as W
+
+
+def _keys(mat, lens):
+    return [mat[i, : lens[i]].tobytes() for i in range(len(lens))]
+
+
+def test_c4_keys_are_tuple_encoded():
+    p = W.C4Params()
+    users = np.array([0, 7, 12345678, 999999, 42])
+    items = np.array([1, 255, 256, 65535, 3000])
+    for kind in range(4):
+        mat, lens = W.c4_keys(p, users, items, np.full(len(users), kind))
+        got = _keys(mat, lens)
+        for u, i, k in zip(users, items, got):
+            pk = W.tuple_pack(p.subspace, W.c4_user_string(p, int(u)), int(i))
+            prefix = pk[: len(pk) - (2 if i < 256 else 3)]  # subspace + packed string
+            want = [pk, pk + b"\x00", *W.tuple_range(prefix)][kind]
+            assert k == want, (kind, u, i, k, want)
+            assert len(k) <= 100
+            assert W.c4_user_split(p, int(u)) <= k
+
+
+def test_c4_history_sorted_and_wide_reads_cover_one_user():
+    p = W.C4Params(users=300, items=500, history=4000, window=1000)
+    kb, ko, vers = W.c4_history(p, seed=1, start_version=5000)
+    keys = [kb[ko[i] : ko[i + 1]].tobytes() for i in range(len(ko) - 1)]
+    assert all(a < b for a, b in zip(keys, keys[1:]))
+    assert len(vers) == len(keys) and vers.min() >= 4000 and vers.max() < 5000
+    # a wide read of a user contains every key of that user and nothing else
+    mat, lens = W.c4_keys(p, np.array([5, 5]), np.array([1, 1]), np.array([2, 3]))
+    b, e = _keys(mat, lens)
+    pre = W.tuple_pack(p.subspace, W.c4_user_string(p, 5), 1)[:-2]
+    assert [k for k in keys if b <= k < e] == [k for k in keys if k.startswith(pre)]
+    # a user range restricts the history to one shard's users
+    kb2, ko2, _ = W.c4_history(p, seed=1, start_version=5000, users=(100, 200))
+    lo, hi = W.c4_user_split(p, 100), W.c4_user_split(p, 200)
+    assert all(lo <= kb2[ko2[i] : ko2[i + 1]].tobytes() < hi for i in range(len(ko2) - 1))
+
+
+def test_c4_reduced_oracle_matches_skiplist(oracle_built):
+    p = W.C4Params(txns=400, users=400, items=200, history=6000, window=6000, staleness=2500)
+    kb, ko, vers = W.c4_history(p, seed=2, start_version=20_000)
+    a, b = oracle_built.OracleConflictSet(), oracle_built.SkipListBaseline()
+    a.load_history(kb, ko, vers)
+    b.load_history(kb, ko, vers)
+    rng = np.random.default_rng(3)
+    now = 20_000
+    seen = set()
+    for _ in range(6):
+        now += p.version_step
+        pb = W.c4_batch(p, rng, now)
+        va, _ = a.detect(pb, now, now - p.window)
+        vb, _ = b.detect(pb, now, now - p.window)
+        assert (va == vb).all()
+        seen |= set(np.unique(va).tolist())
+    assert {0, 2} <= seen  # both conflicts and commits occur
+    assert a.history_size() == b.history_size()

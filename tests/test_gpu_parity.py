@@ -167,6 +167,33 @@ def test_c3_zipf_heavy_contention(engine, oracle_mod):
     e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
 
 
+@pytest.mark.parametrize("gc_interval,delta_limit", [(1, 0), (0, 3000)])
+def test_c4_tuple_keys_window_gc(engine, oracle_mod, gc_interval, delta_limit):
+    """BASELINE config C4, reduced: tuple-encoded keys up to ~100 B whose 16-byte prefixes are
+    shared by every key of a user (comparisons go to the tail bytes), wide Tuple.range() reads, and
+    the window sliding with newOldest = now - window every batch (GC), against the skip-list
+    restatement; after a compaction with GC both hold the same boundary count."""
+    p = W.C4Params(txns=1500, users=3000, items=400, history=80_000, window=12_000, staleness=4_000)
+    kb, ko, vers = W.c4_history(p, seed=4, start_version=100_000)
+    e = EngineDriver(engine, gc_interval=gc_interval, delta_limit=delta_limit)
+    o = oracle_mod.SkipListBaseline()
+    e.load_history(kb, ko, vers)
+    o.load_history(kb, ko, vers)
+    rng = np.random.default_rng(5)
+    now = 100_000
+    seen = set()
+    for i in range(10):
+        now += p.version_step
+        pb = W.c4_batch(p, rng, now)
+        ve, _ = e.detect(pb, now, now - p.window)
+        vo, _ = o.detect(pb, now, now - p.window)
+        assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
+        seen |= set(np.unique(ve).tolist())
+    assert {0, 2} <= seen  # both conflicts and commits
+    if gc_interval == 1:
+        assert e.cs.history_size() == o.history_size()
+
+
 def test_async_pipelined_batches_match_sync(engine):
     rng = np.random.default_rng(4)
     batches = []
