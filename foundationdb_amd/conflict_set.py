@@ -23,7 +23,7 @@ import numpy as np
 from .packing import CommitTransaction, InvertedRange, PackedBatch, _CPackedBatch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfdbcs.so")
+LIB_PATH = os.environ.get("FDBCS_LIB") or os.path.join(_HERE, "libfdbcs.so")
 
 FDBCS_OK = 0
 FDBCS_E_INVALID = -1

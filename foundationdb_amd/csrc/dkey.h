@@ -39,13 +39,44 @@ FDB_HD uint32_t item_class(uint32_t meta) { return meta & 3u; }
 FDB_HD uint32_t item_range(uint32_t meta) { return meta >> 3; }
 FDB_HD uint32_t item_is_end(uint32_t meta) { return (meta >> 2) & 1u; }
 
-// Compare the bytes of two tails [16, min(la, lb)) then lengths.
+#if defined(__HIP_DEVICE_COMPILE__)
+// Eight tail bytes starting at p as a big-endian word, from the two aligned words that hold them
+// (tail arenas start 8-aligned and carry >= 40 bytes of slack past their last tail, so the
+// aligned loads of tail_cmp stay inside the allocation).
+__device__ __forceinline__ uint64_t tail_word(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* w = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint64_t x = w[0], y = w[1];
+    return __builtin_bswap64(sh ? (x >> sh) | (y << (64u - sh)) : x);
+}
+#endif
+
+// Compare the bytes of two tails [16, min(la, lb)) then lengths.  On the device, 32 bytes per
+// step as big-endian words (bytes past the shorter tail masked off): a C4 tuple key shares up to
+// ~80 tail bytes with its neighbours, and a byte loop pays one dependent load per byte.
 FDB_HD int tail_cmp(const uint8_t* ta, uint32_t la, const uint8_t* tb, uint32_t lb) {
     uint32_t n = (la < lb ? la : lb) - 16u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (uint32_t i = 0; i < n; i += 32) {
+        uint64_t a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) a[j] = tail_word(ta + i + 8 * j), b[j] = tail_word(tb + i + 8 * j);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int vb = (int)(n - i) - 8 * j;  // bytes of word j inside the shorter tail
+            if (vb <= 0) break;
+            const uint64_t msk = vb >= 8 ? ~0ull : ~0ull << (64 - 8 * vb);
+            const uint64_t x = a[j] & msk, y = b[j] & msk;
+            if (x != y) return x < y ? -1 : 1;
+        }
+    }
+#else
     for (uint32_t i = 0; i < n; i++) {
         uint8_t a = ta[i], b = tb[i];
         if (a != b) return a < b ? -1 : 1;
     }
+#endif
     return (la > lb) - (la < lb);
 }
 

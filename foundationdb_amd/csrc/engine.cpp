@@ -35,6 +35,7 @@ namespace {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+constexpr int64_t kTailSlack = 64;  // bytes past a tail arena's capacity (dkey.h tail_word reads aligned words)
 constexpr int64_t kTailLimit = (int64_t)1 << 32;    // tail offsets are uint32 (engine.h Hist::lt)
 constexpr int64_t kTailReclaim = (int64_t)1 << 31;  // force the GC repack past half of that
 
@@ -472,7 +473,7 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
         int64_t tcap = std::max<int64_t>(tail_need, cs->tail_cap);
         tcap = std::max<int64_t>(tcap + tcap / 2, 1 << 16);
         DBuf nt, spare;
-        if ((rc = nt.ensure(tcap)) || (rc = spare.ensure(tcap))) return rc;
+        if ((rc = nt.ensure(tcap + kTailSlack)) || (rc = spare.ensure(tcap + kTailSlack))) return rc;
         if (tail_used)
             HIPOK(hipMemcpyAsync(nt.p, cs->htail[cs->tcur].p, tail_used, hipMemcpyDeviceToDevice, cs->stream));
         HIPOK(hipStreamSynchronize(cs->stream));
@@ -513,7 +514,7 @@ int do_upload(fdbcs_batch* b) {
     const size_t o_flags = off;
     off = align_up(off + T, 64);
     const size_t o_tail = off;
-    off = align_up(off + b->tail.size() + 16, 64);
+    off = align_up(off + b->tail.size() + 48, 64);  // slack for dkey.h tail_word
     int rc;
     if ((rc = b->pin_in.ensure(off)) || (rc = b->dev.ensure(off))) return rc;
     char* h = (char*)b->pin_in.p;

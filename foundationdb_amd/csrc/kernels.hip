@@ -263,24 +263,14 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     }
     int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
     const int64_t hi = min(n, kFan * b);
-    if (hi - lo > kFan) {  // long run of shared prefixes: binary search, every lane alike
-        int64_t l = lo, u = hi;
-        while (l < u) {
-            const int64_t mid = (l + u) >> 1;
-            const int r = hist_cmp(h, mid, htail, q, qtail);
-            if (r < 0) {
-                l = mid + 1;
-            } else {
-                u = mid;
-                eq = r == 0;
-            }
-        }
-        return l;
-    }
-    // lower_bound in [lo, lo + span], span <= 64: rounds of kArity probes at a shrinking stride
+    // lower_bound in [lo, lo + span]: rounds of kArity probes at a shrinking stride.  span <= 64
+    // normally; a long run of boundaries sharing q's 16-byte prefix (tuple keys) only starts the
+    // stride higher, so the lanes still compare tails side by side.
     int64_t span = hi - lo;
+    int64_t stride0 = kFan / kArity;
+    while (stride0 * kArity < span) stride0 *= kArity;
     bool eq_cand = false;  // cmp == 0 at the last probe that stopped a count (the answer, if < hi)
-    for (int64_t stride = kFan / kArity; span > 0; stride = stride > kArity ? stride / kArity : 1) {
+    for (int64_t stride = stride0; span > 0; stride = stride > kArity ? stride / kArity : 1) {
         const int64_t p = lo + stride * (gl + 1) - 1;
         const bool v = stride * (gl + 1) <= span && p < hi;
         int r = 1;
@@ -761,6 +751,48 @@ __device__ bool reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* are
     return tie;
 }
 
+// Exact count of the bucket items that share x's hi word and order before it.  The low word and
+// the (length, class, id) word decide branch-free; a pair that needs the bytes beyond the prefix
+// (equal prefixes, both keys longer than 16 bytes) is compared after the scan, so the lanes of a
+// wave run their first such comparison side by side instead of one lane at a time per broadcast
+// item (C4 tuple keys: every range's two endpoints tie on the prefix).  Further ties (hot keys)
+// take a second, serial pass.
+__device__ __forceinline__ int rank_shared_hi(const SortItem* sh, const uint64_t* shi, int m, int t,
+                                              const SortItem& x, const uint8_t* arena) {
+    const uint64_t ax = item_aux(x);
+    const bool xlong = x.len > 16u;
+    int lt = 0, first = -1;
+    bool more = false;
+    for (int q = 0; q < m; q++) {
+        if (shi[q] != x.hi || q == t) continue;
+        const uint64_t ylo = sh[q].lo;
+        if (ylo != x.lo) {
+            lt += ylo < x.lo;
+            continue;
+        }
+        const SortItem y = sh[q];
+        if (xlong && y.len > 16u) {
+            more |= first >= 0;
+            first = first < 0 ? q : first;
+        } else {
+            lt += item_aux(y) < ax;
+        }
+    }
+    if (first >= 0) {
+        const SortItem y = sh[first];
+        lt += item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena) ? 1 : 0;
+    }
+    if (more) {
+        for (int q = first + 1; q < m; q++) {
+            if (shi[q] != x.hi || q == t) continue;
+            const SortItem y = sh[q];
+            if (y.lo == x.lo && y.len > 16u)
+                lt += item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena) ? 1 : 0;
+        }
+    }
+    return lt;
+}
+
 constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by one workgroup
 
 // Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic network padded to a
@@ -803,10 +835,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 lt += h < mh;
                 eq += h == mh;
             }
-            if (eq > 1) {  // another item shares my hi word: order those exactly
-                for (int q = 0; q < m; q++)
-                    if (shi[q] == mh && q != t && item_less_total(sh[q], x, arena)) lt++;
-            }
+            if (eq > 1) lt += rank_shared_hi(sh, shi, m, t, x, arena);
             a[off + lt] = x;
         }
         return;

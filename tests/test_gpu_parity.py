@@ -131,6 +131,44 @@ def test_shared_long_prefixes(engine, oracle_mod):
     run_pair(engine, oracle_mod, seq, gc_interval=0, delta_limit=30)
 
 
+def test_long_shared_prefix_runs(engine, oracle_mod):
+    """Thousands of history boundaries behind one 16-byte prefix (a few huge tuple subspaces): the
+    search must order them by their tail bytes over a run far longer than one 64-boundary block
+    (the cooperative probe rounds start at a stride of 512 or more)."""
+    rng = np.random.default_rng(123)
+    prefixes = [b"\x15\x2a\x02huge-subspace-%d\x00" % i for i in range(3)]
+
+    def key():
+        pre = prefixes[int(rng.integers(0, len(prefixes)))]
+        return pre + bytes(rng.integers(0, 256, size=int(rng.integers(0, 40))).astype(np.uint8))
+
+    hist = sorted({key() for _ in range(20000)})
+    kb = np.frombuffer(b"".join(hist), np.uint8)
+    ko = np.zeros(len(hist) + 1, np.int64)
+    np.cumsum([len(k) for k in hist], out=ko[1:])
+    vers = rng.integers(0, 1000, size=len(hist)).astype(np.int64)
+    e = EngineDriver(engine, gc_interval=0, delta_limit=4000)
+    o = oracle_mod.SkipListBaseline()
+    e.load_history(kb, ko, vers)
+    o.load_history(kb, ko, vers)
+    now = 1000
+    for i in range(6):
+        now += 10
+        txns = []
+        for _ in range(400):
+            def rr():
+                a, b = key(), key()
+                return KeyRange(min(a, b), max(a, b))
+
+            txns.append(CommitTransaction([rr() for _ in range(int(rng.integers(1, 4)))],
+                                          [rr() for _ in range(int(rng.integers(0, 3)))],
+                                          now - int(rng.integers(0, 600)), False))
+        pb = PackedBatch.from_transactions(txns)
+        ve, _ = e.detect(pb, now, 0)
+        vo, _ = o.detect(pb, now, 0)
+        assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
+
+
 def test_c1_skiplisttest(engine, oracle_mod):
     seq = list(W.c1_batches(25, seed=7))
     e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
