@@ -288,7 +288,9 @@ def main():
     bytes_per_launch = kbytes / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    # PMC HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate rocprofv3
+    # passes: scripts/gpu_pmc.sh) of this workload's copy kernels, measured on the same command
+    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
     if os.path.exists(pmc):
         try:
             with open(pmc) as f:
