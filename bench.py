@@ -268,6 +268,9 @@ def main():
         }
         phase["batches"] = sb["batches"]
         phase["compactions"] = sb["compactions"]
+        phase["intra_edges"] = sb["intra_edges"] / max(1, sb["batches"] - sb["intra_fallbacks"])
+        phase["intra_rounds"] = sb["intra_rounds"] / max(1, sb["batches"] - sb["intra_fallbacks"])
+        phase["intra_fallbacks"] = sb["intra_fallbacks"]
     gtxn = sum(gbatches[i][0].n_txn for i in range(args.warmup, total))
     granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(args.warmup, total))
     hist_end = cs.history_size()

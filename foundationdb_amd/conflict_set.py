@@ -68,6 +68,9 @@ class Stats(ctypes.Structure):
         ("compact_bytes", ctypes.c_int64),
         ("ms_compact_kernel", ctypes.c_double),
         ("ms_epilogue", ctypes.c_double),
+        ("intra_edges", ctypes.c_int64),
+        ("intra_rounds", ctypes.c_int64),
+        ("intra_fallbacks", ctypes.c_int64),
     ]
 
     def as_dict(self):

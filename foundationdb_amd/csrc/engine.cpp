@@ -93,6 +93,9 @@ enum Phase {
 
 struct fdbcs_batch;
 
+// ws[k] slots: ensure_workspace TAKEs [0, kWsTileSlot); then the copy-tile index and the scan arena.
+constexpr int kWsTileSlot = 46, kWsArenaSlot = 47;
+
 struct fdbcs_conflict_set {
     int device = 0;
     hipStream_t stream = nullptr;   // stage B: everything that reads or writes the history, in batch order
@@ -132,7 +135,7 @@ struct fdbcs_conflict_set {
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
     // two batch workspaces (alternating batches)
-    DBuf ws[2][41];
+    DBuf ws[2][48];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
     int64_t ws_T = -1, ws_R = -1, ws_W = -1;
     Work work[2]{};
     int64_t edge_cap = 0;
@@ -215,11 +218,11 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
     for (int k = 0; k < 2; k++) {
         Work& w = cs->work[k];
-        int rc = cs->ws[k][39].ensure(8 * words + 64);
+        int rc = cs->ws[k][kWsArenaSlot].ensure(8 * words + 64);
         if (rc) return rc;
-        w.scan_arena = (uint64_t*)cs->ws[k][39].p;
-        if ((rc = cs->ws[k][38].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 1024 + 8)))) return rc;
-        w.tile_first = (int32_t*)cs->ws[k][38].p;
+        w.scan_arena = (uint64_t*)cs->ws[k][kWsArenaSlot].p;
+        if ((rc = cs->ws[k][kWsTileSlot].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 1024 + 8)))) return rc;
+        w.tile_first = (int32_t*)cs->ws[k][kWsTileSlot].p;
         carve_scans(w, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
         HIPOK(hipMemsetAsync(w.scan_arena, 0, 8 * w.scan_words, cs->stream));
         for (int q = 0; q < kNumScans; q++) w.scan[q].error = &w.bsc->debug_error;
@@ -249,6 +252,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     Work& w = cs->work[k];
     int i = 0;
     auto take = [&](size_t bytes, void** ptr) -> int {
+        if (i >= kWsTileSlot) return FDBCS_E_INVALID;  // more TAKE slots than ws[] reserves
         int rc = cs->ws[k][i].ensure(bytes + 64);
         if (rc) return rc;
         *ptr = cs->ws[k][i].p;
@@ -273,12 +277,14 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(pmeta, 4 * E);
     TAKE(cwb, 4 * (E + 1));
     TAKE(crb, 4 * (E + 1));
+    TAKE(cwe, 4 * (E + 1));
     TAKE(segflag, E + 1);
     TAKE(wbpos, 4 * W);
     TAKE(rbpos, 4 * R);
     TAKE(ecnt_a, 4 * R);
     TAKE(ecnt_b, 4 * R);
     TAKE(eoff, 4 * (R + 1));
+    TAKE(poff, 4 * (R + W + 1));
     TAKE(ecur, 4 * R);
     TAKE(edges, 4 * edge_cap);
     TAKE(eptr, 4 * T);
@@ -1183,6 +1189,12 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         // copy kernels: each reads every old boundary of its tier (32 B) and writes the kept ones
         st.ms_merge_kernel += ph(kPhCopyBegin, kPhCopyEnd);
         st.merge_launches += 1;
+        if (b->h_scal->intra_edges < 0) {
+            st.intra_fallbacks += 1;
+        } else {
+            st.intra_edges += b->h_scal->intra_edges;
+            st.intra_rounds += b->h_scal->intra_rounds;
+        }
         st.merge_bytes += 32 * (2 * b->h_scal->d_before - b->h_scal->d_rem);
         if (b->compacted) {
             st.compactions += 1;

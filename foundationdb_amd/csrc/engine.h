@@ -68,7 +68,8 @@ struct Scalars {
     int64_t c_before;      // base size at the start of a compaction
     int64_t c_rem;         // base boundaries removed (overwritten) by the compaction
     int32_t debug_error;   // copied from the batch's BatchScalars by the epilogue (host view only)
-    int32_t pad;
+    int32_t intra_rounds;  // copied from BatchScalars::rounds by the epilogue (host view only)
+    int64_t intra_edges;   // copied from BatchScalars::n_edges (host view only; overflow -> -1)
 };
 
 // Device scalars of one batch workspace (two workspaces alternate, so batch i+1's history-
@@ -133,13 +134,15 @@ struct Work {
     uint32_t* pmeta;       // [E] meta of the item at each position
     int32_t* cwb;          // [E+1] write-begins before each position
     int32_t* crb;          // [E+1] read-begins before each position
+    int32_t* cwe;          // [E+1] write-ends before each position
     uint8_t* segflag;      // [E] bit0: union segment starts here, bit1: one ends here
     int32_t* wbpos;        // [W] positions of write-begins in order
     int32_t* rbpos;        // [R] positions of read-begins in order
-    int32_t* ecnt_a;       // [R]
-    int32_t* ecnt_b;       // [R]
-    int32_t* eoff;         // [R+1]
-    int32_t* ecur;         // [R]
+    int32_t* ecnt_a;       // [R] "a" slots of each read (write-begins inside it)
+    int32_t* ecnt_b;       // [R] (unused; zeroed by the epilogue)
+    int32_t* eoff;         // [R+1] first edge slot of each read
+    int32_t* poff;         // [R+W+1] first candidate pair of each range
+    int32_t* ecur;         // [R] "b" slots taken so far
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction

@@ -933,9 +933,9 @@ struct PosScan {
     const SortItem* sorted;
     int32_t* pos;
     uint32_t* pmeta;
-    int32_t *cwb, *crb, *wbpos, *rbpos;
+    int32_t *cwb, *crb, *cwe, *wbpos, *rbpos;
     int32_t E;
-    __device__ void load(int64_t p, uint32_t (&v)[2]) const {
+    __device__ void load(int64_t p, uint32_t (&v)[3]) const {
         const uint32_t meta = sorted[p].meta;
         pmeta[p] = meta;
         const uint32_t slot = 2 * item_range(meta) + item_is_end(meta);
@@ -943,17 +943,20 @@ struct PosScan {
         const uint32_t c = item_class(meta);
         v[0] = c == kWriteBegin;
         v[1] = c == kReadBegin;
+        v[2] = c == kWriteEnd;
     }
-    __device__ void store(int64_t p, const uint32_t (&ex)[2]) const {
+    __device__ void store(int64_t p, const uint32_t (&ex)[3]) const {
         cwb[p] = (int32_t)ex[0];
         crb[p] = (int32_t)ex[1];
+        cwe[p] = (int32_t)ex[2];
         const uint32_t c = item_class(pmeta[p]);
         if (c == kWriteBegin) wbpos[ex[0]] = (int32_t)p;
         if (c == kReadBegin) rbpos[ex[1]] = (int32_t)p;
     }
-    __device__ void finish(const uint32_t (&tot)[2]) const {
+    __device__ void finish(const uint32_t (&tot)[3]) const {
         cwb[E] = (int32_t)tot[0];
         crb[E] = (int32_t)tot[1];
+        cwe[E] = (int32_t)tot[2];
     }
 };
 
@@ -972,8 +975,8 @@ __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
     const int E = 2 * (b.R + b.W);
     if (E == 0) return;
-    PosScan f{w.items[sorted_buf], w.pos, w.pmeta, w.cwb, w.crb, w.wbpos, w.rbpos, E};
-    launch_scan<2>(s, f, nullptr, E, w.scan[kScanPos]);
+    PosScan f{w.items[sorted_buf], w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, E};
+    launch_scan<3>(s, f, nullptr, E, w.scan[kScanPos]);
 }
 
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
@@ -991,75 +994,98 @@ void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int s
 // (found from the read) or r begins inside (wb, we) (found from the write).  Each such
 // pair is one candidate edge t' -> t: t aborts iff some candidate writer commits.
 
-template <bool FILL>
-__global__ __launch_bounds__(kBlock) void k_edges(BatchDev b, Work w) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= b.R + b.W) return;
-    if (FILL && w.bsc->edge_overflow) return;
-    const int R = b.R;
-    if (g < R) {
-        const int r = g;
-        const int t = b.rowner[r];
-        const int rb = w.pos[2 * r], re = w.pos[2 * r + 1];
-        int cnt = 0;
-        if (rb < re) {
-            const int k0 = w.cwb[rb], k1 = w.cwb[re];
-            int out = FILL ? w.eoff[r] : 0;
-            for (int k = k0; k < k1; k++) {
-                const int p = w.wbpos[k];
+//
+// Every (range, candidate) pair is enumerated in parallel, so a hot key written by hundreds of
+// transactions and read by thousands (Zipf, C3) costs no serial per-range loop:
+//   * read r owns the write-begins inside (rb, re): wbpos[cwb[rb] .. cwb[re]) ("a" pairs);
+//   * write w owns the read-begins inside (wb, we): rbpos[crb[wb] .. crb[we]) ("b" pairs).
+// Read r's edge slots are its a pairs, then one slot per write covering rb; that count is
+// #(write-begins before rb) - #(write-ends before rb), known without enumerating (an empty write
+// has its end before its begin and no read-begin between them, so it counts 0).  Slots whose pair
+// fails the filter (earlier writer, both ranges non-empty) hold -1 and read as an aborted writer.
+
+__device__ __forceinline__ bool range_nonempty(const Work& w, int g) { return w.pos[2 * g] < w.pos[2 * g + 1]; }
+
+// Per range g: slots (reads only) and pairs; exclusive prefixes give each read's first slot and
+// each range's first pair.
+struct EdgePairScan {
+    Work w;
+    int32_t R, G;
+    __device__ void counts(int64_t g, uint32_t& slots, uint32_t& pairs, uint32_t& a) const {
+        slots = pairs = a = 0;
+        if (!range_nonempty(w, (int)g)) return;
+        const int b = w.pos[2 * g], e = w.pos[2 * g + 1];
+        if (g < R) {
+            a = (uint32_t)(w.cwb[e] - w.cwb[b]);
+            const int cover = w.cwb[b] - w.cwe[b];  // < 0 only with an inverted write (invalid input)
+            slots = a + (uint32_t)(cover > 0 ? cover : 0);
+            pairs = a;
+        } else {
+            pairs = (uint32_t)(w.crb[e] - w.crb[b]);
+        }
+    }
+    __device__ void load(int64_t g, uint32_t (&v)[2]) const {
+        uint32_t a;
+        counts(g, v[0], v[1], a);
+        if (g < R) w.ecnt_a[g] = (int32_t)a;
+    }
+    __device__ void store(int64_t g, const uint32_t (&ex)[2]) const {
+        if (g < R) w.eoff[g] = (int32_t)ex[0];
+        w.poff[g] = (int32_t)ex[1];
+    }
+    __device__ void finish(const uint32_t (&tot)[2]) const {
+        w.eoff[R] = (int32_t)tot[0];
+        w.poff[G] = (int32_t)tot[1];
+        w.bsc->n_edges = tot[0];
+        w.bsc->edge_overflow = (int64_t)tot[0] > w.edge_cap || tot[0] > 0x7fffffffu || tot[1] > 0x7fffffffu ? 1 : 0;
+    }
+};
+
+constexpr int kPairsPerThread = 4;
+
+__global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
+    if (w.bsc->edge_overflow) return;
+    const int R = b.R, G = b.R + b.W;
+    const int P = w.poff[G];
+    const int stride = gridDim.x * blockDim.x * kPairsPerThread;
+    for (int q0 = (blockIdx.x * blockDim.x + threadIdx.x) * kPairsPerThread; q0 < P; q0 += stride) {
+        // range owning pair q0: last g with poff[g] <= q0
+        int lo = 0, hi = G;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (w.poff[mid] <= q0) lo = mid; else hi = mid;
+        }
+        int g = lo;
+        const int q1 = min(P, q0 + kPairsPerThread);
+        for (int q = q0; q < q1; q++) {
+            while (w.poff[g + 1] <= q) g++;
+            const int k = q - w.poff[g];
+            if (g < R) {
+                const int r = g, t = b.rowner[r];
+                const int p = w.wbpos[w.cwb[w.pos[2 * r]] + k];
                 const int wr = (int)item_range(w.pmeta[p]) - R;
                 const int tw = b.wowner[wr];
-                if (tw < t && w.pos[2 * (R + wr)] < w.pos[2 * (R + wr) + 1]) {
-                    if (FILL) w.edges[out + cnt] = tw;
-                    cnt++;
-                }
-            }
-        }
-        if (!FILL) w.ecnt_a[r] = cnt;
-    } else {
-        const int wr = g - R;
-        const int tw = b.wowner[wr];
-        const int wb = w.pos[2 * g], we = w.pos[2 * g + 1];
-        if (wb >= we) return;
-        const int k0 = w.crb[wb], k1 = w.crb[we];
-        for (int k = k0; k < k1; k++) {
-            const int p = w.rbpos[k];
-            const int r = (int)item_range(w.pmeta[p]);
-            const int t = b.rowner[r];
-            if (tw < t && w.pos[2 * r] < w.pos[2 * r + 1]) {
-                if (FILL) {
-                    const int slot = atomicAdd(&w.ecur[r], 1);
-                    w.edges[w.eoff[r] + w.ecnt_a[r] + slot] = tw;
-                } else {
-                    atomicAdd(&w.ecnt_b[r], 1);
-                }
+                w.edges[w.eoff[r] + k] = (tw < t && range_nonempty(w, R + wr)) ? tw : -1;
+            } else {
+                const int wr = g - R, tw = b.wowner[wr];
+                const int p = w.rbpos[w.crb[w.pos[2 * g]] + k];
+                const int r = (int)item_range(w.pmeta[p]);
+                if (!range_nonempty(w, r)) continue;  // an empty read owns no slots
+                const int slot = atomicAdd(&w.ecur[r], 1);
+                const int base = w.eoff[r] + w.ecnt_a[r];
+                if (base + slot < w.eoff[r + 1]) w.edges[base + slot] = tw < b.rowner[r] ? tw : -1;
             }
         }
     }
 }
 
-// Edge offsets per read range: exclusive scan of the two candidate counts.
-struct EdgeOffsetScan {
-    const int32_t *a, *b;
-    int32_t* eoff;
-    int32_t R;
-    int64_t cap;
-    BatchScalars* sc;
-    __device__ void load(int64_t r, uint32_t (&v)[1]) const { v[0] = (uint32_t)(a[r] + b[r]); }
-    __device__ void store(int64_t r, const uint32_t (&ex)[1]) const { eoff[r] = (int32_t)ex[0]; }
-    __device__ void finish(const uint32_t (&tot)[1]) const {
-        eoff[R] = (int32_t)tot[0];
-        sc->n_edges = tot[0];
-        sc->edge_overflow = (int64_t)tot[0] > cap || tot[0] > 0x7fffffffu ? 1 : 0;
-    }
-};
-
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    if (G) hipLaunchKernelGGL(k_edges<false>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
-    EdgeOffsetScan f{w.ecnt_a, w.ecnt_b, w.eoff, b.R, w.edge_cap, w.bsc};
-    launch_scan<1>(s, f, nullptr, b.R, w.scan[kScanEdges]);
-    if (G) hipLaunchKernelGGL(k_edges<true>, dim3((G + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
+    launch_scan<2>(s, EdgePairScan{w, b.R, G}, nullptr, G, w.scan[kScanEdges]);
+    if (G) {
+        const int blocks = G / 64 < 64 ? 64 : (G / 64 > 2048 ? 2048 : G / 64);
+        hipLaunchKernelGGL(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
+    }
 }
 
 // ------------------------------------------------------------------ D.CheckIntraBatch: resolution
@@ -1105,7 +1131,8 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
                 const int end = w.eoff[b.roff[t + 1]];
                 uint8_t res = kUndecided;
                 while (p < end) {
-                    const uint8_t sp = vst[w.edges[p]];
+                    const int e = w.edges[p];  // -1: filtered pair (behaves as an aborted writer)
+                    const uint8_t sp = (unsigned)e < (unsigned)T ? vst[e] : kAborted;
                     if (sp == kAborted) {
                         p++;
                         continue;
@@ -1189,7 +1216,8 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
     const int t = b.rowner[r];
     if (!(b.flags[t] & kFlagReport) || w.hist_conf[t] || w.status[t] != kAborted) return;
     for (int p = w.eoff[r]; p < w.eoff[r + 1]; p++) {
-        if (w.status[w.edges[p]] == kCommitted) {
+        const int e = w.edges[p];
+        if ((unsigned)e < (unsigned)b.T && w.status[e] == kCommitted) {
             atomicMin(&w.first_conf[t], r - b.roff[t]);
             return;
         }
@@ -1662,7 +1690,7 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, c
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
     const int64_t E = 2 * (R + W);
-    return kNumScans + scan_granules(E, 2) + scan_granules(R, 1) + 2 * scan_granules(E, 1) +
+    return kNumScans + scan_granules(E, 3) + scan_granules(R + W, 2) + 2 * scan_granules(E, 1) +
            scan_granules(W + 1, 3) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 2);
 }
 
@@ -1670,7 +1698,7 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     (void)T;
     const int64_t E = 2 * (R + W);
     uint64_t* a = w.scan_arena;
-    const int64_t gran[kNumScans] = {scan_granules(E, 2),     scan_granules(R, 1),
+    const int64_t gran[kNumScans] = {scan_granules(E, 3),     scan_granules(R + W, 2),
                                      scan_granules(E, 1),     scan_granules(E, 1),
                                      scan_granules(W + 1, 3), scan_granules(delta_cap + 1, 2),
                                      scan_granules(hist_cap, 2)};
@@ -1826,6 +1854,8 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         sc->tail_used = ep.gc_ran ? sc->tail_gc : sc->tail_next;
         Scalars out = *sc;
         out.debug_error = ep.bsc->debug_error;
+        out.intra_rounds = ep.bsc->rounds;
+        out.intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
         *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;
         ep.bsc->debug_error = 0;
     }

@@ -99,6 +99,9 @@ typedef struct fdbcs_stats {
     int64_t compact_bytes;  /* algorithmic bytes moved by the compaction copy kernel */
     double ms_compact_kernel; /* device time of the compaction copy kernel alone */
     double ms_epilogue;     /* range-max rebuild + verdicts */
+    int64_t intra_edges;    /* candidate intra-batch edges (sum over batches) */
+    int64_t intra_rounds;   /* batch-order resolution rounds (sum over batches) */
+    int64_t intra_fallbacks;/* batches resolved by the sequential MiniConflictSet replay */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
