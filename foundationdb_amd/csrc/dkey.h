@@ -26,11 +26,17 @@ static_assert(sizeof(DKey) == 24, "DKey is 24 bytes");
 // Sort item: a batch endpoint with its key (KeyInfo, SkipList.cpp:77-87).
 // meta = range_id << 3 | is_end << 2 | class, class as extra_ordering
 // (SkipList.cpp:89-91): read-end 0 < write-end 1 < write-begin 2 < read-begin 3.
+// nx = key bytes [16, 19) as a big-endian 24-bit word, zero past the key's end: with it the sort
+// needs the tail arena only when both keys exceed kSortNxLen bytes and agree on 19 (a hot key k and
+// its end key k\0 of singleKeyRange(k), C3, never do).  A bitonic padding item has meta kPadMeta
+// (no endpoint has is_end = 1 with the read-begin class).
 struct __attribute__((aligned(16))) SortItem {
     uint64_t hi, lo;
     uint32_t len, tail;
-    uint32_t meta, pad;
+    uint32_t meta, nx;
 };
+constexpr uint32_t kSortNxLen = 19;
+constexpr uint32_t kPadMeta = 0xffffffffu;
 static_assert(sizeof(SortItem) == 32, "SortItem is 32 bytes");
 
 enum PointClass : uint32_t { kReadEnd = 0, kWriteEnd = 1, kWriteBegin = 2, kReadBegin = 3 };

@@ -138,11 +138,11 @@ struct Work {
     uint8_t* segflag;      // [E] bit0: union segment starts here, bit1: one ends here
     int32_t* wbpos;        // [W] positions of write-begins in order
     int32_t* rbpos;        // [R] positions of read-begins in order
-    int32_t* ecnt_a;       // [R] "a" slots of each read (write-begins inside it)
+    int32_t* ecnt_a;       // [R] (unused)
     int32_t* ecnt_b;       // [R] (unused; zeroed by the epilogue)
     int32_t* eoff;         // [R+1] first edge slot of each read
     int32_t* poff;         // [R+W+1] first candidate pair of each range
-    int32_t* ecur;         // [R] "b" slots taken so far
+    int32_t* ecur;         // [R] edges of each read (slots taken; zeroed by the epilogue)
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction

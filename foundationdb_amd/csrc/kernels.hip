@@ -438,7 +438,13 @@ __device__ __forceinline__ SortItem make_item(const BatchDev& b, int p) {
     it.len = k.len;
     it.tail = k.tail;
     it.meta = ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
-    it.pad = 0;
+    it.nx = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (k.len > 16u) {
+        const uint32_t nb = k.len - 16u < 3u ? k.len - 16u : 3u;
+        it.nx = (uint32_t)(tail_word(b.tail + k.tail) >> 40) & (0xffffffu << (8u * (3u - nb))) & 0xffffffu;
+    }
+#endif
     return it;
 }
 
@@ -455,17 +461,24 @@ __device__ __forceinline__ bool item_less_tail(uint32_t alen, uint32_t atail, ui
     return ameta < bmeta;
 }
 
-// Packed tie-break word: capped length (17 stands for "longer than the prefix"), class, id.
+// Packed tie-break word after equal 16-byte prefixes: key bytes [16, 19), length capped at 20
+// (20 stands for "longer than kSortNxLen"), class, endpoint id.  It decides every pair except two
+// keys both longer than kSortNxLen with equal words (see item_tie).
 __device__ __forceinline__ uint64_t item_aux(const SortItem& a) {
-    const uint64_t l = a.len > 16u ? 17u : a.len;
-    return (l << 40) | ((uint64_t)item_class(a.meta) << 32) | a.meta;
+    const uint64_t l = a.len > kSortNxLen ? kSortNxLen + 1 : a.len;
+    return ((uint64_t)a.nx << 37) | (l << 32) | ((uint64_t)item_class(a.meta) << 30) | (a.meta >> 2);
 }
+// Equal prefixes: does the order need the tail bytes?
+__device__ __forceinline__ bool item_tie(const SortItem& a, const SortItem& b) {
+    return a.len > kSortNxLen && b.len > kSortNxLen && a.nx == b.nx;
+}
+__device__ __forceinline__ bool is_pad(const SortItem& a) { return a.meta == kPadMeta; }
 
 // Branch-free on the common path; the tail comparison (both keys longer than 16 bytes with
 // equal prefixes) is out of line.
 __device__ __forceinline__ bool item_less_total(const SortItem& a, const SortItem& b, const uint8_t* arena) {
     const bool hi_eq = a.hi == b.hi, lo_eq = a.lo == b.lo;
-    if (hi_eq && lo_eq && a.len > 16u && b.len > 16u)
+    if (hi_eq && lo_eq && item_tie(a, b))
         return item_less_tail(a.len, a.tail, a.meta, b.len, b.tail, b.meta, arena);
     const bool aux_lt = item_aux(a) < item_aux(b);
     return (a.hi < b.hi) | (hi_eq & ((a.lo < b.lo) | (lo_eq & aux_lt)));
@@ -509,7 +522,7 @@ __device__ __forceinline__ void rank_count(const SortItem* sh, int cnt, const So
         for (int k = 0; k < P; k++) {
             const bool heq = x.hi == mine[k].hi, leq = x.lo == mine[k].lo;
             rk[k] += ((x.hi < mine[k].hi) | (heq & ((x.lo < mine[k].lo) | (leq & (xa < maux[k]))))) ? 1 : 0;
-            tail |= heq & leq & (x.len > 16u) & (mine[k].len > 16u) & (x.meta != mine[k].meta);
+            tail |= heq && leq && item_tie(x, mine[k]) && x.meta != mine[k].meta;
         }
     };
     int j = 0;
@@ -695,9 +708,9 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uin
     if (p < E) out[off[k] + local[k] + slot] = make_item(b, p);
 }
 
-// Sentinel-aware order for the bitonic network: padding items (pad = 1) sort after every item.
+// Sentinel-aware order for the bitonic network: padding items sort after every item.
 __device__ __forceinline__ bool lt_pad(const SortItem& x, const SortItem& y, const uint8_t* arena) {
-    if (x.pad | y.pad) return y.pad && !x.pad;
+    if (is_pad(x) || is_pad(y)) return is_pad(y) && !is_pad(x);
     return item_less_total(x, y, arena);
 }
 
@@ -708,7 +721,7 @@ __device__ __forceinline__ SortItem shfl_xor_item(const SortItem& x, int j) {
     y.len = __shfl_xor(x.len, j, 64);
     y.tail = __shfl_xor(x.tail, j, 64);
     y.meta = __shfl_xor(x.meta, j, 64);
-    y.pad = __shfl_xor(x.pad, j, 64);
+    y.nx = __shfl_xor(x.nx, j, 64);
     return y;
 }
 
@@ -740,10 +753,10 @@ __device__ bool reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* are
             if (EXACT) {
                 y_less = lt_pad(y, x, arena);
             } else {
-                const uint64_t ax = x.pad ? ~0ull : item_aux(x), ay = y.pad ? ~0ull : item_aux(y);
+                const uint64_t ax = is_pad(x) ? ~0ull : item_aux(x), ay = is_pad(y) ? ~0ull : item_aux(y);
                 const bool heq = y.hi == x.hi, leq = y.lo == x.lo;
                 y_less = (y.hi < x.hi) | (heq & ((y.lo < x.lo) | (leq & (ay < ax))));
-                tie |= heq & leq & (x.len > 16u) & (y.len > 16u) & !(x.pad | y.pad);
+                tie |= heq && leq && item_tie(x, y) && !is_pad(x) && !is_pad(y);
             }
             if (want_smaller == y_less) x = y;
         }
@@ -760,7 +773,6 @@ __device__ bool reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* are
 __device__ __forceinline__ int rank_shared_hi(const SortItem* sh, const uint64_t* shi, int m, int t,
                                               const SortItem& x, const uint8_t* arena) {
     const uint64_t ax = item_aux(x);
-    const bool xlong = x.len > 16u;
     int lt = 0, first = -1;
     bool more = false;
     for (int q = 0; q < m; q++) {
@@ -771,7 +783,7 @@ __device__ __forceinline__ int rank_shared_hi(const SortItem* sh, const uint64_t
             continue;
         }
         const SortItem y = sh[q];
-        if (xlong && y.len > 16u) {
+        if (item_tie(x, y)) {
             more |= first >= 0;
             first = first < 0 ? q : first;
         } else {
@@ -786,7 +798,7 @@ __device__ __forceinline__ int rank_shared_hi(const SortItem* sh, const uint64_t
         for (int q = first + 1; q < m; q++) {
             if (shi[q] != x.hi || q == t) continue;
             const SortItem y = sh[q];
-            if (y.lo == x.lo && y.len > 16u)
+            if (y.lo == x.lo && item_tie(x, y))
                 lt += item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena) ? 1 : 0;
         }
     }
@@ -846,7 +858,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
         while (L < cnt) L <<= 1;
         SortItem x0{};
         x0.hi = x0.lo = ~0ull;  // padding sorts after every endpoint
-        x0.pad = 1;
+        x0.meta = kPadMeta;
         if (t < cnt) x0 = a[off + c + t];
         SortItem x = x0;
         const bool tie = reg_bitonic<false>(x, sh, L, arena);
@@ -999,10 +1011,11 @@ void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int s
 // transactions and read by thousands (Zipf, C3) costs no serial per-range loop:
 //   * read r owns the write-begins inside (rb, re): wbpos[cwb[rb] .. cwb[re]) ("a" pairs);
 //   * write w owns the read-begins inside (wb, we): rbpos[crb[wb] .. crb[we]) ("b" pairs).
-// Read r's edge slots are its a pairs, then one slot per write covering rb; that count is
-// #(write-begins before rb) - #(write-ends before rb), known without enumerating (an empty write
-// has its end before its begin and no read-begin between them, so it counts 0).  Slots whose pair
-// fails the filter (earlier writer, both ranges non-empty) hold -1 and read as an aborted writer.
+// Read r owns eoff[r+1] - eoff[r] slots: its a pairs plus one per write covering rb, a count that
+// is #(write-begins before rb) - #(write-ends before rb), known without enumerating (an empty write
+// has its end before its begin and no read-begin between them, so it counts 0).  Only pairs that
+// pass the filter (earlier writer, both ranges non-empty) take a slot, so read r's edges are
+// edges[eoff[r] .. eoff[r] + ecur[r]).
 
 __device__ __forceinline__ bool range_nonempty(const Work& w, int g) { return w.pos[2 * g] < w.pos[2 * g + 1]; }
 
@@ -1027,7 +1040,6 @@ struct EdgePairScan {
     __device__ void load(int64_t g, uint32_t (&v)[2]) const {
         uint32_t a;
         counts(g, v[0], v[1], a);
-        if (g < R) w.ecnt_a[g] = (int32_t)a;
     }
     __device__ void store(int64_t g, const uint32_t (&ex)[2]) const {
         if (g < R) w.eoff[g] = (int32_t)ex[0];
@@ -1058,22 +1070,38 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
         int g = lo;
         const int q1 = min(P, q0 + kPairsPerThread);
         for (int q = q0; q < q1; q++) {
-            while (w.poff[g + 1] <= q) g++;
+            if (w.poff[g + 1] <= q) {
+                // next range with pairs: gallop forward (ranges without pairs can run for thousands)
+                int step = 1, lo2 = g + 1, hi2 = g + 2;  // poff[lo2] <= q; find hi2 with poff[hi2] > q
+                while (hi2 < G && w.poff[hi2] <= q) {
+                    lo2 = hi2;
+                    step *= 2;
+                    hi2 = min(G, hi2 + step);
+                }
+                while (hi2 - lo2 > 1) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (w.poff[mid] <= q) lo2 = mid; else hi2 = mid;
+                }
+                g = lo2;
+            }
             const int k = q - w.poff[g];
             if (g < R) {
                 const int r = g, t = b.rowner[r];
                 const int p = w.wbpos[w.cwb[w.pos[2 * r]] + k];
                 const int wr = (int)item_range(w.pmeta[p]) - R;
                 const int tw = b.wowner[wr];
-                w.edges[w.eoff[r] + k] = (tw < t && range_nonempty(w, R + wr)) ? tw : -1;
+                if (tw < t && range_nonempty(w, R + wr)) {
+                    const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
+                    if (slot < w.eoff[r + 1]) w.edges[slot] = tw;
+                }
             } else {
                 const int wr = g - R, tw = b.wowner[wr];
                 const int p = w.rbpos[w.crb[w.pos[2 * g]] + k];
                 const int r = (int)item_range(w.pmeta[p]);
-                if (!range_nonempty(w, r)) continue;  // an empty read owns no slots
-                const int slot = atomicAdd(&w.ecur[r], 1);
-                const int base = w.eoff[r] + w.ecnt_a[r];
-                if (base + slot < w.eoff[r + 1]) w.edges[base + slot] = tw < b.rowner[r] ? tw : -1;
+                if (tw < b.rowner[r] && range_nonempty(w, r)) {
+                    const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
+                    if (slot < w.eoff[r + 1]) w.edges[slot] = tw;
+                }
             }
         }
     }
@@ -1127,20 +1155,27 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
             int more = 0;
             for (int t = threadIdx.x; t < T; t += blockDim.x) {
                 if (vst[t] != kUndecided) continue;
+                // resume at edge p: skip aborted writers, stop at the first undecided or committed
                 int p = w.eptr[t];
-                const int end = w.eoff[b.roff[t + 1]];
                 uint8_t res = kUndecided;
-                while (p < end) {
-                    const int e = w.edges[p];  // -1: filtered pair (behaves as an aborted writer)
-                    const uint8_t sp = (unsigned)e < (unsigned)T ? vst[e] : kAborted;
-                    if (sp == kAborted) {
-                        p++;
-                        continue;
+                int r = b.roff[t];
+                const int rend = b.roff[t + 1];
+                for (; r < rend; r++) {
+                    const int s0 = w.eoff[r], s1 = s0 + w.ecur[r];
+                    if (p < s0) p = s0;
+                    while (p < s1) {
+                        const int e = w.edges[p];
+                        const uint8_t sp = (unsigned)e < (unsigned)T ? vst[e] : kAborted;
+                        if (sp == kAborted) {
+                            p++;
+                            continue;
+                        }
+                        if (sp == kCommitted) res = kAborted;
+                        break;
                     }
-                    if (sp == kCommitted) res = kAborted;
-                    break;
+                    if (p < s1) break;
                 }
-                if (p == end) res = kCommitted;
+                if (r == rend) res = kCommitted;
                 w.eptr[t] = p;
                 if (res != kUndecided)
                     vst[t] = res;
@@ -1215,7 +1250,7 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
     if (r >= b.R || sc->edge_overflow) return;
     const int t = b.rowner[r];
     if (!(b.flags[t] & kFlagReport) || w.hist_conf[t] || w.status[t] != kAborted) return;
-    for (int p = w.eoff[r]; p < w.eoff[r + 1]; p++) {
+    for (int p = w.eoff[r]; p < w.eoff[r] + w.ecur[r]; p++) {
         const int e = w.edges[p];
         if ((unsigned)e < (unsigned)b.T && w.status[e] == kCommitted) {
             atomicMin(&w.first_conf[t], r - b.roff[t]);

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(NT) void k_bitonic_probe(SortItem* a, const int32_t
         while (L < m) L <<= 1;
         SortItem x{};
         x.hi = x.lo = ~0ull;
-        x.pad = 1;
+        x.meta = kPadMeta;
         if (t < m) x = a[off + t];
         if (MODE == 0) reg_bitonic<false>(x, sh, L, arena);
         if (t < m) a[off + t] = x;
