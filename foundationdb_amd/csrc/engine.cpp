@@ -221,7 +221,7 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
         int rc = cs->ws[k][kWsArenaSlot].ensure(8 * words + 64);
         if (rc) return rc;
         w.scan_arena = (uint64_t*)cs->ws[k][kWsArenaSlot].p;
-        if ((rc = cs->ws[k][kWsTileSlot].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 1024 + 8)))) return rc;
+        if ((rc = cs->ws[k][kWsTileSlot].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 256 + 8)))) return rc;
         w.tile_first = (int32_t*)cs->ws[k][kWsTileSlot].p;
         carve_scans(w, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
         HIPOK(hipMemsetAsync(w.scan_arena, 0, 8 * w.scan_words, cs->stream));

@@ -1369,7 +1369,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
 }
 
-constexpr int kDeltaTile = 1024;  // copy tile of the (small) delta tier: enough workgroups to fill the chip
+constexpr int kDeltaTile = 256;   // copy tile of the (small) delta tier: ~4 workgroups per CU at C2
 constexpr int kBaseTile = 4096;   // copy tile of the base tier during compaction
 
 // tile_first[t] = first segment whose lo lies in copy tile t or later (segment j's share).
