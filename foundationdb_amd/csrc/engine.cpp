@@ -95,15 +95,20 @@ struct fdbcs_batch;
 
 // ws[k] slots: ensure_workspace TAKEs [0, kWsTileSlot); then the copy-tile index and the scan arena.
 constexpr int kWsTileSlot = 46, kWsArenaSlot = 47;
+// Batch workspaces in rotation: stage A of the next two batches can run while stage B of the
+// current one does (two stage-A streams), so each workspace is reused every third batch.
+constexpr int kNumWork = 3;
 
 struct fdbcs_conflict_set {
     int device = 0;
     hipStream_t stream = nullptr;   // stage B: everything that reads or writes the history, in batch order
-    hipStream_t astream = nullptr;  // stage A: each batch's history-independent sort and candidate edges
-    hipEvent_t ev_a[2] = {};        // stage A of the batch using workspace k is done
-    hipEvent_t ev_b[2] = {};        // stage B (epilogue) of the batch using workspace k is done
-    bool wused[2] = {false, false};
+    hipStream_t astream = nullptr;  // stage A of even batches (and every upload): history-independent
+    hipStream_t astream2 = nullptr; // stage A of odd batches            sort and candidate edges
+    hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
+    hipEvent_t ev_b[kNumWork] = {}; // stage B (epilogue) of the batch using workspace k is done
+    bool wused[kNumWork] = {};
     int wpar = 0;                   // workspace of the next batch
+    int apar = 0;                   // stage-A stream of the next batch
     int timing = 0;       // 0: no events; 1: the copy kernels; 2: every phase (fdbcs_set_timing)
     uint32_t seq = 0;     // batches submitted (completion flag values)
     int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
@@ -134,10 +139,10 @@ struct fdbcs_conflict_set {
     int64_t tail_ub = 0;
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
-    // two batch workspaces (alternating batches)
-    DBuf ws[2][48];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
+    // batch workspaces (rotating)
+    DBuf ws[kNumWork][48];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
     int64_t ws_T = -1, ws_R = -1, ws_W = -1;
-    Work work[2]{};
+    Work work[kNumWork]{};
     int64_t edge_cap = 0;
 
     int inflight = 0;
@@ -216,7 +221,7 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     if (cs->ws_T < 0 || cs->hist_cap <= 0) return FDBCS_OK;
     if (cs->delta_cap <= 0) return FDBCS_OK;
     const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < kNumWork; k++) {
         Work& w = cs->work[k];
         int rc = cs->ws[k][kWsArenaSlot].ensure(8 * words + 64);
         if (rc) return rc;
@@ -234,6 +239,7 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
 // Both streams idle (before reallocating anything either stage uses).
 int sync_all(fdbcs_conflict_set* cs) {
     HIPOK(hipStreamSynchronize(cs->astream));
+    HIPOK(hipStreamSynchronize(cs->astream2));
     HIPOK(hipStreamSynchronize(cs->stream));
     return FDBCS_OK;
 }
@@ -248,7 +254,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     const int64_t E = 2 * (R + W);
     int64_t edge_cap = std::max<int64_t>(16 * R, 1 << 22);
     if (const char* env = getenv("FDBCS_EDGE_CAP")) edge_cap = std::max<int64_t>(1, atoll(env));  // testing knob
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < kNumWork; k++) {
     Work& w = cs->work[k];
     int i = 0;
     auto take = [&](size_t bytes, void** ptr) -> int {
@@ -314,7 +320,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), cs->stream));
     HIPOK(hipMemsetAsync(w.bsc, 0, sizeof(BatchScalars), cs->stream));
     // compaction arrays are shared (stage B only)
-    if (k == 1) {
+    if (k >= 1) {
         Work& w0 = cs->work[0];
         w.c_lo = w0.c_lo, w.c_hi = w0.c_hi, w.c_rem = w0.c_rem, w.c_ins = w0.c_ins, w.c_val = w0.c_val;
         w.c_exact = w0.c_exact;
@@ -593,8 +599,9 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess;
-    for (int k = 0; k < 2 && ok; k++)
+              hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&cs->astream2, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < kNumWork && ok; k++)
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_b[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
@@ -620,6 +627,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (!cs) return;
     (void)hipSetDevice(cs->device);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
+    if (cs->astream2) (void)hipStreamSynchronize(cs->astream2);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
     for (int k = 0; k < 2; k++) {
         cs->hkey[k].release();
@@ -638,11 +646,12 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         for (auto& x : set) x.release();
     cs->scal.release();
     cs->trace_buf.release();
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < kNumWork; k++) {
         if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
     }
     if (cs->astream) (void)hipStreamDestroy(cs->astream);
+    if (cs->astream2) (void)hipStreamDestroy(cs->astream2);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -793,6 +802,7 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
     if (b->state == 2) {  // still in flight: its set (which must outlive it) owns the stream
         (void)hipSetDevice(b->cs->device);
         (void)hipStreamSynchronize(b->cs->astream);
+        (void)hipStreamSynchronize(b->cs->astream2);
         (void)hipStreamSynchronize(b->cs->stream);
         b->cs->inflight--;
     } else if (b->state == 1) {  // uploaded, never submitted: the copy may still be in flight
@@ -959,9 +969,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // Stage A (sort, positions, candidate edges) depends only on this batch: it runs on its own
     // stream and overlaps stage B of the previous batch.  Phase timing (level 2) runs both stages on
     // one stream so the phases are measured one after another.
-    hipStream_t sa = (timing >= 2 || cs->serial) ? s : cs->astream;
+    hipStream_t sa = (timing >= 2 || cs->serial) ? s : (cs->apar ? cs->astream2 : cs->astream);
+    cs->apar ^= 1;
     const int wp = cs->wpar;
-    cs->wpar ^= 1;
+    cs->wpar = (wp + 1) % kNumWork;
     Work& w = cs->work[wp];
     // phase events: level 2 records every phase, level 1 only the copy kernels (roofline)
     auto rec = [&](int ph, int level) -> hipEvent_t {
@@ -979,6 +990,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->wused[wp] = true;
     if (b->state == 0 && (rc = do_upload(b))) return rc;
     if (sa == s || hipEventQuery(b->ev_up) != hipSuccess) HIPOK(hipStreamWaitEvent(s, b->ev_up, 0));
+    if (sa != s && sa != cs->astream && hipEventQuery(b->ev_up) != hipSuccess)
+        HIPOK(hipStreamWaitEvent(sa, b->ev_up, 0));  // the upload ran on astream
     if ((rc = mark(kPhUpload))) return rc;
     const BatchDev& bd = b->bd;
     Scalars* sc = (Scalars*)cs->scal.p;
@@ -1089,6 +1102,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
             if ((spin & 1023) == 1023) {
                 hipError_t e = hipStreamQuery(cs->astream);
+                if (e == hipSuccess || e == hipErrorNotReady) e = hipStreamQuery(cs->astream2);
                 if (e == hipSuccess || e == hipErrorNotReady) e = hipStreamQuery(cs->stream);
                 if (e != hipSuccess && e != hipErrorNotReady) {
                     fprintf(stderr, "fdbcs: stream error while waiting: %s\n", hipGetErrorString(e));
@@ -1111,7 +1125,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                 int nb = (E + 127) / 128;
                 nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
                 std::vector<int32_t> bo(nb + 1);
-                HIPOK(hipMemcpy(bo.data(), cs->work[cs->wpar ^ 1].boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
+                HIPOK(hipMemcpy(bo.data(), cs->work[(cs->wpar + kNumWork - 1) % kNumWork].boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
                 int mx = 0, over = 0;
                 for (int k = 0; k < nb; k++) {
                     const int sz = bo[k + 1] - bo[k];
