@@ -98,6 +98,7 @@ constexpr int kWsTileSlot = 46, kWsArenaSlot = 47;
 // Batch workspaces in rotation: stage A of the next two batches can run while stage B of the
 // current one does (two stage-A streams), so each workspace is reused every third batch.
 constexpr int kNumWork = 3;
+constexpr int kGcEveryCompactions = 4;  // removeBefore cadence of size-triggered compactions
 
 struct fdbcs_conflict_set {
     int device = 0;
@@ -116,6 +117,7 @@ struct fdbcs_conflict_set {
     int64_t max_written = 0;     // highest version present in the history
     int gc_interval = 0;          // compaction (and GC) at least every this many batches; 0: by size only
     int batches_since_compact = 0;
+    int compactions_since_gc = 0;
     int64_t gc_applied = 0;
     int64_t delta_limit = 0;      // compaction once the delta may exceed this; 0: automatic
 
@@ -1055,7 +1057,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->batches_since_compact = 0;
         // removeBefore when the oldest version moved; also whenever the tail arena is half full, for
         // the repack that reclaims the tails of removed boundaries
-        gc = new_oldest > cs->gc_applied || cs->tail_ub > kTailReclaim;
+        // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th
+        // one: a full pass over the base costs ~10x the compaction copy at C2 while one
+        // window-step of oldest-version movement makes few boundaries removable (a boundary goes
+        // only when it and its predecessor are both older, SkipList.cpp:554-561). Verdict-neutral
+        // either way; a forced cadence (gc_interval > 0) keeps GC at every compaction.
+        const bool gc_turn = cs->gc_interval > 0 || ++cs->compactions_since_gc >= kGcEveryCompactions;
+        gc = (new_oldest > cs->gc_applied && gc_turn) || cs->tail_ub > kTailReclaim;
+        if (gc) cs->compactions_since_gc = 0;
     }
     if ((rc = mark(kPhCompact))) return rc;
     if (gc) {
