@@ -1060,7 +1060,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th
         // one: a full pass over the base costs ~10x the compaction copy at C2 while one
         // window-step of oldest-version movement makes few boundaries removable (a boundary goes
-        // only when it and its predecessor are both older, SkipList.cpp:554-561). Verdict-neutral
+        // only when it and its predecessor are both older, SkipList.cpp:555-561). Verdict-neutral
         // either way; a forced cadence (gc_interval > 0) keeps GC at every compaction.
         const bool gc_turn = cs->gc_interval > 0 || ++cs->compactions_since_gc >= kGcEveryCompactions;
         gc = (new_oldest > cs->gc_applied && gc_turn) || cs->tail_ub > kTailReclaim;
