@@ -296,6 +296,8 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(ecur, 4 * R);
     TAKE(edges, 4 * edge_cap);
     TAKE(eptr, 4 * T);
+    TAKE(pre_st, T);
+    TAKE(pre_ep, 4 * T);
     TAKE(cov, 4 * E);
     TAKE(mcs_bits, 8 * (E / 64 + 2));
     TAKE(seg_b, 4 * (W + 1));

@@ -79,7 +79,7 @@ struct BatchScalars {
     int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
-    int32_t pad;
+    int32_t pre_done;      // k_resolve workgroups done with the pre-pass (reset by the epilogue)
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -146,6 +146,8 @@ struct Work {
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction
+    uint8_t* pre_st;       // [T] k_resolve pre-pass: status before the batch-order rounds
+    int32_t* pre_ep;       // [T] k_resolve pre-pass: resume pointer
     int32_t* cov;          // [E]
     uint64_t* mcs_bits;    // [E/64+1] sequential-fallback MiniConflictSet
     // union segments (<= W)

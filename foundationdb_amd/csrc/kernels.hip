@@ -822,10 +822,13 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
         // share it add the exact comparisons against exactly those items (hot keys, long prefixes).
         // Two items per LDS read, two VALU ops per comparison.
         __shared__ __attribute__((aligned(16))) uint64_t shi[kBitonicMax];
+        __shared__ uint64_t slo[kBitonicMax], saux[kBitonicMax];
         SortItem x{};
         if (t < m) {
             sh[t] = x = a[off + t];
             shi[t] = x.hi;
+            slo[t] = x.lo;
+            saux[t] = item_aux(x);
         }
         __syncthreads();
         if (t < m) {
@@ -847,7 +850,35 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 lt += h < mh;
                 eq += h == mh;
             }
-            if (eq > 1) lt += rank_shared_hi(sh, shi, m, t, x, arena);
+            if (eq > 1) {
+                // Items sharing my hi word: low word, then the tie-break word, four items per step
+                // with every LDS load issued first (a read [k, k + d) shares the hi word with its
+                // own end; a hot key fills whole buckets with one prefix).  A pair that needs the
+                // tail bytes (item_tie) sends the item to the exact, deferred-tail path.
+                const uint64_t ax = saux[t], ml = x.lo;
+                const bool xlong = ((ax >> 32) & 31u) == kSortNxLen + 1;
+                int lt2 = 0;
+                bool tie = false;
+                int q = 0;
+                for (; q + 4 <= m; q += 4) {
+                    uint64_t h[4], l[4], w[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) h[u] = shi[q + u], l[u] = slo[q + u], w[u] = saux[q + u];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const bool hs = h[u] == mh, ls = l[u] == ml;
+                        tie |= hs && ls && xlong && (w[u] >> 32) == (ax >> 32) && w[u] != ax;
+                        lt2 += (hs && (l[u] < ml || (ls && w[u] < ax))) ? 1 : 0;
+                    }
+                }
+                for (; q < m; q++) {
+                    const uint64_t h = shi[q], l = slo[q], w = saux[q];
+                    const bool hs = h == mh, ls = l == ml;
+                    tie |= hs && ls && xlong && (w >> 32) == (ax >> 32) && w != ax;
+                    lt2 += (hs && (l < ml || (ls && w < ax))) ? 1 : 0;
+                }
+                lt += tie ? rank_shared_hi(sh, shi, m, t, x, arena) : lt2;
+            }
             a[off + lt] = x;
         }
         return;
@@ -1111,7 +1142,7 @@ void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
     launch_scan<2>(s, EdgePairScan{w, b.R, G}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
-        const int blocks = G / 64 < 64 ? 64 : (G / 64 > 2048 ? 2048 : G / 64);
+        const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
         hipLaunchKernelGGL(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
     }
 }
@@ -1139,15 +1170,91 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
         if (blockIdx.x == 0 && threadIdx.x == 0) sc->rounds = 0;
         return;
     }
+    // Pre-pass on every workgroup, one wave per transaction: skip the candidate writers already
+    // known aborted (history conflict or TooOld), 64 edges per step with one ballot, and commit
+    // the transactions left with none; the rest keep a resume pointer at their first writer not
+    // known aborted.  These are exactly the decisions round one would make, but a hot key's reader
+    // (hundreds of aborted writers, C3) costs a few ballots instead of a serial walk, and every
+    // transaction's chain of dependent loads runs on its own wave across the chip.
+    const bool pre = !sc->edge_overflow;
+    if (pre) {
+        const int lane = threadIdx.x & 63;
+        const int nwaves = gridDim.x * (blockDim.x >> 6);
+        for (int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < T; t += nwaves) {
+            uint8_t s0 = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
+            const int r0 = b.roff[t], r1 = b.roff[t + 1];
+            int p = r0 < r1 ? w.eoff[r0] : 0;
+            if (s0 == kUndecided) {
+                int r = r0;
+                for (; r < r1; r++) {
+                    const int q0 = w.eoff[r], q1 = q0 + w.ecur[r];
+                    int first = q1;
+                    for (int base = q0; base < q1; base += 64) {
+                        const int q = base + lane;
+                        bool live = false;
+                        if (q < q1) {
+                            const int e = w.edges[q];
+                            live = (unsigned)e < (unsigned)T && !w.hist_conf[e] && !(b.flags[e] & kFlagTooOld);
+                        }
+                        const uint64_t m = __ballot(live);
+                        if (m) {
+                            first = base + (int)__builtin_ctzll(m);
+                            break;
+                        }
+                    }
+                    if (first < q1) {
+                        p = first;
+                        break;
+                    }
+                }
+                if (r == r1) s0 = kCommitted;
+            }
+            if (lane == 0) {
+                w.pre_st[t] = s0;
+                w.pre_ep[t] = p;
+            }
+        }
+        // publish (MI355X_MICROARCH.md, inter-workgroup visibility: producer form): every storing
+        // wave waits for its stores, then one lane releases at agent scope and arrives
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&sc->pre_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (blockIdx.x != 0) return;  // batch-order rounds run in one workgroup
+    // wait (bounded) for every workgroup's pre-pass; on timeout start from scratch instead (the
+    // late writers write pre_st / pre_ep, which are then not read: still exact)
+    __shared__ int s_pre;
+    if (threadIdx.x == 0) {
+        int ok = 0;
+        if (pre) {
+            // consumer form: relaxed poll, then one agent acquire and its wait, then the barrier
+            for (int spin = 0; spin < (1 << 22); spin++) {
+                if (__hip_atomic_load(&sc->pre_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) {
+                    ok = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_pre = ok;
+    }
+    __syncthreads();
+    const bool use_pre = s_pre != 0;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        st[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
+        st[t] = use_pre ? w.pre_st[t] : ((w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided);
         w.first_conf[t] = INT_MAX;
     }
     __syncthreads();
     int rounds = 0;
     if (!sc->edge_overflow) {
-        for (int t = threadIdx.x; t < T; t += blockDim.x) w.eptr[t] = w.eoff[b.roff[t]];
+        for (int t = threadIdx.x; t < T; t += blockDim.x)
+            w.eptr[t] = use_pre ? w.pre_ep[t] : (b.roff[t] < b.roff[t + 1] ? w.eoff[b.roff[t]] : 0);
         volatile uint8_t* vst = st;
         for (;;) {
             if (threadIdx.x == 0) s_more = 0;
@@ -1163,15 +1270,23 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
                 for (; r < rend; r++) {
                     const int s0 = w.eoff[r], s1 = s0 + w.ecur[r];
                     if (p < s0) p = s0;
+                    // four edges per step, loads issued together: a hot key's reader skips hundreds
+                    // of aborted writers
                     while (p < s1) {
-                        const int e = w.edges[p];
-                        const uint8_t sp = (unsigned)e < (unsigned)T ? vst[e] : kAborted;
-                        if (sp == kAborted) {
-                            p++;
-                            continue;
+                        int e[4];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) e[u] = p + u < s1 ? w.edges[p + u] : -1;
+                        int u = 0;
+                        uint8_t sp = kAborted;
+                        for (; u < 4 && p + u < s1; u++) {
+                            sp = (unsigned)e[u] < (unsigned)T ? vst[e[u]] : kAborted;
+                            if (sp != kAborted) break;
                         }
-                        if (sp == kCommitted) res = kAborted;
-                        break;
+                        p += u;
+                        if (sp != kAborted) {
+                            if (sp == kCommitted) res = kAborted;
+                            break;
+                        }
                     }
                     if (p < s1) break;
                 }
@@ -1261,7 +1376,9 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
 
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report) {
     if (b.T == 0) return;
-    hipLaunchKernelGGL(k_resolve, dim3((b.T + kWG - 1) / kWG), dim3(kWG), (size_t)b.T, s, b, w);
+    // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
+    const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
+    hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kWG), (size_t)b.T, s, b, w);
     if (b.R && report) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
@@ -1889,6 +2006,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         sc->tail_used = ep.gc_ran ? sc->tail_gc : sc->tail_next;
         Scalars out = *sc;
         out.debug_error = ep.bsc->debug_error;
+        ep.bsc->pre_done = 0;  // k_resolve's pre-pass counter (its workgroups have all finished)
         out.intra_rounds = ep.bsc->rounds;
         out.intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
         *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;
