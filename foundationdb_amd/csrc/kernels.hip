@@ -851,33 +851,29 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 eq += h == mh;
             }
             if (eq > 1) {
-                // Items sharing my hi word: low word, then the tie-break word, four items per step
-                // with every LDS load issued first (a read [k, k + d) shares the hi word with its
-                // own end; a hot key fills whole buckets with one prefix).  A pair that needs the
-                // tail bytes (item_tie) sends the item to the exact, deferred-tail path.
+                // Items sharing my hi word.  A key longer than kSortNxLen may need tail compares
+                // (C4 tuple keys): the exact path with deferred tails.  A shorter one never does
+                // (item_tie needs both keys longer): low word, then the tie-break word, four
+                // items per step with every LDS load issued first (a read [k, k + d) shares the
+                // hi word with its own end; a hot key fills whole buckets with one prefix).
                 const uint64_t ax = saux[t], ml = x.lo;
-                const bool xlong = ((ax >> 32) & 31u) == kSortNxLen + 1;
-                int lt2 = 0;
-                bool tie = false;
-                int q = 0;
-                for (; q + 4 <= m; q += 4) {
-                    uint64_t h[4], l[4], w[4];
+                if (((ax >> 32) & 31u) == kSortNxLen + 1) {
+                    lt += rank_shared_hi(sh, shi, m, t, x, arena);
+                } else {
+                    int q = 0;
+                    for (; q + 4 <= m; q += 4) {
+                        uint64_t h[4], l[4], w[4];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) h[u] = shi[q + u], l[u] = slo[q + u], w[u] = saux[q + u];
+                        for (int u = 0; u < 4; u++) h[u] = shi[q + u], l[u] = slo[q + u], w[u] = saux[q + u];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const bool hs = h[u] == mh, ls = l[u] == ml;
-                        tie |= hs && ls && xlong && (w[u] >> 32) == (ax >> 32) && w[u] != ax;
-                        lt2 += (hs && (l[u] < ml || (ls && w[u] < ax))) ? 1 : 0;
+                        for (int u = 0; u < 4; u++)
+                            lt += (h[u] == mh && (l[u] < ml || (l[u] == ml && w[u] < ax))) ? 1 : 0;
+                    }
+                    for (; q < m; q++) {
+                        const uint64_t h = shi[q], l = slo[q], w = saux[q];
+                        lt += (h == mh && (l < ml || (l == ml && w < ax))) ? 1 : 0;
                     }
                 }
-                for (; q < m; q++) {
-                    const uint64_t h = shi[q], l = slo[q], w = saux[q];
-                    const bool hs = h == mh, ls = l == ml;
-                    tie |= hs && ls && xlong && (w >> 32) == (ax >> 32) && w != ax;
-                    lt2 += (hs && (l < ml || (ls && w < ax))) ? 1 : 0;
-                }
-                lt += tie ? rank_shared_hi(sh, shi, m, t, x, arena) : lt2;
             }
             a[off + lt] = x;
         }
