@@ -1429,8 +1429,8 @@ struct SegmentScan {
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
     const int E = 2 * (b.R + b.W);
     Delta d{w.pmeta, w.pos, w.status, b.wowner, b.R};
-    launch_scan<1>(s, CoverScan{d, w.segflag}, nullptr, E, w.scan[kScanCov]);
-    launch_scan<1>(s, SegmentScan{w.segflag, w.seg_b, w.seg_e, sc}, nullptr, E, w.scan[kScanSeg]);
+    launch_scan2<1, CoverScan, 1, SegmentScan>(s, CoverScan{d, w.segflag}, SegmentScan{w.segflag, w.seg_b, w.seg_e, sc}, E,
+                                               w.scan[kScanCov], w.scan[kScanSeg]);
 }
 
 // ------------------------------------------------------------------ D.MergeWrite

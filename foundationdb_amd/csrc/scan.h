@@ -40,19 +40,13 @@ struct ScanState {
     int* error;          // set if a look-back spin exceeded its bound
 };
 
+// One tile of a scan (tile ids come from the caller, in launch order).  Ends with a barrier, so
+// the LDS arrays can be reused by a following stage.
 template <int K, class F>
-__global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr, int64_t n_host, ScanState st) {
-    __shared__ uint32_t sv[K][kScanPad];
-    __shared__ uint32_t swave[K][kScanThreads / 64];
-    __shared__ uint32_t sbase[K];
-    __shared__ int s_tile;
-    const int64_t n = n_ptr ? *n_ptr : n_host;
-    if (threadIdx.x == 0) s_tile = atomicAdd(st.counter, 1);
-    __syncthreads();
-    const int tile = s_tile;
+__device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64_t ntiles, ScanState st,
+                                          uint32_t (&sv)[K][kScanPad], uint32_t (&swave)[K][kScanThreads / 64],
+                                          uint32_t (&sbase)[K]) {
     const int64_t base = (int64_t)tile * kScanTile;
-    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
-    if (tile >= ntiles) return;  // spare tile of a device-sized launch: nobody waits on it
 
     // phase 1: coalesced visits
 #pragma unroll
@@ -172,10 +166,56 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr
         for (int c = 0; c < K; c++) tot[c] = sbase[c] + btot[c];
         f.finish(tot);
     }
+    __syncthreads();
+}
+
+template <int K, class F>
+__global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr, int64_t n_host, ScanState st) {
+    __shared__ uint32_t sv[K][kScanPad];
+    __shared__ uint32_t swave[K][kScanThreads / 64];
+    __shared__ uint32_t sbase[K];
+    __shared__ int s_tile;
+    const int64_t n = n_ptr ? *n_ptr : n_host;
+    if (threadIdx.x == 0) s_tile = atomicAdd(st.counter, 1);
+    __syncthreads();
+    const int tile = s_tile;
+    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+    if (tile >= ntiles) return;  // spare tile of a device-sized launch: nobody waits on it
+    scan_tile<K>(f, n, tile, ntiles, st, sv, swave, sbase);
+}
+
+// Two chained scans over the same n elements in one launch: stage 2's load(i) may read what
+// stage 1's store(i) wrote (both visits of element i run on the same thread).  A tile runs stage
+// 2 after its own stage 1; its stage-2 look-back waits only on tiles that started earlier, which
+// finish their stage 1 without waiting on it, so the chain cannot deadlock.  Saves a launch
+// and its queue gap on the batch-order stream.
+template <int K1, class F1, int K2, class F2>
+__global__ __launch_bounds__(kScanThreads) void k_scan2(F1 f1, F2 f2, int64_t n, ScanState st1, ScanState st2) {
+    constexpr int K = K1 > K2 ? K1 : K2;
+    __shared__ uint32_t sv[K][kScanPad];
+    __shared__ uint32_t swave[K][kScanThreads / 64];
+    __shared__ uint32_t sbase[K];
+    __shared__ int s_tile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(st1.counter, 1);
+    __syncthreads();
+    const int tile = s_tile;
+    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+    if (tile >= ntiles) return;
+    scan_tile<K1>(f1, n, tile, ntiles, st1, reinterpret_cast<uint32_t(&)[K1][kScanPad]>(sv),
+                  reinterpret_cast<uint32_t(&)[K1][kScanThreads / 64]>(swave), reinterpret_cast<uint32_t(&)[K1]>(sbase));
+    scan_tile<K2>(f2, n, tile, ntiles, st2, reinterpret_cast<uint32_t(&)[K2][kScanPad]>(sv),
+                  reinterpret_cast<uint32_t(&)[K2][kScanThreads / 64]>(swave), reinterpret_cast<uint32_t(&)[K2]>(sbase));
 }
 
 // Granules needed for a scan of up to n elements with K components.
 inline int64_t scan_granules(int64_t n, int K) { return ((n > 0 ? n : 1) + kScanTile - 1) / kScanTile * K; }
+
+template <int K1, class F1, int K2, class F2>
+void launch_scan2(hipStream_t s, const F1& f1, const F2& f2, int64_t n, ScanState st1, ScanState st2) {
+    int64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles < 1) tiles = 1;
+    hipLaunchKernelGGL((k_scan2<K1, F1, K2, F2>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f1, f2, n, st1, st2);
+}
 
 template <int K, class F>
 void launch_scan(hipStream_t s, const F& f, const int64_t* n_dev, int64_t n_max, ScanState st) {
