@@ -94,7 +94,7 @@ enum Phase {
 struct fdbcs_batch;
 
 // ws[k] slots: ensure_workspace TAKEs [0, kWsTileSlot); then the copy-tile index and the scan arena.
-constexpr int kWsTileSlot = 46, kWsArenaSlot = 47;
+constexpr int kWsTileSlot = 54, kWsArenaSlot = 55;
 // Batch workspaces in rotation: stage A of the next two batches can run while stage B of the
 // current one does (two stage-A streams), so each workspace is reused every third batch.
 constexpr int kNumWork = 3;
@@ -142,7 +142,7 @@ struct fdbcs_conflict_set {
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
     // batch workspaces (rotating)
-    DBuf ws[kNumWork][48];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
+    DBuf ws[kNumWork][56];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
     int64_t ws_T = -1, ws_R = -1, ws_W = -1;
     Work work[kNumWork]{};
     int64_t edge_cap = 0;
@@ -298,6 +298,8 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(eptr, 4 * T);
     TAKE(pre_st, T);
     TAKE(pre_ep, 4 * T);
+    TAKE(pre_end, 4 * T);
+    TAKE(tedges, 4 * edge_cap);
     TAKE(cov, 4 * E);
     TAKE(mcs_bits, 8 * (E / 64 + 2));
     TAKE(seg_b, 4 * (W + 1));

@@ -147,7 +147,9 @@ struct Work {
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction
     uint8_t* pre_st;       // [T] k_resolve pre-pass: status before the batch-order rounds
-    int32_t* pre_ep;       // [T] k_resolve pre-pass: resume pointer
+    int32_t* pre_ep;       // [T] k_resolve pre-pass: start of t's packed live writers in tedges
+    int32_t* pre_end;      // [T] k_resolve pre-pass: end of t's packed live writers
+    int32_t* tedges;       // [edge_cap] per transaction, its writers not known aborted (packed)
     int32_t* cov;          // [E]
     uint64_t* mcs_bits;    // [E/64+1] sequential-fallback MiniConflictSet
     // union segments (<= W)

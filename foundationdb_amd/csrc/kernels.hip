@@ -1179,35 +1179,31 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
         for (int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < T; t += nwaves) {
             uint8_t s0 = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
             const int r0 = b.roff[t], r1 = b.roff[t + 1];
-            int p = r0 < r1 ? w.eoff[r0] : 0;
+            // t's slots are contiguous over its reads: its live writers are packed at their start
+            const int tbase = r0 < r1 ? w.eoff[r0] : 0;
+            int cnt = 0;
             if (s0 == kUndecided) {
-                int r = r0;
-                for (; r < r1; r++) {
+                for (int r = r0; r < r1; r++) {
                     const int q0 = w.eoff[r], q1 = q0 + w.ecur[r];
-                    int first = q1;
                     for (int base = q0; base < q1; base += 64) {
                         const int q = base + lane;
+                        int e = -1;
                         bool live = false;
                         if (q < q1) {
-                            const int e = w.edges[q];
+                            e = w.edges[q];
                             live = (unsigned)e < (unsigned)T && !w.hist_conf[e] && !(b.flags[e] & kFlagTooOld);
                         }
                         const uint64_t m = __ballot(live);
-                        if (m) {
-                            first = base + (int)__builtin_ctzll(m);
-                            break;
-                        }
-                    }
-                    if (first < q1) {
-                        p = first;
-                        break;
+                        if (live) w.tedges[tbase + cnt + __popcll(m & ((1ull << lane) - 1))] = e;
+                        cnt += __popcll(m);
                     }
                 }
-                if (r == r1) s0 = kCommitted;
+                if (cnt == 0) s0 = kCommitted;
             }
             if (lane == 0) {
                 w.pre_st[t] = s0;
-                w.pre_ep[t] = p;
+                w.pre_ep[t] = tbase;
+                w.pre_end[t] = tbase + cnt;
             }
         }
         // publish (MI355X_MICROARCH.md, inter-workgroup visibility: producer form): every storing
@@ -1261,6 +1257,27 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
                 // resume at edge p: skip aborted writers, stop at the first undecided or committed
                 int p = w.eptr[t];
                 uint8_t res = kUndecided;
+                if (use_pre) {
+                    // the pre-pass packed t's writers not known aborted: one contiguous list
+                    const int end = w.pre_end[t];
+                    while (p < end) {
+                        const int e = w.tedges[p];
+                        const uint8_t sp = vst[e];
+                        if (sp == kAborted) {
+                            p++;
+                            continue;
+                        }
+                        if (sp == kCommitted) res = kAborted;
+                        break;
+                    }
+                    if (p == end) res = kCommitted;
+                    w.eptr[t] = p;
+                    if (res != kUndecided)
+                        vst[t] = res;
+                    else
+                        more = 1;
+                    continue;
+                }
                 int r = b.roff[t];
                 const int rend = b.roff[t + 1];
                 for (; r < rend; r++) {
