@@ -138,8 +138,6 @@ struct Work {
     uint8_t* segflag;      // [E] bit0: union segment starts here, bit1: one ends here
     int32_t* wbpos;        // [W] positions of write-begins in order
     int32_t* rbpos;        // [R] positions of read-begins in order
-    int32_t* ecnt_a;       // [R] (unused)
-    int32_t* ecnt_b;       // [R] (unused; zeroed by the epilogue)
     int32_t* eoff;         // [R+1] first edge slot of each read
     int32_t* poff;         // [R+W+1] first candidate pair of each range
     int32_t* ecur;         // [R] edges of each read (slots taken; zeroed by the epilogue)
@@ -173,6 +171,7 @@ struct Work {
     int64_t *c_lo, *c_hi, *c_rem, *c_ins, *c_val;
     uint8_t* c_exact;
     unsigned long long* trace;  // [kTrSlots] or null
+    int32_t no_prepass;         // FDBCS_RESOLVE_PREPASS=0: resolution rounds without the pre-pass (tests)
 };
 
 // FDBCS_TRACE: device timestamps (wall_clock64 ticks) of kernel sections, for tuning.

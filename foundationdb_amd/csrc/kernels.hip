@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
     // known aborted.  These are exactly the decisions round one would make, but a hot key's reader
     // (hundreds of aborted writers, C3) costs a few ballots instead of a serial walk, and every
     // transaction's chain of dependent loads runs on its own wave across the chip.
-    const bool pre = !sc->edge_overflow;
+    const bool pre = !sc->edge_overflow && !w.no_prepass;
     if (pre) {
         const int lane = threadIdx.x & 63;
         const int nwaves = gridDim.x * (blockDim.x >> 6);
@@ -1895,7 +1895,6 @@ struct Epilogue {
     int compacted, gc_ran;
     uint8_t* zero8;  // hist_conf
     int64_t zero8_n;
-    int32_t* zero32a;  // ecnt_b
     int32_t* zero32b;  // ecur
     int64_t zero32_n;
     uint64_t* zero64;  // scan arena
@@ -1980,10 +1979,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     };
     for (int64_t t = tid; t < ep.T; t += stride) ep.verdict_dev[t] = verdict(t);
     for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
-    for (int64_t i = tid; i < ep.zero32_n; i += stride) {
-        ep.zero32a[i] = 0;
-        ep.zero32b[i] = 0;
-    }
+    for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
     for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
     for (int64_t i = tid; i < kMaxBuckets; i += stride) {
         ep.zero_bc[i] = 0;
@@ -2071,7 +2067,6 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.gc_ran = gc_ran;
     ep.zero8 = w.hist_conf;
     ep.zero8_n = w.cap_T;
-    ep.zero32a = w.ecnt_b;
     ep.zero32b = w.ecur;
     ep.zero32_n = w.cap_R;
     ep.zero64 = w.scan_arena;

@@ -193,7 +193,12 @@ def test_c2_reduced(engine, oracle_mod):
         assert (ve == vo).all(), i
 
 
-def test_c3_zipf_heavy_contention(engine, oracle_mod):
+@pytest.mark.parametrize("prepass", ["1", "0"])
+def test_c3_zipf_heavy_contention(engine, oracle_mod, monkeypatch, prepass):
+    """Zipf hot keys: hundreds of candidate writers per reader, most of them history-aborted.
+    Both resolution paths: with the multi-workgroup pre-pass (packed live-writer lists) and
+    without it (rounds walk the per-read edge lists)."""
+    monkeypatch.setenv("FDBCS_RESOLVE_PREPASS", prepass)
     p = W.C2Params(txns=3000)
     z = W.ZipfGenerator(1_000_000, 0.99)
     rng = np.random.default_rng(3)
