@@ -1032,7 +1032,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_check(s, bd, w, base, delta, htail);
     if ((rc = mark(kPhCheck))) return rc;
     if (sa != s) HIPOK(hipStreamWaitEvent(s, cs->ev_a[wp], 0));
-    launch_resolve(s, bd, w, b->any_report);
+    launch_resolve(s, bd, w, b->any_report, (uint8_t*)b->pin_out.dp);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf
         if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
         HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));

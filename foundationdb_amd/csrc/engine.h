@@ -214,7 +214,8 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report);
+// verdict_out: the batch's host-mapped verdict bytes (the epilogue publishes them with the flag).
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out);
 void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 // `srcm` are the source tier's levels: its key index is searched, its top level reset for the

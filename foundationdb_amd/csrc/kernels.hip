@@ -1151,7 +1151,14 @@ void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
 // rounds terminate.  If the candidate edges overflowed, the workgroup replays MiniConflictSet
 // sequentially over point indices instead (exact, slower).
 
-__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
+// vout: the batch's host-mapped verdict bytes (ConflictSet.h:40-44 encoding), written here as soon
+// as each status is final so the epilogue only publishes scalars and the completion flag.
+__device__ __forceinline__ uint8_t verdict_byte(const BatchDev& b, int t, uint8_t status) {
+    if (b.flags[t] & kFlagTooOld) return 1;  // TransactionTooOld
+    return status == kCommitted ? 2 : 0;     // TransactionCommitted : TransactionConflict
+}
+
+__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vout) {
     BatchScalars* sc = w.bsc;
     extern __shared__ __attribute__((aligned(16))) uint8_t st[];
     __shared__ int s_more;
@@ -1160,8 +1167,10 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
         // no candidate writer anywhere: every admitted transaction without a history conflict
         // commits (SkipList.cpp:817-833 with an empty MiniConflictSet); all workgroups share the work
         for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
-            w.status[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
+            const uint8_t st = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
+            w.status[t] = st;
             w.first_conf[t] = INT_MAX;
+            vout[t] = verdict_byte(b, t, st);
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) sc->rounds = 0;
         return;
@@ -1366,7 +1375,10 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w) {
         rounds = -1;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += blockDim.x) w.status[t] = st[t];
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        w.status[t] = st[t];
+        vout[t] = verdict_byte(b, t, st[t]);
+    }
     if (threadIdx.x == 0) sc->rounds = rounds;
 }
 
@@ -1387,11 +1399,11 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
     }
 }
 
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report) {
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out) {
     if (b.T == 0) return;
     // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
     const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
-    hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kWG), (size_t)b.T, s, b, w);
+    hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kWG), (size_t)b.T, s, b, w, verdict_out);
     if (b.R && report) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
@@ -1989,22 +2001,9 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     __syncthreads();
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiZero);
     if (blockIdx.x != 0) return;
-    // Workgroup 0 writes what the host reads (host-mapped, 16 verdicts per store), then publishes
-    // the batch's sequence number; everything else this launch writes is read only by later
-    // kernels on the same stream.
-    for (int64_t q = threadIdx.x; q * 16 < ep.T; q += blockDim.x) {
-        uint32_t wv[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int64_t t = q * 16 + k;
-            if (t < ep.T) wv[k >> 2] |= (uint32_t)verdict(t) << (8 * (k & 3));
-        }
-        if (q * 16 + 16 <= ep.T) {
-            *reinterpret_cast<uint4*>(ep.verdict_out + q * 16) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-        } else {
-            for (int k = 0; q * 16 + k < ep.T; k++) ep.verdict_out[q * 16 + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
-        }
-    }
+    // Workgroup 0 writes the scalars the host reads next to the verdicts (which k_resolve already
+    // wrote to the host-mapped buffer), then publishes the batch's sequence number; everything
+    // else this launch writes is read only by later kernels on the same stream.
     if (threadIdx.x == 0) {
         if (ep.compacted) {
             sc->n = ep.gc_ran ? sc->n_gc : sc->n_next;
