@@ -150,6 +150,7 @@ struct fdbcs_conflict_set {
     int inflight = 0;
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
     int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket (testing knob; 0 = default)
+    int sample_per = 0;     // FDBCS_SORT_SAMPLES: splitter samples per bucket (0 = default 8)
     bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)
@@ -601,6 +602,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     cs->device = device;
     if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
     if (const char* v = getenv("FDBCS_SORT_BUCKET")) cs->bucket_target = atoi(v);
+    if (const char* v = getenv("FDBCS_SORT_SAMPLES")) cs->sample_per = atoi(v);
     if (const char* v = getenv("FDBCS_TRACE")) cs->trace = v[0] == '1';
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
@@ -1019,9 +1021,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(hipMemcpy(w.trace, init, sizeof(init), hipMemcpyHostToDevice));
     }
     // ---- stage A: D.Sort and the candidate edges of D.CheckIntraBatch
-    launch_sample(sa, bd, w, cs->bucket_target);
+    launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
     int sorted = 0;
-    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sort_alg, &sorted);
+    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted);
     if ((rc = mark(kPhSort))) return rc;
     launch_positions(sa, bd, w, sorted);
     if (cs->validate) launch_validate_sort(sa, bd, w, sorted);

@@ -203,13 +203,14 @@ struct Tier {
 //   B (reads/writes the history, in batch order): launch_check, launch_resolve, launch_combine,
 //     launch_merge, launch_compact/gc, launch_epilogue.
 // Sample ranking for the sort's splitters.
-void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target);
+void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per);
 // D.CheckRead against the history the previous batch left.
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
                   const uint8_t* htail);
-// bucket_target: endpoints per sample-sort bucket (0 = default 256; tests force oversized buckets).
+// bucket_target: endpoints per sample-sort bucket (0 = default 128; tests force oversized buckets).
+// sample_per: splitter samples per bucket (0 = default 8).
 // alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int alg,
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per, int alg,
                         int* result_buffer);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);

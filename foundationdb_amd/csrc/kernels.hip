@@ -590,8 +590,9 @@ __global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
 
 // Number of samples for nb buckets (about 8 per bucket: the largest of ~550 buckets stays well
 // under the one-pass bitonic size; 4 per bucket let one in ~3 batches pass it at C2).
-__host__ __device__ inline int sample_count(int E, int nb) {
-    int S = 8 * nb;
+// per: samples per bucket (FDBCS_SORT_SAMPLES; 0 = default 8).
+inline int sample_count(int E, int nb, int per) {
+    int S = (per > 0 ? per : 8) * nb;
     S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
     return S > E ? E : S;
 }
@@ -625,12 +626,11 @@ __device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl
     return lo;
 }
 
-__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32_t* srank, int nb,
+__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32_t* srank, int nb, int S,
                                                          uint16_t* bucket, int32_t* bcount, const uint8_t* arena) {
     __shared__ SortItem spl[kMaxBuckets - 1];
     __shared__ int hist[kMaxBuckets];
     const int E = 2 * (b.R + b.W);
-    const int S = sample_count(E, nb);
     // splitter k-1 is the sample of rank k*S/nb (ranks are distinct: items are totally ordered)
     for (int q = threadIdx.x; q < S; q += blockDim.x) {
         const int r = srank[q];
@@ -927,12 +927,12 @@ int sort_buckets(int E, int target) {
     return nb > kMaxBuckets ? kMaxBuckets : nb;
 }
 
-void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target) {
+void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per) {
     const int E = 2 * (b.R + b.W);
     const int nb = E ? sort_buckets(E, bucket_target) : 1;
     if (nb <= 1) return;
     SampleRank c{};
-    c.S = sample_count(E, nb);
+    c.S = sample_count(E, nb, sample_per);
     c.n_slice = (c.S + kSampleSlice - 1) / kSampleSlice;
     c.srank = w.srank;
     c.trace = w.trace;
@@ -948,14 +948,15 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
     hipLaunchKernelGGL(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int alg,
-                        int* result_buffer) {
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
+                        int alg, int* result_buffer) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
     const int nb = sort_buckets(E, bucket_target);
     const int grid = (E + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, w.bucket, w.bcount, b.tail);
+    const int S = nb > 1 ? sample_count(E, nb, sample_per) : 0;
+    hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
     if (alg == 1)
