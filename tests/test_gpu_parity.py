@@ -285,11 +285,13 @@ def test_edge_cases(engine):
     assert ex.value.status == engine.FDBCS_E_VERSION
 
 
-@pytest.mark.parametrize("bucket", ["3000", "40"])
-def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket):
-    """Oversized sort buckets (chunked rank sort + merges through memory) and tiny ones, with keys
-    longer than the 16-byte prefix, give the same verdicts and reports."""
+@pytest.mark.parametrize("bucket,samples", [("3000", "0"), ("40", "0"), ("160", "2"), ("64", "1")])
+def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket, samples):
+    """Oversized sort buckets (chunked rank sort + merges through memory), tiny ones, and sparse
+    splitter samples (skewed buckets), with keys longer than the 16-byte prefix, give the same
+    verdicts and reports."""
     monkeypatch.setenv("FDBCS_SORT_BUCKET", bucket)
+    monkeypatch.setenv("FDBCS_SORT_SAMPLES", samples)
     rng = np.random.default_rng(31)
     seq = []
     now = 10
