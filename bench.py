@@ -3,15 +3,29 @@
 
 Workload (BASELINE.json configs[1], "C2"): a single-MI355X resolver with 5000-transaction commit
 batches, 5 read + 2 write conflict ranges per transaction, 16-byte uniform keys, over a
-5M-boundary MVCC history prefilled across a 5e6-version window.  A step is one
-ConflictBatch::detectConflicts pass (SkipList.cpp:844-890) over one batch, inputs already resident
-in HBM (uploaded before the timed region).
+5M-boundary MVCC history prefilled across a 5e6-version window.  `--workload c1|c3|c4` selects the
+other BASELINE configurations (skipListTest, Zipf hot keys, tuple keys over a 50M-boundary window).
+
+A step is one ConflictBatch::detectConflicts (SkipList.cpp:844-890) over one batch.  The timed
+region of `value` holds, per batch, the H2D copy of the packed batch, every kernel and the verdict
+bytes back in host memory (H2D/D2H included, generation excluded); addTransaction
+(the host-side normalization into pinned staging) happens before it, as the reference's "Detect
+only" figure excludes addTransaction (SkipList.cpp:1069-1078, 1087-1090).  `total_txns_per_s`
+is the reference's "total" figure: addTransaction inside the timed loop as well.
+
+After timing, the same batch sequence (warmup, timed, total and breakdown batches) is replayed on
+the CPU restatement of the reference algorithm (oracle/skiplist_baseline.cpp) and every GPU
+verdict is compared: `parity` in the JSON line.  At N=1 that replay's time over the timed batches
+is `cpu_baseline` (single thread, pinned to one core like skipListTest's setAffinity(0),
+SkipList.cpp:1015).
 
 N > 1 (torchrun, one rank per GPU): the key space is range-sharded across ranks like FDB's
 multi-resolver split (CommitProxyServer.actor.cpp:147-174).  Every rank builds the same global batch
 of N x 5000 transactions, keeps its routed sub-batch, resolves it on its GPU, and the verdicts are
 combined by an RCCL all-reduce MAX of conflict bytes (= proxy min over resolvers,
-CommitProxyServer.actor.cpp:772-777).  Weak scaling: per-GPU work is fixed.
+CommitProxyServer.actor.cpp:772-777).  Weak scaling: per-GPU work is fixed.  Parity at N > 1:
+every rank replays its own routed sub-batches on its own CPU restatement (G reference conflict
+sets fed the same routing).
 
 Prints ONE JSON line on rank 0.
 """
@@ -29,7 +43,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+import roofline  # noqa: E402
+
+WINDOW = 8  # batches in flight (submitted, not yet waited) in the timed loops
 
 
 def parse():
@@ -37,20 +53,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--txns", type=int, default=5000)
+    ap.add_argument("--txns", type=int, default=0, help="transactions per batch per GPU; 0 = the workload's")
     ap.add_argument("--history", type=int, default=0,
-                    help="history boundaries per GPU; 0 = the workload's (5M for c2/c3, 50M for c4)")
+                    help="history boundaries per GPU; 0 = the workload's (5M for c2/c3, 50M for c4, empty for c1)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--gc-interval", type=int, default=0,
                     help="force a compaction (+GC) at least every N batches; 0 = when the delta tier is full")
     ap.add_argument("--delta-limit", type=int, default=0, help="delta-tier bound; 0 = automatic (~base/16)")
     ap.add_argument("--timing", type=int, default=1, choices=[0, 1],
-                    help="events in the timed region: 0 none, 1 around the copy kernels (roofline)")
+                    help="events in the timed region: 0 none, 1 around the hot kernels (roofline)")
+    ap.add_argument("--total-steps", type=int, default=-1,
+                    help="batches of the add+detect ('total') pass; -1 = --steps, 0 = skip")
     ap.add_argument("--breakdown-steps", type=int, default=16,
                     help="extra batches after the timed region with every phase timed (diagnostic)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="bound on the CPU replay (parity + cpu_baseline); batches past it are not checked")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU replay (no parity, no baseline)")
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the verdict all-reduce (nccl = RCCL over xGMI)")
     return ap.parse_args()
@@ -64,8 +83,10 @@ def workload_params(args):
     from foundationdb_amd import workloads as W
 
     if args.workload == "c4":
-        return W.C4Params(txns=args.txns, history=args.history or 50_000_000)
-    return W.C2Params(txns=args.txns, history=args.history or 5_000_000)
+        return W.C4Params(txns=args.txns or 5000, history=args.history or 50_000_000)
+    if args.workload == "c1":
+        return W.C2Params(txns=args.txns or 2500, reads=1, writes=1, history=args.history or 0)
+    return W.C2Params(txns=args.txns or 5000, history=args.history or 5_000_000)
 
 
 def sharding_for(args, p, world):
@@ -76,6 +97,8 @@ def sharding_for(args, p, world):
         return None
     if args.workload == "c4":  # every key shares the subspace: split by user
         return KeyRangeSharding([W.c4_user_split(p, g * p.users // world) for g in range(1, world)])
+    if args.workload == "c1":  # setK keys share 12 bytes of '.': split on the integer
+        return KeyRangeSharding([W.setk([g * 20_000_000 // world])[0].tobytes() for g in range(1, world)])
     return KeyRangeSharding.uniform(world)
 
 
@@ -83,6 +106,8 @@ def shard_history(args, p, seed, rank, world, start_version):
     """Prefill: p.history boundaries inside this rank's key range."""
     from foundationdb_amd.workloads import c2_history, c4_history
 
+    if args.workload == "c1" or p.history == 0:
+        return np.zeros(0, np.uint8), np.zeros(1, np.int64), np.zeros(0, np.int64)
     if args.workload == "c4":
         users = (rank * p.users // world, (rank + 1) * p.users // world)
         return c4_history(p, seed=seed * 1000 + rank, start_version=start_version, users=users)
@@ -111,9 +136,11 @@ def make_batches(args, p, n_batches, world, start_version):
 
     import dataclasses
 
+    if args.workload == "c1":  # skipListTest: snapshot v, now v + 50, newOldest v (SkipList.cpp:1063-1077)
+        return list(W.c1_batches(n_batches, seed=args.seed, data_per_batch=2 * p.txns * world))
     rng = np.random.default_rng(args.seed)
     zipf = W.ZipfGenerator(1_000_000, 0.99) if args.workload == "c3" else None
-    gp = dataclasses.replace(p, txns=args.txns * world)
+    gp = dataclasses.replace(p, txns=p.txns * world)
     out = []
     now = start_version
     for _ in range(n_batches):
@@ -126,45 +153,80 @@ def make_batches(args, p, n_batches, world, start_version):
     return out
 
 
-def cpu_baseline(args, p, kb, ko, vers, batches):
-    """Skip-list restatement of the reference (oracle/skiplist_baseline.cpp), single thread,
-    over a bounded sample of the same workload."""
-    from oracle import oracle
-
-    oracle.build()
-    sl = oracle.SkipListBaseline()
-    t0 = time.time()
-    sl.load_history(kb, ko, vers)
-    load_s = time.time() - t0
-    done_txn = 0
-    done_batches = 0
-    spent = 0.0
-    for pb, now, no in batches:
-        t = time.perf_counter()
-        sl.detect(pb, now, no)
-        spent += time.perf_counter() - t
-        done_txn += pb.n_txn
-        done_batches += 1
-        if spent >= args.cpu_seconds:
-            break
+def cpu_model():
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {
+    return cpu
+
+
+def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
+    """Replay every batch in order on the CPU restatement (oracle/skiplist_baseline.cpp): compare
+    each GPU verdict vector and time the batches in `timed` (single thread, pinned to one core)."""
+    from oracle import oracle
+
+    oracle.build()
+    try:  # skipListTest pins itself to one core (setAffinity(0), SkipList.cpp:1015)
+        cores = sorted(os.sched_getaffinity(0))
+        os.sched_setaffinity(0, {cores[(rank * 2) % len(cores)]})
+    except (AttributeError, OSError):
+        cores = []
+    sl = oracle.SkipListBaseline()
+    t0 = time.time()
+    sl.load_history(kb, ko, vers)
+    load_s = time.time() - t0
+    checked = mismatches = txn_mismatch = 0
+    spent = 0.0
+    done_txn = done_batches = 0
+    first_bad = None
+    t_begin = time.time()
+    for i, b in enumerate(mine):
+        _, now, no = gbatches[i]
+        t = time.perf_counter()
+        v, _ = sl.detect(b, now, no)
+        dt = time.perf_counter() - t
+        if i in timed:
+            spent += dt
+            done_txn += b.n_txn
+            done_batches += 1
+        g = gpu_verdicts[i]
+        if g is not None:
+            checked += 1
+            bad = int((g != v).sum())
+            if bad:
+                mismatches += 1
+                txn_mismatch += bad
+                if first_bad is None:
+                    first_bad = i
+        if time.time() - t_begin > args.cpu_seconds:
+            break
+    if cores:
+        os.sched_setaffinity(0, set(cores))
+    parity = {
+        "reference": "oracle/skiplist_baseline.cpp (reference algorithm, restated; cross-checked vs "
+        "oracle/semantic_oracle.cpp in tests/test_oracle.py)",
+        "batches_checked": checked,
+        "batches_total": len(mine),
+        "mismatched_batches": mismatches,
+        "mismatched_txns": txn_mismatch,
+        "first_mismatch": first_bad,
+    }
+    base = {
         "value": done_txn / spent if spent > 0 else None,
         "unit": "txns/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{done_batches} {args.workload.upper()} batches x {args.txns} txns on a {len(vers)}-boundary history "
-        f"({spent:.1f}s CPU, load {load_s:.1f}s), skip-list restatement oracle/skiplist_baseline.cpp, "
-        f"1 thread on {cpu}",
+        "label": "reference algorithm, restated (oracle/skiplist_baseline.cpp)",
+        "sample": f"{done_batches} timed {args.workload.upper()} batches (after replaying the warmup batches) on a "
+        f"{len(vers)}-boundary history ({spent:.1f}s CPU, history load {load_s:.1f}s), 1 thread pinned to one core "
+        f"of {cpu_model()} (nproc {os.cpu_count()})",
     }
+    return parity, base
 
 
 def main():
@@ -187,15 +249,16 @@ def main():
 
     fbuild.build()
     from foundationdb_amd import conflict_set as C
-    from foundationdb_amd import workloads as W
     from foundationdb_amd.sharding import KeyRangeSharding
 
     p = workload_params(args)
     start_version = 10_000_000
     t0 = time.time()
     kb, ko, vers = shard_history(args, p, args.seed, rank, world, start_version)
-    total = args.warmup + args.steps
-    n_all = total + args.breakdown_steps
+    n_total = args.steps if args.total_steps < 0 else args.total_steps
+    timed_lo, timed_hi = args.warmup, args.warmup + args.steps
+    total_lo, total_hi = timed_hi, timed_hi + n_total
+    n_all = total_hi + args.breakdown_steps
     gbatches = make_batches(args, p, n_all, world, start_version)
     sharding = sharding_for(args, p, world)
     routed = [sharding.route(pb)[rank] for pb, _, _ in gbatches] if sharding else None
@@ -205,103 +268,163 @@ def main():
     cs.set_gc_interval(args.gc_interval)
     cs.set_delta_limit(args.delta_limit)
     cs.set_timing(args.timing)
-    cs.load_history(kb, ko, vers, 0)
+    if len(vers):
+        cs.load_history(kb, ko, vers, 0)
     mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
     maxT = max(b.n_txn for b in mine)
     maxR = max(b.n_reads for b in mine)
     maxW = max(b.n_writes for b in mine)
+
     def tail_bytes(ko):
         return int(np.maximum(np.diff(ko) - 16, 0).sum())
 
     tail_total = tail_bytes(ko) + sum(tail_bytes(b.key_offsets) for b in mine) + (1 << 20)
     cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, tail_total, maxT, maxR, maxW)
-    objs = []
-    for b in mine:
-        o = C.ConflictBatch(cs)
-        o.add_packed(b)
-        o.upload()
-        objs.append(o)
-    torch.cuda.synchronize()
+    verdicts = [None] * n_all
 
-    def run(lo, hi, combine):
+    def combine(i, v):
+        T = gbatches[i][0].n_txn
+        c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+
+    def run(lo, hi, objs):
+        """Submit batches lo..hi-1 (objs: packed ConflictBatch objects, or None: pack inside the
+        loop), keeping at most WINDOW in flight; upload (H2D), kernels and verdicts each time."""
+        inflight = []
         for i in range(lo, hi):
             _, now, no = gbatches[i]
-            objs[i].detect_async(now, no)
-        for i in range(lo, hi):
-            v = objs[i].wait()
-            if combine:
-                T = gbatches[i][0].n_txn
-                c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
-                dist.all_reduce(c, op=dist.ReduceOp.MAX)
+            if objs is None:
+                o = C.ConflictBatch(cs)
+                o.add_packed(mine[i])
+            else:
+                o = objs[i]
+            o.detect_async(now, no)
+            inflight.append((i, o))
+            if len(inflight) > WINDOW:
+                j, oj = inflight.pop(0)
+                verdicts[j] = oj.wait()
+                if dist is not None:
+                    combine(j, verdicts[j])
+                oj.close()
+        for j, oj in inflight:
+            verdicts[j] = oj.wait()
+            if dist is not None:
+                combine(j, verdicts[j])
+            oj.close()
 
-    run(0, args.warmup, dist is not None)
-    torch.cuda.synchronize()
-    cs.reset_stats()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    run(args.warmup, total, dist is not None)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    def packed(lo, hi):
+        objs = {}
+        for i in range(lo, hi):
+            o = C.ConflictBatch(cs)
+            o.add_packed(mine[i])  # addTransaction: normalized into pinned staging, not uploaded
+            objs[i] = o
+        return objs
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
+
+    run(0, timed_lo, packed(0, timed_lo))
+    objs = packed(timed_lo, timed_hi)
+    cs.reset_stats()
+    barrier()
+    t_start = time.perf_counter()
+    run(timed_lo, timed_hi, objs)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t_start)
     st = cs.stats()
+
+    total_elapsed = None
+    if n_total > 0:  # the reference's "total": addTransaction inside the loop as well
+        barrier()
+        t_start = time.perf_counter()
+        run(total_lo, total_hi, None)
+        barrier()
+        total_elapsed = max_over_ranks(time.perf_counter() - t_start)
+
     # diagnostic phase split: extra batches with every phase timed (each event costs queue time,
     # so these are outside the timed region)
     phase = None
     if args.breakdown_steps > 0:
         cs.set_timing(2)
         cs.reset_stats()
-        run(total, n_all, dist is not None)
+        run(total_hi, n_all, packed(total_hi, n_all))
         torch.cuda.synchronize()
         sb = cs.stats()
         phase = {
             k: sb[k] / max(1, sb["batches"])
-            for k in ("ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_compact", "ms_gc",
-                      "ms_epilogue", "ms_total")
+            for k in ("ms_upload", "ms_check_read", "ms_sort", "ms_intra", "ms_combine", "ms_merge", "ms_compact",
+                      "ms_gc", "ms_epilogue", "ms_total")
         }
         phase["batches"] = sb["batches"]
         phase["compactions"] = sb["compactions"]
         phase["intra_edges"] = sb["intra_edges"] / max(1, sb["batches"] - sb["intra_fallbacks"])
         phase["intra_rounds"] = sb["intra_rounds"] / max(1, sb["batches"] - sb["intra_fallbacks"])
         phase["intra_fallbacks"] = sb["intra_fallbacks"]
-    gtxn = sum(gbatches[i][0].n_txn for i in range(args.warmup, total))
-    granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(args.warmup, total))
+    gtxn = sum(gbatches[i][0].n_txn for i in range(timed_lo, timed_hi))
+    granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(timed_lo, timed_hi))
+    ttxn = sum(gbatches[i][0].n_txn for i in range(total_lo, total_hi))
     hist_end = cs.history_size()
+    cs.close()
 
-    # Dominant kernel: of the two copy kernels (delta merge every batch, compaction of the base every
-    # ~16 batches) the one with the larger total device time; both are HBM-bound rewrites of a
-    # sorted boundary array reading 32 B per old boundary and writing 32 B per kept one.
-    kernels = {
-        "merge": ("k_merge_copy<BatchIns> (delta-tier merge)", st["ms_merge_kernel"], st["merge_launches"],
-                  st["merge_bytes"]),
-        "compact": ("k_merge_copy<CompactIns> (base-tier compaction)", st["ms_compact_kernel"], st["compactions"],
-                    st["compact_bytes"]),
-    }
-    dom = max(kernels, key=lambda k: kernels[k][1])
-    kname, kms, klaunch, kbytes = kernels[dom]
-    launches = max(1, klaunch)
-    avg_ms = kms / launches
-    bytes_per_launch = kbytes / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    # PMC HBM bytes per launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate rocprofv3
-    # passes: scripts/gpu_pmc.sh) of this workload's copy kernels, measured on the same command
-    pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
-    if os.path.exists(pmc):
-        try:
-            with open(pmc) as f:
-                traffic = json.load(f).get(f"{dom}_bytes_per_launch")
-        except Exception:
-            traffic = None
-    other = kernels["compact" if dom == "merge" else "merge"]
+    # roofline: the hot kernel with the largest device time in the timed region (HIP events on the
+    # stream each kernel runs on), algorithmic bytes from the §8(d) model (roofline.py)
+    kern = roofline.kernels_from_stats(st) if args.timing >= 1 else {}
+    dom = roofline.dominant(kern)
+    roof = None
+    if dom is not None:
+        k = kern[dom]
+        traffic = None
+        # PMC HBM bytes per launch of the same kernel on the same command (FETCH_SIZE x2 gfx950
+        # correction + WRITE_SIZE, separate rocprofv3 passes: scripts/gpu_pmc.sh)
+        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    traffic = json.load(f).get(f"{dom}_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {
+            "kernel": k["kernel"],
+            "bound": "hbm",
+            "achieved": k["achieved_GBps"],
+            "peak": roofline.HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": k["frac"],
+            "traffic": traffic,
+            "avg_launch_ms": k["avg_launch_ms"],
+            "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"],
+        }
 
+    parity = cpu_base = None
+    if not args.no_cpu_baseline:
+        timed = set(range(timed_lo, timed_hi))
+        parity, cpu_base = cpu_replay(args, kb, ko, vers, mine, gbatches, verdicts, timed, rank)
+        if dist is not None:
+            t = torch.tensor([parity["batches_checked"], parity["mismatched_batches"], parity["mismatched_txns"]],
+                             dtype=torch.int64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            parity["batches_checked"], parity["mismatched_batches"], parity["mismatched_txns"] = (
+                int(x) for x in t.tolist())
+            parity["scope"] = f"{world} ranks, each against its own restatement fed the same routing"
+
+    cfg_desc = {
+        "c1": "skipListTest (SkipList.cpp:1023-1077): 1R+1W per txn, setK 16-byte keys over [0, 2e7), empty initial "
+        "history, now = v+50, newOldest = v",
+        "c2": "5R+2W ranges/txn, 16-byte uniform keys",
+        "c3": "5R+2W ranges/txn, YCSB Zipf(0.99) hot keys over 1M Mako-style 16-byte keys",
+        "c4": "1 wide Tuple.range() read + 4 point reads + 2 point writes per txn, tuple keys (subspace, user string, "
+        "int) up to 100 B",
+    }[args.workload]
     out = {
         "metric": "resolved txns/sec (conflict ranges checked/sec) per batch; HBM GB/s vs peak",
         "value": gtxn / elapsed,
@@ -316,46 +439,29 @@ def main():
         "dtype": "u8/int64 (byte keys, int64 versions)",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.workload.upper()}: {args.txns}-txn batches per GPU, 5R+2W ranges/txn, "
-            + {"c2": "16-byte uniform keys", "c3": "YCSB Zipf(0.99) hot keys over 1M Mako-style 16-byte keys",
-               "c4": "tuple keys (subspace, user string, int) up to 100 B, 1 wide Tuple.range() read per txn"}[
-                args.workload]
-            + f", {p.history}-boundary MVCC history per GPU (5e6-version window)",
-            "global_batch_txns": args.txns * world,
+            "workload": f"{args.workload.upper()}: {p.txns}-txn batches per GPU, {cfg_desc}, "
+            + (f"{p.history}-boundary MVCC history per GPU (5e6-version window)" if p.history else "no prefill"),
+            "global_batch_txns": p.txns * world,
             "parallelism": f"key-range shards x{world}" if world > 1 else "single resolver",
+            "timed_region": "per batch: H2D of the packed batch, all kernels, verdict bytes in host memory "
+            f"({WINDOW} batches in flight); addTransaction packing outside (reference 'Detect only')",
             "gc_interval": args.gc_interval,
             "delta_limit": args.delta_limit or "auto",
         },
         "conflict_ranges_per_s": granges / elapsed,
+        "total_txns_per_s": ttxn / total_elapsed if total_elapsed else None,
+        "total_note": "reference 'total' (SkipList.cpp:1082-1085): addTransaction + detect, per batch in the loop",
+        "parity": parity,
         "history_boundaries_end": hist_end,
         "phase_ms_per_batch": phase,
         "compactions": st["compactions"],
-        "other_copy_kernel": {
-            "kernel": other[0],
-            "launches": other[2],
-            "avg_launch_ms": other[1] / max(1, other[2]),
-            "achieved_GBps": (other[3] / max(1, other[2])) / (other[1] / max(1, other[2]) * 1e-3) / 1e9
-            if other[1] > 0 else None,
-        },
-        "roofline": {
-            "kernel": kname,
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "avg_launch_ms": avg_ms,
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-        },
+        "kernels": kern,
+        "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, p, kb, ko, vers, gbatches[args.warmup :])
+    if rank == 0 and world == 1:
+        out["cpu_baseline"] = cpu_base
     elif rank == 0:
         out["cpu_baseline"] = None
-    for o in objs:
-        o.close()
-    cs.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -71,6 +71,13 @@ class Stats(ctypes.Structure):
         ("intra_edges", ctypes.c_int64),
         ("intra_rounds", ctypes.c_int64),
         ("intra_fallbacks", ctypes.c_int64),
+        ("ms_check_kernel", ctypes.c_double),
+        ("check_launches", ctypes.c_int64),
+        ("check_reads", ctypes.c_int64),
+        ("check_history", ctypes.c_int64),
+        ("ms_sort_kernel", ctypes.c_double),
+        ("sort_launches", ctypes.c_int64),
+        ("sort_items", ctypes.c_int64),
     ]
 
     def as_dict(self):

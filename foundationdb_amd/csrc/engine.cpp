@@ -86,12 +86,14 @@ struct HBuf {
 
 enum Phase {
     kPhStart, kPhUpload, kPhSort, kPhEdges, kPhCheck, kPhIntra, kPhCombine, kPhCopyBegin, kPhCopyEnd, kPhMerge,
-    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd, kPhCount
+    kPhCompBegin, kPhCompEnd, kPhCompact, kPhGc, kPhEpilogue, kPhEnd,
+    kPhCheckBegin, kPhCheckEnd, kPhSortBegin, kPhSortEnd, kPhCount
 };
 
 }  // namespace
 
 struct fdbcs_batch;
+struct BatchSlot;
 
 // ws[k] slots: ensure_workspace TAKEs [0, kWsTileSlot); then the copy-tile index and the scan arena.
 constexpr int kWsTileSlot = 54, kWsArenaSlot = 55;
@@ -159,47 +161,64 @@ struct fdbcs_conflict_set {
     int sort_alg = 0;       // FDBCS_SORT_ALG: per-bucket sort (0 rank count, 1 bitonic network)
     DBuf trace_buf;
     fdbcs_stats stats{};
+    std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
+};
+
+// Host/device staging of one batch.  Batches are short-lived (one per commit batch, as the
+// reference's ConflictBatch), so their pinned and device buffers come from a per-set pool instead
+// of fresh hipHostMalloc / hipMalloc calls.  `ev_free` (stage B, after the epilogue) guards the
+// device copy: a slot's next upload waits for it.
+struct BatchSlot {
+    DBuf dev;
+    HBuf pin_in;
+    HBuf pin_out;
+    DBuf dverdict;
+    hipEvent_t ev[kPhCount] = {};
+    bool events_made = false;
+    hipEvent_t ev_up = nullptr;    // upload done (recorded on stage A's stream)
+    hipEvent_t ev_free = nullptr;  // the last batch using this slot finished on the device
+    bool free_recorded = false;
 };
 
 struct fdbcs_batch {
     fdbcs_conflict_set* cs = nullptr;
+    BatchSlot* slot = nullptr;
     int report_enabled = 0;
     int state = 0;  // 0 adding, 1 uploaded, 2 submitted, 3 done
-    // host staging (pageable)
+    // host staging (pageable); in `direct` mode (one fdbcs_batch_add_packed) the endpoint keys,
+    // owners and tails were normalized straight into slot->pin_in at add time
     std::vector<int64_t> snap;
     std::vector<uint8_t> flags;
     std::vector<int32_t> roff{0}, woff{0};
     std::vector<int32_t> rowner, wowner;
     std::vector<DKey> rkeys, wkeys;
     std::vector<uint8_t> tail;
+    bool direct = false;
+    size_t d_keys = 0, d_rown = 0, d_wown = 0, d_tail = 0, d_small = 0;  // pin_in offsets (direct mode)
+    size_t d_tail_bytes = 0;
     // device copy
-    DBuf dev;
-    HBuf pin_in;
     BatchDev bd{};
     size_t tail_bytes = 0;
     // results
-    HBuf pin_out;
-    DBuf dverdict;
     uint8_t* h_verdict = nullptr;
     Scalars* h_scal = nullptr;
     uint8_t* h_rconf = nullptr;
     uint8_t* h_hist = nullptr;
     int32_t* h_first = nullptr;
-    hipEvent_t ev[kPhCount] = {};
-    bool events_made = false;
-    hipEvent_t ev_up = nullptr;  // upload done (recorded on stage A's stream)
     bool gc_ran = false;
     bool compacted = false;
     uint32_t seq = 0;
     volatile uint32_t* h_flag = nullptr;
     uint32_t recorded = 0;  // phases whose events were recorded (bit per Phase)
     bool any_report = false;
+    int64_t check_hist = 0;  // boundaries (both tiers, upper bound) the read check searched
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
 
     int32_t T() const { return (int32_t)snap.size(); }
     int32_t R() const { return roff.back(); }
     int32_t W() const { return woff.back(); }
+    size_t tail_size() const { return direct ? d_tail_bytes : tail.size(); }
 };
 
 namespace {
@@ -507,62 +526,124 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
 }
 
 int ensure_events(fdbcs_batch* b) {
-    if (b->events_made) return FDBCS_OK;
-    for (int i = 0; i < kPhCount; i++) HIPOK(hipEventCreate(&b->ev[i]));
-    b->events_made = true;
+    BatchSlot* sl = b->slot;
+    if (sl->events_made) return FDBCS_OK;
+    for (int i = 0; i < kPhCount; i++) HIPOK(hipEventCreate(&sl->ev[i]));
+    sl->events_made = true;
     return FDBCS_OK;
+}
+
+void release_slot(BatchSlot* sl) {
+    if (!sl) return;
+    if (sl->events_made)
+        for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
+    if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
+    if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
+    sl->dev.release();
+    sl->dverdict.release();
+    sl->pin_in.release();
+    sl->pin_out.release();
+    delete sl;
+}
+
+// Layout of a batch in pin_in / dev: [keys | rowner | wowner | snap | roff | woff | flags | tail].
+// add_packed normalizes keys, owners and tails in place; the tail region is last so a capacity
+// sized for an upper bound of the tail bytes costs no upload.
+struct UploadLayout {
+    size_t keys, rown, wown, snap, roff, woff, flags, tail, total;
+};
+UploadLayout upload_layout(size_t T, size_t R, size_t W, size_t tail_bytes) {
+    UploadLayout L;
+    size_t off = 0;
+    L.keys = off;
+    off = align_up(off + sizeof(DKey) * 2 * (R + W), 64);
+    L.rown = off;
+    off = align_up(off + 4 * R, 64);
+    L.wown = off;
+    off = align_up(off + 4 * W, 64);
+    L.snap = off;
+    off = align_up(off + 8 * T, 64);
+    L.roff = off;
+    off = align_up(off + 4 * (T + 1), 64);
+    L.woff = off;
+    off = align_up(off + 4 * (T + 1), 64);
+    L.flags = off;
+    off = align_up(off + T, 64);
+    L.tail = off;
+    off = align_up(off + tail_bytes + 48, 64);  // slack for dkey.h tail_word
+    L.total = off;
+    return L;
+}
+
+// Prefix words of a key (dkey_prefix), two big-endian loads when the key has 16 bytes or more.
+inline void fast_prefix(const uint8_t* p, uint32_t len, uint64_t* hi, uint64_t* lo) {
+    if (len >= 16) {
+        uint64_t h, l;
+        memcpy(&h, p, 8);
+        memcpy(&l, p + 8, 8);
+        *hi = __builtin_bswap64(h);
+        *lo = __builtin_bswap64(l);
+    } else {
+        dkey_prefix(p, len, hi, lo);
+    }
+}
+
+// A direct-mode batch back into the pageable vectors (a second add call after add_packed).
+void materialize(fdbcs_batch* b) {
+    if (!b->direct) return;
+    const char* h = (const char*)b->slot->pin_in.p;
+    const size_t R = b->R(), W = b->W();
+    const DKey* k = (const DKey*)(h + b->d_keys);
+    b->rkeys.assign(k, k + 2 * R);
+    b->wkeys.assign(k + 2 * R, k + 2 * (R + W));
+    const int32_t* ro = (const int32_t*)(h + b->d_rown);
+    const int32_t* wo = (const int32_t*)(h + b->d_wown);
+    b->rowner.assign(ro, ro + R);
+    b->wowner.assign(wo, wo + W);
+    const uint8_t* t = (const uint8_t*)(h + b->d_tail);
+    b->tail.assign(t, t + b->d_tail_bytes);
+    b->direct = false;
 }
 
 int do_upload(fdbcs_batch* b) {
     fdbcs_conflict_set* cs = b->cs;
+    BatchSlot* sl = b->slot;
     const size_t T = b->T(), R = b->R(), W = b->W();
-    // layout: snap | roff | woff | rowner | wowner | keys | flags | tail
-    size_t off = 0;
-    const size_t o_snap = off;
-    off = align_up(off + 8 * T, 64);
-    const size_t o_roff = off;
-    off = align_up(off + 4 * (T + 1), 64);
-    const size_t o_woff = off;
-    off = align_up(off + 4 * (T + 1), 64);
-    const size_t o_rown = off;
-    off = align_up(off + 4 * R, 64);
-    const size_t o_wown = off;
-    off = align_up(off + 4 * W, 64);
-    const size_t o_keys = off;
-    off = align_up(off + sizeof(DKey) * 2 * (R + W), 64);
-    const size_t o_flags = off;
-    off = align_up(off + T, 64);
-    const size_t o_tail = off;
-    off = align_up(off + b->tail.size() + 48, 64);  // slack for dkey.h tail_word
+    const UploadLayout L = upload_layout(T, R, W, b->tail_size());
     int rc;
-    if ((rc = b->pin_in.ensure(off)) || (rc = b->dev.ensure(off))) return rc;
-    char* h = (char*)b->pin_in.p;
-    memcpy(h + o_snap, b->snap.data(), 8 * T);
-    memcpy(h + o_roff, b->roff.data(), 4 * (T + 1));
-    memcpy(h + o_woff, b->woff.data(), 4 * (T + 1));
-    if (R) memcpy(h + o_rown, b->rowner.data(), 4 * R);
-    if (W) memcpy(h + o_wown, b->wowner.data(), 4 * W);
-    if (R) memcpy(h + o_keys, b->rkeys.data(), sizeof(DKey) * 2 * R);
-    if (W) memcpy(h + o_keys + sizeof(DKey) * 2 * R, b->wkeys.data(), sizeof(DKey) * 2 * W);
-    if (T) memcpy(h + o_flags, b->flags.data(), T);
-    if (!b->tail.empty()) memcpy(h + o_tail, b->tail.data(), b->tail.size());
-    // on stage A's stream (its kernels read the batch first); stage B waits for ev_up
-    if (!b->ev_up) HIPOK(hipEventCreateWithFlags(&b->ev_up, hipEventDisableTiming));
-    HIPOK(hipMemcpyAsync(b->dev.p, h, off, hipMemcpyHostToDevice, cs->astream));
-    HIPOK(hipEventRecord(b->ev_up, cs->astream));
-    char* d = (char*)b->dev.p;
+    if (!b->direct && (rc = sl->pin_in.ensure(L.total))) return rc;
+    if ((rc = sl->dev.ensure(L.total))) return rc;
+    char* h = (char*)sl->pin_in.p;
+    if (!b->direct) {  // add_transaction path: normalized keys are in the pageable vectors
+        if (R) memcpy(h + L.keys, b->rkeys.data(), sizeof(DKey) * 2 * R);
+        if (W) memcpy(h + L.keys + sizeof(DKey) * 2 * R, b->wkeys.data(), sizeof(DKey) * 2 * W);
+        if (R) memcpy(h + L.rown, b->rowner.data(), 4 * R);
+        if (W) memcpy(h + L.wown, b->wowner.data(), 4 * W);
+        if (!b->tail.empty()) memcpy(h + L.tail, b->tail.data(), b->tail.size());
+    }
+    memcpy(h + L.snap, b->snap.data(), 8 * T);
+    memcpy(h + L.roff, b->roff.data(), 4 * (T + 1));
+    memcpy(h + L.woff, b->woff.data(), 4 * (T + 1));
+    if (T) memcpy(h + L.flags, b->flags.data(), T);
+    // on stage A's stream (its kernels read the batch first); stage B waits for ev_up.  A reused
+    // slot's device copy may still be read by the epilogue of the batch that used it last.
+    if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
+    if (sl->free_recorded) HIPOK(hipStreamWaitEvent(cs->astream, sl->ev_free, 0));
+    HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
+    HIPOK(hipEventRecord(sl->ev_up, cs->astream));
+    char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
     b->bd.R = (int32_t)R;
     b->bd.W = (int32_t)W;
-    b->bd.snap = (int64_t*)(d + o_snap);
-    b->bd.roff = (int32_t*)(d + o_roff);
-    b->bd.woff = (int32_t*)(d + o_woff);
-    b->bd.rowner = (int32_t*)(d + o_rown);
-    b->bd.wowner = (int32_t*)(d + o_wown);
-    b->bd.keys = (DKey*)(d + o_keys);
-    b->bd.flags = (uint8_t*)(d + o_flags);
-    b->bd.tail = (uint8_t*)(d + o_tail);
-    b->tail_bytes = b->tail.size();
+    b->bd.snap = (int64_t*)(d + L.snap);
+    b->bd.roff = (int32_t*)(d + L.roff);
+    b->bd.woff = (int32_t*)(d + L.woff);
+    b->bd.rowner = (int32_t*)(d + L.rown);
+    b->bd.wowner = (int32_t*)(d + L.wown);
+    b->bd.keys = (DKey*)(d + L.keys);
+    b->bd.flags = (uint8_t*)(d + L.flags);
+    b->bd.tail = (uint8_t*)(d + L.tail);
+    b->tail_bytes = b->tail_size();
     b->state = 1;
     return FDBCS_OK;
 }
@@ -656,6 +737,8 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         for (auto& x : set) x.release();
     cs->scal.release();
     cs->trace_buf.release();
+    for (BatchSlot* sl : cs->pool) release_slot(sl);
+    cs->pool.clear();
     for (int k = 0; k < kNumWork; k++) {
         if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
@@ -802,6 +885,16 @@ int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) 
     fdbcs_batch* b = new (std::nothrow) fdbcs_batch();
     if (!b) return FDBCS_E_NOMEM;
     b->cs = cs;
+    if (!cs->pool.empty()) {
+        b->slot = cs->pool.back();
+        cs->pool.pop_back();
+    } else {
+        b->slot = new (std::nothrow) BatchSlot();
+        if (!b->slot) {
+            delete b;
+            return FDBCS_E_NOMEM;
+        }
+    }
     b->report_enabled = report_keys ? 1 : 0;
     *out = b;
     return FDBCS_OK;
@@ -819,13 +912,8 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
         (void)hipSetDevice(b->cs->device);
         (void)hipStreamSynchronize(b->cs->astream);
     }
-    if (b->events_made)
-        for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(b->ev[i]);
-    if (b->ev_up) (void)hipEventDestroy(b->ev_up);
-    b->dev.release();
-    b->dverdict.release();
-    b->pin_in.release();
-    b->pin_out.release();
+    // the slot goes back to the set's pool (its buffers and events are reused by the next batch)
+    if (b->slot) b->cs->pool.push_back(b->slot);
     delete b;
 }
 
@@ -848,6 +936,7 @@ int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int repor
         if (write_begin_len[i] < 0 || write_end_len[i] < 0 ||
             cmp_bytes(write_begin[i], write_begin_len[i], write_end[i], write_end_len[i]) > 0)
             return FDBCS_E_INVALID;
+    materialize(b);
     const int32_t t = b->T();
     uint8_t fl = (report_conflicting_keys && b->report_enabled) ? kFlagReport : 0;
     const bool too_old = read_snapshot < b->cs->oldest && n_reads > 0;  // SkipList.cpp:770
@@ -871,6 +960,81 @@ int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int repor
     return FDBCS_OK;
 }
 
+// addTransaction of a whole (validated) packed batch into an empty batch: the endpoint keys are
+// normalized straight into the batch's pinned staging (no per-range vectors, no copy at upload).
+static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
+    const int32_t T = pb->n_txn;
+    const int64_t oldest = b->cs->oldest;
+    b->snap.assign(pb->read_snapshot, pb->read_snapshot + T);
+    b->flags.resize(T);
+    b->roff.resize(T + 1);
+    b->woff.resize(T + 1);
+    int32_t Ra = 0, Wa = 0;
+    for (int32_t t = 0; t < T; t++) {
+        const int32_t nr = pb->read_offsets[t + 1] - pb->read_offsets[t];
+        const int32_t nw = pb->write_offsets[t + 1] - pb->write_offsets[t];
+        uint8_t fl = (pb->report_conflicting_keys && pb->report_conflicting_keys[t] && b->report_enabled)
+                         ? kFlagReport
+                         : 0;
+        const bool too_old = pb->read_snapshot[t] < oldest && nr > 0;  // SkipList.cpp:770
+        if (too_old) fl |= kFlagTooOld;
+        b->flags[t] = fl;
+        b->roff[t] = Ra;
+        b->woff[t] = Wa;
+        if (!too_old) {
+            Ra += nr;
+            Wa += nw;
+        }
+    }
+    b->roff[T] = Ra;
+    b->woff[T] = Wa;
+    const int64_t nk = 2 * ((int64_t)pb->read_offsets[T] + pb->write_offsets[T]);
+    const size_t tail_bound = nk ? (size_t)(pb->key_offsets[nk] - pb->key_offsets[0]) : 0;
+    const UploadLayout L = upload_layout(T, Ra, Wa, tail_bound);
+    if (int rc = b->slot->pin_in.ensure(L.total)) return rc;
+    char* h = (char*)b->slot->pin_in.p;
+    DKey* keys = (DKey*)(h + L.keys);
+    int32_t* rown = (int32_t*)(h + L.rown);
+    int32_t* wown = (int32_t*)(h + L.wown);
+    uint8_t* tail = (uint8_t*)(h + L.tail);
+    size_t tb = 0;
+    auto put = [&](DKey* out, int64_t k) {
+        const uint8_t* p = pb->key_bytes + pb->key_offsets[k];
+        const uint32_t len = (uint32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]);
+        fast_prefix(p, len, &out->hi, &out->lo);
+        out->len = len;
+        out->tail = 0;
+        if (len > 16) {
+            out->tail = (uint32_t)tb;
+            memcpy(tail + tb, p + 16, len - 16);
+            tb += len - 16;
+        }
+    };
+    const int32_t R = pb->read_offsets[T];
+    DKey* wk = keys + 2 * (size_t)Ra;
+    for (int32_t t = 0; t < T; t++) {
+        if (b->flags[t] & kFlagTooOld) continue;
+        const int32_t ra = b->roff[t], wa = b->woff[t];
+        for (int32_t r = pb->read_offsets[t], i = 0; r < pb->read_offsets[t + 1]; r++, i++) {
+            put(keys + 2 * (size_t)(ra + i), 2 * (int64_t)r);
+            put(keys + 2 * (size_t)(ra + i) + 1, 2 * (int64_t)r + 1);
+            rown[ra + i] = t;
+        }
+        for (int32_t w = pb->write_offsets[t], i = 0; w < pb->write_offsets[t + 1]; w++, i++) {
+            put(wk + 2 * (size_t)(wa + i), 2 * ((int64_t)R + w));
+            put(wk + 2 * (size_t)(wa + i) + 1, 2 * ((int64_t)R + w) + 1);
+            wown[wa + i] = t;
+        }
+    }
+    b->direct = true;
+    b->d_keys = L.keys;
+    b->d_rown = L.rown;
+    b->d_wown = L.wown;
+    b->d_tail = L.tail;
+    b->d_tail_bytes = tb;
+    return FDBCS_OK;
+}
+
 int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     if (!b || !pb || pb->n_txn < 0) return FDBCS_E_INVALID;
     if (b->state != 0) return FDBCS_E_STATE;
@@ -891,6 +1055,8 @@ int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
             return FDBCS_E_INVALID;
     }
     const int64_t oldest = b->cs->oldest;
+    if (b->T() == 0 && !b->direct) return add_packed_direct(b, pb);
+    materialize(b);
     b->snap.reserve(b->snap.size() + T);
     for (int32_t t = 0; t < T; t++) {
         const int32_t tt = b->T();
@@ -942,12 +1108,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (now < cs->max_written) return FDBCS_E_VERSION;
     if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
     // tail offsets are 32-bit: refuse a batch that could overflow the arena (GC repacks it long before)
-    if (cs->tail_ub + (int64_t)b->tail.size() + 1 >= kTailLimit) return FDBCS_E_NOMEM;
+    if (cs->tail_ub + (int64_t)b->tail_size() + 1 >= kTailLimit) return FDBCS_E_NOMEM;
     const int64_t T = b->T(), R = b->R(), W = b->W();
     int rc;
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
     if ((rc = ensure_delta(cs, cs->nd_ub + 2 * W + 1))) return rc;
-    if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail.size() + 1)))
+    if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail_size() + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
     // results (host-mapped, written by the epilogue): verdicts | scalars | completion flag, then the
@@ -958,15 +1124,16 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const size_t o_hc = align_up(o_rc + R + 1, 64);
     const size_t o_fc = align_up(o_hc + T + 1, 64);
     const size_t out_bytes = o_fc + 4 * (T + 1);
-    if ((rc = b->pin_out.ensure(out_bytes, true))) return rc;
-    char* ho = (char*)b->pin_out.p;
+    BatchSlot* sl = b->slot;
+    if ((rc = sl->pin_out.ensure(out_bytes, true))) return rc;
+    char* ho = (char*)sl->pin_out.p;
     b->h_verdict = (uint8_t*)ho;
     b->h_scal = (Scalars*)(ho + o_sc);
     b->h_flag = (volatile uint32_t*)(ho + o_fl);
     b->h_rconf = (uint8_t*)(ho + o_rc);
     b->h_hist = (uint8_t*)(ho + o_hc);
     b->h_first = (int32_t*)(ho + o_fc);
-    if ((rc = b->dverdict.ensure(T + 64))) return rc;
+    if ((rc = sl->dverdict.ensure(T + 64))) return rc;
     b->any_report = false;
     for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
     b->seq = ++cs->seq;
@@ -988,7 +1155,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     auto rec = [&](int ph, int level) -> hipEvent_t {
         if (timing < level) return nullptr;
         b->recorded |= 1u << ph;
-        return b->ev[ph];
+        return sl->ev[ph];
     };
     auto mark = [&](int ph) -> int {
         if (hipEvent_t e = rec(ph, 2)) HIPOK(hipEventRecord(e, s));
@@ -999,9 +1166,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (cs->wused[wp] && sa != s) HIPOK(hipStreamWaitEvent(sa, cs->ev_b[wp], 0));
     cs->wused[wp] = true;
     if (b->state == 0 && (rc = do_upload(b))) return rc;
-    if (sa == s || hipEventQuery(b->ev_up) != hipSuccess) HIPOK(hipStreamWaitEvent(s, b->ev_up, 0));
-    if (sa != s && sa != cs->astream && hipEventQuery(b->ev_up) != hipSuccess)
-        HIPOK(hipStreamWaitEvent(sa, b->ev_up, 0));  // the upload ran on astream
+    if (sa == s || hipEventQuery(sl->ev_up) != hipSuccess) HIPOK(hipStreamWaitEvent(s, sl->ev_up, 0));
+    if (sa != s && sa != cs->astream && hipEventQuery(sl->ev_up) != hipSuccess)
+        HIPOK(hipStreamWaitEvent(sa, sl->ev_up, 0));  // the upload ran on astream
     if ((rc = mark(kPhUpload))) return rc;
     const BatchDev& bd = b->bd;
     Scalars* sc = (Scalars*)cs->scal.p;
@@ -1023,7 +1190,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- stage A: D.Sort and the candidate edges of D.CheckIntraBatch
     launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
     int sorted = 0;
-    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted);
+    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted, rec(kPhSortBegin, 1),
+                       rec(kPhSortEnd, 1));
     if ((rc = mark(kPhSort))) return rc;
     launch_positions(sa, bd, w, sorted);
     if (cs->validate) launch_validate_sort(sa, bd, w, sorted);
@@ -1031,10 +1199,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (sa != s) HIPOK(hipEventRecord(cs->ev_a[wp], sa));
     if ((rc = mark(kPhEdges))) return rc;
     // ---- stage B: D.CheckRead against the history the previous batch left, then batch order
+    b->check_hist = cs->n_ub + cs->nd_ub;
+    if (hipEvent_t e = rec(kPhCheckBegin, 1)) HIPOK(hipEventRecord(e, s));
     launch_check(s, bd, w, base, delta, htail);
+    if (hipEvent_t e = rec(kPhCheckEnd, 1)) HIPOK(hipEventRecord(e, s));
     if ((rc = mark(kPhCheck))) return rc;
     if (sa != s) HIPOK(hipStreamWaitEvent(s, cs->ev_a[wp], 0));
-    launch_resolve(s, bd, w, b->any_report, (uint8_t*)b->pin_out.dp);
+    launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf
         if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
         HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
@@ -1087,11 +1258,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = mark(kPhGc))) return rc;
     b->gc_ran = gc;
     b->compacted = compact;
-    char* hd = (char*)b->pin_out.dp;
+    char* hd = (char*)sl->pin_out.dp;
     launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
-                    gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)b->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
+                    gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1);
     if (sa != s) HIPOK(hipEventRecord(cs->ev_b[wp], s));
+    if (!sl->ev_free) HIPOK(hipEventCreateWithFlags(&sl->ev_free, hipEventDisableTiming));
+    HIPOK(hipEventRecord(sl->ev_free, s));
+    sl->free_recorded = true;
     if ((rc = mark(kPhEpilogue))) return rc;
     HIPOK(hipGetLastError());
     if ((rc = mark(kPhEnd))) return rc;
@@ -1105,7 +1279,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     } else {
         cs->nd_ub = nd_after;
     }
-    cs->tail_ub += (int64_t)b->tail.size();
+    cs->tail_ub += (int64_t)b->tail_size();
     cs->inflight++;
     b->state = 2;
     return FDBCS_OK;
@@ -1200,13 +1374,13 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         st.read_ranges += b->R();
         st.write_ranges += b->W();
         // timing events may trail the completion flag: wait for the last one recorded
-        for (int e : {(int)kPhEnd, (int)kPhCompEnd, (int)kPhCopyEnd})
+        for (int e : {(int)kPhEnd, (int)kPhCompEnd, (int)kPhCopyEnd, (int)kPhCheckEnd})
             if ((b->recorded >> e) & 1u) {
-                HIPOK(hipEventSynchronize(b->ev[e]));
+                HIPOK(hipEventSynchronize(b->slot->ev[e]));
                 break;
             }
         auto ph = [&](int a, int z) {
-            return ((b->recorded >> a) & (b->recorded >> z) & 1u) ? ev_ms(b->ev[a], b->ev[z]) : 0.0;
+            return ((b->recorded >> a) & (b->recorded >> z) & 1u) ? ev_ms(b->slot->ev[a], b->slot->ev[z]) : 0.0;
         };
         st.ms_upload += ph(kPhStart, kPhUpload);
         st.ms_sort += ph(kPhUpload, kPhSort);
@@ -1227,11 +1401,26 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             st.intra_edges += b->h_scal->intra_edges;
             st.intra_rounds += b->h_scal->intra_rounds;
         }
-        st.merge_bytes += 32 * (2 * b->h_scal->d_before - b->h_scal->d_rem);
+        // algorithmic bytes of the copy kernels (roofline.py): read every kept old boundary and
+        // write every boundary of the result, 32 B each (16 B key, 8 B length/tail, 8 B version)
+        st.merge_bytes += 32 * ((b->h_scal->d_before - b->h_scal->d_rem) + b->h_scal->nd_next);
+        if ((b->recorded >> kPhCheckEnd) & 1u) {
+            st.ms_check_kernel += ph(kPhCheckBegin, kPhCheckEnd);
+            st.check_launches += b->R() > 0;
+            st.check_reads += b->R();
+            st.check_history += b->R() > 0 ? b->check_hist : 0;
+        }
+        if ((b->recorded >> kPhSortEnd) & 1u) {
+            st.ms_sort_kernel += ph(kPhSortBegin, kPhSortEnd);
+            st.sort_launches += 1;
+            st.sort_items += 2 * (int64_t)(b->R() + b->W());
+        }
         if (b->compacted) {
             st.compactions += 1;
             st.ms_compact_kernel += ph(kPhCompBegin, kPhCompEnd);
-            st.compact_bytes += 32 * (2 * b->h_scal->c_before - b->h_scal->c_rem);
+            // kept base boundaries read, delta boundaries inserted read, result written
+            const int64_t kept = b->h_scal->c_before - b->h_scal->c_rem;
+            st.compact_bytes += 32 * (kept + (b->h_scal->n_next - kept) + b->h_scal->n_next);
         }
         cs->inflight--;
         if (cs->inflight == 0) {
@@ -1269,7 +1458,7 @@ int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out,
 int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr) {
     if (!b || !dptr) return FDBCS_E_INVALID;
     if (b->state < 2) return FDBCS_E_STATE;
-    *dptr = b->dverdict.p;
+    *dptr = b->slot->dverdict.p;
     return FDBCS_OK;
 }
 

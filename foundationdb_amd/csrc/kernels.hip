@@ -949,7 +949,7 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
-                        int alg, int* result_buffer) {
+                        int alg, int* result_buffer, hipEvent_t sort_begin, hipEvent_t sort_end) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
@@ -959,10 +959,12 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
     hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
+    if (sort_begin) (void)hipEventRecord(sort_begin, s);
     if (alg == 1)
         hipLaunchKernelGGL(k_bucket_sort<1>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
     else
         hipLaunchKernelGGL(k_bucket_sort<0>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    if (sort_end) (void)hipEventRecord(sort_end, s);
 }
 
 // ------------------------------------------------------------------ positions

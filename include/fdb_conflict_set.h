@@ -102,6 +102,14 @@ typedef struct fdbcs_stats {
     int64_t intra_edges;    /* candidate intra-batch edges (sum over batches) */
     int64_t intra_rounds;   /* batch-order resolution rounds (sum over batches) */
     int64_t intra_fallbacks;/* batches resolved by the sequential MiniConflictSet replay */
+    /* Roofline inputs of the other hot kernels (timing level >= 1), see roofline.py. */
+    double ms_check_kernel; /* device time of the read-check kernel (D.CheckRead) */
+    int64_t check_launches;
+    int64_t check_reads;    /* read ranges checked (sum over launches) */
+    int64_t check_history;  /* boundaries searched: base + delta tier size at check time (sum) */
+    double ms_sort_kernel;  /* device time of the per-bucket sort kernel (D.Sort) */
+    int64_t sort_launches;
+    int64_t sort_items;     /* endpoints sorted (sum over launches) */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
@@ -138,8 +146,9 @@ int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes
 int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every);
 int fdbcs_set_delta_limit(fdbcs_conflict_set* cs, int64_t boundaries);
 /* Device timing of the pipeline (HIP events; each recorded event costs a few microseconds of
- * queue time, so production runs keep them off): 0 = none (default), 1 = the two history copy
- * kernels only (fills ms_merge_kernel / ms_compact_kernel), 2 = every phase of fdbcs_stats. */
+ * queue time, so production runs keep them off): 0 = none (default), 1 = the hot kernels only
+ * (read check, bucket sort, the two history copy kernels: ms_*_kernel), 2 = every phase of
+ * fdbcs_stats. */
 int fdbcs_set_timing(fdbcs_conflict_set* cs, int32_t level);
 
 /* ConflictBatch(cs, conflictingKeyRangeMap, arena) — SkipList.cpp:749-752.

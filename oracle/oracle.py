@@ -21,11 +21,10 @@ _LIBS = {}
 
 
 def build(force: bool = False) -> None:
-    need = force or not all(
-        os.path.exists(os.path.join(HERE, n)) for n in ("liboracle.so", "libskiplist_baseline.so")
-    )
-    if need:
-        subprocess.check_call(["make", "-s", "-C", HERE, "all"])
+    """make is incremental: rebuilds a checker library only when its sources changed."""
+    if force:
+        subprocess.check_call(["make", "-s", "-C", HERE, "clean"])
+    subprocess.check_call(["make", "-s", "-C", HERE, "all"])
 
 
 def _lib(name: str):

@@ -439,10 +439,12 @@ int main(int argc, char** argv) {
     for (int r = 0; r < reps + 1; r++) {
         zero();
         CK(hipEventRecord(ev[0], s));
-        launch_sample(s, b, w, 0);
+        launch_sample(s, b, w, 0, 0);
         CK(hipEventRecord(ev[1], s));
         const int grid = (E + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, w.bucket, w.bcount, b.tail);
+        const int S = sample_count(E, nb, 0);
+        hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount,
+                           b.tail);
         CK(hipEventRecord(ev[2], s));
         hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff,
                            nb, w.items[0]);
