@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <new>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/fdb_conflict_set.h"
@@ -162,6 +163,7 @@ struct fdbcs_conflict_set {
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
+    std::unordered_set<fdbcs_batch*> live;  // batches not yet destroyed (detached if the set goes first)
 };
 
 // Host/device staging of one batch.  Batches are short-lived (one per commit batch, as the
@@ -739,6 +741,10 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->trace_buf.release();
     for (BatchSlot* sl : cs->pool) release_slot(sl);
     cs->pool.clear();
+    // batches that outlive their set (e.g. garbage-collection order in a binding) keep their own
+    // slot and refuse every further call
+    for (fdbcs_batch* b : cs->live) b->cs = nullptr;
+    cs->live.clear();
     for (int k = 0; k < kNumWork; k++) {
         if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
@@ -895,6 +901,7 @@ int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) 
             return FDBCS_E_NOMEM;
         }
     }
+    cs->live.insert(b);
     b->report_enabled = report_keys ? 1 : 0;
     *out = b;
     return FDBCS_OK;
@@ -902,6 +909,11 @@ int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) 
 
 void fdbcs_batch_destroy(fdbcs_batch* b) {
     if (!b) return;
+    if (!b->cs) {  // its set was destroyed first (and synchronized its streams)
+        release_slot(b->slot);
+        delete b;
+        return;
+    }
     if (b->state == 2) {  // still in flight: its set (which must outlive it) owns the stream
         (void)hipSetDevice(b->cs->device);
         (void)hipStreamSynchronize(b->cs->astream);
@@ -914,6 +926,7 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
     }
     // the slot goes back to the set's pool (its buffers and events are reused by the next batch)
     if (b->slot) b->cs->pool.push_back(b->slot);
+    b->cs->live.erase(b);
     delete b;
 }
 
@@ -923,7 +936,7 @@ int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int repor
                                 const uint8_t* const* write_begin, const int32_t* write_begin_len,
                                 const uint8_t* const* write_end, const int32_t* write_end_len) {
     if (!b || n_reads < 0 || n_writes < 0) return FDBCS_E_INVALID;
-    if (b->state != 0) return FDBCS_E_STATE;
+    if (b->state != 0 || !b->cs) return FDBCS_E_STATE;
     if ((n_reads && (!read_begin || !read_end || !read_begin_len || !read_end_len)) ||
         (n_writes && (!write_begin || !write_end || !write_begin_len || !write_end_len)))
         return FDBCS_E_INVALID;
@@ -1037,7 +1050,7 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
 
 int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     if (!b || !pb || pb->n_txn < 0) return FDBCS_E_INVALID;
-    if (b->state != 0) return FDBCS_E_STATE;
+    if (b->state != 0 || !b->cs) return FDBCS_E_STATE;
     const int32_t T = pb->n_txn;
     if (T == 0) return FDBCS_OK;
     if (!pb->read_snapshot || !pb->read_offsets || !pb->write_offsets || !pb->key_offsets) return FDBCS_E_INVALID;
@@ -1095,6 +1108,7 @@ int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
 
 int fdbcs_batch_upload(fdbcs_batch* b) {
     if (!b) return FDBCS_E_INVALID;
+    if (!b->cs) return FDBCS_E_STATE;
     if (b->state != 0) return b->state == 1 ? FDBCS_OK : FDBCS_E_STATE;
     HIPOK(hipSetDevice(b->cs->device));
     return do_upload(b);
@@ -1102,6 +1116,7 @@ int fdbcs_batch_upload(fdbcs_batch* b) {
 
 int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_version) {
     if (!b) return FDBCS_E_INVALID;
+    if (!b->cs) return FDBCS_E_STATE;
     if (b->state > 1) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
     HIPOK(hipSetDevice(cs->device));
@@ -1287,6 +1302,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
 
 int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, int32_t* n_too_old) {
     if (!b) return FDBCS_E_INVALID;
+    if (b->state == 2 && !b->cs) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
     if (b->state == 2) {
         HIPOK(hipSetDevice(cs->device));

@@ -390,3 +390,23 @@ def test_sharded_engines_match_sharded_oracles(engine, oracle_mod):
             assert (ve[g] == vo[g]).all()
         assert (KeyRangeSharding.combine(pb.n_txn, parts, ve) == KeyRangeSharding.combine(pb.n_txn, parts, vo)).all()
         now += 3
+
+
+def test_batch_outliving_its_set_is_refused_not_corrupting(engine):
+    """Batches take pinned staging from a per-set pool; a batch destroyed after its set (garbage
+    collection order in a binding) must neither touch the freed set nor crash, and calls on it are
+    refused with FDBCS_E_STATE."""
+    rng = np.random.default_rng(77)
+    for _ in range(3):
+        cs = engine.ConflictSet(0)
+        done = engine.ConflictBatch(cs)
+        done.add_packed(W.random_small_batch(rng, 50, now=10))
+        done.detect_conflicts(10, 0)
+        pending = engine.ConflictBatch(cs)
+        pending.add_packed(W.random_small_batch(rng, 50, now=11))
+        cs.close()
+        with pytest.raises(engine.FdbcsError) as ex:
+            pending.detect_conflicts(11, 0)
+        assert ex.value.status == engine.FDBCS_E_STATE
+        pending.close()
+        done.close()
