@@ -173,7 +173,7 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
     oracle.build()
     try:  # skipListTest pins itself to one core (setAffinity(0), SkipList.cpp:1015)
         cores = sorted(os.sched_getaffinity(0))
-        os.sched_setaffinity(0, {cores[(rank * 2) % len(cores)]})
+        os.sched_setaffinity(0, {cores[(len(cores) // 2 + 2 * rank) % len(cores)]})  # away from core 0's IRQs
     except (AttributeError, OSError):
         cores = []
     sl = oracle.SkipListBaseline()
@@ -380,6 +380,17 @@ def main():
     # stream each kernel runs on), algorithmic bytes from the §8(d) model (roofline.py)
     kern = roofline.kernels_from_stats(st) if args.timing >= 1 else {}
     dom = roofline.dominant(kern)
+    # the rocprof-dominant kernel of this workload (scripts/prof_summary.py --dominant over the
+    # committed profile) wins over the event totals, which inflate stage-A kernels a little
+    dom_file = os.path.join(ROOT, "profiles", f"dominant_{args.workload}.json")
+    if os.path.exists(dom_file):
+        try:
+            with open(dom_file) as f:
+                d = json.load(f).get("dominant")
+            if d in kern:
+                dom = d
+        except Exception:
+            pass
     roof = None
     if dom is not None:
         k = kern[dom]

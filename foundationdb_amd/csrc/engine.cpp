@@ -590,6 +590,41 @@ inline void fast_prefix(const uint8_t* p, uint32_t len, uint64_t* hi, uint64_t* 
     }
 }
 
+// Result buffer of a batch (host-mapped, written by the kernels): verdicts | scalars | completion
+// flag, then the report copies rconf | hist | first_conf.
+struct ResultLayout {
+    size_t sc, fl, rc, hc, fc, total;
+};
+ResultLayout result_layout(size_t T, size_t R) {
+    ResultLayout L;
+    L.sc = (size_t)verdict_scalars_offset((int64_t)T);
+    L.fl = align_up(L.sc + sizeof(Scalars), 64);
+    L.rc = L.fl + 64;
+    L.hc = align_up(L.rc + R + 1, 64);
+    L.fc = align_up(L.hc + T + 1, 64);
+    L.total = L.fc + 4 * (T + 1);
+    return L;
+}
+
+// Every allocation a batch of this shape needs, made at add time so that detect (the timed,
+// latency-critical call) never allocates: device copy, pinned result buffer, device verdicts.
+int ensure_slot(BatchSlot* sl, size_t upload_bytes, size_t T, size_t R) {
+    int rc;
+    if ((rc = sl->dev.ensure(upload_bytes))) return rc;
+    if ((rc = sl->pin_out.ensure(result_layout(T, R).total, true))) return rc;
+    return sl->dverdict.ensure(T + 64);
+}
+
+int make_slot_events(BatchSlot* sl) {
+    if (!sl->events_made) {
+        for (int i = 0; i < kPhCount; i++) HIPOK(hipEventCreate(&sl->ev[i]));
+        sl->events_made = true;
+    }
+    if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
+    if (!sl->ev_free) HIPOK(hipEventCreateWithFlags(&sl->ev_free, hipEventDisableTiming));
+    return FDBCS_OK;
+}
+
 // A direct-mode batch back into the pageable vectors (a second add call after add_packed).
 void materialize(fdbcs_batch* b) {
     if (!b->direct) return;
@@ -614,7 +649,7 @@ int do_upload(fdbcs_batch* b) {
     const UploadLayout L = upload_layout(T, R, W, b->tail_size());
     int rc;
     if (!b->direct && (rc = sl->pin_in.ensure(L.total))) return rc;
-    if ((rc = sl->dev.ensure(L.total))) return rc;
+    if ((rc = ensure_slot(sl, L.total, T, R))) return rc;
     char* h = (char*)sl->pin_in.p;
     if (!b->direct) {  // add_transaction path: normalized keys are in the pageable vectors
         if (R) memcpy(h + L.keys, b->rkeys.data(), sizeof(DKey) * 2 * R);
@@ -900,6 +935,11 @@ int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) 
             delete b;
             return FDBCS_E_NOMEM;
         }
+        if (int rc = make_slot_events(b->slot)) {
+            release_slot(b->slot);
+            delete b;
+            return rc;
+        }
     }
     cs->live.insert(b);
     b->report_enabled = report_keys ? 1 : 0;
@@ -1023,6 +1063,7 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
             tb += len - 16;
         }
     };
+    if (int rc = ensure_slot(b->slot, L.total, T, Ra)) return rc;
     const int32_t R = pb->read_offsets[T];
     DKey* wk = keys + 2 * (size_t)Ra;
     for (int32_t t = 0; t < T; t++) {
@@ -1133,12 +1174,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = ensure_events(b))) return rc;
     // results (host-mapped, written by the epilogue): verdicts | scalars | completion flag, then the
     // report copies rconf | hist | first_conf
-    const size_t o_sc = (size_t)verdict_scalars_offset(T);
-    const size_t o_fl = align_up(o_sc + sizeof(Scalars), 64);
-    const size_t o_rc = o_fl + 64;
-    const size_t o_hc = align_up(o_rc + R + 1, 64);
-    const size_t o_fc = align_up(o_hc + T + 1, 64);
-    const size_t out_bytes = o_fc + 4 * (T + 1);
+    const ResultLayout RL = result_layout(T, R);
+    const size_t o_sc = RL.sc, o_fl = RL.fl, o_rc = RL.rc, o_hc = RL.hc, o_fc = RL.fc, out_bytes = RL.total;
     BatchSlot* sl = b->slot;
     if ((rc = sl->pin_out.ensure(out_bytes, true))) return rc;
     char* ho = (char*)sl->pin_out.p;

@@ -110,8 +110,12 @@ class _CSBase:
         vv = np.ascontiguousarray(versions, np.int64)
         self._fn["load_history"](self._h, len(vv), _p(kb), _p(ko), _p(vv), header_version)
 
-    def detect(self, pb, now: int, new_oldest: int, gc: bool = True):
-        """Returns (verdicts uint8[T], conflicting: dict txn -> sorted list of read indices)."""
+    def detect(self, pb, now: int, new_oldest: int, gc=True):
+        """Returns (verdicts uint8[T], conflicting: dict txn -> sorted list of read indices).
+
+        gc: False = no removeBefore; True = a full removeBefore pass (history size comparable with
+        the GPU engine after its full GC); "bounded" = the reference's bounded, resumable
+        removeBefore (SkipList.cpp:880-889; the skip-list restatement only)."""
         T = pb.n_txn
         verdicts = np.zeros(T, np.uint8)
         cap = max(1, pb.n_reads)
@@ -119,7 +123,8 @@ class _CSBase:
         idx = np.zeros(cap, np.int32)
         cs = pb.c_struct()
         n = self._fn["detect"](
-            self._h, ctypes.byref(cs), now, new_oldest, _p(verdicts), _p(off), _p(idx), cap, 1 if gc else 0
+            self._h, ctypes.byref(cs), now, new_oldest, _p(verdicts), _p(off), _p(idx), cap,
+            2 if gc == "bounded" else (1 if gc else 0)
         )
         if n < 0:
             raise RuntimeError("oracle detect failed")
@@ -161,6 +166,17 @@ class OracleConflictSet(_CSBase):
 class SkipListBaseline(_CSBase):
     _libname = "libskiplist_baseline.so"
     _prefix = "slb_"
+
+    PHASES = ("add", "sort", "check_read", "intra", "combine", "merge", "remove_before", "total")
+
+    def last_times(self) -> dict:
+        """Seconds per phase of the last detect (the reference's PerfDoubleCounters, SkipList.cpp:49-51)."""
+        f = self._L.slb_last_times
+        f.restype = None
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        out = np.zeros(8, np.float64)
+        f(self._h, _p(out))
+        return dict(zip(self.PHASES, out.tolist()))
 
 
 def point_compare(a: bytes, a_begin: bool, a_write: bool, b: bytes, b_begin: bool, b_write: bool) -> int:

@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 kernel-trace stats of a short bench run; summaries land in gpurun_out/prof/.
+# rocprofv3 kernel-trace stats of a short bench run; summaries land in gpurun_out/prof/, plus the
+# rocprof-dominant roofline kernel (dominant.json, copy to profiles/dominant_<workload>.json).
 set -u
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
@@ -9,4 +10,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 rc=$?
 echo "rocprof rc=$rc" >&2
 find gpurun_out/prof -name "*stats*" >&2
+[ $rc -eq 0 ] && python3 scripts/prof_summary.py $(find gpurun_out/prof -name "*kernel_stats.csv" | head -1) \
+  --dominant gpurun_out/prof/dominant.json > gpurun_out/prof/summary.txt
 exit $rc

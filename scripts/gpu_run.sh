@@ -24,5 +24,5 @@ cat gpurun_out/bench.json >&2
 tail -5 gpurun_out/bench.err >&2
 if [ "${PROFILE:-0}" = "1" ]; then
   step profile 600 bash scripts/gpu_profile.sh
-  python3 scripts/prof_summary.py gpurun_out/prof/run_kernel_stats.csv >&2 || true
+  cat gpurun_out/prof/summary.txt >&2 || true
 fi

@@ -1,7 +1,8 @@
-"""Per-launch HBM bytes of the two history copy kernels from rocprofv3 --pmc CSVs.
+"""Per-launch HBM bytes of the roofline kernels (roofline.py) from rocprofv3 --pmc CSVs.
 
-k_merge_copy<BatchIns> merges a batch into the delta tier; k_merge_copy<CompactIns> folds the delta
-into the base tier.  FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
+k_check_reads is the read check, k_bucket_sort the endpoint sort, k_merge_copy<BatchIns> merges a
+batch into the delta tier, k_merge_copy<CompactIns> folds the delta into the base tier.
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
 the bytes of a wide (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md, HBM); the copy
 reads 16-B keys and 8-B length/version words, so both the raw and the x2-corrected fetch figures
 are reported.
@@ -12,7 +13,8 @@ import json
 import os
 import sys
 
-KERNELS = {"merge": "BatchIns", "compact": "CompactIns"}
+KERNELS = {"check": "k_check_reads", "sort": "k_bucket_sort", "merge": "k_merge_copy<fdbcs::BatchIns",
+           "compact": "k_merge_copy<fdbcs::CompactIns"}
 
 root = sys.argv[1]
 out = {}
@@ -24,7 +26,7 @@ for key, tag in KERNELS.items():
         for f in files:
             for r in csv.DictReader(open(f)):
                 name = r.get("Kernel_Name", "")
-                if "k_merge_copy" in name and tag in name and r.get("Counter_Name") == c:
+                if tag in name and r.get("Counter_Name") == c:
                     vals.append(float(r["Counter_Value"]))
         per[c] = sum(vals) / len(vals) if vals else None
         out[f"{key}_{c}_kib_per_launch"] = per[c]

@@ -183,3 +183,40 @@ def test_deterministic_random_restatement():
     words (r0 << 32) ^ r1; raw words of mt19937(1) start 1791095845, 4282876139."""
     g = W.DeterministicRandom(1).gen64(1)[0]
     assert int(g) == (1791095845 << 32) ^ 4282876139
+
+
+def test_bounded_remove_before_matches_oracle(oracle_built):
+    """The skip-list restatement's bounded, resumable removeBefore (SkipList.cpp:880-889: at most
+    3 x |combined writes| + 10 nodes per batch, resuming at removalKey) is verdict-neutral and only
+    ever shrinks the history toward what a full pass leaves."""
+    rng = np.random.default_rng(23)
+    for trial in range(30):
+        a, b, c = oracle_built.OracleConflictSet(), oracle_built.SkipListBaseline(), oracle_built.SkipListBaseline()
+        for pb, now, no in _random_sequence(rng, n_batches=12, alphabet=2 + trial % 3, max_len=2 + trial % 3):
+            va, ca = a.detect(pb, now, no, gc=True)
+            vb, cb = b.detect(pb, now, no, gc="bounded")
+            vc, _ = c.detect(pb, now, no, gc=False)
+            assert (va == vb).all() and (va == vc).all()
+            assert ca == cb
+            assert a.history_size() <= b.history_size() <= c.history_size()
+
+
+def test_skiplist_restatement_c2_shape(oracle_built):
+    """C2-shaped batches (5R+2W, 16-byte keys, prefilled history) through the interleaved CheckMax /
+    striped-find restatement with bounded GC, against the semantic oracle."""
+    p = W.C2Params(txns=600, history=30_000, staleness=20_000, window=40_000)
+    kb, ko, vers = W.c2_history(p, seed=3, start_version=100_000)
+    a, b = oracle_built.OracleConflictSet(), oracle_built.SkipListBaseline()
+    a.load_history(kb, ko, vers)
+    b.load_history(kb, ko, vers)
+    rng = np.random.default_rng(4)
+    now = 100_000
+    seen = set()
+    for _ in range(8):
+        now += p.version_step
+        pb = W.c2_batch(p, rng, now)
+        va, _ = a.detect(pb, now, now - p.window, gc=False)
+        vb, _ = b.detect(pb, now, now - p.window, gc="bounded")
+        assert (va == vb).all()
+        seen |= set(np.unique(va).tolist())
+    assert {0, 2} <= seen
