@@ -64,6 +64,8 @@ def parse():
                     help="events in the timed region: 0 none, 1 around the hot kernels (roofline)")
     ap.add_argument("--total-steps", type=int, default=-1,
                     help="batches of the add+detect ('total') pass; -1 = --steps, 0 = skip")
+    ap.add_argument("--resident-steps", type=int, default=20,
+                    help="batches of the device-resident pass (uploaded before its timed region; diagnostic)")
     ap.add_argument("--breakdown-steps", type=int, default=16,
                     help="extra batches after the timed region with every phase timed (diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
@@ -257,7 +259,8 @@ def main():
     kb, ko, vers = shard_history(args, p, args.seed, rank, world, start_version)
     n_total = args.steps if args.total_steps < 0 else args.total_steps
     timed_lo, timed_hi = args.warmup, args.warmup + args.steps
-    total_lo, total_hi = timed_hi, timed_hi + n_total
+    res_lo, res_hi = timed_hi, timed_hi + args.resident_steps
+    total_lo, total_hi = res_hi, res_hi + n_total
     n_all = total_hi + args.breakdown_steps
     gbatches = make_batches(args, p, n_all, world, start_version)
     sharding = sharding_for(args, p, world)
@@ -287,30 +290,39 @@ def main():
         c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
 
+    host = {"add": 0.0, "submit": 0.0, "wait": 0.0}
+
     def run(lo, hi, objs):
         """Submit batches lo..hi-1 (objs: packed ConflictBatch objects, or None: pack inside the
         loop), keeping at most WINDOW in flight; upload (H2D), kernels and verdicts each time."""
         inflight = []
+        pc = time.perf_counter
+
+        def retire(j, oj):
+            t = pc()
+            verdicts[j] = oj.wait()
+            host["wait"] += pc() - t
+            if dist is not None:
+                combine(j, verdicts[j])
+            oj.close()
+
         for i in range(lo, hi):
             _, now, no = gbatches[i]
+            t = pc()
             if objs is None:
                 o = C.ConflictBatch(cs)
                 o.add_packed(mine[i])
             else:
                 o = objs[i]
+            t1 = pc()
             o.detect_async(now, no)
+            host["add"] += t1 - t
+            host["submit"] += pc() - t1
             inflight.append((i, o))
             if len(inflight) > WINDOW:
-                j, oj = inflight.pop(0)
-                verdicts[j] = oj.wait()
-                if dist is not None:
-                    combine(j, verdicts[j])
-                oj.close()
+                retire(*inflight.pop(0))
         for j, oj in inflight:
-            verdicts[j] = oj.wait()
-            if dist is not None:
-                combine(j, verdicts[j])
-            oj.close()
+            retire(j, oj)
 
     def packed(lo, hi):
         objs = {}
@@ -337,11 +349,25 @@ def main():
     objs = packed(timed_lo, timed_hi)
     cs.reset_stats()
     barrier()
+    for k in host:
+        host[k] = 0.0
     t_start = time.perf_counter()
     run(timed_lo, timed_hi, objs)
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t_start)
     st = cs.stats()
+    host_timed = {k: v / args.steps * 1e3 for k, v in host.items()}
+
+    resident_elapsed = None
+    if args.resident_steps > 0:  # diagnostic: batches uploaded before the timed region
+        objs = packed(res_lo, res_hi)
+        for o in objs.values():
+            o.upload()
+        barrier()
+        t_start = time.perf_counter()
+        run(res_lo, res_hi, objs)
+        barrier()
+        resident_elapsed = max_over_ranks(time.perf_counter() - t_start)
 
     total_elapsed = None
     if n_total > 0:  # the reference's "total": addTransaction inside the loop as well
@@ -461,6 +487,9 @@ def main():
         },
         "conflict_ranges_per_s": granges / elapsed,
         "total_txns_per_s": ttxn / total_elapsed if total_elapsed else None,
+        "device_resident_txns_per_s": (sum(gbatches[i][0].n_txn for i in range(res_lo, res_hi)) / resident_elapsed
+                                       if resident_elapsed else None),
+        "host_ms_per_batch": host_timed,
         "total_note": "reference 'total' (SkipList.cpp:1082-1085): addTransaction + detect, per batch in the loop",
         "parity": parity,
         "history_boundaries_end": hist_end,

@@ -37,8 +37,10 @@ namespace {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 constexpr int64_t kTailSlack = 64;  // bytes past a tail arena's capacity (dkey.h tail_word reads aligned words)
-constexpr int64_t kTailLimit = (int64_t)1 << 32;    // tail offsets are uint32 (engine.h Hist::lt)
-constexpr int64_t kTailReclaim = (int64_t)1 << 31;  // force the GC repack past half of that
+// History tails are 8-byte aligned and addressed in 8-byte units by the uint32 Hist::lt.y: the
+// arena holds up to 32 GiB of tail bytes per conflict set (detect refuses a batch past that).
+constexpr int64_t kTailLimit = (int64_t)8 << 32;
+constexpr int64_t kTailReclaimDefault = kTailLimit / 2;  // force the GC repack past half of that
 
 // Grow-only device allocation.
 struct DBuf {
@@ -160,6 +162,8 @@ struct fdbcs_conflict_set {
     int astreams = 1;         // FDBCS_ASTREAMS: stage-A streams (1, or 2 to alternate batches; same
                               // C3 throughput, and C2 measured 36.2M vs 35.1M txns/s mean with 1)
     int sort_alg = 0;       // FDBCS_SORT_ALG: per-bucket sort (0 rank count, 1 bitonic network)
+    int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
+    bool dma_upload = false;  // FDBCS_UPLOAD=dma: hipMemcpyAsync instead of the k_upload kernel
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -648,7 +652,7 @@ int do_upload(fdbcs_batch* b) {
     const size_t T = b->T(), R = b->R(), W = b->W();
     const UploadLayout L = upload_layout(T, R, W, b->tail_size());
     int rc;
-    if (!b->direct && (rc = sl->pin_in.ensure(L.total))) return rc;
+    if (!b->direct && (rc = sl->pin_in.ensure(L.total, true))) return rc;
     if ((rc = ensure_slot(sl, L.total, T, R))) return rc;
     char* h = (char*)sl->pin_in.p;
     if (!b->direct) {  // add_transaction path: normalized keys are in the pageable vectors
@@ -666,7 +670,12 @@ int do_upload(fdbcs_batch* b) {
     // slot's device copy may still be read by the epilogue of the batch that used it last.
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
     if (sl->free_recorded) HIPOK(hipStreamWaitEvent(cs->astream, sl->ev_free, 0));
-    HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
+    if (cs->dma_upload) {
+        HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
+    } else {
+        launch_upload(cs->astream, sl->pin_in.dp, sl->dev.p, (int64_t)L.total);
+        HIPOK(hipGetLastError());
+    }
     HIPOK(hipEventRecord(sl->ev_up, cs->astream));
     char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
@@ -726,6 +735,8 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
     if (const char* v = getenv("FDBCS_ASTREAMS")) cs->astreams = atoi(v) == 1 ? 1 : 2;
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
+    if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
+    if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
               (cs->astreams == 1 || hipStreamCreateWithFlags(&cs->astream2, hipStreamNonBlocking) == hipSuccess);
@@ -877,9 +888,11 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
         dkey_prefix(p, (uint32_t)len, &hi, &lo);
         k[i] = make_ulonglong2(hi, lo);
         uint32_t toff = 0;
-        if (len > 16) {
-            toff = (uint32_t)tail.size();
+        if (len > 16) {  // 8-byte aligned, offset in 8-byte units
+            if ((int64_t)tail.size() + len >= kTailLimit) return FDBCS_E_NOMEM;
+            toff = (uint32_t)(tail.size() / 8);
             tail.insert(tail.end(), p + 16, p + len);
+            tail.resize((tail.size() + 7) / 8 * 8, 0);
         }
         lt[i] = make_uint2((uint32_t)len, toff);
         maxv = std::max(maxv, versions[i]);
@@ -1044,7 +1057,7 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     const int64_t nk = 2 * ((int64_t)pb->read_offsets[T] + pb->write_offsets[T]);
     const size_t tail_bound = nk ? (size_t)(pb->key_offsets[nk] - pb->key_offsets[0]) : 0;
     const UploadLayout L = upload_layout(T, Ra, Wa, tail_bound);
-    if (int rc = b->slot->pin_in.ensure(L.total)) return rc;
+    if (int rc = b->slot->pin_in.ensure(L.total, true)) return rc;
     char* h = (char*)b->slot->pin_in.p;
     DKey* keys = (DKey*)(h + L.keys);
     int32_t* rown = (int32_t*)(h + L.rown);
@@ -1164,12 +1177,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (now < cs->max_written) return FDBCS_E_VERSION;
     if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
     // tail offsets are 32-bit: refuse a batch that could overflow the arena (GC repacks it long before)
-    if (cs->tail_ub + (int64_t)b->tail_size() + 1 >= kTailLimit) return FDBCS_E_NOMEM;
+    // history tail bytes this batch can append (each inserted tail padded to 8 bytes)
+    const int64_t tail_add = (int64_t)b->tail_size() + 16 * (int64_t)b->W();
+    if (cs->tail_ub + tail_add + 1 >= kTailLimit) return FDBCS_E_NOMEM;
     const int64_t T = b->T(), R = b->R(), W = b->W();
     int rc;
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
     if ((rc = ensure_delta(cs, cs->nd_ub + 2 * W + 1))) return rc;
-    if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + (int64_t)b->tail_size() + 1)))
+    if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + tail_add + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
     // results (host-mapped, written by the epilogue): verdicts | scalars | completion flag, then the
@@ -1277,7 +1292,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // (SkipList.cpp:880-889) runs with it whenever the oldest version moved.
     bool compact = nd_after > delta_limit_for(cs, cs->n_ub);
     if (cs->gc_interval > 0 && ++cs->batches_since_compact >= cs->gc_interval) compact = true;
-    if (cs->tail_ub > kTailReclaim) compact = true;
+    if (cs->tail_ub > cs->tail_reclaim) compact = true;
     bool gc = false;
     int final_base = bsrc;
     const int64_t base_hint = cs->n_ub + nd_after + 1;
@@ -1295,7 +1310,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // only when it and its predecessor are both older, SkipList.cpp:555-561). Verdict-neutral
         // either way; a forced cadence (gc_interval > 0) keeps GC at every compaction.
         const bool gc_turn = cs->gc_interval > 0 || ++cs->compactions_since_gc >= kGcEveryCompactions;
-        gc = (new_oldest > cs->gc_applied && gc_turn) || cs->tail_ub > kTailReclaim;
+        gc = (new_oldest > cs->gc_applied && gc_turn) || cs->tail_ub > cs->tail_reclaim;
         if (gc) cs->compactions_since_gc = 0;
     }
     if ((rc = mark(kPhCompact))) return rc;
@@ -1331,7 +1346,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     } else {
         cs->nd_ub = nd_after;
     }
-    cs->tail_ub += (int64_t)b->tail_size();
+    cs->tail_ub += tail_add;
     cs->inflight++;
     b->state = 2;
     return FDBCS_OK;

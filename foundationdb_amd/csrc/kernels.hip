@@ -22,13 +22,30 @@ namespace fdbcs {
 
 // ------------------------------------------------------------------ helpers
 
+// History tails are 8-byte aligned and Hist::lt.y counts 8-byte units (32 GiB of tail arena per
+// conflict set with a 32-bit offset).
+__device__ __forceinline__ const uint8_t* hist_tail(const uint8_t* htail, uint32_t unit) {
+    return htail + 8 * (size_t)unit;
+}
+__device__ __forceinline__ uint32_t tail_units(uint32_t len) { return len > 16u ? (len - 16u + 7u) / 8u : 0u; }
+
+// Copy the n tail bytes at src (any alignment; the arena has >= 16 bytes of slack past them) to the
+// 8-aligned dst as whole words; the bytes past n in the last word are never compared (tail_cmp).
+__device__ __forceinline__ void copy_tail_words(uint8_t* dst, const uint8_t* src, uint32_t n) {
+    const uintptr_t a = (uintptr_t)src;
+    const uint64_t* w = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    uint64_t* d = (uint64_t*)dst;
+    for (uint32_t i = 0; i < (n + 7u) / 8u; i++) d[i] = sh ? (w[i] >> sh) | (w[i + 1] << (64u - sh)) : w[i];
+}
+
 __device__ __forceinline__ int hist_cmp(const Hist& h, int64_t i, const uint8_t* htail, const DKey& q,
                                         const uint8_t* qtail) {
     ulonglong2 k = h.key[i];
     if (k.x != q.hi) return k.x < q.hi ? -1 : 1;
     if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
     uint2 lt = h.lt[i];
-    if (lt.x > 16u && q.len > 16u) return tail_cmp(htail + lt.y, lt.x, qtail + q.tail, q.len);
+    if (lt.x > 16u && q.len > 16u) return tail_cmp(hist_tail(htail, lt.y), lt.x, qtail + q.tail, q.len);
     return (lt.x > q.len) - (lt.x < q.len);
 }
 
@@ -1511,7 +1528,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     w.seg_ins[s] = endins ? 2 : 1;
     w.seg_endins[s] = endins ? 1 : 0;
     w.seg_vend[s] = hi > 0 ? h.ver[hi - 1] : kHole;
-    w.seg_tlen[s] = (kb.len > 16 ? kb.len - 16 : 0) + ((endins && ke.len > 16) ? ke.len - 16 : 0);
+    w.seg_tlen[s] = tail_units(kb.len) + (endins ? tail_units(ke.len) : 0u);  // 8-byte units
 }
 
 constexpr int kDeltaTile = 256;   // copy tile of the (small) delta tier: ~4 workgroups per CU at C2
@@ -1528,7 +1545,7 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
     for (int64_t t = t0; t <= n / tile + 1; t++) tile_first[t] = (int32_t)U;
 }
 
-// Exclusive prefixes of removed boundaries, inserted boundaries and tail bytes per union segment,
+// Exclusive prefixes of removed boundaries, inserted boundaries and tail units per union segment,
 // plus tile_first for the copy.
 struct SegSumScan {
     Segs g;
@@ -1556,7 +1573,7 @@ struct SegSumScan {
         *io.before = n;
         *io.removed = tot[0];
         *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
-        sc->tail_next = sc->tail_used + (int64_t)tot[2];
+        sc->tail_next = sc->tail_used + 8 * (int64_t)tot[2];
     }
 };
 
@@ -1671,13 +1688,13 @@ struct BatchIns {
         return b.keys[2 * (int)item_range(pmeta[pos]) + end];
     }
     __device__ void operator()(int s, Hist dst, int64_t o) const {
-        int64_t toff = sc->tail_used + tlen[s];
+        int64_t tu = sc->tail_used / 8 + tlen[s];  // 8-byte unit of this segment's first tail
         const DKey kb = key(seg_b[s], 0);
         uint32_t tb = 0;
         if (kb.len > 16) {
-            tb = (uint32_t)toff;
-            for (uint32_t k = 0; k < kb.len - 16; k++) htail[toff + k] = b.tail[kb.tail + k];
-            toff += kb.len - 16;
+            tb = (uint32_t)tu;
+            copy_tail_words(htail + 8 * tu, b.tail + kb.tail, kb.len - 16);
+            tu += tail_units(kb.len);
         }
         dst.key[o] = make_ulonglong2(kb.hi, kb.lo);
         dst.lt[o] = make_uint2(kb.len, tb);
@@ -1686,8 +1703,8 @@ struct BatchIns {
             const DKey ke = key(seg_e[s], 1);
             uint32_t te = 0;
             if (ke.len > 16) {
-                te = (uint32_t)toff;
-                for (uint32_t k = 0; k < ke.len - 16; k++) htail[toff + k] = b.tail[ke.tail + k];
+                te = (uint32_t)tu;
+                copy_tail_words(htail + 8 * tu, b.tail + ke.tail, ke.len - 16);
             }
             dst.key[o + 1] = make_ulonglong2(ke.hi, ke.lo);
             dst.lt[o + 1] = make_uint2(ke.len, te);
@@ -1746,9 +1763,9 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     q.hi = k.x;
     q.lo = k.y;
     q.len = lt.x;
-    q.tail = lt.y;
+    q.tail = 0;  // the query's tail arena below starts at its own tail
     bool exact;
-    const int64_t lo = group_lower_bound(base, basem, nb, q, htail, htail, exact);
+    const int64_t lo = group_lower_bound(base, basem, nb, q, htail, hist_tail(htail, lt.y), exact);
     if ((gt % kArity) != 0) return;
     const int64_t dv = delta.ver[j];
     w.c_lo[j] = lo;
@@ -1834,21 +1851,20 @@ struct GcScan {
     uint8_t* tdst;
     int64_t v, hdr;
     Scalars* sc;
-    // [0] kept boundaries, [1] tail bytes of the kept boundaries (their offsets in the new arena)
+    // [0] kept boundaries, [1] tail units of the kept boundaries (their offsets in the new arena)
     __device__ void load(int64_t i, uint32_t (&x)[2]) const {
         const bool keep = gc_keep(src, i, v, hdr);
-        const uint32_t len = src.lt[i].x;
         x[0] = keep ? 1u : 0u;
-        x[1] = keep && len > 16u ? len - 16u : 0u;
+        x[1] = keep ? tail_units(src.lt[i].x) : 0u;
     }
     __device__ void store(int64_t i, const uint32_t (&ex)[2]) const {
         if (!gc_keep(src, i, v, hdr)) return;
         const int64_t o = ex[0];
         uint2 lt = src.lt[i];
         if (lt.x > 16u) {
-            const uint8_t* a = tsrc + lt.y;
-            uint8_t* d = tdst + ex[1];
-            for (uint32_t k = 0; k < lt.x - 16u; k++) d[k] = a[k];
+            const uint64_t* a = (const uint64_t*)hist_tail(tsrc, lt.y);
+            uint64_t* d = (uint64_t*)hist_tail(tdst, ex[1]);
+            for (uint32_t k = 0; k < tail_units(lt.x); k++) d[k] = a[k];
             lt.y = ex[1];
         }
         dst.key[o] = src.key[i];
@@ -1857,7 +1873,7 @@ struct GcScan {
     }
     __device__ void finish(const uint32_t (&tot)[2]) const {
         sc->n_gc = tot[0];
-        sc->tail_gc = tot[1];
+        sc->tail_gc = 8 * (int64_t)tot[1];
     }
 };
 
@@ -2031,6 +2047,33 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         trace_max(ep.trace, kTrEpiFence);
         __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// ------------------------------------------------------------------ batch upload
+//
+// H2D of a packed batch as a kernel reading the pinned, host-mapped staging buffer over PCIe:
+// an ordinary launch on stage A's stream, so the host never blocks in the copy call (a DMA-engine
+// hipMemcpyAsync behind cross-stream waits held the submitting thread ~0.5 ms per batch).  Each
+// lane moves 16-byte words, four in flight.
+__global__ __launch_bounds__(kBlock) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = src[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < 4; k++) dst[i + k * stride] = v[k];
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes) {
+    const int64_t n16 = (bytes + 15) / 16;
+    int64_t blocks = (n16 + 4 * kBlock - 1) / (4 * kBlock);
+    blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+    hipLaunchKernelGGL(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)host_mapped, (uint4*)dst,
+                       n16);
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {

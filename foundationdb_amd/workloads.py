@@ -333,12 +333,15 @@ def c4_keys(p: C4Params, user: np.ndarray, item: np.ndarray, kind: np.ndarray):
 
 
 def c4_history(p: C4Params, seed: int, start_version: int, users: Tuple[int, int] | None = None,
-               chunk: int = 1_000_000):
+               chunk: int = 2_000_000):
     """Prefilled history of about p.history boundaries: random distinct (user, item) keys (users
     in [users[0], users[1]) when given), each a boundary k and its keyAfter k + b"\\0", with versions
     spread over the window (the step function single-key writes leave).  Sorted by construction:
     tuple order is (user, item) because the user digits are fixed width and positive ints encode
-    order-preservingly (Tuple.cpp:72-117).  Returns (key_bytes, key_offsets, versions)."""
+    order-preservingly (Tuple.cpp:72-117).  Returns (key_bytes, key_offsets, versions).
+
+    Same bytes as c4_keys row by row, built from a per-user prefix table (the user prefix is the
+    long shared part of every key) so the 50M-boundary window generates in seconds."""
     rng = np.random.default_rng(seed + 4000037)
     u0, u1 = users if users is not None else (0, p.users)
     span = p.items - 1
@@ -346,14 +349,45 @@ def c4_history(p: C4Params, seed: int, start_version: int, users: Tuple[int, int
     user = code // span
     item = code % span + 1
     n = 2 * len(code)
+    ulo = int(user.min()) if len(user) else 0
+    uids = np.arange(ulo, int(user.max()) + 1 if len(user) else 0)
+    # prefix(user) = subspace 0x02 "user" 8 digits filler 0x00 (c4_keys without the item)
+    S = len(p.subspace)
+    f0 = S + 13
+    PW = f0 + p.max_filler + 1
+    ptab = np.zeros((len(uids), PW), np.uint8)
+    ptab[:, :S] = np.frombuffer(p.subspace, np.uint8)
+    ptab[:, S] = 0x02
+    ptab[:, S + 1 : S + 5] = np.frombuffer(b"user", np.uint8)
+    v = uids.copy()
+    for d in range(7, -1, -1):
+        ptab[:, S + 5 + d] = ord("0") + (v % 10)
+        v //= 10
+    Lf = c4_filler_len(p, uids)
+    cols = np.arange(PW)[None, :]
+    ptab[(cols >= f0) & (cols < (f0 + Lf)[:, None])] = ord("x")
+    plen = f0 + Lf + 1
     lens = np.empty(n, np.int64)
+    nb = np.where(item >= 256, 2, 1)
     parts = []
+    wcols = np.arange(PW + 4)[None, :]
     for a in range(0, len(code), chunk):
-        m = len(code[a : a + chunk])
-        mat, ln = c4_keys(p, np.repeat(user[a : a + chunk], 2), np.repeat(item[a : a + chunk], 2),
-                          np.tile(np.array([0, 1], np.int64), m))
-        lens[2 * a : 2 * a + 2 * m] = ln
-        parts.append(mat[np.arange(C4_WIDTH)[None, :] < ln[:, None]])
+        ur = np.repeat(user[a : a + chunk] - ulo, 2)
+        m2 = len(ur)
+        tab = np.zeros((m2, PW + 4), np.uint8)
+        tab[:, :PW] = ptab[ur]
+        pl = plen[ur]
+        rows = np.arange(m2)
+        nbr = np.repeat(nb[a : a + chunk], 2)
+        itr = np.repeat(item[a : a + chunk], 2)
+        tab[rows, pl] = (0x14 + nbr).astype(np.uint8)  # positive int code (Tuple.cpp:72-117)
+        two = nbr == 2
+        tab[rows[two], pl[two] + 1] = (itr[two] >> 8).astype(np.uint8)
+        tab[rows[two], pl[two] + 2] = (itr[two] & 0xFF).astype(np.uint8)
+        tab[rows[~two], pl[~two] + 1] = itr[~two].astype(np.uint8)
+        ln = pl + 1 + nbr + np.tile(np.array([0, 1], np.int64), m2 // 2)  # keyAfter: trailing 0x00
+        lens[2 * a : 2 * a + m2] = ln
+        parts.append(tab[wcols < ln[:, None]])
     kb = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
     ko = np.zeros(n + 1, np.int64)
     np.cumsum(lens, out=ko[1:])

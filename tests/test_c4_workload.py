@@ -61,3 +61,24 @@ def test_c4_reduced_oracle_matches_skiplist(oracle_built):
         seen |= set(np.unique(va).tolist())
     assert {0, 2} <= seen  # both conflicts and commits occur
     assert a.history_size() == b.history_size()
+
+
+def test_c4_history_rows_equal_c4_keys():
+    """The per-user-prefix history builder emits exactly the c4_keys bytes of every (user, item, kind)."""
+    p = W.C4Params(users=500, items=3000, history=40_000)
+    kb, ko, vers = W.c4_history(p, seed=9, start_version=1_000_000)
+    span = p.items - 1
+    keys = [kb[ko[i]:ko[i + 1]].tobytes() for i in range(len(ko) - 1)]
+    users = np.array([int(k[len(p.subspace) + 5:len(p.subspace) + 13]) for k in keys[0::2]])
+    # recover each item from its tuple int encoding and rebuild the pair with c4_keys
+    sample = np.arange(0, len(keys) // 2, 97)
+    for j in sample:
+        k = keys[2 * j]
+        plen = k.index(b"\x00", len(p.subspace) + 13) + 1
+        nb = k[plen] - 0x14
+        item = int.from_bytes(k[plen + 1:plen + 1 + nb], "big")
+        mat, ln = W.c4_keys(p, np.array([users[j]] * 2), np.array([item] * 2), np.array([0, 1]))
+        assert mat[0, : ln[0]].tobytes() == k
+        assert mat[1, : ln[1]].tobytes() == keys[2 * j + 1]
+    assert len(set(keys)) == len(keys) and keys == sorted(keys)
+    assert len(vers) == len(keys) and span > 0
