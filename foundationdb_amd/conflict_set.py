@@ -78,6 +78,7 @@ class Stats(ctypes.Structure):
         ("ms_sort_kernel", ctypes.c_double),
         ("sort_launches", ctypes.c_int64),
         ("sort_items", ctypes.c_int64),
+        ("gc_runs", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -1483,6 +1483,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             st.sort_launches += 1;
             st.sort_items += 2 * (int64_t)(b->R() + b->W());
         }
+        st.gc_runs += b->gc_ran ? 1 : 0;
         if (b->compacted) {
             st.compactions += 1;
             st.ms_compact_kernel += ph(kPhCompBegin, kPhCompEnd);

@@ -110,6 +110,7 @@ typedef struct fdbcs_stats {
     double ms_sort_kernel;  /* device time of the per-bucket sort kernel (D.Sort) */
     int64_t sort_launches;
     int64_t sort_items;     /* endpoints sorted (sum over launches) */
+    int64_t gc_runs;        /* removeBefore passes (full, over the base tier after a compaction) */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */

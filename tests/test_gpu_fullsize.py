@@ -1,0 +1,252 @@
+"""GPU parity at the BASELINE configurations' full sizes, on the measured path.
+
+Every test drives the engine the way bench.py does (detect_async with several batches in flight,
+three rotating workspaces, stage A running ahead, size-triggered compaction and GC) and compares
+every verdict with the CPU restatement of the reference (oracle/skiplist_baseline.cpp, itself
+cross-checked against the semantic oracle in test_oracle.py).  A second, independent model, a
+key-space brute force over committed write ranges, pins verdicts and conflicting-key reports
+(ConflictRange / ReportConflictingKeys workload properties, fdbserver/workloads/
+ConflictRange.actor.cpp:226-316, ReportConflictingKeys.actor.cpp:201-278).
+"""
+import time
+
+import numpy as np
+import pytest
+
+from foundationdb_amd import workloads as W
+from foundationdb_amd.packing import CommitTransaction, KeyRange, PackedBatch
+
+pytestmark = pytest.mark.gpu
+
+WINDOW = 8
+
+
+@pytest.fixture(scope="module")
+def oracle_mod():
+    from oracle import oracle
+
+    oracle.build()
+    return oracle
+
+
+def pipeline(engine, cs, seq, on_done, window=WINDOW):
+    """Submit (pb, now, newOldest) batches with `window` in flight; on_done(i, verdicts) in order."""
+    inflight = []
+    for i, (pb, now, no) in enumerate(seq):
+        b = engine.ConflictBatch(cs)
+        b.add_packed(pb)
+        b.detect_async(now, no)
+        inflight.append((i, b))
+        if len(inflight) > window:
+            j, bj = inflight.pop(0)
+            on_done(j, bj.wait())
+            bj.close()
+    for j, bj in inflight:
+        on_done(j, bj.wait())
+        bj.close()
+
+
+def check_against_restatement(oracle_mod, kb, ko, vers, seq, got, gc="bounded"):
+    sl = oracle_mod.SkipListBaseline()
+    if len(vers):
+        sl.load_history(kb, ko, vers)
+    for i, (pb, now, no) in enumerate(seq):
+        v, _ = sl.detect(pb, now, no, gc=gc)
+        bad = np.nonzero(got[i] != v)[0]
+        assert len(bad) == 0, (i, bad[:10], got[i][bad[:10]], v[bad[:10]])
+    return sl
+
+
+def test_async_pipeline_full_c2(engine, oracle_mod):
+    """C2 at full size (5M-boundary history, 5000 txns x 5R+2W) through the async pipeline for 72
+    batches: crosses several size-triggered compactions and a removeBefore pass."""
+    p = W.C2Params()
+    start = 10_000_000
+    kb, ko, vers = W.c2_history(p, seed=1, start_version=start)
+    rng = np.random.default_rng(101)
+    seq, now = [], start
+    for _ in range(72):
+        now += p.version_step
+        seq.append((W.c2_batch(p, rng, now), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    got = {}
+    pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
+    st = cs.stats()
+    assert st["compactions"] >= 3, st["compactions"]
+    assert st["gc_runs"] >= 1, st["gc_runs"]
+    check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
+    cs.close()
+
+
+def test_async_pipeline_full_c3(engine, oracle_mod):
+    """C3 at full size: Zipf(0.99) hot keys, 5000 txns per batch over the 5M-boundary history,
+    heavy intra-batch conflicts resolved in batch order on the device."""
+    p = W.C2Params()
+    start = 10_000_000
+    kb, ko, vers = W.c2_history(p, seed=2, start_version=start)
+    z = W.ZipfGenerator(1_000_000, 0.99)
+    rng = np.random.default_rng(102)
+    seq, now = [], start
+    for _ in range(24):
+        now += p.version_step
+        seq.append((W.c3_batch(p, rng, now, z), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    got = {}
+    pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
+    st = cs.stats()
+    assert st["intra_edges"] > 0
+    check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
+    assert any((got[i] == 0).sum() > 500 for i in got)  # heavy contention really happened
+    cs.close()
+
+
+def test_full_c4_window_gc_and_tail_reclaim(engine, oracle_mod, monkeypatch):
+    """C4 at full size: 50M boundaries of tuple keys (~1.9 GB of tail bytes), the window sliding
+    every batch.  The tail-reclaim threshold is lowered to just above the loaded arena so the
+    size-triggered path compacts, runs removeBefore and repacks the tails within a few batches.
+    Every verdict matches the restatement, and after each device removeBefore the boundary count
+    equals the restatement's after a full removeBefore on the same batch."""
+    p = W.C4Params()
+    start = 10_000_000
+    t0 = time.time()
+    kb, ko, vers = W.c4_history(p, seed=1000, start_version=start)
+    tl = np.diff(ko) - 16
+    tail0 = int(((tl[tl > 0] + 7) // 8 * 8).sum())  # the loaded arena: tails padded to 8 bytes
+    monkeypatch.setenv("FDBCS_TAIL_RECLAIM", str(tail0 + 3_000_000))
+    rng = np.random.default_rng(103)
+    seq, now = [], start
+    for _ in range(8):
+        now += p.version_step
+        seq.append((W.c4_batch(p, rng, now), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    n0 = cs.history_size()
+    assert n0 == len(vers)
+    sl = oracle_mod.SkipListBaseline()
+    sl.load_history(kb, ko, vers)
+    gcs = 0
+    for i, (pb, now_i, no) in enumerate(seq):  # one batch at a time: the GC schedule is observed
+        b = engine.ConflictBatch(cs)
+        b.add_packed(pb)
+        v = b.detect_conflicts(now_i, no)
+        b.close()
+        ran = cs.stats()["gc_runs"] > gcs
+        gcs = cs.stats()["gc_runs"]
+        vo, _ = sl.detect(pb, now_i, no, gc=ran)  # full removeBefore exactly where the device ran one
+        bad = np.nonzero(v != vo)[0]
+        assert len(bad) == 0, (i, bad[:10])
+        if ran:
+            assert cs.history_size() == sl.history_size(), (i, cs.history_size(), sl.history_size())
+    assert gcs >= 1, "tail reclaim never forced a removeBefore"
+    assert time.time() - t0 < 600
+
+
+def brute_force(seq, history=(), oldest0=0):
+    """Key-space model over committed write ranges (versions only grow, so the history's max over a
+    read range exceeds the snapshot iff some committed write intersecting it is newer).  Returns per
+    batch (verdicts, reports): reports hold every history-conflicting read, or the first read that
+    meets an earlier committed write of the same batch (SkipList.cpp:641-645, 821-828)."""
+    written = list(history)  # (begin, end, version)
+    oldest = oldest0
+    out = []
+    for pb, now, no in seq:
+        txns = pb.to_transactions()
+        verdict, conf, batch_w = [], {}, []
+        for t, tr in enumerate(txns):
+            if tr.read_snapshot < oldest and tr.read_conflict_ranges:
+                verdict.append(1)
+                continue
+            hist = [i for i, r in enumerate(tr.read_conflict_ranges)
+                    if any(b < r.end and r.begin < e and v > tr.read_snapshot for b, e, v in written)]
+            if hist:
+                verdict.append(0)
+                if tr.report_conflicting_keys:
+                    conf[t] = hist
+                continue
+            intra = [i for i, r in enumerate(tr.read_conflict_ranges)
+                     if any(w.begin < r.end and r.begin < w.end for w in batch_w)]
+            if intra:
+                verdict.append(0)
+                if tr.report_conflicting_keys:
+                    conf[t] = intra[:1]
+            else:
+                verdict.append(2)
+                batch_w.extend(w for w in tr.write_conflict_ranges if w.begin < w.end)
+        written.extend((w.begin, w.end, now) for w in batch_w)
+        oldest = max(oldest, no)
+        out.append((np.array(verdict, np.uint8), conf))
+    return out
+
+
+def nonempty_batch(rng, n, now, alphabet=3, max_len=3):
+    def key():
+        return bytes(int(x) for x in rng.integers(0, alphabet, size=int(rng.integers(0, max_len + 1))))
+
+    def rr():
+        while True:
+            a, b = key(), key()
+            if a != b:
+                return KeyRange(min(a, b), max(a, b))
+
+    txns = [CommitTransaction([rr() for _ in range(int(rng.integers(0, 4)))],
+                              [rr() for _ in range(int(rng.integers(0, 3)))],
+                              int(now - rng.integers(0, 12)), bool(rng.random() < 0.6)) for _ in range(n)]
+    return PackedBatch.from_transactions(txns)
+
+
+@pytest.mark.parametrize("gc_interval,delta_limit", [(1, 0), (0, 12)])
+def test_engine_matches_keyspace_bruteforce(engine, gc_interval, delta_limit):
+    """An independent model (no skip list, no step function: committed write ranges with versions)
+    pins the engine's verdicts and conflicting-key reports.  Non-empty ranges only (NativeAPI never
+    sends empty ones, NativeAPI.actor.cpp:3192-3194); touching, nesting and shared prefixes abound."""
+    rng = np.random.default_rng(404 + gc_interval)
+    for trial in range(6):
+        seq, now = [], 20
+        for _ in range(10):
+            seq.append((nonempty_batch(rng, int(rng.integers(5, 80)), now), now, now - int(rng.integers(3, 9))))
+            now += int(rng.integers(1, 4))
+        want = brute_force(seq)
+        cs = engine.ConflictSet(0)
+        cs.set_gc_interval(gc_interval)
+        cs.set_delta_limit(delta_limit)
+        for i, (pb, now_i, no) in enumerate(seq):
+            m = {}
+            b = engine.ConflictBatch(cs, m)
+            b.add_packed(pb)
+            v = b.detect_conflicts(now_i, no)
+            b.close()
+            wv, wc = want[i]
+            assert (v == wv).all(), (trial, i, np.nonzero(v != wv)[0][:8])
+            got = {t: sorted(x) for t, x in m.items() if x}
+            assert got == wc, (trial, i)
+            # ConflictRange soundness / precision (ConflictRange.actor.cpp:226-316): a committed txn
+            # read nothing newer than its snapshot; every aborted non-TooOld txn has a reason
+            for t, tr in enumerate(pb.to_transactions()):
+                if v[t] == 0 and tr.report_conflicting_keys:
+                    assert got.get(t), (trial, i, t)
+        cs.close()
+
+
+def test_worst_case_dependency_chain(engine, oracle_mod):
+    """Batch-order resolution's adversarial case: transaction t reads the key transaction t-1
+    writes, 5000 deep, so each verdict depends on the previous one (commit, abort, commit, ...)."""
+    T = 5000
+    keys = [b"chain%06d" % i for i in range(T + 1)]
+    txns = [CommitTransaction([KeyRange(keys[t], keys[t] + b"\x00")], [KeyRange(keys[t + 1], keys[t + 1] + b"\x00")],
+                              100, False) for t in range(T)]
+    pb = PackedBatch.from_transactions(txns)
+    cs = engine.ConflictSet(0)
+    cs.set_timing(2)
+    b = engine.ConflictBatch(cs)
+    b.add_packed(pb)
+    v = b.detect_conflicts(100, 0)
+    b.close()
+    expect = np.array([2 if t % 2 == 0 else 0 for t in range(T)], np.uint8)
+    assert (v == expect).all()
+    vo, _ = oracle_mod.OracleConflictSet().detect(pb, 100, 0)
+    assert (vo == v).all()
+    st = cs.stats()
+    print(f"chain of {T}: {st['intra_rounds']} resolution rounds, intra phase {st['ms_intra']:.3f} ms")
+    cs.close()
