@@ -263,6 +263,7 @@ class ConflictBatch:
         self.conflicting_key_range_map = conflicting_key_range_map
         self.transaction_count = 0
         self._report: List[bool] = []
+        self._has_reads: List[bool] = []
         self._keep = []  # arrays that must outlive add calls (keys are copied by the library)
         self.verdicts: Optional[np.ndarray] = None
 
@@ -310,6 +311,7 @@ class ConflictBatch:
         _check(rc, "addTransaction")
         self.transaction_count += 1
         self._report.append(bool(tr.report_conflicting_keys))
+        self._has_reads.append(len(tr.read_conflict_ranges) > 0)
 
     def add_packed(self, pb: PackedBatch) -> None:
         """addTransaction for every transaction of a packed batch, in order."""
@@ -317,6 +319,7 @@ class ConflictBatch:
         _check(load_library().fdbcs_batch_add_packed(self._h, ctypes.byref(cs)), "addTransaction(packed)")
         self.transaction_count += pb.n_txn
         self._report.extend(bool(x) for x in pb.report)
+        self._has_reads.extend((np.diff(pb.read_offsets) > 0).tolist())
 
     def upload(self) -> None:
         _check(load_library().fdbcs_batch_upload(self._h), "upload")
@@ -370,10 +373,11 @@ class ConflictBatch:
         m = self.conflicting_key_range_map
         if m is None:
             return
-        # the reference creates an entry for every reporting, admitted transaction
-        # ((*conflictingKeyRangeMap)[t], SkipList.cpp:782-784) and appends conflicting read indices
+        # the reference creates (*conflictingKeyRangeMap)[t] while registering the read ranges of a
+        # reporting, admitted transaction (SkipList.cpp:777-784): only transactions with reads get
+        # an entry; conflicting read indices are appended to it
         for t, rep in enumerate(self._report):
-            if rep and self.verdicts[t] != TransactionTooOld:
+            if rep and self._has_reads[t] and self.verdicts[t] != TransactionTooOld:
                 entry = m.setdefault(t, [])
                 if self.verdicts[t] == TransactionConflict:
                     entry.extend(self.conflicting_reads(t))

@@ -102,6 +102,7 @@ struct ConflictBatchT {
                                                       (int32_t)wb.size(), wb.data(), wbl.data(), we.data(), wel.data()),
                           "addTransaction");
         report.push_back(tr.report_conflicting_keys);
+        hasReads.push_back(!tr.read_conflict_ranges.empty());
     }
 
     // SkipList.cpp:844-890: nonConflicting / tooOld lists as in :869-876.
@@ -119,8 +120,10 @@ struct ConflictBatchT {
         if (map) {
             std::vector<int32_t> idx;
             for (int t = 0; t < (int)report.size(); t++) {
-                if (!report[t] || verdicts[t] == TransactionTooOld) continue;
-                auto& entry = (*map)[t];  // SkipList.cpp:782-784 creates the entry
+                // the reference creates the entry while registering a reporting transaction's read
+                // ranges (SkipList.cpp:777-784): admitted (not TooOld) and with at least one read
+                if (!report[t] || !hasReads[t] || verdicts[t] == TransactionTooOld) continue;
+                auto& entry = (*map)[t];
                 int32_t n = 0;
                 fdbcs_shim::check(fdbcs_batch_conflicting_reads(b, t, nullptr, 0, &n), "conflictingReads");
                 idx.resize(n > 0 ? n : 1);
@@ -141,6 +144,7 @@ private:
     fdbcs_batch* b = nullptr;
     std::function<void(typename ConflictingKeyRangeMap::mapped_type&, int)> append;
     std::vector<bool> report;
+    std::vector<bool> hasReads;
     std::vector<uint8_t> verdicts;
 };
 

@@ -128,9 +128,13 @@ class _CSBase:
         )
         if n < 0:
             raise RuntimeError("oracle detect failed")
+        # conflictingKeyRangeMap as the reference fills it: an entry for every reporting transaction
+        # that was admitted with at least one read range (created in addTransaction,
+        # SkipList.cpp:777-784), holding the conflicting read indices (empty if it committed)
         conf = {}
+        roff = pb.read_offsets
         for t in range(T):
-            if pb.report[t] and off[t + 1] > off[t]:
+            if pb.report[t] and roff[t + 1] > roff[t] and verdicts[t] != 1:
                 conf[t] = idx[off[t] : off[t + 1]].tolist()
         return verdicts, conf
 

@@ -69,7 +69,7 @@ class EngineDriver:
         b.add_packed(pb)
         v = b.detect_conflicts(now, new_oldest)
         b.close()
-        return v, {t: sorted(x) for t, x in m.items() if x}
+        return v, {t: sorted(x) for t, x in m.items()}
 
 
 def nonempty(conf):

@@ -221,6 +221,9 @@ def test_engine_matches_keyspace_bruteforce(engine, gc_interval, delta_limit):
             assert (v == wv).all(), (trial, i, np.nonzero(v != wv)[0][:8])
             got = {t: sorted(x) for t, x in m.items() if x}
             assert got == wc, (trial, i)
+            # entries exist exactly for reporting, admitted transactions with reads (SkipList.cpp:777-784)
+            roff = pb.read_offsets
+            assert set(m) == {t for t in range(pb.n_txn) if pb.report[t] and roff[t + 1] > roff[t] and v[t] != 1}
             # ConflictRange soundness / precision (ConflictRange.actor.cpp:226-316): a committed txn
             # read nothing newer than its snapshot; every aborted non-TooOld txn has a reason
             for t, tr in enumerate(pb.to_transactions()):

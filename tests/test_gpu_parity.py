@@ -32,8 +32,8 @@ def run_pair(engine, oracle_mod, seq, gc_interval=1, clear=None, check_conf=True
         ve, ce = e.detect(pb, now, no)
         vo, co = o.detect(pb, now, no)
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10], ve[ve != vo][:10], vo[ve != vo][:10])
-        if check_conf:
-            assert ce == nonempty(co), i
+        if check_conf:  # the whole conflictingKeyRangeMap: entries (even empty ones) and contents
+            assert ce == co, i
     return e, o
 
 
@@ -46,7 +46,7 @@ def test_kat_scenarios(engine):
             v, c = e.detect(pb, now, no)
             assert v.tolist() == expect, (scn["name"], i, v.tolist(), expect)
             if conf:
-                assert c == conf, (scn["name"], c, conf)
+                assert nonempty(c) == conf, (scn["name"], c, conf)
 
 
 def test_frozen_random_fixtures(engine):
@@ -55,7 +55,7 @@ def test_frozen_random_fixtures(engine):
         for pb, now, no, verdict, conf in seq:
             v, c = e.detect(pb, now, no)
             assert (v == verdict).all(), s
-            assert c == conf, s
+            assert nonempty(c) == conf, s
 
 
 @pytest.mark.parametrize("alphabet,max_len", [(2, 2), (3, 3), (4, 5), (256, 2), (3, 24), (2, 40)])

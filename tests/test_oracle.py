@@ -220,3 +220,21 @@ def test_skiplist_restatement_c2_shape(oracle_built):
         assert (va == vb).all()
         seen |= set(np.unique(va).tolist())
     assert {0, 2} <= seen
+
+
+def test_conflicting_key_map_entries_follow_add_transaction(oracle_built):
+    """conflictingKeyRangeMap[t] is created while addTransaction registers a reporting transaction's
+    read ranges (SkipList.cpp:777-784): a reporting transaction that only writes gets no entry, a
+    reporting reader that commits gets an empty one, a TooOld one none."""
+    txns = [
+        CommitTransaction([], [KeyRange(b"a", b"b")], 10, True),             # writes only
+        CommitTransaction([KeyRange(b"x", b"y")], [], 10, True),             # reads, commits
+        CommitTransaction([KeyRange(b"a", b"c")], [], 10, True),             # reads what txn 0 wrote
+        CommitTransaction([KeyRange(b"m", b"n")], [], 1, True),              # TooOld below
+    ]
+    pb = PackedBatch.from_transactions(txns)
+    cs = oracle_built.OracleConflictSet()
+    cs.set_oldest_version(5)
+    v, conf = cs.detect(pb, 10, 5)
+    assert v.tolist() == [2, 2, 0, 1]
+    assert conf == {1: [], 2: [0]}
