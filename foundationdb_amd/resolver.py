@@ -126,6 +126,7 @@ class Resolver:
         self.proxy_info: Dict[object, _ProxyRequestsInfo] = {}
         self.debug_min_recent_state_version = 0
         self._held: List[ResolveTransactionBatchRequest] = []
+        self._past_pressure: set = set()  # held requests already through the back-pressure loop (:126-133)
         self.counters = {k: 0 for k in (
             "ResolveBatchIn", "ResolveBatchStart", "ResolvedTransactions", "ResolvedBytes",
             "ResolvedReadConflictRanges", "ResolvedWriteConflictRanges", "TransactionsAccepted",
@@ -152,6 +153,7 @@ class Resolver:
             for r in list(self._held):
                 if self._ready(r):
                     self._held.remove(r)
+                    self._past_pressure.discard(id(r))
                     done.append((r, self._resolve(r)))
                     progress = True
                     break
@@ -167,11 +169,14 @@ class Resolver:
 
     def _ready(self, req) -> bool:
         info = self.proxy_info.setdefault(self._proxy_key(req), _ProxyRequestsInfo())
-        # back-pressure on state-transaction memory (:126-131)
-        if (self.total_state_bytes > self.state_memory_limit and self.recent_state_transaction_sizes
-                and info.last_version > self.recent_state_transaction_sizes[0][0]
-                and req.version > self.needed_version):
-            return False
+        # back-pressure on state-transaction memory (:126-133): checked until the request gets past
+        # it once; after that the actor only waits on its predecessor version (:139-150)
+        if id(req) not in self._past_pressure:
+            if (self.total_state_bytes > self.state_memory_limit and self.recent_state_transaction_sizes
+                    and info.last_version > self.recent_state_transaction_sizes[0][0]
+                    and req.version > self.needed_version):
+                return False
+            self._past_pressure.add(id(req))
         # :143-146: a proxy behind the oldest recent state version raises neededVersion
         if self.recent_state_transaction_sizes and info.last_version <= self.recent_state_transaction_sizes[0][0]:
             self.needed_version = max(self.needed_version, req.prev_version)

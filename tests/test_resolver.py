@@ -34,8 +34,9 @@ class OracleBatch:
                 too_old.append(t)
             elif x == TransactionCommitted:
                 non_conflicting.append(t)
-            if self.map is not None and self.txns[t].report_conflicting_keys and x != TransactionTooOld:
-                self.map.setdefault(t, []).extend(conf.get(t, []) if x == TransactionConflict else [])
+        if self.map is not None:  # the oracle returns exactly the reference's map entries
+            for t, x in conf.items():
+                self.map.setdefault(t, []).extend(x)
         return v
 
 
@@ -122,6 +123,20 @@ def test_state_memory_back_pressure_holds_a_proxy_that_is_ahead(oracle_built):
     assert r.submit(Req(30, 40, 0, [], proxy="A")) == [] and [q.version for q in r.held] == [40]
     r.state_memory_limit = 10**6
     assert [q.version for q, _ in r.poll()] == [40]
+
+
+def test_back_pressure_is_checked_once_at_arrival(oracle_built):
+    """A request that got past the state-memory check while it waited for its predecessor is not
+    held again when that predecessor pushes totalStateBytes over the limit: the actor checks
+    back-pressure once (Resolver.actor.cpp:126-133), then only waits on the version (:139-150)."""
+    r = _resolver(oracle_built, commit_proxy_count=2, state_memory_limit=4)
+    r.submit(Req(-1, 10, -1, []))
+    assert r.submit(Req(20, 30, 0, [], proxy="A")) == []  # waits for v20, no state bytes yet
+    done = r.submit(Req(10, 20, 0, [_txn()], [0], {0: [(b"\xff/a", b"0123456789")]}, proxy="A"))
+    assert [q.version for q, _ in done] == [20, 30]
+    assert r.total_state_bytes > r.state_memory_limit
+    # a request arriving now does meet the back-pressure loop
+    assert r.submit(Req(30, 40, 0, [], proxy="A")) == [] and [q.version for q in r.held] == [40]
 
 
 def test_conflicting_key_map_reported(oracle_built):
