@@ -164,6 +164,9 @@ struct fdbcs_conflict_set {
     int sort_alg = 0;       // FDBCS_SORT_ALG: per-bucket sort (0 rank count, 1 bitonic network)
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
     bool dma_upload = false;  // FDBCS_UPLOAD=dma: hipMemcpyAsync instead of the k_upload kernel
+    int upload_blocks = 32;   // FDBCS_UPLOAD_BLOCKS: workgroups of the k_upload kernel
+    int check_version = 2;    // FDBCS_CHECK: read-check kernel (2 LDS-staged fused search, 1 four lookups)
+    int check_grid = 1024;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -673,7 +676,7 @@ int do_upload(fdbcs_batch* b) {
     if (cs->dma_upload) {
         HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
     } else {
-        launch_upload(cs->astream, sl->pin_in.dp, sl->dev.p, (int64_t)L.total);
+        launch_upload(cs->astream, sl->pin_in.dp, sl->dev.p, (int64_t)L.total, cs->upload_blocks);
         HIPOK(hipGetLastError());
     }
     HIPOK(hipEventRecord(sl->ev_up, cs->astream));
@@ -736,6 +739,9 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_ASTREAMS")) cs->astreams = atoi(v) == 1 ? 1 : 2;
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
+    if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
+    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : 2;
+    if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
@@ -1268,7 +1274,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- stage B: D.CheckRead against the history the previous batch left, then batch order
     b->check_hist = cs->n_ub + cs->nd_ub;
     if (hipEvent_t e = rec(kPhCheckBegin, 1)) HIPOK(hipEventRecord(e, s));
-    launch_check(s, bd, w, base, delta, htail);
+    launch_check(s, bd, w, base, delta, htail, cs->check_version, cs->check_grid);
     if (hipEvent_t e = rec(kPhCheckEnd, 1)) HIPOK(hipEventRecord(e, s));
     if ((rc = mark(kPhCheck))) return rc;
     if (sa != s) HIPOK(hipStreamWaitEvent(s, cs->ev_a[wp], 0));

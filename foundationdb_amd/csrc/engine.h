@@ -205,8 +205,10 @@ struct Tier {
 // Sample ranking for the sort's splitters.
 void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per);
 // D.CheckRead against the history the previous batch left.
+// check_version: 2 = LDS-staged fused begin/end search (default), 1 = four lookups per read.
+// check_grid_cap: workgroups of the version-2 kernel (each loops over reads).
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail);
+                  const uint8_t* htail, int check_version = 2, int check_grid_cap = 2048);
 // bucket_target: endpoints per sample-sort bucket (0 = default 128; tests force oversized buckets).
 // sample_per: splitter samples per bucket (0 = default 8).
 // alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
@@ -234,7 +236,7 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
                Scalars* sc, int64_t oldest, int64_t header_version, int64_t grid_hint_n);
 // H2D of `bytes` (16-byte multiple, both sides 16-aligned) from host-mapped pinned memory, as a kernel.
-void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes);
+void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes, int max_blocks);
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 // Range-max levels of a tier whose size is *n (lvl[3] reset first).

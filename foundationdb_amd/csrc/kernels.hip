@@ -441,6 +441,225 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
     }
 }
 
+// ---- D.CheckRead, LDS-staged: the top levels of both tiers' sample trees live in LDS, and one
+// lane group finds a read's begin AND end in a tier, sharing every node until the two paths part.
+//
+// Per read two groups of kArity lanes (base tier, delta tier) instead of four.  A short read
+// [k, k + d) meets the same nodes all the way down and the same 64-boundary block, so the end
+// search costs no extra dependent load; each staged level saves one (~0.5 us on a loaded chip).
+constexpr int kCheckThreads = 256;
+constexpr int kCheckReadLanes = 2 * kArity;                   // base group, delta group
+constexpr int kCheckReadsPerBlock = kCheckThreads / kCheckReadLanes;
+constexpr int kLdsTreeBase = 1536;                            // staged sample keys of the base tier
+constexpr int kLdsTreeDelta = 512;                            // ... of the delta tier (24 + 8 KiB)
+
+// Entries of sample-tree level L over n boundaries: the samples are every 64th boundary and each
+// level above takes every kArity-th entry, so sz(L) = ceil(n / (64 * 8^L)).
+__device__ __forceinline__ int64_t tree_sz(int64_t n, int L) {
+    const int sh = 6 + 3 * L;
+    return (n + ((int64_t)1 << sh) - 1) >> sh;
+}
+__device__ __forceinline__ int tree_top(int64_t n) {
+    int top = 0;
+    while (top + 1 < kIdxLevels && tree_sz(n, top) > kArity) top++;
+    return top;
+}
+
+// One tier's sample tree as the check kernel sees it: levels [lds_lo, top] are staged in LDS at
+// the per-level offsets `off` (an LDS table shared by the workgroup, uniform reads).
+struct TreeRef {
+    int64_t n;
+    int top, lds_lo;
+    const int* off;       // [kIdxLevels] LDS index of level L's first entry
+    const ulonglong2* lds;
+};
+
+__device__ __forceinline__ ulonglong2 tree_entry(const MaxLevels& m, const TreeRef& t, int L, int64_t i) {
+    return L >= t.lds_lo ? t.lds[t.off[L] + i] : m.skey[L][i];
+}
+
+// Levels of a tier to stage: from the top down while they fit `budget` entries; fills off[] and
+// returns lds_lo (top + 1: none).
+__device__ __forceinline__ int plan_stage(int64_t n, int top, int budget, int lds_base, int* off) {
+    int lo = top + 1;
+    int64_t used = 0;
+    for (int L = top; L >= 0 && n > 0; L--) {
+        const int64_t z = tree_sz(n, L);
+        if (used + z > budget) break;
+        off[L] = lds_base + (int)used;
+        used += z;
+        lo = L;
+    }
+    return lo;
+}
+
+// lower_bound of qb and (want_e) of qe >= qb over one tier, by one aligned group of kArity lanes.
+// lb / eqb: begin's position and whether the boundary there equals qb; le: end's position.
+__device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevels& m, const TreeRef& tv,
+                                                   const DKey& qb, const DKey& qe, bool want_e, const uint8_t* htail,
+                                                   const uint8_t* qtail, int64_t& lb, bool& eqb, int64_t& le) {
+    const int gl = threadIdx.x & (kArity - 1);
+    const int g0 = threadIdx.x & 63 & ~(kArity - 1);
+    lb = le = 0;
+    eqb = false;
+    const int64_t n = tv.n;
+    if (n <= 0) return;
+    auto peq = [](const ulonglong2& k, const DKey& q) { return k.x == q.hi && k.y == q.lo; };
+    const int top = tv.top;
+    int64_t cb = 0, ce = 0;
+    bool kb = false, ke = false;  // `known` of the begin / end search
+    bool doneb = false, donee = !want_e;
+    const int64_t sztop = tree_sz(n, top);
+    for (int64_t j0 = 0; j0 < sztop && !(doneb && donee); j0 += kArity) {
+        const bool v = j0 + gl < sztop;
+        const ulonglong2 e = tree_entry(m, tv, top, v ? j0 + gl : 0);
+        const int nv = __popc(gmask(v));
+        if (!doneb) {
+            const int k = __popc(gmask(v && prefix_less(e, qb)));
+            if (top == 0 && k < nv) kb = !((gmask(v && peq(e, qb)) >> k) & 1u);
+            cb += k;
+            doneb = k < kArity;
+        }
+        if (!donee) {
+            const int k = __popc(gmask(v && prefix_less(e, qe)));
+            if (top == 0 && k < nv) ke = !((gmask(v && peq(e, qe)) >> k) & 1u);
+            ce += k;
+            donee = k < kArity;
+        }
+    }
+    if (!want_e) ce = cb;
+    for (int L = top; L > 0; L--) {
+        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, A c]
+        const int64_t szl = tree_sz(n, L - 1);
+        const int64_t bb = kArity * (cb - 1) + 1, be = min((int64_t)kArity * cb, szl);
+        const int64_t eb = kArity * (ce - 1) + 1, ee = min((int64_t)kArity * ce, szl);
+        const bool vb = cb > 0 && bb + gl < be;
+        const bool ve = want_e && ce > 0 && eb + gl < ee;
+        const ulonglong2 xb = tree_entry(m, tv, L - 1, vb ? bb + gl : 0);
+        const ulonglong2 xe = (ce == cb) ? xb : tree_entry(m, tv, L - 1, ve ? eb + gl : 0);
+        const int nb = __popc(gmask(vb)), kb_ = __popc(gmask(vb && prefix_less(xb, qb)));
+        const int ne = __popc(gmask(ve)), ke_ = __popc(gmask(ve && prefix_less(xe, qe)));
+        if (L == 1) {
+            if (kb_ < nb) kb = !((gmask(vb && peq(xb, qb)) >> kb_) & 1u);
+            if (ke_ < ne) ke = !((gmask(ve && peq(xe, qe)) >> ke_) & 1u);
+        }
+        if (cb > 0) cb = bb + kb_;
+        if (ce > 0 && want_e) ce = eb + ke_;
+    }
+    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
+    const int64_t sz0 = tree_sz(n, 0);
+    auto run_end = [&](int64_t c, bool known, const DKey& q) {
+        int64_t b = c;
+        for (; !known;) {
+            const bool v = b + gl < sz0;
+            const ulonglong2 k = m.skey[0][v ? b + gl : 0];
+            const uint32_t same = gmask(v && peq(k, q));
+            const int run = __ffs(~same) - 1;
+            b += run;
+            if (run < kArity) break;
+        }
+        return b;
+    };
+    const int64_t bbk = run_end(cb, kb, qb);
+    const int64_t bek = want_e ? run_end(ce, ke, qe) : 0;
+    // in-block rounds of kArity probes at a shrinking stride, both searches side by side; a probe
+    // both searches make is loaded once
+    int64_t lo_b = cb > 0 ? kFan * (cb - 1) + 1 : 0, hi_b = min(n, kFan * bbk);
+    int64_t lo_e = ce > 0 ? kFan * (ce - 1) + 1 : 0, hi_e = want_e ? min(n, kFan * bek) : 0;
+    int64_t sp_b = hi_b - lo_b, sp_e = want_e ? hi_e - lo_e : 0;
+    int64_t st_b = kFan / kArity, st_e = kFan / kArity;
+    while (st_b * kArity < sp_b) st_b *= kArity;
+    while (st_e * kArity < sp_e) st_e *= kArity;
+    bool act_b = sp_b > 0, act_e = sp_e > 0;
+    bool eqc = false;
+    while (act_b || act_e) {
+        const int64_t pb = lo_b + st_b * (gl + 1) - 1, pe = lo_e + st_e * (gl + 1) - 1;
+        const bool vb = act_b && st_b * (gl + 1) <= sp_b && pb < hi_b;
+        const bool ve = act_e && st_e * (gl + 1) <= sp_e && pe < hi_e;
+        const ulonglong2 xb = h.key[vb ? pb : 0];
+        const ulonglong2 xe = (vb && ve && pe == pb) ? xb : h.key[ve ? pe : 0];
+        int rb = 1, re = 1;
+        if (vb) rb = probe_cmp(h, pb, xb, htail, qb, qtail);
+        if (ve) re = probe_cmp(h, pe, xe, htail, qe, qtail);
+        if (act_b) {
+            const int nv = __popc(gmask(vb)), cnt = __popc(gmask(vb && rb < 0));
+            const int stop = __shfl(rb, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
+            if (cnt < nv) eqc = stop == 0;
+            lo_b += st_b * cnt;
+            sp_b = cnt < nv ? st_b - 1 : sp_b - st_b * cnt;
+            if (st_b == 1 || sp_b <= 0) act_b = false;
+            st_b = st_b > kArity ? st_b / kArity : 1;
+        }
+        if (act_e) {
+            const int nv = __popc(gmask(ve)), cnt = __popc(gmask(ve && re < 0));
+            lo_e += st_e * cnt;
+            sp_e = cnt < nv ? st_e - 1 : sp_e - st_e * cnt;
+            if (st_e == 1 || sp_e <= 0) act_e = false;
+            st_e = st_e > kArity ? st_e / kArity : 1;
+        }
+    }
+    lb = lo_b;
+    eqb = lo_b < hi_b ? eqc : false;
+    le = lo_e;
+}
+
+struct CheckReads2 {
+    Tier base, delta;
+    const uint8_t* htail;
+    uint8_t *hist_conf, *rconf;
+    unsigned long long* trace;
+};
+
+__global__ __launch_bounds__(kCheckThreads) void k_check_reads2(BatchDev b, CheckReads2 c) {
+    __shared__ ulonglong2 s_tree[kLdsTreeBase + kLdsTreeDelta];
+    __shared__ int s_off[2][kIdxLevels];
+    __shared__ int s_lo[2];
+    if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
+    const int64_t nt[2] = {*c.base.n, *c.delta.n};
+    const int top[2] = {tree_top(nt[0]), tree_top(nt[1])};
+    if (threadIdx.x < 2) {
+        const int t = threadIdx.x;
+        s_lo[t] = plan_stage(nt[t], top[t], t ? kLdsTreeDelta : kLdsTreeBase, t ? kLdsTreeBase : 0, s_off[t]);
+    }
+    __syncthreads();
+    for (int t = 0; t < 2; t++) {  // stage the planned levels (uniform loop bounds)
+        const MaxLevels& m = t ? c.delta.m : c.base.m;
+        for (int L = s_lo[t]; L <= top[t]; L++) {
+            const int64_t z = tree_sz(nt[t], L);
+            for (int64_t i = threadIdx.x; i < z; i += blockDim.x) s_tree[s_off[t][L] + i] = m.skey[L][i];
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int grp = (threadIdx.x / kArity) & 1;  // 0: base tier, 1: delta tier
+    const int lead = lane & ~(kCheckReadLanes - 1);
+    const Tier& tier = grp ? c.delta : c.base;
+    const TreeRef tv{nt[grp], top[grp], s_lo[grp], s_off[grp], s_tree};
+    for (int64_t r0 = (int64_t)blockIdx.x * kCheckReadsPerBlock; r0 < b.R;
+         r0 += (int64_t)gridDim.x * kCheckReadsPerBlock) {
+        const int64_t r = r0 + threadIdx.x / kCheckReadLanes;
+        const bool live = r < b.R;
+        const int rr = live ? (int)r : 0;
+        const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+        const int64_t snap = b.snap[b.rowner[rr]];  // issued before the search
+        const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+        int64_t lb = 0, le = 0;
+        bool eq = false;
+        if (live) group_lower_bound2(tier.h, tier.m, tv, kb, ke, !degenerate, c.htail, b.tail, lb, eq, le);
+        bool conf = false;
+        if (live && (threadIdx.x & (kArity - 1)) == 0 && (grp == 0 || tv.n > 0))
+            conf = tier_conflict(tier.h, tier.m, grp == 0 ? tier.hdr : kHole, lb, eq, le, degenerate, snap);
+        const int dconf = __shfl((int)conf, lead + kArity, 64);
+        if (live && lane == lead) {
+            conf = conf || dconf;
+            c.rconf[r] = conf ? 1 : 0;
+            if (conf) c.hist_conf[b.rowner[r]] = 1;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
+}
+
 // ------------------------------------------------------------------ D.Sort
 
 // Endpoint item p of the batch (KeyInfo, SkipList.cpp:77-87): range g = p / 2, end = p & 1.
@@ -958,11 +1177,18 @@ void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_t
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail) {
+                  const uint8_t* htail, int check_version, int check_grid_cap) {
     if (b.R == 0) return;
-    CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
-    const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
+    if (check_version == 1) {  // FDBCS_CHECK=1: four independent lookups per read, no LDS staging
+        CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
+        const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
+        return;
+    }
+    CheckReads2 c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
+    int64_t grid = ((int64_t)b.R + kCheckReadsPerBlock - 1) / kCheckReadsPerBlock;
+    grid = grid > check_grid_cap ? check_grid_cap : grid;
+    hipLaunchKernelGGL(k_check_reads2, dim3((unsigned)grid), dim3(kCheckThreads), 0, s, b, c);
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
@@ -2055,23 +2281,26 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
 // an ordinary launch on stage A's stream, so the host never blocks in the copy call (a DMA-engine
 // hipMemcpyAsync behind cross-stream waits held the submitting thread ~0.5 ms per batch).  Each
 // lane moves 16-byte words, four in flight.
+// Few workgroups with many loads in flight each: PCIe latency x bandwidth needs ~100 KB in flight,
+// and waves parked on host reads hold CU slots the overlapping stage-B kernels want.
+constexpr int kUploadUnroll = 8;
 __global__ __launch_bounds__(kBlock) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        uint4 v[4];
+    for (; i + (kUploadUnroll - 1) * stride < n16; i += kUploadUnroll * stride) {
+        uint4 v[kUploadUnroll];
 #pragma unroll
-        for (int k = 0; k < 4; k++) v[k] = src[i + k * stride];
+        for (int k = 0; k < kUploadUnroll; k++) v[k] = src[i + k * stride];
 #pragma unroll
-        for (int k = 0; k < 4; k++) dst[i + k * stride] = v[k];
+        for (int k = 0; k < kUploadUnroll; k++) dst[i + k * stride] = v[k];
     }
     for (; i < n16; i += stride) dst[i] = src[i];
 }
 
-void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes) {
+void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes, int max_blocks) {
     const int64_t n16 = (bytes + 15) / 16;
-    int64_t blocks = (n16 + 4 * kBlock - 1) / (4 * kBlock);
-    blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+    int64_t blocks = (n16 + kUploadUnroll * kBlock - 1) / (kUploadUnroll * kBlock);
+    blocks = blocks < 1 ? 1 : (blocks > max_blocks ? max_blocks : blocks);
     hipLaunchKernelGGL(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)host_mapped, (uint4*)dst,
                        n16);
 }
