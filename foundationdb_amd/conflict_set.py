@@ -118,6 +118,7 @@ SIGNATURES = {
     "fdbcs_batch_wait": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "fdbcs_batch_conflicting_reads": (ctypes.c_int, [_VP, _I32, _VP, _I32, ctypes.POINTER(_I32)]),
     "fdbcs_batch_device_verdicts": (ctypes.c_int, [_VP, ctypes.POINTER(_VP)]),
+    "fdbcs_debug_kernel_time": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "fdbcs_strerror": (ctypes.c_char_p, [ctypes.c_int]),
 }
 
@@ -355,6 +356,13 @@ class ConflictBatch:
                 non_conflicting.append(t)
         self._collect_conflicting_keys()
         return v
+
+    def debug_kernel_time(self, which: int = 0, reps: int = 50) -> float:
+        """Average device microseconds of one launch of a pipeline kernel on this (uploaded, not
+        yet detected) batch against the current history: 0 = the read check.  Tuning only."""
+        us = ctypes.c_double()
+        _check(load_library().fdbcs_debug_kernel_time(self._h, which, reps, ctypes.byref(us)), "debugKernelTime")
+        return us.value
 
     def device_verdicts_ptr(self) -> int:
         p = ctypes.c_void_p()

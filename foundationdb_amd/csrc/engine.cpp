@@ -1537,4 +1537,39 @@ int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr) {
     return FDBCS_OK;
 }
 
+int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch) {
+    if (!b || !us_per_launch || reps <= 0 || which != 0) return FDBCS_E_INVALID;
+    if (!b->cs) return FDBCS_E_STATE;
+    fdbcs_conflict_set* cs = b->cs;
+    HIPOK(hipSetDevice(cs->device));
+    if (b->state == 0)
+        if (int rc = fdbcs_batch_upload(b)) return rc;
+    if (b->state != 1) return FDBCS_E_STATE;
+    if (cs->inflight) return FDBCS_E_STATE;
+    const int64_t T = b->T(), R = b->R(), W = b->W();
+    if (int rc = ensure_workspace(cs, T, R, W)) return rc;
+    if (int rc = sync_all(cs)) return rc;
+    Work& w = cs->work[cs->wpar];
+    Scalars* sc = (Scalars*)cs->scal.p;
+    const Tier base{hist_of(cs, cs->cur), levels_of(cs, cs->cur), &sc->n, cs->header_version};
+    const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->nd, kHole};
+    hipEvent_t e0, e1;
+    HIPOK(hipEventCreate(&e0));
+    HIPOK(hipEventCreate(&e1));
+    launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version, cs->check_grid);
+    HIPOK(hipEventRecord(e0, cs->stream));
+    for (int i = 0; i < reps; i++)
+        launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version,
+                     cs->check_grid);
+    HIPOK(hipEventRecord(e1, cs->stream));
+    HIPOK(hipEventSynchronize(e1));
+    *us_per_launch = ev_ms(e0, e1) * 1000.0 / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    // the check leaves per-transaction conflict flags the next batch on this workspace expects zeroed
+    HIPOK(hipMemsetAsync(w.hist_conf, 0, w.cap_T, cs->stream));
+    HIPOK(hipStreamSynchronize(cs->stream));
+    return FDBCS_OK;
+}
+
 }  // extern "C"

@@ -187,6 +187,11 @@ int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out,
  * detect until the batch is destroyed) for on-device combine (RCCL). */
 int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr);
 
+/* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
+ * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the
+ * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead). */
+int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch);
+
 const char* fdbcs_strerror(int status);
 
 #ifdef __cplusplus
