@@ -390,12 +390,13 @@ void carve_index(MaxLevels& m, ulonglong2* base, int64_t cap) {
         m.skey[L] = base;
         base += idx_level_cap(cap, L);
     }
+    m.skey8 = base;  // cap / 8 + 2 entries
 }
 
 int64_t index_bytes(int64_t cap) {
     int64_t n = 0;
     for (int L = 0; L < kIdxLevels; L++) n += idx_level_cap(cap, L);
-    return 16 * n;
+    return 16 * (n + cap / 8 + 2);
 }
 
 MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {

@@ -43,6 +43,7 @@ struct MaxLevels {
     int64_t* lvl[kMaxLevels];       // lvl[0] == current Hist::ver
     const ulonglong2* keys;         // the tier's keys (source of the samples)
     ulonglong2* skey[kIdxLevels];   // [ceil(n / (64 * A^L))]
+    ulonglong2* skey8;              // [ceil(n / 8)] prefix of every 8th boundary: the level below skey[0]
 };
 __host__ __device__ inline int64_t idx_level_cap(int64_t cap, int L) {
     int64_t d = 64;

@@ -495,6 +495,13 @@ __device__ __forceinline__ int plan_stage(int64_t n, int top, int budget, int ld
 
 // lower_bound of qb and (want_e) of qe >= qb over one tier, by one aligned group of kArity lanes.
 // lb / eqb: begin's position and whether the boundary there equals qb; le: end's position.
+//
+// The descent runs through the sample tree (top levels from LDS), then through skey8 (every 8th
+// boundary), so that a lookup touches one 128-byte line per level and a final run of 8
+// consecutive boundaries: 8-ary all the way down.  Every level counts the entries whose prefix is
+// below q's; `known` says whether the first entry not below q has a different prefix (else a run
+// of boundaries sharing q's 16-byte prefix, tuple keys, widens the final span and the strided
+// rounds below compare tails).
 __device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevels& m, const TreeRef& tv,
                                                    const DKey& qb, const DKey& qe, bool want_e, const uint8_t* htail,
                                                    const uint8_t* qtail, int64_t& lb, bool& eqb, int64_t& le) {
@@ -505,54 +512,58 @@ __device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevel
     const int64_t n = tv.n;
     if (n <= 0) return;
     auto peq = [](const ulonglong2& k, const DKey& q) { return k.x == q.hi && k.y == q.lo; };
+    // level L >= 0: sample tree; level -1: skey8
+    auto entry = [&](int L, int64_t i) { return L >= 0 ? tree_entry(m, tv, L, i) : m.skey8[i]; };
+    auto level_sz = [&](int L) { return L >= 0 ? tree_sz(n, L) : (n + 7) / 8; };
     const int top = tv.top;
     int64_t cb = 0, ce = 0;
-    bool kb = false, ke = false;  // `known` of the begin / end search
-    bool doneb = false, donee = !want_e;
-    const int64_t sztop = tree_sz(n, top);
-    for (int64_t j0 = 0; j0 < sztop && !(doneb && donee); j0 += kArity) {
-        const bool v = j0 + gl < sztop;
-        const ulonglong2 e = tree_entry(m, tv, top, v ? j0 + gl : 0);
-        const int nv = __popc(gmask(v));
-        if (!doneb) {
-            const int k = __popc(gmask(v && prefix_less(e, qb)));
-            if (top == 0 && k < nv) kb = !((gmask(v && peq(e, qb)) >> k) & 1u);
-            cb += k;
-            doneb = k < kArity;
-        }
-        if (!donee) {
-            const int k = __popc(gmask(v && prefix_less(e, qe)));
-            if (top == 0 && k < nv) ke = !((gmask(v && peq(e, qe)) >> k) & 1u);
-            ce += k;
-            donee = k < kArity;
+    bool kb = true, ke = true;  // known: the first entry not below q has another prefix (true past the end)
+    {
+        bool doneb = false, donee = !want_e;
+        const int64_t sztop = tree_sz(n, top);
+        for (int64_t j0 = 0; j0 < sztop && !(doneb && donee); j0 += kArity) {
+            const bool v = j0 + gl < sztop;
+            const ulonglong2 e = entry(top, v ? j0 + gl : 0);
+            const int nv = __popc(gmask(v));
+            if (!doneb) {
+                const int k = __popc(gmask(v && prefix_less(e, qb)));
+                if (k < nv) kb = !((gmask(v && peq(e, qb)) >> k) & 1u);
+                cb += k;
+                doneb = k < kArity;
+            }
+            if (!donee) {
+                const int k = __popc(gmask(v && prefix_less(e, qe)));
+                if (k < nv) ke = !((gmask(v && peq(e, qe)) >> k) & 1u);
+                ce += k;
+                donee = k < kArity;
+            }
         }
     }
-    if (!want_e) ce = cb;
-    for (int L = top; L > 0; L--) {
-        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, A c]
-        const int64_t szl = tree_sz(n, L - 1);
+    if (!want_e) ce = cb, ke = kb;
+    for (int L = top; L > -1; L--) {
+        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, A c]; entry A c is the parent's
+        // entry c, so when the whole node is below q the parent's `known` carries down
+        const int64_t szl = level_sz(L - 1);
         const int64_t bb = kArity * (cb - 1) + 1, be = min((int64_t)kArity * cb, szl);
         const int64_t eb = kArity * (ce - 1) + 1, ee = min((int64_t)kArity * ce, szl);
         const bool vb = cb > 0 && bb + gl < be;
         const bool ve = want_e && ce > 0 && eb + gl < ee;
-        const ulonglong2 xb = tree_entry(m, tv, L - 1, vb ? bb + gl : 0);
-        const ulonglong2 xe = (ce == cb) ? xb : tree_entry(m, tv, L - 1, ve ? eb + gl : 0);
+        const ulonglong2 xb = entry(L - 1, vb ? bb + gl : 0);
+        const ulonglong2 xe = (ce == cb) ? xb : entry(L - 1, ve ? eb + gl : 0);
         const int nb = __popc(gmask(vb)), kb_ = __popc(gmask(vb && prefix_less(xb, qb)));
         const int ne = __popc(gmask(ve)), ke_ = __popc(gmask(ve && prefix_less(xe, qe)));
-        if (L == 1) {
-            if (kb_ < nb) kb = !((gmask(vb && peq(xb, qb)) >> kb_) & 1u);
-            if (ke_ < ne) ke = !((gmask(ve && peq(xe, qe)) >> ke_) & 1u);
-        }
+        if (kb_ < nb) kb = !((gmask(vb && peq(xb, qb)) >> kb_) & 1u);
+        if (ke_ < ne) ke = !((gmask(ve && peq(xe, qe)) >> ke_) & 1u);
         if (cb > 0) cb = bb + kb_;
         if (ce > 0 && want_e) ce = eb + ke_;
     }
-    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
-    const int64_t sz0 = tree_sz(n, 0);
+    // skey8 entries sharing q's prefix past the count widen the final span
+    const int64_t sz8 = (n + 7) / 8;
     auto run_end = [&](int64_t c, bool known, const DKey& q) {
         int64_t b = c;
         for (; !known;) {
-            const bool v = b + gl < sz0;
-            const ulonglong2 k = m.skey[0][v ? b + gl : 0];
+            const bool v = b + gl < sz8;
+            const ulonglong2 k = m.skey8[v ? b + gl : 0];
             const uint32_t same = gmask(v && peq(k, q));
             const int run = __ffs(~same) - 1;
             b += run;
@@ -562,12 +573,13 @@ __device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevel
     };
     const int64_t bbk = run_end(cb, kb, qb);
     const int64_t bek = want_e ? run_end(ce, ke, qe) : 0;
-    // in-block rounds of kArity probes at a shrinking stride, both searches side by side; a probe
-    // both searches make is loaded once
-    int64_t lo_b = cb > 0 ? kFan * (cb - 1) + 1 : 0, hi_b = min(n, kFan * bbk);
-    int64_t lo_e = ce > 0 ? kFan * (ce - 1) + 1 : 0, hi_e = want_e ? min(n, kFan * bek) : 0;
+    // boundaries: rounds of kArity probes at a shrinking stride (one round of 8 consecutive keys
+    // unless a shared-prefix run widened the span), both searches side by side; a probe both
+    // searches make is loaded once
+    int64_t lo_b = cb > 0 ? 8 * (cb - 1) + 1 : 0, hi_b = min(n, 8 * bbk);
+    int64_t lo_e = ce > 0 ? 8 * (ce - 1) + 1 : 0, hi_e = want_e ? min(n, 8 * bek) : 0;
     int64_t sp_b = hi_b - lo_b, sp_e = want_e ? hi_e - lo_e : 0;
-    int64_t st_b = kFan / kArity, st_e = kFan / kArity;
+    int64_t st_b = 1, st_e = 1;
     while (st_b * kArity < sp_b) st_b *= kArity;
     while (st_e * kArity < sp_e) st_e *= kArity;
     bool act_b = sp_b > 0, act_e = sp_e > 0;
@@ -2189,6 +2201,12 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         const int64_t b1l = b1_0 + lane;  // lane q < 16 owns block b1_0 + q
         ulonglong2 sk = make_ulonglong2(0, 0);
         if (lane < kFan / 4 && b1l < n1) sk = m.keys[b1l * kFan];  // sampled key of the block
+        // every 8th boundary of the wave's 16 blocks (128 entries of skey8, two per lane)
+#pragma unroll
+        for (int h8 = 0; h8 < 2; h8++) {
+            const int64_t e8 = b1_0 * (kFan / 8) + h8 * 64 + lane;
+            if (e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
+        }
         int64_t mine = LLONG_MIN;
 #pragma unroll
         for (int q = 0; q < kFan / 4; q++) {
