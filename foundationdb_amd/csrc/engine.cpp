@@ -166,7 +166,7 @@ struct fdbcs_conflict_set {
     bool dma_upload = false;  // FDBCS_UPLOAD=dma: hipMemcpyAsync instead of the k_upload kernel
     int upload_blocks = 32;   // FDBCS_UPLOAD_BLOCKS: workgroups of the k_upload kernel
     int check_version = 2;    // FDBCS_CHECK: read-check kernel (2 LDS-staged fused search, 1 four lookups)
-    int check_grid = 1024;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check
+    int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -391,6 +391,7 @@ void carve_index(MaxLevels& m, ulonglong2* base, int64_t cap) {
         base += idx_level_cap(cap, L);
     }
     m.skey8 = base;  // cap / 8 + 2 entries
+    m.idx_cap = cap;
 }
 
 int64_t index_bytes(int64_t cap) {

@@ -44,6 +44,8 @@ struct MaxLevels {
     const ulonglong2* keys;         // the tier's keys (source of the samples)
     ulonglong2* skey[kIdxLevels];   // [ceil(n / (64 * A^L))]
     ulonglong2* skey8;              // [ceil(n / 8)] prefix of every 8th boundary: the level below skey[0]
+    int64_t idx_cap;                // capacity the levels were carved for: skey[L] = skey[0] + sum of
+                                    // idx_level_cap(idx_cap, l < L), computable without indexing skey[]
 };
 __host__ __device__ inline int64_t idx_level_cap(int64_t cap, int L) {
     int64_t d = 64;

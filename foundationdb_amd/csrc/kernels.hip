@@ -129,6 +129,26 @@ __device__ __forceinline__ int probe_cmp(const Hist& h, int64_t i, const ulonglo
     if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
     return hist_cmp(h, i, htail, q, qtail);  // equal prefixes: length / tail
 }
+// The same with a word-at-a-time tail comparison (one pair of 8-byte words live, not four): keeps
+// the read check's register footprint low; equal 16-byte prefixes are the rare path.
+__device__ __forceinline__ int probe_cmp_lean(const Hist& h, int64_t i, const ulonglong2& k, const uint8_t* htail,
+                                              const DKey& q, const uint8_t* qtail) {
+    if (k.x != q.hi) return k.x < q.hi ? -1 : 1;
+    if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
+    const uint2 lt = h.lt[i];
+    if (lt.x > 16u && q.len > 16u) {
+        const uint8_t* ta = hist_tail(htail, lt.y);
+        const uint8_t* tb = qtail + q.tail;
+        const uint32_t nb = (lt.x < q.len ? lt.x : q.len) - 16u;
+        for (uint32_t o = 0; o < nb; o += 8) {
+            const int vb = (int)(nb - o);
+            const uint64_t msk = vb >= 8 ? ~0ull : ~0ull << (64 - 8 * vb);
+            const uint64_t x = tail_word(ta + o) & msk, y = tail_word(tb + o) & msk;
+            if (x != y) return x < y ? -1 : 1;
+        }
+    }
+    return (lt.x > q.len) - (lt.x < q.len);
+}
 
 // std::lower_bound of q over the n boundaries of a tier, through its search tree: one 16-wide
 // probe per tree level down to a 64-boundary block, then two probes inside the block (about 6
@@ -447,9 +467,8 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
 // Per read two groups of kArity lanes (base tier, delta tier) instead of four.  A short read
 // [k, k + d) meets the same nodes all the way down and the same 64-boundary block, so the end
 // search costs no extra dependent load; each staged level saves one (~0.5 us on a loaded chip).
-constexpr int kCheckThreads = 256;
-constexpr int kCheckReadLanes = 2 * kArity;                   // base group, delta group
-constexpr int kCheckReadsPerBlock = kCheckThreads / kCheckReadLanes;
+constexpr int kCheckThreads = 512;  // 8 waves sharing one LDS copy of the staged levels
+constexpr int kCheckReadsPerBlock = kCheckThreads / (2 * kArity);  // a base group and a delta group per read
 constexpr int kLdsTreeBase = 1536;                            // staged sample keys of the base tier
 constexpr int kLdsTreeDelta = 512;                            // ... of the delta tier (24 + 8 KiB)
 
@@ -474,8 +493,12 @@ struct TreeRef {
     const ulonglong2* lds;
 };
 
-__device__ __forceinline__ ulonglong2 tree_entry(const MaxLevels& m, const TreeRef& t, int L, int64_t i) {
-    return L >= t.lds_lo ? t.lds[t.off[L] + i] : m.skey[L][i];
+// Offset of sample-tree level L from skey[0] (levels are carved back to back, engine.cpp
+// carve_index): no dynamic index into MaxLevels::skey[], which would put the struct in scratch.
+__device__ __forceinline__ int64_t skey_offset(const MaxLevels& m, int L) {
+    int64_t off = 0;
+    for (int l = 0; l < L; l++) off += idx_level_cap(m.idx_cap, l);
+    return off;
 }
 
 // Levels of a tier to stage: from the top down while they fit `budget` entries; fills off[] and
@@ -512,10 +535,15 @@ __device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevel
     const int64_t n = tv.n;
     if (n <= 0) return;
     auto peq = [](const ulonglong2& k, const DKey& q) { return k.x == q.hi && k.y == q.lo; };
-    // level L >= 0: sample tree; level -1: skey8
-    auto entry = [&](int L, int64_t i) { return L >= 0 ? tree_entry(m, tv, L, i) : m.skey8[i]; };
-    auto level_sz = [&](int L) { return L >= 0 ? tree_sz(n, L) : (n + 7) / 8; };
+    // level L >= 0: sample tree (staged levels from LDS); level -1: skey8.  `off` tracks the global
+    // offset of the level being read as the descent goes down.
     const int top = tv.top;
+    int64_t off = skey_offset(m, top);
+    auto entry = [&](int L, int64_t i) {
+        if (L < 0) return m.skey8[i];
+        return L >= tv.lds_lo ? tv.lds[tv.off[L] + i] : m.skey[0][off + i];
+    };
+    auto level_sz = [&](int L) { return L >= 0 ? tree_sz(n, L) : (n + 7) / 8; };
     int64_t cb = 0, ce = 0;
     bool kb = true, ke = true;  // known: the first entry not below q has another prefix (true past the end)
     {
@@ -544,6 +572,7 @@ __device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevel
         // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, A c]; entry A c is the parent's
         // entry c, so when the whole node is below q the parent's `known` carries down
         const int64_t szl = level_sz(L - 1);
+        if (L - 1 >= 0) off -= idx_level_cap(m.idx_cap, L - 1);
         const int64_t bb = kArity * (cb - 1) + 1, be = min((int64_t)kArity * cb, szl);
         const int64_t eb = kArity * (ce - 1) + 1, ee = min((int64_t)kArity * ce, szl);
         const bool vb = cb > 0 && bb + gl < be;
@@ -591,8 +620,8 @@ __device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevel
         const ulonglong2 xb = h.key[vb ? pb : 0];
         const ulonglong2 xe = (vb && ve && pe == pb) ? xb : h.key[ve ? pe : 0];
         int rb = 1, re = 1;
-        if (vb) rb = probe_cmp(h, pb, xb, htail, qb, qtail);
-        if (ve) re = probe_cmp(h, pe, xe, htail, qe, qtail);
+        if (vb) rb = probe_cmp_lean(h, pb, xb, htail, qb, qtail);
+        if (ve) re = probe_cmp_lean(h, pe, xe, htail, qe, qtail);
         if (act_b) {
             const int nv = __popc(gmask(vb)), cnt = __popc(gmask(vb && rb < 0));
             const int stop = __shfl(rb, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
@@ -622,10 +651,17 @@ struct CheckReads2 {
     unsigned long long* trace;
 };
 
-__global__ __launch_bounds__(kCheckThreads) void k_check_reads2(BatchDev b, CheckReads2 c) {
+// The tier a wave searches is wave-uniform (waves [0, 4) the base tier, [4, 8) the delta tier, for
+// the same 32 reads), so the tier's pointers and tree shape stay in scalar registers; the two
+// verdicts meet in LDS.  Each wave's 8 lane groups take 8 reads.
+constexpr int kCheckWavesPerTier = kCheckThreads / 64 / 2;
+
+__global__ __launch_bounds__(kCheckThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void k_check_reads2(BatchDev b, CheckReads2 c) {
     __shared__ ulonglong2 s_tree[kLdsTreeBase + kLdsTreeDelta];
     __shared__ int s_off[2][kIdxLevels];
     __shared__ int s_lo[2];
+    __shared__ uint8_t s_conf[2][kCheckReadsPerBlock];
     if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
     const int64_t nt[2] = {*c.base.n, *c.delta.n};
     const int top[2] = {tree_top(nt[0]), tree_top(nt[1])};
@@ -638,18 +674,20 @@ __global__ __launch_bounds__(kCheckThreads) void k_check_reads2(BatchDev b, Chec
         const MaxLevels& m = t ? c.delta.m : c.base.m;
         for (int L = s_lo[t]; L <= top[t]; L++) {
             const int64_t z = tree_sz(nt[t], L);
-            for (int64_t i = threadIdx.x; i < z; i += blockDim.x) s_tree[s_off[t][L] + i] = m.skey[L][i];
+            const ulonglong2* src = m.skey[0] + skey_offset(m, L);
+            for (int64_t i = threadIdx.x; i < z; i += blockDim.x) s_tree[s_off[t][L] + i] = src[i];
         }
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int grp = (threadIdx.x / kArity) & 1;  // 0: base tier, 1: delta tier
-    const int lead = lane & ~(kCheckReadLanes - 1);
-    const Tier& tier = grp ? c.delta : c.base;
-    const TreeRef tv{nt[grp], top[grp], s_lo[grp], s_off[grp], s_tree};
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = wave >= kCheckWavesPerTier ? 1 : 0;  // wave-uniform tier
+    const Tier tier = t ? c.delta : c.base;
+    const TreeRef tv{nt[t], top[t], s_lo[t], s_off[t], s_tree};
+    const int slot = (wave - t * kCheckWavesPerTier) * (64 / kArity) + ((threadIdx.x & 63) / kArity);
+    const bool leader = (threadIdx.x & (kArity - 1)) == 0;
     for (int64_t r0 = (int64_t)blockIdx.x * kCheckReadsPerBlock; r0 < b.R;
          r0 += (int64_t)gridDim.x * kCheckReadsPerBlock) {
-        const int64_t r = r0 + threadIdx.x / kCheckReadLanes;
+        const int64_t r = r0 + slot;
         const bool live = r < b.R;
         const int rr = live ? (int)r : 0;
         const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
@@ -659,16 +697,18 @@ __global__ __launch_bounds__(kCheckThreads) void k_check_reads2(BatchDev b, Chec
         bool eq = false;
         if (live) group_lower_bound2(tier.h, tier.m, tv, kb, ke, !degenerate, c.htail, b.tail, lb, eq, le);
         bool conf = false;
-        if (live && (threadIdx.x & (kArity - 1)) == 0 && (grp == 0 || tv.n > 0))
-            conf = tier_conflict(tier.h, tier.m, grp == 0 ? tier.hdr : kHole, lb, eq, le, degenerate, snap);
-        const int dconf = __shfl((int)conf, lead + kArity, 64);
-        if (live && lane == lead) {
-            conf = conf || dconf;
-            c.rconf[r] = conf ? 1 : 0;
-            if (conf) c.hist_conf[b.rowner[r]] = 1;
+        if (live && leader && (t == 0 || tv.n > 0))
+            conf = tier_conflict(tier.h, tier.m, t == 0 ? tier.hdr : kHole, lb, eq, le, degenerate, snap);
+        if (leader) s_conf[t][slot] = conf ? 1 : 0;
+        __syncthreads();
+        if (threadIdx.x < kCheckReadsPerBlock && r0 + threadIdx.x < b.R) {
+            const int64_t rw = r0 + threadIdx.x;
+            const bool cf = s_conf[0][threadIdx.x] | s_conf[1][threadIdx.x];
+            c.rconf[rw] = cf ? 1 : 0;
+            if (cf) c.hist_conf[b.rowner[rw]] = 1;
         }
+        __syncthreads();
     }
-    __syncthreads();
     if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
 
