@@ -136,6 +136,7 @@ __device__ __forceinline__ int probe_cmp_lean(const Hist& h, int64_t i, const ul
     if (k.x != q.hi) return k.x < q.hi ? -1 : 1;
     if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
     const uint2 lt = h.lt[i];
+#if defined(__HIP_DEVICE_COMPILE__)
     if (lt.x > 16u && q.len > 16u) {
         const uint8_t* ta = hist_tail(htail, lt.y);
         const uint8_t* tb = qtail + q.tail;
@@ -147,6 +148,7 @@ __device__ __forceinline__ int probe_cmp_lean(const Hist& h, int64_t i, const ul
             if (x != y) return x < y ? -1 : 1;
         }
     }
+#endif
     return (lt.x > q.len) - (lt.x < q.len);
 }
 
