@@ -469,8 +469,6 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
 // Per read two groups of kArity lanes (base tier, delta tier) instead of four.  A short read
 // [k, k + d) meets the same nodes all the way down and the same 64-boundary block, so the end
 // search costs no extra dependent load; each staged level saves one (~0.5 us on a loaded chip).
-constexpr int kCheckThreads = 512;  // 8 waves sharing one LDS copy of the staged levels
-constexpr int kCheckReadsPerBlock = kCheckThreads / (2 * kArity);  // a base group and a delta group per read
 constexpr int kLdsTreeBase = 1536;                            // staged sample keys of the base tier
 constexpr int kLdsTreeDelta = 512;                            // ... of the delta tier (24 + 8 KiB)
 
@@ -656,14 +654,14 @@ struct CheckReads2 {
 // The tier a wave searches is wave-uniform (waves [0, 4) the base tier, [4, 8) the delta tier, for
 // the same 32 reads), so the tier's pointers and tree shape stay in scalar registers; the two
 // verdicts meet in LDS.  Each wave's 8 lane groups take 8 reads.
-constexpr int kCheckWavesPerTier = kCheckThreads / 64 / 2;
-
-__global__ __launch_bounds__(kCheckThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void k_check_reads2(BatchDev b, CheckReads2 c) {
+template <int NT>
+__device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckReads2& c) {
+    constexpr int kReadsPerBlock = NT / (2 * kArity);
+    constexpr int kWavesPerTier = NT / 64 / 2;
     __shared__ ulonglong2 s_tree[kLdsTreeBase + kLdsTreeDelta];
     __shared__ int s_off[2][kIdxLevels];
     __shared__ int s_lo[2];
-    __shared__ uint8_t s_conf[2][kCheckReadsPerBlock];
+    __shared__ uint8_t s_conf[2][kReadsPerBlock];
     if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
     const int64_t nt[2] = {*c.base.n, *c.delta.n};
     const int top[2] = {tree_top(nt[0]), tree_top(nt[1])};
@@ -682,13 +680,13 @@ void k_check_reads2(BatchDev b, CheckReads2 c) {
     }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t = wave >= kCheckWavesPerTier ? 1 : 0;  // wave-uniform tier
+    const int t = wave >= kWavesPerTier ? 1 : 0;  // wave-uniform tier
     const Tier tier = t ? c.delta : c.base;
     const TreeRef tv{nt[t], top[t], s_lo[t], s_off[t], s_tree};
-    const int slot = (wave - t * kCheckWavesPerTier) * (64 / kArity) + ((threadIdx.x & 63) / kArity);
+    const int slot = (wave - t * kWavesPerTier) * (64 / kArity) + ((threadIdx.x & 63) / kArity);
     const bool leader = (threadIdx.x & (kArity - 1)) == 0;
-    for (int64_t r0 = (int64_t)blockIdx.x * kCheckReadsPerBlock; r0 < b.R;
-         r0 += (int64_t)gridDim.x * kCheckReadsPerBlock) {
+    for (int64_t r0 = (int64_t)blockIdx.x * kReadsPerBlock; r0 < b.R;
+         r0 += (int64_t)gridDim.x * kReadsPerBlock) {
         const int64_t r = r0 + slot;
         const bool live = r < b.R;
         const int rr = live ? (int)r : 0;
@@ -703,7 +701,7 @@ void k_check_reads2(BatchDev b, CheckReads2 c) {
             conf = tier_conflict(tier.h, tier.m, t == 0 ? tier.hdr : kHole, lb, eq, le, degenerate, snap);
         if (leader) s_conf[t][slot] = conf ? 1 : 0;
         __syncthreads();
-        if (threadIdx.x < kCheckReadsPerBlock && r0 + threadIdx.x < b.R) {
+        if (threadIdx.x < kReadsPerBlock && r0 + threadIdx.x < b.R) {
             const int64_t rw = r0 + threadIdx.x;
             const bool cf = s_conf[0][threadIdx.x] | s_conf[1][threadIdx.x];
             c.rconf[rw] = cf ? 1 : 0;
@@ -713,6 +711,12 @@ void k_check_reads2(BatchDev b, CheckReads2 c) {
     }
     if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
+
+// Variants (FDBCS_CHECK): 2 = 512 threads, 3 = 256 threads, 4 = 512 threads at 8 waves per SIMD.
+__global__ __launch_bounds__(512) void k_check_reads2(BatchDev b, CheckReads2 c) { check_reads_body<512>(b, c); }
+__global__ __launch_bounds__(256) void k_check_reads3(BatchDev b, CheckReads2 c) { check_reads_body<256>(b, c); }
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void k_check_reads4(BatchDev b, CheckReads2 c) { check_reads_body<512>(b, c); }
 
 // ------------------------------------------------------------------ D.Sort
 
@@ -1240,9 +1244,16 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
         return;
     }
     CheckReads2 c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
-    int64_t grid = ((int64_t)b.R + kCheckReadsPerBlock - 1) / kCheckReadsPerBlock;
+    const int nt = check_version == 3 ? 256 : 512;
+    const int per_block = nt / (2 * kArity);  // a base group and a delta group per read
+    int64_t grid = ((int64_t)b.R + per_block - 1) / per_block;
     grid = grid > check_grid_cap ? check_grid_cap : grid;
-    hipLaunchKernelGGL(k_check_reads2, dim3((unsigned)grid), dim3(kCheckThreads), 0, s, b, c);
+    if (check_version == 3)
+        hipLaunchKernelGGL(k_check_reads3, dim3((unsigned)grid), dim3(256), 0, s, b, c);
+    else if (check_version == 4)
+        hipLaunchKernelGGL(k_check_reads4, dim3((unsigned)grid), dim3(512), 0, s, b, c);
+    else
+        hipLaunchKernelGGL(k_check_reads2, dim3((unsigned)grid), dim3(512), 0, s, b, c);
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
