@@ -654,7 +654,10 @@ struct CheckReads2 {
 // The tier a wave searches is wave-uniform (waves [0, 4) the base tier, [4, 8) the delta tier, for
 // the same 32 reads), so the tier's pointers and tree shape stay in scalar registers; the two
 // verdicts meet in LDS.  Each wave's 8 lane groups take 8 reads.
-template <int NT>
+// BYWAVE: the tier a wave searches is wave-uniform (waves [0, NT/128) the base tier, the rest the
+// delta tier, for the same reads; the two verdicts meet in LDS), else each read's base group and
+// delta group sit side by side in one wave and meet by a shuffle.
+template <int NT, bool BYWAVE>
 __device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckReads2& c) {
     constexpr int kReadsPerBlock = NT / (2 * kArity);
     constexpr int kWavesPerTier = NT / 64 / 2;
@@ -679,12 +682,19 @@ __device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckR
         }
     }
     __syncthreads();
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t = wave >= kWavesPerTier ? 1 : 0;  // wave-uniform tier
-    const Tier tier = t ? c.delta : c.base;
-    const TreeRef tv{nt[t], top[t], s_lo[t], s_off[t], s_tree};
-    const int slot = (wave - t * kWavesPerTier) * (64 / kArity) + ((threadIdx.x & 63) / kArity);
+    const int lane = threadIdx.x & 63;
     const bool leader = (threadIdx.x & (kArity - 1)) == 0;
+    int t, slot;
+    if (BYWAVE) {
+        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        t = wave >= kWavesPerTier ? 1 : 0;
+        slot = (wave - t * kWavesPerTier) * (64 / kArity) + (lane / kArity);
+    } else {
+        t = (threadIdx.x / kArity) & 1;
+        slot = threadIdx.x / (2 * kArity);
+    }
+    const Tier& tier = t ? c.delta : c.base;
+    const TreeRef tv{nt[t], top[t], s_lo[t], s_off[t], s_tree};
     for (int64_t r0 = (int64_t)blockIdx.x * kReadsPerBlock; r0 < b.R;
          r0 += (int64_t)gridDim.x * kReadsPerBlock) {
         const int64_t r = r0 + slot;
@@ -699,24 +709,34 @@ __device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckR
         bool conf = false;
         if (live && leader && (t == 0 || tv.n > 0))
             conf = tier_conflict(tier.h, tier.m, t == 0 ? tier.hdr : kHole, lb, eq, le, degenerate, snap);
-        if (leader) s_conf[t][slot] = conf ? 1 : 0;
-        __syncthreads();
-        if (threadIdx.x < kReadsPerBlock && r0 + threadIdx.x < b.R) {
-            const int64_t rw = r0 + threadIdx.x;
-            const bool cf = s_conf[0][threadIdx.x] | s_conf[1][threadIdx.x];
-            c.rconf[rw] = cf ? 1 : 0;
-            if (cf) c.hist_conf[b.rowner[rw]] = 1;
+        if (BYWAVE) {
+            if (leader) s_conf[t][slot] = conf ? 1 : 0;
+            __syncthreads();
+            if (threadIdx.x < kReadsPerBlock && r0 + threadIdx.x < b.R) {
+                const int64_t rw = r0 + threadIdx.x;
+                const bool cf = s_conf[0][threadIdx.x] | s_conf[1][threadIdx.x];
+                c.rconf[rw] = cf ? 1 : 0;
+                if (cf) c.hist_conf[b.rowner[rw]] = 1;
+            }
+            __syncthreads();
+        } else {
+            const int lead = lane & ~(2 * kArity - 1);
+            const int dconf = __shfl((int)conf, lead + kArity, 64);
+            if (live && lane == lead) {
+                conf = conf || dconf;
+                c.rconf[r] = conf ? 1 : 0;
+                if (conf) c.hist_conf[b.rowner[r]] = 1;
+            }
         }
-        __syncthreads();
     }
     if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
 
-// Variants (FDBCS_CHECK): 2 = 512 threads, 3 = 256 threads, 4 = 512 threads at 8 waves per SIMD.
-__global__ __launch_bounds__(512) void k_check_reads2(BatchDev b, CheckReads2 c) { check_reads_body<512>(b, c); }
-__global__ __launch_bounds__(256) void k_check_reads3(BatchDev b, CheckReads2 c) { check_reads_body<256>(b, c); }
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void k_check_reads4(BatchDev b, CheckReads2 c) { check_reads_body<512>(b, c); }
+// Variants (FDBCS_CHECK): 2 = base and delta groups of a read in one wave, 256 threads (default);
+// 3 = the same, 512 threads; 4 = wave-uniform tiers, 512 threads.
+__global__ __launch_bounds__(256) void k_check_reads2(BatchDev b, CheckReads2 c) { check_reads_body<256, false>(b, c); }
+__global__ __launch_bounds__(512) void k_check_reads3(BatchDev b, CheckReads2 c) { check_reads_body<512, false>(b, c); }
+__global__ __launch_bounds__(512) void k_check_reads4(BatchDev b, CheckReads2 c) { check_reads_body<512, true>(b, c); }
 
 // ------------------------------------------------------------------ D.Sort
 
@@ -1244,16 +1264,16 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
         return;
     }
     CheckReads2 c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
-    const int nt = check_version == 3 ? 256 : 512;
+    const int nt = check_version == 2 ? 256 : 512;
     const int per_block = nt / (2 * kArity);  // a base group and a delta group per read
     int64_t grid = ((int64_t)b.R + per_block - 1) / per_block;
     grid = grid > check_grid_cap ? check_grid_cap : grid;
     if (check_version == 3)
-        hipLaunchKernelGGL(k_check_reads3, dim3((unsigned)grid), dim3(256), 0, s, b, c);
+        hipLaunchKernelGGL(k_check_reads3, dim3((unsigned)grid), dim3(512), 0, s, b, c);
     else if (check_version == 4)
         hipLaunchKernelGGL(k_check_reads4, dim3((unsigned)grid), dim3(512), 0, s, b, c);
     else
-        hipLaunchKernelGGL(k_check_reads2, dim3((unsigned)grid), dim3(512), 0, s, b, c);
+        hipLaunchKernelGGL(k_check_reads2, dim3((unsigned)grid), dim3(256), 0, s, b, c);
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,

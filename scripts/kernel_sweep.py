@@ -22,7 +22,7 @@ def one(workload):
         kb, ko, vers = W.c4_history(p, seed=1000, start_version=start)
         mk = lambda rng, now: W.c4_batch(p, rng, now)
     else:
-        p = W.C2Params()
+        p = W.C2Params(history=int(os.environ.get("HISTORY", 5_000_000)), txns=int(os.environ.get("TXNS", 5000)))
         kb, ko, vers = W.c2_history(p, seed=1, start_version=start)
         z = W.ZipfGenerator(1_000_000, 0.99) if workload == "c3" else None
         mk = (lambda rng, now: W.c3_batch(p, rng, now, z)) if z else (lambda rng, now: W.c2_batch(p, rng, now))
@@ -52,6 +52,7 @@ if __name__ == "__main__":
     workload = os.environ.get("WORKLOAD", "c2")
     for spec in sys.argv[1:]:
         env = dict(os.environ)
+        env.pop("WORKLOAD", None)
         for kv in spec.split():
             if "=" in kv:
                 k, v = kv.split("=", 1)
@@ -61,4 +62,5 @@ if __name__ == "__main__":
         if r.returncode:
             print(spec, "FAILED", r.stderr[-2000:], flush=True)
             sys.exit(r.returncode)
+        w = env.get("WORKLOAD_OVERRIDE", workload)
         print(f"{workload} {spec:40s} check us: {json.loads(r.stdout.strip().splitlines()[-1])}", flush=True)
