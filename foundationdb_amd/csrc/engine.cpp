@@ -349,6 +349,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     w.cap_R = R;
     // the epilogue of every batch re-zeroes these for the batch after next; start them zeroed
     HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
+    HIPOK(hipMemsetAsync(w.rconf, 0, R, cs->stream));
     HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
     HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 2048, cs->stream));
     HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 2048, cs->stream));
@@ -742,7 +743,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
-    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(4, std::max(1, atoi(v)));
+    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -1570,6 +1571,7 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     (void)hipEventDestroy(e1);
     // the check leaves per-transaction conflict flags the next batch on this workspace expects zeroed
     HIPOK(hipMemsetAsync(w.hist_conf, 0, w.cap_T, cs->stream));
+    HIPOK(hipMemsetAsync(w.rconf, 0, w.cap_R, cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
     return FDBCS_OK;
 }

@@ -20,6 +20,8 @@
 
 namespace fdbcs {
 
+thread_local LaunchList* t_record = nullptr;
+
 // ------------------------------------------------------------------ helpers
 
 // History tails are 8-byte aligned and Hist::lt.y counts 8-byte units (32 GiB of tail arena per
@@ -286,6 +288,83 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
         const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
         const bool v = base + gl < end;
         const ulonglong2 e = m.skey[L - 1][v ? base + gl : 0];
+        const int k = __popc(gmask(v && prefix_less(e, q)));
+        if (L == 1 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+        c = base + k;
+    }
+    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
+    int64_t b = c;
+    for (; !bknown;) {
+        const bool v = b + gl < sz[0];
+        const ulonglong2 k = m.skey[0][v ? b + gl : 0];
+        const uint32_t same = gmask(v && k.x == q.hi && k.y == q.lo);
+        const int run = __ffs(~same) - 1;  // leading lanes equal to q's prefix
+        b += run;
+        if (run < kArity) break;
+    }
+    int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
+    const int64_t hi = min(n, kFan * b);
+    // lower_bound in [lo, lo + span]: rounds of kArity probes at a shrinking stride.  span <= 64
+    // normally; a long run of boundaries sharing q's 16-byte prefix (tuple keys) only starts the
+    // stride higher, so the lanes still compare tails side by side.
+    int64_t span = hi - lo;
+    int64_t stride0 = kFan / kArity;
+    while (stride0 * kArity < span) stride0 *= kArity;
+    bool eq_cand = false;  // cmp == 0 at the last probe that stopped a count (the answer, if < hi)
+    for (int64_t stride = stride0; span > 0; stride = stride > kArity ? stride / kArity : 1) {
+        const int64_t p = lo + stride * (gl + 1) - 1;
+        const bool v = stride * (gl + 1) <= span && p < hi;
+        int r = 1;
+        if (v) r = probe_cmp(h, p, h.key[p], htail, q, qtail);
+        const uint32_t valid = gmask(v);
+        const int cnt = __popc(gmask(v && r < 0));
+        const int stop = __shfl(r, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
+        if (cnt < __popc(valid)) eq_cand = stop == 0;  // lane cnt probed a key >= q
+        lo += stride * cnt;
+        span = cnt < __popc(valid) ? stride - 1 : span - stride * cnt;
+        if (stride == 1) break;
+    }
+    if (lo < hi) eq = eq_cand;
+    return lo;
+}
+
+// group_lower_bound with the levels [lds_lo, top] of the sample tree read from LDS (`lds`, level L
+// at offset off[L]); the caller keeps lds_lo wave-uniform so the two paths never diverge in a wave.
+__device__ __forceinline__ int64_t group_lower_bound_lds(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
+                                                         const uint8_t* htail, const uint8_t* qtail, bool& eq,
+                                                         const ulonglong2* lds, const int* off, int lds_lo) {
+    const int gl = threadIdx.x & (kArity - 1);
+    const int g0 = threadIdx.x & 63 & ~(kArity - 1);  // first lane of the group
+    eq = false;
+    if (n <= 0) return 0;
+    int64_t sz[kIdxLevels];
+    sz[0] = (n + kFan - 1) / kFan;
+#pragma unroll
+    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + kArity - 1) / kArity;
+    int top = 0;
+    while (top + 1 < kIdxLevels && sz[top] > kArity) top++;
+    // c = number of entries of level `top` whose prefix is < q.  When level 0 is probed, also learn
+    // whether the first sample not below q shares q's prefix (`bknown`: it does not).
+    auto prefix_eq = [&](const ulonglong2& k) { return k.x == q.hi && k.y == q.lo; };
+    int64_t c = 0;
+    bool bknown = false;
+    for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
+        const bool v = j0 + gl < sz[top];
+        const int64_t ej = v ? j0 + gl : 0;
+        const ulonglong2 e = top >= lds_lo ? lds[off[top] + ej] : m.skey[top][ej];
+        const int k = __popc(gmask(v && prefix_less(e, q)));
+        if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+        c += k;
+        if (k < kArity) break;
+    }
+    for (int L = top; L > 0; L--) {
+        if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
+        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, Ac]
+        const int64_t base = (int64_t)kArity * (c - 1) + 1;
+        const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
+        const bool v = base + gl < end;
+        const int64_t ej = v ? base + gl : 0;
+        const ulonglong2 e = L - 1 >= lds_lo ? lds[off[L - 1] + ej] : m.skey[L - 1][ej];
         const int k = __popc(gmask(v && prefix_less(e, q)));
         if (L == 1 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
         c = base + k;
@@ -737,6 +816,66 @@ __device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckR
 __global__ __launch_bounds__(256) void k_check_reads2(BatchDev b, CheckReads2 c) { check_reads_body<256, false>(b, c); }
 __global__ __launch_bounds__(512) void k_check_reads3(BatchDev b, CheckReads2 c) { check_reads_body<512, false>(b, c); }
 __global__ __launch_bounds__(512) void k_check_reads4(BatchDev b, CheckReads2 c) { check_reads_body<512, true>(b, c); }
+
+// Variant 5: the v1 shape (one lane group per key: a read's begin and end, in the base and in the
+// delta tier, 32 lanes) with the tiers' top sample-tree levels staged in LDS and the tier
+// wave-uniform (even waves search the base tier, odd waves the delta tier, for the same four
+// reads each), so the LDS-or-global choice never diverges inside a wave.  Either tier's wave sets
+// the conflict flags (rconf is zeroed by the previous epilogue on this workspace).
+template <int NT>
+__device__ __forceinline__ void check_reads_v5(const BatchDev& b, const CheckReads2& c) {
+    constexpr int kReadsPerBlock = NT / 64 / 2 * 4;
+    __shared__ ulonglong2 s_tree[kLdsTreeBase + kLdsTreeDelta];
+    __shared__ int s_off[2][kIdxLevels];
+    __shared__ int s_lo[2];
+    if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
+    const int64_t nt[2] = {*c.base.n, *c.delta.n};
+    const int top[2] = {tree_top(nt[0]), tree_top(nt[1])};
+    if (threadIdx.x < 2) {
+        const int t = threadIdx.x;
+        s_lo[t] = plan_stage(nt[t], top[t], t ? kLdsTreeDelta : kLdsTreeBase, t ? kLdsTreeBase : 0, s_off[t]);
+    }
+    __syncthreads();
+    for (int t = 0; t < 2; t++) {
+        const MaxLevels& m = t ? c.delta.m : c.base.m;
+        for (int L = s_lo[t]; L <= top[t]; L++) {
+            const int64_t z = tree_sz(nt[t], L);
+            const ulonglong2* src = m.skey[0] + skey_offset(m, L);
+            for (int64_t i = threadIdx.x; i < z; i += blockDim.x) s_tree[s_off[t][L] + i] = src[i];
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = wave & 1;
+    const Tier& tier = t ? c.delta : c.base;
+    const int64_t n = nt[t];
+    const int lds_lo = s_lo[t];
+    const int slot = (wave >> 1) * 4 + lane / (2 * kArity);  // this wave's 4 reads
+    const bool is_end = (lane / kArity) & 1;
+    for (int64_t r0 = (int64_t)blockIdx.x * kReadsPerBlock; r0 < b.R; r0 += (int64_t)gridDim.x * kReadsPerBlock) {
+        const int64_t r = r0 + slot;
+        const bool live = r < b.R;
+        const int rr = live ? (int)r : 0;
+        const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+        const int64_t snap = b.snap[b.rowner[rr]];
+        const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+        int64_t lb = 0;
+        bool eq = false;
+        if (live && n > 0 && !(is_end && degenerate))
+            lb = group_lower_bound_lds(tier.h, tier.m, n, is_end ? ke : kb, c.htail, b.tail, eq, s_tree, s_off[t],
+                                       lds_lo);
+        const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // begin groups take their end's position
+        if (live && !is_end && (lane & (kArity - 1)) == 0 && (t == 0 || n > 0)) {
+            if (tier_conflict(tier.h, tier.m, t == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
+                c.rconf[r] = 1;
+                c.hist_conf[b.rowner[r]] = 1;
+            }
+        }
+    }
+    if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
+}
+__global__ __launch_bounds__(256) void k_check_reads5(BatchDev b, CheckReads2 c) { check_reads_v5<256>(b, c); }
 
 // ------------------------------------------------------------------ D.Sort
 
@@ -1251,7 +1390,7 @@ void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_t
     c.srank = w.srank;
     c.trace = w.trace;
     const int grid = c.n_slice * ((c.S + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_sample, dim3(grid), dim3(kBlock), 0, s, b, c);
+    fdb_launch(k_sample, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
@@ -1260,7 +1399,7 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
     if (check_version == 1) {  // FDBCS_CHECK=1: four independent lookups per read, no LDS staging
         CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
         const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
+        fdb_launch(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
         return;
     }
     CheckReads2 c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
@@ -1268,12 +1407,17 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
     const int per_block = nt / (2 * kArity);  // a base group and a delta group per read
     int64_t grid = ((int64_t)b.R + per_block - 1) / per_block;
     grid = grid > check_grid_cap ? check_grid_cap : grid;
+    if (check_version == 5) {
+        const int64_t g5 = ((int64_t)b.R + 7) / 8;  // 256 threads: 2 wave pairs x 4 reads
+        fdb_launch(k_check_reads5, dim3((unsigned)(g5 > check_grid_cap ? check_grid_cap : g5)), dim3(256), 0, s, b, c);
+        return;
+    }
     if (check_version == 3)
-        hipLaunchKernelGGL(k_check_reads3, dim3((unsigned)grid), dim3(512), 0, s, b, c);
+        fdb_launch(k_check_reads3, dim3((unsigned)grid), dim3(512), 0, s, b, c);
     else if (check_version == 4)
-        hipLaunchKernelGGL(k_check_reads4, dim3((unsigned)grid), dim3(512), 0, s, b, c);
+        fdb_launch(k_check_reads4, dim3((unsigned)grid), dim3(512), 0, s, b, c);
     else
-        hipLaunchKernelGGL(k_check_reads2, dim3((unsigned)grid), dim3(256), 0, s, b, c);
+        fdb_launch(k_check_reads2, dim3((unsigned)grid), dim3(256), 0, s, b, c);
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
@@ -1284,15 +1428,15 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
     const int nb = sort_buckets(E, bucket_target);
     const int grid = (E + kBlock - 1) / kBlock;
     const int S = nb > 1 ? sample_count(E, nb, sample_per) : 0;
-    hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
+    fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
+    fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
-    if (sort_begin) (void)hipEventRecord(sort_begin, s);
+    fdb_event(LaunchList::kTimingRecord, sort_begin, s);
     if (alg == 1)
-        hipLaunchKernelGGL(k_bucket_sort<1>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        fdb_launch(k_bucket_sort<1>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
     else
-        hipLaunchKernelGGL(k_bucket_sort<0>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
-    if (sort_end) (void)hipEventRecord(sort_end, s);
+        fdb_launch(k_bucket_sort<0>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    fdb_event(LaunchList::kTimingRecord, sort_end, s);
 }
 
 // ------------------------------------------------------------------ positions
@@ -1353,7 +1497,7 @@ void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int s
     BatchScalars* sc = w.bsc;
     const int E = 2 * (b.R + b.W);
     if (E == 0) return;
-    hipLaunchKernelGGL(k_validate_sort, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf],
+    fdb_launch(k_validate_sort, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf],
                        w.pos, w.pmeta, E, b.tail, sc);
 }
 
@@ -1470,7 +1614,7 @@ void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     launch_scan<2>(s, EdgePairScan{w, b.R, G}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
         const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
-        hipLaunchKernelGGL(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
+        fdb_launch(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
     }
 }
 
@@ -1734,8 +1878,8 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
     if (b.T == 0) return;
     // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
     const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
-    hipLaunchKernelGGL(k_resolve, dim3(grid), dim3(kWG), (size_t)b.T, s, b, w, verdict_out);
-    if (b.R && report) hipLaunchKernelGGL(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
+    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (size_t)b.T, s, b, w, verdict_out);
+    if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
 // ------------------------------------------------------------------ D.Combine
@@ -2037,18 +2181,18 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
                   hipEvent_t copy_begin, hipEvent_t copy_end) {
     const int Wn = b.W > 0 ? b.W : 1;
-    hipLaunchKernelGGL(k_seg_search, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
+    fdb_launch(k_seg_search, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
                        htail, sc,
                        &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
                    w.scan[kScanSegSum]);
-    if (copy_begin) (void)hipEventRecord(copy_begin, s);
+    fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{b, w.pmeta, w.seg_b, w.seg_e, w.seg_tlen, w.seg_vend, w.seg_endins, htail, sc, now};
-    hipLaunchKernelGGL((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile)), dim3(kBlock), 0,
+    fdb_launch((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile)), dim3(kBlock), 0,
                        s, batch_segs(w), src,
                        dst, &sc->nd, &sc->n_segments, ins);
-    if (copy_end) (void)hipEventRecord(copy_end, s);
+    fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -2133,17 +2277,17 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
                     int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end) {
     int64_t blocks = (kArity * delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
+    fdb_launch(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
                        &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n);
     const Segs g{w.c_lo, w.c_hi, w.c_rem, w.c_ins, w.tile_first};
     const TierIO io{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem};
     launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
                    w.scan[kScanCompact]);
-    if (copy_begin) (void)hipEventRecord(copy_begin, s);
-    hipLaunchKernelGGL((k_merge_copy<CompactIns, kBaseTile>), dim3(copy_tiles(grid_hint_n, kBaseTile)), dim3(kBlock), 0,
+    fdb_event(LaunchList::kTimingRecord, copy_begin, s);
+    fdb_launch((k_merge_copy<CompactIns, kBaseTile>), dim3(copy_tiles(grid_hint_n, kBaseTile)), dim3(kBlock), 0,
                        s, g, base, dst,
                        &sc->n, &sc->nd_next, CompactIns{delta, w.c_val, w.c_ins});
-    if (copy_end) (void)hipEventRecord(copy_end, s);
+    fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 
 // ------------------------------------------------------------------ D.RemoveBefore
@@ -2237,6 +2381,8 @@ struct Epilogue {
     int compacted, gc_ran;
     uint8_t* zero8;  // hist_conf
     int64_t zero8_n;
+    uint8_t* zero8r;  // rconf (read-check variants that only set flags)
+    int64_t zero8r_n;
     int32_t* zero32b;  // ecur
     int64_t zero32_n;
     uint64_t* zero64;  // scan arena
@@ -2327,6 +2473,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     };
     for (int64_t t = tid; t < ep.T; t += stride) ep.verdict_dev[t] = verdict(t);
     for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
+    for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
     for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
     for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
     for (int64_t i = tid; i < kMaxBuckets; i += stride) {
@@ -2392,7 +2539,7 @@ void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t by
     const int64_t n16 = (bytes + 15) / 16;
     int64_t blocks = (n16 + kUploadUnroll * kBlock - 1) / (kUploadUnroll * kBlock);
     blocks = blocks < 1 ? 1 : (blocks > max_blocks ? max_blocks : blocks);
-    hipLaunchKernelGGL(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)host_mapped, (uint4*)dst,
+    fdb_launch(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)host_mapped, (uint4*)dst,
                        n16);
 }
 
@@ -2410,10 +2557,10 @@ static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
 
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
                      int64_t grid_hint_n) {
-    hipLaunchKernelGGL(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
+    fdb_launch(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
     Epilogue ep{};
     ep.trace = nullptr;
-    hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, n, ep);
+    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, n, ep);
 }
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
@@ -2432,6 +2579,8 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.gc_ran = gc_ran;
     ep.zero8 = w.hist_conf;
     ep.zero8_n = w.cap_T;
+    ep.zero8r = w.rconf;
+    ep.zero8r_n = w.cap_R;
     ep.zero32b = w.ecur;
     ep.zero32_n = w.cap_R;
     ep.zero64 = w.scan_arena;
@@ -2442,7 +2591,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     ep.bsc = w.bsc;
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
-    hipLaunchKernelGGL(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
+    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
                        (const int64_t*)nullptr, ep);
 }
 

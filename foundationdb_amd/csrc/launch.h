@@ -1,0 +1,127 @@
+// launch.h — kernel submission for the engine: launch now, or record into a LaunchList.
+//
+// A LaunchList is one pipeline stage of one batch as data: kernel launches (host stub, grid,
+// block, dynamic LDS, argument values) and event records / waits.  The engine either replays it
+// onto streams (direct mode) or feeds it, as per-batch parameters, to the nodes of a cached
+// hipGraph of the same shape: one hipGraphLaunch per batch instead of ~20 runtime calls
+// (tools/launchbench.hip: 15 launches ~45 us of host time, their graph 6 us, a node parameter
+// update 0.12 us).  Every kernel launch of the pipeline goes through fdb_launch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <tuple>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+namespace fdbcs {
+
+struct LaunchList {
+    enum Kind : uint8_t {
+        kKernel = 0,
+        kTimingRecord = 1,  // event record kept in graph mode (phase / roofline timing)
+        kSyncRecord = 2,    // cross-stream ordering, direct mode only (a graph is ordered already)
+        kSyncWait = 3,
+    };
+    struct Rec {
+        Kind kind;
+        const void* func;
+        hipEvent_t event;
+        dim3 grid, block;
+        uint32_t shmem;
+        uint32_t arg0, nargs;  // argument slots [arg0, arg0 + nargs) of argoff / argp
+    };
+    std::vector<Rec> recs;
+    std::vector<uint32_t> argoff;  // byte offset of each argument value in `arena`
+    std::vector<unsigned char> arena;
+    std::vector<void*> argp;       // finalize(): pointers into arena, in argoff order
+
+    void clear() {
+        recs.clear();
+        argoff.clear();
+        arena.clear();
+        argp.clear();
+    }
+    template <typename T>
+    void push_arg(const T& v) {
+        constexpr size_t al = alignof(T) < 16 ? 16 : alignof(T);
+        const size_t off = (arena.size() + al - 1) / al * al;
+        arena.resize(off + sizeof(T));
+        memcpy(arena.data() + off, &v, sizeof(T));
+        argoff.push_back((uint32_t)off);
+    }
+    void finalize() {
+        argp.resize(argoff.size());
+        for (size_t i = 0; i < argoff.size(); i++) argp[i] = arena.data() + argoff[i];
+    }
+    // Shape of the list as a graph sees it: the kernels and timing events in order.
+    uint64_t signature() const {
+        uint64_t h = 1469598103934665603ull;
+        for (const Rec& r : recs) {
+            if (r.kind == kSyncRecord || r.kind == kSyncWait) continue;
+            const uint64_t x = r.kind == kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u;
+            h = (h ^ x) * 1099511628211ull;
+        }
+        return h;
+    }
+    // Direct mode: submit in order (waits and records on `s`).
+    hipError_t replay(hipStream_t s) {
+        finalize();
+        for (const Rec& r : recs) {
+            hipError_t e = hipSuccess;
+            switch (r.kind) {
+                case kKernel:
+                    e = hipLaunchKernel(r.func, r.grid, r.block, argp.data() + r.arg0, r.shmem, s);
+                    break;
+                case kTimingRecord:
+                case kSyncRecord:
+                    e = hipEventRecord(r.event, s);
+                    break;
+                case kSyncWait:
+                    e = hipStreamWaitEvent(s, r.event, 0);
+                    break;
+            }
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+};
+
+// Non-null while the engine records a stage: fdb_launch / fdb_event append to it.
+extern thread_local LaunchList* t_record;
+
+template <typename... P, typename... A>
+inline void fdb_launch(void (*k)(P...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, A&&... a) {
+    static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+    if (LaunchList* L = t_record) {
+        LaunchList::Rec r{LaunchList::kKernel, (const void*)k, nullptr, grid, block, shmem, (uint32_t)L->argoff.size(),
+                          (uint32_t)sizeof...(P)};
+        (L->push_arg(static_cast<std::decay_t<P>>(a)), ...);
+        L->recs.push_back(r);
+        return;
+    }
+    std::tuple<std::decay_t<P>...> vals(static_cast<std::decay_t<P>>(a)...);
+    std::apply(
+        [&](auto&... v) {
+            void* args[] = {(void*)&v..., nullptr};
+            (void)hipLaunchKernel((const void*)k, grid, block, args, shmem, s);
+        },
+        vals);
+}
+
+// kind: LaunchList::kTimingRecord, kSyncRecord or kSyncWait (a wait of `s` on the event).
+inline void fdb_event(LaunchList::Kind kind, hipEvent_t e, hipStream_t s) {
+    if (!e) return;
+    if (LaunchList* L = t_record) {
+        L->recs.push_back({kind, nullptr, e, dim3(), dim3(), 0, 0, 0});
+        return;
+    }
+    if (kind == LaunchList::kSyncWait)
+        (void)hipStreamWaitEvent(s, e, 0);
+    else
+        (void)hipEventRecord(e, s);
+}
+
+}  // namespace fdbcs

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "launch.h"
+
 namespace fdbcs {
 
 constexpr int kScanThreads = 256;
@@ -214,14 +216,14 @@ template <int K1, class F1, int K2, class F2>
 void launch_scan2(hipStream_t s, const F1& f1, const F2& f2, int64_t n, ScanState st1, ScanState st2) {
     int64_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles < 1) tiles = 1;
-    hipLaunchKernelGGL((k_scan2<K1, F1, K2, F2>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f1, f2, n, st1, st2);
+    fdb_launch((k_scan2<K1, F1, K2, F2>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f1, f2, n, st1, st2);
 }
 
 template <int K, class F>
 void launch_scan(hipStream_t s, const F& f, const int64_t* n_dev, int64_t n_max, ScanState st) {
     int64_t tiles = (n_max + kScanTile - 1) / kScanTile;
     if (tiles < 1) tiles = 1;
-    hipLaunchKernelGGL((k_scan<K, F>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f, n_dev, n_max, st);
+    fdb_launch((k_scan<K, F>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f, n_dev, n_max, st);
 }
 
 }  // namespace fdbcs
