@@ -165,11 +165,25 @@ struct fdbcs_conflict_set {
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
     bool dma_upload = false;  // FDBCS_UPLOAD=dma: hipMemcpyAsync instead of the k_upload kernel
     int upload_blocks = 32;   // FDBCS_UPLOAD_BLOCKS: workgroups of the k_upload kernel
-    int check_version = 2;    // FDBCS_CHECK: read-check kernel (2 LDS-staged fused search, 1 four lookups)
+    int check_version = 1;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants)
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
+    // Graph mode (FDBCS_GRAPH, default on when no phase timing / tracing): every detect launches
+    // ONE cached hipGraph holding stage A of this batch beside stage B of the previous batch (two
+    // independent branches on one stream); this batch's stage B waits here for the next launch or
+    // for a wait/flush.
+    bool use_graph = true;
+    LaunchList rec_a, rec_b, pending_b;
+    fdbcs_batch* pending_batch = nullptr;
+    struct GraphEntry {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        std::vector<hipGraphNode_t> nodes_a, nodes_b;
+    };
+    std::vector<std::pair<std::pair<uint64_t, uint64_t>, GraphEntry>> graphs;
+    int64_t graph_launches = 0;
     std::unordered_set<fdbcs_batch*> live;  // batches not yet destroyed (detached if the set goes first)
 };
 
@@ -270,8 +284,11 @@ int ensure_scan_arena(fdbcs_conflict_set* cs) {
     return FDBCS_OK;
 }
 
+int flush_pending(fdbcs_conflict_set* cs);
+
 // Both streams idle (before reallocating anything either stage uses).
 int sync_all(fdbcs_conflict_set* cs) {
+    if (int rc = flush_pending(cs)) return rc;
     HIPOK(hipStreamSynchronize(cs->astream));
     if (cs->astream2) HIPOK(hipStreamSynchronize(cs->astream2));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -429,6 +446,7 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
 
 // Read the exact history size/tail usage back (synchronizes the stream).
 int sync_sizes(fdbcs_conflict_set* cs) {
+    if (int rc = flush_pending(cs)) return rc;
     Scalars s;
     HIPOK(hipMemcpyAsync(&s, cs->scal.p, sizeof(s), hipMemcpyDeviceToHost, cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -673,16 +691,18 @@ int do_upload(fdbcs_batch* b) {
     memcpy(h + L.woff, b->woff.data(), 4 * (T + 1));
     if (T) memcpy(h + L.flags, b->flags.data(), T);
     // on stage A's stream (its kernels read the batch first); stage B waits for ev_up.  A reused
-    // slot's device copy may still be read by the epilogue of the batch that used it last.
+    // slot's device copy may still be read by the epilogue of the batch that used it last.  While
+    // the engine records stage A (t_record set) these become records of that stage.
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
-    if (sl->free_recorded) HIPOK(hipStreamWaitEvent(cs->astream, sl->ev_free, 0));
-    if (cs->dma_upload) {
+    if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess)
+        fdb_event(LaunchList::kSyncWait, sl->ev_free, cs->astream);
+    if (cs->dma_upload && !t_record) {
         HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
     } else {
         launch_upload(cs->astream, sl->pin_in.dp, sl->dev.p, (int64_t)L.total, cs->upload_blocks);
-        HIPOK(hipGetLastError());
+        if (!t_record) HIPOK(hipGetLastError());
     }
-    HIPOK(hipEventRecord(sl->ev_up, cs->astream));
+    fdb_event(LaunchList::kSyncRecord, sl->ev_up, cs->astream);
     char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
     b->bd.R = (int32_t)R;
@@ -698,6 +718,87 @@ int do_upload(fdbcs_batch* b) {
     b->tail_bytes = b->tail_size();
     b->state = 1;
     return FDBCS_OK;
+}
+
+// ---- graph mode
+//
+// A graph node per kernel and per timing event of stage A (one chain) and stage B (another chain,
+// no edge between them), built once per pair of stage shapes (LaunchList::signature) and reused:
+// per batch only the node parameters change (hipGraphExecKernelNodeSetParams, ~0.1 us each).
+
+int add_chain(hipGraph_t g, LaunchList& L, std::vector<hipGraphNode_t>& nodes) {
+    L.finalize();
+    hipGraphNode_t prev = nullptr;
+    for (const LaunchList::Rec& r : L.recs) {
+        hipGraphNode_t n = nullptr;
+        if (r.kind == LaunchList::kKernel) {
+            hipKernelNodeParams p{};
+            p.func = const_cast<void*>(r.func);
+            p.gridDim = r.grid;
+            p.blockDim = r.block;
+            p.sharedMemBytes = r.shmem;
+            p.kernelParams = L.argp.data() + r.arg0;
+            HIPOK(hipGraphAddKernelNode(&n, g, prev ? &prev : nullptr, prev ? 1 : 0, &p));
+        } else if (r.kind == LaunchList::kTimingRecord) {
+            HIPOK(hipGraphAddEventRecordNode(&n, g, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
+        } else {
+            continue;  // cross-stream ordering: implicit in one graph on one stream
+        }
+        nodes.push_back(n);
+        prev = n;
+    }
+    return FDBCS_OK;
+}
+
+int set_chain(hipGraphExec_t ex, LaunchList& L, const std::vector<hipGraphNode_t>& nodes) {
+    L.finalize();
+    size_t k = 0;
+    for (const LaunchList::Rec& r : L.recs) {
+        if (r.kind == LaunchList::kKernel) {
+            hipKernelNodeParams p{};
+            p.func = const_cast<void*>(r.func);
+            p.gridDim = r.grid;
+            p.blockDim = r.block;
+            p.sharedMemBytes = r.shmem;
+            p.kernelParams = L.argp.data() + r.arg0;
+            HIPOK(hipGraphExecKernelNodeSetParams(ex, nodes[k++], &p));
+        } else if (r.kind == LaunchList::kTimingRecord) {
+            HIPOK(hipGraphExecEventRecordNodeSetEvent(ex, nodes[k++], r.event));
+        }
+    }
+    return FDBCS_OK;
+}
+
+// Launch stage lists A and B (either may be empty) as one graph on the set's stream.
+int launch_graph(fdbcs_conflict_set* cs, LaunchList& A, LaunchList& B) {
+    const std::pair<uint64_t, uint64_t> key{A.recs.empty() ? 0 : A.signature(), B.recs.empty() ? 0 : B.signature()};
+    fdbcs_conflict_set::GraphEntry* ge = nullptr;
+    for (auto& kv : cs->graphs)
+        if (kv.first == key) ge = &kv.second;
+    if (!ge) {
+        fdbcs_conflict_set::GraphEntry e;
+        HIPOK(hipGraphCreate(&e.graph, 0));
+        int rc;
+        if ((rc = add_chain(e.graph, A, e.nodes_a)) || (rc = add_chain(e.graph, B, e.nodes_b))) return rc;
+        HIPOK(hipGraphInstantiate(&e.exec, e.graph, nullptr, nullptr, 0));
+        cs->graphs.push_back({key, e});
+        ge = &cs->graphs.back().second;
+    } else {
+        int rc;
+        if ((rc = set_chain(ge->exec, A, ge->nodes_a)) || (rc = set_chain(ge->exec, B, ge->nodes_b))) return rc;
+    }
+    HIPOK(hipGraphLaunch(ge->exec, cs->stream));
+    cs->graph_launches++;
+    return FDBCS_OK;
+}
+
+int flush_pending(fdbcs_conflict_set* cs) {
+    if (!cs->pending_batch) return FDBCS_OK;
+    LaunchList none;
+    cs->pending_batch = nullptr;
+    int rc = launch_graph(cs, none, cs->pending_b);
+    cs->pending_b.clear();
+    return rc;
 }
 
 double ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -742,6 +843,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_ASTREAMS")) cs->astreams = atoi(v) == 1 ? 1 : 2;
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
+    if (const char* v = getenv("FDBCS_GRAPH")) cs->use_graph = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
@@ -774,6 +876,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
 void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (!cs) return;
     (void)hipSetDevice(cs->device);
+    (void)flush_pending(cs);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
     if (cs->astream2) (void)hipStreamSynchronize(cs->astream2);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
@@ -796,6 +899,11 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->trace_buf.release();
     for (BatchSlot* sl : cs->pool) release_slot(sl);
     cs->pool.clear();
+    for (auto& kv : cs->graphs) {
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+    }
+    cs->graphs.clear();
     // batches that outlive their set (e.g. garbage-collection order in a binding) keep their own
     // slot and refuse every further call
     for (fdbcs_batch* b : cs->live) b->cs = nullptr;
@@ -813,6 +921,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
 int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     if (!cs) return FDBCS_E_INVALID;
     HIPOK(hipSetDevice(cs->device));
+    if (int rc = flush_pending(cs)) return rc;
     if (int rc = sync_all(cs)) return rc;
     HIPOK(hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -880,6 +989,7 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
                        const int64_t* versions, int64_t header_version) {
     if (!cs || n < 0 || (n > 0 && (!key_bytes || !key_offsets || !versions))) return FDBCS_E_INVALID;
     HIPOK(hipSetDevice(cs->device));
+    if (int rc = sync_all(cs)) return rc;
     std::vector<ulonglong2> k(n);
     std::vector<uint2> lt(n);
     std::vector<uint8_t> tail;
@@ -978,6 +1088,7 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
     }
     if (b->state == 2) {  // still in flight: its set (which must outlive it) owns the stream
         (void)hipSetDevice(b->cs->device);
+        (void)flush_pending(b->cs);
         (void)hipStreamSynchronize(b->cs->astream);
         if (b->cs->astream2) (void)hipStreamSynchronize(b->cs->astream2);
         (void)hipStreamSynchronize(b->cs->stream);
@@ -1219,6 +1330,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
 
     hipStream_t s = cs->stream;
     const int timing = cs->timing;
+    // Graph mode: both stages become one graph launch (see launch_graph); phase timing, tracing and
+    // the serial / two-stream debugging modes submit directly.
+    const bool graph = cs->use_graph && timing < 2 && !cs->serial && !cs->trace && cs->astreams == 1 &&
+                       !cs->dma_upload;
     // Stage A (sort, positions, candidate edges) depends only on this batch: it runs on its own
     // stream and overlaps stage B of the previous batch.  Phase timing (level 2) runs both stages on
     // one stream so the phases are measured one after another.
@@ -1227,25 +1342,32 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const int wp = cs->wpar;
     cs->wpar = (wp + 1) % kNumWork;
     Work& w = cs->work[wp];
-    // phase events: level 2 records every phase, level 1 only the copy kernels (roofline)
+    // phase events: level 2 records every phase, level 1 only the hot kernels (roofline)
     auto rec = [&](int ph, int level) -> hipEvent_t {
         if (timing < level) return nullptr;
         b->recorded |= 1u << ph;
         return sl->ev[ph];
     };
     auto mark = [&](int ph) -> int {
-        if (hipEvent_t e = rec(ph, 2)) HIPOK(hipEventRecord(e, s));
+        if (hipEvent_t e = rec(ph, 2)) fdb_event(LaunchList::kTimingRecord, e, s);
         return FDBCS_OK;
     };
-    if ((rc = mark(kPhStart))) return rc;
+    const bool was_uploaded = b->state == 1;
+    if (graph && was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess)
+        HIPOK(hipStreamWaitEvent(s, sl->ev_up, 0));  // uploaded early (fdbcs_batch_upload) on stage A's stream
+    LaunchList& la = cs->rec_a;
+    LaunchList& lb = cs->rec_b;
+    la.clear();
+    lb.clear();
+    // ---- record stage A: upload, D.Sort and the candidate edges of D.CheckIntraBatch
+    t_record = &la;
+    if ((rc = mark(kPhStart))) return t_record = nullptr, rc;
     // workspace wp was last used by the batch before the previous one: its epilogue re-zeroed it
-    if (cs->wused[wp] && sa != s) HIPOK(hipStreamWaitEvent(sa, cs->ev_b[wp], 0));
+    if (cs->wused[wp] && sa != s && hipEventQuery(cs->ev_b[wp]) != hipSuccess)
+        fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     cs->wused[wp] = true;
-    if (b->state == 0 && (rc = do_upload(b))) return rc;
-    if (sa == s || hipEventQuery(sl->ev_up) != hipSuccess) HIPOK(hipStreamWaitEvent(s, sl->ev_up, 0));
-    if (sa != s && sa != cs->astream && hipEventQuery(sl->ev_up) != hipSuccess)
-        HIPOK(hipStreamWaitEvent(sa, sl->ev_up, 0));  // the upload ran on astream
-    if ((rc = mark(kPhUpload))) return rc;
+    if (b->state == 0 && (rc = do_upload(b))) return t_record = nullptr, rc;
+    if ((rc = mark(kPhUpload))) return t_record = nullptr, rc;
     const BatchDev& bd = b->bd;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
@@ -1263,37 +1385,39 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
             init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin) ? ~0ull : 0ull;
         HIPOK(hipMemcpy(w.trace, init, sizeof(init), hipMemcpyHostToDevice));
     }
-    // ---- stage A: D.Sort and the candidate edges of D.CheckIntraBatch
     launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
     int sorted = 0;
     launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted, rec(kPhSortBegin, 1),
                        rec(kPhSortEnd, 1));
-    if ((rc = mark(kPhSort))) return rc;
+    mark(kPhSort);
     launch_positions(sa, bd, w, sorted);
     if (cs->validate) launch_validate_sort(sa, bd, w, sorted);
     launch_edges(sa, bd, w);
-    if (sa != s) HIPOK(hipEventRecord(cs->ev_a[wp], sa));
-    if ((rc = mark(kPhEdges))) return rc;
-    // ---- stage B: D.CheckRead against the history the previous batch left, then batch order
+    if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_a[wp], sa);
+    mark(kPhEdges);
+    // ---- record stage B: D.CheckRead against the history the previous batch left, then batch order
+    t_record = &lb;
+    if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
     b->check_hist = cs->n_ub + cs->nd_ub;
-    if (hipEvent_t e = rec(kPhCheckBegin, 1)) HIPOK(hipEventRecord(e, s));
+    fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
     launch_check(s, bd, w, base, delta, htail, cs->check_version, cs->check_grid);
-    if (hipEvent_t e = rec(kPhCheckEnd, 1)) HIPOK(hipEventRecord(e, s));
-    if ((rc = mark(kPhCheck))) return rc;
-    if (sa != s) HIPOK(hipStreamWaitEvent(s, cs->ev_a[wp], 0));
+    fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
+    mark(kPhCheck);
+    if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp);
-    if (b->any_report) {  // before the epilogue re-zeroes hist_conf
-        if (R) HIPOK(hipMemcpyAsync(b->h_rconf, w.rconf, R, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(b->h_hist, w.hist_conf, T, hipMemcpyDeviceToHost, s));
-        HIPOK(hipMemcpyAsync(b->h_first, w.first_conf, 4 * T, hipMemcpyDeviceToHost, s));
+    if (b->any_report) {  // before the epilogue re-zeroes hist_conf (into the host-mapped results)
+        char* hdv = (char*)sl->pin_out.dp;
+        if (R) launch_copy_bytes(s, hdv + o_rc, w.rconf, R);
+        launch_copy_bytes(s, hdv + o_hc, w.hist_conf, T);
+        launch_copy_bytes(s, hdv + o_fc, w.first_conf, 4 * T);
     }
-    if ((rc = mark(kPhIntra))) return rc;
+    mark(kPhIntra);
     launch_combine(s, bd, w, sc);
-    if ((rc = mark(kPhCombine))) return rc;
+    mark(kPhCombine);
     // D.MergeWrite into the delta tier
     launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
                  rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1));
-    if ((rc = mark(kPhMerge))) return rc;
+    mark(kPhMerge);
     const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
@@ -1311,18 +1435,17 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
                        rec(kPhCompEnd, 1));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
-        // removeBefore when the oldest version moved; also whenever the tail arena is half full, for
-        // the repack that reclaims the tails of removed boundaries
         // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th
         // one: a full pass over the base costs ~10x the compaction copy at C2 while one
         // window-step of oldest-version movement makes few boundaries removable (a boundary goes
         // only when it and its predecessor are both older, SkipList.cpp:555-561). Verdict-neutral
-        // either way; a forced cadence (gc_interval > 0) keeps GC at every compaction.
+        // either way; a forced cadence (gc_interval > 0) keeps GC at every compaction.  Past the
+        // tail-reclaim threshold the GC also repacks the tail arena.
         const bool gc_turn = cs->gc_interval > 0 || ++cs->compactions_since_gc >= kGcEveryCompactions;
         gc = (new_oldest > cs->gc_applied && gc_turn) || cs->tail_ub > cs->tail_reclaim;
         if (gc) cs->compactions_since_gc = 0;
     }
-    if ((rc = mark(kPhCompact))) return rc;
+    mark(kPhCompact);
     if (gc) {
         launch_gc(s, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), htail,
                   (uint8_t*)cs->htail[cs->tcur ^ 1].p, sc, std::max(new_oldest, cs->gc_applied), cs->header_version,
@@ -1331,20 +1454,36 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         final_base ^= 1;
         cs->gc_applied = new_oldest;
     }
-    if ((rc = mark(kPhGc))) return rc;
+    mark(kPhGc);
     b->gc_ran = gc;
     b->compacted = compact;
     char* hd = (char*)sl->pin_out.dp;
     launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
                     gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1);
-    if (sa != s) HIPOK(hipEventRecord(cs->ev_b[wp], s));
-    if (!sl->ev_free) HIPOK(hipEventCreateWithFlags(&sl->ev_free, hipEventDisableTiming));
-    HIPOK(hipEventRecord(sl->ev_free, s));
+    if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
+    fdb_event(LaunchList::kSyncRecord, sl->ev_free, s);
     sl->free_recorded = true;
-    if ((rc = mark(kPhEpilogue))) return rc;
-    HIPOK(hipGetLastError());
-    if ((rc = mark(kPhEnd))) return rc;
+    mark(kPhEpilogue);
+    mark(kPhEnd);
+    t_record = nullptr;
+    // ---- submit
+    if (graph) {
+        // stage A of this batch beside the pending stage B of the previous one; this batch's
+        // stage B waits for the next detect (or a wait / flush)
+        LaunchList none;
+        const bool prev = cs->pending_batch != nullptr;
+        cs->pending_batch = nullptr;
+        rc = launch_graph(cs, la, prev ? cs->pending_b : none);
+        std::swap(cs->pending_b, lb);
+        if (rc) return rc;
+        cs->pending_batch = b;
+    } else {
+        if (flush_pending(cs)) return FDBCS_E_DEVICE;
+        HIPOK(la.replay(sa));
+        HIPOK(lb.replay(s));
+        HIPOK(hipGetLastError());
+    }
     cs->cur = final_base;
     cs->dcur = dnew;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
@@ -1367,6 +1506,8 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
     fdbcs_conflict_set* cs = b->cs;
     if (b->state == 2) {
         HIPOK(hipSetDevice(cs->device));
+        if (cs->pending_batch == b)  // its stage B still waits for the next detect: launch it now
+            if (int rc = flush_pending(cs)) return rc;
         // the epilogue's last workgroup publishes b->seq; poll it (checking the stream for errors)
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
             if ((spin & 1023) == 1023) {

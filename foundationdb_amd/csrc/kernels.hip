@@ -2543,6 +2543,21 @@ void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t by
                        n16);
 }
 
+// Report side outputs (rconf, hist_conf, first_conf) into the batch's host-mapped result buffer:
+// a kernel rather than a DMA copy so it can be a node of the batch's graph.
+__global__ __launch_bounds__(kBlock) void k_copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                       int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n) {
+    if (n <= 0) return;
+    int64_t blocks = (n + kBlock - 1) / kBlock;
+    blocks = blocks > 256 ? 256 : blocks;
+    fdb_launch(k_copy_bytes, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t*)dst, (const uint8_t*)src, n);
+}
+
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lvl3[i] = LLONG_MIN;
 }
