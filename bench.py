@@ -357,6 +357,9 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t_start)
     st = cs.stats()
     host_timed = {k: v / args.steps * 1e3 for k, v in host.items()}
+    for k in ("host_ms_prepare", "host_ms_record", "host_ms_submit"):  # inside detect_async (engine's clock)
+        host_timed["engine_" + k[8:]] = st[k] / max(1, st["batches"])
+    host_timed["graph_launches"] = st["graph_launches"]
 
     resident_elapsed = None
     if args.resident_steps > 0:  # diagnostic: batches uploaded before the timed region

@@ -79,6 +79,10 @@ class Stats(ctypes.Structure):
         ("sort_launches", ctypes.c_int64),
         ("sort_items", ctypes.c_int64),
         ("gc_runs", ctypes.c_int64),
+        ("host_ms_prepare", ctypes.c_double),
+        ("host_ms_record", ctypes.c_double),
+        ("host_ms_submit", ctypes.c_double),
+        ("graph_launches", ctypes.c_int64),
     ]
 
     def as_dict(self):

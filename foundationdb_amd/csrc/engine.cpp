@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <new>
 #include <unordered_set>
 #include <vector>
@@ -1288,11 +1289,16 @@ int fdbcs_batch_upload(fdbcs_batch* b) {
     return do_upload(b);
 }
 
+static inline double host_ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_version) {
     if (!b) return FDBCS_E_INVALID;
     if (!b->cs) return FDBCS_E_STATE;
     if (b->state > 1) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
+    const auto t_begin = std::chrono::steady_clock::now();
     HIPOK(hipSetDevice(cs->device));
     if (now < cs->max_written) return FDBCS_E_VERSION;
     if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
@@ -1359,6 +1365,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     LaunchList& lb = cs->rec_b;
     la.clear();
     lb.clear();
+    cs->stats.host_ms_prepare += host_ms_since(t_begin);
+    const auto t_rec = std::chrono::steady_clock::now();
     // ---- record stage A: upload, D.Sort and the candidate edges of D.CheckIntraBatch
     t_record = &la;
     if ((rc = mark(kPhStart))) return t_record = nullptr, rc;
@@ -1467,6 +1475,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhEpilogue);
     mark(kPhEnd);
     t_record = nullptr;
+    cs->stats.host_ms_record += host_ms_since(t_rec);
+    const auto t_sub = std::chrono::steady_clock::now();
     // ---- submit
     if (graph) {
         // stage A of this batch beside the pending stage B of the previous one; this batch's
@@ -1484,6 +1494,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(lb.replay(s));
         HIPOK(hipGetLastError());
     }
+    cs->stats.host_ms_submit += host_ms_since(t_sub);
+    cs->stats.graph_launches = cs->graph_launches;
     cs->cur = final_base;
     cs->dcur = dnew;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882

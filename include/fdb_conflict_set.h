@@ -111,6 +111,12 @@ typedef struct fdbcs_stats {
     int64_t sort_launches;
     int64_t sort_items;     /* endpoints sorted (sum over launches) */
     int64_t gc_runs;        /* removeBefore passes (full, over the base tier after a compaction) */
+    /* Host time inside fdbcs_batch_detect_async (milliseconds, summed): capacity checks and result
+     * buffers, the host part of the upload, recording both stages, submitting them. */
+    double host_ms_prepare;
+    double host_ms_record;
+    double host_ms_submit;
+    int64_t graph_launches; /* batches submitted as one graph launch */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
