@@ -278,8 +278,9 @@ def main():
     maxR = max(b.n_reads for b in mine)
     maxW = max(b.n_writes for b in mine)
 
-    def tail_bytes(ko):
-        return int(np.maximum(np.diff(ko) - 16, 0).sum())
+    def tail_bytes(ko):  # history tail bytes, each tail padded to 8 (engine.cpp padded_tail)
+        t = np.diff(ko) - 16
+        return int(((t[t > 0] + 7) // 8 * 8).sum())
 
     tail_total = tail_bytes(ko) + sum(tail_bytes(b.key_offsets) for b in mine) + (1 << 20)
     cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, tail_total, maxT, maxR, maxW)

@@ -236,6 +236,7 @@ struct fdbcs_batch {
     uint32_t recorded = 0;  // phases whose events were recorded (bit per Phase)
     bool any_report = false;
     int64_t check_hist = 0;  // boundaries (both tiers, upper bound) the read check searched
+    int64_t wtail = 0;       // history tail bytes the batch's write endpoints could add (8-byte padded)
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
 
@@ -605,6 +606,9 @@ UploadLayout upload_layout(size_t T, size_t R, size_t W, size_t tail_bytes) {
     L.total = off;
     return L;
 }
+
+// History tail bytes a key of this length takes when inserted (8-byte aligned, kernels.hip tail_units).
+inline int64_t padded_tail(int32_t len) { return len > 16 ? ((int64_t)len - 16 + 7) / 8 * 8 : 0; }
 
 // Prefix words of a key (dkey_prefix), two big-endian loads when the key has 16 bytes or more.
 inline void fast_prefix(const uint8_t* p, uint32_t len, uint64_t* hi, uint64_t* lo) {
@@ -1139,6 +1143,7 @@ int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int repor
         for (int32_t i = 0; i < n_writes; i++) {
             add_key(b, b->wkeys, write_begin[i], write_begin_len[i]);
             add_key(b, b->wkeys, write_end[i], write_end_len[i]);
+            b->wtail += padded_tail(write_begin_len[i]) + padded_tail(write_end_len[i]);
             b->wowner.push_back(t);
         }
     }
@@ -1211,6 +1216,8 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
         for (int32_t w = pb->write_offsets[t], i = 0; w < pb->write_offsets[t + 1]; w++, i++) {
             put(wk + 2 * (size_t)(wa + i), 2 * ((int64_t)R + w));
             put(wk + 2 * (size_t)(wa + i) + 1, 2 * ((int64_t)R + w) + 1);
+            b->wtail += padded_tail((int32_t)wk[2 * (size_t)(wa + i)].len) +
+                        padded_tail((int32_t)wk[2 * (size_t)(wa + i) + 1].len);
             wown[wa + i] = t;
         }
     }
@@ -1269,6 +1276,7 @@ int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
             for (int32_t w = w0; w < w1; w++) {
                 for (int e = 0; e < 2; e++) {
                     const int64_t k = 2 * ((int64_t)R + w) + e;
+                    b->wtail += padded_tail((int32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]));
                     add_key(b, b->wkeys, pb->key_bytes + pb->key_offsets[k],
                             (int32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]));
                 }
@@ -1304,7 +1312,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
     // tail offsets are 32-bit: refuse a batch that could overflow the arena (GC repacks it long before)
     // history tail bytes this batch can append (each inserted tail padded to 8 bytes)
-    const int64_t tail_add = (int64_t)b->tail_size() + 16 * (int64_t)b->W();
+    // only write endpoints ever enter the history (merge inserts segment begins and ends)
+    const int64_t tail_add = b->wtail;
     if (cs->tail_ub + tail_add + 1 >= kTailLimit) return FDBCS_E_NOMEM;
     const int64_t T = b->T(), R = b->R(), W = b->W();
     int rc;

@@ -23,6 +23,13 @@ __global__ void k_spin(int us, int* out) {
     if (threadIdx.x == 0 && out) atomicAdd(out, 1);
 }
 
+struct BigArg {
+    void* p[80];
+};
+__global__ void k_bigarg(BigArg b) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && b.p[79]) atomicAdd((int*)b.p[79], 1);
+}
+
 int main() {
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -74,6 +81,53 @@ int main() {
         for (int i = 0; i < n; i++) CK(hipGraphExecKernelNodeSetParams(ge, nodes[i & 7], &p));
         auto t1 = std::chrono::steady_clock::now();
         printf("hipGraphExecKernelNodeSetParams: %.2f us\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / n);
+    }
+    // a 30-node chain of kernels with 640-byte arguments: launch cost and per-node update cost
+    {
+        BigArg big{};
+        big.p[79] = d;
+        hipGraph_t g2;
+        CK(hipGraphCreate(&g2, 0));
+        hipGraphNode_t prev = nullptr, n2[30];
+        for (int i = 0; i < 30; i++) {
+            hipKernelNodeParams p{};
+            void* args[] = {&big};
+            p.func = (void*)k_bigarg;
+            p.gridDim = dim3(64);
+            p.blockDim = dim3(256);
+            p.kernelParams = args;
+            CK(hipGraphAddKernelNode(&n2[i], g2, prev ? &prev : nullptr, prev ? 1 : 0, &p));
+            prev = n2[i];
+        }
+        hipGraphExec_t ge2;
+        CK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+        const int n = 300;
+        auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < n; i++) CK(hipGraphLaunch(ge2, s));
+        auto t1 = std::chrono::steady_clock::now();
+        CK(hipStreamSynchronize(s));
+        printf("hipGraphLaunch, 30 nodes x 640-byte args: %.2f us\n",
+               std::chrono::duration<double, std::micro>(t1 - t0).count() / n);
+        hipKernelNodeParams p{};
+        void* args[] = {&big};
+        p.func = (void*)k_bigarg;
+        p.gridDim = dim3(64);
+        p.blockDim = dim3(256);
+        p.kernelParams = args;
+        t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < 3000; i++) CK(hipGraphExecKernelNodeSetParams(ge2, n2[i % 30], &p));
+        t1 = std::chrono::steady_clock::now();
+        printf("SetParams, 640-byte args:                  %.2f us\n",
+               std::chrono::duration<double, std::micro>(t1 - t0).count() / 3000);
+        t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < n; i++) {
+            for (int k = 0; k < 30; k++) CK(hipGraphExecKernelNodeSetParams(ge2, n2[k], &p));
+            CK(hipGraphLaunch(ge2, s));
+        }
+        t1 = std::chrono::steady_clock::now();
+        CK(hipStreamSynchronize(s));
+        printf("30 SetParams + launch:                     %.2f us\n",
+               std::chrono::duration<double, std::micro>(t1 - t0).count() / n);
     }
     CK(hipStreamSynchronize(s));
     return 0;
