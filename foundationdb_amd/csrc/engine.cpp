@@ -171,11 +171,13 @@ struct fdbcs_conflict_set {
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
-    // Graph mode (FDBCS_GRAPH, default on when no phase timing / tracing): every detect launches
-    // ONE cached hipGraph holding stage A of this batch beside stage B of the previous batch (two
-    // independent branches on one stream); this batch's stage B waits here for the next launch or
-    // for a wait/flush.
-    bool use_graph = true;
+    // Graph mode (FDBCS_GRAPH=1; off by default): every detect launches ONE cached hipGraph holding
+    // stage A of this batch beside stage B of the previous batch (two independent branches on one
+    // stream); this batch's stage B waits here for the next launch or for a wait/flush.  Measured
+    // slower than direct launches at C2 (24.6M vs 27.2M txns/s): the kernels take 200-700-byte
+    // argument structs, and a node parameter update costs 0.76 us at 640 bytes
+    // (tools/graphbench.hip), so updating ~30 nodes costs as much host time as launching them.
+    bool use_graph = false;
     LaunchList rec_a, rec_b, pending_b;
     fdbcs_batch* pending_batch = nullptr;
     struct GraphEntry {
