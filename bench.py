@@ -246,7 +246,9 @@ def main():
 
         torch.cuda.set_device(device)
         dist.init_process_group(args.backend)
-    cdev = "cuda" if args.backend == "nccl" else "cpu"
+    # collectives run on device tensors whenever there is a GPU: RCCL ("nccl"), or gloo's CUDA
+    # all-reduce in one-GPU rehearsals (several ranks on one card, where RCCL refuses)
+    cdev = "cuda" if torch.cuda.is_available() else "cpu"
     from foundationdb_amd import build as fbuild
 
     fbuild.build()
@@ -286,10 +288,27 @@ def main():
     cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, tail_total, maxT, maxR, maxW)
     verdicts = [None] * n_all
 
-    def combine(i, v):
+    # Multi-GPU combine (CommitProxyServer.actor.cpp:764-780): each rank scatters 2 - verdict of its
+    # sub-batch into a zeroed T-byte buffer ON THE DEVICE (fdbcs_batch_scatter_conflict_bytes, on
+    # torch's stream after the batch's epilogue) and one RCCL MAX all-reduce combines them.  The
+    # routed transaction ids are uploaded once, like the inputs.  gloo (CPU rehearsals) combines
+    # host copies instead.
+    on_device = dist is not None and cdev != "cpu"
+    ids_dev = {}
+    if on_device:
+        for i in range(n_all):
+            ids_dev[i] = torch.from_numpy(routed[i].txn_ids.astype(np.int32)).to(cdev)
+    combined = {}
+
+    def combine(i, o, v):
         T = gbatches[i][0].n_txn
-        c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
+        if on_device:
+            c = torch.zeros(T, dtype=torch.uint8, device=cdev)
+            o.scatter_conflict_bytes(ids_dev[i].data_ptr(), c.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        else:
+            c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        combined[i] = c
 
     host = {"add": 0.0, "submit": 0.0, "wait": 0.0}
 
@@ -304,7 +323,7 @@ def main():
             verdicts[j] = oj.wait()
             host["wait"] += pc() - t
             if dist is not None:
-                combine(j, verdicts[j])
+                combine(j, oj, verdicts[j])
             oj.close()
 
         for i in range(lo, hi):
@@ -446,6 +465,17 @@ def main():
             "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"],
         }
 
+    combine_check = None
+    if dist is not None:
+        # the device-side combine against host-built conflict bytes of the same verdicts
+        bad = 0
+        for i in sorted(combined):
+            h = torch.from_numpy(KeyRangeSharding.conflict_bytes(gbatches[i][0].n_txn, routed[i], verdicts[i])).to(cdev)
+            dist.all_reduce(h, op=dist.ReduceOp.MAX)
+            bad += int(not torch.equal(h, combined[i]))
+        combine_check = {"batches": len(combined), "mismatched": bad,
+                         "path": (f"device scatter + {'RCCL' if args.backend == 'nccl' else 'gloo'} MAX all-reduce"
+                                  if on_device else "host bytes + all-reduce")}
     parity = cpu_base = None
     if not args.no_cpu_baseline:
         timed = set(range(timed_lo, timed_hi))
@@ -496,6 +526,7 @@ def main():
         "host_ms_per_batch": host_timed,
         "total_note": "reference 'total' (SkipList.cpp:1082-1085): addTransaction + detect, per batch in the loop",
         "parity": parity,
+        "combine_check": combine_check,
         "history_boundaries_end": hist_end,
         "phase_ms_per_batch": phase,
         "compactions": st["compactions"],

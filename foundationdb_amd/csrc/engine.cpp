@@ -204,6 +204,10 @@ struct BatchSlot {
     hipEvent_t ev_up = nullptr;    // upload done (recorded on stage A's stream)
     hipEvent_t ev_free = nullptr;  // the last batch using this slot finished on the device
     bool free_recorded = false;
+    // fdbcs_batch_scatter_conflict_bytes: the caller's stream read dverdict; the slot's next
+    // upload waits for ev_user (recorded on that stream after the scatter).
+    hipEvent_t ev_user = nullptr, ev_done = nullptr;
+    bool user_recorded = false;
 };
 
 struct fdbcs_batch {
@@ -573,6 +577,8 @@ void release_slot(BatchSlot* sl) {
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
     if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
+    if (sl->ev_user) (void)hipEventDestroy(sl->ev_user);
+    if (sl->ev_done) (void)hipEventDestroy(sl->ev_done);
     sl->dev.release();
     sl->dverdict.release();
     sl->pin_in.release();
@@ -703,6 +709,13 @@ int do_upload(fdbcs_batch* b) {
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
     if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess)
         fdb_event(LaunchList::kSyncWait, sl->ev_free, cs->astream);
+    if (sl->user_recorded) {  // an external stream still reads this slot's verdict bytes
+        if (hipEventQuery(sl->ev_user) != hipSuccess) {
+            HIPOK(hipStreamWaitEvent(cs->astream, sl->ev_user, 0));
+            HIPOK(hipStreamWaitEvent(cs->stream, sl->ev_user, 0));
+        }
+        sl->user_recorded = false;
+    }
     if (cs->dma_upload && !t_record) {
         HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
     } else {
@@ -1701,6 +1714,27 @@ int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr) {
     if (!b || !dptr) return FDBCS_E_INVALID;
     if (b->state < 2) return FDBCS_E_STATE;
     *dptr = b->slot->dverdict.p;
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_scatter_conflict_bytes(fdbcs_batch* b, const int32_t* dev_txn_ids, uint8_t* dev_out, void* stream) {
+    if (!b || (!dev_txn_ids && b->T() > 0) || (!dev_out && b->T() > 0)) return FDBCS_E_INVALID;
+    if (!b->cs || b->state < 2) return FDBCS_E_STATE;
+    fdbcs_conflict_set* cs = b->cs;
+    HIPOK(hipSetDevice(cs->device));
+    if (cs->pending_batch == b)
+        if (int rc = flush_pending(cs)) return rc;
+    BatchSlot* sl = b->slot;
+    hipStream_t st = (hipStream_t)stream;
+    if (!sl->ev_done) HIPOK(hipEventCreateWithFlags(&sl->ev_done, hipEventDisableTiming));
+    if (!sl->ev_user) HIPOK(hipEventCreateWithFlags(&sl->ev_user, hipEventDisableTiming));
+    // everything submitted to the batch-order stream so far includes this batch's epilogue
+    HIPOK(hipEventRecord(sl->ev_done, cs->stream));
+    HIPOK(hipStreamWaitEvent(st, sl->ev_done, 0));
+    launch_scatter_conflicts(st, (const uint8_t*)sl->dverdict.p, dev_txn_ids, b->T(), dev_out);
+    HIPOK(hipGetLastError());
+    HIPOK(hipEventRecord(sl->ev_user, st));
+    sl->user_recorded = true;
     return FDBCS_OK;
 }
 

@@ -2558,6 +2558,21 @@ void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n) {
     fdb_launch(k_copy_bytes, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t*)dst, (const uint8_t*)src, n);
 }
 
+// On-device combine input (multi-GPU): out[ids[i]] = 2 - verdict[i], the conflict byte the RCCL
+// MAX all-reduce combines (CommitProxyServer.actor.cpp:764-780 as a max of 2 - verdict).
+__global__ __launch_bounds__(kBlock) void k_scatter_conflicts(const uint8_t* __restrict__ v, const int32_t* __restrict__ ids,
+                                                              int64_t n, uint8_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[ids[i]] = (uint8_t)(2 - v[i]);
+}
+
+void launch_scatter_conflicts(hipStream_t s, const uint8_t* verdict, const int32_t* ids, int64_t n, uint8_t* out) {
+    if (n <= 0) return;
+    int64_t blocks = (n + kBlock - 1) / kBlock;
+    blocks = blocks > 1024 ? 1024 : blocks;
+    fdb_launch(k_scatter_conflicts, dim3((unsigned)blocks), dim3(kBlock), 0, s, verdict, ids, n, out);
+}
+
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lvl3[i] = LLONG_MIN;
 }

@@ -193,6 +193,15 @@ int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out,
  * detect until the batch is destroyed) for on-device combine (RCCL). */
 int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr);
 
+/* On-device combine for key-range sharded resolvers (one per GPU): on the caller's HIP stream
+ * `stream` (a hipStream_t, e.g. the stream an RCCL all-reduce runs on), after this batch's
+ * verdicts are final, write dev_out[dev_txn_ids[i]] = 2 - verdict[i] for each of the batch's
+ * transactions i (dev_out pre-zeroed by the caller).  An element-wise MAX all-reduce of dev_out
+ * over the resolvers then holds 2 - min(verdict), the proxy's combine
+ * (CommitProxyServer.actor.cpp:764-780).  The batch may be destroyed right after the call: its
+ * staging is not reused before the scatter has run. */
+int fdbcs_batch_scatter_conflict_bytes(fdbcs_batch* b, const int32_t* dev_txn_ids, uint8_t* dev_out, void* stream);
+
 /* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
  * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the
  * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead). */

@@ -89,3 +89,29 @@ def test_client_increments_on_engine(engine):
     for k in range(len(committed)):
         assert int.from_bytes(store.read(b"ctr%d" % k, store.version), "little") == committed[k]
     assert 0 < committed.sum() < 40 * 30
+
+
+def test_device_conflict_bytes_scatter(engine):
+    """fdbcs_batch_scatter_conflict_bytes writes 2 - verdict at each routed transaction's global
+    index on the caller's stream: the input of the multi-GPU MAX all-reduce (bench.py)."""
+    import torch
+
+    sh = KeyRangeSharding.uniform(2)
+    rng = np.random.default_rng(41)
+    cs = engine.ConflictSet(0)
+    now = 10
+    for _ in range(6):
+        pb = W.random_small_batch(rng, 400, alphabet=256, max_len=3, now=now, staleness=10)
+        part = sh.route(pb)[1]
+        b = engine.ConflictBatch(cs)
+        b.add_packed(part.batch)
+        b.detect_async(now, now - 5)
+        ids = torch.from_numpy(part.txn_ids.astype(np.int32)).cuda()
+        out = torch.zeros(pb.n_txn, dtype=torch.uint8, device="cuda")
+        b.scatter_conflict_bytes(ids.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        v = b.wait()
+        b.close()  # the slot may be reused at once: its next upload waits for the scatter
+        want = KeyRangeSharding.conflict_bytes(pb.n_txn, part, v)
+        assert np.array_equal(out.cpu().numpy(), want)
+        now += 3
+    cs.close()
