@@ -288,25 +288,26 @@ def main():
     cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, tail_total, maxT, maxR, maxW)
     verdicts = [None] * n_all
 
-    # Multi-GPU combine (CommitProxyServer.actor.cpp:764-780): each rank scatters 2 - verdict of its
-    # sub-batch into a zeroed T-byte buffer ON THE DEVICE (fdbcs_batch_scatter_conflict_bytes, on
-    # torch's stream after the batch's epilogue) and one RCCL MAX all-reduce combines them.  The
-    # routed transaction ids are uploaded once, like the inputs.  gloo (CPU rehearsals) combines
-    # host copies instead.
+    # Multi-GPU combine (CommitProxyServer.actor.cpp:764-780): each batch's stage B also writes its
+    # conflict bytes 2 - verdict at the routed transactions' global indices (0 elsewhere) into a
+    # T-byte device buffer (fdbcs_batch_set_conflict_output), complete when the batch is; one MAX
+    # all-reduce over the ranks (RCCL; gloo's CUDA all-reduce in one-GPU rehearsals) combines them.
     on_device = dist is not None and cdev != "cpu"
-    ids_dev = {}
+    outbuf = {}
     if on_device:
         for i in range(n_all):
-            ids_dev[i] = torch.from_numpy(routed[i].txn_ids.astype(np.int32)).to(cdev)
+            outbuf[i] = torch.empty(gbatches[i][0].n_txn, dtype=torch.uint8, device=cdev)
     combined = {}
 
-    def combine(i, o, v):
-        T = gbatches[i][0].n_txn
+    def attach(i, o):
         if on_device:
-            c = torch.zeros(T, dtype=torch.uint8, device=cdev)
-            o.scatter_conflict_bytes(ids_dev[i].data_ptr(), c.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            o.set_conflict_output(routed[i].txn_ids, gbatches[i][0].n_txn, outbuf[i].data_ptr())
+
+    def combine(i, v):
+        if on_device:
+            c = outbuf[i]
         else:
-            c = torch.from_numpy(KeyRangeSharding.conflict_bytes(T, routed[i], v)).to(cdev)
+            c = torch.from_numpy(KeyRangeSharding.conflict_bytes(gbatches[i][0].n_txn, routed[i], v)).to(cdev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
         combined[i] = c
 
@@ -323,7 +324,7 @@ def main():
             verdicts[j] = oj.wait()
             host["wait"] += pc() - t
             if dist is not None:
-                combine(j, oj, verdicts[j])
+                combine(j, verdicts[j])
             oj.close()
 
         for i in range(lo, hi):
@@ -332,6 +333,7 @@ def main():
             if objs is None:
                 o = C.ConflictBatch(cs)
                 o.add_packed(mine[i])
+                attach(i, o)
             else:
                 o = objs[i]
             t1 = pc()
@@ -349,6 +351,7 @@ def main():
         for i in range(lo, hi):
             o = C.ConflictBatch(cs)
             o.add_packed(mine[i])  # addTransaction: normalized into pinned staging, not uploaded
+            attach(i, o)
             objs[i] = o
         return objs
 
@@ -474,7 +477,7 @@ def main():
             dist.all_reduce(h, op=dist.ReduceOp.MAX)
             bad += int(not torch.equal(h, combined[i]))
         combine_check = {"batches": len(combined), "mismatched": bad,
-                         "path": (f"device scatter + {'RCCL' if args.backend == 'nccl' else 'gloo'} MAX all-reduce"
+                         "path": (f"device conflict bytes + {'RCCL' if args.backend == 'nccl' else 'gloo'} MAX all-reduce"
                                   if on_device else "host bytes + all-reduce")}
     parity = cpu_base = None
     if not args.no_cpu_baseline:

@@ -122,7 +122,7 @@ SIGNATURES = {
     "fdbcs_batch_wait": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "fdbcs_batch_conflicting_reads": (ctypes.c_int, [_VP, _I32, _VP, _I32, ctypes.POINTER(_I32)]),
     "fdbcs_batch_device_verdicts": (ctypes.c_int, [_VP, ctypes.POINTER(_VP)]),
-    "fdbcs_batch_scatter_conflict_bytes": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "fdbcs_batch_set_conflict_output": (ctypes.c_int, [_VP, _VP, ctypes.c_int32, _VP]),
     "fdbcs_debug_kernel_time": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "fdbcs_strerror": (ctypes.c_char_p, [ctypes.c_int]),
 }
@@ -374,13 +374,13 @@ class ConflictBatch:
         _check(load_library().fdbcs_batch_device_verdicts(self._h, ctypes.byref(p)), "deviceVerdicts")
         return p.value or 0
 
-    def scatter_conflict_bytes(self, dev_txn_ids: int, dev_out: int, stream: int) -> None:
-        """fdbcs_batch_scatter_conflict_bytes: dev_out[dev_txn_ids[i]] = 2 - verdict[i] on the
-        HIP stream `stream` (device pointers and a hipStream_t as integers, e.g. a torch tensor's
-        data_ptr() and torch.cuda.current_stream().cuda_stream)."""
-        _check(load_library().fdbcs_batch_scatter_conflict_bytes(self._h, ctypes.c_void_p(dev_txn_ids),
-                                                                 ctypes.c_void_p(dev_out), ctypes.c_void_p(stream)),
-               "scatterConflictBytes")
+    def set_conflict_output(self, txn_ids: np.ndarray, n_global: int, dev_out: int) -> None:
+        """fdbcs_batch_set_conflict_output: detect also writes the multi-resolver conflict bytes of
+        this batch's transactions (global indices `txn_ids`) into device memory `dev_out` (an
+        address, e.g. a torch tensor's data_ptr())."""
+        ids = np.ascontiguousarray(txn_ids, dtype=np.int32)
+        _check(load_library().fdbcs_batch_set_conflict_output(self._h, _VP(ids.ctypes.data if ids.size else 0),
+                                                              int(n_global), _VP(dev_out)), "setConflictOutput")
 
     def conflicting_reads(self, t: int) -> List[int]:
         L = load_library()

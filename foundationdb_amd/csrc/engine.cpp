@@ -204,10 +204,7 @@ struct BatchSlot {
     hipEvent_t ev_up = nullptr;    // upload done (recorded on stage A's stream)
     hipEvent_t ev_free = nullptr;  // the last batch using this slot finished on the device
     bool free_recorded = false;
-    // fdbcs_batch_scatter_conflict_bytes: the caller's stream read dverdict; the slot's next
-    // upload waits for ev_user (recorded on that stream after the scatter).
-    hipEvent_t ev_user = nullptr, ev_done = nullptr;
-    bool user_recorded = false;
+    HBuf pin_inv;  // fdbcs_batch_set_conflict_output: global -> batch transaction map (host-mapped)
 };
 
 struct fdbcs_batch {
@@ -242,6 +239,9 @@ struct fdbcs_batch {
     uint32_t recorded = 0;  // phases whose events were recorded (bit per Phase)
     bool any_report = false;
     int64_t check_hist = 0;  // boundaries (both tiers, upper bound) the read check searched
+    std::vector<int32_t> out_ids;  // fdbcs_batch_set_conflict_output: global index per transaction
+    int32_t out_n = 0;
+    uint8_t* out_dev = nullptr;
     int64_t wtail = 0;       // history tail bytes the batch's write endpoints could add (8-byte padded)
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
@@ -577,8 +577,6 @@ void release_slot(BatchSlot* sl) {
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
     if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
-    if (sl->ev_user) (void)hipEventDestroy(sl->ev_user);
-    if (sl->ev_done) (void)hipEventDestroy(sl->ev_done);
     sl->dev.release();
     sl->dverdict.release();
     sl->pin_in.release();
@@ -709,13 +707,7 @@ int do_upload(fdbcs_batch* b) {
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
     if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess)
         fdb_event(LaunchList::kSyncWait, sl->ev_free, cs->astream);
-    if (sl->user_recorded) {  // an external stream still reads this slot's verdict bytes
-        if (hipEventQuery(sl->ev_user) != hipSuccess) {
-            HIPOK(hipStreamWaitEvent(cs->astream, sl->ev_user, 0));
-            HIPOK(hipStreamWaitEvent(cs->stream, sl->ev_user, 0));
-        }
-        sl->user_recorded = false;
-    }
+
     if (cs->dma_upload && !t_record) {
         HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
     } else {
@@ -1351,6 +1343,15 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     b->h_hist = (uint8_t*)(ho + o_hc);
     b->h_first = (int32_t*)(ho + o_fc);
     if ((rc = sl->dverdict.ensure(T + 64))) return rc;
+    if (b->out_dev && b->out_n > 0) {
+        // global -> batch transaction map, read by k_conflict_output straight from host-mapped
+        // memory (n_global * 4 bytes; the slot's previous batch finished with it: its flag was seen)
+        if ((int64_t)b->out_ids.size() != T) return FDBCS_E_STATE;  // transactions added after the call
+        if ((rc = sl->pin_inv.ensure(4 * (size_t)b->out_n + 64, true))) return rc;
+        int32_t* inv = (int32_t*)sl->pin_inv.p;
+        std::fill(inv, inv + b->out_n, -1);
+        for (int32_t t = 0; t < (int32_t)T; t++) inv[b->out_ids[t]] = t;
+    }
     b->any_report = false;
     for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
     b->seq = ++cs->seq;
@@ -1437,6 +1438,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhCheck);
     if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp);
+    if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
+        launch_conflict_output(s, bd, w, (const int32_t*)sl->pin_inv.dp, b->out_n, b->out_dev);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf (into the host-mapped results)
         char* hdv = (char*)sl->pin_out.dp;
         if (R) launch_copy_bytes(s, hdv + o_rc, w.rconf, R);
@@ -1717,24 +1720,16 @@ int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr) {
     return FDBCS_OK;
 }
 
-int fdbcs_batch_scatter_conflict_bytes(fdbcs_batch* b, const int32_t* dev_txn_ids, uint8_t* dev_out, void* stream) {
-    if (!b || (!dev_txn_ids && b->T() > 0) || (!dev_out && b->T() > 0)) return FDBCS_E_INVALID;
-    if (!b->cs || b->state < 2) return FDBCS_E_STATE;
-    fdbcs_conflict_set* cs = b->cs;
-    HIPOK(hipSetDevice(cs->device));
-    if (cs->pending_batch == b)
-        if (int rc = flush_pending(cs)) return rc;
-    BatchSlot* sl = b->slot;
-    hipStream_t st = (hipStream_t)stream;
-    if (!sl->ev_done) HIPOK(hipEventCreateWithFlags(&sl->ev_done, hipEventDisableTiming));
-    if (!sl->ev_user) HIPOK(hipEventCreateWithFlags(&sl->ev_user, hipEventDisableTiming));
-    // everything submitted to the batch-order stream so far includes this batch's epilogue
-    HIPOK(hipEventRecord(sl->ev_done, cs->stream));
-    HIPOK(hipStreamWaitEvent(st, sl->ev_done, 0));
-    launch_scatter_conflicts(st, (const uint8_t*)sl->dverdict.p, dev_txn_ids, b->T(), dev_out);
-    HIPOK(hipGetLastError());
-    HIPOK(hipEventRecord(sl->ev_user, st));
-    sl->user_recorded = true;
+int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int32_t n_global, uint8_t* dev_out) {
+    if (!b || n_global < 0 || (n_global > 0 && !dev_out)) return FDBCS_E_INVALID;
+    if (!b->cs || b->state >= 2) return FDBCS_E_STATE;
+    const int32_t T = b->T();
+    if (T > 0 && !txn_ids) return FDBCS_E_INVALID;
+    for (int32_t t = 0; t < T; t++)
+        if (txn_ids[t] < 0 || txn_ids[t] >= n_global) return FDBCS_E_INVALID;
+    b->out_ids.assign(txn_ids, txn_ids + T);
+    b->out_n = n_global;
+    b->out_dev = dev_out;
     return FDBCS_OK;
 }
 

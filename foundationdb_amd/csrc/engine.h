@@ -240,8 +240,9 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, c
                Scalars* sc, int64_t oldest, int64_t header_version, int64_t grid_hint_n);
 // Byte copy (device -> host-mapped result buffer), as a kernel.
 void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n);
-// out[ids[i]] = 2 - verdict[i] for i < n (multi-GPU conflict bytes), on the caller's stream.
-void launch_scatter_conflicts(hipStream_t s, const uint8_t* verdict, const int32_t* ids, int64_t n, uint8_t* out);
+// Multi-resolver conflict bytes out[g] = 2 - verdict of batch transaction inv[g] (0 if inv[g] < 0).
+void launch_conflict_output(hipStream_t s, const BatchDev& b, const Work& w, const int32_t* inv, int64_t n,
+                            uint8_t* out);
 // H2D of `bytes` (16-byte multiple, both sides 16-aligned) from host-mapped pinned memory, as a kernel.
 void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes, int max_blocks);
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);

@@ -2558,19 +2558,29 @@ void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n) {
     fdb_launch(k_copy_bytes, dim3((unsigned)blocks), dim3(kBlock), 0, s, (uint8_t*)dst, (const uint8_t*)src, n);
 }
 
-// On-device combine input (multi-GPU): out[ids[i]] = 2 - verdict[i], the conflict byte the RCCL
-// MAX all-reduce combines (CommitProxyServer.actor.cpp:764-780 as a max of 2 - verdict).
-__global__ __launch_bounds__(kBlock) void k_scatter_conflicts(const uint8_t* __restrict__ v, const int32_t* __restrict__ ids,
-                                                              int64_t n, uint8_t* __restrict__ out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        out[ids[i]] = (uint8_t)(2 - v[i]);
+// Multi-resolver combine input (fdbcs_batch_set_conflict_output): out[g] = 2 - verdict of the
+// batch transaction inv[g] (0 where the global transaction was not routed here); an element-wise
+// MAX all-reduce over resolvers then holds 2 - min(verdict) (CommitProxyServer.actor.cpp:764-780).
+// inv is host-mapped (n_global int32 over PCIe, read once).  Runs after k_resolve on the
+// batch-order stream, so it is complete before the epilogue publishes the completion flag.
+__global__ __launch_bounds__(kBlock) void k_conflict_output(BatchDev b, const uint8_t* __restrict__ status,
+                                                            const int32_t* __restrict__ inv, int64_t n,
+                                                            uint8_t* __restrict__ out) {
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x) {
+        const int t = inv[g];
+        uint8_t c = 0;
+        if (t >= 0) c = (uint8_t)(2 - verdict_byte(b, t, status[t]));
+        out[g] = c;
+    }
 }
 
-void launch_scatter_conflicts(hipStream_t s, const uint8_t* verdict, const int32_t* ids, int64_t n, uint8_t* out) {
+void launch_conflict_output(hipStream_t s, const BatchDev& b, const Work& w, const int32_t* inv, int64_t n,
+                            uint8_t* out) {
     if (n <= 0) return;
     int64_t blocks = (n + kBlock - 1) / kBlock;
     blocks = blocks > 1024 ? 1024 : blocks;
-    fdb_launch(k_scatter_conflicts, dim3((unsigned)blocks), dim3(kBlock), 0, s, verdict, ids, n, out);
+    fdb_launch(k_conflict_output, dim3((unsigned)blocks), dim3(kBlock), 0, s, b, (const uint8_t*)w.status, inv, n,
+               out);
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {

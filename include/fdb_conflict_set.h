@@ -193,14 +193,14 @@ int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out,
  * detect until the batch is destroyed) for on-device combine (RCCL). */
 int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr);
 
-/* On-device combine for key-range sharded resolvers (one per GPU): on the caller's HIP stream
- * `stream` (a hipStream_t, e.g. the stream an RCCL all-reduce runs on), after this batch's
- * verdicts are final, write dev_out[dev_txn_ids[i]] = 2 - verdict[i] for each of the batch's
- * transactions i (dev_out pre-zeroed by the caller).  An element-wise MAX all-reduce of dev_out
- * over the resolvers then holds 2 - min(verdict), the proxy's combine
- * (CommitProxyServer.actor.cpp:764-780).  The batch may be destroyed right after the call: its
- * staging is not reused before the scatter has run. */
-int fdbcs_batch_scatter_conflict_bytes(fdbcs_batch* b, const int32_t* dev_txn_ids, uint8_t* dev_out, void* stream);
+/* On-device combine for key-range sharded resolvers (one per GPU).  Call after the batch's
+ * transactions are added and before detect: txn_ids[t] in [0, n_global) is the global index (in
+ * the proxy's batch) of the batch's transaction t.  Detect then also writes dev_out[0, n_global)
+ * (device memory of this GPU, any allocator) with the conflict byte 2 - verdict of each routed
+ * transaction and 0 elsewhere, complete when the batch is (fdbcs_batch_wait returns).  An
+ * element-wise MAX all-reduce of dev_out over the resolvers holds 2 - min(verdict), the proxy's
+ * combine (CommitProxyServer.actor.cpp:764-780). */
+int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int32_t n_global, uint8_t* dev_out);
 
 /* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
  * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the

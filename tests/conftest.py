@@ -23,6 +23,11 @@ def oracle_built():
 @pytest.fixture(scope="session")
 def engine():
     """The HIP engine; GPU tests only.  Builds in-tree if needed and fails loudly without a device."""
+    import torch
+
+    # torch ships its own HIP runtime: let it probe the device before the engine's runtime
+    # initializes (the order bench.py uses), so tests can hand torch device memory to the engine
+    torch.cuda.is_available()
     from foundationdb_amd import build, conflict_set
 
     os.environ.setdefault("FDBCS_VALIDATE", "1")  # device-side sort/permutation invariant checks

@@ -37,4 +37,4 @@ def test_two_rank_bench_parity(engine, workload):
     assert out["n_gpus"] == 2 and out["value"] > 0
     assert out["parity"]["batches_checked"] >= 2 * 10 and out["parity"]["mismatched_batches"] == 0
     assert out["combine_check"]["mismatched"] == 0 and out["combine_check"]["batches"] == 10
-    assert out["combine_check"]["path"].startswith("device scatter")
+    assert out["combine_check"]["path"].startswith("device conflict bytes")

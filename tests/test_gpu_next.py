@@ -91,9 +91,10 @@ def test_client_increments_on_engine(engine):
     assert 0 < committed.sum() < 40 * 30
 
 
-def test_device_conflict_bytes_scatter(engine):
-    """fdbcs_batch_scatter_conflict_bytes writes 2 - verdict at each routed transaction's global
-    index on the caller's stream: the input of the multi-GPU MAX all-reduce (bench.py)."""
+def test_device_conflict_output(engine):
+    """fdbcs_batch_set_conflict_output: detect also writes 2 - verdict at each routed transaction's
+    global index (0 elsewhere) into torch-allocated device memory, complete when the batch is:
+    the input of the multi-GPU MAX all-reduce (bench.py)."""
     import torch
 
     sh = KeyRangeSharding.uniform(2)
@@ -103,14 +104,14 @@ def test_device_conflict_bytes_scatter(engine):
     for _ in range(6):
         pb = W.random_small_batch(rng, 400, alphabet=256, max_len=3, now=now, staleness=10)
         part = sh.route(pb)[1]
+        out = torch.full((pb.n_txn,), 7, dtype=torch.uint8, device="cuda")  # every byte is written
+        torch.cuda.synchronize()  # torch's fill is on torch's stream: finish it before the engine writes
         b = engine.ConflictBatch(cs)
         b.add_packed(part.batch)
+        b.set_conflict_output(part.txn_ids, pb.n_txn, out.data_ptr())
         b.detect_async(now, now - 5)
-        ids = torch.from_numpy(part.txn_ids.astype(np.int32)).cuda()
-        out = torch.zeros(pb.n_txn, dtype=torch.uint8, device="cuda")
-        b.scatter_conflict_bytes(ids.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
         v = b.wait()
-        b.close()  # the slot may be reused at once: its next upload waits for the scatter
+        b.close()
         want = KeyRangeSharding.conflict_bytes(pb.n_txn, part, v)
         assert np.array_equal(out.cpu().numpy(), want)
         now += 3
