@@ -31,7 +31,7 @@ def test_two_rank_bench_parity(engine, workload):
            "--backend", "gloo", "--cpu-seconds", "20"]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, "\n".join([l for l in r.stderr.splitlines() if "[rank1]" in l][-30:]) + r.stderr[-1500:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0

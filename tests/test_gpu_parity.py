@@ -410,3 +410,29 @@ def test_batch_outliving_its_set_is_refused_not_corrupting(engine):
         assert ex.value.status == engine.FDBCS_E_STATE
         pending.close()
         done.close()
+
+
+def test_empty_batches(engine, oracle_mod):
+    """A resolver receives a request every batch even when no transaction routed to it has ranges
+    there (Resolver.actor.cpp:103-310): empty batches and transactions without ranges must still
+    advance the set (oldest version, GC) and agree with the oracle afterwards."""
+    from tests.helpers import EngineDriver
+
+    eng = EngineDriver(engine)
+    ora = oracle_mod.OracleConflictSet()
+    rng = np.random.default_rng(61)
+    now = 10
+    empty = PackedBatch.from_transactions([])
+    no_ranges = PackedBatch.from_transactions([CommitTransaction([], [], now - 1) for _ in range(5)])
+    for i in range(12):
+        if i % 3 == 0:
+            pb = empty
+        elif i % 3 == 1:
+            pb = no_ranges
+        else:
+            pb = W.random_small_batch(rng, 200, alphabet=8, max_len=2, now=now, staleness=15)
+        ve, ce = eng.detect(pb, now, now - 12)
+        vo, co = ora.detect(pb, now, now - 12)
+        assert (ve == vo).all()
+        assert ce == {t: sorted(v) for t, v in co.items()}
+        now += 4
