@@ -524,7 +524,7 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
     cs->delta_cap = cap;
     launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->nd,
                     cs->dlvl3_n, std::max<int64_t>(cs->nd_ub, 1));
-    HIPOK(hipGetLastError());
+    HIPOK(take_launch_error());
     HIPOK(hipStreamSynchronize(cs->stream));
     return ensure_scan_arena(cs);
 }
@@ -543,7 +543,7 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
         cs->hist_cap = cap;
         launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n,
                         cs->lvl3_n, std::max<int64_t>(cs->n_ub, 1));
-        HIPOK(hipGetLastError());
+        HIPOK(take_launch_error());
     }
     if (tail_need > cs->tail_cap) {
         int64_t tcap = std::max<int64_t>(tail_need, cs->tail_cap);
@@ -712,7 +712,7 @@ int do_upload(fdbcs_batch* b) {
         HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
     } else {
         launch_upload(cs->astream, sl->pin_in.dp, sl->dev.p, (int64_t)L.total, cs->upload_blocks);
-        if (!t_record) HIPOK(hipGetLastError());
+        if (!t_record) HIPOK(take_launch_error());
     }
     fdb_event(LaunchList::kSyncRecord, sl->ev_up, cs->astream);
     char* d = (char*)sl->dev.p;
@@ -1043,7 +1043,7 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
     launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n, cs->lvl3_n,
                     std::max<int64_t>(n, 1));
-    HIPOK(hipGetLastError());
+    HIPOK(take_launch_error());
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
     cs->max_written = maxv;
@@ -1519,7 +1519,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (flush_pending(cs)) return FDBCS_E_DEVICE;
         HIPOK(la.replay(sa));
         HIPOK(lb.replay(s));
-        HIPOK(hipGetLastError());
+        HIPOK(take_launch_error());
     }
     cs->stats.host_ms_submit += host_ms_since(t_sub);
     cs->stats.graph_launches = cs->graph_launches;

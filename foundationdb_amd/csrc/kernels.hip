@@ -21,6 +21,7 @@
 namespace fdbcs {
 
 thread_local LaunchList* t_record = nullptr;
+thread_local hipError_t t_launch_error = hipSuccess;
 
 // ------------------------------------------------------------------ helpers
 

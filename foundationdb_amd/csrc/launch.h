@@ -91,6 +91,15 @@ struct LaunchList {
 
 // Non-null while the engine records a stage: fdb_launch / fdb_event append to it.
 extern thread_local LaunchList* t_record;
+// First failed direct launch since the last take_launch_error().  The engine checks its own
+// launches this way rather than with hipGetLastError(), whose per-thread "last error" also holds
+// failures of other HIP users in the process (torch shares the runtime) that they never cleared.
+extern thread_local hipError_t t_launch_error;
+inline hipError_t take_launch_error() {
+    const hipError_t e = t_launch_error;
+    t_launch_error = hipSuccess;
+    return e;
+}
 
 template <typename... P, typename... A>
 inline void fdb_launch(void (*k)(P...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, A&&... a) {
@@ -106,7 +115,8 @@ inline void fdb_launch(void (*k)(P...), dim3 grid, dim3 block, uint32_t shmem, h
     std::apply(
         [&](auto&... v) {
             void* args[] = {(void*)&v..., nullptr};
-            (void)hipLaunchKernel((const void*)k, grid, block, args, shmem, s);
+            const hipError_t e = hipLaunchKernel((const void*)k, grid, block, args, shmem, s);
+            if (e != hipSuccess && t_launch_error == hipSuccess) t_launch_error = e;
         },
         vals);
 }
