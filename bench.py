@@ -72,6 +72,11 @@ def parse():
                     help="bound on the CPU replay (parity + cpu_baseline); batches past it are not checked")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU replay (no parity, no baseline)")
     ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4"])
+    ap.add_argument("--reshard", action="store_true",
+                    help="N>1: dynamic resharding (resolver iops samples + resolutionBalancing + keyResolvers "
+                    "history, foundationdb_amd/balancing.py) instead of the static split")
+    ap.add_argument("--reshard-preroll", type=int, default=200,
+                    help="global batches routed (not resolved) to train the balancer before the run")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the verdict all-reduce (nccl = RCCL over xGMI)")
     return ap.parse_args()
@@ -101,7 +106,32 @@ def sharding_for(args, p, world):
         return KeyRangeSharding([W.c4_user_split(p, g * p.users // world) for g in range(1, world)])
     if args.workload == "c1":  # setK keys share 12 bytes of '.': split on the integer
         return KeyRangeSharding([W.setk([g * 20_000_000 // world])[0].tobytes() for g in range(1, world)])
+    if args.workload == "c3":  # Mako keys share 'mako': split on the item index (Zipf: rank 0 is hot)
+        return KeyRangeSharding([W.mako_keys(np.array([g * 1_000_000 // world]))[0].tobytes() for g in range(1, world)])
     return KeyRangeSharding.uniform(world)
+
+
+def route_all(args, p, world, gbatches):
+    """Per global batch, the ShardBatches of every rank (identical on all ranks: the routing and the
+    balancer are deterministic functions of the global batches)."""
+    from foundationdb_amd import balancing as B
+    from foundationdb_amd.sharding import KeyResolvers
+
+    sh = sharding_for(args, p, world)
+    if sh is None:
+        return None, None
+    if not args.reshard:
+        return [sh.route(pb) for pb, _, _ in gbatches], None
+    # compressed time: balance every 20 batches (MIN_BALANCE_TIME is 0.2 s = 200 batches at 1e6
+    # versions/s); the reference's simulation knobs for the sample and the threshold
+    br = B.BalancedRouting(world, KeyResolvers.from_sharding(sh), seed=args.seed, min_balance_difference=10_000,
+                           balance_time=20 * p.version_step / B.VERSIONS_PER_SECOND, key_bytes_per_sample=1_000)
+    first = gbatches[0][1] - p.version_step * (args.reshard_preroll + 1)
+    pre = make_batches(args, p, args.reshard_preroll, world, first, seed_offset=7919)
+    for pb, now, _ in pre:
+        br.route(pb, now)
+    routed = [br.route(pb, now) for pb, now, _ in gbatches]
+    return routed, {"moves": br.balancer.moves_made, "map": [(b.hex(), o) for b, o in br.kr.current_map()]}
 
 
 def shard_history(args, p, seed, rank, world, start_version):
@@ -132,15 +162,15 @@ def shard_history(args, p, seed, rank, world, start_version):
     return kb, ko, vers
 
 
-def make_batches(args, p, n_batches, world, start_version):
+def make_batches(args, p, n_batches, world, start_version, seed_offset=0):
     """Global batches (identical on every rank) with their (now, newOldest)."""
     from foundationdb_amd import workloads as W
 
     import dataclasses
 
     if args.workload == "c1":  # skipListTest: snapshot v, now v + 50, newOldest v (SkipList.cpp:1063-1077)
-        return list(W.c1_batches(n_batches, seed=args.seed, data_per_batch=2 * p.txns * world))
-    rng = np.random.default_rng(args.seed)
+        return list(W.c1_batches(n_batches, seed=args.seed + seed_offset, data_per_batch=2 * p.txns * world))
+    rng = np.random.default_rng(args.seed + seed_offset)
     zipf = W.ZipfGenerator(1_000_000, 0.99) if args.workload == "c3" else None
     gp = dataclasses.replace(p, txns=p.txns * world)
     out = []
@@ -265,8 +295,11 @@ def main():
     total_lo, total_hi = res_hi, res_hi + n_total
     n_all = total_hi + args.breakdown_steps
     gbatches = make_batches(args, p, n_all, world, start_version)
-    sharding = sharding_for(args, p, world)
-    routed = [sharding.route(pb)[rank] for pb, _, _ in gbatches] if sharding else None
+    all_routed, reshard = route_all(args, p, world, gbatches)
+    routed = [r[rank] for r in all_routed] if all_routed else None
+    if all_routed:
+        shares = np.array([[r[g].batch.n_txn for g in range(world)] for r in all_routed]).sum(0)
+        log(f"[rank {rank}] routed sub-transactions per rank: {shares.tolist()}")
     log(f"[rank {rank}] generated history {len(vers)} + {n_all} batches in {time.time() - t0:.1f}s")
 
     cs = C.ConflictSet(device)
@@ -530,6 +563,7 @@ def main():
         "total_note": "reference 'total' (SkipList.cpp:1082-1085): addTransaction + detect, per batch in the loop",
         "parity": parity,
         "combine_check": combine_check,
+        "reshard": reshard,
         "history_boundaries_end": hist_end,
         "phase_ms_per_batch": phase,
         "compactions": st["compactions"],

@@ -22,13 +22,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("workload", ["c2", "c3"])
-def test_two_rank_bench_parity(engine, workload):
+@pytest.mark.parametrize("workload,extra", [("c2", []), ("c3", []), ("c3", ["--reshard", "--reshard-preroll", "60"])])
+def test_two_rank_bench_parity(engine, workload, extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--workload", workload, "--steps", "8", "--warmup", "2", "--txns", "1000",
            "--history", "200000", "--resident-steps", "0", "--total-steps", "0", "--breakdown-steps", "0",
-           "--backend", "gloo", "--cpu-seconds", "20"]
+           "--backend", "gloo", "--cpu-seconds", "20"] + extra
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, "\n".join([l for l in r.stderr.splitlines() if "[rank1]" in l][-30:]) + r.stderr[-1500:]
@@ -38,3 +38,5 @@ def test_two_rank_bench_parity(engine, workload):
     assert out["parity"]["batches_checked"] >= 2 * 10 and out["parity"]["mismatched_batches"] == 0
     assert out["combine_check"]["mismatched"] == 0 and out["combine_check"]["batches"] == 10
     assert out["combine_check"]["path"].startswith("device conflict bytes")
+    if extra:
+        assert out["reshard"]["moves"] > 0  # the hot rank gave key ranges away
