@@ -242,6 +242,7 @@ struct fdbcs_batch {
     std::vector<int32_t> out_ids;  // fdbcs_batch_set_conflict_output: global index per transaction
     int32_t out_n = 0;
     uint8_t* out_dev = nullptr;
+    int32_t max_len = 0;  // longest key added (the sort stages tail windows only past kSortNxLen)
     int64_t wtail = 0;       // history tail bytes the batch's write endpoints could add (8-byte padded)
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
@@ -259,6 +260,7 @@ void add_key(fdbcs_batch* b, std::vector<DKey>& out, const uint8_t* p, int32_t l
     dkey_prefix(p, (uint32_t)len, &k.hi, &k.lo);
     k.len = (uint32_t)len;
     k.tail = 0;
+    if (len > b->max_len) b->max_len = len;
     if (len > 16) {
         k.tail = (uint32_t)b->tail.size();
         b->tail.insert(b->tail.end(), p + 16, p + len);
@@ -1203,6 +1205,7 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
         fast_prefix(p, len, &out->hi, &out->lo);
         out->len = len;
         out->tail = 0;
+        if ((int32_t)len > b->max_len) b->max_len = (int32_t)len;
         if (len > 16) {
             out->tail = (uint32_t)tb;
             memcpy(tail + tb, p + 16, len - 16);
@@ -1421,7 +1424,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
     int sorted = 0;
     launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted, rec(kPhSortBegin, 1),
-                       rec(kPhSortEnd, 1));
+                       rec(kPhSortEnd, 1), b->max_len > (int32_t)kSortNxLen);
     mark(kPhSort);
     launch_positions(sa, bd, w, sorted);
     if (cs->validate) launch_validate_sort(sa, bd, w, sorted);

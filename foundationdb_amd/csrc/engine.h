@@ -217,7 +217,8 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
 // alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
 // sort_begin / sort_end (optional): events around the per-bucket sort kernel (roofline timing).
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per, int alg,
-                        int* result_buffer, hipEvent_t sort_begin = nullptr, hipEvent_t sort_end = nullptr);
+                        int* result_buffer, hipEvent_t sort_begin = nullptr, hipEvent_t sort_end = nullptr,
+                        bool long_keys = true);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);

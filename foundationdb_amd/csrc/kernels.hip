@@ -1261,9 +1261,47 @@ __device__ __forceinline__ int rank_shared_hi(const SortItem* sh, const uint64_t
 
 constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by one workgroup
 
+// Tail windows: bytes [16, 16 + 8 kTailWin) of a bucket's long keys, as big-endian words zero-padded
+// past each key's end, staged in LDS once per item so the comparisons among keys that share their
+// 16-byte prefix (C4: every key of one user; a range's begin and end) read LDS instead of issuing
+// dependent global loads per pair.  Zero padding keeps the order exact: equal words over the
+// shorter tail's words leave the shorter key first, which the length compare then decides.
+constexpr int kTailWin = 12;  // 96 tail bytes: keys up to 112 bytes compare without the arena
+__device__ __forceinline__ void load_tail_window(uint64_t* win, const uint8_t* arena, uint32_t tail, uint32_t len) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t n = len > 16u ? len - 16u : 0u;
+    uint64_t w[kTailWin];
+#pragma unroll
+    for (int j = 0; j < kTailWin; j++) w[j] = (uint32_t)(8 * j) < n ? tail_word(arena + tail + 8 * j) : 0ull;
+#pragma unroll
+    for (int j = 0; j < kTailWin; j++) {
+        const int vb = (int)n - 8 * j;  // bytes of word j inside the tail
+        win[j] = vb >= 8 ? w[j] : (vb <= 0 ? 0ull : w[j] & (~0ull << (64 - 8 * vb)));
+    }
+#endif
+}
+// item_less_tail with both keys' windows in LDS (arena only past the windows).
+__device__ __forceinline__ bool item_less_tail_win(const uint64_t* wa, uint32_t alen, uint32_t atail, uint32_t ameta,
+                                                   const uint64_t* wb, uint32_t blen, uint32_t btail, uint32_t bmeta,
+                                                   const uint8_t* arena) {
+    const uint32_t m = (alen < blen ? alen : blen) - 16u;  // common tail bytes
+    const int nw = (int)((m + 7u) / 8u);
+    const int k = nw < kTailWin ? nw : kTailWin;
+    for (int j = 0; j < k; j++)
+        if (wa[j] != wb[j]) return wa[j] < wb[j];
+    if (nw > kTailWin)  // both tails run past the window: the rest from the arena
+        return item_less_tail(alen, atail, ameta, blen, btail, bmeta, arena);
+    if (alen != blen) return alen < blen;
+    const uint32_t ca = item_class(ameta), cb = item_class(bmeta);
+    if (ca != cb) return ca < cb;
+    return ameta < bmeta;
+}
+
 // Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic network padded to a
 // power of two; oversized buckets (skewed sample) sort kBitonicMax chunks, then merge through memory.
-template <int ALG>
+// WIN: the batch has keys longer than kSortNxLen (tail windows staged in LDS; a separate
+// instantiation keeps the LDS footprint, and the occupancy, of short-key batches unchanged).
+template <int ALG, bool WIN>
 __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
                                                               const uint8_t* arena) {
     __shared__ SortItem sh[kBitonicMax];  // exchange buffer
@@ -1277,6 +1315,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
         // Two items per LDS read, two VALU ops per comparison.
         __shared__ __attribute__((aligned(16))) uint64_t shi[kBitonicMax];
         __shared__ uint64_t slo[kBitonicMax], saux[kBitonicMax];
+        __shared__ uint64_t swin[WIN ? kBitonicMax : 1][kTailWin];
         SortItem x{};
         if (t < m) {
             sh[t] = x = a[off + t];
@@ -1284,6 +1323,9 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
             slo[t] = x.lo;
             saux[t] = item_aux(x);
         }
+        // keys longer than kSortNxLen may tie on (prefix, bytes 16-18): stage their tail windows
+        const bool lng = WIN && t < m && x.len > kSortNxLen;
+        if (WIN && __syncthreads_or(lng) && lng) load_tail_window(swin[t], arena, x.tail, x.len);
         __syncthreads();
         if (t < m) {
             int lt = 0, eq = 0;
@@ -1311,8 +1353,28 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 // items per step with every LDS load issued first (a read [k, k + d) shares the
                 // hi word with its own end; a hot key fills whole buckets with one prefix).
                 const uint64_t ax = saux[t], ml = x.lo;
-                if (((ax >> 32) & 31u) == kSortNxLen + 1) {
-                    lt += rank_shared_hi(sh, shi, m, t, x, arena);
+                if (!WIN && ((ax >> 32) & 31u) == kSortNxLen + 1) {
+                    lt += rank_shared_hi(sh, shi, m, t, x, arena);  // not reached: WIN covers long keys
+                } else if (((ax >> 32) & 31u) == kSortNxLen + 1) {
+                    // long key: (low word, tie-break word) decide unless both are long with equal
+                    // bytes 16-18; those compare tail windows in LDS
+                    for (int q = 0; q < m; q++) {
+                        if (shi[q] != mh || q == t) continue;
+                        const uint64_t l = slo[q];
+                        if (l != ml) {
+                            lt += l < ml;
+                            continue;
+                        }
+                        const uint64_t w = saux[q];
+                        if (((w >> 32) & 31u) == kSortNxLen + 1 && (w >> 37) == (ax >> 37)) {
+                            const SortItem y = sh[q];
+                            lt += item_less_tail_win(swin[q], y.len, y.tail, y.meta, swin[t], x.len, x.tail, x.meta, arena)
+                                      ? 1
+                                      : 0;
+                        } else {
+                            lt += w < ax;
+                        }
+                    }
                 } else {
                     int q = 0;
                     for (; q + 4 <= m; q += 4) {
@@ -1422,7 +1484,7 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
-                        int alg, int* result_buffer, hipEvent_t sort_begin, hipEvent_t sort_end) {
+                        int alg, int* result_buffer, hipEvent_t sort_begin, hipEvent_t sort_end, bool long_keys) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
@@ -1434,9 +1496,11 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
                        w.items[0]);
     fdb_event(LaunchList::kTimingRecord, sort_begin, s);
     if (alg == 1)
-        fdb_launch(k_bucket_sort<1>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        fdb_launch(k_bucket_sort<1, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+    else if (long_keys)
+        fdb_launch(k_bucket_sort<0, true>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
     else
-        fdb_launch(k_bucket_sort<0>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        fdb_launch(k_bucket_sort<0, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
     fdb_event(LaunchList::kTimingRecord, sort_end, s);
 }
 
