@@ -168,6 +168,7 @@ struct fdbcs_conflict_set {
     int upload_blocks = 32;   // FDBCS_UPLOAD_BLOCKS: workgroups of the k_upload kernel
     int check_version = 1;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants)
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
+    bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -858,6 +859,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
     if (const char* v = getenv("FDBCS_GRAPH")) cs->use_graph = v[0] != '0';
+    if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
@@ -1424,7 +1426,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
     int sorted = 0;
     launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted, rec(kPhSortBegin, 1),
-                       rec(kPhSortEnd, 1), b->max_len > (int32_t)kSortNxLen);
+                       rec(kPhSortEnd, 1), cs->sort_win && b->max_len > (int32_t)kSortNxLen);
     mark(kPhSort);
     launch_positions(sa, bd, w, sorted);
     if (cs->validate) launch_validate_sort(sa, bd, w, sorted);

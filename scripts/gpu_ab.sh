@@ -19,6 +19,7 @@ k = d.get("kernels", {})
 print(sys.argv[2], "| value %.2fM resident %s total %s" % (d["value"] / 1e6, d.get("device_resident_txns_per_s"), d.get("total_txns_per_s")),
       "| host", {a: round(b, 3) for a, b in (d.get("host_ms_per_batch") or {}).items()},
       "| check_us", round(k["check"]["avg_launch_ms"] * 1e3, 1) if "check" in k else None,
+      "| sort_us", round(k["sort"]["avg_launch_ms"] * 1e3, 1) if "sort" in k else None,
       "| parity", (d.get("parity") or {}).get("mismatched_batches"))
 PY
 done
