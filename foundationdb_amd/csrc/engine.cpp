@@ -1739,7 +1739,7 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
 }
 
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch) {
-    if (!b || !us_per_launch || reps <= 0 || which != 0) return FDBCS_E_INVALID;
+    if (!b || !us_per_launch || reps <= 0 || which < 0 || which > 4) return FDBCS_E_INVALID;
     if (!b->cs) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
     HIPOK(hipSetDevice(cs->device));
@@ -1754,6 +1754,11 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     Scalars* sc = (Scalars*)cs->scal.p;
     const Tier base{hist_of(cs, cs->cur), levels_of(cs, cs->cur), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->nd, kHole};
+    if (which >= 1) {  // the sort kernels
+        HIPOK(debug_time_sort(cs->stream, b->bd, w, cs->bucket_target, cs->sample_per,
+                              cs->sort_win && b->max_len > (int32_t)kSortNxLen, which, reps, us_per_launch));
+        return FDBCS_OK;
+    }
     hipEvent_t e0, e1;
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));

@@ -220,6 +220,8 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
                         int* result_buffer, hipEvent_t sort_begin = nullptr, hipEvent_t sort_end = nullptr,
                         bool long_keys = true);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
+hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
+                           bool long_keys, int which, int reps, double* us);
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);
 // verdict_out: the batch's host-mapped verdict bytes (the epilogue publishes them with the flag).

@@ -1504,6 +1504,57 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
     fdb_event(LaunchList::kTimingRecord, sort_end, s);
 }
 
+// Diagnostics (fdbcs_debug_kernel_time, which 1-4): isolated device time of one sort kernel
+// (1 k_sample, 2 k_bucket_count, 3 k_bucket_scatter, 4 k_bucket_sort) over `reps` runs of the
+// whole sort on an idle stream; the zeroed scratch is reset before each run, outside the timing.
+hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
+                           bool long_keys, int which, int reps, double* us) {
+    const int E = 2 * (b.R + b.W);
+    if (E == 0) return hipErrorInvalidValue;
+    const int nb = sort_buckets(E, bucket_target);
+    const int grid = (E + kBlock - 1) / kBlock;
+    const int S = nb > 1 ? sample_count(E, nb, sample_per) : 0;
+    hipEvent_t e0, e1;
+    hipError_t err;
+    if ((err = hipEventCreate(&e0)) || (err = hipEventCreate(&e1))) return err;
+    double total = 0;
+    for (int r = 0; r < reps && err == hipSuccess; r++) {
+        (void)hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), s);
+        (void)hipMemsetAsync(w.bcount, 0, 4 * kMaxBuckets, s);
+        (void)hipMemsetAsync(w.bcursor, 0, 4 * kMaxBuckets, s);
+        auto at = [&](int k) { if (which == k) (void)hipEventRecord(e0, s); };
+        auto after = [&](int k) { if (which == k) (void)hipEventRecord(e1, s); };
+        at(1);
+        launch_sample(s, b, w, bucket_target, sample_per);
+        after(1);
+        at(2);
+        fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
+        after(2);
+        at(3);
+        fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
+                   w.items[0]);
+        after(3);
+        at(4);
+        if (long_keys)
+            fdb_launch(k_bucket_sort<0, true>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        else
+            fdb_launch(k_bucket_sort<0, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        after(4);
+        if ((err = hipEventSynchronize(e1))) break;
+        float ms = 0;
+        if ((err = hipEventElapsedTime(&ms, e0, e1))) break;
+        total += ms;
+    }
+    (void)hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), s);
+    (void)hipMemsetAsync(w.bcount, 0, 4 * kMaxBuckets, s);
+    (void)hipMemsetAsync(w.bcursor, 0, 4 * kMaxBuckets, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *us = total * 1000.0 / reps;
+    return err;
+}
+
 // ------------------------------------------------------------------ positions
 
 // Positions (KeyInfo::pIndex, SkipList.cpp:814) and, in the same scan, the number of write-begins

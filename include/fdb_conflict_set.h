@@ -204,7 +204,8 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
 
 /* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
  * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the
- * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead). */
+ * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead); 1-4 = the
+ * endpoint sort's kernels (sample ranking, bucket count, scatter, per-bucket sort). */
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch);
 
 const char* fdbcs_strerror(int status);

@@ -1,5 +1,6 @@
-"""Device time of the read-check kernel alone (fdbcs_debug_kernel_time) on a full-size workload,
-under the env-knob variants given on the command line ("FDBCS_CHECK=1", "FDBCS_CHECK_GRID=512"...).
+"""Device time of pipeline kernels alone (fdbcs_debug_kernel_time) on a full-size workload, under
+the env-knob variants given on the command line ("FDBCS_CHECK=1", "FDBCS_SORT_WIN=0"...).  WHICH
+lists the kernels (0 read check, 1 sample, 2 bucket count, 3 scatter, 4 bucket sort; default 0).
 Each variant runs in a fresh subprocess (knobs are read when a conflict set is created)."""
 import json
 import os
@@ -18,7 +19,7 @@ def one(workload):
 
     start = 10_000_000
     if workload == "c4":
-        p = W.C4Params()
+        p = W.C4Params(history=int(os.environ.get("HISTORY", 50_000_000)))
         kb, ko, vers = W.c4_history(p, seed=1000, start_version=start)
         mk = lambda rng, now: W.c4_batch(p, rng, now)
     else:
@@ -40,7 +41,8 @@ def one(workload):
     for i in range(3):
         b = C.ConflictBatch(cs)
         b.add_packed(mk(rng, now + 1000))
-        out.append(b.debug_kernel_time(0, 40))
+        which = [int(x) for x in os.environ.get("WHICH", "0").split(",")]
+        out.append({w: round(b.debug_kernel_time(w, 40), 1) for w in which})
         b.close()
     return out
 
@@ -63,4 +65,4 @@ if __name__ == "__main__":
             print(spec, "FAILED", r.stderr[-2000:], flush=True)
             sys.exit(r.returncode)
         w = env.get("WORKLOAD_OVERRIDE", workload)
-        print(f"{workload} {spec:40s} check us: {json.loads(r.stdout.strip().splitlines()[-1])}", flush=True)
+        print(f"{workload} {spec:40s} us: {json.loads(r.stdout.strip().splitlines()[-1])}", flush=True)
