@@ -14,6 +14,9 @@
 //
 // Memory-bound integer/byte work: no MFMA anywhere (BASELINE.json north_star).
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
 #include <limits.h>
 
 #include "engine.h"
@@ -1544,6 +1547,16 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int 
         float ms = 0;
         if ((err = hipEventElapsedTime(&ms, e0, e1))) break;
         total += ms;
+    }
+    if (err == hipSuccess && getenv("FDBCS_DEBUG_BUCKETS")) {  // bucket-size balance of the last run
+        std::vector<int32_t> cnt(nb);
+        (void)hipMemcpy(cnt.data(), w.bcount, 4 * (size_t)nb, hipMemcpyDeviceToHost);
+        int mx = 0, over = 0;
+        for (int k = 0; k < nb; k++) {
+            mx = cnt[k] > mx ? cnt[k] : mx;
+            over += cnt[k] > kBitonicMax;
+        }
+        fprintf(stderr, "fdbcs sort: E=%d nb=%d S=%d max bucket=%d over %d=%d\n", E, nb, S, mx, kBitonicMax, over);
     }
     (void)hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), s);
     (void)hipMemsetAsync(w.bcount, 0, 4 * kMaxBuckets, s);

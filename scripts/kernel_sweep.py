@@ -66,3 +66,6 @@ if __name__ == "__main__":
             sys.exit(r.returncode)
         w = env.get("WORKLOAD_OVERRIDE", workload)
         print(f"{workload} {spec:40s} us: {json.loads(r.stdout.strip().splitlines()[-1])}", flush=True)
+        for line in r.stderr.splitlines():
+            if line.startswith("fdbcs sort"):
+                print("   ", line, flush=True)
