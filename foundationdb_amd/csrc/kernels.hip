@@ -1312,27 +1312,29 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
     if (m <= 1) return;
     const int t = threadIdx.x;
     if (ALG == 0 && m <= kBitonicMax) {
-        // Rank count on the high key word: rank = #items whose hi word is smaller, exact whenever no
-        // other item of the bucket shares my hi word (distinct keys: the common case).  Items that
-        // share it add the exact comparisons against exactly those items (hot keys, long prefixes).
-        // Two items per LDS read, two VALU ops per comparison.
+        // Rank count.  Pass 1 counts the items below my high key word (two per LDS read): exact
+        // whenever no other item of the bucket shares that word (distinct keys, C2).  Items that
+        // share it (hot keys; C4 tuple keys share a whole subspace and user prefix) run pass 2 over
+        // the low word the same way; only items whose full 16-byte prefix repeats in the bucket (a
+        // range's begin and end, keys of one C4 user) run pass 3, which orders them by the
+        // tie-break word (bytes 16-18, length, class, id) or, for two keys longer than 19 bytes
+        // that agree on it, by their tails: windows staged in LDS for exactly those items (WIN),
+        // else the arena.
         __shared__ __attribute__((aligned(16))) uint64_t shi[kBitonicMax];
-        __shared__ uint64_t slo[kBitonicMax], saux[kBitonicMax];
+        __shared__ __attribute__((aligned(16))) uint64_t slo[kBitonicMax];
+        __shared__ uint64_t saux[kBitonicMax];
         __shared__ uint64_t swin[WIN ? kBitonicMax : 1][kTailWin];
         SortItem x{};
         if (t < m) {
-            sh[t] = x = a[off + t];
+            x = a[off + t];
             shi[t] = x.hi;
             slo[t] = x.lo;
             saux[t] = item_aux(x);
         }
-        // keys longer than kSortNxLen may tie on (prefix, bytes 16-18): stage their tail windows
-        const bool lng = WIN && t < m && x.len > kSortNxLen;
-        if (WIN && __syncthreads_or(lng) && lng) load_tail_window(swin[t], arena, x.tail, x.len);
         __syncthreads();
+        int lt = 0, eq = 0, eq2 = 0;
+        const uint64_t mh = x.hi, ml = x.lo;
         if (t < m) {
-            int lt = 0, eq = 0;
-            const uint64_t mh = x.hi;
             int j = 0;
             for (; j + 8 <= m; j += 8) {
                 ulonglong2 p[4];
@@ -1349,53 +1351,52 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 lt += h < mh;
                 eq += h == mh;
             }
-            if (eq > 1) {
-                // Items sharing my hi word.  A key longer than kSortNxLen may need tail compares
-                // (C4 tuple keys): the exact path with deferred tails.  A shorter one never does
-                // (item_tie needs both keys longer): low word, then the tie-break word, four
-                // items per step with every LDS load issued first (a read [k, k + d) shares the
-                // hi word with its own end; a hot key fills whole buckets with one prefix).
-                const uint64_t ax = saux[t], ml = x.lo;
-                if (!WIN && ((ax >> 32) & 31u) == kSortNxLen + 1) {
-                    lt += rank_shared_hi(sh, shi, m, t, x, arena);  // not reached: WIN covers long keys
-                } else if (((ax >> 32) & 31u) == kSortNxLen + 1) {
-                    // long key: (low word, tie-break word) decide unless both are long with equal
-                    // bytes 16-18; those compare tail windows in LDS
-                    for (int q = 0; q < m; q++) {
-                        if (shi[q] != mh || q == t) continue;
-                        const uint64_t l = slo[q];
-                        if (l != ml) {
-                            lt += l < ml;
-                            continue;
-                        }
-                        const uint64_t w = saux[q];
-                        if (((w >> 32) & 31u) == kSortNxLen + 1 && (w >> 37) == (ax >> 37)) {
-                            const SortItem y = sh[q];
-                            lt += item_less_tail_win(swin[q], y.len, y.tail, y.meta, swin[t], x.len, x.tail, x.meta, arena)
-                                      ? 1
-                                      : 0;
-                        } else {
-                            lt += w < ax;
-                        }
-                    }
-                } else {
-                    int q = 0;
-                    for (; q + 4 <= m; q += 4) {
-                        uint64_t h[4], l[4], w[4];
+        }
+        if (t < m && eq > 1) {  // pass 2: items sharing my hi word, by the low word
+            int j = 0;
+            for (; j + 8 <= m; j += 8) {
+                ulonglong2 p[4], q[4];
 #pragma unroll
-                        for (int u = 0; u < 4; u++) h[u] = shi[q + u], l[u] = slo[q + u], w[u] = saux[q + u];
+                for (int u = 0; u < 4; u++) {
+                    p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
+                    q[u] = *reinterpret_cast<const ulonglong2*>(&slo[j + 2 * u]);
+                }
 #pragma unroll
-                        for (int u = 0; u < 4; u++)
-                            lt += (h[u] == mh && (l[u] < ml || (l[u] == ml && w[u] < ax))) ? 1 : 0;
-                    }
-                    for (; q < m; q++) {
-                        const uint64_t h = shi[q], l = slo[q], w = saux[q];
-                        lt += (h == mh && (l < ml || (l == ml && w < ax))) ? 1 : 0;
-                    }
+                for (int u = 0; u < 4; u++) {
+                    lt += (p[u].x == mh && q[u].x < ml) + (p[u].y == mh && q[u].y < ml);
+                    eq2 += (p[u].x == mh && q[u].x == ml) + (p[u].y == mh && q[u].y == ml);
                 }
             }
-            a[off + lt] = x;
+            for (; j < m; j++) {
+                const uint64_t h = shi[j], l = slo[j];
+                lt += h == mh && l < ml;
+                eq2 += h == mh && l == ml;
+            }
         }
+        // pass 3 inputs: tail windows of long keys whose prefix repeats (read by their group only)
+        const uint64_t ax = saux[t < m ? t : 0];
+        const bool lng = t < m && eq2 > 1 && ((ax >> 32) & 31u) == kSortNxLen + 1;
+        if (WIN) {
+            if (__syncthreads_or(lng) && lng) load_tail_window(swin[t], arena, x.tail, x.len);
+            __syncthreads();
+        }
+        if (t < m && eq2 > 1) {  // pass 3: items sharing my 16-byte prefix
+            for (int q = 0; q < m; q++) {
+                if (shi[q] != mh || slo[q] != ml || q == t) continue;
+                const uint64_t w = saux[q];
+                if (lng && ((w >> 32) & 31u) == kSortNxLen + 1 && (w >> 37) == (ax >> 37)) {
+                    const SortItem y = a[off + q];  // len / tail / meta of the other key (global, rare)
+                    lt += (WIN ? item_less_tail_win(swin[q], y.len, y.tail, y.meta, swin[t], x.len, x.tail, x.meta, arena)
+                               : item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena))
+                              ? 1
+                              : 0;
+                } else {
+                    lt += w < ax;
+                }
+            }
+        }
+        __syncthreads();  // every item is read (pass 3) before any is overwritten in place
+        if (t < m) a[off + lt] = x;
         return;
     }
     for (int c = 0; c < m; c += kBitonicMax) {
