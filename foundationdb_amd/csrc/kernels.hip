@@ -1221,47 +1221,6 @@ __device__ bool reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* are
     return tie;
 }
 
-// Exact count of the bucket items that share x's hi word and order before it.  The low word and
-// the (length, class, id) word decide branch-free; a pair that needs the bytes beyond the prefix
-// (equal prefixes, both keys longer than 16 bytes) is compared after the scan, so the lanes of a
-// wave run their first such comparison side by side instead of one lane at a time per broadcast
-// item (C4 tuple keys: every range's two endpoints tie on the prefix).  Further ties (hot keys)
-// take a second, serial pass.
-__device__ __forceinline__ int rank_shared_hi(const SortItem* sh, const uint64_t* shi, int m, int t,
-                                              const SortItem& x, const uint8_t* arena) {
-    const uint64_t ax = item_aux(x);
-    int lt = 0, first = -1;
-    bool more = false;
-    for (int q = 0; q < m; q++) {
-        if (shi[q] != x.hi || q == t) continue;
-        const uint64_t ylo = sh[q].lo;
-        if (ylo != x.lo) {
-            lt += ylo < x.lo;
-            continue;
-        }
-        const SortItem y = sh[q];
-        if (item_tie(x, y)) {
-            more |= first >= 0;
-            first = first < 0 ? q : first;
-        } else {
-            lt += item_aux(y) < ax;
-        }
-    }
-    if (first >= 0) {
-        const SortItem y = sh[first];
-        lt += item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena) ? 1 : 0;
-    }
-    if (more) {
-        for (int q = first + 1; q < m; q++) {
-            if (shi[q] != x.hi || q == t) continue;
-            const SortItem y = sh[q];
-            if (y.lo == x.lo && item_tie(x, y))
-                lt += item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena) ? 1 : 0;
-        }
-    }
-    return lt;
-}
-
 constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by one workgroup
 
 // Tail windows: bytes [16, 16 + 8 kTailWin) of a bucket's long keys, as big-endian words zero-padded
@@ -1312,17 +1271,17 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
     if (m <= 1) return;
     const int t = threadIdx.x;
     if (ALG == 0 && m <= kBitonicMax) {
-        // Rank count.  Pass 1 counts the items below my high key word (two per LDS read): exact
-        // whenever no other item of the bucket shares that word (distinct keys, C2).  Items that
-        // share it (hot keys; C4 tuple keys share a whole subspace and user prefix) run pass 2 over
-        // the low word the same way; only items whose full 16-byte prefix repeats in the bucket (a
-        // range's begin and end, keys of one C4 user) run pass 3, which orders them by the
-        // tie-break word (bytes 16-18, length, class, id) or, for two keys longer than 19 bytes
-        // that agree on it, by their tails: windows staged in LDS for exactly those items (WIN),
-        // else the arena.
+        // Rank count on (high word, low word, tie-break word), each pass only for the items that
+        // tie on the previous words, two (pass 1) or four items per step with all LDS loads issued
+        // first.  Pass 1 alone is exact for distinct keys (C2); pass 2 serves items sharing the
+        // high word (hot keys; C4 tuple keys share a whole subspace); pass 3 items sharing the
+        // 16-byte prefix (a range's begin and end).  The tie-break word (bytes 16-18, length,
+        // class, id) leaves only keys longer than 19 bytes that agree on it unordered by key:
+        // those sit in contiguous runs after the ranking, and each run is then sorted by its tails
+        // (windows staged in LDS for exactly the run members) by one thread.
         __shared__ __attribute__((aligned(16))) uint64_t shi[kBitonicMax];
         __shared__ __attribute__((aligned(16))) uint64_t slo[kBitonicMax];
-        __shared__ uint64_t saux[kBitonicMax];
+        __shared__ __attribute__((aligned(16))) uint64_t saux[kBitonicMax];
         __shared__ uint64_t swin[WIN ? kBitonicMax : 1][kTailWin];
         SortItem x{};
         if (t < m) {
@@ -1333,7 +1292,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
         }
         __syncthreads();
         int lt = 0, eq = 0, eq2 = 0;
-        const uint64_t mh = x.hi, ml = x.lo;
+        const uint64_t mh = x.hi, ml = x.lo, ax = t < m ? saux[t] : 0;
         if (t < m) {
             int j = 0;
             for (; j + 8 <= m; j += 8) {
@@ -1352,17 +1311,17 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 eq += h == mh;
             }
         }
-        if (t < m && eq > 1) {  // pass 2: items sharing my hi word, by the low word
+        if (t < m && eq > 1) {  // pass 2: my high word repeats
             int j = 0;
-            for (; j + 8 <= m; j += 8) {
-                ulonglong2 p[4], q[4];
+            for (; j + 4 <= m; j += 4) {
+                ulonglong2 p[2], q[2];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < 2; u++) {
                     p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
                     q[u] = *reinterpret_cast<const ulonglong2*>(&slo[j + 2 * u]);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < 2; u++) {
                     lt += (p[u].x == mh && q[u].x < ml) + (p[u].y == mh && q[u].y < ml);
                     eq2 += (p[u].x == mh && q[u].x == ml) + (p[u].y == mh && q[u].y == ml);
                 }
@@ -1373,30 +1332,70 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 eq2 += h == mh && l == ml;
             }
         }
-        // pass 3 inputs: tail windows of long keys whose prefix repeats (read by their group only)
-        const uint64_t ax = saux[t < m ? t : 0];
-        const bool lng = t < m && eq2 > 1 && ((ax >> 32) & 31u) == kSortNxLen + 1;
-        if (WIN) {
-            if (__syncthreads_or(lng) && lng) load_tail_window(swin[t], arena, x.tail, x.len);
-            __syncthreads();
+        if (t < m && eq2 > 1) {  // pass 3: my 16-byte prefix repeats
+            int j = 0;
+            for (; j + 4 <= m; j += 4) {
+                ulonglong2 p[2], q[2], w[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
+                    q[u] = *reinterpret_cast<const ulonglong2*>(&slo[j + 2 * u]);
+                    w[u] = *reinterpret_cast<const ulonglong2*>(&saux[j + 2 * u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    lt += (p[u].x == mh && q[u].x == ml && w[u].x < ax) + (p[u].y == mh && q[u].y == ml && w[u].y < ax);
+                }
+            }
+            for (; j < m; j++) lt += shi[j] == mh && slo[j] == ml && saux[j] < ax;
         }
-        if (t < m && eq2 > 1) {  // pass 3: items sharing my 16-byte prefix
-            for (int q = 0; q < m; q++) {
-                if (shi[q] != mh || slo[q] != ml || q == t) continue;
-                const uint64_t w = saux[q];
-                if (lng && ((w >> 32) & 31u) == kSortNxLen + 1 && (w >> 37) == (ax >> 37)) {
-                    const SortItem y = a[off + q];  // len / tail / meta of the other key (global, rare)
-                    lt += (WIN ? item_less_tail_win(swin[q], y.len, y.tail, y.meta, swin[t], x.len, x.tail, x.meta, arena)
-                               : item_less_tail(y.len, y.tail, y.meta, x.len, x.tail, x.meta, arena))
-                              ? 1
-                              : 0;
-                } else {
-                    lt += w < ax;
+        if (!WIN) {
+            if (t < m) a[off + lt] = x;  // exact: no key is longer than kSortNxLen
+            return;
+        }
+        __syncthreads();  // ranks done: the arrays are reused in sorted order
+        if (t < m) {
+            sh[lt] = x;
+            shi[lt] = x.hi;
+            slo[lt] = x.lo;
+            saux[lt] = ax;
+        }
+        __syncthreads();
+        // runs of long keys that agree on (prefix, tie-break word minus class and id)
+        auto same = [&](int p0, int p1) {
+            const uint64_t w0 = saux[p0], w1 = saux[p1];
+            return shi[p0] == shi[p1] && slo[p0] == slo[p1] && ((w0 >> 32) & 31u) == kSortNxLen + 1 &&
+                   ((w1 >> 32) & 31u) == kSortNxLen + 1 && (w0 >> 37) == (w1 >> 37);
+        };
+        const bool in_run = t < m && ((t > 0 && same(t - 1, t)) || (t + 1 < m && same(t, t + 1)));
+        if (__syncthreads_or(in_run)) {
+            if (in_run) load_tail_window(swin[t], arena, sh[t].tail, sh[t].len);
+        }
+        __syncthreads();
+        if (in_run && (t == 0 || !same(t - 1, t))) {
+            int e = t + 1;
+            while (e < m && same(e - 1, e)) e++;
+            // insertion sort of positions [t, e) by (tail, class, id); swap items and windows
+            for (int i = t + 1; i < e; i++) {
+                for (int k = i; k > t; k--) {
+                    const SortItem& u = sh[k - 1];
+                    const SortItem& v = sh[k];
+                    if (!item_less_tail_win(swin[k], v.len, v.tail, v.meta, swin[k - 1], u.len, u.tail, u.meta, arena))
+                        break;
+                    const SortItem tmpi = sh[k - 1];
+                    sh[k - 1] = sh[k];
+                    sh[k] = tmpi;
+#pragma unroll
+                    for (int z = 0; z < kTailWin; z++) {
+                        const uint64_t tw = swin[k - 1][z];
+                        swin[k - 1][z] = swin[k][z];
+                        swin[k][z] = tw;
+                    }
                 }
             }
         }
-        __syncthreads();  // every item is read (pass 3) before any is overwritten in place
-        if (t < m) a[off + lt] = x;
+        __syncthreads();
+        if (t < m) a[off + t] = sh[t];
         return;
     }
     for (int c = 0; c < m; c += kBitonicMax) {
