@@ -1271,11 +1271,10 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
     if (m <= 1) return;
     const int t = threadIdx.x;
     if (ALG == 0 && m <= kBitonicMax) {
-        // Rank count on (high word, low word, tie-break word), each pass only for the items that
-        // tie on the previous words, two (pass 1) or four items per step with all LDS loads issued
-        // first.  Pass 1 alone is exact for distinct keys (C2); pass 2 serves items sharing the
-        // high word (hot keys; C4 tuple keys share a whole subspace); pass 3 items sharing the
-        // 16-byte prefix (a range's begin and end).  The tie-break word (bytes 16-18, length,
+        // Rank count on (high word, low word, tie-break word), with all LDS loads of a step issued
+        // first.  Pass 1 (high word, eight items per step) alone is exact for distinct keys (C2);
+        // pass 2 (low word, then tie-break word) serves items sharing the high word (hot keys,
+        // single-key writes [k, k\0); C4 tuple keys share a whole subspace).  The tie-break word (bytes 16-18, length,
         // class, id) leaves only keys longer than 19 bytes that agree on it unordered by key:
         // those sit in contiguous runs after the ranking, and each run is then sorted by its tails
         // (windows staged in LDS for exactly the run members) by one thread.
@@ -1291,7 +1290,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
             saux[t] = item_aux(x);
         }
         __syncthreads();
-        int lt = 0, eq = 0, eq2 = 0;
+        int lt = 0, eq = 0;
         const uint64_t mh = x.hi, ml = x.lo, ax = t < m ? saux[t] : 0;
         if (t < m) {
             int j = 0;
@@ -1311,28 +1310,7 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 eq += h == mh;
             }
         }
-        if (t < m && eq > 1) {  // pass 2: my high word repeats
-            int j = 0;
-            for (; j + 4 <= m; j += 4) {
-                ulonglong2 p[2], q[2];
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
-                    q[u] = *reinterpret_cast<const ulonglong2*>(&slo[j + 2 * u]);
-                }
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    lt += (p[u].x == mh && q[u].x < ml) + (p[u].y == mh && q[u].y < ml);
-                    eq2 += (p[u].x == mh && q[u].x == ml) + (p[u].y == mh && q[u].y == ml);
-                }
-            }
-            for (; j < m; j++) {
-                const uint64_t h = shi[j], l = slo[j];
-                lt += h == mh && l < ml;
-                eq2 += h == mh && l == ml;
-            }
-        }
-        if (t < m && eq2 > 1) {  // pass 3: my 16-byte prefix repeats
+        if (t < m && eq > 1) {  // pass 2: my high word repeats: (low word, tie-break word)
             int j = 0;
             for (; j + 4 <= m; j += 4) {
                 ulonglong2 p[2], q[2], w[2];
@@ -1344,10 +1322,14 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                 }
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
-                    lt += (p[u].x == mh && q[u].x == ml && w[u].x < ax) + (p[u].y == mh && q[u].y == ml && w[u].y < ax);
+                    lt += (p[u].x == mh && (q[u].x < ml || (q[u].x == ml && w[u].x < ax))) +
+                          (p[u].y == mh && (q[u].y < ml || (q[u].y == ml && w[u].y < ax)));
                 }
             }
-            for (; j < m; j++) lt += shi[j] == mh && slo[j] == ml && saux[j] < ax;
+            for (; j < m; j++) {
+                const uint64_t h = shi[j], l = slo[j], w = saux[j];
+                lt += h == mh && (l < ml || (l == ml && w < ax));
+            }
         }
         if (!WIN) {
             if (t < m) a[off + lt] = x;  // exact: no key is longer than kSortNxLen
