@@ -111,6 +111,8 @@ struct fdbcs_conflict_set {
     hipStream_t stream = nullptr;   // stage B: everything that reads or writes the history, in batch order
     hipStream_t astream = nullptr;  // stage A (and every upload): history-independent sort and edges
     hipStream_t astream2 = nullptr; // stage A of odd batches when FDBCS_ASTREAMS=2
+    hipStream_t ustream = nullptr;  // batch uploads (k_upload over PCIe), so batch i+1's upload overlaps
+                                    // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
     hipEvent_t ev_b[kNumWork] = {}; // stage B (epilogue) of the batch using workspace k is done
     bool wused[kNumWork] = {};
@@ -300,6 +302,7 @@ int flush_pending(fdbcs_conflict_set* cs);
 // Both streams idle (before reallocating anything either stage uses).
 int sync_all(fdbcs_conflict_set* cs) {
     if (int rc = flush_pending(cs)) return rc;
+    HIPOK(hipStreamSynchronize(cs->ustream));
     HIPOK(hipStreamSynchronize(cs->astream));
     if (cs->astream2) HIPOK(hipStreamSynchronize(cs->astream2));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -684,7 +687,8 @@ void materialize(fdbcs_batch* b) {
     b->direct = false;
 }
 
-int do_upload(fdbcs_batch* b) {
+// own_stream: launch now on the upload stream (not recorded); else record onto stage A's stream.
+int do_upload(fdbcs_batch* b, bool own_stream) {
     fdbcs_conflict_set* cs = b->cs;
     BatchSlot* sl = b->slot;
     const size_t T = b->T(), R = b->R(), W = b->W();
@@ -704,20 +708,25 @@ int do_upload(fdbcs_batch* b) {
     memcpy(h + L.roff, b->roff.data(), 4 * (T + 1));
     memcpy(h + L.woff, b->woff.data(), 4 * (T + 1));
     if (T) memcpy(h + L.flags, b->flags.data(), T);
-    // on stage A's stream (its kernels read the batch first); stage B waits for ev_up.  A reused
-    // slot's device copy may still be read by the epilogue of the batch that used it last.  While
-    // the engine records stage A (t_record set) these become records of that stage.
+    // On the upload stream, issued now (own_stream), or recorded into stage A (graph mode, phase
+    // timing); both stages wait for ev_up.  A reused slot's device copy may still be read by the
+    // epilogue of the batch that used it last.
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
+    LaunchList* const saved = t_record;
+    if (own_stream) t_record = nullptr;
+    hipStream_t us = own_stream ? cs->ustream : cs->astream;
+    int urc = FDBCS_OK;
     if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess)
-        fdb_event(LaunchList::kSyncWait, sl->ev_free, cs->astream);
-
+        fdb_event(LaunchList::kSyncWait, sl->ev_free, us);
     if (cs->dma_upload && !t_record) {
-        HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, cs->astream));
+        if (hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us) != hipSuccess) urc = FDBCS_E_DEVICE;
     } else {
-        launch_upload(cs->astream, sl->pin_in.dp, sl->dev.p, (int64_t)L.total, cs->upload_blocks);
-        if (!t_record) HIPOK(take_launch_error());
+        launch_upload(us, sl->pin_in.dp, sl->dev.p, (int64_t)L.total, cs->upload_blocks);
+        if (!t_record && take_launch_error() != hipSuccess) urc = FDBCS_E_DEVICE;
     }
-    fdb_event(LaunchList::kSyncRecord, sl->ev_up, cs->astream);
+    fdb_event(LaunchList::kSyncRecord, sl->ev_up, us);
+    t_record = saved;
+    if (urc) return urc;
     char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
     b->bd.R = (int32_t)R;
@@ -866,6 +875,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
               (cs->astreams == 1 || hipStreamCreateWithFlags(&cs->astream2, hipStreamNonBlocking) == hipSuccess);
     for (int k = 0; k < kNumWork && ok; k++)
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
@@ -893,6 +903,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (!cs) return;
     (void)hipSetDevice(cs->device);
     (void)flush_pending(cs);
+    if (cs->ustream) (void)hipStreamSynchronize(cs->ustream);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
     if (cs->astream2) (void)hipStreamSynchronize(cs->astream2);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
@@ -928,6 +939,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
     }
+    if (cs->ustream) (void)hipStreamDestroy(cs->ustream);
     if (cs->astream) (void)hipStreamDestroy(cs->astream);
     if (cs->astream2) (void)hipStreamDestroy(cs->astream2);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
@@ -1105,12 +1117,14 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
     if (b->state == 2) {  // still in flight: its set (which must outlive it) owns the stream
         (void)hipSetDevice(b->cs->device);
         (void)flush_pending(b->cs);
+        (void)hipStreamSynchronize(b->cs->ustream);
         (void)hipStreamSynchronize(b->cs->astream);
         if (b->cs->astream2) (void)hipStreamSynchronize(b->cs->astream2);
         (void)hipStreamSynchronize(b->cs->stream);
         b->cs->inflight--;
     } else if (b->state == 1) {  // uploaded, never submitted: the copy may still be in flight
         (void)hipSetDevice(b->cs->device);
+        (void)hipStreamSynchronize(b->cs->ustream);
         (void)hipStreamSynchronize(b->cs->astream);
     }
     // the slot goes back to the set's pool (its buffers and events are reused by the next batch)
@@ -1306,7 +1320,7 @@ int fdbcs_batch_upload(fdbcs_batch* b) {
     if (!b->cs) return FDBCS_E_STATE;
     if (b->state != 0) return b->state == 1 ? FDBCS_OK : FDBCS_E_STATE;
     HIPOK(hipSetDevice(b->cs->device));
-    return do_upload(b);
+    return do_upload(b, true);
 }
 
 static inline double host_ms_since(std::chrono::steady_clock::time_point t0) {
@@ -1404,7 +1418,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (cs->wused[wp] && sa != s && hipEventQuery(cs->ev_b[wp]) != hipSuccess)
         fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     cs->wused[wp] = true;
-    if (b->state == 0 && (rc = do_upload(b))) return t_record = nullptr, rc;
+    // the upload runs on its own stream unless the batch's launches go into one graph or phases
+    // are timed one after another
+    const bool own_upload = !graph && timing < 2 && !cs->serial;
+    if (b->state == 0 && (rc = do_upload(b, own_upload))) return t_record = nullptr, rc;
+    // stage A reads the batch: wait for the upload stream
+    if (own_upload || (was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess))
+        fdb_event(LaunchList::kSyncWait, sl->ev_up, sa);
     if ((rc = mark(kPhUpload))) return t_record = nullptr, rc;
     const BatchDev& bd = b->bd;
     Scalars* sc = (Scalars*)cs->scal.p;
