@@ -111,6 +111,12 @@ struct fdbcs_conflict_set {
     hipStream_t stream = nullptr;   // stage B: everything that reads or writes the history, in batch order
     hipStream_t astream = nullptr;  // stage A (and every upload): history-independent sort and edges
     hipStream_t astream2 = nullptr; // stage A of odd batches when FDBCS_ASTREAMS=2
+    hipStream_t cstream = nullptr;  // split read check: the base-tier half (history-independent between
+                                    // compactions) beside stage A
+    hipEvent_t ev_c[kNumWork] = {}; // base-tier check of the batch using workspace k is done
+    hipEvent_t ev_cmp = nullptr;    // stage B of the last batch that rewrote the base (compaction / GC)
+    bool cmp_recorded = false;
+    bool split_check = true;        // FDBCS_SPLIT_CHECK=0: one read check over both tiers in stage B
     hipStream_t ustream = nullptr;  // batch uploads (k_upload over PCIe), so batch i+1's upload overlaps
                                     // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
@@ -181,7 +187,7 @@ struct fdbcs_conflict_set {
     // argument structs, and a node parameter update costs 0.76 us at 640 bytes
     // (tools/graphbench.hip), so updating ~30 nodes costs as much host time as launching them.
     bool use_graph = false;
-    LaunchList rec_a, rec_b, pending_b;
+    LaunchList rec_a, rec_b, rec_c, pending_b;
     fdbcs_batch* pending_batch = nullptr;
     struct GraphEntry {
         hipGraph_t graph = nullptr;
@@ -303,6 +309,7 @@ int flush_pending(fdbcs_conflict_set* cs);
 int sync_all(fdbcs_conflict_set* cs) {
     if (int rc = flush_pending(cs)) return rc;
     HIPOK(hipStreamSynchronize(cs->ustream));
+    HIPOK(hipStreamSynchronize(cs->cstream));
     HIPOK(hipStreamSynchronize(cs->astream));
     if (cs->astream2) HIPOK(hipStreamSynchronize(cs->astream2));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -869,6 +876,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
     if (const char* v = getenv("FDBCS_GRAPH")) cs->use_graph = v[0] != '0';
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
+    if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
@@ -876,9 +884,12 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&cs->cstream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess &&
               (cs->astreams == 1 || hipStreamCreateWithFlags(&cs->astream2, hipStreamNonBlocking) == hipSuccess);
     for (int k = 0; k < kNumWork && ok; k++)
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&cs->ev_c[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_b[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fdbcs_destroy_conflict_set(cs);
@@ -904,6 +915,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     (void)hipSetDevice(cs->device);
     (void)flush_pending(cs);
     if (cs->ustream) (void)hipStreamSynchronize(cs->ustream);
+    if (cs->cstream) (void)hipStreamSynchronize(cs->cstream);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
     if (cs->astream2) (void)hipStreamSynchronize(cs->astream2);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
@@ -937,9 +949,12 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->live.clear();
     for (int k = 0; k < kNumWork; k++) {
         if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
+        if (cs->ev_c[k]) (void)hipEventDestroy(cs->ev_c[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
     }
     if (cs->ustream) (void)hipStreamDestroy(cs->ustream);
+    if (cs->cstream) (void)hipStreamDestroy(cs->cstream);
+    if (cs->ev_cmp) (void)hipEventDestroy(cs->ev_cmp);
     if (cs->astream) (void)hipStreamDestroy(cs->astream);
     if (cs->astream2) (void)hipStreamDestroy(cs->astream2);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
@@ -1118,6 +1133,7 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
         (void)hipSetDevice(b->cs->device);
         (void)flush_pending(b->cs);
         (void)hipStreamSynchronize(b->cs->ustream);
+        (void)hipStreamSynchronize(b->cs->cstream);
         (void)hipStreamSynchronize(b->cs->astream);
         if (b->cs->astream2) (void)hipStreamSynchronize(b->cs->astream2);
         (void)hipStreamSynchronize(b->cs->stream);
@@ -1407,16 +1423,22 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(hipStreamWaitEvent(s, sl->ev_up, 0));  // uploaded early (fdbcs_batch_upload) on stage A's stream
     LaunchList& la = cs->rec_a;
     LaunchList& lb = cs->rec_b;
+    LaunchList& lc = cs->rec_c;
     la.clear();
     lb.clear();
+    lc.clear();
+    // Split read check: the base tier changes only at compactions, so unless one is still pending
+    // on the stream its half of D.CheckRead runs beside stage A on its own stream; stage B keeps the
+    // delta half.  One graph per batch cannot express the wait, so graph mode keeps one check.
+    const bool split = cs->split_check && !graph && !cs->serial && timing < 2;
     cs->stats.host_ms_prepare += host_ms_since(t_begin);
     const auto t_rec = std::chrono::steady_clock::now();
     // ---- record stage A: upload, D.Sort and the candidate edges of D.CheckIntraBatch
     t_record = &la;
     if ((rc = mark(kPhStart))) return t_record = nullptr, rc;
     // workspace wp was last used by the batch before the previous one: its epilogue re-zeroed it
-    if (cs->wused[wp] && sa != s && hipEventQuery(cs->ev_b[wp]) != hipSuccess)
-        fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
+    const bool ws_busy = cs->wused[wp] && hipEventQuery(cs->ev_b[wp]) != hipSuccess;
+    if (ws_busy && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     cs->wused[wp] = true;
     // the upload runs on its own stream unless the batch's launches go into one graph or phases
     // are timed one after another
@@ -1453,15 +1475,32 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_edges(sa, bd, w);
     if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_a[wp], sa);
     mark(kPhEdges);
+    if (split) {  // ---- record the base-tier check (its own stream)
+        t_record = &lc;
+        hipStream_t sc_ = cs->cstream;
+        fdb_event(LaunchList::kSyncWait, sl->ev_up, sc_);
+        if (ws_busy) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sc_);
+        if (cs->cmp_recorded && hipEventQuery(cs->ev_cmp) != hipSuccess) fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
+        fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
+        launch_check_tier(sc_, bd, w, base, true, htail);
+        fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
+        fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
+    }
     // ---- record stage B: D.CheckRead against the history the previous batch left, then batch order
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
-    b->check_hist = cs->n_ub + cs->nd_ub;
-    fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-    launch_check(s, bd, w, base, delta, htail, cs->check_version, cs->check_grid);
-    fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
+    if (split) {
+        b->check_hist = cs->n_ub;  // the timed (base-tier) check
+        launch_check_tier(s, bd, w, delta, false, htail);
+    } else {
+        b->check_hist = cs->n_ub + cs->nd_ub;
+        fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
+        launch_check(s, bd, w, base, delta, htail, cs->check_version, cs->check_grid);
+        fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
+    }
     mark(kPhCheck);
     if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
+    if (split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp);
     if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
         launch_conflict_output(s, bd, w, (const int32_t*)sl->pin_inv.dp, b->out_n, b->out_dev);
@@ -1521,8 +1560,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
                     gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1);
-    if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
+    if (sa != s || split) fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
     fdb_event(LaunchList::kSyncRecord, sl->ev_free, s);
+    if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
+        fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, s);
+        cs->cmp_recorded = true;
+    }
     sl->free_recorded = true;
     mark(kPhEpilogue);
     mark(kPhEnd);
@@ -1543,6 +1586,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     } else {
         if (flush_pending(cs)) return FDBCS_E_DEVICE;
         HIPOK(la.replay(sa));
+        if (split) HIPOK(lc.replay(cs->cstream));
         HIPOK(lb.replay(s));
         HIPOK(take_launch_error());
     }

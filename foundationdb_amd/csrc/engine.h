@@ -212,6 +212,10 @@ void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_t
 // check_grid_cap: workgroups of the version-2 kernel (each loops over reads).
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
                   const uint8_t* htail, int check_version = 2, int check_grid_cap = 2048);
+// D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
+// delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
+void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
+                       const uint8_t* htail);
 // bucket_target: endpoints per sample-sort bucket (0 = default 128; tests force oversized buckets).
 // sample_per: splitter samples per bucket (0 = default 8).
 // alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).

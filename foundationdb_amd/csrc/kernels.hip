@@ -546,6 +546,36 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
     }
 }
 
+// One tier only (the split check): 2 lane groups per read locate its begin / end in `tier`; a
+// conflict sets the read's and its transaction's flags (zeroed beforehand by the epilogue that last
+// used the workspace), so the base-tier launch (stage A, on its own stream) and the delta-tier
+// launch (stage B) OR into the same flags.  is_base: the tier's header version applies below its
+// first boundary (the delta's header is kHole: the base shows through).
+constexpr int kTierLanes = 2 * kArity;
+__device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& tier, bool is_base, const uint8_t* htail,
+                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot) {
+    const int lane = threadIdx.x & 63;
+    const int r = (int)(slot / kTierLanes);
+    const int grp = (lane / kArity) & 1;
+    const int lead = lane & ~(kTierLanes - 1);
+    const bool live = r < b.R;
+    const int rr = live ? r : 0;
+    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+    const int64_t n = *tier.n;
+    const int64_t snap = b.snap[b.rowner[rr]];
+    int64_t lb = 0;
+    bool eq = false;
+    if (live && !(grp && degenerate) && (is_base || n > 0))
+        lb = group_lower_bound(tier.h, tier.m, n, grp ? ke : kb, htail, b.tail, eq);
+    const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // group 0 takes the end key's position
+    if (live && lane == lead && (is_base || n > 0) &&
+        tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
+        rconf[r] = 1;
+        hist_conf[b.rowner[r]] = 1;
+    }
+}
+
 // ---- D.CheckRead, LDS-staged: the top levels of both tiers' sample trees live in LDS, and one
 // lane group finds a read's begin AND end in a tier, sharing every node until the two paths part.
 //
@@ -1062,6 +1092,25 @@ struct CheckReads {
     uint8_t *hist_conf, *rconf;
     unsigned long long* trace;
 };
+
+// Split check: base tier (stage A, own stream) or delta tier (stage B); two instantiations so
+// profiles tell the launches apart.
+template <bool BASE>
+__global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const uint8_t* htail, uint8_t* hist_conf,
+                                                       uint8_t* rconf) {
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    check_read_tier(b, t, BASE, htail, hist_conf, rconf, slot);
+}
+
+void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
+                       const uint8_t* htail) {
+    if (b.R == 0) return;
+    const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
+    if (is_base)
+        fdb_launch(k_check_tier<true>, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf);
+    else
+        fdb_launch(k_check_tier<false>, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf);
+}
 
 __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c) {
     if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);

@@ -10,7 +10,8 @@ N = live history boundaries, F = 9 (fan-out of a 128-byte node holding 8 keys), 
 levels resident in LDS (not fetched from HBM per lookup), R / W = read / write ranges, T = txns,
 E = 2 (R + W) endpoints.
 
-* D.CheckRead (k_check_reads), per launch:
+* D.CheckRead (k_check_tier<true>: the base tier, N = base boundaries; k_check_reads over both
+  tiers when the check is not split), per launch:
     search    2R(P+L) + 2R*4 + 2R*128*max(0, ceil(log_F N) - l)
     range-max R*2V + T
 * D.Sort (k_bucket_sort): one read and one write of every 32-byte sort item: 2 * 32 * E.
@@ -68,7 +69,8 @@ def kernels_from_stats(st: dict, lds_levels: int = 0) -> dict:
         avg_reads = st["check_reads"] / n
         avg_hist = st["check_history"] / n
         avg_txn = st["transactions"] / max(1, st["batches"])
-        out["check"] = kernel_entry("k_check_reads (D.CheckRead: search + range max)", st["ms_check_kernel"], n,
+        out["check"] = kernel_entry("k_check_tier<true> (D.CheckRead, base tier: search + range max)",
+                                    st["ms_check_kernel"], n,
                                     n * check_bytes(avg_reads, avg_txn, avg_hist, lds_levels))
         out["check"]["model"] = {"reads": avg_reads, "history": avg_hist, "lds_levels": lds_levels,
                                  "search_levels": search_levels(avg_hist)}

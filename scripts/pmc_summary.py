@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KERNELS = {"check": "k_check_reads", "sort": "k_bucket_sort", "merge": "k_merge_copy<fdbcs::BatchIns",
+KERNELS = {"check": "k_check_tier<true>", "sort": "k_bucket_sort", "merge": "k_merge_copy<fdbcs::BatchIns",
            "compact": "k_merge_copy<fdbcs::CompactIns"}
 
 root = sys.argv[1]
