@@ -308,6 +308,38 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     }
     int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
     const int64_t hi = min(n, kFan * b);
+    if (b == c && m.skey8) {
+        // Boundary 64(c-1) < q < boundary 64c (sample c's prefix is greater): the answer lies in one
+        // 64-boundary block.  Round one probes the starts of its eight 8-groups through skey8 (one
+        // 128-byte line, not eight); round two the seven keys after the last start below q (one
+        // line).  Prefix ties compare lengths / tails against the boundary itself (probe_cmp).
+        const int64_t B = c > 0 ? kFan * (c - 1) : 0;
+        const int64_t p8 = B + 8 * gl;
+        const bool v8 = p8 < hi;
+        int r8 = 1;
+        if (v8) r8 = probe_cmp(h, p8, m.skey8[p8 / 8], htail, q, qtail);
+        const int k8 = __popc(gmask(v8 && r8 < 0));  // group starts below q
+        const int r_first = __shfl(r8, g0, 64);
+        if (k8 == 0) {  // c == 0 and q <= boundary 0
+            eq = hi > 0 && r_first == 0;
+            return 0;
+        }
+        const int64_t g = B + 8 * (k8 - 1);  // boundary g < q; the answer is in (g, min(g + 8, hi)]
+        const int64_t gend = min(g + 8, hi);
+        const int64_t pk = g + 1 + gl;
+        const bool vk = gl < 7 && pk < gend;
+        int rk = 1;
+        if (vk) rk = probe_cmp(h, pk, h.key[pk], htail, q, qtail);
+        const int k1 = __popc(gmask(vk && rk < 0));
+        const int64_t lb = g + 1 + k1;
+        const int r_stop = __shfl(rk, g0 + (k1 < 7 ? k1 : 6), 64);
+        const int r_next = __shfl(r8, g0 + (k8 < kArity ? k8 : kArity - 1), 64);
+        if (lb < gend)
+            eq = r_stop == 0;  // the probe that stopped the count
+        else if (lb < hi)
+            eq = r_next == 0;  // lb = g + 8: the next group's start, probed in round one
+        return lb;
+    }
     // lower_bound in [lo, lo + span]: rounds of kArity probes at a shrinking stride.  span <= 64
     // normally; a long run of boundaries sharing q's 16-byte prefix (tuple keys) only starts the
     // stride higher, so the lanes still compare tails side by side.
