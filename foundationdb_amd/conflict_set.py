@@ -357,7 +357,9 @@ class ConflictBatch:
         for t in range(self.transaction_count):
             if too_old_transactions is not None and v[t] == TransactionTooOld:
                 too_old_transactions.append(t)
-            elif v[t] == TransactionCommitted and non_conflicting is not None:
+            elif v[t] != TransactionConflict and non_conflicting is not None:
+                # a TooOld transaction registered no ranges, so its conflict status is false: without
+                # a tooOld list the reference counts it as non-conflicting (SkipList.cpp:869-876)
                 non_conflicting.append(t)
         self._collect_conflicting_keys()
         return v

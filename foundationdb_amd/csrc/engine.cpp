@@ -251,6 +251,7 @@ struct fdbcs_batch {
     std::vector<int32_t> out_ids;  // fdbcs_batch_set_conflict_output: global index per transaction
     int32_t out_n = 0;
     uint8_t* out_dev = nullptr;
+    int wp = 0;           // the workspace this batch's detect used
     int32_t max_len = 0;  // longest key added (the sort stages tail windows only past kSortNxLen)
     int64_t wtail = 0;       // history tail bytes the batch's write endpoints could add (8-byte padded)
     std::vector<int32_t> conf_off, conf_idx;
@@ -1364,7 +1365,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + tail_add + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
-    // results (host-mapped, written by the epilogue): verdicts | scalars | completion flag, then the
+    // results (host-mapped; verdicts written by k_resolve, scalars and flag by the epilogue):
+    // verdicts | scalars | completion flag, then the
     // report copies rconf | hist | first_conf
     const ResultLayout RL = result_layout(T, R);
     const size_t o_sc = RL.sc, o_fl = RL.fl, o_rc = RL.rc, o_hc = RL.hc, o_fc = RL.fc, out_bytes = RL.total;
@@ -1407,6 +1409,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (cs->astreams == 2) cs->apar ^= 1;
     const int wp = cs->wpar;
     cs->wpar = (wp + 1) % kNumWork;
+    b->wp = wp;
     Work& w = cs->work[wp];
     // phase events: level 2 records every phase, level 1 only the hot kernels (roofline)
     auto rec = [&](int ph, int level) -> hipEvent_t {
@@ -1640,10 +1643,9 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             auto us = [&](int a, int z) { return (double)((long long)(tr[z] - tr[a])) / 100.0; };  // 100 MHz
             {
                 const int E = 2 * (b->R() + b->W());
-                int nb = (E + 127) / 128;
-                nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+                const int nb = E ? sort_buckets(E, cs->bucket_target) : 1;  // as launch_sort_points
                 std::vector<int32_t> bo(nb + 1);
-                HIPOK(hipMemcpy(bo.data(), cs->work[(cs->wpar + kNumWork - 1) % kNumWork].boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
+                HIPOK(hipMemcpy(bo.data(), cs->work[b->wp].boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
                 int mx = 0, over = 0;
                 for (int k = 0; k < nb; k++) {
                     const int sz = bo[k + 1] - bo[k];

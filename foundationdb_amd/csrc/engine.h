@@ -223,6 +223,8 @@ void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Ti
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per, int alg,
                         int* result_buffer, hipEvent_t sort_begin = nullptr, hipEvent_t sort_end = nullptr,
                         bool long_keys = true);
+// Sample-sort buckets for E endpoints at `target` endpoints per bucket (0 = default).
+int sort_buckets(int E, int target);
 void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
                            bool long_keys, int which, int reps, double* us);
@@ -257,9 +259,10 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
 // Range-max levels of a tier whose size is *n (lvl[3] reset first).
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
                      int64_t grid_hint_n);
-// Verdicts, scalar roll-over, scratch zeroing and the range-max levels of the tier that changed
-// (the base after a compaction, else the delta).
-// verdict_out / flag are host-mapped: the host waits for *flag == seq instead of an event.
+// Scalar roll-over, the device copy of the verdicts, scratch zeroing and the range-max levels of
+// the tier that changed (the base after a compaction, else the delta).  k_resolve already wrote the
+// verdict bytes into the host-mapped result; the epilogue publishes the scalars after them and
+// then the completion flag (the host waits for *flag == seq instead of an event).
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n);

@@ -2558,8 +2558,9 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
 //
 // One workgroup per 4096 boundaries: each wave reduces 16 blocks of 64 versions to level 1, wave 0
 // reduces the 64 level-1 values to level 2, and level 3 is built by atomicMax (reset beforehand).
-// With a batch attached the same launch writes the verdicts, publishes the scalars next to them for
-// the single D2H copy, and zeroes the scratch the next batch expects zeroed.
+// With a batch attached the same launch writes the device copy of the verdicts (k_resolve already
+// wrote the host-mapped bytes), publishes the scalars after them and then the completion flag, and
+// zeroes the scratch the next batch on the workspace expects zeroed.
 
 struct Epilogue {
     const uint8_t* flags;

@@ -114,8 +114,8 @@ struct ConflictBatchT {
         for (int i = 0; i < (int)verdicts.size(); i++) {
             if (tooOldTransactions && verdicts[i] == TransactionTooOld)
                 tooOldTransactions->push_back(i);
-            else if (verdicts[i] == TransactionCommitted)
-                nonConflicting.push_back(i);
+            else if (verdicts[i] != TransactionConflict)  // TooOld lands here without a tooOld list:
+                nonConflicting.push_back(i);               // its conflict status stays false (:869-876)
         }
         if (map) {
             std::vector<int32_t> idx;

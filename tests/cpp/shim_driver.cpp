@@ -82,6 +82,46 @@ int main() {
         printf("b3 commit=%zu report0=%zu idx=%d arena=%d\n", ok.size(), ckr[0].size(),
                ckr[0].size() ? ckr[0].v[0] : -1, arena.pushes);
     }
+    // batch 4: raise oldestVersion to 35; batch 5 then holds a reader below it (TooOld, SkipList.cpp:770),
+    // a writer-only transaction below it (not TooOld: it has no reads) and a reporting writer-only
+    // transaction (no map entry: the entry is created in addTransaction's read loop, :781-784)
+    {
+        ConflictBatch batch(cs);
+        std::vector<int> ok;
+        batch.detectConflicts(40, 35, ok);
+    }
+    {
+        std::map<int, std::vector<int>> ckr;
+        ConflictBatch batch(cs, &ckr);
+        Txn a, w, r;
+        a.read_conflict_ranges.push_back({{"x"}, {"y"}});
+        a.read_snapshot = 20;
+        w.write_conflict_ranges.push_back({{"x"}, {"y"}});
+        w.read_snapshot = 20;
+        r.write_conflict_ranges.push_back({{"p"}, {"q"}});
+        r.read_snapshot = 38;
+        r.report_conflicting_keys = true;
+        batch.addTransaction(a);
+        batch.addTransaction(w);
+        batch.addTransaction(r);
+        std::vector<int> ok, tooOld, late;
+        batch.detectConflicts(50, 35, ok, &tooOld);
+        batch.GetTooOldTransactions(late);  // SkipList.cpp:836-842
+        printf("b5 commit=%zu tooold=%zu late=%zu late0=%d entries=%zu\n", ok.size(), tooOld.size(), late.size(),
+               late.empty() ? -1 : late[0], ckr.size());
+    }
+    // batch 6: without a tooOld list the reference files a TooOld transaction as non-conflicting
+    // (its conflict status is never set, SkipList.cpp:869-876)
+    {
+        ConflictBatch batch(cs);
+        Txn a;
+        a.read_conflict_ranges.push_back({{"x"}, {"y"}});
+        a.read_snapshot = 20;
+        batch.addTransaction(a);
+        std::vector<int> ok;
+        batch.detectConflicts(60, 35, ok);
+        printf("b6 commit=%zu first=%d\n", ok.size(), ok.empty() ? -1 : ok[0]);
+    }
     destroyConflictSet(cs);
     return 0;
 }

@@ -369,6 +369,8 @@ def test_cpp_shim_driver(tmp_path):
     assert "b1 commit=2 tooold=0 report1=1" in out, out
     assert "b2 commit=1 first=1" in out, out
     assert "b3 commit=0 report0=1 idx=1 arena=1" in out, out
+    assert "b5 commit=2 tooold=1 late=1 late0=0 entries=0" in out, out
+    assert "b6 commit=1 first=0" in out, out
 
 
 def test_sharded_engines_match_sharded_oracles(engine, oracle_mod):
