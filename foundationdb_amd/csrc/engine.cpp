@@ -177,6 +177,7 @@ struct fdbcs_conflict_set {
     int check_version = 1;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants)
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
+    int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -878,6 +879,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_GRAPH")) cs->use_graph = v[0] != '0';
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = v[0] != '0';
+    if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
@@ -1412,8 +1414,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     b->wp = wp;
     Work& w = cs->work[wp];
     // phase events: level 2 records every phase, level 1 only the hot kernels (roofline)
+    // level-1 (roofline) events on one batch in timing_every: each event record is a runtime call
+    // on the submitting thread, and the per-launch averages need only a sample of the batches
+    const bool sampled = timing >= 2 || cs->timing_every <= 1 || b->seq % (uint32_t)cs->timing_every == 0;
     auto rec = [&](int ph, int level) -> hipEvent_t {
-        if (timing < level) return nullptr;
+        if (timing < level || (level == 1 && !sampled)) return nullptr;
         b->recorded |= 1u << ph;
         return sl->ev[ph];
     };
