@@ -178,6 +178,7 @@ struct fdbcs_conflict_set {
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
+    bool fuse_epilogue = true;  // FDBCS_FUSE_EPILOGUE=0: separate k_epilogue after every merge
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -880,6 +881,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
+    if (const char* v = getenv("FDBCS_FUSE_EPILOGUE")) cs->fuse_epilogue = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
@@ -1521,10 +1523,6 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhIntra);
     launch_combine(s, bd, w, sc);
     mark(kPhCombine);
-    // D.MergeWrite into the delta tier
-    launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
-                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1));
-    mark(kPhMerge);
     const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
@@ -1533,6 +1531,16 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     bool compact = nd_after > delta_limit_for(cs, cs->n_ub);
     if (cs->gc_interval > 0 && ++cs->batches_since_compact >= cs->gc_interval) compact = true;
     if (cs->tail_ub > cs->tail_reclaim) compact = true;
+    // D.MergeWrite into the delta tier.  Without a compaction the merge copy also does the epilogue
+    // (index and levels of the new delta, scratch, scalars, completion flag): one launch fewer on
+    // the batch-order stream.
+    char* hd = (char*)sl->pin_out.dp;
+    const bool fuse = !compact && cs->fuse_epilogue && timing < 2 && !cs->trace;
+    const FusedEpilogue fe{dlevels_of(cs, dnew), nd_after + 1, (uint8_t*)hd, (uint8_t*)sl->dverdict.p,
+                           (uint32_t*)(hd + o_fl), b->seq};
+    launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
+                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), fuse ? &fe : nullptr);
+    mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;
     const int64_t base_hint = cs->n_ub + nd_after + 1;
@@ -1564,10 +1572,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhGc);
     b->gc_ran = gc;
     b->compacted = compact;
-    char* hd = (char*)sl->pin_out.dp;
-    launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
-                    gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
-                    compact ? base_hint : nd_after + 1);
+    if (!fuse)
+        launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
+                        gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
+                        compact ? base_hint : nd_after + 1);
     if (sa != s || split) fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
     fdb_event(LaunchList::kSyncRecord, sl->ev_free, s);
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base

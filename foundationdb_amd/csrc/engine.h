@@ -83,6 +83,7 @@ struct BatchScalars {
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
     int32_t pre_done;      // k_resolve workgroups done with the pre-pass (reset by the epilogue)
+    int32_t epi_done;      // merge-copy workgroups done (fused epilogue: the last one publishes)
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -236,9 +237,20 @@ void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 // `srcm` are the source tier's levels: its key index is searched, its top level reset for the
 // epilogue's rebuild.
+// Epilogue fused into the merge copy (a batch without compaction): the copy also writes the new
+// delta's search index and range-max levels, the device verdicts and the workspace zeroing, and
+// its last workgroup publishes the scalars and the completion flag (no k_epilogue launch).
+struct FusedEpilogue {
+    MaxLevels m;          // the delta tier's levels / index
+    int64_t out_ub;       // upper bound of the new delta's size (levels reset range)
+    uint8_t* verdict_out;
+    uint8_t* verdict_dev;
+    uint32_t* flag;
+    uint32_t seq;
+};
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end);
+                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe = nullptr);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,

@@ -2129,6 +2129,127 @@ void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc
                                                w.scan[kScanCov], w.scan[kScanSeg]);
 }
 
+// Epilogue work of a batch (k_epilogue, or fused into the merge copy when the batch does not
+// compact): device verdict copy, scratch zeroing, scalars and the completion flag.
+struct Epilogue {
+    const uint8_t* flags;
+    const uint8_t* status;
+    uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T) (host-mapped)
+    uint8_t* verdict_dev;  // [T] device copy of the verdicts (on-device combine)
+    uint32_t* flag;        // host-mapped completion word, set to `seq` last
+    uint32_t seq;
+    unsigned long long* trace;
+    int32_t T;
+    int compacted, gc_ran;
+    uint8_t* zero8;  // hist_conf
+    int64_t zero8_n;
+    uint8_t* zero8r;  // rconf (read-check variants that only set flags)
+    int64_t zero8r_n;
+    int32_t* zero32b;  // ecur
+    int64_t zero32_n;
+    uint64_t* zero64;  // scan arena
+    int64_t zero64_n;
+    int32_t* zero_bc;  // sample-sort bucket counts and cursors [kMaxBuckets]
+    int32_t* zero_bk;
+    int32_t* zero_rank;  // sample ranks + done counter [kMaxSample + 64]
+    BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
+};
+
+// ---- epilogue fused into the delta merge copy (batches without a compaction): the copy writes
+// every boundary of the new delta tier once, so it also writes the tier's search index
+// (skey8 / skey levels: position-indexed) and folds the versions into the range-max levels with
+// atomicMax (levels 1 and 2, reset by k_seg_search; level 3 from level 2 by the last workgroup,
+// which then publishes the scalars and the completion flag).  Saves the epilogue launch and its
+// queue gap on the batch-order stream.
+__device__ __forceinline__ void epi_index_store(const MaxLevels& m, int64_t o, const ulonglong2& key) {
+    if ((o & 7) != 0) return;
+    m.skey8[o >> 3] = key;
+    if ((o & 63) != 0) return;
+    int64_t d = o >> 6;
+    m.skey[0][d] = key;
+    for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
+        d /= kArity;
+        m.skey[L][d] = key;
+    }
+}
+// Wave-cooperative max of (output position o, version v) into levels 1 and 2: one atomic per
+// distinct 64-boundary block of the wave.  Every lane of the wave calls it (o < 0: no output).
+__device__ __forceinline__ void epi_wave_levels(const MaxLevels& m, int64_t o, int64_t v) {
+    const int64_t key = o >= 0 ? (o >> 6) : -1;
+    bool pending = key >= 0;
+    for (;;) {
+        const uint64_t act = __ballot(pending);
+        if (!act) break;
+        const int leader = __ffsll((long long)act) - 1;
+        const int64_t k0 = __shfl(key, leader, 64);
+        const bool mine = pending && key == k0;
+        int64_t x = mine ? v : LLONG_MIN;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t y = __shfl_xor(x, off, 64);
+            x = y > x ? y : x;
+        }
+        if ((threadIdx.x & 63) == leader) {
+            atomicMax((long long*)&m.lvl[1][k0], (long long)x);
+            atomicMax((long long*)&m.lvl[2][k0 >> 6], (long long)x);
+        }
+        pending = pending && !mine;
+    }
+}
+__device__ __forceinline__ void epi_point_levels(const MaxLevels& m, int64_t o, int64_t v) {
+    atomicMax((long long*)&m.lvl[1][o >> 6], (long long)v);
+    atomicMax((long long*)&m.lvl[2][o >> 12], (long long)v);
+}
+// Grid-stride part: device verdicts and the scratch the workspace's next batch expects zeroed.
+__device__ __forceinline__ void epi_zero(const Epilogue& ep) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = tid; t < ep.T; t += stride)
+        ep.verdict_dev[t] = (ep.flags[t] & kFlagTooOld) ? 1 : (ep.status[t] == kCommitted ? 2 : 0);
+    for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
+    for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
+    for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
+    for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
+    for (int64_t i = tid; i < kMaxBuckets; i += stride) {
+        ep.zero_bc[i] = 0;
+        ep.zero_bk[i] = 0;
+    }
+    for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
+}
+// Last workgroup: level 3 from level 2, scalar roll-over, scalars next to the verdicts, flag.
+__device__ void epi_finish(const MaxLevels& m, Scalars* sc, const Epilogue& ep) {
+    const int64_t n0 = __hip_atomic_load(&sc->nd_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan, n3 = (n2 + kFan - 1) / kFan;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t j = wid; j < n3; j += blockDim.x >> 6) {
+        const int64_t i = j * kFan + lane;
+        int64_t x = i < n2 ? __hip_atomic_load((long long*)&m.lvl[2][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : LLONG_MIN;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t y = __shfl_xor(x, off, 64);
+            x = y > x ? y : x;
+        }
+        if (lane == 0) m.lvl[3][j] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sc->nd = n0;
+        sc->tail_used = sc->tail_next;
+        Scalars out = *sc;
+        out.debug_error = ep.bsc->debug_error;
+        out.intra_rounds = ep.bsc->rounds;
+        out.intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
+        ep.bsc->pre_done = 0;
+        ep.bsc->debug_error = 0;
+        ep.bsc->epi_done = 0;
+        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;
+    }
+    __syncthreads();
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------ D.MergeWrite
 //
 // mergeWriteConflictRanges (SkipList.cpp:899-924, 414-424): for each union segment [B, E):
@@ -2144,11 +2265,13 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
 
 __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, MaxLevels hm,
                                                        const uint8_t* htail, const Scalars* sc, const int64_t* n_in,
-                                                       int64_t* lvl3, int64_t lvl3_n) {
+                                                       int64_t* lvl3, int64_t lvl3_n, int64_t lvl1_n) {
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // the history check of this batch is done with the old hierarchy: reset its top level for the
-    // epilogue's atomicMax build
+    // epilogue's atomicMax build (and levels 1-2 when the merge copy builds them: fused epilogue)
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = gt; i < lvl1_n; i += (int64_t)gridDim.x * blockDim.x) hm.lvl[1][i] = LLONG_MIN;
+    for (int64_t i = gt; i < (lvl1_n + kFan - 1) / kFan; i += (int64_t)gridDim.x * blockDim.x) hm.lvl[2][i] = LLONG_MIN;
     // 2*kArity lanes per union segment: lane group 0 locates B, group 1 locates E (cooperative search)
     const int U = sc->n_segments;
     const int s = (int)(gt / (2 * kArity)), role = (int)((gt / kArity) & 1);
@@ -2297,7 +2420,12 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                         dst.key[dsto[k]] = make_ulonglong2(khi[k], klo[k]);
                         reinterpret_cast<uint64_t*>(dst.lt)[dsto[k]] = lt[k];
                         dst.ver[dsto[k]] = (int64_t)vv[k];
+                        if (Ins::kEpi && ins.epi) epi_index_store(ins.em, dsto[k], make_ulonglong2(khi[k], klo[k]));
                     }
+                }
+                if (Ins::kEpi && ins.epi) {
+#pragma unroll
+                    for (int k = 0; k < kPer; k++) epi_wave_levels(ins.em, dsto[k], (int64_t)vv[k]);
                 }
             }
         } else {
@@ -2313,16 +2441,40 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                 dst.key[o] = src.key[i];
                 dst.lt[o] = src.lt[i];
                 dst.ver[o] = src.ver[i];
+                if (Ins::kEpi && ins.epi) {
+                    epi_index_store(ins.em, o, src.key[i]);
+                    epi_point_levels(ins.em, o, src.ver[i]);
+                }
             }
         }
         for (int sg = s_ins0 + threadIdx.x; sg < s_ins1; sg += blockDim.x)
             ins(sg, dst, g.lo[sg] - g.rem[sg] + g.ins[sg]);
         __syncthreads();
     }
+    if (Ins::kEpi && ins.epi) {  // fused epilogue: scratch + verdict copy, then the last workgroup publishes
+        epi_zero(ins.ep);
+        __shared__ int s_last;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int prev = __hip_atomic_fetch_add(&ins.ep.bsc->epi_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev == (int)gridDim.x - 1;
+        }
+        __syncthreads();
+        if (s_last) {
+            __threadfence();
+            epi_finish(ins.em, ins.esc, ins.ep);
+        }
+    }
 }
 
 // Inserts of a union segment: B at `now`, E (when needed) at the version it had.
 struct BatchIns {
+    static constexpr bool kEpi = true;
+    int epi;            // fused epilogue (no compaction this batch): index + levels + publish
+    MaxLevels em;       // the delta tier's levels / index (the arrays both delta buffers share)
+    Scalars* esc;
+    Epilogue ep;
     BatchDev b;
     const uint32_t* pmeta;
     const int32_t *seg_b, *seg_e;
@@ -2346,6 +2498,10 @@ struct BatchIns {
         dst.key[o] = make_ulonglong2(kb.hi, kb.lo);
         dst.lt[o] = make_uint2(kb.len, tb);
         dst.ver[o] = now;
+        if (epi) {
+            epi_index_store(em, o, make_ulonglong2(kb.hi, kb.lo));
+            epi_point_levels(em, o, now);
+        }
         if (endins[s]) {
             const DKey ke = key(seg_e[s], 1);
             uint32_t te = 0;
@@ -2356,6 +2512,10 @@ struct BatchIns {
             dst.key[o + 1] = make_ulonglong2(ke.hi, ke.lo);
             dst.lt[o + 1] = make_uint2(ke.len, te);
             dst.ver[o + 1] = vend[s];
+            if (epi) {
+                epi_index_store(em, o + 1, make_ulonglong2(ke.hi, ke.lo));
+                epi_point_levels(em, o + 1, vend[s]);
+            }
         }
     }
 };
@@ -2369,21 +2529,65 @@ static unsigned copy_tiles(int64_t grid_hint_n, int tile) {
     return (unsigned)tiles;
 }
 
+static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, int gc_ran, uint8_t* verdict_out,
+                              uint8_t* verdict_dev, uint32_t* flag, uint32_t seq) {
+    Epilogue ep{};
+    ep.verdict_dev = verdict_dev;
+    ep.flag = flag;
+    ep.seq = seq;
+    ep.trace = w.trace;
+    ep.flags = b.flags;
+    ep.status = w.status;
+    ep.verdict_out = verdict_out;
+    ep.T = b.T;
+    ep.compacted = compacted;
+    ep.gc_ran = gc_ran;
+    ep.zero8 = w.hist_conf;
+    ep.zero8_n = w.cap_T;
+    ep.zero8r = w.rconf;
+    ep.zero8r_n = w.cap_R;
+    ep.zero32b = w.ecur;
+    ep.zero32_n = w.cap_R;
+    ep.zero64 = w.scan_arena;
+    ep.zero64_n = w.scan_words;
+    ep.zero_bc = w.bcount;
+    ep.zero_bk = w.bcursor;
+    ep.zero_rank = w.srank;
+    ep.bsc = w.bsc;
+    return ep;
+}
+
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end) {
+                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe) {
     const int Wn = b.W > 0 ? b.W : 1;
+    // fused epilogue: levels 1-2 of the new delta are built by atomicMax in the copy (reset here)
+    const int64_t lvl1_n = fe ? (fe->out_ub + kFan - 1) / kFan + 1 : 0;
     fdb_launch(k_seg_search, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
-                       htail, sc,
-                       &sc->nd, srcm.lvl[3], lvl3_n);
+               htail, sc, &sc->nd, srcm.lvl[3], lvl3_n, lvl1_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
                    w.scan[kScanSegSum]);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
-    BatchIns ins{b, w.pmeta, w.seg_b, w.seg_e, w.seg_tlen, w.seg_vend, w.seg_endins, htail, sc, now};
+    BatchIns ins{};
+    ins.epi = fe ? 1 : 0;
+    if (fe) {
+        ins.em = fe->m;
+        ins.esc = sc;
+        ins.ep = make_epilogue(b, w, 0, 0, fe->verdict_out, fe->verdict_dev, fe->flag, fe->seq);
+    }
+    ins.b = b;
+    ins.pmeta = w.pmeta;
+    ins.seg_b = w.seg_b;
+    ins.seg_e = w.seg_e;
+    ins.tlen = w.seg_tlen;
+    ins.vend = w.seg_vend;
+    ins.endins = w.seg_endins;
+    ins.htail = htail;
+    ins.sc = sc;
+    ins.now = now;
     fdb_launch((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile)), dim3(kBlock), 0,
-                       s, batch_segs(w), src,
-                       dst, &sc->nd, &sc->n_segments, ins);
+               s, batch_segs(w), src, dst, &sc->nd, &sc->n_segments, ins);
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 
@@ -2462,6 +2666,12 @@ struct CompactIns {
         dst.lt[o] = delta.lt[s];
         dst.ver[o] = val[s];
     }
+    // no fused epilogue (the compaction's epilogue rebuilds the base tier's levels)
+    static constexpr bool kEpi = false;
+    int epi = 0;
+    MaxLevels em{};
+    Scalars* esc = nullptr;
+    Epilogue ep{};
 };
 
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
@@ -2562,29 +2772,7 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
 // wrote the host-mapped bytes), publishes the scalars after them and then the completion flag, and
 // zeroes the scratch the next batch on the workspace expects zeroed.
 
-struct Epilogue {
-    const uint8_t* flags;
-    const uint8_t* status;
-    uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T) (host-mapped)
-    uint8_t* verdict_dev;  // [T] device copy of the verdicts (on-device combine)
-    uint32_t* flag;        // host-mapped completion word, set to `seq` last
-    uint32_t seq;
-    unsigned long long* trace;
-    int32_t T;
-    int compacted, gc_ran;
-    uint8_t* zero8;  // hist_conf
-    int64_t zero8_n;
-    uint8_t* zero8r;  // rconf (read-check variants that only set flags)
-    int64_t zero8r_n;
-    int32_t* zero32b;  // ecur
-    int64_t zero32_n;
-    uint64_t* zero64;  // scan arena
-    int64_t zero64_n;
-    int32_t* zero_bc;  // sample-sort bucket counts and cursors [kMaxBuckets]
-    int32_t* zero_bk;
-    int32_t* zero_rank;  // sample ranks + done counter [kMaxSample + 64]
-    BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
-};
+
 
 // Range-max levels over lvl[0][0, n0) (lvl[3] reset beforehand); with a batch attached, also the
 // verdicts and the scalar roll-over.  n0 comes from `n_levels` or, for a batch, from the tier
@@ -2799,29 +2987,7 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n) {
-    Epilogue ep;
-    ep.verdict_dev = verdict_dev;
-    ep.flag = flag;
-    ep.seq = seq;
-    ep.trace = w.trace;
-    ep.flags = b.flags;
-    ep.status = w.status;
-    ep.verdict_out = verdict_out;
-    ep.T = b.T;
-    ep.compacted = compacted;
-    ep.gc_ran = gc_ran;
-    ep.zero8 = w.hist_conf;
-    ep.zero8_n = w.cap_T;
-    ep.zero8r = w.rconf;
-    ep.zero8r_n = w.cap_R;
-    ep.zero32b = w.ecur;
-    ep.zero32_n = w.cap_R;
-    ep.zero64 = w.scan_arena;
-    ep.zero64_n = w.scan_words;
-    ep.zero_bc = w.bcount;
-    ep.zero_bk = w.bcursor;
-    ep.zero_rank = w.srank;
-    ep.bsc = w.bsc;
+    const Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq);
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
     fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
