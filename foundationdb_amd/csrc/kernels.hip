@@ -1313,13 +1313,11 @@ constexpr int kTailWin = 12;  // 96 tail bytes: keys up to 112 bytes compare wit
 __device__ __forceinline__ void load_tail_window(uint64_t* win, const uint8_t* arena, uint32_t tail, uint32_t len) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t n = len > 16u ? len - 16u : 0u;
-    uint64_t w[kTailWin];
-#pragma unroll
-    for (int j = 0; j < kTailWin; j++) w[j] = (uint32_t)(8 * j) < n ? tail_word(arena + tail + 8 * j) : 0ull;
 #pragma unroll
     for (int j = 0; j < kTailWin; j++) {
         const int vb = (int)n - 8 * j;  // bytes of word j inside the tail
-        win[j] = vb >= 8 ? w[j] : (vb <= 0 ? 0ull : w[j] & (~0ull << (64 - 8 * vb)));
+        const uint64_t x = vb > 0 ? tail_word(arena + tail + 8 * j) : 0ull;
+        win[j] = vb >= 8 ? x : (vb <= 0 ? 0ull : x & (~0ull << (64 - 8 * vb)));
     }
 #endif
 }
@@ -1445,9 +1443,12 @@ __global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortI
                     const SortItem& v = sh[k];
                     if (!item_less_tail_win(swin[k], v.len, v.tail, v.meta, swin[k - 1], u.len, u.tail, u.meta, arena))
                         break;
-                    const SortItem tmpi = sh[k - 1];
-                    sh[k - 1] = sh[k];
-                    sh[k] = tmpi;
+                    const ulonglong2 t0 = reinterpret_cast<const ulonglong2*>(&sh[k - 1])[0],
+                                     t1 = reinterpret_cast<const ulonglong2*>(&sh[k - 1])[1];
+                    reinterpret_cast<ulonglong2*>(&sh[k - 1])[0] = reinterpret_cast<const ulonglong2*>(&sh[k])[0];
+                    reinterpret_cast<ulonglong2*>(&sh[k - 1])[1] = reinterpret_cast<const ulonglong2*>(&sh[k])[1];
+                    reinterpret_cast<ulonglong2*>(&sh[k])[0] = t0;
+                    reinterpret_cast<ulonglong2*>(&sh[k])[1] = t1;
 #pragma unroll
                     for (int z = 0; z < kTailWin; z++) {
                         const uint64_t tw = swin[k - 1][z];
@@ -2167,9 +2168,13 @@ __device__ __forceinline__ void epi_index_store(const MaxLevels& m, int64_t o, c
     if ((o & 63) != 0) return;
     int64_t d = o >> 6;
     m.skey[0][d] = key;
+    // level L at skey[0] + sum of the lower levels' capacities (no dynamic index into skey[]:
+    // that would copy the kernel-argument struct to scratch)
+    int64_t off = 0;
     for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
+        off += idx_level_cap(m.idx_cap, L - 1);
         d /= kArity;
-        m.skey[L][d] = key;
+        m.skey[0][off + d] = key;
     }
 }
 // Wave-cooperative max of (output position o, version v) into levels 1 and 2: one atomic per
@@ -2215,8 +2220,23 @@ __device__ __forceinline__ void epi_zero(const Epilogue& ep) {
     }
     for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
 }
+// The scalars after the verdicts in the host-mapped result (word by word: a local Scalars copy
+// would live in scratch), with the workspace's batch statistics; resets the workspace counters.
+__device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogue& ep) {
+    static_assert(sizeof(Scalars) % 8 == 0, "Scalars is copied in 8-byte words");
+    Scalars* out = (Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T));
+    const uint64_t* from = (const uint64_t*)sc;
+    uint64_t* to = (uint64_t*)out;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(Scalars) / 8); i++) to[i] = from[i];
+    out->debug_error = ep.bsc->debug_error;
+    out->intra_rounds = ep.bsc->rounds;
+    out->intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
+    ep.bsc->pre_done = 0;  // k_resolve's pre-pass counter (its workgroups have all finished)
+    ep.bsc->debug_error = 0;
+}
 // Last workgroup: level 3 from level 2, scalar roll-over, scalars next to the verdicts, flag.
-__device__ void epi_finish(const MaxLevels& m, Scalars* sc, const Epilogue& ep) {
+__device__ __forceinline__ void epi_finish(const MaxLevels& m, Scalars* sc, const Epilogue& ep) {
     const int64_t n0 = __hip_atomic_load(&sc->nd_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan, n3 = (n2 + kFan - 1) / kFan;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2235,14 +2255,8 @@ __device__ void epi_finish(const MaxLevels& m, Scalars* sc, const Epilogue& ep) 
     if (threadIdx.x == 0) {
         sc->nd = n0;
         sc->tail_used = sc->tail_next;
-        Scalars out = *sc;
-        out.debug_error = ep.bsc->debug_error;
-        out.intra_rounds = ep.bsc->rounds;
-        out.intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
-        ep.bsc->pre_done = 0;
-        ep.bsc->debug_error = 0;
+        publish_scalars(sc, ep);
         ep.bsc->epi_done = 0;
-        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;
     }
     __syncthreads();
     __threadfence_system();
@@ -2823,10 +2837,12 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
                 m.lvl[1][b1l] = mine;
                 m.skey[0][b1l] = sk;
                 // search-tree levels above: block b1l is entry b1l / A^L of level L when divisible
-                int64_t d = b1l;
+                // (arithmetic level offsets: a dynamic index into skey[] would spill the argument)
+                int64_t d = b1l, off = 0;
                 for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
+                    off += idx_level_cap(m.idx_cap, L - 1);
                     d /= kArity;
-                    m.skey[L][d] = sk;
+                    m.skey[0][off + d] = sk;
                 }
             }
             l1[wid * (kFan / 4) + lane] = mine;
@@ -2876,13 +2892,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
             sc->nd = sc->nd_next;
         }
         sc->tail_used = ep.gc_ran ? sc->tail_gc : sc->tail_next;
-        Scalars out = *sc;
-        out.debug_error = ep.bsc->debug_error;
-        ep.bsc->pre_done = 0;  // k_resolve's pre-pass counter (its workgroups have all finished)
-        out.intra_rounds = ep.bsc->rounds;
-        out.intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
-        *(Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T)) = out;
-        ep.bsc->debug_error = 0;
+        publish_scalars(sc, ep);
     }
     __syncthreads();
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiHost);
