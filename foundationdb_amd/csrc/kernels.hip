@@ -2467,18 +2467,19 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
     }
     if (Ins::kEpi && ins.epi) {  // fused epilogue: scratch + verdict copy, then the last workgroup publishes
         epi_zero(ins.ep);
+        // Completion count without a device-scope release (an L2 write-back per workgroup would
+        // stall every tile): the last workgroup only reads levels 1-2, which were updated by
+        // device-scope atomics, so each wave merely waits for its own atomics to be performed.
+        // Plain stores (the tier, its index) reach later kernels through the kernel boundary.
         __shared__ int s_last;
-        __threadfence();
+        __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         if (threadIdx.x == 0) {
-            const int prev = __hip_atomic_fetch_add(&ins.ep.bsc->epi_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            const int prev = __hip_atomic_fetch_add(&ins.ep.bsc->epi_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_last = prev == (int)gridDim.x - 1;
         }
         __syncthreads();
-        if (s_last) {
-            __threadfence();
-            epi_finish(ins.em, ins.esc, ins.ep);
-        }
+        if (s_last) epi_finish(ins.em, ins.esc, ins.ep);
     }
 }
 
