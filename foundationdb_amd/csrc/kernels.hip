@@ -2177,8 +2177,10 @@ __device__ __forceinline__ void epi_index_store(const MaxLevels& m, int64_t o, c
         m.skey[0][off + d] = key;
     }
 }
-// Wave-cooperative max of (output position o, version v) into levels 1 and 2: one atomic per
-// distinct 64-boundary block of the wave.  Every lane of the wave calls it (o < 0: no output).
+// Wave-cooperative max of (output position o, version v) into level 1: one atomic per distinct
+// 64-boundary block of the wave.  Every lane of the wave calls it (o < 0: no output).  Levels 2
+// and 3 are built from level 1 by the last workgroup (atomics on their few entries would
+// serialize thousands of updates per address).
 __device__ __forceinline__ void epi_wave_levels(const MaxLevels& m, int64_t o, int64_t v) {
     const int64_t key = o >= 0 ? (o >> 6) : -1;
     bool pending = key >= 0;
@@ -2194,16 +2196,12 @@ __device__ __forceinline__ void epi_wave_levels(const MaxLevels& m, int64_t o, i
             const int64_t y = __shfl_xor(x, off, 64);
             x = y > x ? y : x;
         }
-        if ((threadIdx.x & 63) == leader) {
-            atomicMax((long long*)&m.lvl[1][k0], (long long)x);
-            atomicMax((long long*)&m.lvl[2][k0 >> 6], (long long)x);
-        }
+        if ((threadIdx.x & 63) == leader) atomicMax((long long*)&m.lvl[1][k0], (long long)x);
         pending = pending && !mine;
     }
 }
 __device__ __forceinline__ void epi_point_levels(const MaxLevels& m, int64_t o, int64_t v) {
     atomicMax((long long*)&m.lvl[1][o >> 6], (long long)v);
-    atomicMax((long long*)&m.lvl[2][o >> 12], (long long)v);
 }
 // Grid-stride part: device verdicts and the scratch the workspace's next batch expects zeroed.
 __device__ __forceinline__ void epi_zero(const Epilogue& ep) {
@@ -2240,10 +2238,21 @@ __device__ __forceinline__ void epi_finish(const MaxLevels& m, Scalars* sc, cons
     const int64_t n0 = __hip_atomic_load(&sc->nd_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan, n3 = (n2 + kFan - 1) / kFan;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t j = wid; j < n3; j += blockDim.x >> 6) {
+    for (int64_t j = wid; j < n2; j += blockDim.x >> 6) {  // level 2 from level 1 (device-scope atomics)
         const int64_t i = j * kFan + lane;
-        int64_t x = i < n2 ? __hip_atomic_load((long long*)&m.lvl[2][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+        int64_t x = i < n1 ? __hip_atomic_load((long long*)&m.lvl[1][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                            : LLONG_MIN;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t y = __shfl_xor(x, off, 64);
+            x = y > x ? y : x;
+        }
+        if (lane == 0) m.lvl[2][j] = x;
+    }
+    __syncthreads();
+    for (int64_t j = wid; j < n3; j += blockDim.x >> 6) {  // level 3 from level 2 (this workgroup)
+        const int64_t i = j * kFan + lane;
+        int64_t x = i < n2 ? m.lvl[2][i] : LLONG_MIN;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const int64_t y = __shfl_xor(x, off, 64);
