@@ -178,7 +178,11 @@ struct fdbcs_conflict_set {
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
-    bool fuse_epilogue = true;  // FDBCS_FUSE_EPILOGUE=0: separate k_epilogue after every merge
+    // FDBCS_FUSE_EPILOGUE=1: the merge copy of a batch without compaction also does the epilogue
+    // (index, levels, scratch, publication) and k_epilogue is not launched.  Measured slower at
+    // C2 (27.5M vs 30.1M txns/s): level 1 by atomics and levels 2-3 rebuilt by one last workgroup
+    // through device-scope loads cost more than the launch they save.  Off by default.
+    bool fuse_epilogue = false;
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
