@@ -438,3 +438,31 @@ def test_empty_batches(engine, oracle_mod):
         assert (ve == vo).all()
         assert ce == {t: sorted(v) for t, v in co.items()}
         now += 4
+
+
+@pytest.mark.parametrize("knobs", [{"FDBCS_FUSE_EPILOGUE": "1"}, {"FDBCS_SPLIT_CHECK": "0"}, {"FDBCS_SORT_WIN": "0"}])
+def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
+    """Non-default pipeline variants kept for measurement stay exact: the epilogue
+    fused into the merge copy, the unsplit read check, and long-key sorting without LDS windows."""
+    saved = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
+    try:
+        eng = EngineDriver(engine, gc_interval=0, delta_limit=400)  # compactions every few batches
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    ora = oracle_mod.OracleConflictSet()
+    rng = np.random.default_rng(71)
+    now = 10
+    for i in range(20):
+        pb = W.random_small_batch(rng, 250, alphabet=6 if i % 2 else 200, max_len=24 if i % 3 == 0 else 3, now=now,
+                                  staleness=12)
+        ve, ce = eng.detect(pb, now, now - 9)
+        vo, co = ora.detect(pb, now, now - 9)
+        assert (ve == vo).all()
+        assert ce == {t: sorted(v) for t, v in co.items()}
+        now += 4
+    assert eng.cs.history_size() > 0
