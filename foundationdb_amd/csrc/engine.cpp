@@ -177,6 +177,11 @@ struct fdbcs_conflict_set {
     int check_version = 1;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants)
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
+    bool sorted_reads = false; // FDBCS_SORTED_READS=1: the split check waits for stage A and takes reads
+                               // in sorted begin-key order (A/B)
+    bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
+    bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
+                              // even for batches with keys over 16 bytes (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
     // FDBCS_FUSE_EPILOGUE=1: the merge copy of a batch without compaction also does the epilogue
     // (index, levels, scratch, publication) and k_epilogue is not launched.  Measured slower at
@@ -884,6 +889,9 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_GRAPH")) cs->use_graph = v[0] != '0';
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = v[0] != '0';
+    if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
+    if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
+    if (const char* v = getenv("FDBCS_SORTED_READS")) cs->sorted_reads = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_FUSE_EPILOGUE")) cs->fuse_epilogue = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
@@ -1445,6 +1453,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // on the stream its half of D.CheckRead runs beside stage A on its own stream; stage B keeps the
     // delta half.  One graph per batch cannot express the wait, so graph mode keeps one check.
     const bool split = cs->split_check && !graph && !cs->serial && timing < 2;
+    const bool sorted_reads = split && cs->sorted_reads && sa != s;
     cs->stats.host_ms_prepare += host_ms_since(t_begin);
     const auto t_rec = std::chrono::steady_clock::now();
     // ---- record stage A: upload, D.Sort and the candidate edges of D.CheckIntraBatch
@@ -1463,6 +1472,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sa);
     if ((rc = mark(kPhUpload))) return t_record = nullptr, rc;
     const BatchDev& bd = b->bd;
+    const bool long_keys = cs->long_probe && b->max_len > 16;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
@@ -1495,8 +1505,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sc_);
         if (ws_busy) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sc_);
         if (cs->cmp_recorded && hipEventQuery(cs->ev_cmp) != hipSuccess) fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
+        if (sorted_reads) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
-        launch_check_tier(sc_, bd, w, base, true, htail);
+        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, sorted_reads);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
@@ -1505,7 +1516,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        launch_check_tier(s, bd, w, delta, false, htail);
+        if (sorted_reads) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
+        launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax, sorted_reads);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
@@ -1543,7 +1555,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const FusedEpilogue fe{dlevels_of(cs, dnew), nd_after + 1, (uint8_t*)hd, (uint8_t*)sl->dverdict.p,
                            (uint32_t*)(hd + o_fl), b->seq};
     launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
-                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), fuse ? &fe : nullptr);
+                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), fuse ? &fe : nullptr, long_keys);
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;

@@ -215,8 +215,10 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
                   const uint8_t* htail, int check_version = 2, int check_grid_cap = 2048);
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
 // delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
+// long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail);
+                       const uint8_t* htail, bool long_keys = false, bool lead_rmax = false,
+                       bool sorted_reads = false);
 // bucket_target: endpoints per sample-sort bucket (0 = default 128; tests force oversized buckets).
 // sample_per: splitter samples per bucket (0 = default 8).
 // alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
@@ -250,7 +252,8 @@ struct FusedEpilogue {
 };
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe = nullptr);
+                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe = nullptr,
+                  bool long_keys = false);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,

@@ -250,6 +250,70 @@ __device__ __forceinline__ int64_t tree_lower_bound(const Hist& h, const MaxLeve
     return lb;
 }
 
+// ---- long-key probes (batches with keys over 16 bytes: C4 tuple keys)
+//
+// Keys of one tuple subspace/user share their 16-byte prefix, so the last rounds of a lookup tie
+// on the prefix and compare tails.  The generic probe loads the boundary's (len, tail) only after
+// its prefix tied, then the two tails 32 bytes per dependent round, each tail word through two
+// unaligned loads.  The long-key probe instead holds the query's tail words in registers for the
+// whole lookup (kQW words), loads the boundary's (len, tail) beside its prefix, and reads the
+// history tail (8-byte aligned in its arena) as whole words, kHW per round: one dependent round
+// after the prefix for tails up to 48 bytes, two up to 96.
+constexpr int kQW = 12;  // query tail words in registers: keys up to 112 bytes compare without reloads
+[[maybe_unused]] constexpr int kHW = 6;  // history tail words per load round
+struct QTail {
+    uint64_t w[kQW];  // big-endian words of query bytes [16, 16 + 8 kQW), garbage past the key's end
+};
+
+__device__ __forceinline__ void load_qtail(QTail& qt, const DKey& q, const uint8_t* qtail) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t n = q.len > 16u ? q.len - 16u : 0u;
+    const uintptr_t a = (uintptr_t)(qtail + q.tail);
+    const uint64_t* w = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint32_t cnt = ((uint32_t)(a & 7u) + n + 7u) / 8u;  // aligned words holding the tail
+    uint64_t raw[kQW + 1];
+#pragma unroll
+    for (int j = 0; j <= kQW; j++) raw[j] = (uint32_t)j < cnt ? w[j] : 0ull;
+#pragma unroll
+    for (int j = 0; j < kQW; j++) qt.w[j] = __builtin_bswap64(sh ? (raw[j] >> sh) | (raw[j + 1] << (64u - sh)) : raw[j]);
+#endif
+}
+
+// probe_cmp with the boundary's (len, tail) already loaded and the query tail in registers.
+__device__ __forceinline__ int probe_cmp_long(const ulonglong2& k, const uint2& lt, const uint8_t* htail, const DKey& q,
+                                              const QTail& qt, const uint8_t* qtail) {
+    if (k.x != q.hi) return k.x < q.hi ? -1 : 1;
+    if (k.y != q.lo) return k.y < q.lo ? -1 : 1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (lt.x > 16u && q.len > 16u) {
+        const uint64_t* ha = (const uint64_t*)hist_tail(htail, lt.y);
+        const uint32_t n = (lt.x < q.len ? lt.x : q.len) - 16u;  // common tail bytes
+        const int nw = (int)((n + 7u) / 8u);
+#pragma unroll
+        for (int j0 = 0; j0 < kQW; j0 += kHW) {
+            if (j0 >= nw) break;
+            uint64_t x[kHW];
+#pragma unroll
+            for (int u = 0; u < kHW; u++) x[u] = j0 + u < nw ? ha[j0 + u] : 0ull;
+#pragma unroll
+            for (int u = 0; u < kHW; u++) {
+                const int j = j0 + u;
+                const int vb = (int)n - 8 * j;  // bytes of word j inside the shorter tail
+                if (vb <= 0) break;
+                const uint64_t msk = vb >= 8 ? ~0ull : ~0ull << (64 - 8 * vb);
+                const uint64_t hx = __builtin_bswap64(x[u]) & msk, qy = qt.w[j] & msk;
+                if (hx != qy) return hx < qy ? -1 : 1;
+            }
+        }
+        if (nw > kQW)  // both tails run past the registers: the rest from memory
+            return tail_cmp(hist_tail(htail, lt.y) + 8 * kQW, lt.x - 8 * kQW, qtail + q.tail + 8 * kQW,
+                            q.len - 8 * kQW);
+    }
+#endif
+    return (lt.x > q.len) - (lt.x < q.len);
+}
+
 // ---- cooperative search: kArity lanes per query, one kArity-entry tree node per level
 //
 // Each lane of an aligned kArity-lane group loads one entry of the node, so a level is one
@@ -260,12 +324,26 @@ __device__ __forceinline__ uint32_t gmask(bool pred) {
     return (uint32_t)(m >> (threadIdx.x & 63 & ~(kArity - 1))) & ((1u << kArity) - 1u);
 }
 
+// LONG: the long-key probes above (the batch has keys over 16 bytes); same result.
+template <bool LONG = false>
 __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
                                                      const uint8_t* htail, const uint8_t* qtail, bool& eq) {
     const int gl = threadIdx.x & (kArity - 1);
     const int g0 = threadIdx.x & 63 & ~(kArity - 1);  // first lane of the group
     eq = false;
     if (n <= 0) return 0;
+    QTail qt;
+    if constexpr (LONG) load_qtail(qt, q, qtail);  // in flight during the descent
+    // one probe of boundary p (prefix k): the long-key form loads (len, tail) beside the prefix
+    auto probe = [&](int64_t p, const ulonglong2* kp) -> int {
+        if constexpr (LONG) {
+            const ulonglong2 k = *kp;
+            const uint2 lt = h.lt[p];
+            return probe_cmp_long(k, lt, htail, q, qt, qtail);
+        } else {
+            return probe_cmp(h, p, *kp, htail, q, qtail);
+        }
+    };
     int64_t sz[kIdxLevels];
     sz[0] = (n + kFan - 1) / kFan;
 #pragma unroll
@@ -317,7 +395,7 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
         const int64_t p8 = B + 8 * gl;
         const bool v8 = p8 < hi;
         int r8 = 1;
-        if (v8) r8 = probe_cmp(h, p8, m.skey8[p8 / 8], htail, q, qtail);
+        if (v8) r8 = probe(p8, &m.skey8[p8 / 8]);
         const int k8 = __popc(gmask(v8 && r8 < 0));  // group starts below q
         const int r_first = __shfl(r8, g0, 64);
         if (k8 == 0) {  // c == 0 and q <= boundary 0
@@ -329,7 +407,7 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
         const int64_t pk = g + 1 + gl;
         const bool vk = gl < 7 && pk < gend;
         int rk = 1;
-        if (vk) rk = probe_cmp(h, pk, h.key[pk], htail, q, qtail);
+        if (vk) rk = probe(pk, &h.key[pk]);
         const int k1 = __popc(gmask(vk && rk < 0));
         const int64_t lb = g + 1 + k1;
         const int r_stop = __shfl(rk, g0 + (k1 < 7 ? k1 : 6), 64);
@@ -351,7 +429,7 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
         const int64_t p = lo + stride * (gl + 1) - 1;
         const bool v = stride * (gl + 1) <= span && p < hi;
         int r = 1;
-        if (v) r = probe_cmp(h, p, h.key[p], htail, q, qtail);
+        if (v) r = probe(p, &h.key[p]);
         const uint32_t valid = gmask(v);
         const int cnt = __popc(gmask(v && r < 0));
         const int stop = __shfl(r, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
@@ -584,25 +662,90 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
 // launch (stage B) OR into the same flags.  is_base: the tier's header version applies below its
 // first boundary (the delta's header is kHole: the base shows through).
 constexpr int kTierLanes = 2 * kArity;
+
+// range_max by the kTierLanes lanes of one read (all call with the same lo / hi): at each level of
+// the 64-ary hierarchy the partial blocks at both ends (< 2 kFan entries, or the whole rest at the
+// last level) are read kTierLanes entries per coalesced access, 8 accesses per lane in flight, and
+// max-reduced across the lanes; stops after a level once above `snap`.  A wide read (C4's
+// Tuple.range() over a user's ~50 boundaries) costs one round of loads instead of a dependent scan
+// by one lane.
+__device__ __forceinline__ int64_t group_range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
+    const int sl = threadIdx.x & (kTierLanes - 1);
+    int64_t best = LLONG_MIN;
+    for (int L = 0; L < kMaxLevels; L++) {
+        const int64_t* a = m.lvl[L];
+        const bool last = hi - lo <= 2 * kFan || L == kMaxLevels - 1;
+        const int64_t lo2 = last ? 0 : (lo + kFan - 1) / kFan, hi2 = last ? 0 : hi / kFan;
+        const int64_t le = last ? hi : lo2 * kFan;  // left part [lo, le)
+        const int64_t rs = last ? hi : hi2 * kFan;  // right part [rs, hi)
+        const int64_t nl = le - lo, cnt = nl + (hi - rs);
+        for (int64_t base = 0; base < cnt; base += 8 * kTierLanes) {
+            int64_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int64_t k = base + u * kTierLanes + sl;
+                v[u] = k < cnt ? a[k < nl ? lo + k : rs + (k - nl)] : LLONG_MIN;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) best = v[u] > best ? v[u] : best;
+        }
+#pragma unroll
+        for (int o = 1; o < kTierLanes; o <<= 1) {
+            const int64_t y = __shfl_xor(best, o, 64);
+            best = y > best ? y : best;
+        }
+        if (last || best > snap) return best;
+        lo = lo2;
+        hi = hi2;
+    }
+    return best;
+}
+
+template <bool LONG = false>
 __device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& tier, bool is_base, const uint8_t* htail,
-                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot) {
+                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot, int lead_rmax,
+                                                const int32_t* rbpos, const uint32_t* pmeta) {
     const int lane = threadIdx.x & 63;
-    const int r = (int)(slot / kTierLanes);
+    const int k = (int)(slot / kTierLanes);
     const int grp = (lane / kArity) & 1;
     const int lead = lane & ~(kTierLanes - 1);
-    const bool live = r < b.R;
-    const int rr = live ? r : 0;
+    const bool live = k < b.R;
+    // rbpos: the batch is sorted (stage A done): lane group k takes the read with the k-th smallest
+    // begin key, so neighbouring lookups share tree nodes, cache lines and pages
+    const int rr = !live ? 0 : (rbpos ? (int)item_range(pmeta[rbpos[k]]) : k);
+    const int r = rr;
     const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
     const int64_t n = *tier.n;
     const int64_t snap = b.snap[b.rowner[rr]];
+    const bool active = live && (is_base || n > 0);  // uniform over the read's lanes
     int64_t lb = 0;
     bool eq = false;
-    if (live && !(grp && degenerate) && (is_base || n > 0))
-        lb = group_lower_bound(tier.h, tier.m, n, grp ? ke : kb, htail, b.tail, eq);
-    const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // group 0 takes the end key's position
-    if (live && lane == lead && (is_base || n > 0) &&
-        tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
+    if (active && !(grp && degenerate))
+        lb = group_lower_bound<LONG>(tier.h, tier.m, n, grp ? ke : kb, htail, b.tail, eq);
+    // every lane of the read: the begin key's position (group 0) and the end key's (group 1)
+    const int64_t lbb = __shfl(lb, lead, 64);
+    const int eqb = __shfl((int)eq, lead, 64);
+    const int64_t j = __shfl(lb, lead + kArity, 64);
+    bool conf = false;
+    if (lead_rmax) {  // FDBCS_GROUP_RMAX=0 (A/B): the range max by the read's first lane alone
+        if (active && lane == lead && tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
+            rconf[r] = 1;
+            hist_conf[b.rowner[r]] = 1;
+        }
+        return;
+    }
+    if (active) {  // tier_conflict with the range max shared by the read's lanes
+        const int64_t hdr = is_base ? tier.hdr : kHole;
+        if (degenerate) {
+            conf = (lbb > 0 ? tier.h.ver[lbb - 1] : hdr) > snap;
+        } else {
+            const int64_t ub = lbb + (eqb ? 1 : 0);
+            // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
+            conf = (ub == 0 && hdr > snap) || group_range_max(tier.m, ub > 0 ? ub - 1 : 0, j, snap) > snap;
+        }
+    }
+    if (active && lane == lead && conf) {
         rconf[r] = 1;
         hist_conf[b.rowner[r]] = 1;
     }
@@ -1127,21 +1270,23 @@ struct CheckReads {
 
 // Split check: base tier (stage A, own stream) or delta tier (stage B); two instantiations so
 // profiles tell the launches apart.
-template <bool BASE>
+// LONG: the batch has keys over 16 bytes (long-key probes, group_lower_bound<true>).
+template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const uint8_t* htail, uint8_t* hist_conf,
-                                                       uint8_t* rconf) {
+                                                       uint8_t* rconf, int lead_rmax, const int32_t* rbpos,
+                                                       const uint32_t* pmeta) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    check_read_tier(b, t, BASE, htail, hist_conf, rconf, slot);
+    check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax, rbpos, pmeta);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail) {
+                       const uint8_t* htail, bool long_keys, bool lead_rmax, bool sorted_reads) {
     if (b.R == 0) return;
     const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
-    if (is_base)
-        fdb_launch(k_check_tier<true>, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf);
-    else
-        fdb_launch(k_check_tier<false>, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf);
+    auto k = is_base ? (long_keys ? k_check_tier<true, true> : k_check_tier<true, false>)
+                     : (long_keys ? k_check_tier<false, true> : k_check_tier<false, false>);
+    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, lead_rmax ? 1 : 0,
+               sorted_reads ? (const int32_t*)w.rbpos : nullptr, sorted_reads ? (const uint32_t*)w.pmeta : nullptr);
 }
 
 __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c) {
@@ -2286,6 +2431,7 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
     return b.keys[2 * g + end];
 }
 
+template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, MaxLevels hm,
                                                        const uint8_t* htail, const Scalars* sc, const int64_t* n_in,
                                                        int64_t* lvl3, int64_t lvl3_n, int64_t lvl1_n) {
@@ -2306,7 +2452,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist 
     if (live) {
         kb = seg_key(b, w, w.seg_b[s], 0);
         ke = seg_key(b, w, w.seg_e[s], 1);
-        pos = group_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        pos = group_lower_bound<LONG>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
     }
     const int lane = threadIdx.x & 63;
     const int64_t hi = __shfl(pos, (lane + kArity) & 63, 64);
@@ -2583,11 +2729,11 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe) {
+                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe, bool long_keys) {
     const int Wn = b.W > 0 ? b.W : 1;
     // fused epilogue: levels 1-2 of the new delta are built by atomicMax in the copy (reset here)
     const int64_t lvl1_n = fe ? (fe->out_ub + kFan - 1) / kFan + 1 : 0;
-    fdb_launch(k_seg_search, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
+    fdb_launch(long_keys ? k_seg_search<true> : k_seg_search<false>, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
                htail, sc, &sc->nd, srcm.lvl[3], lvl3_n, lvl1_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,

@@ -169,6 +169,46 @@ def test_long_shared_prefix_runs(engine, oracle_mod):
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
+@pytest.mark.parametrize("plen", [30, 60, 104, 150])
+def test_very_long_shared_prefixes(engine, oracle_mod, plen):
+    """Keys sharing prefixes of 30-150 bytes, so that tail comparisons end inside the long-key
+    probe's first word round (48 bytes), its second (96), and past the query words it holds in
+    registers (the rest compared from memory); history and batch keys of every length around them."""
+    rng = np.random.default_rng(plen)
+    prefixes = [bytes([0x15, 0x2a + i]) + b"x" * (plen - 2) for i in range(2)]
+
+    def key():
+        pre = prefixes[int(rng.integers(0, len(prefixes)))]
+        cut = int(rng.integers(plen - 20, plen + 1))  # some keys end inside the shared prefix
+        return pre[:cut] + bytes(rng.integers(0, 3, size=int(rng.integers(0, 6))).astype(np.uint8))
+
+    hist = sorted({key() for _ in range(6000)})
+    kb = np.frombuffer(b"".join(hist), np.uint8)
+    ko = np.zeros(len(hist) + 1, np.int64)
+    np.cumsum([len(k) for k in hist], out=ko[1:])
+    vers = rng.integers(0, 1000, size=len(hist)).astype(np.int64)
+    e = EngineDriver(engine, gc_interval=0, delta_limit=1500)
+    o = oracle_mod.SkipListBaseline()
+    e.load_history(kb, ko, vers)
+    o.load_history(kb, ko, vers)
+    now = 1000
+    for i in range(6):
+        now += 10
+        txns = []
+        for _ in range(300):
+            def rr():
+                a, b = key(), key()
+                return KeyRange(min(a, b), max(a, b))
+
+            txns.append(CommitTransaction([rr() for _ in range(int(rng.integers(1, 4)))],
+                                          [rr() for _ in range(int(rng.integers(0, 3)))],
+                                          now - int(rng.integers(0, 600)), False))
+        pb = PackedBatch.from_transactions(txns)
+        ve, _ = e.detect(pb, now, 0)
+        vo, _ = o.detect(pb, now, 0)
+        assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
+
+
 def test_c1_skiplisttest(engine, oracle_mod):
     seq = list(W.c1_batches(25, seed=7))
     e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
@@ -440,7 +480,9 @@ def test_empty_batches(engine, oracle_mod):
         now += 4
 
 
-@pytest.mark.parametrize("knobs", [{"FDBCS_FUSE_EPILOGUE": "1"}, {"FDBCS_SPLIT_CHECK": "0"}, {"FDBCS_SORT_WIN": "0"}])
+@pytest.mark.parametrize("knobs", [{"FDBCS_FUSE_EPILOGUE": "1"}, {"FDBCS_SPLIT_CHECK": "0"}, {"FDBCS_SORT_WIN": "0"},
+                                   {"FDBCS_LONG_PROBE": "0"}, {"FDBCS_GROUP_RMAX": "0"},
+                                   {"FDBCS_SORTED_READS": "1"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the epilogue
     fused into the merge copy, the unsplit read check, and long-key sorting without LDS windows."""
