@@ -14,7 +14,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -198,6 +201,35 @@ struct fdbcs_conflict_set {
     // argument structs, and a node parameter update costs 0.76 us at 640 bytes
     // (tools/graphbench.hip), so updating ~30 nodes costs as much host time as launching them.
     bool use_graph = false;
+    // FDBCS_GRAPH=2: stage graphs.  The launches of each stage (A on its stream, B on the batch-order
+    // stream) go out as one cached hipGraph per stage shape on the stage's own stream, with the
+    // cross-stream event waits and records around it issued directly, so the stages still overlap
+    // across streams as in direct mode while the submitting thread makes ~3 graph launches instead
+    // of ~20 kernel launches per batch.
+    bool stage_graphs = false;
+    struct StageGraph {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        std::vector<hipGraphNode_t> nodes;
+    };
+    std::vector<std::pair<uint64_t, StageGraph>> stage_cache;
+    // FDBCS_SUBMIT_THREAD=1: two submitting threads.  A helper thread issues stage A of batch i
+    // (and its base-tier check) while the calling thread issues stage B of batch i-1, which waited
+    // (as in graph mode) for this call: kernel launches on two streams from two threads take about
+    // half the wall time of one thread's (tools/threadbench.hip: 3.4 -> 1.85 us per launch).  The
+    // check of batch i waits (host side) until stage B of batch i-1 is issued, because it may wait
+    // on that stage's compaction event; stage B of batch i waits for the helper to go idle.
+    bool submit_thread = false;
+    std::thread worker;
+    std::mutex wmu;
+    std::condition_variable wcv;
+    std::atomic<int> wjob{0};           // 0 idle, 1 job queued or running, 2 exit
+    std::atomic<uint32_t> b_issued{0};  // stage-B lists issued (by the calling thread)
+    uint32_t b_recorded = 0;            // stage-B lists recorded
+    std::atomic<int> werr{0};           // first HIP error of the helper
+    LaunchList work_a, work_c;          // the helper's lists
+    hipStream_t work_sa = nullptr;
+    uint32_t work_need_b = 0;           // the check goes out once b_issued >= this
     LaunchList rec_a, rec_b, rec_c, pending_b;
     fdbcs_batch* pending_batch = nullptr;
     struct GraphEntry {
@@ -835,11 +867,147 @@ int launch_graph(fdbcs_conflict_set* cs, LaunchList& A, LaunchList& B) {
     return FDBCS_OK;
 }
 
+// Stage graphs (FDBCS_GRAPH=2): the event waits leading a stage list and the event records
+// trailing it are issued directly on `st`; the kernels and timing events between them run as one
+// cached graph (keyed by their shape, node parameters updated per batch).  A list with a wait or
+// record between its kernels, or fewer than two kernels, is replayed directly.
+int launch_stage(fdbcs_conflict_set* cs, LaunchList& L, hipStream_t st) {
+    auto is_sync = [](const LaunchList::Rec& r) {
+        return r.kind == LaunchList::kSyncWait || r.kind == LaunchList::kSyncRecord;
+    };
+    const size_t n = L.recs.size();
+    size_t i0 = 0, i1 = n;
+    while (i0 < n && is_sync(L.recs[i0])) i0++;
+    while (i1 > i0 && is_sync(L.recs[i1 - 1])) i1--;
+    int kernels = 0;
+    bool mid_sync = false;
+    uint64_t key = 1469598103934665603ull;
+    for (size_t i = i0; i < i1; i++) {
+        const LaunchList::Rec& r = L.recs[i];
+        kernels += r.kind == LaunchList::kKernel ? 1 : 0;
+        mid_sync |= is_sync(r);
+        key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u)) * 1099511628211ull;
+    }
+    if (mid_sync || kernels < 2) {
+        HIPOK(L.replay(st));
+        return FDBCS_OK;
+    }
+    L.finalize();
+    for (size_t i = 0; i < i0; i++) HIPOK(L.issue(L.recs[i], st));
+    fdbcs_conflict_set::StageGraph* sg = nullptr;
+    for (auto& kv : cs->stage_cache)
+        if (kv.first == key) sg = &kv.second;
+    auto params = [&](const LaunchList::Rec& r) {
+        hipKernelNodeParams p{};
+        p.func = const_cast<void*>(r.func);
+        p.gridDim = r.grid;
+        p.blockDim = r.block;
+        p.sharedMemBytes = r.shmem;
+        p.kernelParams = L.argp.data() + r.arg0;
+        return p;
+    };
+    if (!sg) {
+        fdbcs_conflict_set::StageGraph g;
+        HIPOK(hipGraphCreate(&g.graph, 0));
+        hipGraphNode_t prev = nullptr;
+        for (size_t i = i0; i < i1; i++) {
+            const LaunchList::Rec& r = L.recs[i];
+            hipGraphNode_t nd = nullptr;
+            if (r.kind == LaunchList::kKernel) {
+                const hipKernelNodeParams p = params(r);
+                HIPOK(hipGraphAddKernelNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, &p));
+            } else {
+                HIPOK(hipGraphAddEventRecordNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
+            }
+            g.nodes.push_back(nd);
+            prev = nd;
+        }
+        HIPOK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
+        cs->stage_cache.push_back({key, g});
+        sg = &cs->stage_cache.back().second;
+    } else {
+        size_t k = 0;
+        for (size_t i = i0; i < i1; i++) {
+            const LaunchList::Rec& r = L.recs[i];
+            if (r.kind == LaunchList::kKernel) {
+                const hipKernelNodeParams p = params(r);
+                HIPOK(hipGraphExecKernelNodeSetParams(sg->exec, sg->nodes[k++], &p));
+            } else {
+                HIPOK(hipGraphExecEventRecordNodeSetEvent(sg->exec, sg->nodes[k++], r.event));
+            }
+        }
+    }
+    HIPOK(hipGraphLaunch(sg->exec, st));
+    cs->graph_launches++;
+    for (size_t i = i1; i < n; i++) HIPOK(L.issue(L.recs[i], st));
+    return FDBCS_OK;
+}
+
+// ---- two submitting threads (FDBCS_SUBMIT_THREAD=1)
+void worker_main(fdbcs_conflict_set* cs) {
+    (void)hipSetDevice(cs->device);
+    for (;;) {
+        int j = 0;
+        for (int spin = 0; spin < 20000 && (j = cs->wjob.load(std::memory_order_acquire)) == 0; spin++)
+            std::this_thread::yield();
+        if (j == 0) {
+            std::unique_lock<std::mutex> lk(cs->wmu);
+            cs->wcv.wait(lk, [&] { return (j = cs->wjob.load(std::memory_order_acquire)) != 0; });
+        }
+        if (j == 2) return;
+        hipError_t e = cs->work_a.replay(cs->work_sa);
+        if (!cs->work_c.recs.empty()) {
+            while (cs->b_issued.load(std::memory_order_acquire) < cs->work_need_b) std::this_thread::yield();
+            const hipError_t e2 = cs->work_c.replay(cs->cstream);
+            if (e == hipSuccess) e = e2;
+        }
+        if (e != hipSuccess) {
+            int expected = 0;
+            cs->werr.compare_exchange_strong(expected, (int)e);
+        }
+        cs->wjob.store(0, std::memory_order_release);
+    }
+}
+
+// Wait until the helper has issued its job; its first error, if any.
+int worker_wait(fdbcs_conflict_set* cs) {
+    if (!cs->worker.joinable()) return FDBCS_OK;
+    while (cs->wjob.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    return cs->werr.exchange(0) ? FDBCS_E_DEVICE : FDBCS_OK;
+}
+
+void worker_start_job(fdbcs_conflict_set* cs) {
+    if (!cs->worker.joinable()) cs->worker = std::thread(worker_main, cs);
+    {
+        std::lock_guard<std::mutex> lk(cs->wmu);
+        cs->wjob.store(1, std::memory_order_release);
+    }
+    cs->wcv.notify_one();
+}
+
+void worker_stop(fdbcs_conflict_set* cs) {
+    if (!cs->worker.joinable()) return;
+    (void)worker_wait(cs);
+    {
+        std::lock_guard<std::mutex> lk(cs->wmu);
+        cs->wjob.store(2, std::memory_order_release);
+    }
+    cs->wcv.notify_one();
+    cs->worker.join();
+}
+
 int flush_pending(fdbcs_conflict_set* cs) {
+    if (int rc = worker_wait(cs)) return rc;  // stage A / check of the pending batch issued
     if (!cs->pending_batch) return FDBCS_OK;
-    LaunchList none;
     cs->pending_batch = nullptr;
-    int rc = launch_graph(cs, none, cs->pending_b);
+    int rc = FDBCS_OK;
+    if (cs->submit_thread) {
+        if (cs->pending_b.replay(cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
+        cs->b_issued.fetch_add(1, std::memory_order_release);
+    } else {
+        LaunchList none;
+        rc = launch_graph(cs, none, cs->pending_b);
+    }
     cs->pending_b.clear();
     return rc;
 }
@@ -886,7 +1054,11 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_ASTREAMS")) cs->astreams = atoi(v) == 1 ? 1 : 2;
     if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "dma") == 0;
-    if (const char* v = getenv("FDBCS_GRAPH")) cs->use_graph = v[0] != '0';
+    if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
+    if (const char* v = getenv("FDBCS_GRAPH")) {
+        cs->use_graph = v[0] == '1';
+        cs->stage_graphs = v[0] == '2';
+    }
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = v[0] != '0';
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
@@ -931,6 +1103,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (!cs) return;
     (void)hipSetDevice(cs->device);
     (void)flush_pending(cs);
+    worker_stop(cs);
     if (cs->ustream) (void)hipStreamSynchronize(cs->ustream);
     if (cs->cstream) (void)hipStreamSynchronize(cs->cstream);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
@@ -960,6 +1133,11 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
     }
     cs->graphs.clear();
+    for (auto& kv : cs->stage_cache) {
+        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
+    }
+    cs->stage_cache.clear();
     // batches that outlive their set (e.g. garbage-collection order in a binding) keep their own
     // slot and refuse every further call
     for (fdbcs_batch* b : cs->live) b->cs = nullptr;
@@ -1454,6 +1632,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // delta half.  One graph per batch cannot express the wait, so graph mode keeps one check.
     const bool split = cs->split_check && !graph && !cs->serial && timing < 2;
     const bool sorted_reads = split && cs->sorted_reads && sa != s;
+    // two submitting threads: this batch's stage A and check go out from the helper, stage B on the
+    // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it
+    // records cannot be queried here: waits on its events are kept unconditionally.
+    const bool threaded = cs->submit_thread && !graph && !(cs->stage_graphs && timing < 2) && timing < 2 &&
+                          !cs->trace && sa != s;
     cs->stats.host_ms_prepare += host_ms_since(t_begin);
     const auto t_rec = std::chrono::steady_clock::now();
     // ---- record stage A: upload, D.Sort and the candidate edges of D.CheckIntraBatch
@@ -1472,7 +1655,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sa);
     if ((rc = mark(kPhUpload))) return t_record = nullptr, rc;
     const BatchDev& bd = b->bd;
-    const bool long_keys = cs->long_probe && b->max_len > 16;
+    // long-key probes pay off once tails run past a word (a 17-byte end key k\0 of a 16-byte key
+    // ties on the prefix with k only, and the length decides)
+    const bool long_keys = cs->long_probe && b->max_len > 24;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
@@ -1504,7 +1689,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         hipStream_t sc_ = cs->cstream;
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sc_);
         if (ws_busy) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sc_);
-        if (cs->cmp_recorded && hipEventQuery(cs->ev_cmp) != hipSuccess) fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
+        if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
+            fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
         if (sorted_reads) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
         launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, sorted_reads);
@@ -1514,9 +1700,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- record stage B: D.CheckRead against the history the previous batch left, then batch order
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
+    // stage graphs: every wait of stage B leads its list (the delta check then starts after stage A)
+    const bool hoist = cs->stage_graphs && !graph && timing < 2;
+    if (hoist && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
+    if (hoist && split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        if (sorted_reads) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
+        if (sorted_reads && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
         launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax, sorted_reads);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
@@ -1525,8 +1715,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     mark(kPhCheck);
-    if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
-    if (split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
+    if (sa != s && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
+    if (split && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp);
     if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
         launch_conflict_output(s, bd, w, (const int32_t*)sl->pin_inv.dp, b->out_n, b->out_dev);
@@ -1616,10 +1806,36 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (rc) return rc;
         cs->pending_batch = b;
     } else {
-        if (flush_pending(cs)) return FDBCS_E_DEVICE;
-        HIPOK(la.replay(sa));
-        if (split) HIPOK(lc.replay(cs->cstream));
-        HIPOK(lb.replay(s));
+        if (threaded) {
+            // the helper issues this batch's stage A and check while this thread issues the
+            // previous batch's stage B; this batch's stage B waits for the next call (or a flush)
+            if ((rc = worker_wait(cs))) return rc;
+            std::swap(cs->work_a, la);
+            std::swap(cs->work_c, lc);  // empty unless split
+            cs->work_sa = sa;
+            const bool prev = cs->pending_batch != nullptr;
+            cs->work_need_b = cs->b_recorded;  // every stage B recorded so far, batch i-1's included
+            worker_start_job(cs);
+            if (prev) {
+                cs->pending_batch = nullptr;
+                const hipError_t e = cs->pending_b.replay(s);
+                cs->b_issued.fetch_add(1, std::memory_order_release);
+                if (e != hipSuccess) return FDBCS_E_DEVICE;
+            }
+            std::swap(cs->pending_b, lb);
+            cs->b_recorded++;
+            cs->pending_batch = b;
+        } else if (flush_pending(cs)) {
+            return FDBCS_E_DEVICE;
+        } else if (hoist) {
+            if ((rc = launch_stage(cs, la, sa))) return rc;
+            if (split && (rc = launch_stage(cs, lc, cs->cstream))) return rc;
+            if ((rc = launch_stage(cs, lb, s))) return rc;
+        } else {
+            HIPOK(la.replay(sa));
+            if (split) HIPOK(lc.replay(cs->cstream));
+            HIPOK(lb.replay(s));
+        }
         HIPOK(take_launch_error());
     }
     cs->stats.host_ms_submit += host_ms_since(t_sub);

@@ -1908,8 +1908,15 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
             if (w.poff[mid] <= q0) lo = mid; else hi = mid;
         }
         int g = lo;
-        const int q1 = min(P, q0 + kPairsPerThread);
-        for (int q = q0; q < q1; q++) {
+        // the ranges of the thread's pairs first (consecutive pairs mostly share one range), then
+        // each dependent step of the pair filter for all of them at once: four chains of gathers
+        // in flight per thread instead of one after another (C3: 1.85M pairs per batch)
+        int gq[kPairsPerThread], kq[kPairsPerThread];
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; u++) {
+            const int q = q0 + u;
+            gq[u] = -1;
+            if (q >= P) continue;
             if (w.poff[g + 1] <= q) {
                 // next range with pairs: gallop forward (ranges without pairs can run for thousands)
                 int step = 1, lo2 = g + 1, hi2 = g + 2;  // poff[lo2] <= q; find hi2 with poff[hi2] > q
@@ -1924,25 +1931,40 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
                 }
                 g = lo2;
             }
-            const int k = q - w.poff[g];
-            if (g < R) {
-                const int r = g, t = b.rowner[r];
-                const int p = w.wbpos[w.cwb[w.pos[2 * r]] + k];
-                const int wr = (int)item_range(w.pmeta[p]) - R;
-                const int tw = b.wowner[wr];
-                if (tw < t && range_nonempty(w, R + wr)) {
-                    const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
-                    if (slot < w.eoff[r + 1]) w.edges[slot] = tw;
-                }
-            } else {
-                const int wr = g - R, tw = b.wowner[wr];
-                const int p = w.rbpos[w.crb[w.pos[2 * g]] + k];
-                const int r = (int)item_range(w.pmeta[p]);
-                if (tw < b.rowner[r] && range_nonempty(w, r)) {
-                    const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
-                    if (slot < w.eoff[r + 1]) w.edges[slot] = tw;
-                }
-            }
+            gq[u] = g;
+            kq[u] = q - w.poff[g];
+        }
+        // partner endpoint: read g's k-th write-begin inside it, or write g's k-th read-begin
+        int part[kPairsPerThread];
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; u++) {
+            const int gg = gq[u];
+            part[u] = 0;
+            if (gg < 0) continue;
+            part[u] = gg < R ? w.wbpos[w.cwb[w.pos[2 * gg]] + kq[u]] : w.rbpos[w.crb[w.pos[2 * gg]] + kq[u]];
+        }
+        int rd[kPairsPerThread], tw[kPairsPerThread];
+        bool ok[kPairsPerThread];
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; u++) {
+            const int gg = gq[u];
+            ok[u] = false;
+            rd[u] = tw[u] = 0;
+            if (gg < 0) continue;
+            const int other = (int)item_range(w.pmeta[part[u]]);
+            const int r = gg < R ? gg : other;            // the read
+            const int wr = (gg < R ? other : gg) - R;     // the write
+            rd[u] = r;
+            tw[u] = b.wowner[wr];
+            // earlier writer, both ranges non-empty (the pair's own range is: it has pairs)
+            ok[u] = tw[u] < b.rowner[r] && range_nonempty(w, gg < R ? R + wr : r);
+        }
+#pragma unroll
+        for (int u = 0; u < kPairsPerThread; u++) {
+            if (!ok[u]) continue;
+            const int r = rd[u];
+            const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
+            if (slot < w.eoff[r + 1]) w.edges[slot] = tw[u];
         }
     }
 }
@@ -2007,17 +2029,29 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
             if (s0 == kUndecided) {
                 for (int r = r0; r < r1; r++) {
                     const int q0 = w.eoff[r], q1 = q0 + w.ecur[r];
-                    for (int base = q0; base < q1; base += 64) {
-                        const int q = base + lane;
-                        int e = -1;
-                        bool live = false;
-                        if (q < q1) {
-                            e = w.edges[q];
-                            live = (unsigned)e < (unsigned)T && !w.hist_conf[e] && !(b.flags[e] & kFlagTooOld);
+                    // 256 edges per step: the four 64-edge loads, then their writers' flags, are
+                    // issued together (a hot key's reader has thousands of edges)
+                    for (int base = q0; base < q1; base += 4 * 64) {
+                        int e[4];
+                        bool live[4];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const int q = base + 64 * u + lane;
+                            e[u] = q < q1 ? w.edges[q] : -1;
                         }
-                        const uint64_t m = __ballot(live);
-                        if (live) w.tedges[tbase + cnt + __popcll(m & ((1ull << lane) - 1))] = e;
-                        cnt += __popcll(m);
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const bool in = (unsigned)e[u] < (unsigned)T;
+                            const int ee = in ? e[u] : 0;
+                            const uint8_t hc = w.hist_conf[ee], fl = b.flags[ee];
+                            live[u] = in && !hc && !(fl & kFlagTooOld);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const uint64_t m = __ballot(live[u]);
+                            if (live[u]) w.tedges[tbase + cnt + __popcll(m & ((1ull << lane) - 1))] = e[u];
+                            cnt += __popcll(m);
+                        }
                     }
                 }
                 if (cnt == 0) s0 = kCommitted;

@@ -66,25 +66,24 @@ struct LaunchList {
         }
         return h;
     }
+    // One record, now, on `s` (after finalize()).
+    hipError_t issue(const Rec& r, hipStream_t s) {
+        switch (r.kind) {
+            case kKernel:
+                return hipLaunchKernel(r.func, r.grid, r.block, argp.data() + r.arg0, r.shmem, s);
+            case kTimingRecord:
+            case kSyncRecord:
+                return hipEventRecord(r.event, s);
+            case kSyncWait:
+                return hipStreamWaitEvent(s, r.event, 0);
+        }
+        return hipSuccess;
+    }
     // Direct mode: submit in order (waits and records on `s`).
     hipError_t replay(hipStream_t s) {
         finalize();
-        for (const Rec& r : recs) {
-            hipError_t e = hipSuccess;
-            switch (r.kind) {
-                case kKernel:
-                    e = hipLaunchKernel(r.func, r.grid, r.block, argp.data() + r.arg0, r.shmem, s);
-                    break;
-                case kTimingRecord:
-                case kSyncRecord:
-                    e = hipEventRecord(r.event, s);
-                    break;
-                case kSyncWait:
-                    e = hipStreamWaitEvent(s, r.event, 0);
-                    break;
-            }
-            if (e != hipSuccess) return e;
-        }
+        for (const Rec& r : recs)
+            if (hipError_t e = issue(r, s)) return e;
         return hipSuccess;
     }
 };

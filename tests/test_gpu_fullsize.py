@@ -57,9 +57,12 @@ def check_against_restatement(oracle_mod, kb, ko, vers, seq, got, gc="bounded"):
     return sl
 
 
-def test_async_pipeline_full_c2(engine, oracle_mod):
+@pytest.mark.parametrize("submit_thread", ["0", "1"])
+def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
     """C2 at full size (5M-boundary history, 5000 txns x 5R+2W) through the async pipeline for 72
-    batches: crosses several size-triggered compactions and a removeBefore pass."""
+    batches: crosses several size-triggered compactions and a removeBefore pass; with one and with
+    two submitting threads (FDBCS_SUBMIT_THREAD)."""
+    monkeypatch.setenv("FDBCS_SUBMIT_THREAD", submit_thread)
     p = W.C2Params()
     start = 10_000_000
     kb, ko, vers = W.c2_history(p, seed=1, start_version=start)
