@@ -390,6 +390,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(items[0], sizeof(SortItem) * E);
     TAKE(items[1], sizeof(SortItem) * E);
     TAKE(splitters, sizeof(SortItem) * 2048);
+    TAKE(samples, sizeof(SortItem) * 8192);
     TAKE(bucket, 2 * E);
     TAKE(bcount, 4 * 2048);
     TAKE(bcursor, 4 * 2048);

@@ -129,6 +129,7 @@ struct Work {
     int32_t* first_conf;   // [T]
     SortItem* items[2];    // [E] sorted endpoints / bucket-sort scratch
     SortItem* splitters;   // [2047] sample-sort splitters
+    SortItem* samples;     // [8192] the sample items (written by k_sample, read by k_bucket_count)
     uint16_t* bucket;      // [E] bucket of each endpoint
     int32_t* bcount;       // [2048] endpoints per bucket (zeroed per batch)
     int32_t* bcursor;      // [2048] scatter cursors (zeroed per batch)

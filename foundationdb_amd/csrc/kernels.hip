@@ -1226,6 +1226,7 @@ __device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((
 struct SampleRank {
     int S, n_slice;
     int32_t* srank;  // [S] ranks (zeroed by the previous epilogue on this workspace)
+    SortItem* samples;  // [S] the sample items, for k_bucket_count
     unsigned long long* trace;
 };
 
@@ -1241,6 +1242,7 @@ __global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
     const int i = y * blockDim.x + threadIdx.x;
     if (i < S) {
         SortItem mine[1] = {make_item(b, sample_pos(i, E, S))};
+        if (x == 0) c.samples[i] = mine[0];
         int cnt[1] = {0};
         bool tail = false;
         rank_count<1>(sl, cj, mine, cnt, tail);
@@ -1309,16 +1311,28 @@ __device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl
     return lo;
 }
 
-__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32_t* srank, int nb, int S,
-                                                         uint16_t* bucket, int32_t* bcount, const uint8_t* arena) {
+__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32_t* srank, const SortItem* samples,
+                                                         int nb, int S, uint16_t* bucket, int32_t* bcount,
+                                                         const uint8_t* arena) {
     __shared__ SortItem spl[kMaxBuckets - 1];
     __shared__ int hist[kMaxBuckets];
     const int E = 2 * (b.R + b.W);
-    // splitter k-1 is the sample of rank k*S/nb (ranks are distinct: items are totally ordered)
-    for (int q = threadIdx.x; q < S; q += blockDim.x) {
-        const int r = srank[q];
-        const int k = (int)(((int64_t)r * nb + S - 1) / S);
-        if (k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r) spl[k - 1] = make_item(b, sample_pos(q, E, S));
+    // splitter k-1 is the sample of rank k*S/nb (ranks are distinct: items are totally ordered);
+    // the sample items come ready-made from k_sample, four ranks and items in flight per thread
+    // (no dependent key and tail loads per sample)
+    for (int q0 = threadIdx.x; q0 < S; q0 += 4 * blockDim.x) {
+        int r[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u * blockDim.x;
+            r[u] = q < S ? srank[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int q = q0 + u * blockDim.x;
+            const int k = (int)(((int64_t)r[u] * nb + S - 1) / S);
+            if (q < S && k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r[u]) spl[k - 1] = samples[q];
+        }
     }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
     __syncthreads();
@@ -1663,6 +1677,7 @@ void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_t
     c.S = sample_count(E, nb, sample_per);
     c.n_slice = (c.S + kSampleSlice - 1) / kSampleSlice;
     c.srank = w.srank;
+    c.samples = w.samples;
     c.trace = w.trace;
     const int grid = c.n_slice * ((c.S + kBlock - 1) / kBlock);
     fdb_launch(k_sample, dim3(grid), dim3(kBlock), 0, s, b, c);
@@ -1703,7 +1718,8 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
     const int nb = sort_buckets(E, bucket_target);
     const int grid = (E + kBlock - 1) / kBlock;
     const int S = nb > 1 ? sample_count(E, nb, sample_per) : 0;
-    fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
+    fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, w.samples, nb, S, w.bucket, w.bcount,
+               b.tail);
     fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
     fdb_event(LaunchList::kTimingRecord, sort_begin, s);
@@ -1740,7 +1756,8 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int 
         launch_sample(s, b, w, bucket_target, sample_per);
         after(1);
         at(2);
-        fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, nb, S, w.bucket, w.bcount, b.tail);
+        fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, w.samples, nb, S, w.bucket, w.bcount,
+               b.tail);
         after(2);
         at(3);
         fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
