@@ -476,9 +476,8 @@ def main():
                 dom = d
         except Exception:
             pass
-    roof = None
-    if dom is not None:
-        k = kern[dom]
+    def roof_block(name):
+        k = kern[name]
         traffic = None
         # PMC HBM bytes per launch of the same kernel on the same command (FETCH_SIZE x2 gfx950
         # correction + WRITE_SIZE, separate rocprofv3 passes: scripts/gpu_pmc.sh)
@@ -486,10 +485,10 @@ def main():
         if os.path.exists(pmc):
             try:
                 with open(pmc) as f:
-                    traffic = json.load(f).get(f"{dom}_bytes_per_launch")
+                    traffic = json.load(f).get(f"{name}_bytes_per_launch")
             except Exception:
                 traffic = None
-        roof = {
+        return {
             "kernel": k["kernel"],
             "bound": "hbm",
             "achieved": k["achieved_GBps"],
@@ -500,6 +499,11 @@ def main():
             "avg_launch_ms": k["avg_launch_ms"],
             "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"],
         }
+
+    roof = roof_block(dom) if dom is not None else None
+    # north_star's roofline target is on the search / merge kernels: when the dominant kernel is
+    # another one (the LDS-bound bucket sort), the read check's block rides along
+    roof_search = roof_block("check") if dom not in (None, "check") and "check" in kern else None
 
     combine_check = None
     if dist is not None:
@@ -569,6 +573,7 @@ def main():
         "compactions": st["compactions"],
         "kernels": kern,
         "roofline": roof,
+        "roofline_search": roof_search,
     }
     if rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_base

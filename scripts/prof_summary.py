@@ -9,7 +9,7 @@ import json
 import sys
 
 ROOF = {  # bench/roofline.py key -> kernel name fragment
-    "check": "k_check_tier<true>",
+    "check": "k_check_tier<true",
     "sort": "k_bucket_sort",
     "merge": "k_merge_copy<fdbcs::BatchIns",
     "compact": "k_merge_copy<fdbcs::CompactIns",
