@@ -180,6 +180,7 @@ struct fdbcs_conflict_set {
     int check_version = 1;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants)
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
+    bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
     bool sorted_reads = false; // FDBCS_SORTED_READS=1: the split check waits for stage A and takes reads
                                // in sorted begin-key order (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
@@ -403,6 +404,10 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(cwe, 4 * (E + 1));
     TAKE(segflag, E + 1);
     TAKE(wbpos, 4 * W);
+    TAKE(wlead, 4 * (W + 1));
+    TAKE(wtxn, 4 * (W + 1));
+    TAKE(gidx, 4 * (W + 1));
+    TAKE(gminc, 4 * (W + 1));
     TAKE(rbpos, 4 * R);
     TAKE(eoff, 4 * (R + 1));
     TAKE(poff, 4 * (R + W + 1));
@@ -1065,12 +1070,15 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
     if (const char* v = getenv("FDBCS_SORTED_READS")) cs->sorted_reads = v[0] != '0';
+    if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_FUSE_EPILOGUE")) cs->fuse_epilogue = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
+    static std::once_flag attr_once;
+    std::call_once(attr_once, init_kernel_attributes);
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
@@ -1606,6 +1614,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->wpar = (wp + 1) % kNumWork;
     b->wp = wp;
     Work& w = cs->work[wp];
+    // write groups need the group minima in the resolver's LDS beside the status bytes
+    w.groups = cs->write_groups && W > 0 && W <= kMaxGroupWrites && T <= kMaxTxnLds ? 1 : 0;
     // phase events: level 2 records every phase, level 1 only the hot kernels (roofline)
     // level-1 (roofline) events on one batch in timing_every: each event record is a runtime call
     // on the submitting thread, and the per-launch averages need only a sample of the batches

@@ -17,6 +17,7 @@ constexpr int kSortTile = 4096;    // endpoints per LDS sort tile (128 KiB of LD
 constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
 constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)
 constexpr int kGcTile = 4096;      // history elements per GC / merge tile
+constexpr int kMaxGroupWrites = 12288;  // write groups: 8 bytes of resolver LDS per write
 constexpr int kMaxTxnLds = 49152;  // transactions whose status bytes fit the resolver's LDS (> the
                                    // reference's 32768-transaction batch cap, fdbserver/Knobs.cpp:370)
 
@@ -146,6 +147,14 @@ struct Work {
     int32_t* eoff;         // [R+1] first edge slot of each read
     int32_t* poff;         // [R+W+1] first candidate pair of each range
     int32_t* ecur;         // [R] edges of each read (slots taken; zeroed by the epilogue)
+    // write groups (groups != 0): consecutive write-begins (in sorted order) whose writes contain
+    // exactly the same read-begins are one group; a read gets one edge T + j per group j (j = the
+    // group's first write-begin index) instead of one per writer (C3: a hot key's writers)
+    int32_t* wlead;        // [W] per write-begin index: 2 first of a group, 1 member, 0 none
+    int32_t* wtxn;         // [W] transaction of the write with that write-begin
+    int32_t* gidx;         // [W] group of each member (k_resolve)
+    int32_t* gminc;        // [W] per group: least committed member transaction (k_resolve)
+    int32_t groups = 0;    // set per batch
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction
@@ -263,6 +272,8 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
 // the empty arena tdst (reclaiming the bytes of removed and overwritten boundaries).
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
                Scalars* sc, int64_t oldest, int64_t header_version, int64_t grid_hint_n);
+// Kernel attributes set once per process (the resolver's dynamic LDS above 64 KiB).
+void init_kernel_attributes();
 // Byte copy (device -> host-mapped result buffer), as a kernel.
 void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n);
 // Multi-resolver conflict bytes out[g] = 2 - verdict of batch transaction inv[g] (0 if inv[g] < 0).

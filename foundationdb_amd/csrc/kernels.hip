@@ -1878,11 +1878,39 @@ __device__ __forceinline__ bool range_nonempty(const Work& w, int g) { return w.
 
 // Per range g: slots (reads only) and pairs; exclusive prefixes give each read's first slot and
 // each range's first pair.
+// The read-begins a write contains, as an interval of read-begin indices (empty: none).
+__device__ __forceinline__ uint2 write_rb_interval(const Work& w, int g) {
+    const int b = w.pos[2 * g], e = w.pos[2 * g + 1];
+    if (b >= e) return make_uint2(0, 0);
+    const int lo = w.crb[b], hi = w.crb[e];
+    return hi > lo ? make_uint2((uint32_t)lo, (uint32_t)hi) : make_uint2(0, 0);
+}
+
 struct EdgePairScan {
     Work w;
     int32_t R, G;
+    const int32_t* wowner;
     __device__ void counts(int64_t g, uint32_t& slots, uint32_t& pairs, uint32_t& a) const {
         slots = pairs = a = 0;
+        if (g >= R && w.groups) {
+            // write-begin index j of this write; it leads a group unless the write before it in
+            // sorted order contains the same read-begins (then that group's edges cover it)
+            const int j = w.cwb[w.pos[2 * g]];
+            const uint2 iv = write_rb_interval(w, (int)g);
+            int lead = 0;
+            if (iv.y > iv.x) {
+                lead = 2;
+                if (j > 0) {
+                    const int gp = (int)item_range(w.pmeta[w.wbpos[j - 1]]);
+                    const uint2 ip = write_rb_interval(w, gp);
+                    if (ip.x == iv.x && ip.y == iv.y) lead = 1;
+                }
+            }
+            w.wlead[j] = lead;
+            w.wtxn[j] = wowner[g - R];
+            if (lead == 2) pairs = iv.y - iv.x;
+            return;
+        }
         if (!range_nonempty(w, (int)g)) return;
         const int b = w.pos[2 * g], e = w.pos[2 * g + 1];
         if (g < R) {
@@ -1972,6 +2000,13 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
             const int r = gg < R ? gg : other;            // the read
             const int wr = (gg < R ? other : gg) - R;     // the write
             rd[u] = r;
+            if (gg >= R && w.groups) {
+                // write group led by this write: one edge T + j for the group (its members'
+                // transactions are compared with the reader's in the resolution rounds)
+                tw[u] = b.T + w.cwb[w.pos[2 * gg]];
+                ok[u] = range_nonempty(w, r);
+                continue;
+            }
             tw[u] = b.wowner[wr];
             // earlier writer, both ranges non-empty (the pair's own range is: it has pairs)
             ok[u] = tw[u] < b.rowner[r] && range_nonempty(w, gg < R ? R + wr : r);
@@ -1988,7 +2023,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
 
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    launch_scan<2>(s, EdgePairScan{w, b.R, G}, nullptr, G, w.scan[kScanEdges]);
+    launch_scan<2>(s, EdgePairScan{w, b.R, G, b.wowner}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
         const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
         fdb_launch(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
@@ -2061,7 +2096,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
                             const bool in = (unsigned)e[u] < (unsigned)T;
                             const int ee = in ? e[u] : 0;
                             const uint8_t hc = w.hist_conf[ee], fl = b.flags[ee];
-                            live[u] = in && !hc && !(fl & kFlagTooOld);
+                            live[u] = in ? (!hc && !(fl & kFlagTooOld)) : e[u] >= T;  // group edges stay
                         }
 #pragma unroll
                         for (int u = 0; u < 4; u++) {
@@ -2117,12 +2152,67 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
     }
     __syncthreads();
     int rounds = 0;
+    // write groups: per group j (its first write-begin index), the least transaction among its
+    // members not aborted (minLive) and among its committed members (minComm), recomputed from the
+    // statuses at the start of every round, in LDS after the status bytes
+    const int NW = w.groups ? b.W : 0;
+    int32_t* minLive = (int32_t*)(st + ((T + 15) & ~15));
+    int32_t* minComm = minLive + NW;
+    auto group_minima = [&](const volatile uint8_t* sv) {
+        for (int j = threadIdx.x; j < NW; j += blockDim.x) minLive[j] = minComm[j] = INT_MAX;
+        __syncthreads();
+        for (int x = threadIdx.x; x < NW; x += blockDim.x) {
+            if (!w.wlead[x]) continue;
+            const int tw = w.wtxn[x], j = w.gidx[x];
+            const uint8_t sx = sv[tw];
+            if (sx != kAborted) atomicMin(&minLive[j], tw);
+            if (sx == kCommitted) atomicMin(&minComm[j], tw);
+        }
+        __syncthreads();
+    };
+    if (NW && !sc->edge_overflow) {
+        // group of each member: its nearest group start at or before it (block max-scan over
+        // contiguous chunks of write-begin indices)
+        __shared__ int s_wmax[kWG / 64];
+        const int per = (NW + blockDim.x - 1) / blockDim.x, x0 = threadIdx.x * per;
+        int last = -1;
+        for (int x = x0; x < x0 + per && x < NW; x++)
+            if (w.wlead[x] == 2) last = x;
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        int v = last;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(v, o, 64);
+            if (lane >= o) v = y > v ? y : v;
+        }
+        if (lane == 63) s_wmax[wid] = v;
+        __syncthreads();
+        int carry = -1;
+        for (int q = 0; q < wid; q++) carry = s_wmax[q] > carry ? s_wmax[q] : carry;
+        const int prev_in_wave = __shfl_up(v, 1, 64);
+        if (lane > 0) carry = prev_in_wave > carry ? prev_in_wave : carry;
+        for (int x = x0; x < x0 + per && x < NW; x++) {
+            if (w.wlead[x] == 2) carry = x;
+            w.gidx[x] = carry;
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+    // the group rule for reader t and group edge e = T + j: a committed member before t aborts t,
+    // an undecided one before t makes it wait, otherwise the group is no obstacle
+    auto group_status = [&](int e, int t) -> uint8_t {
+        const int j = e - T;
+        if (minComm[j] < t) return kCommitted;
+        if (minLive[j] < t) return kUndecided;
+        return kAborted;
+    };
     if (!sc->edge_overflow) {
         for (int t = threadIdx.x; t < T; t += blockDim.x)
             w.eptr[t] = use_pre ? w.pre_ep[t] : (b.roff[t] < b.roff[t + 1] ? w.eoff[b.roff[t]] : 0);
         volatile uint8_t* vst = st;
         for (;;) {
             if (threadIdx.x == 0) s_more = 0;
+            if (NW) group_minima(vst);
             __syncthreads();
             int more = 0;
             for (int t = threadIdx.x; t < T; t += blockDim.x) {
@@ -2135,7 +2225,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
                     const int end = w.pre_end[t];
                     while (p < end) {
                         const int e = w.tedges[p];
-                        const uint8_t sp = vst[e];
+                        const uint8_t sp = e >= T ? group_status(e, t) : vst[e];
                         if (sp == kAborted) {
                             p++;
                             continue;
@@ -2165,7 +2255,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
                         int u = 0;
                         uint8_t sp = kAborted;
                         for (; u < 4 && p + u < s1; u++) {
-                            sp = (unsigned)e[u] < (unsigned)T ? vst[e[u]] : kAborted;
+                            sp = (unsigned)e[u] < (unsigned)T ? vst[e[u]] : (e[u] >= T && NW ? group_status(e[u], t) : kAborted);
                             if (sp != kAborted) break;
                         }
                         p += u;
@@ -2239,6 +2329,10 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         rounds = -1;
     }
     __syncthreads();
+    if (NW && !sc->edge_overflow) {  // final committed minima per group (conflicting-key reports)
+        group_minima(st);
+        for (int j = threadIdx.x; j < NW; j += blockDim.x) w.gminc[j] = minComm[j];
+    }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         w.status[t] = st[t];
         vout[t] = verdict_byte(b, t, st[t]);
@@ -2256,18 +2350,26 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
     if (!(b.flags[t] & kFlagReport) || w.hist_conf[t] || w.status[t] != kAborted) return;
     for (int p = w.eoff[r]; p < w.eoff[r] + w.ecur[r]; p++) {
         const int e = w.edges[p];
-        if ((unsigned)e < (unsigned)b.T && w.status[e] == kCommitted) {
+        if (((unsigned)e < (unsigned)b.T && w.status[e] == kCommitted) ||
+            (w.groups && e >= b.T && w.gminc[e - b.T] < t)) {
             atomicMin(&w.first_conf[t], r - b.roff[t]);
             return;
         }
     }
 }
 
+void init_kernel_attributes() {
+    // status bytes (<= kMaxTxnLds) + write-group minima (<= 8 kMaxGroupWrites) + static LDS
+    (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ((kMaxTxnLds + 15) / 16 * 16) + 8 * kMaxGroupWrites);
+}
+
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out) {
     if (b.T == 0) return;
     // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
     const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
-    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (size_t)b.T, s, b, w, verdict_out);
+    const size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
+    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (uint32_t)lds, s, b, w, verdict_out);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
