@@ -406,7 +406,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(wbpos, 4 * W);
     TAKE(wlead, 4 * (W + 1));
     TAKE(wtxn, 4 * (W + 1));
-    TAKE(gidx, 4 * (W + 1));
+    TAKE(members, 8 * (W + 1));
     TAKE(gminc, 4 * (W + 1));
     TAKE(rbpos, 4 * R);
     TAKE(eoff, 4 * (R + 1));

@@ -152,7 +152,7 @@ struct Work {
     // group's first write-begin index) instead of one per writer (C3: a hot key's writers)
     int32_t* wlead;        // [W] per write-begin index: 2 first of a group, 1 member, 0 none
     int32_t* wtxn;         // [W] transaction of the write with that write-begin
-    int32_t* gidx;         // [W] group of each member (k_resolve)
+    int2* members;         // [W] (transaction, group) of each group member, compacted (k_resolve)
     int32_t* gminc;        // [W] per group: least committed member transaction (k_resolve)
     int32_t groups = 0;    // set per batch
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge

@@ -2158,26 +2158,49 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
     const int NW = w.groups ? b.W : 0;
     int32_t* minLive = (int32_t*)(st + ((T + 15) & ~15));
     int32_t* minComm = minLive + NW;
+    __shared__ int s_nmem;
+    __shared__ int s_wred[kWG / 64];
     auto group_minima = [&](const volatile uint8_t* sv) {
         for (int j = threadIdx.x; j < NW; j += blockDim.x) minLive[j] = minComm[j] = INT_MAX;
         __syncthreads();
-        for (int x = threadIdx.x; x < NW; x += blockDim.x) {
-            if (!w.wlead[x]) continue;
-            const int tw = w.wtxn[x], j = w.gidx[x];
-            const uint8_t sx = sv[tw];
-            if (sx != kAborted) atomicMin(&minLive[j], tw);
-            if (sx == kCommitted) atomicMin(&minComm[j], tw);
+        const int M = s_nmem;
+        for (int m0 = threadIdx.x; m0 < M; m0 += 4 * blockDim.x) {
+            int2 e[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int m = m0 + u * blockDim.x;
+                e[u] = m < M ? w.members[m] : make_int2(-1, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (e[u].x < 0) continue;
+                const uint8_t sx = sv[e[u].x];
+                if (sx != kAborted) atomicMin(&minLive[e[u].y], e[u].x);
+                if (sx == kCommitted) atomicMin(&minComm[e[u].y], e[u].x);
+            }
         }
         __syncthreads();
     };
     if (NW && !sc->edge_overflow) {
-        // group of each member: its nearest group start at or before it (block max-scan over
-        // contiguous chunks of write-begin indices)
-        __shared__ int s_wmax[kWG / 64];
+        // compact the group members once: (transaction, group = nearest group start at or before
+        // it).  Each thread takes a contiguous run of <= 12 write-begin indices (W <=
+        // kMaxGroupWrites), all its loads in flight; a block max-scan carries the group start in,
+        // a block sum places the thread's members.
+        constexpr int kPer = (kMaxGroupWrites + kWG - 1) / kWG;
         const int per = (NW + blockDim.x - 1) / blockDim.x, x0 = threadIdx.x * per;
-        int last = -1;
-        for (int x = x0; x < x0 + per && x < NW; x++)
-            if (w.wlead[x] == 2) last = x;
+        int lw[kPer], tx[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const bool in = k < per && x0 + k < NW;
+            lw[k] = in ? w.wlead[x0 + k] : 0;
+            tx[k] = in ? w.wtxn[x0 + k] : 0;
+        }
+        int last = -1, nm = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if (lw[k] == 2) last = x0 + k;
+            nm += lw[k] != 0 ? 1 : 0;
+        }
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         int v = last;
 #pragma unroll
@@ -2185,16 +2208,21 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
             const int y = __shfl_up(v, o, 64);
             if (lane >= o) v = y > v ? y : v;
         }
-        if (lane == 63) s_wmax[wid] = v;
+        if (lane == 63) s_wred[wid] = v;
         __syncthreads();
         int carry = -1;
-        for (int q = 0; q < wid; q++) carry = s_wmax[q] > carry ? s_wmax[q] : carry;
+        for (int q = 0; q < wid; q++) carry = s_wred[q] > carry ? s_wred[q] : carry;
         const int prev_in_wave = __shfl_up(v, 1, 64);
         if (lane > 0) carry = prev_in_wave > carry ? prev_in_wave : carry;
-        for (int x = x0; x < x0 + per && x < NW; x++) {
-            if (w.wlead[x] == 2) carry = x;
-            w.gidx[x] = carry;
+        __syncthreads();
+        int total;
+        int off = block_excl_sum<int>(nm, s_wred, &total);
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if (lw[k] == 2) carry = x0 + k;
+            if (lw[k] != 0) w.members[off++] = make_int2(tx[k], carry);
         }
+        if (threadIdx.x == 0) s_nmem = total;
         __threadfence_block();
         __syncthreads();
     }
