@@ -36,6 +36,9 @@ using namespace fdbcs;
         }                                                                                             \
     } while (0)
 
+// Base-tier size from which the read check splits by default (FDBCS_SPLIT_CHECK=2).
+constexpr int64_t kSplitCheckMinBase = 16 << 20;
+
 namespace {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -119,7 +122,12 @@ struct fdbcs_conflict_set {
     hipEvent_t ev_c[kNumWork] = {}; // base-tier check of the batch using workspace k is done
     hipEvent_t ev_cmp = nullptr;    // stage B of the last batch that rewrote the base (compaction / GC)
     bool cmp_recorded = false;
-    bool split_check = true;        // FDBCS_SPLIT_CHECK=0: one read check over both tiers in stage B
+    // FDBCS_SPLIT_CHECK: 0 = one read check over both tiers in stage B, 1 = the base-tier half on
+    // its own stream beside stage A, 2 (default) = split only over a large base tier (>= 16M
+    // boundaries): there the base check is long (C4: ~150 us) and must leave the batch-order
+    // chain; over a 5M base (C2) the single launch measured faster (device-resident 34.0M vs
+    // 32.1M txns/s: one launch and two cross-stream events fewer, no third stream competing)
+    int split_check = 2;
     hipStream_t ustream = nullptr;  // batch uploads (k_upload over PCIe), so batch i+1's upload overlaps
                                     // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
@@ -1066,7 +1074,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
         cs->stage_graphs = v[0] == '2';
     }
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
-    if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = v[0] != '0';
+    if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
     if (const char* v = getenv("FDBCS_SORTED_READS")) cs->sorted_reads = v[0] != '0';
@@ -1641,7 +1649,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // Split read check: the base tier changes only at compactions, so unless one is still pending
     // on the stream its half of D.CheckRead runs beside stage A on its own stream; stage B keeps the
     // delta half.  One graph per batch cannot express the wait, so graph mode keeps one check.
-    const bool split = cs->split_check && !graph && !cs->serial && timing < 2;
+    const bool split = (cs->split_check == 1 || (cs->split_check == 2 && cs->n_ub >= kSplitCheckMinBase)) && !graph &&
+                       !cs->serial && timing < 2;
     const bool sorted_reads = split && cs->sorted_reads && sa != s;
     // two submitting threads: this batch's stage A and check go out from the helper, stage B on the
     // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it

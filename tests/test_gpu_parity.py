@@ -131,10 +131,12 @@ def test_shared_long_prefixes(engine, oracle_mod):
     run_pair(engine, oracle_mod, seq, gc_interval=0, delta_limit=30)
 
 
-def test_long_shared_prefix_runs(engine, oracle_mod):
+@pytest.mark.parametrize("split", ["1", "2"])
+def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split):
     """Thousands of history boundaries behind one 16-byte prefix (a few huge tuple subspaces): the
     search must order them by their tail bytes over a run far longer than one 64-boundary block
     (the cooperative probe rounds start at a stride of 512 or more)."""
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(123)
     prefixes = [b"\x15\x2a\x02huge-subspace-%d\x00" % i for i in range(3)]
 
@@ -169,11 +171,14 @@ def test_long_shared_prefix_runs(engine, oracle_mod):
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
+@pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("plen", [30, 60, 104, 150])
-def test_very_long_shared_prefixes(engine, oracle_mod, plen):
+def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split):
     """Keys sharing prefixes of 30-150 bytes, so that tail comparisons end inside the long-key
     probe's first word round (48 bytes), its second (96), and past the query words it holds in
-    registers (the rest compared from memory); history and batch keys of every length around them."""
+    registers (the rest compared from memory); history and batch keys of every length around them.
+    split "1": the split read check (long-key probes in both check launches); "2": the default."""
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(plen)
     prefixes = [bytes([0x15, 0x2a + i]) + b"x" * (plen - 2) for i in range(2)]
 
@@ -480,10 +485,13 @@ def test_empty_batches(engine, oracle_mod):
         now += 4
 
 
-@pytest.mark.parametrize("knobs", [{"FDBCS_FUSE_EPILOGUE": "1"}, {"FDBCS_SPLIT_CHECK": "0"}, {"FDBCS_SORT_WIN": "0"},
-                                   {"FDBCS_LONG_PROBE": "0"}, {"FDBCS_GROUP_RMAX": "0"},
-                                   {"FDBCS_SORTED_READS": "1"}, {"FDBCS_GRAPH": "2"},
-                                   {"FDBCS_SUBMIT_THREAD": "1"}, {"FDBCS_WRITE_GROUPS": "0"}])
+@pytest.mark.parametrize("knobs", [{"FDBCS_FUSE_EPILOGUE": "1"}, {"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
+                                   {"FDBCS_SORT_WIN": "0"},
+                                   {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
+                                   {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"},
+                                   {"FDBCS_SORTED_READS": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
+                                   {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
+                                   {"FDBCS_WRITE_GROUPS": "0"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the epilogue
     fused into the merge copy, the unsplit read check, and long-key sorting without LDS windows."""
