@@ -2079,17 +2079,39 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
             const int tbase = r0 < r1 ? w.eoff[r0] : 0;
             int cnt = 0;
             if (s0 == kUndecided) {
-                for (int r = r0; r < r1; r++) {
-                    const int q0 = w.eoff[r], q1 = q0 + w.ecur[r];
-                    // 256 edges per step: the four 64-edge loads, then their writers' flags, are
-                    // issued together (a hot key's reader has thousands of edges)
-                    for (int base = q0; base < q1; base += 4 * 64) {
+                // t's reads 64 at a time, their edge runs flattened into one index space so the
+                // loads of every read's edges go out together (per-read chains no longer add up);
+                // 256 edges per step: four 64-edge loads, then their writers' flags
+                for (int rb = r0; rb < r1; rb += 64) {
+                    const int nr = min(64, r1 - rb);
+                    const int myq = lane < nr ? w.eoff[rb + lane] : 0;
+                    const int myn = lane < nr ? w.ecur[rb + lane] : 0;
+                    int incl = myn;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int y = __shfl_up(incl, o, 64);
+                        if (lane >= o) incl += y;
+                    }
+                    const int excl = incl - myn;  // lanes >= nr hold the total
+                    const int total = __shfl(incl, 63, 64);
+                    for (int f0 = 0; f0 < total; f0 += 4 * 64) {
                         int e[4];
                         bool live[4];
 #pragma unroll
                         for (int u = 0; u < 4; u++) {
-                            const int q = base + 64 * u + lane;
-                            e[u] = q < q1 ? w.edges[q] : -1;
+                            const int f = f0 + 64 * u + lane;
+                            const int fc = f < total ? f : total - 1;
+                            // the read holding flattened edge fc: the last lane with excl <= fc
+                            // (binary lifting, every lane shuffling in step)
+                            int lo = 0;
+#pragma unroll
+                            for (int step = 32; step > 0; step >>= 1) {
+                                const int cand = lo + step;
+                                const int ex = __shfl(excl, cand < 64 ? cand : 63, 64);
+                                if (cand < 64 && ex <= fc) lo = cand;
+                            }
+                            const int q = __shfl(myq, lo, 64) + fc - __shfl(excl, lo, 64);
+                            e[u] = f < total ? w.edges[q] : -1;
                         }
 #pragma unroll
                         for (int u = 0; u < 4; u++) {
