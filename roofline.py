@@ -69,7 +69,7 @@ def kernels_from_stats(st: dict, lds_levels: int = 0) -> dict:
         avg_reads = st["check_reads"] / n
         avg_hist = st["check_history"] / n
         avg_txn = st["transactions"] / max(1, st["batches"])
-        out["check"] = kernel_entry("k_check_tier<true> (D.CheckRead, base tier: search + range max)",
+        out["check"] = kernel_entry("D.CheckRead: k_check_reads (both tiers) or k_check_tier<base> (split), search + range max",
                                     st["ms_check_kernel"], n,
                                     n * check_bytes(avg_reads, avg_txn, avg_hist, lds_levels))
         out["check"]["model"] = {"reads": avg_reads, "history": avg_hist, "lds_levels": lds_levels,

@@ -13,8 +13,10 @@ import json
 import os
 import sys
 
-KERNELS = {"check": "k_check_tier<true>", "sort": "k_bucket_sort", "merge": "k_merge_copy<fdbcs::BatchIns",
-           "compact": "k_merge_copy<fdbcs::CompactIns"}
+# the read check: k_check_reads over both tiers (default over a base tier < 16M boundaries) or the
+# split check's base-tier launch k_check_tier<true, ...>
+KERNELS = {"check": ("k_check_tier<true", "k_check_reads"), "sort": ("k_bucket_sort",),
+           "merge": ("k_merge_copy<fdbcs::BatchIns",), "compact": ("k_merge_copy<fdbcs::CompactIns",)}
 
 root = sys.argv[1]
 out = {}
@@ -26,7 +28,7 @@ for key, tag in KERNELS.items():
         for f in files:
             for r in csv.DictReader(open(f)):
                 name = r.get("Kernel_Name", "")
-                if tag in name and r.get("Counter_Name") == c:
+                if any(t in name for t in tag) and r.get("Counter_Name") == c:
                     vals.append(float(r["Counter_Value"]))
         per[c] = sum(vals) / len(vals) if vals else None
         out[f"{key}_{c}_kib_per_launch"] = per[c]

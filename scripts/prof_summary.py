@@ -8,11 +8,12 @@ import csv
 import json
 import sys
 
-ROOF = {  # bench/roofline.py key -> kernel name fragment
-    "check": "k_check_tier<true",
-    "sort": "k_bucket_sort",
-    "merge": "k_merge_copy<fdbcs::BatchIns",
-    "compact": "k_merge_copy<fdbcs::CompactIns",
+ROOF = {  # bench/roofline.py key -> kernel name fragments (the read check: k_check_reads over
+    # both tiers, or the split check's base-tier launch k_check_tier<true, ...>)
+    "check": ("k_check_tier<true", "k_check_reads"),
+    "sort": ("k_bucket_sort",),
+    "merge": ("k_merge_copy<fdbcs::BatchIns",),
+    "compact": ("k_merge_copy<fdbcs::CompactIns",),
 }
 
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -24,9 +25,9 @@ for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
 if "--dominant" in sys.argv:
     out = sys.argv[sys.argv.index("--dominant") + 1]
     totals = {}
-    for k, frag in ROOF.items():
+    for k, frags in ROOF.items():
         for r in rows:
-            if frag in r["Name"]:
+            if any(f in r["Name"] for f in frags):
                 totals[k] = totals.get(k, 0.0) + float(r["TotalDurationNs"])
     top = max(totals, key=totals.get) if totals else None
     all_top = max(rows, key=lambda r: float(r["TotalDurationNs"]))["Name"].split("(")[0] if rows else None
