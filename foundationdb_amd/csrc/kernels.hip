@@ -1237,11 +1237,13 @@ __global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
     const int x = blockIdx.x % c.n_slice, y = blockIdx.x / c.n_slice;
     const int j0 = x * kSampleSlice;
     const int cj = min(kSampleSlice, S - j0);
+    const int i = y * blockDim.x + threadIdx.x;
+    // this thread's sample is loaded before the slice barrier (its loads overlap the slice's)
+    SortItem mine[1];
+    if (i < S) mine[0] = make_item(b, sample_pos(i, E, S));
     for (int t = threadIdx.x; t < cj; t += blockDim.x) sl[t] = make_item(b, sample_pos(j0 + t, E, S));
     __syncthreads();
-    const int i = y * blockDim.x + threadIdx.x;
     if (i < S) {
-        SortItem mine[1] = {make_item(b, sample_pos(i, E, S))};
         if (x == 0) c.samples[i] = mine[0];
         int cnt[1] = {0};
         bool tail = false;
@@ -1317,6 +1319,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32
     __shared__ SortItem spl[kMaxBuckets - 1];
     __shared__ int hist[kMaxBuckets];
     const int E = 2 * (b.R + b.W);
+    // this thread's endpoint first: its key loads overlap the splitter fill below
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    SortItem it{};
+    if (p < E) it = make_item(b, p);
     // splitter k-1 is the sample of rank k*S/nb (ranks are distinct: items are totally ordered);
     // the sample items come ready-made from k_sample, four ranks and items in flight per thread
     // (no dependent key and tail loads per sample)
@@ -1336,9 +1342,8 @@ __global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32
     }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p < E) {
-        const int k = bucket_of(make_item(b, p), spl, nb - 1, arena);
+        const int k = bucket_of(it, spl, nb - 1, arena);
         bucket[p] = (uint16_t)k;
         atomicAdd(&hist[k], 1);
     }
@@ -1383,16 +1388,20 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uin
                                                            int32_t* bcursor, int32_t* boff_out, int nb, SortItem* out) {
     __shared__ int off[kMaxBuckets + 1];
     __shared__ int local[kMaxBuckets];
+    const int E = 2 * (b.R + b.W);
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    // this thread's bucket and endpoint first: their loads overlap the bucket prefix
+    const int kb = p < E ? (int)bucket[p] : -1;
+    SortItem it{};
+    if (p < E) it = make_item(b, p);
     bucket_prefix(bcount, nb, off);
     if (blockIdx.x == 0)
         for (int k = threadIdx.x; k <= nb; k += blockDim.x) boff_out[k] = off[k];
     for (int k = threadIdx.x; k < nb; k += blockDim.x) local[k] = 0;
     __syncthreads();
-    const int E = 2 * (b.R + b.W);
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
     int k = -1, slot = 0;
     if (p < E) {
-        k = bucket[p];
+        k = kb;
         slot = atomicAdd(&local[k], 1);  // order inside a bucket is irrelevant: it is sorted next
     }
     __syncthreads();
@@ -1402,7 +1411,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uin
         local[q] = c ? atomicAdd(&bcursor[q], c) : 0;
     }
     __syncthreads();
-    if (p < E) out[off[k] + local[k] + slot] = make_item(b, p);
+    if (p < E) out[off[k] + local[k] + slot] = it;
 }
 
 // Sentinel-aware order for the bitonic network: padding items sort after every item.

@@ -26,6 +26,12 @@ __global__ void k_step(int* x, int i) {
     if (threadIdx.x == 0) x[(i + 1) & 1023] = x[i & 1023] + 1;
 }
 
+// Holds stream 0 until the host has queued everything (bounded spin on a host-mapped word), so the
+// device then runs the queued chains back to back, free of the host's submission rate.
+__global__ void k_block(const volatile int* flag) {
+    for (long spins = 0; spins < (1l << 24) && *flag == 0; spins++) __builtin_amdgcn_s_sleep(8);
+}
+
 static double run(int Q, int K, int batches, int blocks) {
     std::vector<hipStream_t> s(Q);
     std::vector<hipEvent_t> ev(Q);
@@ -36,8 +42,17 @@ static double run(int Q, int K, int batches, int blocks) {
         CK(hipMalloc(&buf[q], 4096));
         CK(hipMemset(buf[q], 0, 4096));
     }
+    int* flag = nullptr;
+    int* dflag = nullptr;
+    CK(hipHostMalloc(&flag, 64, hipHostMallocMapped));
+    *flag = 0;
+    CK(hipHostGetDevicePointer((void**)&dflag, flag, 0));
+    hipEvent_t go;
+    CK(hipEventCreateWithFlags(&go, hipEventDisableTiming));
     CK(hipDeviceSynchronize());
-    const auto t0 = std::chrono::steady_clock::now();
+    hipLaunchKernelGGL(k_block, dim3(1), dim3(64), 0, s[0], dflag);
+    CK(hipEventRecord(go, s[0]));
+    for (int q = 1; q < Q; q++) CK(hipStreamWaitEvent(s[q], go, 0));
     for (int b = 0; b < batches; b++) {
         for (int q = 0; q < Q; q++) {
             if (b > 0 && Q > 1) CK(hipStreamWaitEvent(s[q], ev[(q + 1) % Q], 0));
@@ -45,8 +60,12 @@ static double run(int Q, int K, int batches, int blocks) {
             CK(hipEventRecord(ev[q], s[q]));
         }
     }
+    const auto t0 = std::chrono::steady_clock::now();
+    __atomic_store_n(flag, 1, __ATOMIC_SEQ_CST);
     CK(hipDeviceSynchronize());
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    CK(hipEventDestroy(go));
+    CK(hipHostFree(flag));
     for (int q = 0; q < Q; q++) {
         CK(hipStreamDestroy(s[q]));
         CK(hipEventDestroy(ev[q]));
@@ -56,7 +75,7 @@ static double run(int Q, int K, int batches, int blocks) {
 }
 
 int main() {
-    const int K = 8, batches = 400;
+    const int K = 8, batches = 40;  // <= ~400 packets per queue stay queued behind the blocker
     run(1, K, 20, 1);
     for (int blocks : {1, 256}) {
         for (int Q : {1, 2, 4}) {
