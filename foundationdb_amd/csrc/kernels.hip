@@ -2265,7 +2265,61 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         if (minLive[j] < t) return kUndecided;
         return kAborted;
     };
-    if (!sc->edge_overflow) {
+    constexpr int kTPer = 8;  // transactions per thread held in registers (T <= 8 * kWG)
+    if (!sc->edge_overflow && use_pre && T <= kTPer * (int)blockDim.x) {
+        // Rounds with each thread's transactions' resume pointers in registers, and the first
+        // writer of every undecided transaction loaded together at the start of a round (the
+        // walk's further steps, skipping writers aborted since, are the rare case).
+        int ep[kTPer], en[kTPer];
+#pragma unroll
+        for (int k = 0; k < kTPer; k++) {
+            const int t = threadIdx.x + k * blockDim.x;
+            ep[k] = t < T ? w.pre_ep[t] : 0;
+            en[k] = t < T ? w.pre_end[t] : 0;
+        }
+        volatile uint8_t* vst = st;
+        for (;;) {
+            if (threadIdx.x == 0) s_more = 0;
+            if (NW) group_minima(vst);
+            __syncthreads();
+            int more = 0;
+            int e0[kTPer];
+#pragma unroll
+            for (int k = 0; k < kTPer; k++) {
+                const int t = threadIdx.x + k * blockDim.x;
+                e0[k] = t < T && vst[t] == kUndecided && ep[k] < en[k] ? w.tedges[ep[k]] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < kTPer; k++) {
+                const int t = threadIdx.x + k * blockDim.x;
+                if (t >= T || vst[t] != kUndecided) continue;
+                int p = ep[k];
+                const int end = en[k];
+                uint8_t res = kUndecided;
+                int e = e0[k];
+                while (p < end) {
+                    const uint8_t sp = e >= T ? group_status(e, t) : vst[e];
+                    if (sp == kAborted) {
+                        if (++p < end) e = w.tedges[p];
+                        continue;
+                    }
+                    if (sp == kCommitted) res = kAborted;
+                    break;
+                }
+                if (p == end) res = kCommitted;
+                ep[k] = p;
+                if (res != kUndecided)
+                    vst[t] = res;
+                else
+                    more = 1;
+            }
+            if (more) s_more = 1;
+            __syncthreads();
+            rounds++;
+            if (!s_more) break;
+            __syncthreads();
+        }
+    } else if (!sc->edge_overflow) {
         for (int t = threadIdx.x; t < T; t += blockDim.x)
             w.eptr[t] = use_pre ? w.pre_ep[t] : (b.roff[t] < b.roff[t + 1] ? w.eoff[b.roff[t]] : 0);
         volatile uint8_t* vst = st;
