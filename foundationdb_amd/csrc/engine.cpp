@@ -1695,7 +1695,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(hipStreamSynchronize(s));
         unsigned long long init[kTrSlots];
         for (int i = 0; i < kTrSlots; i++)
-            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin) ? ~0ull : 0ull;
+            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin || i == kTrResBegin) ? ~0ull : 0ull;
         HIPOK(hipMemcpy(w.trace, init, sizeof(init), hipMemcpyHostToDevice));
     }
     launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
@@ -1930,6 +1930,9 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                     us(kTrSampleBegin, kTrSampleEnd), us(kTrCheckBegin, kTrCheckEnd), us(kTrSampleBegin, kTrCheckBegin),
                     us(kTrEpiBegin, kTrEpiLevels), us(kTrEpiLevels, kTrEpiZero), us(kTrEpiZero, kTrEpiHost),
                     us(kTrEpiHost, kTrEpiFence));
+            fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
+                    us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),
+                    us(kTrResRounds, kTrResEnd));
 
 
         }

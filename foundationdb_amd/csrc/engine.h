@@ -192,6 +192,7 @@ struct Work {
 enum TraceSlot {
     kTrSampleBegin, kTrSampleEnd, kTrCheckBegin, kTrCheckEnd,
     kTrEpiBegin, kTrEpiLevels, kTrEpiZero, kTrEpiHost, kTrEpiFence, kTrEpiEnd,
+    kTrResBegin, kTrResPre, kTrResWait, kTrResRounds, kTrResEnd,
     kTrSlots
 };
 __device__ __forceinline__ void trace_min(unsigned long long* tr, int slot) {

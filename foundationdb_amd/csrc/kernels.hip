@@ -2059,6 +2059,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
     extern __shared__ __attribute__((aligned(16))) uint8_t st[];
     __shared__ int s_more;
     const int T = b.T;
+    if (threadIdx.x == 0) trace_min(w.trace, kTrResBegin);
     if (sc->n_edges == 0 && !sc->edge_overflow) {
         // no candidate writer anywhere: every admitted transaction without a history conflict
         // commits (SkipList.cpp:817-833 with an empty MiniConflictSet); all workgroups share the work
@@ -2149,6 +2150,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         // wave waits for its stores, then one lane releases at agent scope and arrives
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2176,6 +2178,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         s_pre = ok;
     }
     __syncthreads();
+    if (threadIdx.x == 0) trace_max(w.trace, kTrResWait);
     const bool use_pre = s_pre != 0;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         st[t] = use_pre ? w.pre_st[t] : ((w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided);
@@ -2442,6 +2445,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         rounds = -1;
     }
     __syncthreads();
+    if (threadIdx.x == 0) trace_max(w.trace, kTrResRounds);
     if (NW && !sc->edge_overflow) {  // final committed minima per group (conflicting-key reports)
         group_minima(st);
         for (int j = threadIdx.x; j < NW; j += blockDim.x) w.gminc[j] = minComm[j];
@@ -2451,6 +2455,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         vout[t] = verdict_byte(b, t, st[t]);
     }
     if (threadIdx.x == 0) sc->rounds = rounds;
+    if (threadIdx.x == 0) trace_max(w.trace, kTrResEnd);
 }
 
 // First conflicting read index of intra-batch aborts that report conflicting keys

@@ -1,4 +1,5 @@
-"""C2 batches run one at a time with FDBCS_TRACE=1: prints device timestamps of kernel sections."""
+"""C2 (or C3: third argument "c3") batches run one at a time with FDBCS_TRACE=1: prints device
+timestamps of kernel sections."""
 import os
 import sys
 
@@ -14,10 +15,11 @@ kb, ko, vers = W.c2_history(p, seed=1, start_version=10_000_000)
 cs = C.ConflictSet(0)
 cs.load_history(kb, ko, vers, 0)
 rng = np.random.default_rng(5)
+zipf = W.ZipfGenerator(1_000_000, 0.99) if len(sys.argv) > 3 and sys.argv[3] == "c3" else None
 now = 10_000_000
 for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 12):
     now += p.version_step
-    pb = W.c2_batch(p, rng, now)
+    pb = W.c3_batch(p, rng, now, zipf) if zipf else W.c2_batch(p, rng, now)
     b = C.ConflictBatch(cs)
     b.add_packed(pb)
     b.upload()
