@@ -155,6 +155,7 @@ struct Work {
     int2* members;         // [W] (transaction, group) of each group member, compacted (k_resolve)
     int32_t* gminc;        // [W] per group: least committed member transaction (k_resolve)
     int32_t groups = 0;    // set per batch
+    int32_t member_lds = 0;  // group members the resolver keeps in LDS (set at its launch)
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction

@@ -2192,18 +2192,21 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
     const int NW = w.groups ? b.W : 0;
     int32_t* minLive = (int32_t*)(st + ((T + 15) & ~15));
     int32_t* minComm = minLive + NW;
+    int2* smembers = (int2*)(minComm + NW);  // the members, when they fit (w.member_lds)
     __shared__ int s_nmem;
+    __shared__ int s_mlds;
     __shared__ int s_wred[kWG / 64];
     auto group_minima = [&](const volatile uint8_t* sv) {
         for (int j = threadIdx.x; j < NW; j += blockDim.x) minLive[j] = minComm[j] = INT_MAX;
         __syncthreads();
         const int M = s_nmem;
+        const int2* mem = s_mlds ? smembers : w.members;
         for (int m0 = threadIdx.x; m0 < M; m0 += 4 * blockDim.x) {
             int2 e[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const int m = m0 + u * blockDim.x;
-                e[u] = m < M ? w.members[m] : make_int2(-1, 0);
+                e[u] = m < M ? mem[m] : make_int2(-1, 0);
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -2251,12 +2254,17 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         __syncthreads();
         int total;
         int off = block_excl_sum<int>(nm, s_wred, &total);
+        const bool in_lds = total <= w.member_lds;  // uniform: every round reads them from LDS
+        int2* mdst = in_lds ? smembers : w.members;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             if (lw[k] == 2) carry = x0 + k;
-            if (lw[k] != 0) w.members[off++] = make_int2(tx[k], carry);
+            if (lw[k] != 0) mdst[off++] = make_int2(tx[k], carry);
         }
-        if (threadIdx.x == 0) s_nmem = total;
+        if (threadIdx.x == 0) {
+            s_nmem = total;
+            s_mlds = in_lds ? 1 : 0;
+        }
         __threadfence_block();
         __syncthreads();
     }
@@ -2476,18 +2484,27 @@ __global__ __launch_bounds__(kBlock) void k_intra_report(BatchDev b, Work w) {
     }
 }
 
+constexpr size_t kResolveLdsMax = 160 * 1024 - 1024;  // dynamic LDS of k_resolve (static uses < 1 KiB)
+
 void init_kernel_attributes() {
-    // status bytes (<= kMaxTxnLds) + write-group minima (<= 8 kMaxGroupWrites) + static LDS
-    (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              ((kMaxTxnLds + 15) / 16 * 16) + 8 * kMaxGroupWrites);
+    // status bytes (<= kMaxTxnLds) + write-group minima (<= 8 kMaxGroupWrites) + the members that
+    // fit, within kResolveLdsMax (the rest of the 160 KiB is the kernel's static LDS)
+    (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLdsMax);
 }
 
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out) {
     if (b.T == 0) return;
     // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
     const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
-    const size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
-    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (uint32_t)lds, s, b, w, verdict_out);
+    size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
+    Work wl = w;
+    wl.member_lds = 0;
+    if (w.groups) {  // the group members too, in what the dynamic LDS limit leaves
+        const size_t room = kResolveLdsMax > lds ? (kResolveLdsMax - lds) / 8 : 0;
+        wl.member_lds = (int32_t)std::min<size_t>(room, (size_t)b.W);
+        lds += 8 * (size_t)wl.member_lds;
+    }
+    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
