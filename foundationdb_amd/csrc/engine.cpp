@@ -175,7 +175,7 @@ struct fdbcs_conflict_set {
     int inflight = 0;
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
     int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket (testing knob; 0 = default)
-    int sample_per = 0;     // FDBCS_SORT_SAMPLES: splitter samples per bucket (0 = default 8)
+    int sample_per = 0;     // FDBCS_SORT_SAMPLES: splitter samples per bucket (0 = default 4)
     bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)

@@ -1254,11 +1254,12 @@ __global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
     if (threadIdx.x == 0) trace_max(c.trace, kTrSampleEnd);
 }
 
-// Number of samples for nb buckets (about 8 per bucket: the largest of ~550 buckets stays well
-// under the one-pass bitonic size; 4 per bucket let one in ~3 batches pass it at C2).
-// per: samples per bucket (FDBCS_SORT_SAMPLES; 0 = default 8).
+// Number of samples for nb buckets: 4 per bucket by default.  With 8 the largest of ~550 buckets
+// stays well under the one-pass size, with 4 one bucket in ~3 batches passes it at C2 and takes
+// the chunked path, but ranking a quarter of the sample pairs wins overall (C4 20.1-20.2M vs
+// 19.5-19.6M txns/s, C3 +1 %, C2 +1 %).  per: FDBCS_SORT_SAMPLES (0 = default).
 inline int sample_count(int E, int nb, int per) {
-    int S = (per > 0 ? per : 8) * nb;
+    int S = (per > 0 ? per : 4) * nb;
     S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
     return S > E ? E : S;
 }

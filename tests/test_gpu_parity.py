@@ -330,7 +330,7 @@ def test_edge_cases(engine):
     assert ex.value.status == engine.FDBCS_E_VERSION
 
 
-@pytest.mark.parametrize("bucket,samples", [("3000", "0"), ("40", "0"), ("160", "2"), ("64", "1")])
+@pytest.mark.parametrize("bucket,samples", [("3000", "0"), ("40", "0"), ("160", "2"), ("64", "1"), ("128", "8")])
 def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket, samples):
     """Oversized sort buckets (chunked rank sort + merges through memory), tiny ones, and sparse
     splitter samples (skewed buckets), with keys longer than the 16-byte prefix, give the same
