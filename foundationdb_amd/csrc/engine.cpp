@@ -2002,8 +2002,12 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             st.intra_rounds += b->h_scal->intra_rounds;
         }
         // algorithmic bytes of the copy kernels (roofline.py): read every kept old boundary and
-        // write every boundary of the result, 32 B each (16 B key, 8 B length/tail, 8 B version)
-        st.merge_bytes += 32 * ((b->h_scal->d_before - b->h_scal->d_rem) + b->h_scal->nd_next);
+        // every inserted one (its key from the batch), write every boundary of the result, 32 B
+        // each (16 B key, 8 B length/tail, 8 B version); kept + inserted = the result's size
+        {
+            const int64_t kept = b->h_scal->d_before - b->h_scal->d_rem, out = b->h_scal->nd_next;
+            st.merge_bytes += 32 * (kept + (out - kept) + out);
+        }
         if ((b->recorded >> kPhCheckEnd) & 1u) {
             st.ms_check_kernel += ph(kPhCheckBegin, kPhCheckEnd);
             st.check_launches += b->R() > 0;
