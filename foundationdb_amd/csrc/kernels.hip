@@ -5,12 +5,16 @@
 // in HBM (structure of arrays) with a 64-ary range-max hierarchy, and every phase
 // of ConflictBatch::detectConflicts is a data-parallel kernel:
 //
-//   D.CheckRead        k_check_reads      per read range: two searches + range max
-//   D.Sort             k_sample, k_bucket_count/scatter/sort   sample sort of endpoints by (key, class)
-//   D.CheckIntraBatch  k_positions, k_edges_*, k_resolve   candidate edges + batch-order rounds
-//   D.Combine          k_combine          coverage scan over sorted endpoints
-//   D.MergeWrite       k_seg_search, k_merge_copy, k_merge_insert, k_blockmax
-//   D.RemoveBefore     k_gc_count / k_gc_scatter
+//   D.CheckRead        k_check_reads (both tiers) or k_check_tier<base / delta> (split check):
+//                      per read range two cooperative tree searches + range max
+//   D.Sort             k_sample, k_bucket_count, k_bucket_scatter, k_bucket_sort: sample sort of
+//                      the endpoints by (key, class, id)
+//   D.CheckIntraBatch  k_scan<PosScan>, k_scan<EdgePairScan>, k_edge_fill, k_resolve: candidate
+//                      edges (one per write group) + batch-order rounds
+//   D.Combine          k_scan2<CoverScan, SegmentScan>: union segments of committed writes
+//   D.MergeWrite       k_seg_search, k_scan<SegSumScan>, k_merge_copy<BatchIns>; compaction:
+//                      k_compact_search, k_scan<CompactSumScan>, k_merge_copy<CompactIns>
+//   D.RemoveBefore     k_scan<GcScan> (with a compaction); k_epilogue: levels, index, scalars
 //
 // Memory-bound integer/byte work: no MFMA anywhere (BASELINE.json north_star).
 #include <hip/hip_runtime.h>
