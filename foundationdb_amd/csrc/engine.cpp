@@ -149,6 +149,7 @@ struct fdbcs_conflict_set {
     // base tier: two buffer sets (ping-pong) + range-max levels
     DBuf hkey[2], hlt[2], hver[2];
     DBuf lvl[kMaxLevels];  // lvl[0]: sampled key index (the level-0 versions are hver[cur])
+    DBuf dir;              // radix directory over the base tier's level-0 samples (k_directory)
     int cur = 0;
     int64_t hist_cap = 0;  // elements per buffer set
     int64_t n_ub = 0;      // upper bound of live base boundaries (exact after a wait)
@@ -204,6 +205,7 @@ struct fdbcs_conflict_set {
     // C2 (27.5M vs 30.1M txns/s): level 1 by atomics and levels 2-3 rebuilt by one last workgroup
     // through device-scope loads cost more than the launch they save.  Off by default.
     bool fuse_epilogue = false;
+    bool directory = true;  // FDBCS_DIRECTORY=0: base-tier lookups descend the whole sample tree (A/B)
     DBuf trace_buf;
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
@@ -507,6 +509,7 @@ MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->lvl[L].p;
     m.keys = (const ulonglong2*)cs->hkey[k].p;
     carve_index(m, (ulonglong2*)cs->lvl[0].p, cs->hist_cap);
+    m.dir = cs->directory ? (const int32_t*)cs->dir.p : nullptr;
     return m;
 }
 
@@ -615,6 +618,7 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
         cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
         if ((rc = grow_sets(cs, cs->hkey, cs->hlt, cs->hver, cs->cur, cs->n_ub, cap))) return rc;
         if ((rc = alloc_levels(cs->lvl, cap, &cs->lvl3_n))) return rc;
+        if (cs->directory && (rc = cs->dir.ensure(4 * ((size_t)kDirSlots + 1)))) return rc;
         cs->hist_cap = cap;
         launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n,
                         cs->lvl3_n, std::max<int64_t>(cs->n_ub, 1));
@@ -1085,6 +1089,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_FUSE_EPILOGUE")) cs->fuse_epilogue = v[0] != '0';
+    if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
@@ -1141,6 +1146,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->htail[0].release();
     cs->htail[1].release();
     for (auto& l : cs->lvl) l.release();
+    cs->dir.release();
     for (auto& l : cs->dlvl) l.release();
     for (auto& x : cs->cws) x.release();
     for (auto& set : cs->ws)

@@ -359,24 +359,52 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     auto prefix_eq = [&](const ulonglong2& k) { return k.x == q.hi && k.y == q.lo; };
     int64_t c = 0;
     bool bknown = false;
-    for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
-        const bool v = j0 + gl < sz[top];
-        const ulonglong2 e = m.skey[top][v ? j0 + gl : 0];
-        const int k = __popc(gmask(v && prefix_less(e, q)));
-        if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
-        c += k;
-        if (k < kArity) break;
+    // the top level's first group is loaded beside the directory slot (no added round trip when
+    // the slot is crowded and the tree is taken)
+    const bool v_top = gl < sz[top];
+    const ulonglong2 e_top = m.skey[top][v_top ? gl : 0];
+    bool direct = false;
+    if (m.dir) {
+        // radix directory (k_directory): the level-0 samples sharing q's first two bytes are
+        // [dir[v], dir[v+1]); a slot of at most two groups is counted directly at level 0
+        const uint32_t dv = (uint32_t)(q.hi >> 48);
+        const int64_t d0 = m.dir[dv], d1 = m.dir[dv + 1];
+        if (d1 - d0 <= 2 * kArity && d1 <= sz[0]) {
+            direct = true;
+            c = d0;
+            bknown = true;  // all of the slot below q: the next sample's first two bytes are greater
+            for (int64_t j0 = d0; j0 < d1; j0 += kArity) {
+                const bool v = j0 + gl < d1;
+                const ulonglong2 e = m.skey[0][v ? j0 + gl : 0];
+                const int k = __popc(gmask(v && prefix_less(e, q)));
+                c += k;
+                if (k < __popc(gmask(v))) {
+                    bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+                    break;
+                }
+            }
+        }
     }
-    for (int L = top; L > 0; L--) {
-        if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
-        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, Ac]
-        const int64_t base = (int64_t)kArity * (c - 1) + 1;
-        const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
-        const bool v = base + gl < end;
-        const ulonglong2 e = m.skey[L - 1][v ? base + gl : 0];
-        const int k = __popc(gmask(v && prefix_less(e, q)));
-        if (L == 1 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
-        c = base + k;
+    if (!direct) {
+        for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
+            const bool v = j0 == 0 ? v_top : j0 + gl < sz[top];
+            const ulonglong2 e = j0 == 0 ? e_top : m.skey[top][v ? j0 + gl : 0];
+            const int k = __popc(gmask(v && prefix_less(e, q)));
+            if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+            c += k;
+            if (k < kArity) break;
+        }
+        for (int L = top; L > 0; L--) {
+            if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
+            // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, Ac]
+            const int64_t base = (int64_t)kArity * (c - 1) + 1;
+            const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
+            const bool v = base + gl < end;
+            const ulonglong2 e = m.skey[L - 1][v ? base + gl : 0];
+            const int k = __popc(gmask(v && prefix_less(e, q)));
+            if (L == 1 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+            c = base + k;
+        }
     }
     // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
     int64_t b = c;
@@ -3435,8 +3463,36 @@ static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
     return g > 4096 ? 4096 : g;
 }
 
+// Radix directory of the base tier (D.CheckRead): dir[v] = number of level-0 samples (keys[64 j],
+// j < ceil(n / 64)) whose first two key bytes are below v, v in [0, 65536].  A lookup whose slot
+// holds at most two sample groups starts at level 0 (one directory load, one or two group loads)
+// instead of descending the ~6 levels above it; slots crowded by shared key prefixes (subspaces,
+// hot ranges) take the tree.  Rebuilt with the base tier's index (compaction, GC, load), one
+// binary search per slot.
+__global__ __launch_bounds__(kBlock) void k_directory(const ulonglong2* keys, const int64_t* np, int32_t* dir) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v > kDirSlots) return;
+    const int64_t S = (*np + kFan - 1) / kFan;
+    int64_t lo = 0, hi = S;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)(keys[mid * kFan].x >> 48) < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    dir[v] = (int32_t)lo;
+}
+
+static void launch_directory(hipStream_t s, const MaxLevels& m, const int64_t* n) {
+    if (!m.dir) return;
+    fdb_launch(k_directory, dim3((kDirSlots + kBlock) / kBlock), dim3(kBlock), 0, s, m.keys, n,
+               const_cast<int32_t*>(m.dir));
+}
+
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
                      int64_t grid_hint_n) {
+    launch_directory(s, m, n);
     fdb_launch(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
     Epilogue ep{};
     ep.trace = nullptr;
@@ -3447,6 +3503,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n) {
     const Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq);
+    if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
     fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,

@@ -171,6 +171,54 @@ def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split):
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
+@pytest.mark.parametrize("directory,split", [("1", "2"), ("1", "1"), ("0", "2")])
+def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split):
+    """The base tier's radix directory (first two key bytes -> level-0 samples): sparse slots
+    counted directly, a crowded slot (one 2-byte prefix holding thousands of boundaries) taking
+    the tree, keys at the slot edges (empty key, 0x0000.., 0xffff.., bare 2-byte keys), and
+    compactions rebuilding the directory between batches."""
+    monkeypatch.setenv("FDBCS_DIRECTORY", directory)
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
+    rng = np.random.default_rng(4242)
+    edges = [b"", b"\x00", b"\x00\x00", b"\x00\x00\x00", b"\x12\x33\xff", b"\x12\x34", b"\x12\x34\x00",
+             b"\x12\x35", b"\xff\xfe\xff", b"\xff\xff", b"\xff\xff\x00", b"\xff\xff\xff\xff"]
+
+    def key():
+        u = rng.random()
+        if u < 0.55:
+            return bytes(rng.integers(0, 256, size=int(rng.integers(1, 20))).astype(np.uint8))
+        if u < 0.9:
+            return b"AB" + bytes(rng.integers(0, 256, size=int(rng.integers(0, 12))).astype(np.uint8))
+        e = edges[int(rng.integers(0, len(edges)))]
+        return e + bytes(rng.integers(0, 4, size=int(rng.integers(0, 3))).astype(np.uint8))
+
+    hist = sorted({key() for _ in range(60000)} | set(edges[1:]))
+    kb = np.frombuffer(b"".join(hist), np.uint8)
+    ko = np.zeros(len(hist) + 1, np.int64)
+    np.cumsum([len(k) for k in hist], out=ko[1:])
+    vers = rng.integers(0, 1000, size=len(hist)).astype(np.int64)
+    e = EngineDriver(engine, gc_interval=2)
+    o = oracle_mod.SkipListBaseline()
+    e.load_history(kb, ko, vers)
+    o.load_history(kb, ko, vers)
+    now = 1000
+    for i in range(8):
+        now += 10
+        txns = []
+        for _ in range(500):
+            def rr():
+                a, b = key(), key()
+                return KeyRange(min(a, b), max(a, b))
+
+            txns.append(CommitTransaction([rr() for _ in range(int(rng.integers(1, 4)))],
+                                          [rr() for _ in range(int(rng.integers(0, 3)))],
+                                          now - int(rng.integers(0, 600)), False))
+        pb = PackedBatch.from_transactions(txns)
+        ve, _ = e.detect(pb, now, 0)
+        vo, _ = o.detect(pb, now, 0, gc=(i + 1) % 2 == 0)
+        assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
+
+
 @pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("plen", [30, 60, 104, 150])
 def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split):
@@ -491,7 +539,8 @@ def test_empty_batches(engine, oracle_mod):
                                    {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_SORTED_READS": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
-                                   {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_UPLOAD": "kernel"}])
+                                   {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_UPLOAD": "kernel"},
+                                   {"FDBCS_DIRECTORY": "0"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the epilogue
     fused into the merge copy, the unsplit read check, and long-key sorting without LDS windows."""
