@@ -6,7 +6,8 @@
 // of ConflictBatch::detectConflicts is a data-parallel kernel:
 //
 //   D.CheckRead        k_check_reads (both tiers) or k_check_tier<base / delta> (split check):
-//                      per read range two cooperative tree searches + range max
+//                      per read range two cooperative tree searches + range max; k_directory:
+//                      the base tier's radix directory (first two key bytes -> level-0 samples)
 //   D.Sort             k_sample, k_bucket_count, k_bucket_scatter, k_bucket_sort: sample sort of
 //                      the endpoints by (key, class, id)
 //   D.CheckIntraBatch  k_scan<PosScan>, k_scan<EdgePairScan>, k_edge_fill, k_resolve: candidate
