@@ -190,7 +190,8 @@ struct fdbcs_conflict_set {
     // vs 30.0M txns/s with the kernel, whose workgroups stall on PCIe reads beside stage A/B.
     bool dma_upload = true;
     int upload_blocks = 32;   // FDBCS_UPLOAD_BLOCKS: workgroups of the k_upload kernel
-    int check_version = 1;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants)
+    int check_version = 6;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants;
+                              // 6 as 1 with the base and delta lookups in separate waves)
     int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
@@ -1091,7 +1092,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_FUSE_EPILOGUE")) cs->fuse_epilogue = v[0] != '0';
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
-    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(5, std::max(1, atoi(v)));
+    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(6, std::max(1, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     static std::once_flag attr_once;

@@ -5,7 +5,7 @@
 // in HBM (structure of arrays) with a 64-ary range-max hierarchy, and every phase
 // of ConflictBatch::detectConflicts is a data-parallel kernel:
 //
-//   D.CheckRead        k_check_reads (both tiers) or k_check_tier<base / delta> (split check):
+//   D.CheckRead        k_check_reads<tier waves> (both tiers) or k_check_tier<base / delta> (split check):
 //                      per read range two cooperative tree searches + range max; k_directory:
 //                      the base tier's radix directory (first two key bytes -> level-0 samples)
 //   D.Sort             k_sample, k_bucket_count, k_bucket_scatter, k_bucket_sort: sample sort of
@@ -689,6 +689,48 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
     }
 }
 
+// check_read with the tiers in separate waves (FDBCS_CHECK=6): a block's first half of waves
+// searches the base tier for its kBlock / kReadLanes reads (16 lanes each: begin and end groups),
+// the second half the delta tier for the same reads, and the delta verdicts reach the base
+// leaders through LDS.  In check_read a wave holds both tiers' groups, so a base lookup taking the
+// radix directory and a delta lookup descending its tree run one after the other (divergent
+// branches of one wave); here each wave runs one of them.
+__device__ __forceinline__ void check_read_tier_waves(const BatchDev& b, const Tier& base, const Tier& delta,
+                                                      const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf) {
+    constexpr int kPerWave = 64 / (2 * kArity);               // reads per wave (16 lanes each)
+    constexpr int kHalf = kBlock / 64 / 2;                    // waves per tier
+    constexpr int kReadsPerBlock = kHalf * kPerWave;          // == kBlock / kReadLanes
+    static_assert(kReadsPerBlock == kBlock / kReadLanes, "same reads per block as check_read");
+    __shared__ uint8_t sconf[kReadsPerBlock];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool is_delta = wave >= kHalf;
+    const int local = (wave % kHalf) * kPerWave + lane / (2 * kArity);
+    const int64_t r = (int64_t)blockIdx.x * kReadsPerBlock + local;
+    const int grp = (lane / kArity) & 1;  // 0 begin key, 1 end key
+    const bool live = r < b.R;
+    const int64_t rr = live ? r : 0;
+    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+    const Tier& tier = is_delta ? delta : base;
+    const int64_t n = *tier.n;
+    const int64_t snap = b.snap[b.rowner[rr]];
+    int64_t lb = 0;
+    bool eq = false;
+    if (live && !(grp && degenerate)) lb = group_lower_bound(tier.h, tier.m, n, grp ? ke : kb, htail, b.tail, eq);
+    const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // the begin group takes the end key's position
+    const bool leader = (lane & (2 * kArity - 1)) == 0;
+    bool conf = false;
+    if (live && leader && (!is_delta || n > 0))
+        conf = tier_conflict(tier.h, tier.m, is_delta ? kHole : tier.hdr, lb, eq, j, degenerate, snap);
+    if (leader && is_delta) sconf[local] = conf ? 1 : 0;
+    __syncthreads();
+    if (live && leader && !is_delta) {
+        conf = conf || sconf[local];
+        rconf[r] = conf ? 1 : 0;
+        if (conf) hist_conf[b.rowner[r]] = 1;
+    }
+}
+
 // One tier only (the split check): 2 lane groups per read locate its begin / end in `tier`; a
 // conflict sets the read's and its transaction's flags (zeroed beforehand by the epilogue that last
 // used the workspace), so the base-tier launch (stage A, on its own stream) and the delta-tier
@@ -1053,7 +1095,7 @@ __device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckR
     if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
 
-// Variants (FDBCS_CHECK): 2 = base and delta groups of a read in one wave, 256 threads (default);
+// Variants (FDBCS_CHECK, A/B; LDS-staged top levels): 2 = base and delta groups of a read in one wave, 256 threads;
 // 3 = the same, 512 threads; 4 = wave-uniform tiers, 512 threads.
 __global__ __launch_bounds__(256) void k_check_reads2(BatchDev b, CheckReads2 c) { check_reads_body<256, false>(b, c); }
 __global__ __launch_bounds__(512) void k_check_reads3(BatchDev b, CheckReads2 c) { check_reads_body<512, false>(b, c); }
@@ -1327,10 +1369,14 @@ void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Ti
                sorted_reads ? (const int32_t*)w.rbpos : nullptr, sorted_reads ? (const uint32_t*)w.pmeta : nullptr);
 }
 
+template <bool TIER_WAVES>
 __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c) {
     if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
+    if constexpr (TIER_WAVES)
+        check_read_tier_waves(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf);
+    else
+        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
     __syncthreads();
     if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
@@ -1729,10 +1775,13 @@ void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_t
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
                   const uint8_t* htail, int check_version, int check_grid_cap) {
     if (b.R == 0) return;
-    if (check_version == 1) {  // FDBCS_CHECK=1: four independent lookups per read, no LDS staging
+    if (check_version == 1 || check_version == 6) {  // four independent lookups per read, no LDS staging
         CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
         const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
-        fdb_launch(k_check_reads, dim3(grid), dim3(kBlock), 0, s, b, c);
+        if (check_version == 6)  // FDBCS_CHECK=6: base and delta lookups in separate waves
+            fdb_launch(k_check_reads<true>, dim3(grid), dim3(kBlock), 0, s, b, c);
+        else
+            fdb_launch(k_check_reads<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
         return;
     }
     CheckReads2 c{base, delta, htail, w.hist_conf, w.rconf, w.trace};

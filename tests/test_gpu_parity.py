@@ -540,7 +540,7 @@ def test_empty_batches(engine, oracle_mod):
                                    {"FDBCS_SORTED_READS": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_UPLOAD": "kernel"},
-                                   {"FDBCS_DIRECTORY": "0"}])
+                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the epilogue
     fused into the merge copy, the unsplit read check, and long-key sorting without LDS windows."""
