@@ -150,6 +150,9 @@ struct fdbcs_conflict_set {
     DBuf hkey[2], hlt[2], hver[2];
     DBuf lvl[kMaxLevels];  // lvl[0]: sampled key index (the level-0 versions are hver[cur])
     DBuf dir;              // radix directory over the base tier's level-0 samples (k_directory)
+    DBuf edir;             // the delta tier's directory (epoch-tagged entries, filled by k_epilogue)
+    uint32_t ddir_epoch = 0;    // epoch of the delta tier's current directory (0: none)
+    uint32_t ddir_counter = 0;  // last epoch handed out
     int cur = 0;
     int64_t hist_cap = 0;  // elements per buffer set
     int64_t n_ub = 0;      // upper bound of live base boundaries (exact after a wait)
@@ -528,6 +531,8 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->dlvl[L].p;
     m.keys = (const ulonglong2*)cs->dkey[k].p;
     carve_index(m, (ulonglong2*)cs->dlvl[0].p, cs->delta_cap);
+    m.edir = (uint64_t*)cs->edir.p;
+    m.edir_epoch = cs->edir.p ? cs->ddir_epoch : 0;
     return m;
 }
 
@@ -1114,6 +1119,11 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
 
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
+    if (!rc && cs->directory) {  // zeroed: epoch 0 entries are never trusted
+        rc = cs->edir.ensure(8 * ((size_t)kDirSlots + 1));
+        if (!rc && hipMemsetAsync(cs->edir.p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream) != hipSuccess)
+            rc = FDBCS_E_DEVICE;
+    }
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
     if (!rc) rc = ensure_delta(cs, 1 << 14);
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
@@ -1148,6 +1158,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->htail[1].release();
     for (auto& l : cs->lvl) l.release();
     cs->dir.release();
+    cs->edir.release();
     for (auto& l : cs->dlvl) l.release();
     for (auto& x : cs->cws) x.release();
     for (auto& set : cs->ws)
@@ -1193,6 +1204,7 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = version;
     cs->max_written = version;
+    cs->ddir_epoch = 0;
     cs->n_ub = 0;
     cs->nd_ub = 0;
     cs->tail_ub = 0;
@@ -1809,6 +1821,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhGc);
     b->gc_ran = gc;
     b->compacted = compact;
+    // the epilogue that rebuilds the delta tier's index also fills its directory under a new epoch
+    // (the fused copy and compactions leave none)
+    if (compact || fuse || !cs->edir.p) {
+        cs->ddir_epoch = 0;
+    } else {
+        if (++cs->ddir_counter == 0) ++cs->ddir_counter;
+        cs->ddir_epoch = cs->ddir_counter;
+    }
     if (!fuse)
         launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
                         gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,

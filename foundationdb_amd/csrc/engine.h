@@ -39,7 +39,8 @@ struct Hist {
 // lookup descends the tree with kArity cooperating lanes, one node (one 128-byte line at A = 8) per
 // level, and lands in one 64-boundary block.
 constexpr int kArity = 8;
-constexpr int kDirSlots = 1 << 16;  // radix directory slots (first two key bytes) of the base tier
+constexpr int kDirSlots = 1 << 16;  // radix directory slots (first two key bytes) of a tier
+constexpr int kDirRun = 64;         // delta directory: slots one sample fills at most (the rest stay stale)
 constexpr int kIdxLevels = 12;  // A^11 * 64 * A boundaries under an A-entry top level
 struct MaxLevels {
     int64_t* lvl[kMaxLevels];       // lvl[0] == current Hist::ver
@@ -49,6 +50,8 @@ struct MaxLevels {
     int64_t idx_cap;                // capacity the levels were carved for: skey[L] = skey[0] + sum of
                                     // idx_level_cap(idx_cap, l < L), computable without indexing skey[]
     const int32_t* dir = nullptr;   // [65537] radix directory over skey[0] (base tier; k_directory)
+    uint64_t* edir = nullptr;       // [65537] delta tier's directory, entries (epoch << 32 | count),
+    uint32_t edir_epoch = 0;        // filled by k_epilogue; lookups trust entries of this epoch (0: off)
 };
 __host__ __device__ inline int64_t idx_level_cap(int64_t cap, int L) {
     int64_t d = 64;

@@ -365,12 +365,23 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     const bool v_top = gl < sz[top];
     const ulonglong2 e_top = m.skey[top][v_top ? gl : 0];
     bool direct = false;
-    if (m.dir) {
-        // radix directory (k_directory): the level-0 samples sharing q's first two bytes are
-        // [dir[v], dir[v+1]); a slot of at most two groups is counted directly at level 0
+    if (m.dir || m.edir_epoch) {
+        // radix directory: the level-0 samples sharing q's first two bytes are [dir[v], dir[v+1])
+        // (base: k_directory, exact; delta: k_epilogue's fill, entries of the current epoch only);
+        // a slot of at most two groups is counted directly at level 0
         const uint32_t dv = (uint32_t)(q.hi >> 48);
-        const int64_t d0 = m.dir[dv], d1 = m.dir[dv + 1];
-        if (d1 - d0 <= 2 * kArity && d1 <= sz[0]) {
+        int64_t d0, d1;
+        bool have = true;
+        if (m.dir) {
+            d0 = m.dir[dv];
+            d1 = m.dir[dv + 1];
+        } else {
+            const uint64_t x0 = m.edir[dv], x1 = m.edir[dv + 1];
+            have = (uint32_t)(x0 >> 32) == m.edir_epoch && (uint32_t)(x1 >> 32) == m.edir_epoch;
+            d0 = (uint32_t)x0;
+            d1 = (uint32_t)x1;
+        }
+        if (have && d1 - d0 <= 2 * kArity && d1 <= sz[0]) {
             direct = true;
             c = d0;
             bknown = true;  // all of the slot below q: the next sample's first two bytes are greater
@@ -3341,7 +3352,11 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         }
         const int64_t b1l = b1_0 + lane;  // lane q < 16 owns block b1_0 + q
         ulonglong2 sk = make_ulonglong2(0, 0);
-        if (lane < kFan / 4 && b1l < n1) sk = m.keys[b1l * kFan];  // sampled key of the block
+        uint64_t prev_hi = 0;  // the previous block's sampled key (delta directory fill)
+        if (lane < kFan / 4 && b1l < n1) {
+            sk = m.keys[b1l * kFan];  // sampled key of the block
+            if (m.edir_epoch && b1l > 0) prev_hi = m.keys[(b1l - 1) * kFan].x;
+        }
         // every 8th boundary of the wave's 16 blocks (128 entries of skey8, two per lane)
 #pragma unroll
         for (int h8 = 0; h8 < 2; h8++) {
@@ -3370,6 +3385,17 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
                     off += idx_level_cap(m.idx_cap, L - 1);
                     d /= kArity;
                     m.skey[0][off + d] = sk;
+                }
+                if (m.edir_epoch) {
+                    // delta directory: slots (top16(previous sample), top16(this sample)] hold this
+                    // sample's index (the first sample not below them); the last sample also fills
+                    // the slots above it with n1.  At most kDirRun slots per run: slots left over keep
+                    // an older epoch and send their lookups down the tree.
+                    const uint64_t tag = (uint64_t)m.edir_epoch << 32;
+                    const int64_t a = b1l > 0 ? (int64_t)(prev_hi >> 48) : -1, c = (int64_t)(sk.x >> 48);
+                    for (int64_t v = a + 1; v <= c && v <= a + kDirRun; v++) m.edir[v] = tag | (uint64_t)b1l;
+                    if (b1l == n1 - 1)
+                        for (int64_t v = c + 1; v <= kDirSlots && v <= c + kDirRun; v++) m.edir[v] = tag | (uint64_t)n1;
                 }
             }
             l1[wid * (kFan / 4) + lane] = mine;

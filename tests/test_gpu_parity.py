@@ -171,12 +171,14 @@ def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split):
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
-@pytest.mark.parametrize("directory,split", [("1", "2"), ("1", "1"), ("0", "2")])
-def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split):
+@pytest.mark.parametrize("directory,split,gc", [("1", "2", 2), ("1", "1", 2), ("0", "2", 2), ("1", "2", 0)])
+def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split, gc):
     """The base tier's radix directory (first two key bytes -> level-0 samples): sparse slots
     counted directly, a crowded slot (one 2-byte prefix holding thousands of boundaries) taking
     the tree, keys at the slot edges (empty key, 0x0000.., 0xffff.., bare 2-byte keys), and
-    compactions rebuilding the directory between batches."""
+    compactions rebuilding the directory between batches; gc=0 keeps every batch in the delta
+    tier, whose directory k_epilogue refills per batch under a new epoch (runs over kDirRun slots
+    stay stale and take the tree)."""
     monkeypatch.setenv("FDBCS_DIRECTORY", directory)
     monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(4242)
@@ -197,7 +199,7 @@ def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split
     ko = np.zeros(len(hist) + 1, np.int64)
     np.cumsum([len(k) for k in hist], out=ko[1:])
     vers = rng.integers(0, 1000, size=len(hist)).astype(np.int64)
-    e = EngineDriver(engine, gc_interval=2)
+    e = EngineDriver(engine, gc_interval=gc, delta_limit=100000 if gc == 0 else 0)
     o = oracle_mod.SkipListBaseline()
     e.load_history(kb, ko, vers)
     o.load_history(kb, ko, vers)
