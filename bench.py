@@ -13,11 +13,20 @@ bytes back in host memory (H2D/D2H included, generation excluded)
 only" figure excludes addTransaction (SkipList.cpp:1069-1078, 1087-1090).  `total_txns_per_s`
 is the reference's "total" figure: addTransaction inside the timed loop as well.
 
-After timing, the same batch sequence (warmup, timed, total and breakdown batches) is replayed on
-the CPU restatement of the reference algorithm (oracle/skiplist_baseline.cpp) and every GPU
-verdict is compared: `parity` in the JSON line.  At N=1 that replay's time over the timed batches
-is `cpu_baseline` (single thread, pinned to one core like skipListTest's setAffinity(0),
-SkipList.cpp:1015).
+Passes, in order, each on its own batches: warmup; a per-kernel profile (events around every
+kernel, timing level 3) that names the dominant kernel (largest device time); the timed region
+(events around that kernel only, on 1 batch in 4: `roofline`); device-resident, add+detect
+("total"), synchronous (one batch at a time through detect_conflicts, as Resolver.actor.cpp:179-194
+calls it: `sync_*` and per-batch latency), device-bound (batches queued behind a hold kernel, then
+released: the device's own rate) and per-phase breakdown passes.
+
+After timing, the whole batch sequence is replayed on the CPU restatement of the reference
+algorithm (oracle/skiplist_baseline.cpp, with the reference's bounded removeBefore,
+SkipList.cpp:880-889) and every GPU verdict is compared: `parity` in the JSON line.  That replay's
+time over the timed batches is `cpu_baseline`: one thread pinned to one core like skipListTest's
+setAffinity(0) (SkipList.cpp:1015), per phase as the reference's PerfDoubleCounters
+(SkipList.cpp:49-51, 1082-1102); at N > 1 every rank replays its own routed sub-batches on its own
+pinned core at the same time (G resolvers on G cores), over the max of their times.
 
 N > 1 (torchrun, one rank per GPU): the key space is range-sharded across ranks like FDB's
 multi-resolver split (CommitProxyServer.actor.cpp:147-174).  Every rank builds the same global batch
@@ -68,6 +77,12 @@ def parse():
                     help="batches of the device-resident pass (uploaded before its timed region; diagnostic)")
     ap.add_argument("--breakdown-steps", type=int, default=16,
                     help="extra batches after the timed region with every phase timed (diagnostic)")
+    ap.add_argument("--profile-steps", type=int, default=16,
+                    help="batches with events around every kernel (per-kernel table, dominant kernel)")
+    ap.add_argument("--sync-steps", type=int, default=20,
+                    help="batches resolved one at a time (window 1: the Resolver's synchronous call)")
+    ap.add_argument("--hold-steps", type=int, default=16,
+                    help="batches queued behind a hold kernel, then released (device-bound rate)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="bound on the CPU replay (parity + cpu_baseline); batches past it are not checked")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU replay (no parity, no baseline)")
@@ -185,6 +200,33 @@ def make_batches(args, p, n_batches, world, start_version, seed_offset=0):
     return out
 
 
+def directory_share(kb, ko, batches):
+    """Share of the read lookups whose first two key bytes fall in a sparse slot (<= 16 level-0
+    samples) of the base tier's radix directory, estimated on the prefilled history: those start
+    at level 0 (roofline.lookup_bytes)."""
+    n = len(ko) - 1
+    if n < 64:
+        return 0.0
+
+    def slot(bytes_, offs, idx):
+        a = offs[idx]
+        ln = offs[idx + 1] - a
+        b0 = np.where(ln > 0, bytes_[np.minimum(a, len(bytes_) - 1)], 0).astype(np.int64)
+        b1 = np.where(ln > 1, bytes_[np.minimum(a + 1, len(bytes_) - 1)], 0).astype(np.int64)
+        return b0 * 256 + b1
+
+    counts = np.bincount(slot(kb, ko, np.arange(0, n, 64)), minlength=65536)
+    hits = tot = 0
+    for b in batches[:4]:
+        nk = 2 * b.n_reads
+        if nk == 0:
+            continue
+        sl = slot(b.key_bytes, b.key_offsets, np.arange(nk))
+        hits += int((counts[sl] <= 16).sum())
+        tot += nk
+    return hits / tot if tot else 0.0
+
+
 def cpu_model():
     cpu = platform.processor() or platform.machine()
     try:
@@ -215,17 +257,24 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
     checked = mismatches = txn_mismatch = 0
     spent = 0.0
     done_txn = done_batches = 0
+    done_global = 0
+    phases = {k: 0.0 for k in oracle.SkipListBaseline.PHASES}
     first_bad = None
     t_begin = time.time()
     for i, b in enumerate(mine):
         _, now, no = gbatches[i]
         t = time.perf_counter()
-        v, _ = sl.detect(b, now, no)
+        # the reference's removeBefore: bounded to 3|combined|+10 nodes, resumed at removalKey
+        # (SkipList.cpp:880-889); verdict-neutral, so parity holds against the GPU's full GC
+        v, _ = sl.detect(b, now, no, gc="bounded")
         dt = time.perf_counter() - t
         if i in timed:
             spent += dt
             done_txn += b.n_txn
+            done_global += gbatches[i][0].n_txn
             done_batches += 1
+            for k, x in sl.last_times().items():
+                phases[k] += x
         g = gpu_verdicts[i]
         if g is not None:
             checked += 1
@@ -248,15 +297,22 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
         "mismatched_txns": txn_mismatch,
         "first_mismatch": first_bad,
     }
+    names = {"add": "Add", "sort": "D.Sort", "check_read": "D.CheckRead", "intra": "D.CheckIntraBatch",
+             "combine": "D.Combine", "merge": "D.MergeWrite", "remove_before": "D.RemoveBefore", "total": "Detect"}
     base = {
         "value": done_txn / spent if spent > 0 else None,
         "unit": "txns/s",
         "cores": 1,
         "kind": "port",
         "label": "reference algorithm, restated (oracle/skiplist_baseline.cpp)",
+        "gc": "bounded removeBefore (3*|combined|+10 nodes from removalKey, SkipList.cpp:880-889)",
+        "phase_ms_per_batch": {names[k]: 1e3 * x / max(1, done_batches) for k, x in phases.items()},
         "sample": f"{done_batches} timed {args.workload.upper()} batches (after replaying the warmup batches) on a "
-        f"{len(vers)}-boundary history ({spent:.1f}s CPU, history load {load_s:.1f}s), 1 thread pinned to one core "
-        f"of {cpu_model()} (nproc {os.cpu_count()})",
+        f"{len(vers)}-boundary history ({spent:.1f}s CPU, history load {load_s:.1f}s), bounded removeBefore, "
+        f"1 thread pinned to one core of {cpu_model()} (nproc {os.cpu_count()})",
+        "_spent": spent,
+        "_global_txns": done_global,
+        "_batches": done_batches,
     }
     return parity, base
 
@@ -290,10 +346,16 @@ def main():
     t0 = time.time()
     kb, ko, vers = shard_history(args, p, args.seed, rank, world, start_version)
     n_total = args.steps if args.total_steps < 0 else args.total_steps
-    timed_lo, timed_hi = args.warmup, args.warmup + args.steps
-    res_lo, res_hi = timed_hi, timed_hi + args.resident_steps
-    total_lo, total_hi = res_hi, res_hi + n_total
-    n_all = total_hi + args.breakdown_steps
+    # batch index ranges of the passes, in order
+    spans = {}
+    at = 0
+    for name, n in (("warmup", args.warmup), ("profile", args.profile_steps), ("timed", args.steps),
+                    ("resident", args.resident_steps), ("total", n_total), ("sync", args.sync_steps),
+                    ("hold", args.hold_steps), ("breakdown", args.breakdown_steps)):
+        spans[name] = (at, at + n)
+        at += n
+    n_all = at
+    timed_lo, timed_hi = spans["timed"]
     gbatches = make_batches(args, p, n_all, world, start_version)
     all_routed, reshard = route_all(args, p, world, gbatches)
     routed = [r[rank] for r in all_routed] if all_routed else None
@@ -305,7 +367,6 @@ def main():
     cs = C.ConflictSet(device)
     cs.set_gc_interval(args.gc_interval)
     cs.set_delta_limit(args.delta_limit)
-    cs.set_timing(args.timing)
     if len(vers):
         cs.load_history(kb, ko, vers, 0)
     mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
@@ -346,16 +407,19 @@ def main():
 
     host = {"add": 0.0, "submit": 0.0, "wait": 0.0}
 
-    def run(lo, hi, objs):
+    def run(lo, hi, objs, window=WINDOW, lat=None):
         """Submit batches lo..hi-1 (objs: packed ConflictBatch objects, or None: pack inside the
-        loop), keeping at most WINDOW in flight; upload (H2D), kernels and verdicts each time."""
+        loop), keeping at most `window` in flight; upload (H2D), kernels and verdicts each time.
+        lat: per-batch submit-to-verdicts seconds are appended (window 1: the synchronous call)."""
         inflight = []
         pc = time.perf_counter
 
-        def retire(j, oj):
+        def retire(j, oj, t_sub):
             t = pc()
             verdicts[j] = oj.wait()
             host["wait"] += pc() - t
+            if lat is not None:
+                lat.append(pc() - t_sub)
             if dist is not None:
                 combine(j, verdicts[j])
             oj.close()
@@ -373,11 +437,11 @@ def main():
             o.detect_async(now, no)
             host["add"] += t1 - t
             host["submit"] += pc() - t1
-            inflight.append((i, o))
-            if len(inflight) > WINDOW:
+            inflight.append((i, o, t1))
+            if len(inflight) >= window:
                 retire(*inflight.pop(0))
-        for j, oj in inflight:
-            retire(j, oj)
+        for j, oj, ts in inflight:
+            retire(j, oj, ts)
 
     def packed(lo, hi):
         objs = {}
@@ -401,7 +465,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    run(0, timed_lo, packed(0, timed_lo))
+    def pass_txns(name):
+        lo, hi = spans[name]
+        return sum(gbatches[i][0].n_txn for i in range(lo, hi))
+
+    run(*spans["warmup"], packed(*spans["warmup"]))
+
+    # per-kernel profile: events around every kernel of every batch (timing level 3), pipelined as
+    # in the timed region; the dominant kernel (largest device time) is then timed in the timed
+    # region itself (level 1, 1 batch in 4, on the stream it runs on)
+    kprof = {}
+    dominant = None
+    if args.profile_steps > 0:
+        cs.reset_stats()
+        cs.set_timing(3)
+        run(*spans["profile"], packed(*spans["profile"]))
+        kprof = cs.kernel_profile()
+        st_prof = cs.stats()
+        dominant = max(kprof, key=lambda k: kprof[k]["ms"]) if kprof else None
+    cs.set_timing(args.timing)
+    if dominant and args.timing >= 1:
+        cs.set_timed_kernel(dominant)
+
     objs = packed(timed_lo, timed_hi)
     cs.reset_stats()
     barrier()
@@ -412,19 +497,21 @@ def main():
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t_start)
     st = cs.stats()
+    kprof_timed = cs.kernel_profile()
     host_timed = {k: v / args.steps * 1e3 for k, v in host.items()}
     for k in ("host_ms_prepare", "host_ms_record", "host_ms_submit"):  # inside detect_async (engine's clock)
         host_timed["engine_" + k[8:]] = st[k] / max(1, st["batches"])
-    host_timed["graph_launches"] = st["graph_launches"]
+    cs.set_timed_kernel(None)
+    cs.set_timing(0)
 
     resident_elapsed = None
     if args.resident_steps > 0:  # diagnostic: batches uploaded before the timed region
-        objs = packed(res_lo, res_hi)
+        objs = packed(*spans["resident"])
         for o in objs.values():
             o.upload()
         barrier()
         t_start = time.perf_counter()
-        run(res_lo, res_hi, objs)
+        run(*spans["resident"], objs)
         barrier()
         resident_elapsed = max_over_ranks(time.perf_counter() - t_start)
 
@@ -432,9 +519,48 @@ def main():
     if n_total > 0:  # the reference's "total": addTransaction inside the loop as well
         barrier()
         t_start = time.perf_counter()
-        run(total_lo, total_hi, None)
+        run(*spans["total"], None)
         barrier()
         total_elapsed = max_over_ranks(time.perf_counter() - t_start)
+
+    sync = None
+    if args.sync_steps > 0:
+        # one batch at a time, as the Resolver calls detectConflicts (Resolver.actor.cpp:179-194): the
+        # batch is added beforehand, then detect (H2D, kernels, verdicts back) and wait back to back
+        lat = []
+        objs = packed(*spans["sync"])
+        barrier()
+        t_start = time.perf_counter()
+        run(*spans["sync"], objs, window=1, lat=lat)
+        barrier()
+        sync_elapsed = max_over_ranks(time.perf_counter() - t_start)
+        lat_ms = np.array(lat) * 1e3
+        sync = {"txns_per_s": pass_txns("sync") / sync_elapsed,
+                "latency_ms_p50": float(np.percentile(lat_ms, 50)),
+                "latency_ms_p99": float(np.percentile(lat_ms, 99)),
+                "latency_ms_mean": float(lat_ms.mean()), "batches": len(lat)}
+
+    device_bound = None
+    if args.hold_steps > 0 and dist is None:
+        # every stream held, the batches submitted behind the hold, then released: the device runs
+        # them back to back at its own rate, whatever the submitting thread's cost
+        objs = packed(*spans["hold"])
+        for o in objs.values():
+            o.upload()
+        torch.cuda.synchronize()
+        cs.debug_hold(True)
+        lo, hi = spans["hold"]
+        for i in range(lo, hi):
+            _, now, no = gbatches[i]
+            objs[i].detect_async(now, no)
+        t_start = time.perf_counter()
+        cs.debug_hold(False)
+        for i in range(lo, hi):
+            verdicts[i] = objs[i].wait()
+            objs[i].close()
+        dev_elapsed = time.perf_counter() - t_start
+        device_bound = {"txns_per_s": pass_txns("hold") / dev_elapsed, "ms_per_batch": dev_elapsed / (hi - lo) * 1e3,
+                        "batches": hi - lo}
 
     # diagnostic phase split: extra batches with every phase timed (each event costs queue time,
     # so these are outside the timed region)
@@ -442,7 +568,7 @@ def main():
     if args.breakdown_steps > 0:
         cs.set_timing(2)
         cs.reset_stats()
-        run(total_hi, n_all, packed(total_hi, n_all))
+        run(*spans["breakdown"], packed(*spans["breakdown"]))
         torch.cuda.synchronize()
         sb = cs.stats()
         phase = {
@@ -455,55 +581,37 @@ def main():
         phase["intra_edges"] = sb["intra_edges"] / max(1, sb["batches"] - sb["intra_fallbacks"])
         phase["intra_rounds"] = sb["intra_rounds"] / max(1, sb["batches"] - sb["intra_fallbacks"])
         phase["intra_fallbacks"] = sb["intra_fallbacks"]
-    gtxn = sum(gbatches[i][0].n_txn for i in range(timed_lo, timed_hi))
+    gtxn = pass_txns("timed")
     granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(timed_lo, timed_hi))
-    ttxn = sum(gbatches[i][0].n_txn for i in range(total_lo, total_hi))
+    ttxn = pass_txns("total")
     hist_end = cs.history_size()
     cs.close()
 
-    # roofline: the hot kernel with the largest device time in the timed region (HIP events on the
-    # stream each kernel runs on), algorithmic bytes from the §8(d) model (roofline.py)
-    kern = roofline.kernels_from_stats(st) if args.timing >= 1 else {}
-    dom = roofline.dominant(kern)
-    # the rocprof-dominant kernel of this workload (scripts/prof_summary.py --dominant over the
-    # committed profile) wins over the event totals, which inflate stage-A kernels a little
-    dom_file = os.path.join(ROOT, "profiles", f"dominant_{args.workload}.json")
-    if os.path.exists(dom_file):
-        try:
-            with open(dom_file) as f:
-                d = json.load(f).get("dominant")
-            if d in kern:
-                dom = d
-        except Exception:
-            pass
-    def roof_block(name):
-        k = kern[name]
-        traffic = None
-        # PMC HBM bytes per launch of the same kernel on the same command (FETCH_SIZE x2 gfx950
-        # correction + WRITE_SIZE, separate rocprofv3 passes: scripts/gpu_pmc.sh)
-        pmc = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
-        if os.path.exists(pmc):
-            try:
-                with open(pmc) as f:
-                    traffic = json.load(f).get(f"{name}_bytes_per_launch")
-            except Exception:
-                traffic = None
-        return {
-            "kernel": k["kernel"],
+    # Roofline.  The per-kernel table comes from the profile pass (events around every kernel);
+    # the dominant kernel's line from the timed region's own events (fdbcs_set_timed_kernel).
+    # Algorithmic bytes per launch: roofline.py (SURVEY §8(d) model per kernel, batch shapes of
+    # this run).
+    shape = roofline.shape_of(mine[timed_lo:timed_hi], st_prof if args.profile_steps > 0 else st, len(vers),
+                              dir_share=directory_share(kb, ko, mine[timed_lo:timed_hi]))
+    table = roofline.kernel_table(kprof, shape, st_prof if args.profile_steps > 0 else None)
+    roof = None
+    if dominant and dominant in kprof_timed:
+        k = kprof_timed[dominant]
+        ent = roofline.entry(dominant, k["ms"], k["launches"], shape, st)
+        roof = {
+            "kernel": dominant,
             "bound": "hbm",
-            "achieved": k["achieved_GBps"],
+            "achieved": ent["achieved_GBps"],
             "peak": roofline.HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": k["frac"],
-            "traffic": traffic,
-            "avg_launch_ms": k["avg_launch_ms"],
-            "algorithmic_bytes_per_launch": k["algorithmic_bytes_per_launch"],
+            "frac": ent["frac"],
+            "traffic": roofline.pmc_traffic(ROOT, args.workload, dominant, p.txns, p.history),
+            "avg_launch_ms": ent["avg_launch_ms"],
+            "launches_timed": k["launches"],
+            "algorithmic_bytes_per_launch": ent["algorithmic_bytes_per_launch"],
+            "model": ent["model"],
+            "profile_avg_launch_ms": table.get(dominant, {}).get("avg_launch_ms"),
         }
-
-    roof = roof_block(dom) if dom is not None else None
-    # north_star's roofline target is on the search / merge kernels: when the dominant kernel is
-    # another one (the LDS-bound bucket sort), the read check's block rides along
-    roof_search = roof_block("check") if dom not in (None, "check") and "check" in kern else None
 
     combine_check = None
     if dist is not None:
@@ -527,6 +635,16 @@ def main():
             parity["batches_checked"], parity["mismatched_batches"], parity["mismatched_txns"] = (
                 int(x) for x in t.tolist())
             parity["scope"] = f"{world} ranks, each against its own restatement fed the same routing"
+            # G resolvers on G cores: every rank replayed its routed sub-batches on its own pinned
+            # core at the same time; the global batches' transactions over the slowest rank's time
+            spent = max_over_ranks(cpu_base["_spent"])
+            cpu_base["value"] = cpu_base["_global_txns"] / spent if spent > 0 else None
+            cpu_base["cores"] = world
+            cpu_base["sample"] = (f"{cpu_base['_batches']} timed global batches, each rank replaying its routed "
+                                  f"sub-batches on its own pinned core ({world} cores at once), slowest rank "
+                                  f"{spent:.1f}s; " + cpu_base["sample"].split(", ", 1)[1])
+        for k in ("_spent", "_global_txns", "_batches"):
+            cpu_base.pop(k, None)
 
     cfg_desc = {
         "c1": "skipListTest (SkipList.cpp:1023-1077): 1R+1W per txn, setK 16-byte keys over [0, 2e7), empty initial "
@@ -536,6 +654,15 @@ def main():
         "c4": "1 wide Tuple.range() read + 4 point reads + 2 point writes per txn, tuple keys (subspace, user string, "
         "int) up to 100 B",
     }[args.workload]
+    dist_info = None
+    if dist is not None:
+        rccl = None
+        try:
+            rccl = ".".join(str(x) for x in torch.cuda.nccl.version())
+        except Exception:
+            pass
+        dist_info = {"world_size": world, "backend": args.backend, "rccl_version": rccl,
+                     "routing": "host KeyRangeSharding.route before the timed region"}
     out = {
         "metric": "resolved txns/sec (conflict ranges checked/sec) per batch; HBM GB/s vs peak",
         "value": gtxn / elapsed,
@@ -561,25 +688,25 @@ def main():
         },
         "conflict_ranges_per_s": granges / elapsed,
         "total_txns_per_s": ttxn / total_elapsed if total_elapsed else None,
-        "device_resident_txns_per_s": (sum(gbatches[i][0].n_txn for i in range(res_lo, res_hi)) / resident_elapsed
-                                       if resident_elapsed else None),
+        "device_resident_txns_per_s": pass_txns("resident") / resident_elapsed if resident_elapsed else None,
+        "sync": sync,
+        "sync_txns_per_s": sync["txns_per_s"] if sync else None,
+        "device_bound": device_bound,
         "host_ms_per_batch": host_timed,
         "total_note": "reference 'total' (SkipList.cpp:1082-1085): addTransaction + detect, per batch in the loop",
         "parity": parity,
         "combine_check": combine_check,
+        "distributed": dist_info,
         "reshard": reshard,
         "history_boundaries_end": hist_end,
         "phase_ms_per_batch": phase,
         "compactions": st["compactions"],
-        "kernels": kern,
+        "kernels": table,
+        "sort_phase": roofline.sort_phase(table),
         "roofline": roof,
-        "roofline_search": roof_search,
     }
-    if rank == 0 and world == 1:
-        out["cpu_baseline"] = cpu_base
-    elif rank == 0:
-        out["cpu_baseline"] = None
     if rank == 0:
+        out["cpu_baseline"] = cpu_base
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -83,6 +83,12 @@ class Stats(ctypes.Structure):
         ("host_ms_record", ctypes.c_double),
         ("host_ms_submit", ctypes.c_double),
         ("graph_launches", ctypes.c_int64),
+        ("compact_launches", ctypes.c_int64),
+        ("merge_bytes_all", ctypes.c_int64),
+        ("compact_bytes_all", ctypes.c_int64),
+        ("delta_sum", ctypes.c_int64),
+        ("base_sum", ctypes.c_int64),
+        ("segments_sum", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -124,6 +130,10 @@ SIGNATURES = {
     "fdbcs_batch_device_verdicts": (ctypes.c_int, [_VP, ctypes.POINTER(_VP)]),
     "fdbcs_batch_set_conflict_output": (ctypes.c_int, [_VP, _VP, ctypes.c_int32, _VP]),
     "fdbcs_debug_kernel_time": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    "fdbcs_kernel_profile": (ctypes.c_int, [_VP, _I32, ctypes.c_char_p, _I32, ctypes.POINTER(_I64),
+                                            ctypes.POINTER(ctypes.c_double)]),
+    "fdbcs_set_timed_kernel": (ctypes.c_int, [_VP, ctypes.c_char_p]),
+    "fdbcs_debug_hold": (ctypes.c_int, [_VP, _I32]),
     "fdbcs_strerror": (ctypes.c_char_p, [ctypes.c_int]),
 }
 
@@ -205,8 +215,29 @@ class ConflictSet:
         _check(load_library().fdbcs_set_gc_interval(self._h, every), "setGcInterval")
 
     def set_timing(self, level: int) -> None:
-        """Device timing: 0 none, 1 copy kernels (roofline), 2 every phase (stats())."""
+        """Device timing: 0 none, 1 the hot kernels on sampled batches (roofline), 2 every phase
+        (stats()), 3 every kernel of every batch (kernel_profile())."""
         _check(load_library().fdbcs_set_timing(self._h, level), "setTiming")
+
+    def kernel_profile(self) -> Dict[str, dict]:
+        """Per-kernel launches and device milliseconds since reset_stats (timing levels 3 and 1)."""
+        L = load_library()
+        out = {}
+        i = 0
+        name = ctypes.create_string_buffer(512)
+        n, ms = ctypes.c_int64(), ctypes.c_double()
+        while L.fdbcs_kernel_profile(self._h, i, name, len(name), ctypes.byref(n), ctypes.byref(ms)) == FDBCS_OK:
+            out[name.value.decode()] = {"launches": n.value, "ms": ms.value}
+            i += 1
+        return out
+
+    def set_timed_kernel(self, name: Optional[str]) -> None:
+        """The kernel timed on sampled batches at timing level 1 (a name kernel_profile() reported)."""
+        _check(load_library().fdbcs_set_timed_kernel(self._h, (name or "").encode()), "setTimedKernel")
+
+    def debug_hold(self, on: bool) -> None:
+        """Diagnostics: hold every stream (on) so batches submitted next queue up; release (off)."""
+        _check(load_library().fdbcs_debug_hold(self._h, 1 if on else 0), "debugHold")
 
     def set_delta_limit(self, boundaries: int) -> None:
         """Delta-tier bound that triggers a compaction; 0 = automatic (~1/16 of the base)."""

@@ -11,12 +11,15 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cxxabi.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <new>
+#include <string>
 #include <thread>
 #include <unordered_set>
 #include <vector>
@@ -116,7 +119,6 @@ struct fdbcs_conflict_set {
     int device = 0;
     hipStream_t stream = nullptr;   // stage B: everything that reads or writes the history, in batch order
     hipStream_t astream = nullptr;  // stage A (and every upload): history-independent sort and edges
-    hipStream_t astream2 = nullptr; // stage A of odd batches when FDBCS_ASTREAMS=2
     hipStream_t cstream = nullptr;  // split read check: the base-tier half (history-independent between
                                     // compactions) beside stage A
     hipEvent_t ev_c[kNumWork] = {}; // base-tier check of the batch using workspace k is done
@@ -134,7 +136,6 @@ struct fdbcs_conflict_set {
     hipEvent_t ev_b[kNumWork] = {}; // stage B (epilogue) of the batch using workspace k is done
     bool wused[kNumWork] = {};
     int wpar = 0;                   // workspace of the next batch
-    int apar = 0;                   // stage-A stream of the next batch
     int timing = 0;       // 0: no events; 1: the copy kernels; 2: every phase (fdbcs_set_timing)
     uint32_t seq = 0;     // batches submitted (completion flag values)
     int64_t oldest = 0;          // ConflictSet::oldestVersion (SkipList.cpp:736)
@@ -183,43 +184,29 @@ struct fdbcs_conflict_set {
     bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)
-    int astreams = 1;         // FDBCS_ASTREAMS: stage-A streams (1, or 2 to alternate batches; same
-                              // C3 throughput, and C2 measured 36.2M vs 35.1M txns/s mean with 1)
-    int sort_alg = 0;       // FDBCS_SORT_ALG: per-bucket sort (0 rank count, 1 bitonic network)
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
-    // Batch upload on the upload stream by the DMA engine (hipMemcpyAsync from the pinned staging
-    // buffer, default) or by the k_upload kernel reading host-mapped memory (FDBCS_UPLOAD=kernel).
-    // With the stages on their own streams the DMA copy overlaps the kernels completely: C2 34.1M
-    // vs 30.0M txns/s with the kernel, whose workgroups stall on PCIe reads beside stage A/B.
-    bool dma_upload = true;
-    int upload_blocks = 32;   // FDBCS_UPLOAD_BLOCKS: workgroups of the k_upload kernel
-    int check_version = 6;    // FDBCS_CHECK: read-check kernel (1 four lookups per read; 2-5 LDS-staged variants;
-                              // 6 as 1 with the base and delta lookups in separate waves)
-    int check_grid = 2048;    // FDBCS_CHECK_GRID: workgroups of the version-2 read check (cap)
+    int check_version = 6;    // FDBCS_CHECK: read-check kernel (1: the four lookups of a read in one wave;
+                              // 6: the base and delta lookups in separate waves)
     bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
-    bool sorted_reads = false; // FDBCS_SORTED_READS=1: the split check waits for stage A and takes reads
-                               // in sorted begin-key order (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
     bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
                               // even for batches with keys over 16 bytes (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
-    // FDBCS_FUSE_EPILOGUE=1: the merge copy of a batch without compaction also does the epilogue
-    // (index, levels, scratch, publication) and k_epilogue is not launched.  Measured slower at
-    // C2 (27.5M vs 30.1M txns/s): level 1 by atomics and levels 2-3 rebuilt by one last workgroup
-    // through device-scope loads cost more than the launch they save.  Off by default.
-    bool fuse_epilogue = false;
     bool directory = true;  // FDBCS_DIRECTORY=0: base-tier lookups descend the whole sample tree (A/B)
     DBuf trace_buf;
+    // Per-kernel device time (fdbcs_kernel_profile): launches and milliseconds by kernel, from the
+    // events of timing level 3 (every kernel) or of the timed kernel at level 1.
+    struct KProf {
+        const void* func;
+        int64_t launches;
+        double ms;
+    };
+    std::vector<KProf> kprof;
+    const void* timed_func = nullptr;  // fdbcs_set_timed_kernel
+    HBuf hold;                         // fdbcs_debug_hold: host-mapped release word of the hold kernels
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
-    // Graph mode (FDBCS_GRAPH=1; off by default): every detect launches ONE cached hipGraph holding
-    // stage A of this batch beside stage B of the previous batch (two independent branches on one
-    // stream); this batch's stage B waits here for the next launch or for a wait/flush.  Measured
-    // slower than direct launches at C2 (24.6M vs 27.2M txns/s): the kernels take 200-700-byte
-    // argument structs, and a node parameter update costs 0.76 us at 640 bytes
-    // (tools/graphbench.hip), so updating ~30 nodes costs as much host time as launching them.
-    bool use_graph = false;
     // FDBCS_GRAPH=2: stage graphs.  The launches of each stage (A on its stream, B on the batch-order
     // stream) go out as one cached hipGraph per stage shape on the stage's own stream, with the
     // cross-stream event waits and records around it issued directly, so the stages still overlap
@@ -251,12 +238,6 @@ struct fdbcs_conflict_set {
     uint32_t work_need_b = 0;           // the check goes out once b_issued >= this
     LaunchList rec_a, rec_b, rec_c, pending_b;
     fdbcs_batch* pending_batch = nullptr;
-    struct GraphEntry {
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t exec = nullptr;
-        std::vector<hipGraphNode_t> nodes_a, nodes_b;
-    };
-    std::vector<std::pair<std::pair<uint64_t, uint64_t>, GraphEntry>> graphs;
     int64_t graph_launches = 0;
     std::unordered_set<fdbcs_batch*> live;  // batches not yet destroyed (detached if the set goes first)
 };
@@ -276,6 +257,11 @@ struct BatchSlot {
     hipEvent_t ev_free = nullptr;  // the last batch using this slot finished on the device
     bool free_recorded = false;
     HBuf pin_inv;  // fdbcs_batch_set_conflict_output: global -> batch transaction map (host-mapped)
+    // per-kernel events of the batch (timing level 3, or the timed kernel at level 1)
+    std::vector<hipEvent_t> prof_pool;
+    size_t prof_next = 0;
+    std::vector<std::pair<const void*, std::pair<hipEvent_t, hipEvent_t>>> prof_spans;
+    LaunchList::Profile prof{&prof_pool, &prof_next, &prof_spans};
 };
 
 struct fdbcs_batch {
@@ -374,7 +360,6 @@ int sync_all(fdbcs_conflict_set* cs) {
     HIPOK(hipStreamSynchronize(cs->ustream));
     HIPOK(hipStreamSynchronize(cs->cstream));
     HIPOK(hipStreamSynchronize(cs->astream));
-    if (cs->astream2) HIPOK(hipStreamSynchronize(cs->astream2));
     HIPOK(hipStreamSynchronize(cs->stream));
     return FDBCS_OK;
 }
@@ -662,6 +647,7 @@ void release_slot(BatchSlot* sl) {
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
     if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
+    for (hipEvent_t e : sl->prof_pool) (void)hipEventDestroy(e);
     sl->dev.release();
     sl->dverdict.release();
     sl->pin_in.release();
@@ -766,8 +752,9 @@ void materialize(fdbcs_batch* b) {
     b->direct = false;
 }
 
-// own_stream: launch now on the upload stream (not recorded); else record onto stage A's stream.
-int do_upload(fdbcs_batch* b, bool own_stream) {
+// H2D of the packed batch by the DMA engine, issued now on `us` (the upload stream, or stage A's
+// stream when the phases are timed one after another); ev_up marks its completion.
+int do_upload(fdbcs_batch* b, hipStream_t us) {
     fdbcs_conflict_set* cs = b->cs;
     BatchSlot* sl = b->slot;
     const size_t T = b->T(), R = b->R(), W = b->W();
@@ -787,25 +774,13 @@ int do_upload(fdbcs_batch* b, bool own_stream) {
     memcpy(h + L.roff, b->roff.data(), 4 * (T + 1));
     memcpy(h + L.woff, b->woff.data(), 4 * (T + 1));
     if (T) memcpy(h + L.flags, b->flags.data(), T);
-    // On the upload stream, issued now (own_stream), or recorded into stage A (graph mode, phase
-    // timing); both stages wait for ev_up.  A reused slot's device copy may still be read by the
-    // epilogue of the batch that used it last.
+    // Both stages wait for ev_up.  A reused slot's device copy may still be read by the epilogue
+    // of the batch that used it last.
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
-    LaunchList* const saved = t_record;
-    if (own_stream) t_record = nullptr;
-    hipStream_t us = own_stream ? cs->ustream : cs->astream;
-    int urc = FDBCS_OK;
-    if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess)
-        fdb_event(LaunchList::kSyncWait, sl->ev_free, us);
-    if (cs->dma_upload && !t_record) {
-        if (hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us) != hipSuccess) urc = FDBCS_E_DEVICE;
-    } else {
-        launch_upload(us, sl->pin_in.dp, sl->dev.p, (int64_t)L.total, cs->upload_blocks);
-        if (!t_record && take_launch_error() != hipSuccess) urc = FDBCS_E_DEVICE;
-    }
-    fdb_event(LaunchList::kSyncRecord, sl->ev_up, us);
-    t_record = saved;
-    if (urc) return urc;
+    (void)cs;
+    if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
+    HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us));
+    HIPOK(hipEventRecord(sl->ev_up, us));
     char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
     b->bd.R = (int32_t)R;
@@ -820,78 +795,6 @@ int do_upload(fdbcs_batch* b, bool own_stream) {
     b->bd.tail = (uint8_t*)(d + L.tail);
     b->tail_bytes = b->tail_size();
     b->state = 1;
-    return FDBCS_OK;
-}
-
-// ---- graph mode
-//
-// A graph node per kernel and per timing event of stage A (one chain) and stage B (another chain,
-// no edge between them), built once per pair of stage shapes (LaunchList::signature) and reused:
-// per batch only the node parameters change (hipGraphExecKernelNodeSetParams, ~0.1 us each).
-
-int add_chain(hipGraph_t g, LaunchList& L, std::vector<hipGraphNode_t>& nodes) {
-    L.finalize();
-    hipGraphNode_t prev = nullptr;
-    for (const LaunchList::Rec& r : L.recs) {
-        hipGraphNode_t n = nullptr;
-        if (r.kind == LaunchList::kKernel) {
-            hipKernelNodeParams p{};
-            p.func = const_cast<void*>(r.func);
-            p.gridDim = r.grid;
-            p.blockDim = r.block;
-            p.sharedMemBytes = r.shmem;
-            p.kernelParams = L.argp.data() + r.arg0;
-            HIPOK(hipGraphAddKernelNode(&n, g, prev ? &prev : nullptr, prev ? 1 : 0, &p));
-        } else if (r.kind == LaunchList::kTimingRecord) {
-            HIPOK(hipGraphAddEventRecordNode(&n, g, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
-        } else {
-            continue;  // cross-stream ordering: implicit in one graph on one stream
-        }
-        nodes.push_back(n);
-        prev = n;
-    }
-    return FDBCS_OK;
-}
-
-int set_chain(hipGraphExec_t ex, LaunchList& L, const std::vector<hipGraphNode_t>& nodes) {
-    L.finalize();
-    size_t k = 0;
-    for (const LaunchList::Rec& r : L.recs) {
-        if (r.kind == LaunchList::kKernel) {
-            hipKernelNodeParams p{};
-            p.func = const_cast<void*>(r.func);
-            p.gridDim = r.grid;
-            p.blockDim = r.block;
-            p.sharedMemBytes = r.shmem;
-            p.kernelParams = L.argp.data() + r.arg0;
-            HIPOK(hipGraphExecKernelNodeSetParams(ex, nodes[k++], &p));
-        } else if (r.kind == LaunchList::kTimingRecord) {
-            HIPOK(hipGraphExecEventRecordNodeSetEvent(ex, nodes[k++], r.event));
-        }
-    }
-    return FDBCS_OK;
-}
-
-// Launch stage lists A and B (either may be empty) as one graph on the set's stream.
-int launch_graph(fdbcs_conflict_set* cs, LaunchList& A, LaunchList& B) {
-    const std::pair<uint64_t, uint64_t> key{A.recs.empty() ? 0 : A.signature(), B.recs.empty() ? 0 : B.signature()};
-    fdbcs_conflict_set::GraphEntry* ge = nullptr;
-    for (auto& kv : cs->graphs)
-        if (kv.first == key) ge = &kv.second;
-    if (!ge) {
-        fdbcs_conflict_set::GraphEntry e;
-        HIPOK(hipGraphCreate(&e.graph, 0));
-        int rc;
-        if ((rc = add_chain(e.graph, A, e.nodes_a)) || (rc = add_chain(e.graph, B, e.nodes_b))) return rc;
-        HIPOK(hipGraphInstantiate(&e.exec, e.graph, nullptr, nullptr, 0));
-        cs->graphs.push_back({key, e});
-        ge = &cs->graphs.back().second;
-    } else {
-        int rc;
-        if ((rc = set_chain(ge->exec, A, ge->nodes_a)) || (rc = set_chain(ge->exec, B, ge->nodes_b))) return rc;
-    }
-    HIPOK(hipGraphLaunch(ge->exec, cs->stream));
-    cs->graph_launches++;
     return FDBCS_OK;
 }
 
@@ -1029,13 +932,8 @@ int flush_pending(fdbcs_conflict_set* cs) {
     if (!cs->pending_batch) return FDBCS_OK;
     cs->pending_batch = nullptr;
     int rc = FDBCS_OK;
-    if (cs->submit_thread) {
-        if (cs->pending_b.replay(cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
-        cs->b_issued.fetch_add(1, std::memory_order_release);
-    } else {
-        LaunchList none;
-        rc = launch_graph(cs, none, cs->pending_b);
-    }
+    if (cs->pending_b.replay(cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
+    cs->b_issued.fetch_add(1, std::memory_order_release);
     cs->pending_b.clear();
     return rc;
 }
@@ -1079,26 +977,16 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_TRACE")) cs->trace = v[0] == '1';
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
-    if (const char* v = getenv("FDBCS_ASTREAMS")) cs->astreams = atoi(v) == 1 ? 1 : 2;
-    if (const char* v = getenv("FDBCS_SORT_ALG")) cs->sort_alg = atoi(v);
-    if (const char* v = getenv("FDBCS_UPLOAD")) cs->dma_upload = strcmp(v, "kernel") != 0;
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
-    if (const char* v = getenv("FDBCS_GRAPH")) {
-        cs->use_graph = v[0] == '1';
-        cs->stage_graphs = v[0] == '2';
-    }
+    if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2';
     if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
-    if (const char* v = getenv("FDBCS_SORTED_READS")) cs->sorted_reads = v[0] != '0';
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
-    if (const char* v = getenv("FDBCS_FUSE_EPILOGUE")) cs->fuse_epilogue = v[0] != '0';
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
-    if (const char* v = getenv("FDBCS_UPLOAD_BLOCKS")) cs->upload_blocks = std::max(1, atoi(v));
-    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = std::min(6, std::max(1, atoi(v)));
-    if (const char* v = getenv("FDBCS_CHECK_GRID")) cs->check_grid = std::max(1, atoi(v));
+    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : 6;
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     static std::once_flag attr_once;
     std::call_once(attr_once, init_kernel_attributes);
@@ -1106,8 +994,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->cstream, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess &&
-              (cs->astreams == 1 || hipStreamCreateWithFlags(&cs->astream2, hipStreamNonBlocking) == hipSuccess);
+              hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < kNumWork && ok; k++)
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_c[k], hipEventDisableTiming) == hipSuccess &&
@@ -1144,7 +1031,6 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (cs->ustream) (void)hipStreamSynchronize(cs->ustream);
     if (cs->cstream) (void)hipStreamSynchronize(cs->cstream);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
-    if (cs->astream2) (void)hipStreamSynchronize(cs->astream2);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
     for (int k = 0; k < 2; k++) {
         cs->hkey[k].release();
@@ -1165,13 +1051,9 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         for (auto& x : set) x.release();
     cs->scal.release();
     cs->trace_buf.release();
+    cs->hold.release();
     for (BatchSlot* sl : cs->pool) release_slot(sl);
     cs->pool.clear();
-    for (auto& kv : cs->graphs) {
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-        if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
-    }
-    cs->graphs.clear();
     for (auto& kv : cs->stage_cache) {
         if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
@@ -1190,7 +1072,6 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (cs->cstream) (void)hipStreamDestroy(cs->cstream);
     if (cs->ev_cmp) (void)hipEventDestroy(cs->ev_cmp);
     if (cs->astream) (void)hipStreamDestroy(cs->astream);
-    if (cs->astream2) (void)hipStreamDestroy(cs->astream2);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
     delete cs;
 }
@@ -1243,7 +1124,7 @@ int fdbcs_set_gc_interval(fdbcs_conflict_set* cs, int32_t every) {
 }
 
 int fdbcs_set_timing(fdbcs_conflict_set* cs, int32_t level) {
-    if (!cs || level < 0 || level > 2) return FDBCS_E_INVALID;
+    if (!cs || level < 0 || level > 3) return FDBCS_E_INVALID;
     cs->timing = level;
     return FDBCS_OK;
 }
@@ -1328,7 +1209,73 @@ int fdbcs_get_stats(fdbcs_conflict_set* cs, fdbcs_stats* out) {
 int fdbcs_reset_stats(fdbcs_conflict_set* cs) {
     if (!cs) return FDBCS_E_INVALID;
     memset(&cs->stats, 0, sizeof(cs->stats));
+    cs->kprof.clear();
     return FDBCS_OK;
+}
+
+// Demangled kernel name without its namespace and argument list ("k_scan<3, fdbcs::PosScan>").
+static std::string kernel_name(const void* func, hipStream_t s) {
+    const char* m = hipKernelNameRefByPtr(func, s);
+    if (!m) return "?";
+    int st = 0;
+    char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+    std::string n = (st == 0 && d) ? d : m;
+    free(d);
+    // drop the return type, namespace prefix and parameter list
+    if (n.rfind("void ", 0) == 0) n = n.substr(5);
+    int depth = 0;
+    for (size_t i = 0; i < n.size(); i++) {
+        if (n[i] == '<') depth++;
+        if (n[i] == '>') depth--;
+        if (n[i] == '(' && depth == 0) {
+            n = n.substr(0, i);
+            break;
+        }
+    }
+    if (n.rfind("fdbcs::", 0) == 0) n = n.substr(7);
+    return n;
+}
+
+int fdbcs_kernel_profile(fdbcs_conflict_set* cs, int32_t index, char* name, int32_t cap, int64_t* launches,
+                         double* ms) {
+    if (!cs || index < 0 || index >= (int32_t)cs->kprof.size()) return FDBCS_E_INVALID;
+    const auto& k = cs->kprof[index];
+    if (name && cap > 0) {
+        const std::string n = kernel_name(k.func, cs->stream);
+        snprintf(name, (size_t)cap, "%s", n.c_str());
+    }
+    if (launches) *launches = k.launches;
+    if (ms) *ms = k.ms;
+    return FDBCS_OK;
+}
+
+int fdbcs_debug_hold(fdbcs_conflict_set* cs, int32_t on) {
+    if (!cs) return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(cs->device));
+    if (int rc = cs->hold.ensure(64, true)) return rc;
+    volatile uint32_t* word = (volatile uint32_t*)cs->hold.p;
+    if (!on) {
+        __atomic_store_n((uint32_t*)word, 1u, __ATOMIC_SEQ_CST);
+        return FDBCS_OK;
+    }
+    if (int rc = sync_all(cs)) return rc;
+    *word = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    for (hipStream_t st : {cs->ustream, cs->astream, cs->cstream, cs->stream}) launch_hold(st, (const uint32_t*)cs->hold.dp);
+    HIPOK(take_launch_error());
+    return FDBCS_OK;
+}
+
+int fdbcs_set_timed_kernel(fdbcs_conflict_set* cs, const char* name) {
+    if (!cs) return FDBCS_E_INVALID;
+    cs->timed_func = nullptr;
+    if (!name || !name[0]) return FDBCS_OK;
+    for (const auto& k : cs->kprof)
+        if (kernel_name(k.func, cs->stream) == name) {
+            cs->timed_func = k.func;
+            return FDBCS_OK;
+        }
+    return FDBCS_E_INVALID;  // only kernels seen by a profiled batch can be named
 }
 
 int fdbcs_batch_new(fdbcs_conflict_set* cs, int report_keys, fdbcs_batch** out) {
@@ -1370,7 +1317,6 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
         (void)hipStreamSynchronize(b->cs->ustream);
         (void)hipStreamSynchronize(b->cs->cstream);
         (void)hipStreamSynchronize(b->cs->astream);
-        if (b->cs->astream2) (void)hipStreamSynchronize(b->cs->astream2);
         (void)hipStreamSynchronize(b->cs->stream);
         b->cs->inflight--;
     } else if (b->state == 1) {  // uploaded, never submitted: the copy may still be in flight
@@ -1571,7 +1517,7 @@ int fdbcs_batch_upload(fdbcs_batch* b) {
     if (!b->cs) return FDBCS_E_STATE;
     if (b->state != 0) return b->state == 1 ? FDBCS_OK : FDBCS_E_STATE;
     HIPOK(hipSetDevice(b->cs->device));
-    return do_upload(b, true);
+    return do_upload(b, b->cs->ustream);
 }
 
 static inline double host_ms_since(std::chrono::steady_clock::time_point t0) {
@@ -1599,6 +1545,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + tail_add + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
+    if (cs->ddir_counter == UINT32_MAX && cs->edir.p) {
+        // the delta directory's 32-bit epoch tag is about to wrap: clear every entry (once per 2^32
+        // batches) so that no entry left by an old fill can carry the reused epoch value
+        if ((rc = sync_all(cs))) return rc;
+        HIPOK(hipMemsetAsync(cs->edir.p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream));
+        HIPOK(hipStreamSynchronize(cs->stream));
+        cs->ddir_counter = 0;
+    }
     // results (host-mapped; verdicts written by k_resolve, scalars and flag by the epilogue):
     // verdicts | scalars | completion flag, then the
     // report copies rconf | hist | first_conf
@@ -1632,15 +1586,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
 
     hipStream_t s = cs->stream;
     const int timing = cs->timing;
-    // Graph mode: both stages become one graph launch (see launch_graph); phase timing, tracing and
-    // the serial / two-stream debugging modes submit directly.
-    const bool graph = cs->use_graph && timing < 2 && !cs->serial && !cs->trace && cs->astreams == 1 &&
-                       !cs->dma_upload;
     // Stage A (sort, positions, candidate edges) depends only on this batch: it runs on its own
     // stream and overlaps stage B of the previous batch.  Phase timing (level 2) runs both stages on
     // one stream so the phases are measured one after another.
-    hipStream_t sa = (timing >= 2 || cs->serial) ? s : (cs->apar ? cs->astream2 : cs->astream);
-    if (cs->astreams == 2) cs->apar ^= 1;
+    hipStream_t sa = (timing >= 2 || cs->serial) ? s : cs->astream;
     const int wp = cs->wpar;
     cs->wpar = (wp + 1) % kNumWork;
     b->wp = wp;
@@ -1651,8 +1600,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // level-1 (roofline) events on one batch in timing_every: each event record is a runtime call
     // on the submitting thread, and the per-launch averages need only a sample of the batches
     const bool sampled = timing >= 2 || cs->timing_every <= 1 || b->seq % (uint32_t)cs->timing_every == 0;
+    // level 3 (per-kernel profile) records only the events around every kernel
+    // level 1 with a timed kernel (fdbcs_set_timed_kernel) records only that kernel's events
     auto rec = [&](int ph, int level) -> hipEvent_t {
-        if (timing < level || (level == 1 && !sampled)) return nullptr;
+        if (timing == 3 || timing < level || (level == 1 && (!sampled || cs->timed_func))) return nullptr;
         b->recorded |= 1u << ph;
         return sl->ev[ph];
     };
@@ -1661,42 +1612,50 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         return FDBCS_OK;
     };
     const bool was_uploaded = b->state == 1;
-    if (graph && was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess)
-        HIPOK(hipStreamWaitEvent(s, sl->ev_up, 0));  // uploaded early (fdbcs_batch_upload) on stage A's stream
     LaunchList& la = cs->rec_a;
     LaunchList& lb = cs->rec_b;
     LaunchList& lc = cs->rec_c;
     la.clear();
     lb.clear();
     lc.clear();
+    // per-kernel events: every kernel at level 3, the kernel fdbcs_set_timed_kernel named at level 1
+    // (sampled batches)
+    sl->prof_next = 0;
+    sl->prof_spans.clear();
+    const bool kprof = timing == 3 || (timing == 1 && sampled && cs->timed_func);
+    for (LaunchList* L : {&la, &lb, &lc}) {
+        L->prof = kprof ? &sl->prof : nullptr;
+        L->timed_func = timing == 3 ? nullptr : cs->timed_func;
+    }
     // Split read check: the base tier changes only at compactions, so unless one is still pending
     // on the stream its half of D.CheckRead runs beside stage A on its own stream; stage B keeps the
-    // delta half.  One graph per batch cannot express the wait, so graph mode keeps one check.
-    const bool split = (cs->split_check == 1 || (cs->split_check == 2 && cs->n_ub >= kSplitCheckMinBase)) && !graph &&
+    // delta half.
+    const bool split = (cs->split_check == 1 || (cs->split_check == 2 && cs->n_ub >= kSplitCheckMinBase)) &&
                        !cs->serial && timing < 2;
-    const bool sorted_reads = split && cs->sorted_reads && sa != s;
     // two submitting threads: this batch's stage A and check go out from the helper, stage B on the
     // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it
     // records cannot be queried here: waits on its events are kept unconditionally.
-    const bool threaded = cs->submit_thread && !graph && !(cs->stage_graphs && timing < 2) && timing < 2 &&
-                          !cs->trace && sa != s;
+    const bool threaded = cs->submit_thread && !(cs->stage_graphs && timing < 2) && timing < 2 && !cs->trace && sa != s;
     cs->stats.host_ms_prepare += host_ms_since(t_begin);
     const auto t_rec = std::chrono::steady_clock::now();
-    // ---- record stage A: upload, D.Sort and the candidate edges of D.CheckIntraBatch
+    // ---- upload (issued now) and record stage A: D.Sort and the candidate edges of D.CheckIntraBatch
+    // The upload runs on its own stream unless the phases are timed one after another (then on
+    // stage A's stream, bracketed by the upload phase's events).
+    const bool own_upload = timing < 2 && !cs->serial;
+    if (hipEvent_t e = rec(kPhStart, 2)) HIPOK(hipEventRecord(e, sa));
+    if (b->state == 0 && (rc = do_upload(b, own_upload ? cs->ustream : sa))) return rc;
+    if (hipEvent_t e = rec(kPhUpload, 2)) HIPOK(hipEventRecord(e, sa));
     t_record = &la;
-    if ((rc = mark(kPhStart))) return t_record = nullptr, rc;
-    // workspace wp was last used by the batch before the previous one: its epilogue re-zeroed it
-    const bool ws_busy = cs->wused[wp] && hipEventQuery(cs->ev_b[wp]) != hipSuccess;
+    // workspace wp was last used by the batch before the previous one: its epilogue re-zeroed it.
+    // ev_b[wp] is recorded by every batch's stage B, whatever its stream layout, so the query is
+    // never answered by a stale or never-recorded event (a timing-level change with batches in
+    // flight included).
+    const bool ws_busy = cs->wused[wp] && (threaded || hipEventQuery(cs->ev_b[wp]) != hipSuccess);
     if (ws_busy && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     cs->wused[wp] = true;
-    // the upload runs on its own stream unless the batch's launches go into one graph or phases
-    // are timed one after another
-    const bool own_upload = !graph && timing < 2 && !cs->serial;
-    if (b->state == 0 && (rc = do_upload(b, own_upload))) return t_record = nullptr, rc;
     // stage A reads the batch: wait for the upload stream
     if (own_upload || (was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess))
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sa);
-    if ((rc = mark(kPhUpload))) return t_record = nullptr, rc;
     const BatchDev& bd = b->bd;
     // long-key probes pay off once tails run past a word (a 17-byte end key k\0 of a 16-byte key
     // ties on the prefix with k only, and the length decides)
@@ -1719,7 +1678,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
     int sorted = 0;
-    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, cs->sort_alg, &sorted, rec(kPhSortBegin, 1),
+    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, &sorted, rec(kPhSortBegin, 1),
                        rec(kPhSortEnd, 1), cs->sort_win && b->max_len > (int32_t)kSortNxLen);
     mark(kPhSort);
     launch_positions(sa, bd, w, sorted);
@@ -1734,9 +1693,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (ws_busy) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sc_);
         if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
             fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
-        if (sorted_reads) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
-        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, sorted_reads);
+        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
@@ -1744,17 +1702,16 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
     // stage graphs: every wait of stage B leads its list (the delta check then starts after stage A)
-    const bool hoist = cs->stage_graphs && !graph && timing < 2;
+    const bool hoist = cs->stage_graphs && timing < 2;
     if (hoist && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
     if (hoist && split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        if (sorted_reads && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
-        launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax, sorted_reads);
+        launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-        launch_check(s, bd, w, base, delta, htail, cs->check_version, cs->check_grid);
+        launch_check(s, bd, w, base, delta, htail, cs->check_version);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     mark(kPhCheck);
@@ -1780,15 +1737,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     bool compact = nd_after > delta_limit_for(cs, cs->n_ub);
     if (cs->gc_interval > 0 && ++cs->batches_since_compact >= cs->gc_interval) compact = true;
     if (cs->tail_ub > cs->tail_reclaim) compact = true;
-    // D.MergeWrite into the delta tier.  Without a compaction the merge copy also does the epilogue
-    // (index and levels of the new delta, scratch, scalars, completion flag): one launch fewer on
-    // the batch-order stream.
+    // D.MergeWrite into the delta tier
     char* hd = (char*)sl->pin_out.dp;
-    const bool fuse = !compact && cs->fuse_epilogue && timing < 2 && !cs->trace;
-    const FusedEpilogue fe{dlevels_of(cs, dnew), nd_after + 1, (uint8_t*)hd, (uint8_t*)sl->dverdict.p,
-                           (uint32_t*)(hd + o_fl), b->seq};
     launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
-                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), fuse ? &fe : nullptr, long_keys);
+                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;
@@ -1822,18 +1774,17 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     b->gc_ran = gc;
     b->compacted = compact;
     // the epilogue that rebuilds the delta tier's index also fills its directory under a new epoch
-    // (the fused copy and compactions leave none)
-    if (compact || fuse || !cs->edir.p) {
+    // (a compaction leaves none).  The epoch tag is 32 bits: before it wraps, every entry is
+    // cleared (ensure_delta_directory), so a slot an old fill left behind is never trusted.
+    if (compact || !cs->edir.p) {
         cs->ddir_epoch = 0;
     } else {
-        if (++cs->ddir_counter == 0) ++cs->ddir_counter;
-        cs->ddir_epoch = cs->ddir_counter;
+        cs->ddir_epoch = ++cs->ddir_counter;
     }
-    if (!fuse)
-        launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
-                        gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
-                        compact ? base_hint : nd_after + 1);
-    if (sa != s || split) fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
+    launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
+                    gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
+                    compact ? base_hint : nd_after + 1);
+    fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
     fdb_event(LaunchList::kSyncRecord, sl->ev_free, s);
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
         fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, s);
@@ -1846,49 +1797,37 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->stats.host_ms_record += host_ms_since(t_rec);
     const auto t_sub = std::chrono::steady_clock::now();
     // ---- submit
-    if (graph) {
-        // stage A of this batch beside the pending stage B of the previous one; this batch's
-        // stage B waits for the next detect (or a wait / flush)
-        LaunchList none;
+    if (threaded) {
+        // the helper issues this batch's stage A and check while this thread issues the
+        // previous batch's stage B; this batch's stage B waits for the next call (or a flush)
+        if ((rc = worker_wait(cs))) return rc;
+        std::swap(cs->work_a, la);
+        std::swap(cs->work_c, lc);  // empty unless split
+        cs->work_sa = sa;
         const bool prev = cs->pending_batch != nullptr;
-        cs->pending_batch = nullptr;
-        rc = launch_graph(cs, la, prev ? cs->pending_b : none);
-        std::swap(cs->pending_b, lb);
-        if (rc) return rc;
-        cs->pending_batch = b;
-    } else {
-        if (threaded) {
-            // the helper issues this batch's stage A and check while this thread issues the
-            // previous batch's stage B; this batch's stage B waits for the next call (or a flush)
-            if ((rc = worker_wait(cs))) return rc;
-            std::swap(cs->work_a, la);
-            std::swap(cs->work_c, lc);  // empty unless split
-            cs->work_sa = sa;
-            const bool prev = cs->pending_batch != nullptr;
-            cs->work_need_b = cs->b_recorded;  // every stage B recorded so far, batch i-1's included
-            worker_start_job(cs);
-            if (prev) {
-                cs->pending_batch = nullptr;
-                const hipError_t e = cs->pending_b.replay(s);
-                cs->b_issued.fetch_add(1, std::memory_order_release);
-                if (e != hipSuccess) return FDBCS_E_DEVICE;
-            }
-            std::swap(cs->pending_b, lb);
-            cs->b_recorded++;
-            cs->pending_batch = b;
-        } else if (flush_pending(cs)) {
-            return FDBCS_E_DEVICE;
-        } else if (hoist) {
-            if ((rc = launch_stage(cs, la, sa))) return rc;
-            if (split && (rc = launch_stage(cs, lc, cs->cstream))) return rc;
-            if ((rc = launch_stage(cs, lb, s))) return rc;
-        } else {
-            HIPOK(la.replay(sa));
-            if (split) HIPOK(lc.replay(cs->cstream));
-            HIPOK(lb.replay(s));
+        cs->work_need_b = cs->b_recorded;  // every stage B recorded so far, batch i-1's included
+        worker_start_job(cs);
+        if (prev) {
+            cs->pending_batch = nullptr;
+            const hipError_t e = cs->pending_b.replay(s);
+            cs->b_issued.fetch_add(1, std::memory_order_release);
+            if (e != hipSuccess) return FDBCS_E_DEVICE;
         }
-        HIPOK(take_launch_error());
+        std::swap(cs->pending_b, lb);
+        cs->b_recorded++;
+        cs->pending_batch = b;
+    } else if (flush_pending(cs)) {
+        return FDBCS_E_DEVICE;
+    } else if (hoist) {
+        if ((rc = launch_stage(cs, la, sa))) return rc;
+        if (split && (rc = launch_stage(cs, lc, cs->cstream))) return rc;
+        if ((rc = launch_stage(cs, lb, s))) return rc;
+    } else {
+        HIPOK(la.replay(sa));
+        if (split) HIPOK(lc.replay(cs->cstream));
+        HIPOK(lb.replay(s));
     }
+    HIPOK(take_launch_error());
     cs->stats.host_ms_submit += host_ms_since(t_sub);
     cs->stats.graph_launches = cs->graph_launches;
     cs->cur = final_base;
@@ -1919,7 +1858,6 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
             if ((spin & 1023) == 1023) {
                 hipError_t e = hipStreamQuery(cs->astream);
-                if (cs->astream2 && (e == hipSuccess || e == hipErrorNotReady)) e = hipStreamQuery(cs->astream2);
                 if (e == hipSuccess || e == hipErrorNotReady) e = hipStreamQuery(cs->stream);
                 if (e != hipSuccess && e != hipErrorNotReady) {
                     fprintf(stderr, "fdbcs: stream error while waiting: %s\n", hipGetErrorString(e));
@@ -2006,6 +1944,18 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                 HIPOK(hipEventSynchronize(b->slot->ev[e]));
                 break;
             }
+        for (const auto& sp : b->slot->prof_spans) {  // per-kernel events (levels 3 and 1)
+            HIPOK(hipEventSynchronize(sp.second.second));
+            const double ms = ev_ms(sp.second.first, sp.second.second);
+            auto it = std::find_if(cs->kprof.begin(), cs->kprof.end(), [&](const auto& k) { return k.func == sp.first; });
+            if (it == cs->kprof.end()) {
+                cs->kprof.push_back({sp.first, 0, 0.0});
+                it = cs->kprof.end() - 1;
+            }
+            it->launches += 1;
+            it->ms += ms;
+        }
+        b->slot->prof_spans.clear();
         auto ph = [&](int a, int z) {
             return ((b->recorded >> a) & (b->recorded >> z) & 1u) ? ev_ms(b->slot->ev[a], b->slot->ev[z]) : 0.0;
         };
@@ -2019,9 +1969,8 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         st.ms_gc += ph(kPhCompact, kPhGc);
         st.ms_epilogue += ph(kPhGc, kPhEpilogue);
         st.ms_total += ph(kPhUpload, kPhEnd);
-        // copy kernels: each reads every old boundary of its tier (32 B) and writes the kept ones
-        st.ms_merge_kernel += ph(kPhCopyBegin, kPhCopyEnd);
-        st.merge_launches += 1;
+        // roofline inputs: a kernel's launches, bytes and device time are counted together, on the
+        // batches whose events were recorded (timing level 1 samples 1 batch in timing_every)
         if (b->h_scal->intra_edges < 0) {
             st.intra_fallbacks += 1;
         } else {
@@ -2033,7 +1982,16 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         // each (16 B key, 8 B length/tail, 8 B version); kept + inserted = the result's size
         {
             const int64_t kept = b->h_scal->d_before - b->h_scal->d_rem, out = b->h_scal->nd_next;
-            st.merge_bytes += 32 * (kept + (out - kept) + out);
+            const int64_t bytes = 32 * (kept + (out - kept) + out);
+            st.merge_bytes_all += bytes;
+            st.delta_sum += b->h_scal->d_before;
+            st.base_sum += b->h_scal->n;
+            st.segments_sum += b->h_scal->n_segments;
+            if ((b->recorded >> kPhCopyEnd) & 1u) {
+                st.ms_merge_kernel += ph(kPhCopyBegin, kPhCopyEnd);
+                st.merge_launches += 1;
+                st.merge_bytes += bytes;
+            }
         }
         if ((b->recorded >> kPhCheckEnd) & 1u) {
             st.ms_check_kernel += ph(kPhCheckBegin, kPhCheckEnd);
@@ -2049,10 +2007,15 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         st.gc_runs += b->gc_ran ? 1 : 0;
         if (b->compacted) {
             st.compactions += 1;
-            st.ms_compact_kernel += ph(kPhCompBegin, kPhCompEnd);
             // kept base boundaries read, delta boundaries inserted read, result written
             const int64_t kept = b->h_scal->c_before - b->h_scal->c_rem;
-            st.compact_bytes += 32 * (kept + (b->h_scal->n_next - kept) + b->h_scal->n_next);
+            const int64_t bytes = 32 * (kept + (b->h_scal->n_next - kept) + b->h_scal->n_next);
+            st.compact_bytes_all += bytes;
+            if ((b->recorded >> kPhCompEnd) & 1u) {
+                st.ms_compact_kernel += ph(kPhCompBegin, kPhCompEnd);
+                st.compact_launches += 1;
+                st.compact_bytes += bytes;
+            }
         }
         cs->inflight--;
         if (cs->inflight == 0) {
@@ -2099,8 +2062,11 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
     if (!b->cs || b->state >= 2) return FDBCS_E_STATE;
     const int32_t T = b->T();
     if (T > 0 && !txn_ids) return FDBCS_E_INVALID;
-    for (int32_t t = 0; t < T; t++)
+    std::vector<uint8_t> seen((size_t)n_global, 0);
+    for (int32_t t = 0; t < T; t++) {
         if (txn_ids[t] < 0 || txn_ids[t] >= n_global) return FDBCS_E_INVALID;
+        if (seen[txn_ids[t]]++) return FDBCS_E_INVALID;  // one batch transaction per global index
+    }
     b->out_ids.assign(txn_ids, txn_ids + T);
     b->out_n = n_global;
     b->out_dev = dev_out;
@@ -2131,11 +2097,10 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     hipEvent_t e0, e1;
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));
-    launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version, cs->check_grid);
+    launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version);
     HIPOK(hipEventRecord(e0, cs->stream));
     for (int i = 0; i < reps; i++)
-        launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version,
-                     cs->check_grid);
+        launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version);
     HIPOK(hipEventRecord(e1, cs->stream));
     HIPOK(hipEventSynchronize(e1));
     *us_per_launch = ev_ms(e0, e1) * 1000.0 / reps;

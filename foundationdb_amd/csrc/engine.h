@@ -89,7 +89,6 @@ struct BatchScalars {
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
     int32_t pre_done;      // k_resolve workgroups done with the pre-pass (reset by the epilogue)
-    int32_t epi_done;      // merge-copy workgroups done (fused epilogue: the last one publishes)
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -226,21 +225,19 @@ struct Tier {
 // Sample ranking for the sort's splitters.
 void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per);
 // D.CheckRead against the history the previous batch left.
-// check_version: 2 = LDS-staged fused begin/end search (default), 1 = four lookups per read.
-// check_grid_cap: workgroups of the version-2 kernel (each loops over reads).
+// check_version: 6 = base and delta lookups in separate waves (default), 1 = in one wave.
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, int check_version = 2, int check_grid_cap = 2048);
+                  const uint8_t* htail, int check_version = 6);
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
 // delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
 // long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys = false, bool lead_rmax = false,
-                       bool sorted_reads = false);
+                       const uint8_t* htail, bool long_keys = false, bool lead_rmax = false);
 // bucket_target: endpoints per sample-sort bucket (0 = default 128; tests force oversized buckets).
 // sample_per: splitter samples per bucket (0 = default 8).
 // alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
 // sort_begin / sort_end (optional): events around the per-bucket sort kernel (roofline timing).
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per, int alg,
+void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
                         int* result_buffer, hipEvent_t sort_begin = nullptr, hipEvent_t sort_end = nullptr,
                         bool long_keys = true);
 // Sample-sort buckets for E endpoints at `target` endpoints per bucket (0 = default).
@@ -256,21 +253,9 @@ void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 // `srcm` are the source tier's levels: its key index is searched, its top level reset for the
 // epilogue's rebuild.
-// Epilogue fused into the merge copy (a batch without compaction): the copy also writes the new
-// delta's search index and range-max levels, the device verdicts and the workspace zeroing, and
-// its last workgroup publishes the scalars and the completion flag (no k_epilogue launch).
-struct FusedEpilogue {
-    MaxLevels m;          // the delta tier's levels / index
-    int64_t out_ub;       // upper bound of the new delta's size (levels reset range)
-    uint8_t* verdict_out;
-    uint8_t* verdict_dev;
-    uint32_t* flag;
-    uint32_t seq;
-};
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe = nullptr,
-                  bool long_keys = false);
+                  hipEvent_t copy_begin, hipEvent_t copy_end, bool long_keys = false);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
@@ -279,6 +264,8 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
 // the empty arena tdst (reclaiming the bytes of removed and overwritten boundaries).
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
                Scalars* sc, int64_t oldest, int64_t header_version, int64_t grid_hint_n);
+// Hold `s` until *release != 0 (host-mapped word; bounded spin).
+void launch_hold(hipStream_t s, const uint32_t* release);
 // Kernel attributes set once per process (the resolver's dynamic LDS above 64 KiB).
 void init_kernel_attributes();
 // Byte copy (device -> host-mapped result buffer), as a kernel.
@@ -286,8 +273,6 @@ void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n);
 // Multi-resolver conflict bytes out[g] = 2 - verdict of batch transaction inv[g] (0 if inv[g] < 0).
 void launch_conflict_output(hipStream_t s, const BatchDev& b, const Work& w, const int32_t* inv, int64_t n,
                             uint8_t* out);
-// H2D of `bytes` (16-byte multiple, both sides 16-aligned) from host-mapped pinned memory, as a kernel.
-void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes, int max_blocks);
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 // Range-max levels of a tier whose size is *n (lvl[3] reset first).

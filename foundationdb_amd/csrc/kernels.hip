@@ -486,83 +486,6 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     return lo;
 }
 
-// group_lower_bound with the levels [lds_lo, top] of the sample tree read from LDS (`lds`, level L
-// at offset off[L]); the caller keeps lds_lo wave-uniform so the two paths never diverge in a wave.
-__device__ __forceinline__ int64_t group_lower_bound_lds(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
-                                                         const uint8_t* htail, const uint8_t* qtail, bool& eq,
-                                                         const ulonglong2* lds, const int* off, int lds_lo) {
-    const int gl = threadIdx.x & (kArity - 1);
-    const int g0 = threadIdx.x & 63 & ~(kArity - 1);  // first lane of the group
-    eq = false;
-    if (n <= 0) return 0;
-    int64_t sz[kIdxLevels];
-    sz[0] = (n + kFan - 1) / kFan;
-#pragma unroll
-    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + kArity - 1) / kArity;
-    int top = 0;
-    while (top + 1 < kIdxLevels && sz[top] > kArity) top++;
-    // c = number of entries of level `top` whose prefix is < q.  When level 0 is probed, also learn
-    // whether the first sample not below q shares q's prefix (`bknown`: it does not).
-    auto prefix_eq = [&](const ulonglong2& k) { return k.x == q.hi && k.y == q.lo; };
-    int64_t c = 0;
-    bool bknown = false;
-    for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
-        const bool v = j0 + gl < sz[top];
-        const int64_t ej = v ? j0 + gl : 0;
-        const ulonglong2 e = top >= lds_lo ? lds[off[top] + ej] : m.skey[top][ej];
-        const int k = __popc(gmask(v && prefix_less(e, q)));
-        if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
-        c += k;
-        if (k < kArity) break;
-    }
-    for (int L = top; L > 0; L--) {
-        if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
-        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, Ac]
-        const int64_t base = (int64_t)kArity * (c - 1) + 1;
-        const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
-        const bool v = base + gl < end;
-        const int64_t ej = v ? base + gl : 0;
-        const ulonglong2 e = L - 1 >= lds_lo ? lds[off[L - 1] + ej] : m.skey[L - 1][ej];
-        const int k = __popc(gmask(v && prefix_less(e, q)));
-        if (L == 1 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
-        c = base + k;
-    }
-    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
-    int64_t b = c;
-    for (; !bknown;) {
-        const bool v = b + gl < sz[0];
-        const ulonglong2 k = m.skey[0][v ? b + gl : 0];
-        const uint32_t same = gmask(v && k.x == q.hi && k.y == q.lo);
-        const int run = __ffs(~same) - 1;  // leading lanes equal to q's prefix
-        b += run;
-        if (run < kArity) break;
-    }
-    int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
-    const int64_t hi = min(n, kFan * b);
-    // lower_bound in [lo, lo + span]: rounds of kArity probes at a shrinking stride.  span <= 64
-    // normally; a long run of boundaries sharing q's 16-byte prefix (tuple keys) only starts the
-    // stride higher, so the lanes still compare tails side by side.
-    int64_t span = hi - lo;
-    int64_t stride0 = kFan / kArity;
-    while (stride0 * kArity < span) stride0 *= kArity;
-    bool eq_cand = false;  // cmp == 0 at the last probe that stopped a count (the answer, if < hi)
-    for (int64_t stride = stride0; span > 0; stride = stride > kArity ? stride / kArity : 1) {
-        const int64_t p = lo + stride * (gl + 1) - 1;
-        const bool v = stride * (gl + 1) <= span && p < hi;
-        int r = 1;
-        if (v) r = probe_cmp(h, p, h.key[p], htail, q, qtail);
-        const uint32_t valid = gmask(v);
-        const int cnt = __popc(gmask(v && r < 0));
-        const int stop = __shfl(r, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
-        if (cnt < __popc(valid)) eq_cand = stop == 0;  // lane cnt probed a key >= q
-        lo += stride * cnt;
-        span = cnt < __popc(valid) ? stride - 1 : span - stride * cnt;
-        if (stride == 1) break;
-    }
-    if (lo < hi) eq = eq_cand;
-    return lo;
-}
-
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
 __device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
     int64_t best = LLONG_MIN;
@@ -789,16 +712,13 @@ __device__ __forceinline__ int64_t group_range_max(const MaxLevels& m, int64_t l
 
 template <bool LONG = false>
 __device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& tier, bool is_base, const uint8_t* htail,
-                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot, int lead_rmax,
-                                                const int32_t* rbpos, const uint32_t* pmeta) {
+                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot, int lead_rmax) {
     const int lane = threadIdx.x & 63;
     const int k = (int)(slot / kTierLanes);
     const int grp = (lane / kArity) & 1;
     const int lead = lane & ~(kTierLanes - 1);
     const bool live = k < b.R;
-    // rbpos: the batch is sorted (stage A done): lane group k takes the read with the k-th smallest
-    // begin key, so neighbouring lookups share tree nodes, cache lines and pages
-    const int rr = !live ? 0 : (rbpos ? (int)item_range(pmeta[rbpos[k]]) : k);
+    const int rr = live ? k : 0;
     const int r = rr;
     const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
@@ -836,341 +756,6 @@ __device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& t
         hist_conf[b.rowner[r]] = 1;
     }
 }
-
-// ---- D.CheckRead, LDS-staged: the top levels of both tiers' sample trees live in LDS, and one
-// lane group finds a read's begin AND end in a tier, sharing every node until the two paths part.
-//
-// Per read two groups of kArity lanes (base tier, delta tier) instead of four.  A short read
-// [k, k + d) meets the same nodes all the way down and the same 64-boundary block, so the end
-// search costs no extra dependent load; each staged level saves one (~0.5 us on a loaded chip).
-constexpr int kLdsTreeBase = 1536;                            // staged sample keys of the base tier
-constexpr int kLdsTreeDelta = 512;                            // ... of the delta tier (24 + 8 KiB)
-
-// Entries of sample-tree level L over n boundaries: the samples are every 64th boundary and each
-// level above takes every kArity-th entry, so sz(L) = ceil(n / (64 * 8^L)).
-__device__ __forceinline__ int64_t tree_sz(int64_t n, int L) {
-    const int sh = 6 + 3 * L;
-    return (n + ((int64_t)1 << sh) - 1) >> sh;
-}
-__device__ __forceinline__ int tree_top(int64_t n) {
-    int top = 0;
-    while (top + 1 < kIdxLevels && tree_sz(n, top) > kArity) top++;
-    return top;
-}
-
-// One tier's sample tree as the check kernel sees it: levels [lds_lo, top] are staged in LDS at
-// the per-level offsets `off` (an LDS table shared by the workgroup, uniform reads).
-struct TreeRef {
-    int64_t n;
-    int top, lds_lo;
-    const int* off;       // [kIdxLevels] LDS index of level L's first entry
-    const ulonglong2* lds;
-};
-
-// Offset of sample-tree level L from skey[0] (levels are carved back to back, engine.cpp
-// carve_index): no dynamic index into MaxLevels::skey[], which would put the struct in scratch.
-__device__ __forceinline__ int64_t skey_offset(const MaxLevels& m, int L) {
-    int64_t off = 0;
-    for (int l = 0; l < L; l++) off += idx_level_cap(m.idx_cap, l);
-    return off;
-}
-
-// Levels of a tier to stage: from the top down while they fit `budget` entries; fills off[] and
-// returns lds_lo (top + 1: none).
-__device__ __forceinline__ int plan_stage(int64_t n, int top, int budget, int lds_base, int* off) {
-    int lo = top + 1;
-    int64_t used = 0;
-    for (int L = top; L >= 0 && n > 0; L--) {
-        const int64_t z = tree_sz(n, L);
-        if (used + z > budget) break;
-        off[L] = lds_base + (int)used;
-        used += z;
-        lo = L;
-    }
-    return lo;
-}
-
-// lower_bound of qb and (want_e) of qe >= qb over one tier, by one aligned group of kArity lanes.
-// lb / eqb: begin's position and whether the boundary there equals qb; le: end's position.
-//
-// The descent runs through the sample tree (top levels from LDS), then through skey8 (every 8th
-// boundary), so that a lookup touches one 128-byte line per level and a final run of 8
-// consecutive boundaries: 8-ary all the way down.  Every level counts the entries whose prefix is
-// below q's; `known` says whether the first entry not below q has a different prefix (else a run
-// of boundaries sharing q's 16-byte prefix, tuple keys, widens the final span and the strided
-// rounds below compare tails).
-__device__ __forceinline__ void group_lower_bound2(const Hist& h, const MaxLevels& m, const TreeRef& tv,
-                                                   const DKey& qb, const DKey& qe, bool want_e, const uint8_t* htail,
-                                                   const uint8_t* qtail, int64_t& lb, bool& eqb, int64_t& le) {
-    const int gl = threadIdx.x & (kArity - 1);
-    const int g0 = threadIdx.x & 63 & ~(kArity - 1);
-    lb = le = 0;
-    eqb = false;
-    const int64_t n = tv.n;
-    if (n <= 0) return;
-    auto peq = [](const ulonglong2& k, const DKey& q) { return k.x == q.hi && k.y == q.lo; };
-    // level L >= 0: sample tree (staged levels from LDS); level -1: skey8.  `off` tracks the global
-    // offset of the level being read as the descent goes down.
-    const int top = tv.top;
-    int64_t off = skey_offset(m, top);
-    auto entry = [&](int L, int64_t i) {
-        if (L < 0) return m.skey8[i];
-        return L >= tv.lds_lo ? tv.lds[tv.off[L] + i] : m.skey[0][off + i];
-    };
-    auto level_sz = [&](int L) { return L >= 0 ? tree_sz(n, L) : (n + 7) / 8; };
-    int64_t cb = 0, ce = 0;
-    bool kb = true, ke = true;  // known: the first entry not below q has another prefix (true past the end)
-    {
-        bool doneb = false, donee = !want_e;
-        const int64_t sztop = tree_sz(n, top);
-        for (int64_t j0 = 0; j0 < sztop && !(doneb && donee); j0 += kArity) {
-            const bool v = j0 + gl < sztop;
-            const ulonglong2 e = entry(top, v ? j0 + gl : 0);
-            const int nv = __popc(gmask(v));
-            if (!doneb) {
-                const int k = __popc(gmask(v && prefix_less(e, qb)));
-                if (k < nv) kb = !((gmask(v && peq(e, qb)) >> k) & 1u);
-                cb += k;
-                doneb = k < kArity;
-            }
-            if (!donee) {
-                const int k = __popc(gmask(v && prefix_less(e, qe)));
-                if (k < nv) ke = !((gmask(v && peq(e, qe)) >> k) & 1u);
-                ce += k;
-                donee = k < kArity;
-            }
-        }
-    }
-    if (!want_e) ce = cb, ke = kb;
-    for (int L = top; L > -1; L--) {
-        // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, A c]; entry A c is the parent's
-        // entry c, so when the whole node is below q the parent's `known` carries down
-        const int64_t szl = level_sz(L - 1);
-        if (L - 1 >= 0) off -= idx_level_cap(m.idx_cap, L - 1);
-        const int64_t bb = kArity * (cb - 1) + 1, be = min((int64_t)kArity * cb, szl);
-        const int64_t eb = kArity * (ce - 1) + 1, ee = min((int64_t)kArity * ce, szl);
-        const bool vb = cb > 0 && bb + gl < be;
-        const bool ve = want_e && ce > 0 && eb + gl < ee;
-        const ulonglong2 xb = entry(L - 1, vb ? bb + gl : 0);
-        const ulonglong2 xe = (ce == cb) ? xb : entry(L - 1, ve ? eb + gl : 0);
-        const int nb = __popc(gmask(vb)), kb_ = __popc(gmask(vb && prefix_less(xb, qb)));
-        const int ne = __popc(gmask(ve)), ke_ = __popc(gmask(ve && prefix_less(xe, qe)));
-        if (kb_ < nb) kb = !((gmask(vb && peq(xb, qb)) >> kb_) & 1u);
-        if (ke_ < ne) ke = !((gmask(ve && peq(xe, qe)) >> ke_) & 1u);
-        if (cb > 0) cb = bb + kb_;
-        if (ce > 0 && want_e) ce = eb + ke_;
-    }
-    // skey8 entries sharing q's prefix past the count widen the final span
-    const int64_t sz8 = (n + 7) / 8;
-    auto run_end = [&](int64_t c, bool known, const DKey& q) {
-        int64_t b = c;
-        for (; !known;) {
-            const bool v = b + gl < sz8;
-            const ulonglong2 k = m.skey8[v ? b + gl : 0];
-            const uint32_t same = gmask(v && peq(k, q));
-            const int run = __ffs(~same) - 1;
-            b += run;
-            if (run < kArity) break;
-        }
-        return b;
-    };
-    const int64_t bbk = run_end(cb, kb, qb);
-    const int64_t bek = want_e ? run_end(ce, ke, qe) : 0;
-    // boundaries: rounds of kArity probes at a shrinking stride (one round of 8 consecutive keys
-    // unless a shared-prefix run widened the span), both searches side by side; a probe both
-    // searches make is loaded once
-    int64_t lo_b = cb > 0 ? 8 * (cb - 1) + 1 : 0, hi_b = min(n, 8 * bbk);
-    int64_t lo_e = ce > 0 ? 8 * (ce - 1) + 1 : 0, hi_e = want_e ? min(n, 8 * bek) : 0;
-    int64_t sp_b = hi_b - lo_b, sp_e = want_e ? hi_e - lo_e : 0;
-    int64_t st_b = 1, st_e = 1;
-    while (st_b * kArity < sp_b) st_b *= kArity;
-    while (st_e * kArity < sp_e) st_e *= kArity;
-    bool act_b = sp_b > 0, act_e = sp_e > 0;
-    bool eqc = false;
-    while (act_b || act_e) {
-        const int64_t pb = lo_b + st_b * (gl + 1) - 1, pe = lo_e + st_e * (gl + 1) - 1;
-        const bool vb = act_b && st_b * (gl + 1) <= sp_b && pb < hi_b;
-        const bool ve = act_e && st_e * (gl + 1) <= sp_e && pe < hi_e;
-        const ulonglong2 xb = h.key[vb ? pb : 0];
-        const ulonglong2 xe = (vb && ve && pe == pb) ? xb : h.key[ve ? pe : 0];
-        int rb = 1, re = 1;
-        if (vb) rb = probe_cmp_lean(h, pb, xb, htail, qb, qtail);
-        if (ve) re = probe_cmp_lean(h, pe, xe, htail, qe, qtail);
-        if (act_b) {
-            const int nv = __popc(gmask(vb)), cnt = __popc(gmask(vb && rb < 0));
-            const int stop = __shfl(rb, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
-            if (cnt < nv) eqc = stop == 0;
-            lo_b += st_b * cnt;
-            sp_b = cnt < nv ? st_b - 1 : sp_b - st_b * cnt;
-            if (st_b == 1 || sp_b <= 0) act_b = false;
-            st_b = st_b > kArity ? st_b / kArity : 1;
-        }
-        if (act_e) {
-            const int nv = __popc(gmask(ve)), cnt = __popc(gmask(ve && re < 0));
-            lo_e += st_e * cnt;
-            sp_e = cnt < nv ? st_e - 1 : sp_e - st_e * cnt;
-            if (st_e == 1 || sp_e <= 0) act_e = false;
-            st_e = st_e > kArity ? st_e / kArity : 1;
-        }
-    }
-    lb = lo_b;
-    eqb = lo_b < hi_b ? eqc : false;
-    le = lo_e;
-}
-
-struct CheckReads2 {
-    Tier base, delta;
-    const uint8_t* htail;
-    uint8_t *hist_conf, *rconf;
-    unsigned long long* trace;
-};
-
-// The tier a wave searches is wave-uniform (waves [0, 4) the base tier, [4, 8) the delta tier, for
-// the same 32 reads), so the tier's pointers and tree shape stay in scalar registers; the two
-// verdicts meet in LDS.  Each wave's 8 lane groups take 8 reads.
-// BYWAVE: the tier a wave searches is wave-uniform (waves [0, NT/128) the base tier, the rest the
-// delta tier, for the same reads; the two verdicts meet in LDS), else each read's base group and
-// delta group sit side by side in one wave and meet by a shuffle.
-template <int NT, bool BYWAVE>
-__device__ __forceinline__ void check_reads_body(const BatchDev& b, const CheckReads2& c) {
-    constexpr int kReadsPerBlock = NT / (2 * kArity);
-    constexpr int kWavesPerTier = NT / 64 / 2;
-    __shared__ ulonglong2 s_tree[kLdsTreeBase + kLdsTreeDelta];
-    __shared__ int s_off[2][kIdxLevels];
-    __shared__ int s_lo[2];
-    __shared__ uint8_t s_conf[2][kReadsPerBlock];
-    if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
-    const int64_t nt[2] = {*c.base.n, *c.delta.n};
-    const int top[2] = {tree_top(nt[0]), tree_top(nt[1])};
-    if (threadIdx.x < 2) {
-        const int t = threadIdx.x;
-        s_lo[t] = plan_stage(nt[t], top[t], t ? kLdsTreeDelta : kLdsTreeBase, t ? kLdsTreeBase : 0, s_off[t]);
-    }
-    __syncthreads();
-    for (int t = 0; t < 2; t++) {  // stage the planned levels (uniform loop bounds)
-        const MaxLevels& m = t ? c.delta.m : c.base.m;
-        for (int L = s_lo[t]; L <= top[t]; L++) {
-            const int64_t z = tree_sz(nt[t], L);
-            const ulonglong2* src = m.skey[0] + skey_offset(m, L);
-            for (int64_t i = threadIdx.x; i < z; i += blockDim.x) s_tree[s_off[t][L] + i] = src[i];
-        }
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const bool leader = (threadIdx.x & (kArity - 1)) == 0;
-    int t, slot;
-    if (BYWAVE) {
-        const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        t = wave >= kWavesPerTier ? 1 : 0;
-        slot = (wave - t * kWavesPerTier) * (64 / kArity) + (lane / kArity);
-    } else {
-        t = (threadIdx.x / kArity) & 1;
-        slot = threadIdx.x / (2 * kArity);
-    }
-    const Tier& tier = t ? c.delta : c.base;
-    const TreeRef tv{nt[t], top[t], s_lo[t], s_off[t], s_tree};
-    for (int64_t r0 = (int64_t)blockIdx.x * kReadsPerBlock; r0 < b.R;
-         r0 += (int64_t)gridDim.x * kReadsPerBlock) {
-        const int64_t r = r0 + slot;
-        const bool live = r < b.R;
-        const int rr = live ? (int)r : 0;
-        const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
-        const int64_t snap = b.snap[b.rowner[rr]];  // issued before the search
-        const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-        int64_t lb = 0, le = 0;
-        bool eq = false;
-        if (live) group_lower_bound2(tier.h, tier.m, tv, kb, ke, !degenerate, c.htail, b.tail, lb, eq, le);
-        bool conf = false;
-        if (live && leader && (t == 0 || tv.n > 0))
-            conf = tier_conflict(tier.h, tier.m, t == 0 ? tier.hdr : kHole, lb, eq, le, degenerate, snap);
-        if (BYWAVE) {
-            if (leader) s_conf[t][slot] = conf ? 1 : 0;
-            __syncthreads();
-            if (threadIdx.x < kReadsPerBlock && r0 + threadIdx.x < b.R) {
-                const int64_t rw = r0 + threadIdx.x;
-                const bool cf = s_conf[0][threadIdx.x] | s_conf[1][threadIdx.x];
-                c.rconf[rw] = cf ? 1 : 0;
-                if (cf) c.hist_conf[b.rowner[rw]] = 1;
-            }
-            __syncthreads();
-        } else {
-            const int lead = lane & ~(2 * kArity - 1);
-            const int dconf = __shfl((int)conf, lead + kArity, 64);
-            if (live && lane == lead) {
-                conf = conf || dconf;
-                c.rconf[r] = conf ? 1 : 0;
-                if (conf) c.hist_conf[b.rowner[r]] = 1;
-            }
-        }
-    }
-    if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
-}
-
-// Variants (FDBCS_CHECK, A/B; LDS-staged top levels): 2 = base and delta groups of a read in one wave, 256 threads;
-// 3 = the same, 512 threads; 4 = wave-uniform tiers, 512 threads.
-__global__ __launch_bounds__(256) void k_check_reads2(BatchDev b, CheckReads2 c) { check_reads_body<256, false>(b, c); }
-__global__ __launch_bounds__(512) void k_check_reads3(BatchDev b, CheckReads2 c) { check_reads_body<512, false>(b, c); }
-__global__ __launch_bounds__(512) void k_check_reads4(BatchDev b, CheckReads2 c) { check_reads_body<512, true>(b, c); }
-
-// Variant 5: the v1 shape (one lane group per key: a read's begin and end, in the base and in the
-// delta tier, 32 lanes) with the tiers' top sample-tree levels staged in LDS and the tier
-// wave-uniform (even waves search the base tier, odd waves the delta tier, for the same four
-// reads each), so the LDS-or-global choice never diverges inside a wave.  Either tier's wave sets
-// the conflict flags (rconf is zeroed by the previous epilogue on this workspace).
-template <int NT>
-__device__ __forceinline__ void check_reads_v5(const BatchDev& b, const CheckReads2& c) {
-    constexpr int kReadsPerBlock = NT / 64 / 2 * 4;
-    __shared__ ulonglong2 s_tree[kLdsTreeBase + kLdsTreeDelta];
-    __shared__ int s_off[2][kIdxLevels];
-    __shared__ int s_lo[2];
-    if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
-    const int64_t nt[2] = {*c.base.n, *c.delta.n};
-    const int top[2] = {tree_top(nt[0]), tree_top(nt[1])};
-    if (threadIdx.x < 2) {
-        const int t = threadIdx.x;
-        s_lo[t] = plan_stage(nt[t], top[t], t ? kLdsTreeDelta : kLdsTreeBase, t ? kLdsTreeBase : 0, s_off[t]);
-    }
-    __syncthreads();
-    for (int t = 0; t < 2; t++) {
-        const MaxLevels& m = t ? c.delta.m : c.base.m;
-        for (int L = s_lo[t]; L <= top[t]; L++) {
-            const int64_t z = tree_sz(nt[t], L);
-            const ulonglong2* src = m.skey[0] + skey_offset(m, L);
-            for (int64_t i = threadIdx.x; i < z; i += blockDim.x) s_tree[s_off[t][L] + i] = src[i];
-        }
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int t = wave & 1;
-    const Tier& tier = t ? c.delta : c.base;
-    const int64_t n = nt[t];
-    const int lds_lo = s_lo[t];
-    const int slot = (wave >> 1) * 4 + lane / (2 * kArity);  // this wave's 4 reads
-    const bool is_end = (lane / kArity) & 1;
-    for (int64_t r0 = (int64_t)blockIdx.x * kReadsPerBlock; r0 < b.R; r0 += (int64_t)gridDim.x * kReadsPerBlock) {
-        const int64_t r = r0 + slot;
-        const bool live = r < b.R;
-        const int rr = live ? (int)r : 0;
-        const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
-        const int64_t snap = b.snap[b.rowner[rr]];
-        const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-        int64_t lb = 0;
-        bool eq = false;
-        if (live && n > 0 && !(is_end && degenerate))
-            lb = group_lower_bound_lds(tier.h, tier.m, n, is_end ? ke : kb, c.htail, b.tail, eq, s_tree, s_off[t],
-                                       lds_lo);
-        const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // begin groups take their end's position
-        if (live && !is_end && (lane & (kArity - 1)) == 0 && (t == 0 || n > 0)) {
-            if (tier_conflict(tier.h, tier.m, t == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
-                c.rconf[r] = 1;
-                c.hist_conf[b.rowner[r]] = 1;
-            }
-        }
-    }
-    if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
-}
-__global__ __launch_bounds__(256) void k_check_reads5(BatchDev b, CheckReads2 c) { check_reads_v5<256>(b, c); }
 
 // ------------------------------------------------------------------ D.Sort
 
@@ -1364,20 +949,18 @@ struct CheckReads {
 // LONG: the batch has keys over 16 bytes (long-key probes, group_lower_bound<true>).
 template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const uint8_t* htail, uint8_t* hist_conf,
-                                                       uint8_t* rconf, int lead_rmax, const int32_t* rbpos,
-                                                       const uint32_t* pmeta) {
+                                                       uint8_t* rconf, int lead_rmax) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax, rbpos, pmeta);
+    check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys, bool lead_rmax, bool sorted_reads) {
+                       const uint8_t* htail, bool long_keys, bool lead_rmax) {
     if (b.R == 0) return;
     const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
     auto k = is_base ? (long_keys ? k_check_tier<true, true> : k_check_tier<true, false>)
                      : (long_keys ? k_check_tier<false, true> : k_check_tier<false, false>);
-    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, lead_rmax ? 1 : 0,
-               sorted_reads ? (const int32_t*)w.rbpos : nullptr, sorted_reads ? (const uint32_t*)w.pmeta : nullptr);
+    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, lead_rmax ? 1 : 0);
 }
 
 template <bool TIER_WAVES>
@@ -1784,37 +1367,19 @@ void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_t
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, int check_version, int check_grid_cap) {
+                  const uint8_t* htail, int check_version) {
     if (b.R == 0) return;
-    if (check_version == 1 || check_version == 6) {  // four independent lookups per read, no LDS staging
-        CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
-        const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
-        if (check_version == 6)  // FDBCS_CHECK=6: base and delta lookups in separate waves
-            fdb_launch(k_check_reads<true>, dim3(grid), dim3(kBlock), 0, s, b, c);
-        else
-            fdb_launch(k_check_reads<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
-        return;
-    }
-    CheckReads2 c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
-    const int nt = check_version == 2 ? 256 : 512;
-    const int per_block = nt / (2 * kArity);  // a base group and a delta group per read
-    int64_t grid = ((int64_t)b.R + per_block - 1) / per_block;
-    grid = grid > check_grid_cap ? check_grid_cap : grid;
-    if (check_version == 5) {
-        const int64_t g5 = ((int64_t)b.R + 7) / 8;  // 256 threads: 2 wave pairs x 4 reads
-        fdb_launch(k_check_reads5, dim3((unsigned)(g5 > check_grid_cap ? check_grid_cap : g5)), dim3(256), 0, s, b, c);
-        return;
-    }
-    if (check_version == 3)
-        fdb_launch(k_check_reads3, dim3((unsigned)grid), dim3(512), 0, s, b, c);
-    else if (check_version == 4)
-        fdb_launch(k_check_reads4, dim3((unsigned)grid), dim3(512), 0, s, b, c);
+    // four lookups per read: 6 = the base and delta lookups in separate waves, 1 = in one wave
+    CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
+    const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
+    if (check_version == 6)
+        fdb_launch(k_check_reads<true>, dim3(grid), dim3(kBlock), 0, s, b, c);
     else
-        fdb_launch(k_check_reads2, dim3((unsigned)grid), dim3(256), 0, s, b, c);
+        fdb_launch(k_check_reads<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
 void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
-                        int alg, int* result_buffer, hipEvent_t sort_begin, hipEvent_t sort_end, bool long_keys) {
+                        int* result_buffer, hipEvent_t sort_begin, hipEvent_t sort_end, bool long_keys) {
     const int E = 2 * (b.R + b.W);
     *result_buffer = 0;
     if (E == 0) return;
@@ -1826,9 +1391,7 @@ void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int buc
     fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
                        w.items[0]);
     fdb_event(LaunchList::kTimingRecord, sort_begin, s);
-    if (alg == 1)
-        fdb_launch(k_bucket_sort<1, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
-    else if (long_keys)
+    if (long_keys)
         fdb_launch(k_bucket_sort<0, true>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
     else
         fdb_launch(k_bucket_sort<0, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
@@ -2683,68 +2246,6 @@ struct Epilogue {
     BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
 };
 
-// ---- epilogue fused into the delta merge copy (batches without a compaction): the copy writes
-// every boundary of the new delta tier once, so it also writes the tier's search index
-// (skey8 / skey levels: position-indexed) and folds the versions into the range-max levels with
-// atomicMax (levels 1 and 2, reset by k_seg_search; level 3 from level 2 by the last workgroup,
-// which then publishes the scalars and the completion flag).  Saves the epilogue launch and its
-// queue gap on the batch-order stream.
-__device__ __forceinline__ void epi_index_store(const MaxLevels& m, int64_t o, const ulonglong2& key) {
-    if ((o & 7) != 0) return;
-    m.skey8[o >> 3] = key;
-    if ((o & 63) != 0) return;
-    int64_t d = o >> 6;
-    m.skey[0][d] = key;
-    // level L at skey[0] + sum of the lower levels' capacities (no dynamic index into skey[]:
-    // that would copy the kernel-argument struct to scratch)
-    int64_t off = 0;
-    for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
-        off += idx_level_cap(m.idx_cap, L - 1);
-        d /= kArity;
-        m.skey[0][off + d] = key;
-    }
-}
-// Wave-cooperative max of (output position o, version v) into level 1: one atomic per distinct
-// 64-boundary block of the wave.  Every lane of the wave calls it (o < 0: no output).  Levels 2
-// and 3 are built from level 1 by the last workgroup (atomics on their few entries would
-// serialize thousands of updates per address).
-__device__ __forceinline__ void epi_wave_levels(const MaxLevels& m, int64_t o, int64_t v) {
-    const int64_t key = o >= 0 ? (o >> 6) : -1;
-    bool pending = key >= 0;
-    for (;;) {
-        const uint64_t act = __ballot(pending);
-        if (!act) break;
-        const int leader = __ffsll((long long)act) - 1;
-        const int64_t k0 = __shfl(key, leader, 64);
-        const bool mine = pending && key == k0;
-        int64_t x = mine ? v : LLONG_MIN;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const int64_t y = __shfl_xor(x, off, 64);
-            x = y > x ? y : x;
-        }
-        if ((threadIdx.x & 63) == leader) atomicMax((long long*)&m.lvl[1][k0], (long long)x);
-        pending = pending && !mine;
-    }
-}
-__device__ __forceinline__ void epi_point_levels(const MaxLevels& m, int64_t o, int64_t v) {
-    atomicMax((long long*)&m.lvl[1][o >> 6], (long long)v);
-}
-// Grid-stride part: device verdicts and the scratch the workspace's next batch expects zeroed.
-__device__ __forceinline__ void epi_zero(const Epilogue& ep) {
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t = tid; t < ep.T; t += stride)
-        ep.verdict_dev[t] = (ep.flags[t] & kFlagTooOld) ? 1 : (ep.status[t] == kCommitted ? 2 : 0);
-    for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
-    for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
-    for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
-    for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
-    for (int64_t i = tid; i < kMaxBuckets; i += stride) {
-        ep.zero_bc[i] = 0;
-        ep.zero_bk[i] = 0;
-    }
-    for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
-}
 // The scalars after the verdicts in the host-mapped result (word by word: a local Scalars copy
 // would live in scratch), with the workspace's batch statistics; resets the workspace counters.
 __device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogue& ep) {
@@ -2760,46 +2261,6 @@ __device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogu
     ep.bsc->pre_done = 0;  // k_resolve's pre-pass counter (its workgroups have all finished)
     ep.bsc->debug_error = 0;
 }
-// Last workgroup: level 3 from level 2, scalar roll-over, scalars next to the verdicts, flag.
-__device__ __forceinline__ void epi_finish(const MaxLevels& m, Scalars* sc, const Epilogue& ep) {
-    const int64_t n0 = __hip_atomic_load(&sc->nd_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan, n3 = (n2 + kFan - 1) / kFan;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t j = wid; j < n2; j += blockDim.x >> 6) {  // level 2 from level 1 (device-scope atomics)
-        const int64_t i = j * kFan + lane;
-        int64_t x = i < n1 ? __hip_atomic_load((long long*)&m.lvl[1][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : LLONG_MIN;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const int64_t y = __shfl_xor(x, off, 64);
-            x = y > x ? y : x;
-        }
-        if (lane == 0) m.lvl[2][j] = x;
-    }
-    __syncthreads();
-    for (int64_t j = wid; j < n3; j += blockDim.x >> 6) {  // level 3 from level 2 (this workgroup)
-        const int64_t i = j * kFan + lane;
-        int64_t x = i < n2 ? m.lvl[2][i] : LLONG_MIN;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const int64_t y = __shfl_xor(x, off, 64);
-            x = y > x ? y : x;
-        }
-        if (lane == 0) m.lvl[3][j] = x;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        sc->nd = n0;
-        sc->tail_used = sc->tail_next;
-        publish_scalars(sc, ep);
-        ep.bsc->epi_done = 0;
-    }
-    __syncthreads();
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(ep.flag, ep.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // ------------------------------------------------------------------ D.MergeWrite
 //
 // mergeWriteConflictRanges (SkipList.cpp:899-924, 414-424): for each union segment [B, E):
@@ -2816,13 +2277,11 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
 template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, MaxLevels hm,
                                                        const uint8_t* htail, const Scalars* sc, const int64_t* n_in,
-                                                       int64_t* lvl3, int64_t lvl3_n, int64_t lvl1_n) {
+                                                       int64_t* lvl3, int64_t lvl3_n) {
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // the history check of this batch is done with the old hierarchy: reset its top level for the
-    // epilogue's atomicMax build (and levels 1-2 when the merge copy builds them: fused epilogue)
+    // epilogue's atomicMax build
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
-    for (int64_t i = gt; i < lvl1_n; i += (int64_t)gridDim.x * blockDim.x) hm.lvl[1][i] = LLONG_MIN;
-    for (int64_t i = gt; i < (lvl1_n + kFan - 1) / kFan; i += (int64_t)gridDim.x * blockDim.x) hm.lvl[2][i] = LLONG_MIN;
     // 2*kArity lanes per union segment: lane group 0 locates B, group 1 locates E (cooperative search)
     const int U = sc->n_segments;
     const int s = (int)(gt / (2 * kArity)), role = (int)((gt / kArity) & 1);
@@ -2971,12 +2430,7 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                         dst.key[dsto[k]] = make_ulonglong2(khi[k], klo[k]);
                         reinterpret_cast<uint64_t*>(dst.lt)[dsto[k]] = lt[k];
                         dst.ver[dsto[k]] = (int64_t)vv[k];
-                        if (Ins::kEpi && ins.epi) epi_index_store(ins.em, dsto[k], make_ulonglong2(khi[k], klo[k]));
                     }
-                }
-                if (Ins::kEpi && ins.epi) {
-#pragma unroll
-                    for (int k = 0; k < kPer; k++) epi_wave_levels(ins.em, dsto[k], (int64_t)vv[k]);
                 }
             }
         } else {
@@ -2992,41 +2446,16 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                 dst.key[o] = src.key[i];
                 dst.lt[o] = src.lt[i];
                 dst.ver[o] = src.ver[i];
-                if (Ins::kEpi && ins.epi) {
-                    epi_index_store(ins.em, o, src.key[i]);
-                    epi_point_levels(ins.em, o, src.ver[i]);
-                }
             }
         }
         for (int sg = s_ins0 + threadIdx.x; sg < s_ins1; sg += blockDim.x)
             ins(sg, dst, g.lo[sg] - g.rem[sg] + g.ins[sg]);
         __syncthreads();
     }
-    if (Ins::kEpi && ins.epi) {  // fused epilogue: scratch + verdict copy, then the last workgroup publishes
-        epi_zero(ins.ep);
-        // Completion count without a device-scope release (an L2 write-back per workgroup would
-        // stall every tile): the last workgroup only reads levels 1-2, which were updated by
-        // device-scope atomics, so each wave merely waits for its own atomics to be performed.
-        // Plain stores (the tier, its index) reach later kernels through the kernel boundary.
-        __shared__ int s_last;
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int prev = __hip_atomic_fetch_add(&ins.ep.bsc->epi_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = prev == (int)gridDim.x - 1;
-        }
-        __syncthreads();
-        if (s_last) epi_finish(ins.em, ins.esc, ins.ep);
-    }
 }
 
 // Inserts of a union segment: B at `now`, E (when needed) at the version it had.
 struct BatchIns {
-    static constexpr bool kEpi = true;
-    int epi;            // fused epilogue (no compaction this batch): index + levels + publish
-    MaxLevels em;       // the delta tier's levels / index (the arrays both delta buffers share)
-    Scalars* esc;
-    Epilogue ep;
     BatchDev b;
     const uint32_t* pmeta;
     const int32_t *seg_b, *seg_e;
@@ -3050,10 +2479,6 @@ struct BatchIns {
         dst.key[o] = make_ulonglong2(kb.hi, kb.lo);
         dst.lt[o] = make_uint2(kb.len, tb);
         dst.ver[o] = now;
-        if (epi) {
-            epi_index_store(em, o, make_ulonglong2(kb.hi, kb.lo));
-            epi_point_levels(em, o, now);
-        }
         if (endins[s]) {
             const DKey ke = key(seg_e[s], 1);
             uint32_t te = 0;
@@ -3064,10 +2489,6 @@ struct BatchIns {
             dst.key[o + 1] = make_ulonglong2(ke.hi, ke.lo);
             dst.lt[o + 1] = make_uint2(ke.len, te);
             dst.ver[o + 1] = vend[s];
-            if (epi) {
-                epi_index_store(em, o + 1, make_ulonglong2(ke.hi, ke.lo));
-                epi_point_levels(em, o + 1, vend[s]);
-            }
         }
     }
 };
@@ -3111,23 +2532,15 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end, const FusedEpilogue* fe, bool long_keys) {
+                  hipEvent_t copy_begin, hipEvent_t copy_end, bool long_keys) {
     const int Wn = b.W > 0 ? b.W : 1;
-    // fused epilogue: levels 1-2 of the new delta are built by atomicMax in the copy (reset here)
-    const int64_t lvl1_n = fe ? (fe->out_ub + kFan - 1) / kFan + 1 : 0;
     fdb_launch(long_keys ? k_seg_search<true> : k_seg_search<false>, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
-               htail, sc, &sc->nd, srcm.lvl[3], lvl3_n, lvl1_n);
+               htail, sc, &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
     launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
                    w.scan[kScanSegSum]);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
-    ins.epi = fe ? 1 : 0;
-    if (fe) {
-        ins.em = fe->m;
-        ins.esc = sc;
-        ins.ep = make_epilogue(b, w, 0, 0, fe->verdict_out, fe->verdict_dev, fe->flag, fe->seq);
-    }
     ins.b = b;
     ins.pmeta = w.pmeta;
     ins.seg_b = w.seg_b;
@@ -3218,12 +2631,6 @@ struct CompactIns {
         dst.lt[o] = delta.lt[s];
         dst.ver[o] = val[s];
     }
-    // no fused epilogue (the compaction's epilogue rebuilds the base tier's levels)
-    static constexpr bool kEpi = false;
-    int epi = 0;
-    MaxLevels em{};
-    Scalars* esc = nullptr;
-    Epilogue ep{};
 };
 
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
@@ -3457,36 +2864,6 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     }
 }
 
-// ------------------------------------------------------------------ batch upload
-//
-// H2D of a packed batch as a kernel reading the pinned, host-mapped staging buffer over PCIe:
-// an ordinary launch on stage A's stream, so the host never blocks in the copy call (a DMA-engine
-// hipMemcpyAsync behind cross-stream waits held the submitting thread ~0.5 ms per batch).  Each
-// lane moves 16-byte words, four in flight.
-// Few workgroups with many loads in flight each: PCIe latency x bandwidth needs ~100 KB in flight,
-// and waves parked on host reads hold CU slots the overlapping stage-B kernels want.
-constexpr int kUploadUnroll = 8;
-__global__ __launch_bounds__(kBlock) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + (kUploadUnroll - 1) * stride < n16; i += kUploadUnroll * stride) {
-        uint4 v[kUploadUnroll];
-#pragma unroll
-        for (int k = 0; k < kUploadUnroll; k++) v[k] = src[i + k * stride];
-#pragma unroll
-        for (int k = 0; k < kUploadUnroll; k++) dst[i + k * stride] = v[k];
-    }
-    for (; i < n16; i += stride) dst[i] = src[i];
-}
-
-void launch_upload(hipStream_t s, const void* host_mapped, void* dst, int64_t bytes, int max_blocks) {
-    const int64_t n16 = (bytes + 15) / 16;
-    int64_t blocks = (n16 + kUploadUnroll * kBlock - 1) / (kUploadUnroll * kBlock);
-    blocks = blocks < 1 ? 1 : (blocks > max_blocks ? max_blocks : blocks);
-    fdb_launch(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)host_mapped, (uint4*)dst,
-                       n16);
-}
-
 // Report side outputs (rconf, hist_conf, first_conf) into the batch's host-mapped result buffer:
 // a kernel rather than a DMA copy so it can be a node of the batch's graph.
 __global__ __launch_bounds__(kBlock) void k_copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
@@ -3525,6 +2902,17 @@ void launch_conflict_output(hipStream_t s, const BatchDev& b, const Work& w, con
     blocks = blocks > 1024 ? 1024 : blocks;
     fdb_launch(k_conflict_output, dim3((unsigned)blocks), dim3(kBlock), 0, s, b, (const uint8_t*)w.status, inv, n,
                out);
+}
+
+// fdbcs_debug_hold: holds a stream until the host writes the release word (host-mapped), so batches
+// queued behind it then run back to back at the device's own rate.  Bounded (a few seconds): never a hang.
+__global__ void k_hold(const volatile uint32_t* release) {
+    if (threadIdx.x != 0) return;
+    for (int64_t spin = 0; spin < ((int64_t)1 << 22) && *release == 0u; spin++) __builtin_amdgcn_s_sleep(64);
+}
+
+void launch_hold(hipStream_t s, const uint32_t* release) {
+    fdb_launch(k_hold, dim3(1), dim3(64), 0, s, (const volatile uint32_t*)release);
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {

@@ -37,6 +37,26 @@ struct LaunchList {
     std::vector<uint32_t> argoff;  // byte offset of each argument value in `arena`
     std::vector<unsigned char> arena;
     std::vector<void*> argp;       // finalize(): pointers into arena, in argoff order
+    // Per-kernel profile (timing level 3): when set, every recorded kernel is bracketed by two
+    // timing events taken from `pool` (created on demand), and (kernel, begin, end) is noted in
+    // `spans`; the engine reads the elapsed times once the batch is done.
+    struct Profile {
+        std::vector<hipEvent_t>* pool;
+        size_t* next;
+        std::vector<std::pair<const void*, std::pair<hipEvent_t, hipEvent_t>>>* spans;
+        hipEvent_t take() {
+            if (*next == pool->size()) {
+                hipEvent_t e = nullptr;
+                if (hipEventCreate(&e) != hipSuccess) return nullptr;
+                pool->push_back(e);
+            }
+            return (*pool)[(*next)++];
+        }
+    };
+    Profile* prof = nullptr;
+    // Events around the one kernel `timed_func` (timing level 1, roofline of the dominant kernel),
+    // noted in `prof` like the profile spans.
+    const void* timed_func = nullptr;
 
     void clear() {
         recs.clear();
@@ -107,7 +127,14 @@ inline void fdb_launch(void (*k)(P...), dim3 grid, dim3 block, uint32_t shmem, h
         LaunchList::Rec r{LaunchList::kKernel, (const void*)k, nullptr, grid, block, shmem, (uint32_t)L->argoff.size(),
                           (uint32_t)sizeof...(P)};
         (L->push_arg(static_cast<std::decay_t<P>>(a)), ...);
+        const bool timed = L->prof && (!L->timed_func || L->timed_func == (const void*)k);
+        hipEvent_t e0 = timed ? L->prof->take() : nullptr, e1 = timed ? L->prof->take() : nullptr;
+        if (e0 && e1) L->recs.push_back({LaunchList::kTimingRecord, nullptr, e0, dim3(), dim3(), 0, 0, 0});
         L->recs.push_back(r);
+        if (e0 && e1) {
+            L->recs.push_back({LaunchList::kTimingRecord, nullptr, e1, dim3(), dim3(), 0, 0, 0});
+            L->prof->spans->push_back({(const void*)k, {e0, e1}});
+        }
         return;
     }
     std::tuple<std::decay_t<P>...> vals(static_cast<std::decay_t<P>>(a)...);

@@ -116,7 +116,14 @@ typedef struct fdbcs_stats {
     double host_ms_prepare;
     double host_ms_record;
     double host_ms_submit;
-    int64_t graph_launches; /* batches submitted as one graph launch */
+    int64_t graph_launches; /* stage lists submitted as one graph launch (FDBCS_GRAPH=2) */
+    int64_t compact_launches; /* compactions whose copy kernel was timed (compact_bytes counts these only) */
+    /* Shapes of every batch, whatever the timing level (the roofline's byte models, roofline.py). */
+    int64_t merge_bytes_all;   /* algorithmic bytes of every delta-merge copy */
+    int64_t compact_bytes_all; /* algorithmic bytes of every compaction copy */
+    int64_t delta_sum;         /* delta-tier boundaries at the start of each batch's merge, summed */
+    int64_t base_sum;          /* base-tier boundaries after each batch, summed */
+    int64_t segments_sum;      /* union segments of committed writes, summed */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
@@ -207,6 +214,18 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
  * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead); 1-4 = the
  * endpoint sort's kernels (sample ranking, bucket count, scatter, per-bucket sort). */
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch);
+/* Per-kernel device time accumulated since fdbcs_reset_stats: timing level 3 brackets every kernel
+ * of every batch with events, level 1 the kernel named by fdbcs_set_timed_kernel on the sampled
+ * batches.  Entry `index` (0-based; FDBCS_E_INVALID past the last): demangled kernel name (without
+ * namespace and parameters) into name[cap], its timed launches and their total milliseconds. */
+int fdbcs_kernel_profile(fdbcs_conflict_set* cs, int32_t index, char* name, int32_t cap, int64_t* launches,
+                         double* ms);
+/* The kernel timed at level 1 (a name fdbcs_kernel_profile reported; NULL or "" = none). */
+int fdbcs_set_timed_kernel(fdbcs_conflict_set* cs, const char* name);
+/* Diagnostics: on != 0 queues a bounded hold kernel on every stream of the set, so batches
+ * submitted next wait behind it; on == 0 releases them, and they run back to back at the device's
+ * own rate (the device-bound throughput, free of the submitting thread). */
+int fdbcs_debug_hold(fdbcs_conflict_set* cs, int32_t on);
 
 const char* fdbcs_strerror(int status);
 

@@ -1,93 +1,171 @@
-"""Algorithmic bytes per launch of the hot kernels, for the bench roofline.
+"""Algorithmic bytes per launch of every pipeline kernel, for the bench roofline.
 
-The §8(d) model prices the work, not this implementation's traffic: a kernel's `achieved` GB/s is
-these bytes divided by its measured average launch time, and `frac` = achieved / 8 TB/s (MI355X
-HBM3E, /opt/skills/guides/MI355X_MICROARCH.md).  PMC counters (scripts/gpu_pmc.sh) give the
-bytes a kernel really moved; the two side by side show wasted re-reads.
+The model prices the work the kernel must do, not this implementation's traffic: `achieved` GB/s
+is these bytes divided by the kernel's measured average launch time (HIP events around the
+kernel on the stream it runs on), and `frac` = achieved / 8 TB/s (MI355X HBM3E,
+/opt/skills/guides/MI355X_MICROARCH.md).  PMC counters (scripts/gpu_pmc.sh) give the bytes a
+kernel really moved (`traffic`); the two side by side show wasted re-reads.
 
-Notation (§8(d)): P = 16 (key prefix bytes), L = 4 (length/offset bytes), V = 8 (version bytes),
-N = live history boundaries, F = 9 (fan-out of a 128-byte node holding 8 keys), l = search-tree
-levels resident in LDS (not fetched from HBM per lookup), R / W = read / write ranges, T = txns,
-E = 2 (R + W) endpoints.
+Notation (§8(d)): P = 16 (key prefix bytes), V = 8 (version bytes), D = 24 (a batch key record:
+prefix, length, tail offset), I = 32 (a sort item), N / Nd = base / delta history boundaries,
+R / W = read / write ranges, T = transactions, E = 2 (R + W) endpoints, G = R + W ranges,
+U = union segments of committed writes, X = candidate intra-batch edges.
 
-* D.CheckRead (k_check_tier<true>: the base tier, N = base boundaries; k_check_reads over both
-  tiers when the check is not split), per launch:
-    search    2R(P+L) + 2R*4 + 2R*128*max(0, ceil(log_F N) - l)
-    range-max R*2V + T
-* D.Sort (k_bucket_sort): one read and one write of every 32-byte sort item: 2 * 32 * E.
-* D.MergeWrite copy (k_merge_copy<BatchIns>) and compaction copy (k_merge_copy<CompactIns>):
-  32 B (key 16 + length/tail 8 + version 8) per kept boundary read, per inserted boundary read,
-  and per boundary of the result written; counted exactly by the engine from the device scalars
-  (fdbcs_stats.merge_bytes / compact_bytes).
+A lookup in a tier is priced by the nodes it must read: a 128-byte node per search-tree level
+(8 sampled keys), ceil(log_8(N / 64)) levels above the 64-boundary block plus the skey8 line and
+the 8 boundaries of the final group (3 lines); a lookup whose first two key bytes fall in a sparse
+slot of the tier's radix directory starts at level 0 (the directory entry, the level-0 group, the
+skey8 line and the boundary group: `dir_levels`).  Which path a lookup takes depends on the key
+distribution: the bench estimates the directory share from the prefilled history (shape_of).
 """
 from __future__ import annotations
 
+import json
 import math
+import os
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-P, L, V, F = 16, 4, 8, 9
+P, V, D, I = 16, 8, 24, 32
 NODE = 128
 
 
-def search_levels(n: float) -> int:
-    return max(1, math.ceil(math.log(max(n, 2.0), F)))
+def tree_levels(n: float) -> int:
+    """128-byte nodes one lookup reads descending the full tree over n boundaries."""
+    if n <= 0:
+        return 0
+    return max(1, math.ceil(math.log(max(n / 64.0, 2.0), 8))) + 2
 
 
-def check_bytes(reads: float, txns: float, n: float, lds_levels: int = 0) -> float:
-    """Algorithmic bytes of one read-check launch over `reads` ranges and a history of n boundaries."""
-    lv = max(0, search_levels(n) - lds_levels)
-    search = 2 * reads * (P + L) + 2 * reads * 4 + 2 * reads * NODE * lv
-    rmax = reads * 2 * V + txns
-    return search + rmax
+def lookup_bytes(n: float, dir_share: float) -> float:
+    if n <= 0:
+        return 0.0
+    direct = 8 + 3 * NODE
+    return dir_share * direct + (1 - dir_share) * tree_levels(n) * NODE
 
 
-def sort_bytes(items: float) -> float:
-    return 2 * 32 * items
-
-
-def kernel_entry(name: str, ms_total: float, launches: int, bytes_total: float) -> dict:
-    launches = max(1, int(launches))
-    avg_ms = ms_total / launches
-    per = bytes_total / launches
-    ach = per / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+def shape_of(batches, st: dict, history: int, dir_share: float = 1.0) -> dict:
+    """Average batch shape of the measured batches plus per-batch history sizes from the engine's
+    stats (fdbcs_stats: base_sum / delta_sum / segments_sum / intra_edges over `batches`)."""
+    nb = max(1, len(batches))
+    b = max(1, st.get("batches", 0))
+    T = sum(x.n_txn for x in batches) / nb
+    R = sum(x.n_reads for x in batches) / nb
+    W = sum(x.n_writes for x in batches) / nb
     return {
-        "kernel": name,
-        "launches": launches,
-        "total_ms": ms_total,
-        "avg_launch_ms": avg_ms,
-        "algorithmic_bytes_per_launch": per,
-        "achieved_GBps": ach,
-        "frac": ach / HBM_PEAK_GBS,
+        "T": T, "R": R, "W": W, "E": 2 * (R + W), "G": R + W,
+        "N": st.get("base_sum", 0) / b if st.get("base_sum") else float(history),
+        "Nd": st.get("delta_sum", 0) / b,
+        "U": st.get("segments_sum", 0) / b,
+        "X": st.get("intra_edges", 0) / max(1, b - st.get("intra_fallbacks", 0)),
+        "merge_bytes": st.get("merge_bytes_all", 0) / b,
+        "compact_bytes": st.get("compact_bytes_all", 0) / max(1, st.get("compactions", 0)),
+        "dir_share": dir_share,
     }
 
 
-def kernels_from_stats(st: dict, lds_levels: int = 0) -> dict:
-    """Per-kernel roofline entries from fdbcs_stats accumulated at timing level >= 1."""
-    out = {}
-    if st.get("check_launches", 0) > 0:
-        n = st["check_launches"]
-        avg_reads = st["check_reads"] / n
-        avg_hist = st["check_history"] / n
-        avg_txn = st["transactions"] / max(1, st["batches"])
-        out["check"] = kernel_entry("D.CheckRead: k_check_reads (both tiers) or k_check_tier<base> (split), search + range max",
-                                    st["ms_check_kernel"], n,
-                                    n * check_bytes(avg_reads, avg_txn, avg_hist, lds_levels))
-        out["check"]["model"] = {"reads": avg_reads, "history": avg_hist, "lds_levels": lds_levels,
-                                 "search_levels": search_levels(avg_hist)}
-    if st.get("sort_launches", 0) > 0:
-        out["sort"] = kernel_entry("k_bucket_sort (D.Sort)", st["ms_sort_kernel"], st["sort_launches"],
-                                   sort_bytes(st["sort_items"]))
-    if st.get("merge_launches", 0) > 0 and st.get("ms_merge_kernel", 0) > 0:
-        out["merge"] = kernel_entry("k_merge_copy<BatchIns> (D.MergeWrite delta-tier copy)", st["ms_merge_kernel"],
-                                    st["merge_launches"], st["merge_bytes"])
-    if st.get("compactions", 0) > 0 and st.get("ms_compact_kernel", 0) > 0:
-        out["compact"] = kernel_entry("k_merge_copy<CompactIns> (base-tier compaction copy)",
-                                      st["ms_compact_kernel"], st["compactions"], st["compact_bytes"])
+def kernel_bytes(name: str, s: dict):
+    """(bytes per launch, model text) of kernel `name` (engine demangled name) at shape s."""
+    T, R, W, E, G, N, Nd, U, X = (s[k] for k in ("T", "R", "W", "E", "G", "N", "Nd", "U", "X"))
+    S = min(E, max(1024.0, min(8192.0, 4 * math.ceil(E / 128))))
+    nb = min(2048.0, math.ceil(E / 128))
+    look_b, look_d = lookup_bytes(N, s["dir_share"]), lookup_bytes(Nd, 0.5)
+    if name.startswith("k_check_reads"):  # both tiers
+        return (2 * R * (D + look_b + look_d) + R * (4 + V) + 2 * R * V + T,
+                "2R(D + base lookup + delta lookup) + R(owner + snapshot) + range-max ends 2RV + T")
+    if name.startswith("k_check_tier<true"):
+        return (2 * R * (D + look_b) + R * (4 + V) + R * V + T, "base tier: 2R(D + lookup) + R(4+V) + RV + T")
+    if name.startswith("k_check_tier<false"):
+        return (2 * R * (D + look_d) + R * (4 + V) + R * V + T, "delta tier: 2R(D + lookup) + R(4+V) + RV + T")
+    if name == "k_sample":
+        return S * (D + I + 4), "S samples: key read, item written, rank"
+    if name == "k_bucket_count":
+        return E * (D + 2) + nb * (I + 4), "E keys read, E bucket ids written, splitters"
+    if name == "k_bucket_scatter":
+        return E * (2 + D + I) + nb * 8, "E (bucket id + key) read, E items written"
+    if name.startswith("k_bucket_sort"):
+        return 2 * I * E, "one read and one write of every 32-byte item"
+    if name.startswith("k_scan<3, fdbcs::PosScan>"):
+        return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
+    if name.startswith("k_scan<2, fdbcs::EdgePairScan>"):
+        return G * (8 + 24 + 8) + W * 8, "per range: 2 positions, class prefixes at both, slot/pair offsets"
+    if name == "k_edge_fill":
+        return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
+    if name == "k_resolve":
+        return T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16, "statuses, flags, offsets, edges and writer states, verdicts"
+    if name == "k_intra_report":
+        return R * 12, "per read: edge range, first conflict"
+    if name.startswith("k_scan2<1, fdbcs::CoverScan"):
+        return E * (4 + 8 + 1 + 4 + 2) + U * 8, "per position: meta, range ends, writer status, owner, flags; segments"
+    if name.startswith("k_seg_search"):
+        return U * 2 * (D + look_d) + U * 48, "per segment: 2 keys + 2 delta lookups; 6 words written"
+    if name.startswith("k_scan<3, fdbcs::SegSumScan>"):
+        return U * (24 + 24 + 4), "per segment: 3 counts read, 3 prefixes + tile index written"
+    if name.startswith("k_merge_copy<fdbcs::BatchIns"):
+        return s["merge_bytes"], "32 B per kept and inserted boundary read and per result boundary written (device scalars)"
+    if name.startswith("k_merge_copy<fdbcs::CompactIns"):
+        return s["compact_bytes"], "32 B per kept base / inserted delta boundary read and per result boundary written"
+    if name == "k_compact_search":
+        return Nd * (P + 8 + lookup_bytes(N, s["dir_share"]) + 17), "per delta boundary: key + lookup in the base, 2 words"
+    if name.startswith("k_scan<2, fdbcs::CompactSumScan>"):
+        return Nd * (8 + 8 + 1 + 24), "per delta boundary: lo, version, exact flag; 3 words written"
+    if name.startswith("k_scan<2, fdbcs::GcScan>"):
+        return N * (2 * V + 8) + N * 32, "versions (own + predecessor) and lengths read, kept boundaries rewritten"
+    if name == "k_epilogue":
+        n = Nd if Nd > 0 else N
+        return n * V + n / 8 * P * 2 + T * 2 + E * 2, "levels over the tier's versions, sampled keys, verdicts, scratch zeroing"
+    if name == "k_directory":
+        return 65537 * (4 + 17 * P), "65537 slots: binary search over level-0 samples"
+    if name == "k_conflict_output":
+        return T * 6, "per global transaction: map entry, status, conflict byte"
+    if name == "k_copy_bytes":
+        return T * 2, "report side outputs"
+    if name == "k_validate_sort":
+        return E * (I + 8), "sorted items and positions re-read"
+    return None, "no model"
+
+
+def entry(name: str, ms_total: float, launches: int, s: dict, st: dict = None) -> dict:
+    launches = max(1, int(launches))
+    avg_ms = ms_total / launches
+    b, model = kernel_bytes(name, s)
+    out = {"kernel": name, "launches": launches, "total_ms": ms_total, "avg_launch_ms": avg_ms,
+           "algorithmic_bytes_per_launch": b, "model": model}
+    if b is not None and avg_ms > 0:
+        ach = b / (avg_ms * 1e-3) / 1e9
+        out["achieved_GBps"] = ach
+        out["frac"] = ach / HBM_PEAK_GBS
+    else:
+        out["achieved_GBps"] = out["frac"] = None
     return out
 
 
-def dominant(kernels: dict) -> str | None:
-    """The kernel with the largest total device time."""
-    if not kernels:
+def kernel_table(kprof: dict, s: dict, st: dict = None) -> dict:
+    """Every kernel of the profile pass with its roofline entry, largest total device time first."""
+    rows = {k: entry(k, v["ms"], v["launches"], s, st) for k, v in kprof.items() if not k.startswith("k_hold")}
+    return dict(sorted(rows.items(), key=lambda kv: -kv[1]["total_ms"]))
+
+
+SORT_KERNELS = ("k_sample", "k_bucket_count", "k_bucket_scatter", "k_bucket_sort", "k_sort_")
+
+
+def sort_phase(table: dict) -> dict | None:
+    """D.Sort as one unit: the sort kernels' average launch times summed per batch."""
+    ks = {k: v for k, v in table.items() if k.startswith(SORT_KERNELS)}
+    if not ks:
         return None
-    return max(kernels, key=lambda k: kernels[k]["total_ms"])
+    per_batch = sum(v["total_ms"] for v in ks.values()) / max(v["launches"] for v in ks.values())
+    return {"kernels": sorted(ks), "ms_per_batch": per_batch}
+
+
+def pmc_traffic(root: str, workload: str, kernel: str, txns: int, history: int):
+    """HBM bytes per launch of `kernel` from the PMC passes of the SAME configuration
+    (profiles/pmc_<workload>_<txns>_<history>.json, written by scripts/pmc_summary.py: FETCH_SIZE
+    x2 gfx950 correction + WRITE_SIZE, each in its own rocprofv3 pass), or None."""
+    f = os.path.join(root, "profiles", f"pmc_{workload}_{txns}_{history}.json")
+    if not os.path.exists(f):
+        return None
+    try:
+        with open(f) as fh:
+            return json.load(fh).get("bytes_per_launch", {}).get(kernel)
+    except Exception:
+        return None

@@ -535,17 +535,19 @@ def test_empty_batches(engine, oracle_mod):
         now += 4
 
 
-@pytest.mark.parametrize("knobs", [{"FDBCS_FUSE_EPILOGUE": "1"}, {"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
+# Every engine knob that selects a different kernel or submission path (DESIGN.md §5 "Engine knobs")
+# is parity-tested here; knobs measured slower and not kept were deleted with their code.
+@pytest.mark.parametrize("knobs", [{"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
                                    {"FDBCS_SORT_WIN": "0"},
                                    {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_SORTED_READS": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
+                                   {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
-                                   {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_UPLOAD": "kernel"},
-                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}])
+                                   {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
+                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
-    """Non-default pipeline variants kept for measurement stay exact: the epilogue
-    fused into the merge copy, the unsplit read check, and long-key sorting without LDS windows."""
+    """Non-default pipeline variants kept for measurement stay exact: the unsplit and
+    split read checks, the one-wave check, long-key sorting without LDS windows, stage graphs, the
+    helper submitting thread, one candidate edge per writer, the serial stream layout."""
     saved = {k: os.environ.get(k) for k in knobs}
     os.environ.update(knobs)
     try:
@@ -568,3 +570,46 @@ def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
         assert ce == {t: sorted(v) for t, v in co.items()}
         now += 4
     assert eng.cs.history_size() > 0
+
+
+def test_timing_level_changes_with_batches_in_flight(engine, oracle_mod):
+    """Workspace reuse stays ordered when the timing level (and with it the stream layout) changes
+    while more batches than workspaces are in flight (ev_b of a level-2 batch)."""
+    cs = engine.ConflictSet(0)
+    cs.set_gc_interval(3)
+    ora = oracle_mod.OracleConflictSet()
+    rng = np.random.default_rng(2024)
+    now = 10
+    levels = [2, 2, 2, 2, 0, 0, 0, 0, 1, 2, 0, 3, 3, 0, 0, 2, 1, 0]
+    inflight = []
+    for i, lv in enumerate(levels):
+        cs.set_timing(lv)
+        pb = W.random_small_batch(rng, 300, alphabet=5, max_len=3, now=now, staleness=10)
+        b = engine.ConflictBatch(cs)
+        b.add_packed(pb)
+        b.detect_async(now, now - 8)
+        want, _ = ora.detect(pb, now, now - 8)
+        inflight.append((b, want, i))
+        if len(inflight) > 5:  # keep more batches in flight than there are workspaces (3)
+            bb, ww, j = inflight.pop(0)
+            assert (bb.wait() == ww).all(), j
+            bb.close()
+        now += 3
+    for bb, ww, j in inflight:
+        assert (bb.wait() == ww).all(), j
+        bb.close()
+    assert cs.kernel_profile(), "timing level 3 recorded per-kernel events"
+    cs.close()
+
+
+def test_conflict_output_rejects_duplicate_ids(engine):
+    """fdbcs_batch_set_conflict_output: two batch transactions may not share one global index (a
+    duplicate would silently drop a conflict byte from the device combine)."""
+    cs = engine.ConflictSet(0)
+    pb = PackedBatch.from_transactions([CommitTransaction([KeyRange(b"a", b"b")], [], 5) for _ in range(3)])
+    b = engine.ConflictBatch(cs)
+    b.add_packed(pb)
+    with pytest.raises(engine.FdbcsError):
+        b.set_conflict_output(np.array([0, 2, 0], np.int32), 4, 1 << 20)
+    b.close()
+    cs.close()
