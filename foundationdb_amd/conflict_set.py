@@ -89,6 +89,7 @@ class Stats(ctypes.Structure):
         ("delta_sum", ctypes.c_int64),
         ("base_sum", ctypes.c_int64),
         ("segments_sum", ctypes.c_int64),
+        ("sort_big_buckets", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -179,15 +179,18 @@ struct fdbcs_conflict_set {
 
     int inflight = 0;
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
-    int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket (testing knob; 0 = default)
-    int sample_per = 0;     // FDBCS_SORT_SAMPLES: splitter samples per bucket (0 = default 4)
+    int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket on average (0 = kSortTarget)
+    bool sort_cold = false; // FDBCS_SORT_COLD=1: splitters from every batch's own samples (tests)
+    DBuf quant;             // the sort's splitter source, two tables: quantiles of the last batch of
+    int qcur = 0;           // >= kQuantMinE endpoints in table qcur; the next such batch writes the other
+    bool quant_valid = false;
+    int64_t sort_big_buckets = 0;  // buckets past kSlab so far (host view, from the published scalars)
     bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
     int check_version = 6;    // FDBCS_CHECK: read-check kernel (1: the four lookups of a read in one wave;
                               // 6: the base and delta lookups in separate waves)
-    bool sort_win = true;     // FDBCS_SORT_WIN=0: no LDS tail windows in the bucket sort (A/B)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
     bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
@@ -391,15 +394,20 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(rconf, R);
     TAKE(status, T);
     TAKE(first_conf, 4 * T);
-    TAKE(items[0], sizeof(SortItem) * E);
-    TAKE(items[1], sizeof(SortItem) * E);
-    TAKE(splitters, sizeof(SortItem) * 2048);
-    TAKE(samples, sizeof(SortItem) * 8192);
-    TAKE(bucket, 2 * E);
-    TAKE(bcount, 4 * 2048);
-    TAKE(bcursor, 4 * 2048);
-    TAKE(boff, 4 * 2052);
-    TAKE(srank, 4 * (8192 + 64));
+    // the sort's slab holds kSlab endpoints per bucket for the buckets a batch of E endpoints
+    // takes at the default target (sort_bucket_count clamps smaller targets to it)
+    const int64_t slab_buckets = std::min<int64_t>(kSortMaxBuckets, (E + kSortTarget - 1) / kSortTarget + 1);
+    TAKE(items, sizeof(SortItem) * E);
+    TAKE(scnt0, 8 * kSortMaxBuckets);
+    TAKE(scnt1, 8 * kSortMaxBuckets);
+    TAKE(slab, sizeof(SortItem) * kSlab * slab_buckets);
+    TAKE(ovf, sizeof(SortItem) * E);
+    TAKE(ovf_b, 4 * E);
+    TAKE(big, sizeof(SortItem) * E);
+    TAKE(big_p, 4 * E);
+    TAKE(samples, sizeof(SortItem) * kMaxSample);
+    TAKE(srank, 4 * (kMaxSample + 64));
+    w.slab_buckets = (int32_t)slab_buckets;
     TAKE(pos, 4 * E);
     TAKE(pmeta, 4 * E);
     TAKE(cwb, 4 * (E + 1));
@@ -442,9 +450,9 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
     HIPOK(hipMemsetAsync(w.rconf, 0, R, cs->stream));
     HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
-    HIPOK(hipMemsetAsync(w.bcount, 0, 4 * 2048, cs->stream));
-    HIPOK(hipMemsetAsync(w.bcursor, 0, 4 * 2048, cs->stream));
-    HIPOK(hipMemsetAsync(w.srank, 0, 4 * (8192 + 64), cs->stream));
+    HIPOK(hipMemsetAsync(w.scnt0, 0, 8 * kSortMaxBuckets, cs->stream));
+    HIPOK(hipMemsetAsync(w.scnt1, 0, 8 * kSortMaxBuckets, cs->stream));
+    HIPOK(hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), cs->stream));
     HIPOK(hipMemsetAsync(w.bsc, 0, sizeof(BatchScalars), cs->stream));
     // compaction arrays are shared (stage B only)
     if (k >= 1) {
@@ -973,13 +981,12 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     cs->device = device;
     if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
     if (const char* v = getenv("FDBCS_SORT_BUCKET")) cs->bucket_target = atoi(v);
-    if (const char* v = getenv("FDBCS_SORT_SAMPLES")) cs->sample_per = atoi(v);
+    if (const char* v = getenv("FDBCS_SORT_COLD")) cs->sort_cold = v[0] == '1';
     if (const char* v = getenv("FDBCS_TRACE")) cs->trace = v[0] == '1';
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
     if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2';
-    if (const char* v = getenv("FDBCS_SORT_WIN")) cs->sort_win = v[0] != '0';
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
@@ -1005,6 +1012,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     }
 
     int rc = cs->scal.ensure(sizeof(Scalars));
+    if (!rc) rc = cs->quant.ensure(2 * sizeof(SplitKey) * kQuant);
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
     if (!rc && cs->directory) {  // zeroed: epoch 0 entries are never trusted
         rc = cs->edir.ensure(8 * ((size_t)kDirSlots + 1));
@@ -1050,6 +1058,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     for (auto& set : cs->ws)
         for (auto& x : set) x.release();
     cs->scal.release();
+    cs->quant.release();
     cs->trace_buf.release();
     cs->hold.release();
     for (BatchSlot* sl : cs->pool) release_slot(sl);
@@ -1673,16 +1682,31 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(hipStreamSynchronize(s));
         unsigned long long init[kTrSlots];
         for (int i = 0; i < kTrSlots; i++)
-            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin || i == kTrResBegin) ? ~0ull : 0ull;
+            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin || i == kTrResBegin ||
+                       i == kTrPartBegin || i == kTrBktBegin)
+                          ? ~0ull
+                          : 0ull;
         HIPOK(hipMemcpy(w.trace, init, sizeof(init), hipMemcpyHostToDevice));
     }
-    launch_sample(sa, bd, w, cs->bucket_target, cs->sample_per);
-    int sorted = 0;
-    launch_sort_points(sa, bd, w, cs->bucket_target, cs->sample_per, &sorted, rec(kPhSortBegin, 1),
-                       rec(kPhSortEnd, 1), cs->sort_win && b->max_len > (int32_t)kSortNxLen);
+    // D.Sort and the sorted positions.  Splitters: the quantiles the last batch of >= kQuantMinE
+    // endpoints left (stage A runs in batch order on one stream), or this batch's ranked samples
+    // when there are none yet (cold start)
+    {
+        const int64_t E = 2 * (R + W);
+        const int nbk = sort_bucket_count(E, cs->bucket_target, w.slab_buckets);
+        const bool cold = nbk > 1 && (cs->sort_cold || !cs->quant_valid);
+        const bool write_quant = E >= kQuantMinE;
+        SplitKey* qt = (SplitKey*)cs->quant.p;
+        launch_sort(sa, bd, w, qt + cs->qcur * kQuant, write_quant ? qt + (cs->qcur ^ 1) * kQuant : nullptr, cold,
+                    cs->bucket_target, b->max_len > (int32_t)kSortNxLen, cs->validate, rec(kPhSortBegin, 1),
+                    rec(kPhSortEnd, 1));
+        if (write_quant) {
+            cs->qcur ^= 1;
+            cs->quant_valid = true;
+        }
+    }
     mark(kPhSort);
-    launch_positions(sa, bd, w, sorted);
-    if (cs->validate) launch_validate_sort(sa, bd, w, sorted);
+    if (cs->validate) launch_validate_sort(sa, bd, w);
     launch_edges(sa, bd, w);
     if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_a[wp], sa);
     mark(kPhEdges);
@@ -1875,26 +1899,18 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             unsigned long long tr[kTrSlots];
             HIPOK(hipMemcpy(tr, cs->trace_buf.p, sizeof(tr), hipMemcpyDeviceToHost));
             auto us = [&](int a, int z) { return (double)((long long)(tr[z] - tr[a])) / 100.0; };  // 100 MHz
-            {
-                const int E = 2 * (b->R() + b->W());
-                const int nb = E ? sort_buckets(E, cs->bucket_target) : 1;  // as launch_sort_points
-                std::vector<int32_t> bo(nb + 1);
-                HIPOK(hipMemcpy(bo.data(), cs->work[b->wp].boff, 4 * (nb + 1), hipMemcpyDeviceToHost));
-                int mx = 0, over = 0;
-                for (int k = 0; k < nb; k++) {
-                    const int sz = bo[k + 1] - bo[k];
-                    mx = std::max(mx, sz);
-                    over += sz > 512;
-                }
-                fprintf(stderr, "fdbcs trace: %d buckets for %d endpoints, largest %d, over 512: %d\n", nb, E, mx,
-                        over);
-            }
             fprintf(stderr,
                     "fdbcs trace: sample %.2f us, check %.2f us (check starts %+.2f us after sample); epilogue "
                     "levels %.2f, zero %.2f, host %.2f, fence %.2f us\n",
                     us(kTrSampleBegin, kTrSampleEnd), us(kTrCheckBegin, kTrCheckEnd), us(kTrSampleBegin, kTrCheckBegin),
                     us(kTrEpiBegin, kTrEpiLevels), us(kTrEpiLevels, kTrEpiZero), us(kTrEpiZero, kTrEpiHost),
                     us(kTrEpiHost, kTrEpiFence));
+            fprintf(stderr,
+                    "fdbcs trace: sort partition fill %.2f, search %.2f, end %.2f us; bucket prologue %.2f, "
+                    "sorted %.2f, end %.2f us (partition start to bucket start %.2f us)\n",
+                    us(kTrPartBegin, kTrPartFill), us(kTrPartBegin, kTrPartSearch), us(kTrPartBegin, kTrPartEnd),
+                    us(kTrBktBegin, kTrBktPrologue), us(kTrBktBegin, kTrBktSorted), us(kTrBktBegin, kTrBktEnd),
+                    us(kTrPartBegin, kTrBktBegin));
             fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
                     us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),
                     us(kTrResRounds, kTrResEnd));
@@ -2005,6 +2021,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             st.sort_items += 2 * (int64_t)(b->R() + b->W());
         }
         st.gc_runs += b->gc_ran ? 1 : 0;
+        st.sort_big_buckets += b->h_scal->sort_big;
         if (b->compacted) {
             st.compactions += 1;
             // kept base boundaries read, delta boundaries inserted read, result written
@@ -2074,7 +2091,7 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
 }
 
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch) {
-    if (!b || !us_per_launch || reps <= 0 || which < 0 || which > 4) return FDBCS_E_INVALID;
+    if (!b || !us_per_launch || reps <= 0 || which < 0 || which > 2) return FDBCS_E_INVALID;
     if (!b->cs) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
     HIPOK(hipSetDevice(cs->device));
@@ -2090,8 +2107,9 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     const Tier base{hist_of(cs, cs->cur), levels_of(cs, cs->cur), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->nd, kHole};
     if (which >= 1) {  // the sort kernels
-        HIPOK(debug_time_sort(cs->stream, b->bd, w, cs->bucket_target, cs->sample_per,
-                              cs->sort_win && b->max_len > (int32_t)kSortNxLen, which, reps, us_per_launch));
+        if (!cs->quant_valid) return FDBCS_E_STATE;  // warm splitters only: detect a batch first
+        HIPOK(debug_time_sort(cs->stream, b->bd, w, (SplitKey*)cs->quant.p + cs->qcur * kQuant, cs->bucket_target,
+                              b->max_len > (int32_t)kSortNxLen, which, reps, us_per_launch));
         return FDBCS_OK;
     }
     hipEvent_t e0, e1;

@@ -12,7 +12,6 @@ namespace fdbcs {
 
 constexpr int kBlock = 256;        // default workgroup: 4 waves of 64
 constexpr int kWG = 1024;          // single-workgroup kernels (scans, resolution)
-constexpr int kSortThreads = 512;  // bucket-sort workgroups: 8 waves, one endpoint per thread
 constexpr int kSortTile = 4096;    // endpoints per LDS sort tile (128 KiB of LDS)
 constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
 constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)
@@ -79,6 +78,8 @@ struct Scalars {
     int32_t debug_error;   // copied from the batch's BatchScalars by the epilogue (host view only)
     int32_t intra_rounds;  // copied from BatchScalars::rounds by the epilogue (host view only)
     int64_t intra_edges;   // copied from BatchScalars::n_edges (host view only; overflow -> -1)
+    int32_t sort_big;      // copied from BatchScalars::sort_big (host view only)
+    int32_t sort_pad;
 };
 
 // Device scalars of one batch workspace (two workspaces alternate, so batch i+1's history-
@@ -89,6 +90,8 @@ struct BatchScalars {
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
     int32_t pre_done;      // k_resolve workgroups done with the pre-pass (reset by the epilogue)
+    int32_t ovf_n;         // sort: endpoints past their bucket's slab (reset by the epilogue)
+    int32_t sort_big;      // sort: buckets past the slab, sorted by the workgroup path (reset by the epilogue)
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -126,20 +129,46 @@ struct BatchDev {
     uint8_t* tail;       // key bytes beyond 16
 };
 
+// D.Sort geometry (kernels.hip): a bucket holds kSortTarget endpoints on average and is sorted in
+// registers by one wave up to kSlab endpoints; splitters are projections of the quantiles of the
+// last sorted batch (kQuant of them), or of this batch's ranked samples at a cold start.
+constexpr int kSortTarget = 64;
+constexpr int kSlab = 256;
+constexpr int kSortMaxBuckets = 4096;
+constexpr int kQuant = 4096;
+constexpr int kQuantMinE = 2048;  // batches with fewer endpoints leave the quantiles as they are
+constexpr int kMaxSample = 8192;
+// A splitter: the projection of an endpoint onto its first kSplitBytes key bytes (big-endian
+// words, zero past the key), min(len, kSplitBytes + 1), and for keys no longer than kSplitBytes
+// the class and id (meta).  Projections are monotone in the full order (keys tied on their first
+// kSplitBytes bytes share one), so a bucket boundary never separates endpoints the order needs the
+// bytes beyond the window for.
+constexpr int kSplitWords = 8;
+constexpr int kSplitBytes = 8 * kSplitWords;
+struct SplitKey {
+    uint64_t w[kSplitWords];
+    uint32_t len, meta;
+};
+
 // Per-set scratch, sized for the largest batch seen.
 struct Work {
     uint8_t* hist_conf;    // [T]
     uint8_t* rconf;        // [R]
     uint8_t* status;       // [T]
     int32_t* first_conf;   // [T]
-    SortItem* items[2];    // [E] sorted endpoints / bucket-sort scratch
-    SortItem* splitters;   // [2047] sample-sort splitters
-    SortItem* samples;     // [8192] the sample items (written by k_sample, read by k_bucket_count)
-    uint16_t* bucket;      // [E] bucket of each endpoint
-    int32_t* bcount;       // [2048] endpoints per bucket (zeroed per batch)
-    int32_t* bcursor;      // [2048] scatter cursors (zeroed per batch)
-    int32_t* boff;         // [2049] bucket offsets
-    int32_t* srank;        // [8192 + 64] sample ranks, then the done counter (zeroed per batch)
+    // D.Sort (k_sort_partition / k_sort_bucket): endpoints partitioned into buckets between
+    // splitters, each bucket sorted by one wave (or its workgroup past kSlab endpoints)
+    SortItem* items;       // [E] sorted endpoints (FDBCS_VALIDATE only)
+    uint64_t* scnt0;       // [kSortMaxBuckets] per bucket: endpoints | write-begins << 32 (zeroed per batch)
+    uint64_t* scnt1;       // [kSortMaxBuckets] per bucket: read-begins | write-ends << 32 (zeroed per batch)
+    SortItem* slab;        // [slab_buckets * kSlab] each bucket's first kSlab endpoints
+    int32_t slab_buckets;  // buckets the slab holds
+    SortItem* ovf;         // [E] endpoints past their bucket's slab
+    int32_t* ovf_b;        // [E] their buckets
+    SortItem* big;         // [E] a big bucket's endpoints, gathered (workgroup path)
+    int32_t* big_p;        // [E] a big bucket's endpoint ids in sorted order (workgroup path)
+    SortItem* samples;     // [kMaxSample] cold start: sample items (k_sample)
+    int32_t* srank;        // [kMaxSample + 64] cold start: sample ranks (zeroed per batch)
     int32_t* pos;          // [2(R+W)] sorted position of each endpoint
     uint32_t* pmeta;       // [E] meta of the item at each position
     int32_t* cwb;          // [E+1] write-begins before each position
@@ -198,6 +227,8 @@ enum TraceSlot {
     kTrSampleBegin, kTrSampleEnd, kTrCheckBegin, kTrCheckEnd,
     kTrEpiBegin, kTrEpiLevels, kTrEpiZero, kTrEpiHost, kTrEpiFence, kTrEpiEnd,
     kTrResBegin, kTrResPre, kTrResWait, kTrResRounds, kTrResEnd,
+    kTrPartBegin, kTrPartFill, kTrPartSearch, kTrPartEnd,
+    kTrBktBegin, kTrBktPrologue, kTrBktSorted, kTrBktEnd,
     kTrSlots
 };
 __device__ __forceinline__ void trace_min(unsigned long long* tr, int slot) {
@@ -219,11 +250,18 @@ struct Tier {
     int64_t hdr;       // version below the first boundary (kHole for the delta)
 };
 // Per batch, two stages on two streams:
-//   A (history-independent): launch_sample, launch_sort_points, launch_positions, launch_edges;
+//   A (history-independent): launch_sort (D.Sort + positions), launch_edges;
 //   B (reads/writes the history, in batch order): launch_check, launch_resolve, launch_combine,
 //     launch_merge, launch_compact/gc, launch_epilogue.
-// Sample ranking for the sort's splitters.
-void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per);
+// D.Sort and the sorted positions (replaces the sample sort + position scan): splitters from the
+// quantile table `quant` (cold: written first from this batch's ranked samples, k_sample +
+// k_quant_cold), then k_sort_partition and k_sort_bucket.  quant_out: the other table, which
+// receives this batch's quantiles for the next batch (null: keep).  long_keys: the batch has keys
+// longer than kSortNxLen (tail comparisons possible).
+void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
+                 int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end);
+// Buckets of a batch of E endpoints (target 0 = kSortTarget), within the workspace slab.
+int sort_bucket_count(int64_t E, int target, int slab_buckets);
 // D.CheckRead against the history the previous batch left.
 // check_version: 6 = base and delta lookups in separate waves (default), 1 = in one wave.
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
@@ -233,19 +271,12 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
 // long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
                        const uint8_t* htail, bool long_keys = false, bool lead_rmax = false);
-// bucket_target: endpoints per sample-sort bucket (0 = default 128; tests force oversized buckets).
-// sample_per: splitter samples per bucket (0 = default 8).
-// alg: per-bucket sort, 0 = rank count in LDS, 1 = bitonic network (both exact; a tuning knob).
-// sort_begin / sort_end (optional): events around the per-bucket sort kernel (roofline timing).
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
-                        int* result_buffer, hipEvent_t sort_begin = nullptr, hipEvent_t sort_end = nullptr,
-                        bool long_keys = true);
-// Sample-sort buckets for E endpoints at `target` endpoints per bucket (0 = default).
-int sort_buckets(int E, int target);
-void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
-hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
+// Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
+// k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
+hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,
                            bool long_keys, int which, int reps, double* us);
-void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf);
+// FDBCS_VALIDATE: the sorted endpoints are in order and the positions invert the permutation.
+void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);
 // verdict_out: the batch's host-mapped verdict bytes (the epilogue publishes them with the flag).
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out);

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <vector>
 #include <limits.h>
 
@@ -817,28 +818,6 @@ __device__ __forceinline__ bool item_less_total(const SortItem& a, const SortIte
     return (a.hi < b.hi) | (hi_eq & ((a.lo < b.lo) | (lo_eq & aux_lt)));
 }
 
-// Merge-path split + serial merge of A[0,lenA) and B[0,lenB) (stable, A first on ties): writes
-// outputs [d, d+count) of the merged sequence to dst[0, count).
-__device__ __forceinline__ void merge8_to(const SortItem* A, int lenA, const SortItem* B, int lenB, int d,
-                                          SortItem* dst, int count, const uint8_t* arena) {
-    int lo = d - lenB > 0 ? d - lenB : 0;
-    int hi = d < lenA ? d : lenA;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (!item_less_total(B[d - mid - 1], A[mid], arena))
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    int i = lo, j = d - lo;
-    for (int k = 0; k < count; k++) {
-        const bool takeA = (j >= lenB) || (i < lenA && !item_less_total(B[j], A[i], arena));
-        dst[k] = takeA ? A[i] : B[j];
-        i += takeA ? 1 : 0;
-        j += takeA ? 0 : 1;
-    }
-}
-
 // Rank counting: rk[k] += number of items of sh[0, cnt) ordered before mine[k].  Branch-free on
 // the 16-byte prefix and the (length, class, id) tie-break word, 8 LDS reads in flight; a
 // comparison that needs the bytes beyond the prefix (both keys longer than 16 bytes, equal
@@ -876,19 +855,8 @@ __device__ __noinline__ int rank_exact(const SortItem* sh, int cnt, SortItem min
     return r;
 }
 
-// ---- sample sort of the batch endpoints (D.Sort, SkipList.cpp:161-208)
-//
-// 1. k_sample: S evenly spaced endpoints are ranked against each other (each workgroup compares
-//    every sample with a 64-sample slice and adds partial ranks).
-// 2. k_bucket_count: every workgroup picks the nb-1 splitters (the samples of rank k*S/nb) straight
-//    from the ranks into LDS; each endpoint's bucket = number of splitters <= it; per-bucket counts.
-// 3. k_bucket_scatter: bucket offsets (prefix of the counts, recomputed per workgroup) and scatter.
-// 4. k_bucket_sort: one workgroup per bucket (~256 endpoints) ranks its items in LDS and writes
-//    each to its final slot; oversized buckets rank 1024-item chunks, then merge through memory.
-constexpr int kMaxBuckets = 2048;
-constexpr int kMaxSample = 8192;
+// ---- cold start of the sort: samples of the batch ranked against each other
 constexpr int kSampleSlice = 64;
-constexpr int kBucketTarget = 128;
 
 __device__ __forceinline__ int sample_pos(int i, int E, int S) { return (int)(((int64_t)i * E) / S); }
 
@@ -923,16 +891,6 @@ __global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
         if (cnt[0]) atomicAdd(&c.srank[i], cnt[0]);
     }
     if (threadIdx.x == 0) trace_max(c.trace, kTrSampleEnd);
-}
-
-// Number of samples for nb buckets: 4 per bucket by default.  With 8 the largest of ~550 buckets
-// stays well under the one-pass size, with 4 one bucket in ~3 batches passes it at C2 and takes
-// the chunked path, but ranking a quarter of the sample pairs wins overall (C4 20.1-20.2M vs
-// 19.5-19.6M txns/s, C3 +1 %, C2 +1 %).  per: FDBCS_SORT_SAMPLES (0 = default).
-inline int sample_count(int E, int nb, int per) {
-    int S = (per > 0 ? per : 4) * nb;
-    S = S < 1024 ? 1024 : (S > kMaxSample ? kMaxSample : S);
-    return S > E ? E : S;
 }
 
 // D.CheckRead (stage B: reads the history as the previous batch left it), kReadLanes lanes per
@@ -975,397 +933,6 @@ __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c
     if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
 }
 
-__device__ __forceinline__ int bucket_of(const SortItem& it, const SortItem* spl, int nsplit, const uint8_t* arena) {
-    int lo = 0, hi = nsplit;  // number of splitters <= it (items are distinct: < suffices)
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (!item_less_total(it, spl[mid], arena))
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
-__global__ __launch_bounds__(kBlock) void k_bucket_count(BatchDev b, const int32_t* srank, const SortItem* samples,
-                                                         int nb, int S, uint16_t* bucket, int32_t* bcount,
-                                                         const uint8_t* arena) {
-    __shared__ SortItem spl[kMaxBuckets - 1];
-    __shared__ int hist[kMaxBuckets];
-    const int E = 2 * (b.R + b.W);
-    // this thread's endpoint first: its key loads overlap the splitter fill below
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    SortItem it{};
-    if (p < E) it = make_item(b, p);
-    // splitter k-1 is the sample of rank k*S/nb (ranks are distinct: items are totally ordered);
-    // the sample items come ready-made from k_sample, four ranks and items in flight per thread
-    // (no dependent key and tail loads per sample)
-    for (int q0 = threadIdx.x; q0 < S; q0 += 4 * blockDim.x) {
-        int r[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int q = q0 + u * blockDim.x;
-            r[u] = q < S ? srank[q] : -1;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int q = q0 + u * blockDim.x;
-            const int k = (int)(((int64_t)r[u] * nb + S - 1) / S);
-            if (q < S && k >= 1 && k < nb && (int)(((int64_t)k * S) / nb) == r[u]) spl[k - 1] = samples[q];
-        }
-    }
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    if (p < E) {
-        const int k = bucket_of(it, spl, nb - 1, arena);
-        bucket[p] = (uint16_t)k;
-        atomicAdd(&hist[k], 1);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += blockDim.x)
-        if (hist[i]) atomicAdd(&bcount[i], hist[i]);
-}
-
-// off[k] = sum of bcount[0..k) for k <= nb (nb <= kMaxBuckets), by one block.
-__device__ __forceinline__ void bucket_prefix(const int32_t* bcount, int nb, int* off) {
-    __shared__ int wsum[kBlock / 64];
-    constexpr int per = (kMaxBuckets + kBlock) / kBlock;  // covers nb + 1 entries
-    const int a = threadIdx.x * per;
-    int v[per];
-    int sum = 0;
-#pragma unroll
-    for (int k = 0; k < per; k++) {
-        v[k] = a + k < nb ? bcount[a + k] : 0;
-        sum += v[k];
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    int before = 0;
-    for (int q = 0; q < wid; q++) before += wsum[q];
-    int run = before + x - sum;
-#pragma unroll
-    for (int k = 0; k < per; k++) {
-        if (a + k <= nb) off[a + k] = run;
-        run += v[k];
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(kBlock) void k_bucket_scatter(BatchDev b, const uint16_t* bucket, const int32_t* bcount,
-                                                           int32_t* bcursor, int32_t* boff_out, int nb, SortItem* out) {
-    __shared__ int off[kMaxBuckets + 1];
-    __shared__ int local[kMaxBuckets];
-    const int E = 2 * (b.R + b.W);
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    // this thread's bucket and endpoint first: their loads overlap the bucket prefix
-    const int kb = p < E ? (int)bucket[p] : -1;
-    SortItem it{};
-    if (p < E) it = make_item(b, p);
-    bucket_prefix(bcount, nb, off);
-    if (blockIdx.x == 0)
-        for (int k = threadIdx.x; k <= nb; k += blockDim.x) boff_out[k] = off[k];
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) local[k] = 0;
-    __syncthreads();
-    int k = -1, slot = 0;
-    if (p < E) {
-        k = kb;
-        slot = atomicAdd(&local[k], 1);  // order inside a bucket is irrelevant: it is sorted next
-    }
-    __syncthreads();
-    // one global reservation per (workgroup, bucket)
-    for (int q = threadIdx.x; q < nb; q += blockDim.x) {
-        const int c = local[q];
-        local[q] = c ? atomicAdd(&bcursor[q], c) : 0;
-    }
-    __syncthreads();
-    if (p < E) out[off[k] + local[k] + slot] = it;
-}
-
-// Sentinel-aware order for the bitonic network: padding items sort after every item.
-__device__ __forceinline__ bool lt_pad(const SortItem& x, const SortItem& y, const uint8_t* arena) {
-    if (is_pad(x) || is_pad(y)) return is_pad(y) && !is_pad(x);
-    return item_less_total(x, y, arena);
-}
-
-__device__ __forceinline__ SortItem shfl_xor_item(const SortItem& x, int j) {
-    SortItem y;
-    y.hi = __shfl_xor(x.hi, j, 64);
-    y.lo = __shfl_xor(x.lo, j, 64);
-    y.len = __shfl_xor(x.len, j, 64);
-    y.tail = __shfl_xor(x.tail, j, 64);
-    y.meta = __shfl_xor(x.meta, j, 64);
-    y.nx = __shfl_xor(x.nx, j, 64);
-    return y;
-}
-
-// Bitonic network over the workgroup, one item per thread (x = element threadIdx.x; L a power of
-// two <= blockDim.x; threads >= L sit out).  Partners closer than a wave exchange through
-// cross-lane shuffles, farther ones through LDS.  EXACT = false compares (prefix, tie-break word)
-// branch-free and only flags comparisons that would need the bytes beyond the prefix; the caller
-// reruns with EXACT = true when any lane flagged one.
-template <bool EXACT>
-__device__ bool reg_bitonic(SortItem& x, SortItem* sh, int L, const uint8_t* arena) {
-    const int t = threadIdx.x;
-    const bool active = t < L;
-    bool tie = false;
-    for (int k = 2; k <= L; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            SortItem y;
-            if (j >= 64) {
-                if (active) sh[t] = x;
-                __syncthreads();
-                if (active) y = sh[t ^ j];
-                __syncthreads();
-            } else {
-                y = shfl_xor_item(x, j);
-            }
-            if (!active) continue;
-            // ascending runs keep the smaller item at the lower position
-            const bool want_smaller = ((t & j) == 0) == ((t & k) == 0);
-            bool y_less;
-            if (EXACT) {
-                y_less = lt_pad(y, x, arena);
-            } else {
-                const uint64_t ax = is_pad(x) ? ~0ull : item_aux(x), ay = is_pad(y) ? ~0ull : item_aux(y);
-                const bool heq = y.hi == x.hi, leq = y.lo == x.lo;
-                y_less = (y.hi < x.hi) | (heq & ((y.lo < x.lo) | (leq & (ay < ax))));
-                tie |= heq && leq && item_tie(x, y) && !is_pad(x) && !is_pad(y);
-            }
-            if (want_smaller == y_less) x = y;
-        }
-    }
-    return tie;
-}
-
-constexpr int kBitonicMax = kSortThreads;  // endpoints sorted in one pass by one workgroup
-
-// Tail windows: bytes [16, 16 + 8 kTailWin) of a bucket's long keys, as big-endian words zero-padded
-// past each key's end, staged in LDS once per item so the comparisons among keys that share their
-// 16-byte prefix (C4: every key of one user; a range's begin and end) read LDS instead of issuing
-// dependent global loads per pair.  Zero padding keeps the order exact: equal words over the
-// shorter tail's words leave the shorter key first, which the length compare then decides.
-constexpr int kTailWin = 12;  // 96 tail bytes: keys up to 112 bytes compare without the arena
-__device__ __forceinline__ void load_tail_window(uint64_t* win, const uint8_t* arena, uint32_t tail, uint32_t len) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t n = len > 16u ? len - 16u : 0u;
-#pragma unroll
-    for (int j = 0; j < kTailWin; j++) {
-        const int vb = (int)n - 8 * j;  // bytes of word j inside the tail
-        const uint64_t x = vb > 0 ? tail_word(arena + tail + 8 * j) : 0ull;
-        win[j] = vb >= 8 ? x : (vb <= 0 ? 0ull : x & (~0ull << (64 - 8 * vb)));
-    }
-#endif
-}
-// item_less_tail with both keys' windows in LDS (arena only past the windows).
-__device__ __forceinline__ bool item_less_tail_win(const uint64_t* wa, uint32_t alen, uint32_t atail, uint32_t ameta,
-                                                   const uint64_t* wb, uint32_t blen, uint32_t btail, uint32_t bmeta,
-                                                   const uint8_t* arena) {
-    const uint32_t m = (alen < blen ? alen : blen) - 16u;  // common tail bytes
-    const int nw = (int)((m + 7u) / 8u);
-    const int k = nw < kTailWin ? nw : kTailWin;
-    for (int j = 0; j < k; j++)
-        if (wa[j] != wb[j]) return wa[j] < wb[j];
-    if (nw > kTailWin)  // both tails run past the window: the rest from the arena
-        return item_less_tail(alen, atail, ameta, blen, btail, bmeta, arena);
-    if (alen != blen) return alen < blen;
-    const uint32_t ca = item_class(ameta), cb = item_class(bmeta);
-    if (ca != cb) return ca < cb;
-    return ameta < bmeta;
-}
-
-// Sort one bucket in a[off, off+m) (scratch: tmp at the same offsets): bitonic network padded to a
-// power of two; oversized buckets (skewed sample) sort kBitonicMax chunks, then merge through memory.
-// WIN: the batch has keys longer than kSortNxLen (tail windows staged in LDS; a separate
-// instantiation keeps the LDS footprint, and the occupancy, of short-key batches unchanged).
-template <int ALG, bool WIN>
-__global__ __launch_bounds__(kSortThreads) void k_bucket_sort(SortItem* a, SortItem* tmp, const int32_t* boff,
-                                                              const uint8_t* arena) {
-    __shared__ SortItem sh[kBitonicMax];  // exchange buffer
-    const int off = boff[blockIdx.x], m = boff[blockIdx.x + 1] - off;
-    if (m <= 1) return;
-    const int t = threadIdx.x;
-    if (ALG == 0 && m <= kBitonicMax) {
-        // Rank count on (high word, low word, tie-break word), with all LDS loads of a step issued
-        // first.  Pass 1 (high word, eight items per step) alone is exact for distinct keys (C2);
-        // pass 2 (low word, then tie-break word) serves items sharing the high word (hot keys,
-        // single-key writes [k, k\0); C4 tuple keys share a whole subspace).  The tie-break word (bytes 16-18, length,
-        // class, id) leaves only keys longer than 19 bytes that agree on it unordered by key:
-        // those sit in contiguous runs after the ranking, and each run is then sorted by its tails
-        // (windows staged in LDS for exactly the run members) by one thread.
-        __shared__ __attribute__((aligned(16))) uint64_t shi[kBitonicMax];
-        __shared__ __attribute__((aligned(16))) uint64_t slo[kBitonicMax];
-        __shared__ __attribute__((aligned(16))) uint64_t saux[kBitonicMax];
-        __shared__ uint64_t swin[WIN ? kBitonicMax : 1][kTailWin];
-        SortItem x{};
-        if (t < m) {
-            x = a[off + t];
-            shi[t] = x.hi;
-            slo[t] = x.lo;
-            saux[t] = item_aux(x);
-        }
-        __syncthreads();
-        int lt = 0, eq = 0;
-        const uint64_t mh = x.hi, ml = x.lo, ax = t < m ? saux[t] : 0;
-        if (t < m) {
-            int j = 0;
-            for (; j + 8 <= m; j += 8) {
-                ulonglong2 p[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    lt += (p[u].x < mh) + (p[u].y < mh);
-                    eq += (p[u].x == mh) + (p[u].y == mh);
-                }
-            }
-            for (; j < m; j++) {
-                const uint64_t h = shi[j];
-                lt += h < mh;
-                eq += h == mh;
-            }
-        }
-        if (t < m && eq > 1) {  // pass 2: my high word repeats: (low word, tie-break word)
-            int j = 0;
-            for (; j + 4 <= m; j += 4) {
-                ulonglong2 p[2], q[2], w[2];
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    p[u] = *reinterpret_cast<const ulonglong2*>(&shi[j + 2 * u]);
-                    q[u] = *reinterpret_cast<const ulonglong2*>(&slo[j + 2 * u]);
-                    w[u] = *reinterpret_cast<const ulonglong2*>(&saux[j + 2 * u]);
-                }
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    lt += (p[u].x == mh && (q[u].x < ml || (q[u].x == ml && w[u].x < ax))) +
-                          (p[u].y == mh && (q[u].y < ml || (q[u].y == ml && w[u].y < ax)));
-                }
-            }
-            for (; j < m; j++) {
-                const uint64_t h = shi[j], l = slo[j], w = saux[j];
-                lt += h == mh && (l < ml || (l == ml && w < ax));
-            }
-        }
-        if (!WIN) {
-            if (t < m) a[off + lt] = x;  // exact: no key is longer than kSortNxLen
-            return;
-        }
-        __syncthreads();  // ranks done: the arrays are reused in sorted order
-        if (t < m) {
-            sh[lt] = x;
-            shi[lt] = x.hi;
-            slo[lt] = x.lo;
-            saux[lt] = ax;
-        }
-        __syncthreads();
-        // runs of long keys that agree on (prefix, tie-break word minus class and id)
-        auto same = [&](int p0, int p1) {
-            const uint64_t w0 = saux[p0], w1 = saux[p1];
-            return shi[p0] == shi[p1] && slo[p0] == slo[p1] && ((w0 >> 32) & 31u) == kSortNxLen + 1 &&
-                   ((w1 >> 32) & 31u) == kSortNxLen + 1 && (w0 >> 37) == (w1 >> 37);
-        };
-        const bool in_run = t < m && ((t > 0 && same(t - 1, t)) || (t + 1 < m && same(t, t + 1)));
-        if (__syncthreads_or(in_run)) {
-            if (in_run) load_tail_window(swin[t], arena, sh[t].tail, sh[t].len);
-        }
-        __syncthreads();
-        if (in_run && (t == 0 || !same(t - 1, t))) {
-            int e = t + 1;
-            while (e < m && same(e - 1, e)) e++;
-            // insertion sort of positions [t, e) by (tail, class, id); swap items and windows
-            for (int i = t + 1; i < e; i++) {
-                for (int k = i; k > t; k--) {
-                    const SortItem& u = sh[k - 1];
-                    const SortItem& v = sh[k];
-                    if (!item_less_tail_win(swin[k], v.len, v.tail, v.meta, swin[k - 1], u.len, u.tail, u.meta, arena))
-                        break;
-                    const ulonglong2 t0 = reinterpret_cast<const ulonglong2*>(&sh[k - 1])[0],
-                                     t1 = reinterpret_cast<const ulonglong2*>(&sh[k - 1])[1];
-                    reinterpret_cast<ulonglong2*>(&sh[k - 1])[0] = reinterpret_cast<const ulonglong2*>(&sh[k])[0];
-                    reinterpret_cast<ulonglong2*>(&sh[k - 1])[1] = reinterpret_cast<const ulonglong2*>(&sh[k])[1];
-                    reinterpret_cast<ulonglong2*>(&sh[k])[0] = t0;
-                    reinterpret_cast<ulonglong2*>(&sh[k])[1] = t1;
-#pragma unroll
-                    for (int z = 0; z < kTailWin; z++) {
-                        const uint64_t tw = swin[k - 1][z];
-                        swin[k - 1][z] = swin[k][z];
-                        swin[k][z] = tw;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        if (t < m) a[off + t] = sh[t];
-        return;
-    }
-    for (int c = 0; c < m; c += kBitonicMax) {
-        const int cnt = min(kBitonicMax, m - c);
-        int L = 2;
-        while (L < cnt) L <<= 1;
-        SortItem x0{};
-        x0.hi = x0.lo = ~0ull;  // padding sorts after every endpoint
-        x0.meta = kPadMeta;
-        if (t < cnt) x0 = a[off + c + t];
-        SortItem x = x0;
-        const bool tie = reg_bitonic<false>(x, sh, L, arena);
-        if (__syncthreads_or(tie)) {  // long keys sharing a 16-byte prefix: exact network
-            x = x0;
-            reg_bitonic<true>(x, sh, L, arena);
-        }
-        if (t < cnt) a[off + c + t] = x;
-        __syncthreads();
-    }
-    if (m <= kBitonicMax) return;
-    SortItem* src = a + off;
-    SortItem* dst = tmp + off;
-    for (int w = kBitonicMax; w < m; w *= 2) {
-        for (int o0 = 0; o0 < m; o0 += 8 * blockDim.x) {
-            const int o = o0 + threadIdx.x * 8;
-            if (o < m) {
-                const int pb = (o / (2 * w)) * (2 * w);
-                const int lenA = max(0, min(w, m - pb));
-                const int lenB = max(0, min(w, m - pb - w));
-                merge8_to(src + pb, lenA, src + pb + w, lenB, o - pb, dst + o, min(8, m - o), arena);
-            }
-        }
-        __threadfence_block();
-        __syncthreads();
-        SortItem* t = src;
-        src = dst;
-        dst = t;
-    }
-    if (src != a + off) {
-        for (int i = threadIdx.x; i < m; i += blockDim.x) a[off + i] = src[i];
-    }
-}
-
-int sort_buckets(int E, int target) {
-    if (target <= 0) target = kBucketTarget;
-    int nb = (E + target - 1) / target;
-    nb = nb < 1 ? 1 : nb;
-    return nb > kMaxBuckets ? kMaxBuckets : nb;
-}
-
-void launch_sample(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per) {
-    const int E = 2 * (b.R + b.W);
-    const int nb = E ? sort_buckets(E, bucket_target) : 1;
-    if (nb <= 1) return;
-    SampleRank c{};
-    c.S = sample_count(E, nb, sample_per);
-    c.n_slice = (c.S + kSampleSlice - 1) / kSampleSlice;
-    c.srank = w.srank;
-    c.samples = w.samples;
-    c.trace = w.trace;
-    const int grid = c.n_slice * ((c.S + kBlock - 1) / kBlock);
-    fdb_launch(k_sample, dim3(grid), dim3(kBlock), 0, s, b, c);
-}
-
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
                   const uint8_t* htail, int check_version) {
     if (b.R == 0) return;
@@ -1378,122 +945,634 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
         fdb_launch(k_check_reads<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
-void launch_sort_points(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
-                        int* result_buffer, hipEvent_t sort_begin, hipEvent_t sort_end, bool long_keys) {
+// ---- D.Sort (SkipList.cpp:161-208) and the sorted positions (KeyInfo::pIndex, SkipList.cpp:814)
+//
+// Two launches per batch (a cold start adds two small ones before them):
+// 1. k_sort_partition: an endpoint's bucket is the number of splitters not above its projection
+//    (SplitKey: binary search over the splitters' first two key words in LDS; ties there compare
+//    the rest of the 64-byte windows in global memory).  One 64-bit atomic add per endpoint
+//    reserves its slot in the bucket's slab and counts its class; past kSlab it joins the overflow
+//    list.
+// 2. k_sort_bucket: one wave per bucket.  The bucket counts give each bucket's offset and class
+//    offsets (every workgroup reduces them itself: no scan launch).  Every key of a bucket shares
+//    the bytes its two bounding splitters share, so the wave sorts by the 19 key bytes after that
+//    common prefix (two words and a tie-break word, as the whole key's first 19 bytes before):
+//    up to kSlab endpoints in registers, a bitonic network four per lane, cross-lane steps by
+//    shuffles; runs tied on those 19 bytes are then ranked by their tails.  The wave writes each
+//    position's meta, every endpoint's position, the class counts before every position and the
+//    write-begin / read-begin position lists (what the position scan wrote before), and the
+//    quantiles the next batch splits by.  A bucket past kSlab (skew the splitters did not
+//    foresee) is ranked by its whole workgroup.
+// Splitters are the projections of the quantiles of the last batch of at least kQuantMinE
+// endpoints (a resolver's key distribution drifts slowly, and any splitters are exact: they only
+// decide balance); at a cold start, of this batch's samples ranked by k_sample.
+
+// Big-endian 8 key bytes from byte `off` (zero past the key's length): the first 16 bytes come
+// from the prefix words, the rest from the tail bytes [16, len) at `tail`.
+__device__ __forceinline__ uint64_t key_word(uint64_t hi, uint64_t lo, const uint8_t* tail, uint32_t len,
+                                             uint32_t off) {
+    if (off >= len) return 0;
+    uint64_t v;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (off == 0) {
+        v = hi;
+    } else if (off < 8) {
+        v = (hi << (8 * off)) | (lo >> (64 - 8 * off));
+    } else if (off == 8) {
+        v = lo;
+    } else if (off < 16) {
+        v = lo << (8 * (off - 8));
+        if (len > 16) v |= tail_word(tail) >> (64 - 8 * (off - 8));
+    } else {
+        v = tail_word(tail + (off - 16));
+    }
+#else
+    v = 0;
+#endif
+    const uint32_t valid = len - off;
+    return valid >= 8 ? v : v & (~0ull << (8 * (8 - valid)));
+}
+
+// Tie-break word of an endpoint whose key bytes [0, c) are already known equal among the keys it
+// is sorted with: key bytes [c + 16, c + kSortNxLen), length past c capped at kSortNxLen + 1,
+// class, endpoint id (item_aux of the key with its first c bytes removed).
+__device__ __forceinline__ uint64_t aux_at(uint64_t w2, uint32_t len_c, uint32_t meta) {
+    const uint64_t l = len_c > kSortNxLen ? kSortNxLen + 1 : len_c;
+    return ((w2 >> 40) << 37) | (l << 32) | ((uint64_t)item_class(meta) << 30) | (meta >> 2);
+}
+__device__ __forceinline__ bool key3_less(uint64_t ah, uint64_t al, uint64_t aa, uint64_t bh, uint64_t bl,
+                                          uint64_t ba) {
+    return ah < bh || (ah == bh && (al < bl || (al == bl && aa < ba)));
+}
+// Quantile-table entry of splitter k (of nb - 1).
+__device__ __forceinline__ int split_index(int k, int nb) { return (int)(((int64_t)(k + 1) * kQuant) / nb); }
+// Position of quantile q in a sorted batch of E endpoints.
+__device__ __forceinline__ int64_t quant_pos(int q, int64_t E) { return ((int64_t)(q + 1) * E) / (kQuant + 1); }
+
+// The splitter an endpoint projects to.
+__device__ __forceinline__ SplitKey make_split(const SortItem& it, const uint8_t* arena) {
+    SplitKey s;
+    s.w[0] = it.hi;
+    s.w[1] = it.lo;
+#pragma unroll
+    for (int i = 2; i < kSplitWords; i++) s.w[i] = key_word(it.hi, it.lo, arena + it.tail, it.len, 8 * i);
+    s.len = it.len;
+    s.meta = it.meta;
+    return s;
+}
+// Projection order past the first two words: words 2.., min(len, kSplitBytes + 1), then class and
+// id when both keys fit the window.  -1, 0, 1.
+__device__ __forceinline__ int split_cmp_rest(const uint64_t (&a)[kSplitWords], uint32_t alen, uint32_t ameta,
+                                              const SplitKey& b) {
+#pragma unroll
+    for (int i = 2; i < kSplitWords; i++)
+        if (a[i] != b.w[i]) return a[i] < b.w[i] ? -1 : 1;
+    const uint32_t la = alen > kSplitBytes ? kSplitBytes + 1 : alen, lb = b.len > kSplitBytes ? kSplitBytes + 1 : b.len;
+    if (la != lb) return la < lb ? -1 : 1;
+    if (la > kSplitBytes) return 0;  // tied on the window: one projection
+    const uint32_t ca = item_class(ameta), cb = item_class(b.meta);
+    if (ca != cb) return ca < cb ? -1 : 1;
+    return (ameta >> 2) < (b.meta >> 2) ? -1 : ((ameta >> 2) > (b.meta >> 2) ? 1 : 0);
+}
+
+struct SortArgs {
+    const SplitKey* quant;
+    uint64_t *cnt0, *cnt1;
+    SortItem* slab;
+    SortItem* ovf;
+    int32_t* ovf_b;
+    BatchScalars* bsc;
+    int nb;
+    unsigned long long* trace;
+};
+
+__global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_spl[];  // [2 (nb - 1)]: first two key words
+    const int E = 2 * (b.R + b.W), nb = a.nb, ns = nb - 1;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (threadIdx.x == 0) trace_min(a.trace, kTrPartBegin);
+    SortItem it{};
+    if (p < E) it = make_item(b, p);  // in flight during the splitter fill
+    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+        const SplitKey* sk = &a.quant[split_index(k, nb)];
+        s_spl[2 * k] = sk->w[0];
+        s_spl[2 * k + 1] = sk->w[1];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(a.trace, kTrPartFill);
+    if (p >= E) {
+        if (a.trace) trace_max(a.trace, kTrPartEnd);
+        return;
+    }
+    // splitters below my first two words: [0, lo); equal to them: [lo, up)
+    int lo = 0, hi = ns;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
+        if (h < it.hi || (h == it.hi && l < it.lo)) lo = mid + 1; else hi = mid;
+    }
+    int up = lo;
+    hi = ns;
+    while (up < hi) {
+        const int mid = (up + hi) >> 1;
+        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
+        if (h < it.hi || (h == it.hi && l <= it.lo)) up = mid + 1; else hi = mid;
+    }
+    int bk = lo;
+    if (up > lo) {  // ties on 16 bytes (hot keys, shared prefixes): the rest of the window
+        uint64_t wv[kSplitWords];
+        wv[0] = it.hi;
+        wv[1] = it.lo;
+#pragma unroll
+        for (int i = 2; i < kSplitWords; i++) wv[i] = key_word(it.hi, it.lo, b.tail + it.tail, it.len, 8 * i);
+        int l = lo, h = up;  // splitters in [lo, up) not above my projection
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (split_cmp_rest(wv, it.len, it.meta, a.quant[split_index(mid, nb)]) >= 0) l = mid + 1; else h = mid;
+        }
+        bk = l;
+    }
+    if (a.trace) trace_max(a.trace, kTrPartSearch);
+    const uint32_t cls = item_class(it.meta);
+    const unsigned long long old =
+        atomicAdd((unsigned long long*)&a.cnt0[bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
+    if (cls == kReadBegin || cls == kWriteEnd)
+        atomicAdd((unsigned long long*)&a.cnt1[bk], cls == kReadBegin ? 1ull : 1ull << 32);
+    const uint32_t slot = (uint32_t)old;
+    if (slot < (uint32_t)kSlab) {
+        a.slab[(size_t)bk * kSlab + slot] = it;
+    } else {
+        const int o = atomicAdd(&a.bsc->ovf_n, 1);
+        a.ovf[o] = it;
+        a.ovf_b[o] = bk;
+    }
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        trace_max(a.trace, kTrPartEnd);
+    }
+}
+
+// Outputs of k_sort_bucket: what the later kernels read by sorted position.
+struct SortOut {
+    int32_t* pos;      // [E] position of endpoint p
+    uint32_t* pmeta;   // [E] meta at position P
+    int32_t *cwb, *crb, *cwe;  // [E + 1] write-begins / read-begins / write-ends before position P
+    int32_t *wbpos, *rbpos;    // positions of the write-begins / read-begins in order
+    SortItem* items;   // [E] sorted items (FDBCS_VALIDATE) or null
+    SplitKey* quant;   // quantiles of this batch for the next one, or null
+    SortItem* big;     // [E] workgroup path: gathered endpoints of a big bucket
+    int32_t* big_p;    // [E] workgroup path: its endpoint ids in sorted order
+};
+
+// Bitonic network over 64 S (hi, lo, aux) triples of one wave: element s * 64 + lane in slot s of
+// the lane; partners closer than 64 by shuffles, farther ones inside the lane's registers.
+template <int S>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&kh)[4], uint64_t (&kl)[4], uint64_t (&ka)[4]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64 * S; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const int js = j >> 6;
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    if (s & js) continue;
+                    const int t = s | js;
+                    const bool up = ((s * 64 + lane) & k) == 0;
+                    if (key3_less(kh[t], kl[t], ka[t], kh[s], kl[s], ka[s]) == up) {
+                        uint64_t x = kh[s]; kh[s] = kh[t]; kh[t] = x;
+                        x = kl[s]; kl[s] = kl[t]; kl[t] = x;
+                        x = ka[s]; ka[s] = ka[t]; ka[t] = x;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < S; s++) {
+                    const uint64_t yh = __shfl_xor(kh[s], j, 64), yl = __shfl_xor(kl[s], j, 64),
+                                   ya = __shfl_xor(ka[s], j, 64);
+                    const bool up = ((s * 64 + lane) & k) == 0, lower = (lane & j) == 0;
+                    const bool y_less = key3_less(yh, yl, ya, kh[s], kl[s], ka[s]);
+                    if (lower == up ? y_less : !y_less) {
+                        kh[s] = yh;
+                        kl[s] = yl;
+                        ka[s] = ya;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Meta of endpoint p (range p / 2, end p & 1; class as extra_ordering, SkipList.cpp:89-91).
+__device__ __forceinline__ uint32_t endpoint_meta(const BatchDev& b, int p) {
+    const int g = p >> 1, e = p & 1;
+    const uint32_t cls = g < b.R ? (e ? kReadEnd : kReadBegin) : (e ? kWriteEnd : kWriteBegin);
+    return ((uint32_t)g << 3) | ((uint32_t)e << 2) | cls;
+}
+
+// The quantiles of this batch at global position P (several when E < kQuant).
+__device__ __forceinline__ void put_quantiles(const BatchDev& b, SplitKey* quant, int64_t P, int64_t E, int p) {
+    int q = (int)((P * (kQuant + 1) + E - 1) / E) - 1;  // ceil(P (Q+1) / E) - 1
+    if (q < 0) q = 0;
+    if (q >= kQuant || quant_pos(q, E) > P) return;
+    const SplitKey sk = make_split(make_item(b, p), b.tail);
+    for (; q < kQuant && quant_pos(q, E) <= P; q++)
+        if (quant_pos(q, E) == P) quant[q] = sk;
+}
+
+// Writes of sorted position P (endpoint p) given the class counts before it.
+__device__ __forceinline__ void put_position(const BatchDev& b, const SortOut& o, int p, int64_t P, int32_t wb,
+                                             int32_t rb, int32_t we) {
+    const uint32_t meta = endpoint_meta(b, p);
+    const uint32_t cls = item_class(meta);
+    o.pmeta[P] = meta;
+    o.pos[p] = (int32_t)P;
+    o.cwb[P] = wb;
+    o.crb[P] = rb;
+    o.cwe[P] = we;
+    if (cls == kWriteBegin) o.wbpos[wb] = (int32_t)P;
+    if (cls == kReadBegin) o.rbpos[rb] = (int32_t)P;
+    if (o.items) o.items[P] = make_item(b, p);
+}
+
+// Bytes [0, c) shared by every key between splitters a and b (c <= both lengths, <= the window).
+__device__ __forceinline__ uint32_t split_lcp(const SplitKey& a, const SplitKey& b) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < kSplitWords; i++) {
+        const uint64_t x = a.w[i] ^ b.w[i];
+        if (x) {
+            c = 8 * i + (uint32_t)(__builtin_clzll(x) >> 3);
+            break;
+        }
+        c = 8 * (i + 1);
+    }
+    c = c < a.len ? c : a.len;
+    return c < b.len ? c : b.len;
+}
+
+template <bool LONG>
+__global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, SortOut o) {
+    constexpr int kWaves = kBlock / 64;
+    __shared__ uint32_t s_red[8][kWaves];
+    __shared__ uint32_t s_cnt[kWaves][4];   // per wave's bucket: endpoints, write-begins, read-begins, write-ends
+    __shared__ uint32_t s_base[kWaves][4];  // the same counts over every bucket before it
+    __shared__ int32_t s_p[kWaves][kSlab];  // tied runs: endpoint at each final position
+    __shared__ uint8_t s_tie[kWaves][kSlab];
+    __shared__ int s_big[kWaves];
+    __shared__ SortItem s_tile[kBlock];     // workgroup path: a tile of the big bucket
+    __shared__ int s_gather;
+    const int E = 2 * (b.R + b.W), nb = a.nb;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int B0 = blockIdx.x * kWaves;
+    if (threadIdx.x == 0) trace_min(a.trace, kTrBktBegin);
+    // ---- bucket offsets: counts of every bucket before B0 and of all buckets, reduced by the
+    // workgroup (nb <= kSortMaxBuckets: 16 per thread at most, loads issued together)
+    uint32_t pre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
+    for (int k0 = threadIdx.x; k0 < nb; k0 += 4 * kBlock) {
+        uint64_t c0[4], c1[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * kBlock;
+            c0[u] = k < nb ? a.cnt0[k] : 0;
+            c1[u] = k < nb ? a.cnt1[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * kBlock;
+            const uint32_t v[4] = {(uint32_t)c0[u], (uint32_t)(c0[u] >> 32), (uint32_t)c1[u], (uint32_t)(c1[u] >> 32)};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                tot[c] += v[c];
+                pre[c] += k < B0 ? v[c] : 0u;
+            }
+            if (k >= B0 && k < B0 + kWaves)
+#pragma unroll
+                for (int c = 0; c < 4; c++) s_cnt[k - B0][c] = v[c];
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            pre[c] += __shfl_xor(pre[c], off, 64);
+            tot[c] += __shfl_xor(tot[c], off, 64);
+        }
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            s_red[c][wave] = pre[c];
+            s_red[4 + c][wave] = tot[c];
+        }
+    if (threadIdx.x < kWaves && B0 + (int)threadIdx.x >= nb)
+#pragma unroll
+        for (int c = 0; c < 4; c++) s_cnt[threadIdx.x][c] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run[4] = {0, 0, 0, 0};
+        for (int q = 0; q < kWaves; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) run[c] += s_red[c][q];
+        for (int q = 0; q < kWaves; q++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                s_base[q][c] = run[c];
+                run[c] += s_cnt[q][c];
+            }
+        if (blockIdx.x == 0) {  // class totals after the last position
+            uint32_t t4[4] = {0, 0, 0, 0};
+            for (int q = 0; q < kWaves; q++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) t4[c] += s_red[4 + c][q];
+            o.cwb[E] = (int32_t)t4[1];
+            o.crb[E] = (int32_t)t4[2];
+            o.cwe[E] = (int32_t)t4[3];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(a.trace, kTrBktPrologue);
+    // ---- one bucket per wave
+    const int bk = B0 + wave;
+    const int n = (int)s_cnt[wave][0];
+    const int64_t base = s_base[wave][0];
+    if (lane == 0) s_big[wave] = n > kSlab ? 1 : 0;
+    if (bk < nb && n > 0 && n <= kSlab) {
+        // bytes every key of the bucket shares: those its bounding splitters share (none at the ends)
+        // (batches of keys up to kSortNxLen bytes sort exactly on their first 19 bytes: no strip)
+        uint32_t c = 0;
+        if (LONG && bk > 0 && bk < nb - 1)
+            c = split_lcp(a.quant[split_index(bk - 1, nb)], a.quant[split_index(bk, nb)]);
+        uint64_t kh[4], kl[4], ka[4];
+        const int S = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const int k = s * 64 + lane;
+            kh[s] = kl[s] = ka[s] = ~0ull;  // padding sorts after every endpoint
+            if (s < S && k < n) {
+                const SortItem it = a.slab[(size_t)bk * kSlab + k];
+                if (c == 0) {
+                    kh[s] = it.hi;
+                    kl[s] = it.lo;
+                    ka[s] = item_aux(it);
+                } else {  // the key with its first c bytes removed
+                    const uint8_t* t = b.tail + it.tail;
+                    kh[s] = key_word(it.hi, it.lo, t, it.len, c);
+                    kl[s] = key_word(it.hi, it.lo, t, it.len, c + 8);
+                    ka[s] = aux_at(key_word(it.hi, it.lo, t, it.len, c + 16), it.len - c, it.meta);
+                }
+            }
+        }
+        if (S == 1) wave_bitonic<1>(kh, kl, ka);
+        else if (S == 2) wave_bitonic<2>(kh, kl, ka);
+        else wave_bitonic<4>(kh, kl, ka);
+        if (lane == 0) trace_max(a.trace, kTrBktSorted);
+        int ps[4];  // endpoint at each position (id bits of the tie-break word)
+#pragma unroll
+        for (int s = 0; s < 4; s++) ps[s] = (int)(ka[s] & 0x3fffffffull);
+        if (LONG || c > 0) {
+            // positions k, k+1 tied: same two words, both keys longer than kSortNxLen past c with
+            // equal bytes up to there: their order needs the tails
+            bool any = false;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                if (s >= S) break;
+                uint64_t nh = __shfl_down(kh[s], 1, 64), nl = __shfl_down(kl[s], 1, 64),
+                         na = __shfl_down(ka[s], 1, 64);
+                const int s1 = s + 1 < 4 ? s + 1 : 3;
+                const uint64_t h2 = __shfl(kh[s1], 0, 64), l2 = __shfl(kl[s1], 0, 64), a2 = __shfl(ka[s1], 0, 64);
+                if (lane == 63) {  // the next slot's lane 0
+                    nh = h2;
+                    nl = l2;
+                    na = a2;
+                }
+                const int k = s * 64 + lane;
+                const bool tie = k + 1 < n && nh == kh[s] && nl == kl[s] && (na >> 32) == (ka[s] >> 32) &&
+                                 ((ka[s] >> 32) & 31u) == kSortNxLen + 1;
+                s_tie[wave][k] = tie ? 1 : 0;
+                s_p[wave][k] = ps[s];
+                any |= tie;
+            }
+            if (__ballot(any)) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                int fin[4];
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int k = s * 64 + lane;
+                    fin[s] = k;
+                    if (s >= S || k >= n) continue;
+                    const bool in_run = s_tie[wave][k] || (k > 0 && s_tie[wave][k - 1]);
+                    if (!in_run) continue;
+                    int st = k, en = k;
+                    while (st > 0 && s_tie[wave][st - 1]) st--;
+                    while (s_tie[wave][en]) en++;
+                    const SortItem me = make_item(b, ps[s]);
+                    int rank = 0;
+                    for (int j = st; j <= en; j++)
+                        if (j != k) rank += item_less_total(make_item(b, s_p[wave][j]), me, b.tail) ? 1 : 0;
+                    fin[s] = st + rank;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int k = s * 64 + lane;
+                    if (s < S && k < n) s_p[wave][fin[s]] = ps[s];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int s = 0; s < 4; s++) {
+                    const int k = s * 64 + lane;
+                    if (s < S && k < n) ps[s] = s_p[wave][k];
+                }
+            }
+        }
+        // positions, class counts before them, begin lists; quantiles for the next batch
+        uint32_t carry[3] = {s_base[wave][1], s_base[wave][2], s_base[wave][3]};
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            if (s >= S) break;
+            const int k = s * 64 + lane;
+            const bool live = k < n;
+            const uint32_t cls = live ? item_class(endpoint_meta(b, ps[s])) : 4u;
+            const uint32_t f[3] = {cls == kWriteBegin, cls == kReadBegin, cls == kWriteEnd};
+            uint32_t ex[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                uint32_t x = f[q];
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t y = __shfl_up(x, off, 64);
+                    if (lane >= off) x += y;
+                }
+                ex[q] = carry[q] + x - f[q];
+                carry[q] += __shfl(x, 63, 64);
+            }
+            if (live) {
+                put_position(b, o, ps[s], base + k, (int32_t)ex[0], (int32_t)ex[1], (int32_t)ex[2]);
+                if (o.quant) put_quantiles(b, o.quant, base + k, E, ps[s]);
+            }
+        }
+    }
+    // ---- buckets past kSlab: ranked by the whole workgroup, one after another
+    __syncthreads();
+    for (int wv = 0; wv < kWaves; wv++) {
+        if (!s_big[wv] || B0 + wv >= nb) continue;  // uniform: LDS after the barrier
+        const int bb = B0 + wv;
+        const int m = (int)s_cnt[wv][0];
+        const int64_t bbase = s_base[wv][0];
+        if (threadIdx.x == 0) {
+            s_gather = 0;
+            atomicAdd(&a.bsc->sort_big, 1);
+        }
+        for (int i = threadIdx.x; i < kSlab; i += kBlock) o.big[bbase + i] = a.slab[(size_t)bb * kSlab + i];
+        __syncthreads();
+        const int novf = a.bsc->ovf_n;
+        for (int i = threadIdx.x; i < novf; i += kBlock)
+            if (a.ovf_b[i] == bb) o.big[bbase + kSlab + atomicAdd(&s_gather, 1)] = a.ovf[i];
+        __syncthreads();
+        // rank of every endpoint among the bucket's (exact order, tails included)
+        for (int i0 = 0; i0 < m; i0 += kBlock) {
+            const int i = i0 + threadIdx.x;
+            SortItem me{};
+            if (i < m) me = o.big[bbase + i];
+            int rank = 0;
+            for (int j0 = 0; j0 < m; j0 += kBlock) {
+                __syncthreads();
+                if (j0 + (int)threadIdx.x < m) s_tile[threadIdx.x] = o.big[bbase + j0 + threadIdx.x];
+                __syncthreads();
+                const int cnt = min(kBlock, m - j0);
+                if (i < m)
+                    for (int j = 0; j < cnt; j++) rank += item_less_total(s_tile[j], me, b.tail) ? 1 : 0;
+            }
+            if (i < m) o.big_p[bbase + rank] = (int32_t)(me.meta >> 2);  // ranks are distinct
+        }
+        __syncthreads();
+        uint32_t carry[3] = {s_base[wv][1], s_base[wv][2], s_base[wv][3]};
+        for (int k0 = 0; k0 < m; k0 += kBlock) {
+            const int k = k0 + threadIdx.x;
+            const bool live = k < m;
+            const int p = live ? o.big_p[bbase + k] : 0;
+            const uint32_t cls = live ? item_class(endpoint_meta(b, p)) : 4u;
+            uint32_t ex[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const uint32_t f = cls == (q == 0 ? (uint32_t)kWriteBegin : q == 1 ? (uint32_t)kReadBegin
+                                                                                     : (uint32_t)kWriteEnd);
+                uint32_t total;
+                ex[q] = carry[q] + block_excl_sum<uint32_t>(f, &s_red[q][0], &total);
+                carry[q] += total;
+            }
+            if (live) {
+                put_position(b, o, p, bbase + k, (int32_t)ex[0], (int32_t)ex[1], (int32_t)ex[2]);
+                if (o.quant) put_quantiles(b, o.quant, bbase + k, E, p);
+            }
+        }
+        __syncthreads();
+    }
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) trace_max(a.trace, kTrBktEnd);
+    }
+}
+
+// Cold start: the quantile table from this batch's samples ranked by k_sample (one workgroup).
+__global__ __launch_bounds__(kWG) void k_quant_cold(BatchDev b, const SortItem* samples, const int32_t* srank, int S,
+                                                    SplitKey* quant) {
+    __shared__ int32_t inv[kMaxSample];
+    for (int i = threadIdx.x; i < S; i += blockDim.x) inv[srank[i]] = i;
+    __syncthreads();
+    for (int q = threadIdx.x; q < kQuant; q += blockDim.x) {
+        const int r = (int)(((int64_t)(q + 1) * S) / (kQuant + 1));
+        quant[q] = make_split(samples[inv[r]], b.tail);
+    }
+}
+
+int sort_bucket_count(int64_t E, int target, int slab_buckets) {
+    if (target <= 0) target = kSortTarget;
+    int64_t nb = (E + target - 1) / target;
+    const int64_t cap = std::min<int64_t>(kSortMaxBuckets, std::max(1, slab_buckets));
+    return (int)std::max<int64_t>(1, std::min(nb, cap));
+}
+
+static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb) {
+    return SortArgs{quant, w.scnt0, w.scnt1, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
+}
+
+void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
+                 int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end) {
     const int E = 2 * (b.R + b.W);
-    *result_buffer = 0;
     if (E == 0) return;
-    const int nb = sort_buckets(E, bucket_target);
-    const int grid = (E + kBlock - 1) / kBlock;
-    const int S = nb > 1 ? sample_count(E, nb, sample_per) : 0;
-    fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, w.samples, nb, S, w.bucket, w.bcount,
-               b.tail);
-    fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
-                       w.items[0]);
+    const int nb = sort_bucket_count(E, bucket_target, w.slab_buckets);
     fdb_event(LaunchList::kTimingRecord, sort_begin, s);
+    if (cold && nb > 1) {  // splitters from this batch's ranked samples
+        SampleRank c{};
+        c.S = std::min(E, std::min(kMaxSample, std::max(1024, 4 * nb)));
+        c.n_slice = (c.S + kSampleSlice - 1) / kSampleSlice;
+        c.srank = w.srank;
+        c.samples = w.samples;
+        c.trace = w.trace;
+        fdb_launch(k_sample, dim3(c.n_slice * ((c.S + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, b, c);
+        fdb_launch(k_quant_cold, dim3(1), dim3(kWG), 0, s, b, (const SortItem*)w.samples, (const int32_t*)w.srank,
+                   c.S, quant);
+    }
+    const SortArgs a = sort_args(w, quant, nb);
+    fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
+    SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, validate ? w.items : nullptr,
+              quant_out, w.big, w.big_p};
+    const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     if (long_keys)
-        fdb_launch(k_bucket_sort<0, true>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        fdb_launch(k_sort_bucket<true>, dim3(grid), dim3(kBlock), 0, s, b, a, o);
     else
-        fdb_launch(k_bucket_sort<0, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+        fdb_launch(k_sort_bucket<false>, dim3(grid), dim3(kBlock), 0, s, b, a, o);
     fdb_event(LaunchList::kTimingRecord, sort_end, s);
 }
 
-// Diagnostics (fdbcs_debug_kernel_time, which 1-4): isolated device time of one sort kernel
-// (1 k_sample, 2 k_bucket_count, 3 k_bucket_scatter, 4 k_bucket_sort) over `reps` runs of the
-// whole sort on an idle stream; the zeroed scratch is reset before each run, outside the timing.
-hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, int bucket_target, int sample_per,
+// Diagnostics (fdbcs_debug_kernel_time, which 1-2): isolated device time of k_sort_partition or
+// k_sort_bucket (warm splitters) over `reps` runs of the sort on an idle stream; the zeroed
+// scratch is reset before each run, outside the timing.
+hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,
                            bool long_keys, int which, int reps, double* us) {
     const int E = 2 * (b.R + b.W);
     if (E == 0) return hipErrorInvalidValue;
-    const int nb = sort_buckets(E, bucket_target);
-    const int grid = (E + kBlock - 1) / kBlock;
-    const int S = nb > 1 ? sample_count(E, nb, sample_per) : 0;
+    const int nb = sort_bucket_count(E, bucket_target, w.slab_buckets);
     hipEvent_t e0, e1;
     hipError_t err;
     if ((err = hipEventCreate(&e0)) || (err = hipEventCreate(&e1))) return err;
+    const SortArgs a = sort_args(w, quant, nb);
+    SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, nullptr, nullptr, w.big, w.big_p};
+    const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     double total = 0;
     for (int r = 0; r < reps && err == hipSuccess; r++) {
-        (void)hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), s);
-        (void)hipMemsetAsync(w.bcount, 0, 4 * kMaxBuckets, s);
-        (void)hipMemsetAsync(w.bcursor, 0, 4 * kMaxBuckets, s);
-        auto at = [&](int k) { if (which == k) (void)hipEventRecord(e0, s); };
-        auto after = [&](int k) { if (which == k) (void)hipEventRecord(e1, s); };
-        at(1);
-        launch_sample(s, b, w, bucket_target, sample_per);
-        after(1);
-        at(2);
-        fdb_launch(k_bucket_count, dim3(grid), dim3(kBlock), 0, s, b, w.srank, w.samples, nb, S, w.bucket, w.bcount,
-               b.tail);
-        after(2);
-        at(3);
-        fdb_launch(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, s, b, w.bucket, w.bcount, w.bcursor, w.boff, nb,
-                   w.items[0]);
-        after(3);
-        at(4);
+        (void)hipMemsetAsync(w.scnt0, 0, 8 * kSortMaxBuckets, s);
+        (void)hipMemsetAsync(w.scnt1, 0, 8 * kSortMaxBuckets, s);
+        (void)hipMemsetAsync(&w.bsc->ovf_n, 0, 4, s);
+        if (which == 1) (void)hipEventRecord(e0, s);
+        fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
+        if (which == 1) (void)hipEventRecord(e1, s);
+        if (which == 2) (void)hipEventRecord(e0, s);
         if (long_keys)
-            fdb_launch(k_bucket_sort<0, true>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
+            fdb_launch(k_sort_bucket<true>, dim3(grid), dim3(kBlock), 0, s, b, a, o);
         else
-            fdb_launch(k_bucket_sort<0, false>, dim3(nb), dim3(kSortThreads), 0, s, w.items[0], w.items[1], w.boff, b.tail);
-        after(4);
+            fdb_launch(k_sort_bucket<false>, dim3(grid), dim3(kBlock), 0, s, b, a, o);
+        if (which == 2) (void)hipEventRecord(e1, s);
         if ((err = hipEventSynchronize(e1))) break;
         float ms = 0;
         if ((err = hipEventElapsedTime(&ms, e0, e1))) break;
         total += ms;
     }
-    if (err == hipSuccess && getenv("FDBCS_DEBUG_BUCKETS")) {  // bucket-size balance of the last run
-        std::vector<int32_t> cnt(nb);
-        (void)hipMemcpy(cnt.data(), w.bcount, 4 * (size_t)nb, hipMemcpyDeviceToHost);
-        int mx = 0, over = 0;
-        for (int k = 0; k < nb; k++) {
-            mx = cnt[k] > mx ? cnt[k] : mx;
-            over += cnt[k] > kBitonicMax;
-        }
-        fprintf(stderr, "fdbcs sort: E=%d nb=%d S=%d max bucket=%d over %d=%d\n", E, nb, S, mx, kBitonicMax, over);
-    }
-    (void)hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), s);
-    (void)hipMemsetAsync(w.bcount, 0, 4 * kMaxBuckets, s);
-    (void)hipMemsetAsync(w.bcursor, 0, 4 * kMaxBuckets, s);
+    (void)hipMemsetAsync(w.scnt0, 0, 8 * kSortMaxBuckets, s);
+    (void)hipMemsetAsync(w.scnt1, 0, 8 * kSortMaxBuckets, s);
+    (void)hipMemsetAsync(w.bsc, 0, sizeof(BatchScalars), s);
     (void)hipStreamSynchronize(s);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     *us = total * 1000.0 / reps;
     return err;
 }
-
-// ------------------------------------------------------------------ positions
-
-// Positions (KeyInfo::pIndex, SkipList.cpp:814) and, in the same scan, the number of write-begins
-// and read-begins before every position with the compacted position list of each kind.
-struct PosScan {
-    const SortItem* sorted;
-    int32_t* pos;
-    uint32_t* pmeta;
-    int32_t *cwb, *crb, *cwe, *wbpos, *rbpos;
-    int32_t E;
-    __device__ void load(int64_t p, uint32_t (&v)[3]) const {
-        const uint32_t meta = sorted[p].meta;
-        pmeta[p] = meta;
-        const uint32_t slot = 2 * item_range(meta) + item_is_end(meta);
-        if (slot < (uint32_t)E) pos[slot] = (int32_t)p;
-        const uint32_t c = item_class(meta);
-        v[0] = c == kWriteBegin;
-        v[1] = c == kReadBegin;
-        v[2] = c == kWriteEnd;
-    }
-    __device__ void store(int64_t p, const uint32_t (&ex)[3]) const {
-        cwb[p] = (int32_t)ex[0];
-        crb[p] = (int32_t)ex[1];
-        cwe[p] = (int32_t)ex[2];
-        const uint32_t c = item_class(pmeta[p]);
-        if (c == kWriteBegin) wbpos[ex[0]] = (int32_t)p;
-        if (c == kReadBegin) rbpos[ex[1]] = (int32_t)p;
-    }
-    __device__ void finish(const uint32_t (&tot)[3]) const {
-        cwb[E] = (int32_t)tot[0];
-        crb[E] = (int32_t)tot[1];
-        cwe[E] = (int32_t)tot[2];
-    }
-};
 
 // FDBCS_VALIDATE=1: check the endpoint order and that positions invert the permutation.
 __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted, const int32_t* pos,
@@ -1502,24 +1581,17 @@ __global__ __launch_bounds__(kBlock) void k_validate_sort(const SortItem* sorted
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= E) return;
     bool bad = p > 0 && !item_less_total(sorted[p - 1], sorted[p], arena);
+    bad |= sorted[p].meta != pmeta[p];
     const int q = pos[p];  // slot p -> position
     bad |= q < 0 || q >= E || (2 * item_range(pmeta[q]) + item_is_end(pmeta[q])) != (uint32_t)p;
     if (bad) atomicOr(&sc->debug_error, 1);
 }
 
-void launch_positions(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
+void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w) {
     const int E = 2 * (b.R + b.W);
     if (E == 0) return;
-    PosScan f{w.items[sorted_buf], w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, E};
-    launch_scan<3>(s, f, nullptr, E, w.scan[kScanPos]);
-}
-
-void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w, int sorted_buf) {
-    BatchScalars* sc = w.bsc;
-    const int E = 2 * (b.R + b.W);
-    if (E == 0) return;
-    fdb_launch(k_validate_sort, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, w.items[sorted_buf],
-                       w.pos, w.pmeta, E, b.tail, sc);
+    fdb_launch(k_validate_sort, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), 0, s, (const SortItem*)w.items,
+               (const int32_t*)w.pos, (const uint32_t*)w.pmeta, E, (const uint8_t*)b.tail, w.bsc);
 }
 
 // ------------------------------------------------------------------ D.CheckIntraBatch: candidate edges
@@ -2240,9 +2312,9 @@ struct Epilogue {
     int64_t zero32_n;
     uint64_t* zero64;  // scan arena
     int64_t zero64_n;
-    int32_t* zero_bc;  // sample-sort bucket counts and cursors [kMaxBuckets]
-    int32_t* zero_bk;
-    int32_t* zero_rank;  // sample ranks + done counter [kMaxSample + 64]
+    uint64_t* zero_bc;  // sort bucket counts [kSortMaxBuckets] (two arrays)
+    uint64_t* zero_bk;
+    int32_t* zero_rank;  // cold-start sample ranks [kMaxSample + 64]
     BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
 };
 
@@ -2258,8 +2330,11 @@ __device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogu
     out->debug_error = ep.bsc->debug_error;
     out->intra_rounds = ep.bsc->rounds;
     out->intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
+    out->sort_big = ep.bsc->sort_big;
     ep.bsc->pre_done = 0;  // k_resolve's pre-pass counter (its workgroups have all finished)
     ep.bsc->debug_error = 0;
+    ep.bsc->ovf_n = 0;     // the sort's overflow list and big-bucket count (this batch's sort is done)
+    ep.bsc->sort_big = 0;
 }
 // ------------------------------------------------------------------ D.MergeWrite
 //
@@ -2523,8 +2598,8 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
     ep.zero32_n = w.cap_R;
     ep.zero64 = w.scan_arena;
     ep.zero64_n = w.scan_words;
-    ep.zero_bc = w.bcount;
-    ep.zero_bk = w.bcursor;
+    ep.zero_bc = w.scnt0;
+    ep.zero_bk = w.scnt1;
     ep.zero_rank = w.srank;
     ep.bsc = w.bsc;
     return ep;
@@ -2833,7 +2908,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
     for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
     for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
-    for (int64_t i = tid; i < kMaxBuckets; i += stride) {
+    for (int64_t i = tid; i < kSortMaxBuckets; i += stride) {
         ep.zero_bc[i] = 0;
         ep.zero_bk[i] = 0;
     }

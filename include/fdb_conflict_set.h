@@ -124,6 +124,7 @@ typedef struct fdbcs_stats {
     int64_t delta_sum;         /* delta-tier boundaries at the start of each batch's merge, summed */
     int64_t base_sum;          /* base-tier boundaries after each batch, summed */
     int64_t segments_sum;      /* union segments of committed writes, summed */
+    int64_t sort_big_buckets;  /* sort buckets past the per-wave capacity (ranked by their workgroup) */
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
@@ -211,8 +212,8 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
 
 /* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
  * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the
- * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead); 1-4 = the
- * endpoint sort's kernels (sample ranking, bucket count, scatter, per-bucket sort). */
+ * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead); 1-2 = the
+ * endpoint sort's kernels (partition, per-bucket sort; splitters of the last batch detected). */
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch);
 /* Per-kernel device time accumulated since fdbcs_reset_stats: timing level 3 brackets every kernel
  * of every batch with events, level 1 the kernel named by fdbcs_set_timed_kernel on the sampled

@@ -256,3 +256,91 @@ def test_worst_case_dependency_chain(engine, oracle_mod):
     st = cs.stats()
     print(f"chain of {T}: {st['intra_rounds']} resolution rounds, intra phase {st['ms_intra']:.3f} ms")
     cs.close()
+
+
+def test_reference_max_batch_32768(engine, oracle_mod):
+    """The reference's largest commit batch (COMMIT_TRANSACTION_BATCH_COUNT_MAX = 32768,
+    fdbserver/Knobs.cpp:370) at the C2 shape over the 5M-boundary history: T > 8192 takes the
+    resolution rounds' global-memory path and W = 65536 > kMaxGroupWrites turns write groups off.
+    Three batches, pipelined, against the restatement."""
+    p = W.C2Params(txns=32768)
+    kb, ko, vers = W.c2_history(p, seed=9, start_version=10_000_000)
+    rng = np.random.default_rng(32768)
+    seq, now = [], 10_000_000
+    for _ in range(3):
+        now += p.version_step
+        seq.append((W.c2_batch(p, rng, now), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    got = {}
+    pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v), window=3)
+    assert seq[0][0].n_txn == 32768 and seq[0][0].n_writes == 65536
+    check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
+    committed = sum(int((got[i] == 2).sum()) for i in got)
+    assert 0 < committed < 3 * 32768
+    cs.close()
+
+
+def rck_key(n, node_count=10000, client=0, prefix=b"RCK", key_bytes=64):
+    """keyForIndex of the ReportConflictingKeys workload (ReportConflictingKeys.actor.cpp:87-95):
+    prefix + "Cid_%04d" + the bits of the double n / nodeCount as zero-padded hex."""
+    import struct
+
+    bits = struct.unpack("<Q", struct.pack("<d", n / node_count))[0]
+    pad = key_bytes - 8 - len(prefix)
+    return prefix + b"Cid_%04d" % client + b"%0*x" % (pad, bits)
+
+
+def rck_batch(rng, n_txn, now, node_count=10000, mean_ranges=10):
+    """A batch of the workload's transactions (tests/fast/ReportConflictingKeys.toml: keyPrefix RCK,
+    keyBytes 64, nodeCount 10000, 10 read and 10 write ranges per transaction on average; each range
+    [keyForIndex(s), keyForIndex(e)) with s uniform in [0, nodeCount), e in (s, nodeCount], the
+    count geometric with at least one, ReportConflictingKeys.actor.cpp:98-125)."""
+    keys = {}
+
+    def key(i):
+        if i not in keys:
+            keys[i] = rck_key(i, node_count)
+        return keys[i]
+
+    def ranges():
+        out = []
+        while True:
+            s = int(rng.integers(0, node_count))
+            e = int(rng.integers(s + 1, node_count + 1))
+            out.append(KeyRange(key(s), key(e)))
+            if rng.random() >= (mean_ranges - 1.0) / mean_ranges:
+                return out
+
+    txns = [CommitTransaction(ranges(), ranges(), int(now - rng.integers(0, 6)), True) for _ in range(n_txn)]
+    return PackedBatch.from_transactions(txns)
+
+
+def test_report_conflicting_keys_workload_shape(engine):
+    """The reference's own ReportConflictingKeys spec shape (64-byte keys sharing their first ~47
+    bytes, wide ranges, ~10 reads and ~10 writes per transaction) against the key-space model: the
+    verdicts, and the reported conflicting reads exactly (ReportConflictingKeys.actor.cpp:201-278:
+    every reported range is one of the transaction's reads and meets a write it conflicts with; a
+    transaction with no conflict has no such intersection)."""
+    rng = np.random.default_rng(201)
+    seq, now = [], 50
+    for _ in range(6):
+        seq.append((rck_batch(rng, int(rng.integers(60, 160)), now), now, now - 8))
+        now += 3
+    want = brute_force(seq)
+    cs = engine.ConflictSet(0)
+    cs.set_gc_interval(2)
+    for i, (pb, now_i, no) in enumerate(seq):
+        m = {}
+        b = engine.ConflictBatch(cs, m)
+        b.add_packed(pb)
+        v = b.detect_conflicts(now_i, no)
+        b.close()
+        wv, wc = want[i]
+        assert (v == wv).all(), (i, np.nonzero(v != wv)[0][:8])
+        got = {t: sorted(x) for t, x in m.items() if x}
+        assert got == wc, i
+        for t in range(pb.n_txn):  # a conflict always carries a report (the workload's check)
+            if v[t] == 0:
+                assert got.get(t), (i, t)
+    cs.close()

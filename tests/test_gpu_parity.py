@@ -380,23 +380,27 @@ def test_edge_cases(engine):
     assert ex.value.status == engine.FDBCS_E_VERSION
 
 
-@pytest.mark.parametrize("bucket,samples", [("3000", "0"), ("40", "0"), ("160", "2"), ("64", "1"), ("128", "8")])
-def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket, samples):
-    """Oversized sort buckets (chunked rank sort + merges through memory), tiny ones, and sparse
-    splitter samples (skewed buckets), with keys longer than the 16-byte prefix, give the same
-    verdicts and reports."""
+@pytest.mark.parametrize("bucket,cold", [("3000", "0"), ("600", "0"), ("40", "0"), ("160", "1"), ("64", "1"),
+                                         ("8", "0")])
+def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket, cold):
+    """Buckets past the per-wave capacity (ranked by their workgroup, the overflow list gathered),
+    tiny ones, cold-start splitters from the batch's own samples, and warm splitters that no longer
+    fit the keys (a plain batch after prefixed ones and back: most endpoints in a few buckets),
+    with keys longer than the 16-byte prefix, give the same verdicts and reports."""
     monkeypatch.setenv("FDBCS_SORT_BUCKET", bucket)
-    monkeypatch.setenv("FDBCS_SORT_SAMPLES", samples)
+    monkeypatch.setenv("FDBCS_SORT_COLD", cold)
     rng = np.random.default_rng(31)
     seq = []
     now = 10
-    for i in range(4):
+    for i in range(6):
         pb = W.random_small_batch(rng, 700, alphabet=3, max_len=4, now=now, staleness=10, report_frac=0.5)
         if i % 2:  # every key behind a shared 17-byte prefix: prefix ties resolved by the tail bytes
             pb = prefixed(pb, b"\x02tenant\x00orders\x00\x15\x01")
         seq.append((pb, now, now - 3))
         now += 2
-    run_pair(engine, oracle_mod, seq)
+    e, _ = run_pair(engine, oracle_mod, seq)
+    if bucket in ("3000", "600"):
+        assert e.cs.stats()["sort_big_buckets"] > 0  # the workgroup path ran
 
 
 def prefixed(pb, prefix):
@@ -538,7 +542,7 @@ def test_empty_batches(engine, oracle_mod):
 # Every engine knob that selects a different kernel or submission path (DESIGN.md §5 "Engine knobs")
 # is parity-tested here; knobs measured slower and not kept were deleted with their code.
 @pytest.mark.parametrize("knobs", [{"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
-                                   {"FDBCS_SORT_WIN": "0"},
+                                   {"FDBCS_SORT_COLD": "1"},
                                    {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
