@@ -398,8 +398,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     // takes at the default target (sort_bucket_count clamps smaller targets to it)
     const int64_t slab_buckets = std::min<int64_t>(kSortMaxBuckets, (E + kSortTarget - 1) / kSortTarget + 1);
     TAKE(items, sizeof(SortItem) * E);
-    TAKE(scnt0, 8 * kSortMaxBuckets);
-    TAKE(scnt1, 8 * kSortMaxBuckets);
+    TAKE(scnt, 8 * kCntStride * (size_t)kSortMaxBuckets);
     TAKE(slab, sizeof(SortItem) * kSlab * slab_buckets);
     TAKE(ovf, sizeof(SortItem) * E);
     TAKE(ovf_b, 4 * E);
@@ -450,8 +449,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     HIPOK(hipMemsetAsync(w.hist_conf, 0, T, cs->stream));
     HIPOK(hipMemsetAsync(w.rconf, 0, R, cs->stream));
     HIPOK(hipMemsetAsync(w.ecur, 0, 4 * R, cs->stream));
-    HIPOK(hipMemsetAsync(w.scnt0, 0, 8 * kSortMaxBuckets, cs->stream));
-    HIPOK(hipMemsetAsync(w.scnt1, 0, 8 * kSortMaxBuckets, cs->stream));
+    HIPOK(hipMemsetAsync(w.scnt, 0, 8 * kCntStride * (size_t)kSortMaxBuckets, cs->stream));
     HIPOK(hipMemsetAsync(w.srank, 0, 4 * (kMaxSample + 64), cs->stream));
     HIPOK(hipMemsetAsync(w.bsc, 0, sizeof(BatchScalars), cs->stream));
     // compaction arrays are shared (stage B only)

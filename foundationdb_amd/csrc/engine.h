@@ -138,6 +138,7 @@ constexpr int kSortMaxBuckets = 4096;
 constexpr int kQuant = 4096;
 constexpr int kQuantMinE = 2048;  // batches with fewer endpoints leave the quantiles as they are
 constexpr int kMaxSample = 8192;
+constexpr int kCntStride = 16;  // u64 words per sort bucket counter line
 // A splitter: the projection of an endpoint onto its first kSplitBytes key bytes (big-endian
 // words, zero past the key), min(len, kSplitBytes + 1), and for keys no longer than kSplitBytes
 // the class and id (meta).  Projections are monotone in the full order (keys tied on their first
@@ -159,8 +160,8 @@ struct Work {
     // D.Sort (k_sort_partition / k_sort_bucket): endpoints partitioned into buckets between
     // splitters, each bucket sorted by one wave (or its workgroup past kSlab endpoints)
     SortItem* items;       // [E] sorted endpoints (FDBCS_VALIDATE only)
-    uint64_t* scnt0;       // [kSortMaxBuckets] per bucket: endpoints | write-begins << 32 (zeroed per batch)
-    uint64_t* scnt1;       // [kSortMaxBuckets] per bucket: read-begins | write-ends << 32 (zeroed per batch)
+    uint64_t* scnt;        // [kCntStride kSortMaxBuckets] per bucket, one 128-byte line: endpoints |
+                           // write-begins << 32, read-begins | write-ends << 32 (zeroed per batch)
     SortItem* slab;        // [slab_buckets * kSlab] each bucket's first kSlab endpoints
     int32_t slab_buckets;  // buckets the slab holds
     SortItem* ovf;         // [E] endpoints past their bucket's slab

@@ -1035,9 +1035,12 @@ __device__ __forceinline__ int split_cmp_rest(const uint64_t (&a)[kSplitWords], 
     return (ameta >> 2) < (b.meta >> 2) ? -1 : ((ameta >> 2) > (b.meta >> 2) ? 1 : 0);
 }
 
+// Bucket k's counters: cnt[kCntStride k] = endpoints | write-begins << 32, cnt[kCntStride k + 1] =
+// read-begins | write-ends << 32, one bucket per 128-byte line: the atomics of different buckets
+// never share a line (device-scope atomics on one line serialize at the memory side).
 struct SortArgs {
     const SplitKey* quant;
-    uint64_t *cnt0, *cnt1;
+    uint64_t* cnt;
     SortItem* slab;
     SortItem* ovf;
     int32_t* ovf_b;
@@ -1095,9 +1098,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     if (a.trace) trace_max(a.trace, kTrPartSearch);
     const uint32_t cls = item_class(it.meta);
     const unsigned long long old =
-        atomicAdd((unsigned long long*)&a.cnt0[bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
+        atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
     if (cls == kReadBegin || cls == kWriteEnd)
-        atomicAdd((unsigned long long*)&a.cnt1[bk], cls == kReadBegin ? 1ull : 1ull << 32);
+        atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk + 1], cls == kReadBegin ? 1ull : 1ull << 32);
     const uint32_t slot = (uint32_t)old;
     if (slot < (uint32_t)kSlab) {
         a.slab[(size_t)bk * kSlab + slot] = it;
@@ -1235,8 +1238,8 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = k0 + u * kBlock;
-            c0[u] = k < nb ? a.cnt0[k] : 0;
-            c1[u] = k < nb ? a.cnt1[k] : 0;
+            c0[u] = k < nb ? a.cnt[(size_t)kCntStride * k] : 0;
+            c1[u] = k < nb ? a.cnt[(size_t)kCntStride * k + 1] : 0;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1499,7 +1502,7 @@ int sort_bucket_count(int64_t E, int target, int slab_buckets) {
 }
 
 static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb) {
-    return SortArgs{quant, w.scnt0, w.scnt1, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
+    return SortArgs{quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
 }
 
 void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
@@ -1547,8 +1550,7 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     double total = 0;
     for (int r = 0; r < reps && err == hipSuccess; r++) {
-        (void)hipMemsetAsync(w.scnt0, 0, 8 * kSortMaxBuckets, s);
-        (void)hipMemsetAsync(w.scnt1, 0, 8 * kSortMaxBuckets, s);
+        (void)hipMemsetAsync(w.scnt, 0, 8 * kCntStride * (size_t)kSortMaxBuckets, s);
         (void)hipMemsetAsync(&w.bsc->ovf_n, 0, 4, s);
         if (which == 1) (void)hipEventRecord(e0, s);
         fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
@@ -1564,8 +1566,7 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
         if ((err = hipEventElapsedTime(&ms, e0, e1))) break;
         total += ms;
     }
-    (void)hipMemsetAsync(w.scnt0, 0, 8 * kSortMaxBuckets, s);
-    (void)hipMemsetAsync(w.scnt1, 0, 8 * kSortMaxBuckets, s);
+    (void)hipMemsetAsync(w.scnt, 0, 8 * kCntStride * (size_t)kSortMaxBuckets, s);
     (void)hipMemsetAsync(w.bsc, 0, sizeof(BatchScalars), s);
     (void)hipStreamSynchronize(s);
     (void)hipEventDestroy(e0);
@@ -2312,8 +2313,7 @@ struct Epilogue {
     int64_t zero32_n;
     uint64_t* zero64;  // scan arena
     int64_t zero64_n;
-    uint64_t* zero_bc;  // sort bucket counts [kSortMaxBuckets] (two arrays)
-    uint64_t* zero_bk;
+    uint64_t* zero_bc;  // sort bucket counters [kCntStride kSortMaxBuckets] (two words of each line used)
     int32_t* zero_rank;  // cold-start sample ranks [kMaxSample + 64]
     BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
 };
@@ -2598,8 +2598,7 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
     ep.zero32_n = w.cap_R;
     ep.zero64 = w.scan_arena;
     ep.zero64_n = w.scan_words;
-    ep.zero_bc = w.scnt0;
-    ep.zero_bk = w.scnt1;
+    ep.zero_bc = w.scnt;
     ep.zero_rank = w.srank;
     ep.bsc = w.bsc;
     return ep;
@@ -2909,8 +2908,8 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
     for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
     for (int64_t i = tid; i < kSortMaxBuckets; i += stride) {
-        ep.zero_bc[i] = 0;
-        ep.zero_bk[i] = 0;
+        ep.zero_bc[(size_t)kCntStride * i] = 0;
+        ep.zero_bc[(size_t)kCntStride * i + 1] = 0;
     }
     for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
     __syncthreads();

@@ -202,6 +202,33 @@ __global__ __launch_bounds__(256) void k_wavebitonic(const Item* a, Item* o, con
     if (lane < m) o[off + lane] = a[off + id];
 }
 
+
+// bucket reservation pattern of k_sort_partition: one returning 64-bit atomic per element on the
+// counter of a pseudo-random bucket (stride: u64 words between counters)
+__global__ __launch_bounds__(256) void k_resv(unsigned long long* cnt, int stride, int nb, int n, int* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int b = (int)(((uint32_t)i * 2654435761u) % (uint32_t)nb);
+    const unsigned long long old = atomicAdd(&cnt[(size_t)b * stride], 1ull);
+    out[i] = (int)old;
+}
+// the same with the atomics of a workgroup's elements aggregated per bucket in LDS first
+__global__ __launch_bounds__(256) void k_resv_lds(unsigned long long* cnt, int stride, int nb, int n, int* out) {
+    extern __shared__ int hist[];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    const int b = (int)(((uint32_t)i * 2654435761u) % (uint32_t)nb);
+    int local = i < n ? atomicAdd(&hist[b], 1) : 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) {
+        const int c = hist[k];
+        hist[k] = c ? (int)atomicAdd(&cnt[(size_t)k * stride], (unsigned long long)c) : 0;
+    }
+    __syncthreads();
+    if (i < n) out[i] = hist[b] + local;
+}
+
 static int* g_flag = nullptr;
 static int* g_dflag = nullptr;
 
@@ -286,6 +313,24 @@ int main() {
         CK(hipFree(out));
     }
 
+    {
+        unsigned long long* cnt;
+        int* out;
+        CK(hipMalloc(&cnt, 8 * 16 * 4096));
+        CK(hipMalloc(&out, 4 * n));
+        for (int stride : {1, 2, 16}) {
+            auto r = [&] {
+                CK(hipMemsetAsync(cnt, 0, 8 * 16 * 4096, s));
+                hipLaunchKernelGGL(k_resv, dim3((n + 255) / 256), dim3(256), 0, s, cnt, stride, 1094, n, out);
+            };
+            auto rl = [&] {
+                CK(hipMemsetAsync(cnt, 0, 8 * 16 * 4096, s));
+                hipLaunchKernelGGL(k_resv_lds, dim3((n + 255) / 256), dim3(256), 4 * 1094, s, cnt, stride, 1094, n, out);
+            };
+            printf("reserve 70k in 1094 buckets, stride %2d: memset+atomics %.2f us, memset+lds-aggregated %.2f us\n",
+                   stride, timed(s, N, r), timed(s, N, rl));
+        }
+    }
     {
         unsigned long long* ck;
         CK(hipMalloc(&ck, 64));
