@@ -412,7 +412,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(cwb, 4 * (E + 1));
     TAKE(crb, 4 * (E + 1));
     TAKE(cwe, 4 * (E + 1));
-    TAKE(segflag, E + 1);
+    TAKE(wends, 8 * (2 * W + 1));
     TAKE(wbpos, 4 * W);
     TAKE(wlead, 4 * (W + 1));
     TAKE(wtxn, 4 * (W + 1));
@@ -428,7 +428,6 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(pre_ep, 4 * T);
     TAKE(pre_end, 4 * T);
     TAKE(tedges, 4 * edge_cap);
-    TAKE(cov, 4 * E);
     TAKE(mcs_bits, 8 * (E / 64 + 2));
     TAKE(seg_b, 4 * (W + 1));
     TAKE(seg_e, 4 * (W + 1));
@@ -1739,7 +1738,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhCheck);
     if (sa != s && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
     if (split && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
-    launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp);
+    launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp, sc);
     if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
         launch_conflict_output(s, bd, w, (const int32_t*)sl->pin_inv.dp, b->out_n, b->out_dev);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf (into the host-mapped results)
@@ -1749,7 +1748,6 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         launch_copy_bytes(s, hdv + o_fc, w.first_conf, 4 * T);
     }
     mark(kPhIntra);
-    launch_combine(s, bd, w, sc);
     mark(kPhCombine);
     const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;

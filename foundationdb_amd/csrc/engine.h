@@ -113,7 +113,7 @@ struct Segs {
 };
 
 // Scans of one batch (each owns a slice of the per-batch zeroed scan arena).
-enum ScanKind { kScanPos, kScanEdges, kScanCov, kScanSeg, kScanSegSum, kScanCompact, kScanGc, kNumScans };
+enum ScanKind { kScanEdges, kScanSegSum, kScanCompact, kScanGc, kNumScans };
 
 // Device copy of one batch's packed input (tooOld transactions carry no ranges,
 // as in addTransaction, SkipList.cpp:770-790).
@@ -175,7 +175,7 @@ struct Work {
     int32_t* cwb;          // [E+1] write-begins before each position
     int32_t* crb;          // [E+1] read-begins before each position
     int32_t* cwe;          // [E+1] write-ends before each position
-    uint8_t* segflag;      // [E] bit0: union segment starts here, bit1: one ends here
+    int2* wends;           // [2W] write endpoints in sorted order: (position, 2 owner + is-end; -1 empty write)
     int32_t* wbpos;        // [W] positions of write-begins in order
     int32_t* rbpos;        // [R] positions of read-begins in order
     int32_t* eoff;         // [R+1] first edge slot of each read
@@ -197,7 +197,6 @@ struct Work {
     int32_t* pre_ep;       // [T] k_resolve pre-pass: start of t's packed live writers in tedges
     int32_t* pre_end;      // [T] k_resolve pre-pass: end of t's packed live writers
     int32_t* tedges;       // [edge_cap] per transaction, its writers not known aborted (packed)
-    int32_t* cov;          // [E]
     uint64_t* mcs_bits;    // [E/64+1] sequential-fallback MiniConflictSet
     // union segments (<= W)
     int32_t* seg_b;        // position of segment begin
@@ -252,7 +251,7 @@ struct Tier {
 };
 // Per batch, two stages on two streams:
 //   A (history-independent): launch_sort (D.Sort + positions), launch_edges;
-//   B (reads/writes the history, in batch order): launch_check, launch_resolve, launch_combine,
+//   B (reads/writes the history, in batch order): launch_check, launch_resolve (+ D.Combine),
 //     launch_merge, launch_compact/gc, launch_epilogue.
 // D.Sort and the sorted positions (replaces the sample sort + position scan): splitters from the
 // quantile table `quant` (cold: written first from this batch's ranked samples, k_sample +
@@ -280,8 +279,7 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);
 // verdict_out: the batch's host-mapped verdict bytes (the epilogue publishes them with the flag).
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out);
-void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc);
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out, Scalars* sc);
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 // `srcm` are the source tier's levels: its key index is searched, its top level reset for the
 // epilogue's rebuild.

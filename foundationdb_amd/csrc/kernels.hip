@@ -1631,6 +1631,14 @@ struct EdgePairScan {
     const int32_t* wowner;
     __device__ void counts(int64_t g, uint32_t& slots, uint32_t& pairs, uint32_t& a) const {
         slots = pairs = a = 0;
+        if (g >= R) {
+            // the write's two entries in the sorted list of write endpoints (index = write
+            // endpoints before its position), read by D.Combine at the end of k_resolve
+            const int pb = w.pos[2 * g], pe = w.pos[2 * g + 1];
+            const int code = pb < pe ? 2 * wowner[g - R] : -1;
+            w.wends[w.cwb[pb] + w.cwe[pb]] = make_int2(pb, code);
+            w.wends[w.cwb[pe] + w.cwe[pe]] = make_int2(pe, code < 0 ? -1 : code + 1);
+        }
         if (g >= R && w.groups) {
             // write-begin index j of this write; it leads a group unless the write before it in
             // sorted order contains the same read-begins (then that group's edges cover it)
@@ -1784,7 +1792,93 @@ __device__ __forceinline__ uint8_t verdict_byte(const BatchDev& b, int t, uint8_
     return status == kCommitted ? 2 : 0;     // TransactionCommitted : TransactionConflict
 }
 
-__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vout) {
+// D.Combine (combineWriteConflictRanges, SkipList.cpp:926-939), run by workgroup 0 of k_resolve
+// once every status is final: +1 at the begin and -1 at the end of every committed non-empty write,
+// summed over the write endpoints in sorted order (wends, from stage A), gives the coverage before
+// each; a union segment [key(begin), key(end)) starts where coverage leaves 0 and ends where it
+// returns.  Positions that are not write endpoints add nothing, so this equals the coverage over
+// all E positions.  `committed(t)` reads the final status of transaction t.
+__global__ void k_set_i64(int64_t* p, int64_t v) {
+    if (threadIdx.x == 0) *p = v;
+}
+
+template <class Committed>
+__device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed committed) {
+    // wave-strided chunks: wave q of the workgroup owns kPer * 64 consecutive write endpoints,
+    // lane l holding slot k's endpoint q * 64 kPer + 64 k + l, so every load and store of a slot is
+    // one coalesced access; scans run along (k, lane) inside the wave, then across waves by LDS
+    __shared__ int32_t s_wsum[2][kWG / 64];
+    constexpr int kPer = 16;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int n = 2 * W;
+    auto wave_incl = [&](int x) {
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        return x;
+    };
+    int32_t cov = 0, nseg = 0;  // carried over chunks (uniform)
+    for (int c0 = 0; c0 < n; c0 += kPer * (int)blockDim.x) {
+        const int wb = c0 + wid * 64 * kPer;
+        int2 e[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int i = wb + 64 * k + lane;
+            e[k] = i < n ? w.wends[i] : make_int2(0, -1);
+        }
+        // coverage before each endpoint inside the wave
+        int d[kPer], cb[kPer], run = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            d[k] = e[k].y >= 0 && committed(e[k].y >> 1) ? ((e[k].y & 1) ? -1 : 1) : 0;
+            const int x = wave_incl(d[k]);
+            cb[k] = run + x - d[k];
+            run += __shfl(x, 63, 64);
+        }
+        if (lane == 0) s_wsum[0][wid] = run;
+        __syncthreads();
+        int off = cov, tot = 0;
+        for (int q = 0; q < nw; q++) {
+            const int v = s_wsum[0][q];
+            if (q < wid) off += v;
+            tot += v;
+        }
+        // a segment begins where coverage leaves 0 and ends where it returns to 0
+        uint32_t bm = 0, em = 0;
+        int bc[kPer], brun = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const int c = off + cb[k];
+            const int beg = d[k] == 1 && c == 0;
+            if (beg) bm |= 1u << k;
+            if (d[k] == -1 && c == 1) em |= 1u << k;
+            const int x = wave_incl(beg);
+            bc[k] = brun + x - beg;
+            brun += __shfl(x, 63, 64);
+        }
+        if (lane == 0) s_wsum[1][wid] = brun;
+        __syncthreads();
+        int soff = nseg, stot = 0;
+        for (int q = 0; q < nw; q++) {
+            const int v = s_wsum[1][q];
+            if (q < wid) soff += v;
+            stot += v;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if (bm & (1u << k)) w.seg_b[soff + bc[k]] = e[k].x;
+            if (em & (1u << k)) w.seg_e[soff + bc[k] - 1] = e[k].x;
+        }
+        cov += tot;
+        nseg += stot;
+        __syncthreads();  // s_wsum is rewritten by the next chunk
+    }
+    if (threadIdx.x == 0) hs->n_segments = nseg;
+}
+
+__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vout, Scalars* hs) {
     BatchScalars* sc = w.bsc;
     extern __shared__ __attribute__((aligned(16))) uint8_t st[];
     __shared__ int s_more;
@@ -1800,6 +1894,13 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
             vout[t] = verdict_byte(b, t, st);
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) sc->rounds = 0;
+        if (blockIdx.x != 0) return;
+        // the statuses again, into LDS with coalesced loads, for D.Combine's lookups
+        for (int t = threadIdx.x; t < T; t += blockDim.x)
+            st[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
+        __syncthreads();
+        combine_segments(w, b.W, hs, [&](int t) { return st[t] == kCommitted; });
+        if (threadIdx.x == 0) trace_max(w.trace, kTrResEnd);
         return;
     }
     // Pre-pass on every workgroup, one wave per transaction: skip the candidate writers already
@@ -2193,6 +2294,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         vout[t] = verdict_byte(b, t, st[t]);
     }
     if (threadIdx.x == 0) sc->rounds = rounds;
+    combine_segments(w, b.W, hs, [&](int t) { return st[t] == kCommitted; });
     if (threadIdx.x == 0) trace_max(w.trace, kTrResEnd);
 }
 
@@ -2222,8 +2324,11 @@ void init_kernel_attributes() {
     (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLdsMax);
 }
 
-void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out) {
-    if (b.T == 0) return;
+void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out, Scalars* sc) {
+    if (b.T == 0) {  // no transactions, no writes: no union segments
+        fdb_launch(k_set_i64, dim3(1), dim3(64), 0, s, &sc->n_segments, (int64_t)0);
+        return;
+    }
     // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
     const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
     size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
@@ -2234,63 +2339,8 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
         wl.member_lds = (int32_t)std::min<size_t>(room, (size_t)b.W);
         lds += 8 * (size_t)wl.member_lds;
     }
-    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out);
+    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out, sc);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
-}
-
-// ------------------------------------------------------------------ D.Combine
-//
-// combineWriteConflictRanges (SkipList.cpp:926-939): coverage of committed non-empty writes over
-// sorted positions; each maximal covered run is one union segment [key(begin), key(end)).
-
-struct Delta {
-    const uint32_t* pmeta;
-    const int32_t* pos;
-    const uint8_t* status;
-    const int32_t* wowner;
-    int32_t R;
-    // +1 at the begin and -1 at the end of every committed, non-empty write range
-    __device__ int32_t operator()(int64_t p) const {
-        const uint32_t meta = pmeta[p];
-        const uint32_t c = item_class(meta);
-        if (c != kWriteBegin && c != kWriteEnd) return 0;
-        const int g = (int)item_range(meta);
-        if (status[wowner[g - R]] != kCommitted) return 0;
-        if (pos[2 * g] >= pos[2 * g + 1]) return 0;
-        return c == kWriteBegin ? 1 : -1;
-    }
-};
-
-// Coverage before each position; a segment starts where coverage leaves 0 and ends where it returns.
-struct CoverScan {
-    Delta d;
-    uint8_t* segflag;
-    __device__ void load(int64_t p, uint32_t (&v)[1]) const { v[0] = (uint32_t)d(p); }
-    __device__ void store(int64_t p, const uint32_t (&ex)[1]) const {
-        const int32_t before = (int32_t)ex[0], dp = d(p);
-        segflag[p] = (uint8_t)((dp == 1 && before == 0 ? 1 : 0) | (dp == -1 && before == 1 ? 2 : 0));
-    }
-    __device__ void finish(const uint32_t (&)[1]) const {}
-};
-
-struct SegmentScan {
-    const uint8_t* segflag;
-    int32_t *seg_b, *seg_e;
-    Scalars* sc;
-    __device__ void load(int64_t p, uint32_t (&v)[1]) const { v[0] = segflag[p] & 1u; }
-    __device__ void store(int64_t p, const uint32_t (&ex)[1]) const {
-        const uint8_t f = segflag[p];
-        if (f & 1) seg_b[ex[0]] = (int32_t)p;
-        if (f & 2) seg_e[ex[0] - 1] = (int32_t)p;
-    }
-    __device__ void finish(const uint32_t (&tot)[1]) const { sc->n_segments = tot[0]; }
-};
-
-void launch_combine(hipStream_t s, const BatchDev& b, const Work& w, Scalars* sc) {
-    const int E = 2 * (b.R + b.W);
-    Delta d{w.pmeta, w.pos, w.status, b.wowner, b.R};
-    launch_scan2<1, CoverScan, 1, SegmentScan>(s, CoverScan{d, w.segflag}, SegmentScan{w.segflag, w.seg_b, w.seg_e, sc}, E,
-                                               w.scan[kScanCov], w.scan[kScanSeg]);
 }
 
 // Epilogue work of a batch (k_epilogue, or fused into the merge copy when the batch does not
@@ -2349,43 +2399,6 @@ __device__ __forceinline__ const DKey& seg_key(const BatchDev& b, const Work& w,
     return b.keys[2 * g + end];
 }
 
-template <bool LONG>
-__global__ __launch_bounds__(kBlock) void k_seg_search(BatchDev b, Work w, Hist h, MaxLevels hm,
-                                                       const uint8_t* htail, const Scalars* sc, const int64_t* n_in,
-                                                       int64_t* lvl3, int64_t lvl3_n) {
-    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the history check of this batch is done with the old hierarchy: reset its top level for the
-    // epilogue's atomicMax build
-    for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
-    // 2*kArity lanes per union segment: lane group 0 locates B, group 1 locates E (cooperative search)
-    const int U = sc->n_segments;
-    const int s = (int)(gt / (2 * kArity)), role = (int)((gt / kArity) & 1);
-    const bool live = s < U;
-    const int64_t n = *n_in;
-    int64_t pos = 0;
-    bool eq = false;
-    DKey kb{}, ke{};
-    if (live) {
-        kb = seg_key(b, w, w.seg_b[s], 0);
-        ke = seg_key(b, w, w.seg_e[s], 1);
-        pos = group_lower_bound<LONG>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
-    }
-    const int lane = threadIdx.x & 63;
-    const int64_t hi = __shfl(pos, (lane + kArity) & 63, 64);
-    const int exact = __shfl((int)eq, (lane + kArity) & 63, 64);
-    if (!live || (gt % (2 * kArity)) != 0) return;
-    const int64_t lo = pos;
-    const bool glue = s + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[s + 1], 0), b.tail, ke, b.tail) == 0;
-    const bool endins = !exact && !glue;
-    w.seg_lo[s] = lo;
-    w.seg_hi[s] = hi;
-    w.seg_rem[s] = hi - lo;
-    w.seg_ins[s] = endins ? 2 : 1;
-    w.seg_endins[s] = endins ? 1 : 0;
-    w.seg_vend[s] = hi > 0 ? h.ver[hi - 1] : kHole;
-    w.seg_tlen[s] = tail_units(kb.len) + (endins ? tail_units(ke.len) : 0u);  // 8-byte units
-}
-
 constexpr int kDeltaTile = 256;   // copy tile of the (small) delta tier: ~4 workgroups per CU at C2
 constexpr int kBaseTile = 4096;   // copy tile of the base tier during compaction
 
@@ -2400,37 +2413,113 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
     for (int64_t t = t0; t <= n / tile + 1; t++) tile_first[t] = (int32_t)U;
 }
 
-// Exclusive prefixes of removed boundaries, inserted boundaries and tail units per union segment,
-// plus tile_first for the copy.
-struct SegSumScan {
-    Segs g;
-    int64_t* tlen;
-    TierIO io;
-    Scalars* sc;
-    __device__ void load(int64_t j, uint32_t (&v)[3]) const {
-        v[0] = (uint32_t)g.rem[j];
-        v[1] = (uint32_t)g.ins[j];
-        v[2] = (uint32_t)tlen[j];
+// Per union segment (mergeWriteConflictRanges' insertion points, SkipList.cpp:899-924): lo / hi =
+// the delta boundaries [lo, hi) the segment removes (lower bounds of B and E), whether E needs a
+// boundary of its own (no exact match, not glued to the next segment's B) and the version it
+// inherits, then the exclusive prefixes of removed boundaries, inserted boundaries and tail units
+// with one decoupled look-back across tiles, and tile_first for the copy.  One workgroup per tile
+// of kSegPer segments, 16 lanes each (8 locate B, 8 locate E, cooperatively), plus 8 lanes that
+// locate the B of the segment before the tile, whose lo bounds the tile's first copy tiles.
+constexpr int kSegPer = kWG / (2 * kArity) - 1;  // 63
+
+inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / kSegPer + 1; }
+
+template <bool LONG>
+__global__ __launch_bounds__(kWG) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm, const uint8_t* htail,
+                                                  Scalars* sc, TierIO io, int64_t* lvl3, int64_t lvl3_n) {
+    __shared__ int64_t s_lo[kSegPer + 1];       // lo of the segment before the tile, then the tile's
+    __shared__ uint32_t s_val[3][kSegPer + 1];  // removed, inserted, tail units per segment
+    __shared__ uint32_t s_base[3];
+    __shared__ int s_tile;
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the history check of this batch is done with the old hierarchy: reset its top level for the
+    // epilogue's atomicMax build
+    for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanSegSum].counter, 1);
+    __syncthreads();
+    const int tile = s_tile;
+    const int U = (int)sc->n_segments;
+    const int ntiles = U > 0 ? (U + kSegPer - 1) / kSegPer : 1;
+    if (tile >= ntiles) return;  // spare workgroup: nobody waits on it
+    const int64_t n = *io.n_in;
+    const int q = threadIdx.x / (2 * kArity), role = (threadIdx.x / kArity) & 1;
+    const int sg = tile * kSegPer + (q < kSegPer ? q : -1);  // slot kSegPer: the segment before
+    const bool live = sg >= 0 && sg < U && (q < kSegPer || role == 0);
+    int64_t pos = 0;
+    bool eq = false;
+    DKey kb{}, ke{};
+    if (live) {
+        kb = seg_key(b, w, w.seg_b[sg], 0);
+        ke = seg_key(b, w, w.seg_e[sg], 1);
+        pos = group_lower_bound<LONG>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
     }
-    __device__ void store(int64_t j, const uint32_t (&ex)[3]) const {
-        g.rem[j] = ex[0];
-        g.ins[j] = ex[1];
-        tlen[j] = ex[2];
-        fill_tile_first(g.tile_first, g.lo, j, kDeltaTile);
+    const int lane = threadIdx.x & 63;
+    const int64_t hi = __shfl(pos, (lane + kArity) & 63, 64);
+    const int exact = __shfl((int)eq, (lane + kArity) & 63, 64);
+    if (threadIdx.x % (2 * kArity) == 0) {
+        if (q == kSegPer) {
+            s_lo[0] = live ? pos : 0;
+        } else if (live) {
+            const int64_t lo = pos;
+            const bool glue = sg + 1 < U && dkey_cmp(seg_key(b, w, w.seg_b[sg + 1], 0), b.tail, ke, b.tail) == 0;
+            const bool endins = !exact && !glue;
+            w.seg_lo[sg] = lo;
+            w.seg_hi[sg] = hi;
+            w.seg_endins[sg] = endins ? 1 : 0;
+            w.seg_vend[sg] = hi > 0 ? h.ver[hi - 1] : kHole;
+            s_lo[q + 1] = lo;
+            s_val[0][q] = (uint32_t)(hi - lo);
+            s_val[1][q] = endins ? 2 : 1;
+            s_val[2][q] = tail_units(kb.len) + (endins ? tail_units(ke.len) : 0u);  // 8-byte units
+        } else {
+            s_val[0][q] = s_val[1][q] = s_val[2][q] = 0;
+        }
     }
-    __device__ void finish(const uint32_t (&tot)[3]) const {
-        const int64_t U = sc->n_segments, n = *io.n_in;
-        // sentinel entries at U: totals, used by the copy kernel for elements after every segment
-        g.rem[U] = tot[0];
-        g.ins[U] = tot[1];
-        tlen[U] = tot[2];
-        fill_tile_first_tail(g.tile_first, g.lo, U, n, kDeltaTile);
-        *io.before = n;
-        *io.removed = tot[0];
-        *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
-        sc->tail_next = sc->tail_used + 8 * (int64_t)tot[2];
+    __syncthreads();
+    uint32_t ex[3] = {0, 0, 0};
+    if (threadIdx.x < 64) {
+        uint32_t btot[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint32_t v = lane < kSegPer ? s_val[c][lane] : 0u;
+            uint32_t x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            ex[c] = x - v;
+            btot[c] = __shfl(x, 63, 64);
+        }
+        tile_lookback<3>(w.scan[kScanSegSum], tile, btot, s_base);
     }
-};
+    __syncthreads();
+    if (threadIdx.x < 64) {  // lanes 0..kSegPer: the tile's segments, then the one after it
+        const int j = tile * kSegPer + lane;
+        if (lane < kSegPer && j < U) {
+            w.seg_rem[j] = s_base[0] + ex[0];
+            w.seg_ins[j] = s_base[1] + ex[1];
+            w.seg_tlen[j] = s_base[2] + ex[2];
+            // tile_first[t] = j for the copy tiles t in (lo[j-1] / tile, lo[j] / tile]
+            const int64_t t0 = j > 0 ? s_lo[lane] / kDeltaTile + 1 : 0;
+            for (int64_t t = t0; t <= s_lo[lane + 1] / kDeltaTile; t++) w.tile_first[t] = j;
+        }
+        if (tile == ntiles - 1 && j == U) {
+            // sentinel entries at U (totals, for elements after every segment), the remaining copy
+            // tiles and the tier's new size
+            const uint32_t r = s_base[0] + ex[0], in = s_base[1] + ex[1], tl = s_base[2] + ex[2];
+            w.seg_rem[U] = r;
+            w.seg_ins[U] = in;
+            w.seg_tlen[U] = tl;
+            const int64_t t0 = U > 0 ? s_lo[lane] / kDeltaTile + 1 : 0;
+            for (int64_t t = t0; t <= n / kDeltaTile + 1; t++) w.tile_first[t] = U;
+            *io.before = n;
+            *io.removed = r;
+            *io.n_out = n - (int64_t)r + (int64_t)in;
+            sc->tail_next = sc->tail_used + 8 * (int64_t)tl;
+        }
+    }
+}
 
 constexpr int kSegLds = 1024;
 
@@ -2607,12 +2696,9 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
                   hipEvent_t copy_begin, hipEvent_t copy_end, bool long_keys) {
-    const int Wn = b.W > 0 ? b.W : 1;
-    fdb_launch(long_keys ? k_seg_search<true> : k_seg_search<false>, dim3((2 * kArity * Wn + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w, src, srcm,
-               htail, sc, &sc->nd, srcm.lvl[3], lvl3_n);
     const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
-    launch_scan<3>(s, SegSumScan{batch_segs(w), w.seg_tlen, io, sc}, &sc->n_segments, (int64_t)b.W + 1,
-                   w.scan[kScanSegSum]);
+    fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_prep_tiles(b.W)), dim3(kWG), 0, s, b,
+               w, src, srcm, htail, sc, io, srcm.lvl[3], lvl3_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
     ins.b = b;
@@ -2776,18 +2862,17 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, c
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
     const int64_t E = 2 * (R + W);
-    return kNumScans + scan_granules(E, 3) + scan_granules(R + W, 2) + 2 * scan_granules(E, 1) +
-           scan_granules(W + 1, 3) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 2);
+    (void)E;
+    return kNumScans + scan_granules(R + W, 2) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 2);
 }
 
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
     const int64_t E = 2 * (R + W);
     uint64_t* a = w.scan_arena;
-    const int64_t gran[kNumScans] = {scan_granules(E, 3),     scan_granules(R + W, 2),
-                                     scan_granules(E, 1),     scan_granules(E, 1),
-                                     scan_granules(W + 1, 3), scan_granules(delta_cap + 1, 2),
-                                     scan_granules(hist_cap, 2)};
+    (void)E;
+    const int64_t gran[kNumScans] = {scan_granules(R + W, 2), 3 * seg_prep_tiles(W),
+                                     scan_granules(delta_cap + 1, 2), scan_granules(hist_cap, 2)};
     uint64_t* g = a + kNumScans;
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);

@@ -42,6 +42,56 @@ struct ScanState {
     int* error;          // set if a look-back spin exceeded its bound
 };
 
+// Decoupled look-back of one tile over K components, run by one whole wave: publishes the tile's
+// aggregate btot, sums the predecessors' (64 tiles per probe, stopping at the first inclusive
+// prefix; tile -1 reads as an inclusive 0), publishes the inclusive prefix and leaves the
+// exclusive prefix in sbase (lane 0 writes it; the caller's barrier makes it visible).
+template <int K>
+__device__ __forceinline__ void tile_lookback(ScanState st, int64_t tile, const uint32_t (&btot)[K],
+                                              uint32_t (&sbase)[K]) {
+    const int lane = threadIdx.x & 63;
+    uint64_t* g = st.granules;
+    // every component's aggregate first, so successors never wait on this tile's own look-back
+    if (lane < K) {
+#pragma unroll
+        for (int c = 0; c < K; c++)
+            if (lane == c) granule_store(&g[(int64_t)tile * K + c], tile == 0 ? 2 : 1, btot[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < K; c++) {
+        uint32_t prefix = 0;
+        int64_t jhi = (int64_t)tile - 1;
+        uint32_t spins = 0;
+        while (jhi >= 0) {
+            const int64_t j = jhi - lane;
+            const uint64_t x = j >= 0 ? granule_load(&g[j * K + c]) : (2ull << 32);
+            const uint32_t status = (uint32_t)(x >> 32);
+            const uint64_t incl = __ballot(status == 2);
+            const uint64_t zero = __ballot(status == 0);
+            const int first = incl ? __ffsll((long long)incl) - 1 : 63;
+            const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
+            if (zero & upto) {  // a tile in the window has not published yet
+                if (++spins > (1u << 24)) {  // bounded: never hang the GPU
+                    if (lane == 0) atomicOr(st.error, 2);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint32_t v = (lane <= first) ? (uint32_t)x : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            prefix += v;
+            if (incl) break;
+            jhi -= 64;
+        }
+        if (lane == 0) {
+            if (tile > 0) granule_store(&g[(int64_t)tile * K + c], 2, prefix + btot[c]);
+            sbase[c] = prefix;
+        }
+    }
+}
+
 // One tile of a scan (tile ids come from the caller, in launch order).  Ends with a barrier, so
 // the LDS arrays can be reused by a following stage.
 template <int K, class F>
@@ -104,44 +154,8 @@ __device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64
         texcl[c] += before;
         btot[c] = all;
     }
-    // phase 3: look-back by wave 0, 64 predecessor tiles per probe (tile -1 reads as an inclusive 0)
-    if (wid == 0) {
-#pragma unroll
-        for (int c = 0; c < K; c++) {
-            uint64_t* g = st.granules;
-            if (lane == 0) granule_store(&g[(int64_t)tile * K + c], tile == 0 ? 2 : 1, btot[c]);
-            uint32_t prefix = 0;
-            int64_t jhi = (int64_t)tile - 1;
-            uint32_t spins = 0;
-            while (jhi >= 0) {
-                const int64_t j = jhi - lane;
-                const uint64_t x = j >= 0 ? granule_load(&g[j * K + c]) : (2ull << 32);
-                const uint32_t status = (uint32_t)(x >> 32);
-                const uint64_t incl = __ballot(status == 2);
-                const uint64_t zero = __ballot(status == 0);
-                const int first = incl ? __ffsll((long long)incl) - 1 : 63;
-                const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1);
-                if (zero & upto) {  // a tile in the window has not published yet
-                    if (++spins > (1u << 24)) {  // bounded: never hang the GPU
-                        if (lane == 0) atomicOr(st.error, 2);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                uint32_t v = (lane <= first) ? (uint32_t)x : 0u;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-                prefix += v;
-                if (incl) break;
-                jhi -= 64;
-            }
-            if (lane == 0) {
-                if (tile > 0) granule_store(&g[(int64_t)tile * K + c], 2, prefix + btot[c]);
-                sbase[c] = prefix;
-            }
-        }
-    }
+    // phase 3: look-back by wave 0
+    if (wid == 0) tile_lookback<K>(st, tile, btot, sbase);
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < K; c++) {

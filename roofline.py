@@ -91,15 +91,13 @@ def kernel_bytes(name: str, s: dict):
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
     if name == "k_resolve":
-        return T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16, "statuses, flags, offsets, edges and writer states, verdicts"
+        return (T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16 + 2 * W * 8 + U * 8,
+                "statuses, flags, offsets, edges and writer states, verdicts; D.Combine: 2W write endpoints, U segments")
     if name == "k_intra_report":
         return R * 12, "per read: edge range, first conflict"
-    if name.startswith("k_scan2<1, fdbcs::CoverScan"):
-        return E * (4 + 8 + 1 + 4 + 2) + U * 8, "per position: meta, range ends, writer status, owner, flags; segments"
-    if name.startswith("k_seg_search"):
-        return U * 2 * (D + look_d) + U * 48, "per segment: 2 keys + 2 delta lookups; 6 words written"
-    if name.startswith("k_scan<3, fdbcs::SegSumScan>"):
-        return U * (24 + 24 + 4), "per segment: 3 counts read, 3 prefixes + tile index written"
+    if name.startswith("k_seg_prep"):
+        return (U * 2 * (D + look_d) + U * (8 + 8 + 1 + 8 + 24 + 4),
+                "per segment: 2 keys + 2 delta lookups; lo, hi, end flag, inherited version, 3 prefixes, tile index")
     if name.startswith("k_merge_copy<fdbcs::BatchIns"):
         return s["merge_bytes"], "32 B per kept and inserted boundary read and per result boundary written (device scalars)"
     if name.startswith("k_merge_copy<fdbcs::CompactIns"):
