@@ -89,7 +89,6 @@ struct BatchScalars {
     int32_t edge_overflow; // candidate edges exceeded capacity -> sequential fallback
     int32_t rounds;        // resolution rounds used
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
-    int32_t pre_done;      // k_resolve workgroups done with the pre-pass (reset by the epilogue)
     int32_t ovf_n;         // sort: endpoints past their bucket's slab (reset by the epilogue)
     int32_t sort_big;      // sort: buckets past the slab, sorted by the workgroup path (reset by the epilogue)
 };

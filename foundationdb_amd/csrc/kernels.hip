@@ -1878,139 +1878,119 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
     if (threadIdx.x == 0) hs->n_segments = nseg;
 }
 
-__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vout, Scalars* hs) {
-    BatchScalars* sc = w.bsc;
-    extern __shared__ __attribute__((aligned(16))) uint8_t st[];
-    __shared__ int s_more;
+// Pre-pass of the resolution, one wave per transaction across the chip (k_resolve_pre), then the
+// batch-order rounds and D.Combine in one workgroup (k_resolve).  Two launches: the rounds keep the
+// status bytes, group minima and members in up to 159 KiB of LDS, and a single kernel would ask
+// that of every pre-pass workgroup too (one per CU, blocked by whatever else holds LDS there).
+__global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint8_t* vout) {
+    const BatchScalars* sc = w.bsc;
     const int T = b.T;
-    if (threadIdx.x == 0) trace_min(w.trace, kTrResBegin);
+    if (blockIdx.x == 0 && threadIdx.x == 0) trace_min(w.trace, kTrResBegin);
     if (sc->n_edges == 0 && !sc->edge_overflow) {
         // no candidate writer anywhere: every admitted transaction without a history conflict
-        // commits (SkipList.cpp:817-833 with an empty MiniConflictSet); all workgroups share the work
+        // commits (SkipList.cpp:817-833 with an empty MiniConflictSet)
         for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
             const uint8_t st = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
             w.status[t] = st;
             w.first_conf[t] = INT_MAX;
             vout[t] = verdict_byte(b, t, st);
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0) sc->rounds = 0;
-        if (blockIdx.x != 0) return;
-        // the statuses again, into LDS with coalesced loads, for D.Combine's lookups
-        for (int t = threadIdx.x; t < T; t += blockDim.x)
-            st[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
+        if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
+        return;
+    }
+    if (sc->edge_overflow || w.no_prepass) return;
+    // Skip the candidate writers already known aborted (history conflict or TooOld), 64 edges per
+    // step with one ballot, and commit the transactions left with none; the rest keep a resume
+    // pointer at their first writer not known aborted.  These are exactly the decisions round one
+    // would make, but a hot key's reader (hundreds of aborted writers, C3) costs a few ballots
+    // instead of a serial walk, and every transaction's chain of dependent loads runs on its own
+    // wave across the chip.
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * (blockDim.x >> 6);
+    for (int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < T; t += nwaves) {
+        uint8_t s0 = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
+        const int r0 = b.roff[t], r1 = b.roff[t + 1];
+        // t's slots are contiguous over its reads: its live writers are packed at their start
+        const int tbase = r0 < r1 ? w.eoff[r0] : 0;
+        int cnt = 0;
+        if (s0 == kUndecided) {
+            // t's reads 64 at a time, their edge runs flattened into one index space so the loads
+            // of every read's edges go out together (per-read chains no longer add up); 256 edges
+            // per step: four 64-edge loads, then their writers' flags
+            for (int rb = r0; rb < r1; rb += 64) {
+                const int nr = min(64, r1 - rb);
+                const int myq = lane < nr ? w.eoff[rb + lane] : 0;
+                const int myn = lane < nr ? w.ecur[rb + lane] : 0;
+                int incl = myn;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                const int excl = incl - myn;  // lanes >= nr hold the total
+                const int total = __shfl(incl, 63, 64);
+                for (int f0 = 0; f0 < total; f0 += 4 * 64) {
+                    int e[4];
+                    bool live[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int f = f0 + 64 * u + lane;
+                        const int fc = f < total ? f : total - 1;
+                        // the read holding flattened edge fc: the last lane with excl <= fc (binary
+                        // lifting, every lane shuffling in step)
+                        int lo = 0;
+#pragma unroll
+                        for (int step = 32; step > 0; step >>= 1) {
+                            const int cand = lo + step;
+                            const int ex = __shfl(excl, cand < 64 ? cand : 63, 64);
+                            if (cand < 64 && ex <= fc) lo = cand;
+                        }
+                        const int q = __shfl(myq, lo, 64) + fc - __shfl(excl, lo, 64);
+                        e[u] = f < total ? w.edges[q] : -1;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const bool in = (unsigned)e[u] < (unsigned)T;
+                        const int ee = in ? e[u] : 0;
+                        const uint8_t hc = w.hist_conf[ee], fl = b.flags[ee];
+                        live[u] = in ? (!hc && !(fl & kFlagTooOld)) : e[u] >= T;  // group edges stay
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint64_t m = __ballot(live[u]);
+                        if (live[u]) w.tedges[tbase + cnt + __popcll(m & ((1ull << lane) - 1))] = e[u];
+                        cnt += __popcll(m);
+                    }
+                }
+            }
+            if (cnt == 0) s0 = kCommitted;
+        }
+        if (lane == 0) {
+            w.pre_st[t] = s0;
+            w.pre_ep[t] = tbase;
+            w.pre_end[t] = tbase + cnt;
+        }
+    }
+    if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
+}
+
+__global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vout, Scalars* hs) {
+    BatchScalars* sc = w.bsc;
+    extern __shared__ __attribute__((aligned(16))) uint8_t st[];
+    __shared__ int s_more;
+    const int T = b.T;
+    if (threadIdx.x == 0) trace_max(w.trace, kTrResWait);
+    if (sc->n_edges == 0 && !sc->edge_overflow) {
+        // k_resolve_pre decided every transaction: the statuses into LDS (coalesced) for D.Combine
+        for (int t = threadIdx.x; t < T; t += blockDim.x) st[t] = w.status[t];
+        if (threadIdx.x == 0) sc->rounds = 0;
         __syncthreads();
+        if (threadIdx.x == 0) trace_max(w.trace, kTrResRounds);
         combine_segments(w, b.W, hs, [&](int t) { return st[t] == kCommitted; });
         if (threadIdx.x == 0) trace_max(w.trace, kTrResEnd);
         return;
     }
-    // Pre-pass on every workgroup, one wave per transaction: skip the candidate writers already
-    // known aborted (history conflict or TooOld), 64 edges per step with one ballot, and commit
-    // the transactions left with none; the rest keep a resume pointer at their first writer not
-    // known aborted.  These are exactly the decisions round one would make, but a hot key's reader
-    // (hundreds of aborted writers, C3) costs a few ballots instead of a serial walk, and every
-    // transaction's chain of dependent loads runs on its own wave across the chip.
-    const bool pre = !sc->edge_overflow && !w.no_prepass;
-    if (pre) {
-        const int lane = threadIdx.x & 63;
-        const int nwaves = gridDim.x * (blockDim.x >> 6);
-        for (int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < T; t += nwaves) {
-            uint8_t s0 = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
-            const int r0 = b.roff[t], r1 = b.roff[t + 1];
-            // t's slots are contiguous over its reads: its live writers are packed at their start
-            const int tbase = r0 < r1 ? w.eoff[r0] : 0;
-            int cnt = 0;
-            if (s0 == kUndecided) {
-                // t's reads 64 at a time, their edge runs flattened into one index space so the
-                // loads of every read's edges go out together (per-read chains no longer add up);
-                // 256 edges per step: four 64-edge loads, then their writers' flags
-                for (int rb = r0; rb < r1; rb += 64) {
-                    const int nr = min(64, r1 - rb);
-                    const int myq = lane < nr ? w.eoff[rb + lane] : 0;
-                    const int myn = lane < nr ? w.ecur[rb + lane] : 0;
-                    int incl = myn;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const int y = __shfl_up(incl, o, 64);
-                        if (lane >= o) incl += y;
-                    }
-                    const int excl = incl - myn;  // lanes >= nr hold the total
-                    const int total = __shfl(incl, 63, 64);
-                    for (int f0 = 0; f0 < total; f0 += 4 * 64) {
-                        int e[4];
-                        bool live[4];
-#pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const int f = f0 + 64 * u + lane;
-                            const int fc = f < total ? f : total - 1;
-                            // the read holding flattened edge fc: the last lane with excl <= fc
-                            // (binary lifting, every lane shuffling in step)
-                            int lo = 0;
-#pragma unroll
-                            for (int step = 32; step > 0; step >>= 1) {
-                                const int cand = lo + step;
-                                const int ex = __shfl(excl, cand < 64 ? cand : 63, 64);
-                                if (cand < 64 && ex <= fc) lo = cand;
-                            }
-                            const int q = __shfl(myq, lo, 64) + fc - __shfl(excl, lo, 64);
-                            e[u] = f < total ? w.edges[q] : -1;
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const bool in = (unsigned)e[u] < (unsigned)T;
-                            const int ee = in ? e[u] : 0;
-                            const uint8_t hc = w.hist_conf[ee], fl = b.flags[ee];
-                            live[u] = in ? (!hc && !(fl & kFlagTooOld)) : e[u] >= T;  // group edges stay
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; u++) {
-                            const uint64_t m = __ballot(live[u]);
-                            if (live[u]) w.tedges[tbase + cnt + __popcll(m & ((1ull << lane) - 1))] = e[u];
-                            cnt += __popcll(m);
-                        }
-                    }
-                }
-                if (cnt == 0) s0 = kCommitted;
-            }
-            if (lane == 0) {
-                w.pre_st[t] = s0;
-                w.pre_ep[t] = tbase;
-                w.pre_end[t] = tbase + cnt;
-            }
-        }
-        // publish (MI355X_MICROARCH.md, inter-workgroup visibility: producer form): every storing
-        // wave waits for its stores, then one lane releases at agent scope and arrives
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(&sc->pre_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (blockIdx.x != 0) return;  // batch-order rounds run in one workgroup
-    // wait (bounded) for every workgroup's pre-pass; on timeout start from scratch instead (the
-    // late writers write pre_st / pre_ep, which are then not read: still exact)
-    __shared__ int s_pre;
-    if (threadIdx.x == 0) {
-        int ok = 0;
-        if (pre) {
-            // consumer form: relaxed poll, then one agent acquire and its wait, then the barrier
-            for (int spin = 0; spin < (1 << 22); spin++) {
-                if (__hip_atomic_load(&sc->pre_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) {
-                    ok = 1;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        s_pre = ok;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) trace_max(w.trace, kTrResWait);
-    const bool use_pre = s_pre != 0;
+    const bool use_pre = !sc->edge_overflow && !w.no_prepass;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         st[t] = use_pre ? w.pre_st[t] : ((w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided);
         w.first_conf[t] = INT_MAX;
@@ -2329,8 +2309,9 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
         fdb_launch(k_set_i64, dim3(1), dim3(64), 0, s, &sc->n_segments, (int64_t)0);
         return;
     }
-    // one wave per transaction for the pre-pass (the rounds themselves run in workgroup 0)
-    const int grid = (int)(((int64_t)b.T * 64 + kWG - 1) / kWG);
+    // one wave per transaction for the pre-pass, then the rounds in one workgroup
+    fdb_launch(k_resolve_pre, dim3((unsigned)(((int64_t)b.T * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, b, w,
+               verdict_out);
     size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
     Work wl = w;
     wl.member_lds = 0;
@@ -2339,7 +2320,7 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
         wl.member_lds = (int32_t)std::min<size_t>(room, (size_t)b.W);
         lds += 8 * (size_t)wl.member_lds;
     }
-    fdb_launch(k_resolve, dim3(grid), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out, sc);
+    fdb_launch(k_resolve, dim3(1), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out, sc);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 
@@ -2381,7 +2362,6 @@ __device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogu
     out->intra_rounds = ep.bsc->rounds;
     out->intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
     out->sort_big = ep.bsc->sort_big;
-    ep.bsc->pre_done = 0;  // k_resolve's pre-pass counter (its workgroups have all finished)
     ep.bsc->debug_error = 0;
     ep.bsc->ovf_n = 0;     // the sort's overflow list and big-bucket count (this batch's sort is done)
     ep.bsc->sort_big = 0;

@@ -84,12 +84,21 @@ def kernel_bytes(name: str, s: dict):
         return E * (2 + D + I) + nb * 8, "E (bucket id + key) read, E items written"
     if name.startswith("k_bucket_sort"):
         return 2 * I * E, "one read and one write of every 32-byte item"
+    if name == "k_sort_partition":
+        return E * (D + I + 8) + nb * 16, "E keys read, E 32-byte items written to their bucket slabs, a counter word each"
+    if name.startswith("k_sort_bucket"):
+        return (E * (I + 4 + 4 + 12) + G * 4 + nb * 16,
+                "E slab items read; position, meta and 3 class prefixes written per endpoint; R+W begin lists")
     if name.startswith("k_scan<3, fdbcs::PosScan>"):
         return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
     if name.startswith("k_scan<2, fdbcs::EdgePairScan>"):
         return G * (8 + 24 + 8) + W * 8, "per range: 2 positions, class prefixes at both, slot/pair offsets"
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
+    if name == "k_resolve_pre":
+        return (T * (1 + 1 + 4 + 1 + 4) + X * (4 + 1 + 1 + 4) + T * 12,
+                "statuses (hist flag, tooOld flag, verdict, first conflict) or the pre-pass: edges, their writers' "
+                "flags, packed live writers, resume pointers")
     if name == "k_resolve":
         return (T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16 + 2 * W * 8 + U * 8,
                 "statuses, flags, offsets, edges and writer states, verdicts; D.Combine: 2W write endpoints, U segments")
@@ -143,7 +152,7 @@ def kernel_table(kprof: dict, s: dict, st: dict = None) -> dict:
     return dict(sorted(rows.items(), key=lambda kv: -kv[1]["total_ms"]))
 
 
-SORT_KERNELS = ("k_sample", "k_bucket_count", "k_bucket_scatter", "k_bucket_sort", "k_sort_")
+SORT_KERNELS = ("k_sample", "k_quant_cold", "k_bucket_count", "k_bucket_scatter", "k_bucket_sort", "k_sort_")
 
 
 def sort_phase(table: dict) -> dict | None:
