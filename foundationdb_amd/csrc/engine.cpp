@@ -803,33 +803,17 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     return FDBCS_OK;
 }
 
-// Stage graphs (FDBCS_GRAPH=2): the event waits leading a stage list and the event records
-// trailing it are issued directly on `st`; the kernels and timing events between them run as one
-// cached graph (keyed by their shape, node parameters updated per batch).  A list with a wait or
-// record between its kernels, or fewer than two kernels, is replayed directly.
-int launch_stage(fdbcs_conflict_set* cs, LaunchList& L, hipStream_t st) {
-    auto is_sync = [](const LaunchList::Rec& r) {
-        return r.kind == LaunchList::kSyncWait || r.kind == LaunchList::kSyncRecord;
-    };
-    const size_t n = L.recs.size();
-    size_t i0 = 0, i1 = n;
-    while (i0 < n && is_sync(L.recs[i0])) i0++;
-    while (i1 > i0 && is_sync(L.recs[i1 - 1])) i1--;
-    int kernels = 0;
-    bool mid_sync = false;
+// Stage graphs (FDBCS_GRAPH=2): a stage list is cut at its cross-stream waits and records,
+// which are issued directly on `st`; every run of two or more kernels (with the timing events
+// between them) goes out as one cached graph, keyed by its kernels and updated with this batch's
+// node parameters (tools/submitbench.hip: a 5-kernel graph with updates costs ~9 us of host time
+// against ~24 us for its direct launches; a single kernel is launched directly).
+int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1, hipStream_t st) {
     uint64_t key = 1469598103934665603ull;
     for (size_t i = i0; i < i1; i++) {
         const LaunchList::Rec& r = L.recs[i];
-        kernels += r.kind == LaunchList::kKernel ? 1 : 0;
-        mid_sync |= is_sync(r);
         key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u)) * 1099511628211ull;
     }
-    if (mid_sync || kernels < 2) {
-        HIPOK(L.replay(st));
-        return FDBCS_OK;
-    }
-    L.finalize();
-    for (size_t i = 0; i < i0; i++) HIPOK(L.issue(L.recs[i], st));
     fdbcs_conflict_set::StageGraph* sg = nullptr;
     for (auto& kv : cs->stage_cache)
         if (kv.first == key) sg = &kv.second;
@@ -875,7 +859,32 @@ int launch_stage(fdbcs_conflict_set* cs, LaunchList& L, hipStream_t st) {
     }
     HIPOK(hipGraphLaunch(sg->exec, st));
     cs->graph_launches++;
-    for (size_t i = i1; i < n; i++) HIPOK(L.issue(L.recs[i], st));
+    return FDBCS_OK;
+}
+
+int launch_stage(fdbcs_conflict_set* cs, LaunchList& L, hipStream_t st) {
+    auto is_sync = [](const LaunchList::Rec& r) {
+        return r.kind == LaunchList::kSyncWait || r.kind == LaunchList::kSyncRecord;
+    };
+    L.finalize();
+    const size_t n = L.recs.size();
+    size_t i = 0;
+    while (i < n) {
+        if (is_sync(L.recs[i])) {
+            HIPOK(L.issue(L.recs[i], st));
+            i++;
+            continue;
+        }
+        size_t j = i;
+        int kernels = 0;
+        while (j < n && !is_sync(L.recs[j])) kernels += L.recs[j++].kind == LaunchList::kKernel ? 1 : 0;
+        if (kernels >= 2) {
+            if (int rc = launch_graph_run(cs, L, i, j, st)) return rc;
+        } else {
+            for (size_t k = i; k < j; k++) HIPOK(L.issue(L.recs[k], st));
+        }
+        i = j;
+    }
     return FDBCS_OK;
 }
 
@@ -1722,10 +1731,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- record stage B: D.CheckRead against the history the previous batch left, then batch order
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
-    // stage graphs: every wait of stage B leads its list (the delta check then starts after stage A)
-    const bool hoist = cs->stage_graphs && timing < 2;
-    if (hoist && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
-    if (hoist && split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
+    const bool graphs = cs->stage_graphs && timing < 2;
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
         launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax);
@@ -1736,8 +1742,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     mark(kPhCheck);
-    if (sa != s && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
-    if (split && !hoist) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
+    if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
+    if (split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp, sc);
     if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
         launch_conflict_output(s, bd, w, (const int32_t*)sl->pin_inv.dp, b->out_n, b->out_dev);
@@ -1838,7 +1844,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->pending_batch = b;
     } else if (flush_pending(cs)) {
         return FDBCS_E_DEVICE;
-    } else if (hoist) {
+    } else if (graphs) {
         if ((rc = launch_stage(cs, la, sa))) return rc;
         if (split && (rc = launch_stage(cs, lc, cs->cstream))) return rc;
         if ((rc = launch_stage(cs, lb, s))) return rc;
@@ -1910,6 +1916,9 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
                     us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),
                     us(kTrResRounds, kTrResEnd));
+            fprintf(stderr, "fdbcs trace: combine chunk 0: loads %.2f, scan1 %.2f, scan2 %.2f, stores %.2f us\n",
+                    us(kTrResRounds, kTrCmbLoad), us(kTrCmbLoad, kTrCmbScan1), us(kTrCmbScan1, kTrCmbScan2),
+                    us(kTrCmbScan2, kTrCmbStore));
 
 
         }

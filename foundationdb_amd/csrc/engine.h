@@ -228,6 +228,7 @@ enum TraceSlot {
     kTrResBegin, kTrResPre, kTrResWait, kTrResRounds, kTrResEnd,
     kTrPartBegin, kTrPartFill, kTrPartSearch, kTrPartEnd,
     kTrBktBegin, kTrBktPrologue, kTrBktSorted, kTrBktEnd,
+    kTrCmbLoad, kTrCmbScan1, kTrCmbScan2, kTrCmbStore,
     kTrSlots
 };
 __device__ __forceinline__ void trace_min(unsigned long long* tr, int slot) {

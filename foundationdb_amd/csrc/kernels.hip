@@ -1804,40 +1804,51 @@ __global__ void k_set_i64(int64_t* p, int64_t v) {
 
 template <class Committed>
 __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed committed) {
-    // wave-strided chunks: wave q of the workgroup owns kPer * 64 consecutive write endpoints,
-    // lane l holding slot k's endpoint q * 64 kPer + 64 k + l, so every load and store of a slot is
-    // one coalesced access; scans run along (k, lane) inside the wave, then across waves by LDS
+    // each lane owns kPer consecutive write endpoints (one 128-byte run, vector loads), a wave
+    // 64 kPer, the workgroup kPer * blockDim.x per chunk: coverage and segment counts are summed
+    // along the lane's run in registers, so a chunk costs two wave scans (coverage, then segment
+    // begins) plus two cross-wave LDS steps instead of one shuffle scan per slot
     __shared__ int32_t s_wsum[2][kWG / 64];
-    constexpr int kPer = 16;
+    constexpr int kPer = 24;  // one chunk covers 2W <= 24576 (C2: 20000 write endpoints)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int n = 2 * W;
-    auto wave_incl = [&](int x) {
+    auto wave_excl = [&](int x, int& total) {
+        int v = x;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
+            const int y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
         }
-        return x;
+        total = __shfl(v, 63, 64);
+        return v - x;
     };
     int32_t cov = 0, nseg = 0;  // carried over chunks (uniform)
     for (int c0 = 0; c0 < n; c0 += kPer * (int)blockDim.x) {
-        const int wb = c0 + wid * 64 * kPer;
+        const int i0 = c0 + (wid * 64 + lane) * kPer;
         int2 e[kPer];
+        if (i0 + kPer <= n) {
+            const int4* src = (const int4*)(w.wends + i0);
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const int i = wb + 64 * k + lane;
-            e[k] = i < n ? w.wends[i] : make_int2(0, -1);
+            for (int k = 0; k < kPer / 2; k++) {
+                const int4 v = src[k];
+                e[2 * k] = make_int2(v.x, v.y);
+                e[2 * k + 1] = make_int2(v.z, v.w);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; k++) e[k] = i0 + k < n ? w.wends[i0 + k] : make_int2(0, -1);
         }
-        // coverage before each endpoint inside the wave
-        int d[kPer], cb[kPer], run = 0;
+        // +1 at a committed write's begin, -1 at its end; coverage before each endpoint
+        int d[kPer], lsum = 0;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             d[k] = e[k].y >= 0 && committed(e[k].y >> 1) ? ((e[k].y & 1) ? -1 : 1) : 0;
-            const int x = wave_incl(d[k]);
-            cb[k] = run + x - d[k];
-            run += __shfl(x, 63, 64);
+            lsum += d[k];
         }
-        if (lane == 0) s_wsum[0][wid] = run;
+        if (c0 == 0 && threadIdx.x == 0) trace_max(w.trace, kTrCmbLoad);
+        int wtot;
+        const int lex = wave_excl(lsum, wtot);
+        if (lane == 0) s_wsum[0][wid] = wtot;
         __syncthreads();
         int off = cov, tot = 0;
         for (int q = 0; q < nw; q++) {
@@ -1845,20 +1856,22 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
             if (q < wid) off += v;
             tot += v;
         }
+        if (c0 == 0 && threadIdx.x == 0) trace_max(w.trace, kTrCmbScan1);
         // a segment begins where coverage leaves 0 and ends where it returns to 0
         uint32_t bm = 0, em = 0;
-        int bc[kPer], brun = 0;
+        int c = off + lex, nb = 0;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
-            const int c = off + cb[k];
-            const int beg = d[k] == 1 && c == 0;
-            if (beg) bm |= 1u << k;
+            if (d[k] == 1 && c == 0) {
+                bm |= 1u << k;
+                nb++;
+            }
             if (d[k] == -1 && c == 1) em |= 1u << k;
-            const int x = wave_incl(beg);
-            bc[k] = brun + x - beg;
-            brun += __shfl(x, 63, 64);
+            c += d[k];
         }
-        if (lane == 0) s_wsum[1][wid] = brun;
+        int btot;
+        const int bex = wave_excl(nb, btot);
+        if (lane == 0) s_wsum[1][wid] = btot;
         __syncthreads();
         int soff = nseg, stot = 0;
         for (int q = 0; q < nw; q++) {
@@ -1866,10 +1879,18 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
             if (q < wid) soff += v;
             stot += v;
         }
+        // segment j's begin and end: the lane's begins are numbered in order; an end closes the
+        // segment opened last (begins before it in the chunk, plus those before the chunk)
+        if (c0 == 0 && threadIdx.x == 0) trace_max(w.trace, kTrCmbScan2);
+        int j = soff + bex;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
-            if (bm & (1u << k)) w.seg_b[soff + bc[k]] = e[k].x;
-            if (em & (1u << k)) w.seg_e[soff + bc[k] - 1] = e[k].x;
+            if (bm & (1u << k)) w.seg_b[j++] = e[k].x;
+            if (em & (1u << k)) w.seg_e[j - 1] = e[k].x;
+        }
+        if (c0 == 0 && threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            trace_max(w.trace, kTrCmbStore);
         }
         cov += tot;
         nseg += stot;
