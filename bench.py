@@ -239,7 +239,7 @@ def cpu_model():
     return cpu
 
 
-def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
+def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank, n_batches=None):
     """Replay every batch in order on the CPU restatement (oracle/skiplist_baseline.cpp): compare
     each GPU verdict vector and time the batches in `timed` (single thread, pinned to one core)."""
     from oracle import oracle
@@ -261,7 +261,9 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
     phases = {k: 0.0 for k in oracle.SkipListBaseline.PHASES}
     first_bad = None
     t_begin = time.time()
-    for i, b in enumerate(mine):
+    n_batches = len(gbatches) if n_batches is None else n_batches
+    for i in range(n_batches):
+        b = mine(i)  # this resolver's sub-batch (host routing, CommitProxyServer.actor.cpp:118-187)
         _, now, no = gbatches[i]
         t = time.perf_counter()
         # the reference's removeBefore: bounded to 3|combined|+10 nodes, resumed at removalKey
@@ -278,7 +280,8 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
         g = gpu_verdicts[i]
         if g is not None:
             checked += 1
-            bad = int((g != v).sum())
+            # a device-routed batch must hold exactly the host routing's sub-transactions
+            bad = int((g != v).sum()) if len(g) == len(v) else max(len(g), len(v))
             if bad:
                 mismatches += 1
                 txn_mismatch += bad
@@ -292,7 +295,7 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank):
         "reference": "oracle/skiplist_baseline.cpp (reference algorithm, restated; cross-checked vs "
         "oracle/semantic_oracle.cpp in tests/test_oracle.py)",
         "batches_checked": checked,
-        "batches_total": len(mine),
+        "batches_total": n_batches,
         "mismatched_batches": mismatches,
         "mismatched_txns": txn_mismatch,
         "first_mismatch": first_bad,
@@ -357,11 +360,27 @@ def main():
     n_all = at
     timed_lo, timed_hi = spans["timed"]
     gbatches = make_batches(args, p, n_all, world, start_version)
-    all_routed, reshard = route_all(args, p, world, gbatches)
-    routed = [r[rank] for r in all_routed] if all_routed else None
-    if all_routed:
-        shares = np.array([[r[g].batch.n_txn for g in range(world)] for r in all_routed]).sum(0)
-        log(f"[rank {rank}] routed sub-transactions per rank: {shares.tolist()}")
+    # N > 1: the proxy's routing (CommitProxyServer.actor.cpp:118-187) runs on the GPUs inside the
+    # timed region: every rank is the proxy of one share (p.txns transactions) of each global batch,
+    # the shares are all-gathered over xGMI, and every resolver keeps its key range's part on the
+    # device (fdbcs_batch_add_routed).  --reshard keeps the host routing of balancing.py (its
+    # ownership history is not on the device): that path is a feature check, routed before timing.
+    droute = world > 1 and not args.reshard and cdev != "cpu"
+    sh = sharding_for(args, p, world)
+    all_routed, reshard = route_all(args, p, world, gbatches) if (world > 1 and not droute) else (None, None)
+    route_cache = {}
+
+    def routed_at(i):
+        """This rank's ShardBatch of global batch i by the host routing (parity replay, checks)."""
+        if all_routed is not None:
+            return all_routed[i][rank]
+        if i not in route_cache:
+            route_cache[i] = sh.route(gbatches[i][0])[rank]
+        return route_cache[i]
+
+    def mine_at(i):
+        return routed_at(i).batch if world > 1 else gbatches[i][0]
+
     log(f"[rank {rank}] generated history {len(vers)} + {n_all} batches in {time.time() - t0:.1f}s")
 
     cs = C.ConflictSet(device)
@@ -369,23 +388,26 @@ def main():
     cs.set_delta_limit(args.delta_limit)
     if len(vers):
         cs.load_history(kb, ko, vers, 0)
-    mine = [r.batch for r in routed] if routed else [pb for pb, _, _ in gbatches]
-    maxT = max(b.n_txn for b in mine)
-    maxR = max(b.n_reads for b in mine)
-    maxW = max(b.n_writes for b in mine)
 
     def tail_bytes(ko):  # history tail bytes, each tail padded to 8 (engine.cpp padded_tail)
         t = np.diff(ko) - 16
         return int(((t[t > 0] + 7) // 8 * 8).sum())
 
-    tail_total = tail_bytes(ko) + sum(tail_bytes(b.key_offsets) for b in mine) + (1 << 20)
-    cs.reserve(len(vers) + 2 * sum(b.n_writes for b in mine) + 1024, tail_total, maxT, maxR, maxW)
+    # capacity: a resolver's batch is at most the global batch (device routing) or its host-routed part
+    sized = [pb for pb, _, _ in gbatches] if (world == 1 or droute) else [mine_at(i) for i in range(n_all)]
+    maxT = max(b.n_txn for b in sized)
+    maxR = max(b.n_reads for b in sized)
+    maxW = max(b.n_writes for b in sized)
+    maxTail = max(int(np.maximum(np.diff(b.key_offsets) - 16, 0).sum()) for b in sized)
+    tail_total = tail_bytes(ko) + sum(tail_bytes(b.key_offsets) for b in sized) // (world if droute else 1) + (1 << 20)
+    cs.reserve(len(vers) + 2 * sum(b.n_writes for b in sized) + 1024, tail_total, maxT, maxR, maxW)
+    del sized
     verdicts = [None] * n_all
 
     # Multi-GPU combine (CommitProxyServer.actor.cpp:764-780): each batch's stage B also writes its
     # conflict bytes 2 - verdict at the routed transactions' global indices (0 elsewhere) into a
-    # T-byte device buffer (fdbcs_batch_set_conflict_output), complete when the batch is; one MAX
-    # all-reduce over the ranks (RCCL; gloo's CUDA all-reduce in one-GPU rehearsals) combines them.
+    # T-byte device buffer, complete when the batch is; one MAX all-reduce over the ranks (RCCL;
+    # gloo's CUDA all-reduce in one-GPU rehearsals) combines them.
     on_device = dist is not None and cdev != "cpu"
     outbuf = {}
     if on_device:
@@ -393,24 +415,60 @@ def main():
             outbuf[i] = torch.empty(gbatches[i][0].n_txn, dtype=torch.uint8, device=cdev)
     combined = {}
 
+    # device routing: this rank's share of every batch in the wire layout (pinned host memory,
+    # packed per pass like addTransaction), a ring of device share / all-gather buffers
+    RING = WINDOW + 3
+    stride = 0
+    if droute:
+        lo_key = sh.splits[rank - 1] if rank > 0 else None
+        hi_key = sh.splits[rank] if rank < world - 1 else None
+        share_bytes = max(len(C.share_pack(gbatches[i][0].slice_txns(rank * p.txns, (rank + 1) * p.txns)))
+                          for i in range(0, n_all, max(1, n_all // 16)))
+        tb = torch.tensor([share_bytes], dtype=torch.int64, device=cdev)
+        dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+        stride = (int(tb.item()) * 5 // 4 + 4095) // 4096 * 4096  # headroom over the sampled batches
+        share_dev = [torch.empty(stride, dtype=torch.uint8, device=cdev) for _ in range(RING)]
+        gathered = [torch.empty(world * stride, dtype=torch.uint8, device=cdev) for _ in range(RING)]
+        caps = (maxT, maxR, maxW, maxTail)
+
+        def pack_share(i):
+            pin = torch.empty(stride, dtype=torch.uint8, pin_memory=True)
+            C.share_pack(gbatches[i][0].slice_txns(rank * p.txns, (rank + 1) * p.txns), pin.numpy())
+            return pin
+
+        def route_batch(i, pin):
+            """H2D of this rank's share, the all-gather, and the device split into a new batch."""
+            k = i % RING
+            share_dev[k].copy_(pin, non_blocking=True)
+            if args.backend == "nccl":
+                dist.all_gather_into_tensor(gathered[k], share_dev[k])
+            else:  # gloo (one-GPU rehearsals): list form
+                dist.all_gather(list(gathered[k].view(world, stride).unbind(0)), share_dev[k])
+            o = C.ConflictBatch(cs)
+            o.add_routed(gathered[k].data_ptr(), stride, world, p.txns, lo_key, hi_key, caps, outbuf[i].data_ptr(),
+                         gbatches[i][0].n_txn, torch.cuda.current_stream().cuda_stream)
+            return o
+
     def attach(i, o):
         if on_device:
-            o.set_conflict_output(routed[i].txn_ids, gbatches[i][0].n_txn, outbuf[i].data_ptr())
+            r = routed_at(i)
+            o.set_conflict_output(r.txn_ids, gbatches[i][0].n_txn, outbuf[i].data_ptr())
 
     def combine(i, v):
         if on_device:
             c = outbuf[i]
         else:
-            c = torch.from_numpy(KeyRangeSharding.conflict_bytes(gbatches[i][0].n_txn, routed[i], v)).to(cdev)
+            c = torch.from_numpy(KeyRangeSharding.conflict_bytes(gbatches[i][0].n_txn, routed_at(i), v)).to(cdev)
         dist.all_reduce(c, op=dist.ReduceOp.MAX)
         combined[i] = c
 
     host = {"add": 0.0, "submit": 0.0, "wait": 0.0}
 
     def run(lo, hi, objs, window=WINDOW, lat=None):
-        """Submit batches lo..hi-1 (objs: packed ConflictBatch objects, or None: pack inside the
-        loop), keeping at most `window` in flight; upload (H2D), kernels and verdicts each time.
-        lat: per-batch submit-to-verdicts seconds are appended (window 1: the synchronous call)."""
+        """Submit batches lo..hi-1 (objs: packed ConflictBatch objects — or, with device routing,
+        packed shares — or None: pack inside the loop), keeping at most `window` in flight;
+        upload (H2D), routing, kernels and verdicts each time.  lat: per-batch submit-to-verdicts
+        seconds are appended (window 1: the synchronous call)."""
         inflight = []
         pc = time.perf_counter
 
@@ -424,12 +482,36 @@ def main():
                 combine(j, verdicts[j])
             oj.close()
 
+        pending = None  # device routing: a batch routed, its detect issued after the next one's routing
+
+        def detect(j, oj, t_sub):
+            _, now_j, no_j = gbatches[j]
+            t1 = pc()
+            oj.detect_async(now_j, no_j)
+            host["submit"] += pc() - t1
+            inflight.append((j, oj, t_sub))
+            while len(inflight) >= window:
+                retire(*inflight.pop(0))
+
         for i in range(lo, hi):
             _, now, no = gbatches[i]
             t = pc()
+            if droute:
+                pin = objs[i] if objs is not None else pack_share(i)
+                t1 = pc()
+                o = route_batch(i, pin)
+                host["add"] += t1 - t
+                host["submit"] += pc() - t1
+                if pending is not None:
+                    detect(*pending)
+                pending = (i, o, t1)
+                if window == 1:  # the synchronous call: this batch's detect and wait now
+                    detect(*pending)
+                    pending = None
+                continue
             if objs is None:
                 o = C.ConflictBatch(cs)
-                o.add_packed(mine[i])
+                o.add_packed(mine_at(i))
                 attach(i, o)
             else:
                 o = objs[i]
@@ -440,14 +522,20 @@ def main():
             inflight.append((i, o, t1))
             if len(inflight) >= window:
                 retire(*inflight.pop(0))
+        if pending is not None:
+            detect(*pending)
         for j, oj, ts in inflight:
             retire(j, oj, ts)
+        inflight.clear()
 
     def packed(lo, hi):
         objs = {}
         for i in range(lo, hi):
+            if droute:  # the proxy's addTransaction: its share in the wire layout
+                objs[i] = pack_share(i)
+                continue
             o = C.ConflictBatch(cs)
-            o.add_packed(mine[i])  # addTransaction: normalized into pinned staging, not uploaded
+            o.add_packed(mine_at(i))  # addTransaction: normalized into pinned staging, not uploaded
             attach(i, o)
             objs[i] = o
         return objs
@@ -505,7 +593,7 @@ def main():
     cs.set_timing(0)
 
     resident_elapsed = None
-    if args.resident_steps > 0:  # diagnostic: batches uploaded before the timed region
+    if args.resident_steps > 0 and not droute:  # diagnostic: batches uploaded before the timed region
         objs = packed(*spans["resident"])
         for o in objs.values():
             o.upload()
@@ -591,8 +679,9 @@ def main():
     # the dominant kernel's line from the timed region's own events (fdbcs_set_timed_kernel).
     # Algorithmic bytes per launch: roofline.py (SURVEY §8(d) model per kernel, batch shapes of
     # this run).
-    shape = roofline.shape_of(mine[timed_lo:timed_hi], st_prof if args.profile_steps > 0 else st, len(vers),
-                              dir_share=directory_share(kb, ko, mine[timed_lo:timed_hi]))
+    sample = [mine_at(i) for i in range(timed_lo, min(timed_hi, timed_lo + 8))]
+    shape = roofline.shape_of(sample, st_prof if args.profile_steps > 0 else st, len(vers),
+                              dir_share=directory_share(kb, ko, sample))
     table = roofline.kernel_table(kprof, shape, st_prof if args.profile_steps > 0 else None)
     roof = None
     if dominant and dominant in kprof_timed:
@@ -617,17 +706,18 @@ def main():
     if dist is not None:
         # the device-side combine against host-built conflict bytes of the same verdicts
         bad = 0
-        for i in sorted(combined):
-            h = torch.from_numpy(KeyRangeSharding.conflict_bytes(gbatches[i][0].n_txn, routed[i], verdicts[i])).to(cdev)
+        # (the same batches on every rank: the first 24 of the timed region and after)
+        for i in sorted(k for k in combined if k >= timed_lo)[:24]:
+            h = torch.from_numpy(KeyRangeSharding.conflict_bytes(gbatches[i][0].n_txn, routed_at(i), verdicts[i])).to(cdev)
             dist.all_reduce(h, op=dist.ReduceOp.MAX)
             bad += int(not torch.equal(h, combined[i]))
-        combine_check = {"batches": len(combined), "mismatched": bad,
+        combine_check = {"batches": len(sorted(k for k in combined if k >= timed_lo)[:24]), "mismatched": bad,
                          "path": (f"device conflict bytes + {'RCCL' if args.backend == 'nccl' else 'gloo'} MAX all-reduce"
                                   if on_device else "host bytes + all-reduce")}
     parity = cpu_base = None
     if not args.no_cpu_baseline:
         timed = set(range(timed_lo, timed_hi))
-        parity, cpu_base = cpu_replay(args, kb, ko, vers, mine, gbatches, verdicts, timed, rank)
+        parity, cpu_base = cpu_replay(args, kb, ko, vers, mine_at, gbatches, verdicts, timed, rank)
         if dist is not None:
             t = torch.tensor([parity["batches_checked"], parity["mismatched_batches"], parity["mismatched_txns"]],
                              dtype=torch.int64, device=cdev)
@@ -662,7 +752,12 @@ def main():
         except Exception:
             pass
         dist_info = {"world_size": world, "backend": args.backend, "rccl_version": rccl,
-                     "routing": "host KeyRangeSharding.route before the timed region"}
+                     "routing": ("device: each rank packs its share of the global batch (proxy), H2D, all-gather of "
+                                 "the shares, fdbcs_batch_add_routed (k_scan<RouteScan> + k_route_move) per resolver, "
+                                 "inside the timed region" if droute else
+                                 "host (balancing.BalancedRouting) before the timed region: a feature check, not a "
+                                 "throughput figure"),
+                     "share_stride_bytes": stride or None}
     out = {
         "metric": "resolved txns/sec (conflict ranges checked/sec) per batch; HBM GB/s vs peak",
         "value": gtxn / elapsed,

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -130,6 +130,12 @@ SIGNATURES = {
     "fdbcs_batch_conflicting_reads": (ctypes.c_int, [_VP, _I32, _VP, _I32, ctypes.POINTER(_I32)]),
     "fdbcs_batch_device_verdicts": (ctypes.c_int, [_VP, ctypes.POINTER(_VP)]),
     "fdbcs_batch_set_conflict_output": (ctypes.c_int, [_VP, _VP, ctypes.c_int32, _VP]),
+    "fdbcs_share_bytes": (ctypes.c_int, [ctypes.POINTER(_CPackedBatch), ctypes.POINTER(_I64)]),
+    "fdbcs_share_pack": (ctypes.c_int, [ctypes.POINTER(_CPackedBatch), _VP, _I64, ctypes.POINTER(_I64)]),
+    "fdbcs_batch_add_routed": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _VP, _I32, _VP, _I32, _I32, _I32, _I32, _I64,
+                                              _VP, _I64, ctypes.c_uint64]),
+    "fdbcs_batch_routed_info": (ctypes.c_int, [_VP, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32),
+                                               ctypes.POINTER(_VP), ctypes.POINTER(_VP)]),
     "fdbcs_debug_kernel_time": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     "fdbcs_kernel_profile": (ctypes.c_int, [_VP, _I32, ctypes.c_char_p, _I32, ctypes.POINTER(_I64),
                                             ctypes.POINTER(ctypes.c_double)]),
@@ -154,6 +160,22 @@ def load_library(path: str = LIB_PATH):
             f.argtypes = args
         _lib = lib
     return _lib
+
+
+def share_pack(pb: PackedBatch, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """fdbcs_share_pack: a proxy share (a packed batch) in the engine's wire layout, as uint8 (into
+    `out` when given: e.g. a pinned torch buffer's numpy view; the used prefix is returned)."""
+    L = load_library()
+    cs = pb.c_struct()
+    n = _I64()
+    _check(L.fdbcs_share_bytes(ctypes.byref(cs), ctypes.byref(n)), "shareBytes")
+    if out is None:
+        out = np.zeros(n.value, np.uint8)
+    if out.nbytes < n.value:
+        raise ValueError(f"share needs {n.value} bytes, buffer has {out.nbytes}")
+    used = _I64()
+    _check(L.fdbcs_share_pack(ctypes.byref(cs), _VP(out.ctypes.data), out.nbytes, ctypes.byref(used)), "sharePack")
+    return out[: used.value]
 
 
 def strerror(status: int) -> str:
@@ -362,10 +384,38 @@ class ConflictBatch:
     def upload(self) -> None:
         _check(load_library().fdbcs_batch_upload(self._h), "upload")
 
+    def add_routed(self, shares_ptr: int, stride: int, n_shares: int, max_share_txns: int, lo: Optional[bytes],
+                   hi: Optional[bytes], caps: Tuple[int, int, int, int], conflict_out: int = 0, n_global: int = 0,
+                   stream: int = 0) -> None:
+        """fdbcs_batch_add_routed: this resolver's part ([lo, hi); None = unbounded) of the shares
+        gathered at device address `shares_ptr` (`stride` bytes apart), routed on the device once
+        `stream` (a hipStream_t handle, e.g. torch.cuda.current_stream().cuda_stream) gets there.
+        caps = (txns, reads, writes, tail bytes) bounds of the routed batch."""
+        lo_b = bytes(lo) if lo is not None else b""
+        hi_b = bytes(hi) if hi is not None else b""
+        lo_buf = ctypes.create_string_buffer(lo_b, max(1, len(lo_b)))
+        hi_buf = ctypes.create_string_buffer(hi_b, max(1, len(hi_b)))
+        _check(load_library().fdbcs_batch_add_routed(
+            self._h, _VP(shares_ptr), int(stride), int(n_shares), int(max_share_txns), ctypes.cast(lo_buf, _VP),
+            len(lo_b) if lo is not None else -1, ctypes.cast(hi_buf, _VP), len(hi_b) if hi is not None else -1,
+            int(caps[0]), int(caps[1]), int(caps[2]), int(caps[3]), _VP(conflict_out or None), int(n_global),
+            int(stream)), "addRouted")
+        self._routed = True
+
+    def routed_info(self) -> Tuple[int, int, int, int, int]:
+        """(transactions, reads, writes, device address of the global -> batch map, of the read ids)."""
+        T, R, W = _I32(), _I32(), _I32()
+        inv, rid = _VP(), _VP()
+        _check(load_library().fdbcs_batch_routed_info(self._h, ctypes.byref(T), ctypes.byref(R), ctypes.byref(W),
+                                                      ctypes.byref(inv), ctypes.byref(rid)), "routedInfo")
+        return T.value, R.value, W.value, inv.value or 0, rid.value or 0
+
     def detect_async(self, now: int, new_oldest_version: int) -> None:
         _check(load_library().fdbcs_batch_detect_async(self._h, now, new_oldest_version), "detectConflicts")
 
     def wait(self) -> np.ndarray:
+        if getattr(self, "_routed", False):
+            self.transaction_count = self.routed_info()[0]
         v = np.zeros(self.transaction_count, np.uint8)
         _check(load_library().fdbcs_batch_wait(self._h, _p(v), None, None), "wait")
         self.verdicts = v

@@ -171,6 +171,8 @@ struct fdbcs_conflict_set {
     int64_t tail_ub = 0;
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
+    DBuf route_btail;                  // device routing: tails of this resolver's key-range bounds
+    std::vector<uint8_t> route_bounds; // the bounds route_btail holds (lo | hi bytes), to skip re-uploads
     // batch workspaces (rotating)
     DBuf ws[kNumWork][56];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
     int64_t ws_T = -1, ws_R = -1, ws_W = -1;
@@ -260,6 +262,10 @@ struct BatchSlot {
     hipEvent_t ev_free = nullptr;  // the last batch using this slot finished on the device
     bool free_recorded = false;
     HBuf pin_inv;  // fdbcs_batch_set_conflict_output: global -> batch transaction map (host-mapped)
+    // device routing (fdbcs_batch_add_routed): scan state, global -> batch map, read ids, totals
+    DBuf rt_scan, rt_inv, rt_rids, rt_dres;
+    HBuf rt_res;
+    hipEvent_t ev_route_in = nullptr;  // the caller's stream reached the all-gathered shares
     // per-kernel events of the batch (timing level 3, or the timed kernel at level 1)
     std::vector<hipEvent_t> prof_pool;
     size_t prof_next = 0;
@@ -308,10 +314,15 @@ struct fdbcs_batch {
     std::vector<int32_t> conf_off, conf_idx;
     int32_t n_committed = 0, n_too_old = 0;
 
-    int32_t T() const { return (int32_t)snap.size(); }
-    int32_t R() const { return roff.back(); }
-    int32_t W() const { return woff.back(); }
-    size_t tail_size() const { return direct ? d_tail_bytes : tail.size(); }
+    // device-routed batch (fdbcs_batch_add_routed): sizes known once the route kernels finished
+    bool routed = false, route_pending = false;
+    int32_t rT = 0, rR = 0, rW = 0;
+    size_t r_tail = 0;
+
+    int32_t T() const { return routed ? rT : (int32_t)snap.size(); }
+    int32_t R() const { return routed ? rR : roff.back(); }
+    int32_t W() const { return routed ? rW : woff.back(); }
+    size_t tail_size() const { return routed ? r_tail : direct ? d_tail_bytes : tail.size(); }
 };
 
 namespace {
@@ -652,6 +663,12 @@ void release_slot(BatchSlot* sl) {
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
     if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
+    if (sl->ev_route_in) (void)hipEventDestroy(sl->ev_route_in);
+    sl->rt_scan.release();
+    sl->rt_inv.release();
+    sl->rt_rids.release();
+    sl->rt_dres.release();
+    sl->rt_res.release();
     for (hipEvent_t e : sl->prof_pool) (void)hipEventDestroy(e);
     sl->dev.release();
     sl->dverdict.release();
@@ -1527,6 +1544,259 @@ int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     return FDBCS_OK;
 }
 
+// ---- multi-resolver routing: proxy shares (engine.h ShareHeader) and the device split
+
+static size_t share_layout(int32_t T, int64_t R, int64_t W, int64_t tail, ShareHeader* h) {
+    size_t off = sizeof(ShareHeader);
+    h->T = T;
+    h->R = (int32_t)R;
+    h->W = (int32_t)W;
+    h->off_keys = (int64_t)off;
+    off = align_up(off + sizeof(DKey) * 2 * (size_t)(R + W), 64);
+    h->off_snap = (int64_t)off;
+    off = align_up(off + 8 * (size_t)T, 64);
+    h->off_roff = (int64_t)off;
+    off = align_up(off + 4 * ((size_t)T + 1), 64);
+    h->off_woff = (int64_t)off;
+    off = align_up(off + 4 * ((size_t)T + 1), 64);
+    h->off_report = (int64_t)off;
+    off = align_up(off + (size_t)T, 64);
+    h->off_tail = (int64_t)off;
+    h->tail_bytes = tail;
+    off = align_up(off + (size_t)tail + 64, 64);  // slack for dkey.h tail_word
+    h->bytes = (int64_t)off;
+    return off;
+}
+
+static int64_t packed_tail_bytes(const fdbcs_packed_batch* pb) {
+    const int32_t T = pb->n_txn;
+    const int64_t nk = T > 0 ? 2 * ((int64_t)pb->read_offsets[T] + pb->write_offsets[T]) : 0;
+    int64_t tail = 0;
+    for (int64_t k = 0; k < nk; k++) {
+        const int64_t len = pb->key_offsets[k + 1] - pb->key_offsets[k];
+        if (len > 16) tail += len - 16;
+    }
+    return tail;
+}
+
+int fdbcs_share_bytes(const fdbcs_packed_batch* pb, int64_t* out) {
+    if (!pb || !out || pb->n_txn < 0) return FDBCS_E_INVALID;
+    if (pb->n_txn > 0 && (!pb->read_offsets || !pb->write_offsets || !pb->key_offsets)) return FDBCS_E_INVALID;
+    const int32_t T = pb->n_txn;
+    ShareHeader h{};
+    *out = (int64_t)share_layout(T, T ? pb->read_offsets[T] : 0, T ? pb->write_offsets[T] : 0, packed_tail_bytes(pb), &h);
+    return FDBCS_OK;
+}
+
+int fdbcs_share_pack(const fdbcs_packed_batch* pb, void* out, int64_t cap, int64_t* used) {
+    if (!pb || !out || pb->n_txn < 0) return FDBCS_E_INVALID;
+    const int32_t T = pb->n_txn;
+    if (T > 0 && (!pb->read_snapshot || !pb->read_offsets || !pb->write_offsets || !pb->key_offsets))
+        return FDBCS_E_INVALID;
+    const int64_t R = T ? pb->read_offsets[T] : 0, W = T ? pb->write_offsets[T] : 0;
+    const int64_t nk = 2 * (R + W);
+    if (nk && !pb->key_bytes) return FDBCS_E_INVALID;
+    for (int32_t t = 0; t < T; t++)
+        if (pb->read_offsets[t + 1] < pb->read_offsets[t] || pb->write_offsets[t + 1] < pb->write_offsets[t])
+            return FDBCS_E_INVALID;
+    for (int64_t k = 0; k < nk; k += 2) {  // KeyRangeRef: begin <= end (FDBTypes.h:288-291)
+        const int64_t a0 = pb->key_offsets[k], a1 = pb->key_offsets[k + 1], a2 = pb->key_offsets[k + 2];
+        if (a1 < a0 || a2 < a1) return FDBCS_E_INVALID;
+        if (cmp_bytes(pb->key_bytes + a0, (int32_t)(a1 - a0), pb->key_bytes + a1, (int32_t)(a2 - a1)) > 0)
+            return FDBCS_E_INVALID;
+    }
+    ShareHeader h{};
+    const size_t bytes = share_layout(T, R, W, packed_tail_bytes(pb), &h);
+    if ((int64_t)bytes > cap) return FDBCS_E_NOMEM;
+    char* o = (char*)out;
+    memcpy(o, &h, sizeof(h));
+    DKey* keys = (DKey*)(o + h.off_keys);
+    uint8_t* tail = (uint8_t*)(o + h.off_tail);
+    uint32_t tb = 0;
+    for (int64_t k = 0; k < nk; k++) {
+        const uint8_t* p = pb->key_bytes + pb->key_offsets[k];
+        const uint32_t len = (uint32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]);
+        DKey d;
+        fast_prefix(p, len, &d.hi, &d.lo);
+        d.len = len;
+        d.tail = 0;
+        if (len > 16) {
+            d.tail = tb;
+            memcpy(tail + tb, p + 16, len - 16);
+            tb += len - 16;
+        }
+        keys[k] = d;
+    }
+    memset(tail + tb, 0, 64);
+    if (T) {
+        memcpy(o + h.off_snap, pb->read_snapshot, 8 * (size_t)T);
+        memcpy(o + h.off_roff, pb->read_offsets, 4 * ((size_t)T + 1));
+        memcpy(o + h.off_woff, pb->write_offsets, 4 * ((size_t)T + 1));
+        if (pb->report_conflicting_keys)
+            memcpy(o + h.off_report, pb->report_conflicting_keys, (size_t)T);
+        else
+            memset(o + h.off_report, 0, (size_t)T);
+    }
+    if (used) *used = (int64_t)bytes;
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, int32_t n_shares, int32_t max_share_txns,
+                           const uint8_t* lo_key, int32_t lo_len, const uint8_t* hi_key, int32_t hi_len, int32_t cap_txns,
+                           int32_t cap_reads, int32_t cap_writes, int64_t cap_tail, uint8_t* conflict_out,
+                           int64_t n_global, uint64_t after_stream) {
+    if (!b || !shares || stride <= (int64_t)sizeof(ShareHeader) || n_shares <= 0 || max_share_txns < 0 || cap_txns < 0 ||
+        cap_reads < 0 || cap_writes < 0 || cap_tail < 0 || (lo_len > 0 && !lo_key) || (hi_len > 0 && !hi_key) ||
+        n_global < 0 || (conflict_out && n_global > (int64_t)n_shares * max_share_txns))
+        return FDBCS_E_INVALID;
+    if (!b->cs || b->state != 0 || b->T() != 0 || b->direct) return FDBCS_E_STATE;
+    if ((int64_t)cap_txns > kMaxTxnLds) return FDBCS_E_INVALID;
+    if (lo_len >= 0 && hi_len >= 0 && cmp_bytes(lo_key, lo_len, hi_key, hi_len) >= 0) return FDBCS_E_INVALID;
+    fdbcs_conflict_set* cs = b->cs;
+    HIPOK(hipSetDevice(cs->device));
+    BatchSlot* sl = b->slot;
+    int rc;
+    // bounds of this resolver's key range: prefixes by value, tails in a small device arena
+    std::vector<uint8_t> want;
+    auto put_len = [&](int32_t n) {
+        for (int i = 0; i < 4; i++) want.push_back((uint8_t)((uint32_t)n >> (8 * i)));
+    };
+    put_len(lo_len);
+    if (lo_len > 0) want.insert(want.end(), lo_key, lo_key + lo_len);
+    put_len(hi_len);
+    if (hi_len > 0) want.insert(want.end(), hi_key, hi_key + hi_len);
+    RouteArgs a{};
+    std::vector<uint8_t> btail;
+    auto bound = [&](const uint8_t* k, int32_t len, DKey* d) {
+        fast_prefix(k, (uint32_t)len, &d->hi, &d->lo);
+        d->len = (uint32_t)len;
+        d->tail = 0;
+        if (len > 16) {
+            d->tail = (uint32_t)btail.size();
+            btail.insert(btail.end(), k + 16, k + len);
+            while (btail.size() % 8) btail.push_back(0);
+        }
+    };
+    a.has_lo = lo_len >= 0;
+    a.has_hi = hi_len >= 0;
+    if (a.has_lo) bound(lo_key, lo_len, &a.lo);
+    if (a.has_hi) bound(hi_key, hi_len, &a.hi);
+    btail.resize(btail.size() + 64, 0);
+    if (want != cs->route_bounds) {
+        if ((rc = sync_all(cs))) return rc;
+        if ((rc = cs->route_btail.ensure(btail.size()))) return rc;
+        HIPOK(hipMemcpy(cs->route_btail.p, btail.data(), btail.size(), hipMemcpyHostToDevice));
+        cs->route_bounds = want;
+    }
+    a.btail = (const uint8_t*)cs->route_btail.p;
+    // the routed batch's layout at capacity offsets (upload layout)
+    const UploadLayout L = upload_layout((size_t)cap_txns, (size_t)cap_reads, (size_t)cap_writes, (size_t)cap_tail);
+    if ((rc = ensure_slot(sl, L.total + sizeof(DKey) * 2 * ((size_t)cap_writes + 1), (size_t)cap_txns, (size_t)cap_reads)))
+        return rc;
+    const int64_t n_elems = (int64_t)n_shares * max_share_txns;
+    if ((rc = sl->rt_scan.ensure(8 * (size_t)route_scan_words(n_elems)))) return rc;
+    if ((rc = sl->rt_inv.ensure(4 * (size_t)std::max<int64_t>(n_elems, 1)))) return rc;
+    if ((rc = sl->rt_rids.ensure(4 * ((size_t)cap_reads + 1)))) return rc;
+    if ((rc = sl->rt_dres.ensure(sizeof(RouteResult)))) return rc;
+    if ((rc = sl->rt_res.ensure(sizeof(RouteResult), true))) return rc;
+    if ((rc = make_slot_events(sl))) return rc;
+    if (!sl->ev_route_in) HIPOK(hipEventCreateWithFlags(&sl->ev_route_in, hipEventDisableTiming));
+    char* d = (char*)sl->dev.p;
+    a.shares = (const uint8_t*)shares;
+    a.stride = stride;
+    a.n_shares = n_shares;
+    a.tcap = std::max(1, max_share_txns);
+    a.oldest = cs->oldest;  // addTransaction's TooOld test (SkipList.cpp:770) at add time
+    a.report_enabled = 0;  // conflicting-key reports go through the host-routed path (sharding.py)
+    a.cap_T = cap_txns;
+    a.cap_R = cap_reads;
+    a.cap_W = cap_writes;
+    a.cap_tail = cap_tail;
+    a.keys = (DKey*)(d + L.keys);
+    a.wstage = (DKey*)(d + L.total);
+    a.rown = (int32_t*)(d + L.rown);
+    a.wown = (int32_t*)(d + L.wown);
+    a.snap = (int64_t*)(d + L.snap);
+    a.roff = (int32_t*)(d + L.roff);
+    a.woff = (int32_t*)(d + L.woff);
+    a.flags = (uint8_t*)(d + L.flags);
+    a.tail = (uint8_t*)(d + L.tail);
+    a.inv = (int32_t*)sl->rt_inv.p;
+    a.read_ids = (int32_t*)sl->rt_rids.p;
+    a.out_zero = conflict_out;
+    a.out_n = n_global;
+    a.res = (RouteResult*)sl->rt_res.dp;
+    a.dres = (RouteResult*)sl->rt_dres.p;
+    ((RouteResult*)sl->rt_res.p)->error = -1;  // not written yet
+    hipStream_t us = cs->ustream;
+    // the shares are complete on the caller's stream (the all-gather); the slot's previous batch
+    // may still read its device buffer
+    HIPOK(hipEventRecord(sl->ev_route_in, (hipStream_t)(uintptr_t)after_stream));
+    HIPOK(hipStreamWaitEvent(us, sl->ev_route_in, 0));
+    if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
+    HIPOK(hipMemsetAsync(sl->rt_scan.p, 0, 8 * (size_t)route_scan_words(n_elems), us));
+    uint64_t* sw = (uint64_t*)sl->rt_scan.p;
+    ScanState st{sw + 8, (int*)sw, (int*)(sw + 1)};
+    t_record = nullptr;
+    launch_route(us, a, st);
+    HIPOK(take_launch_error());
+    HIPOK(hipEventRecord(sl->ev_up, us));
+    b->bd.keys = a.keys;
+    b->bd.rowner = a.rown;
+    b->bd.wowner = a.wown;
+    b->bd.snap = a.snap;
+    b->bd.roff = a.roff;
+    b->bd.woff = a.woff;
+    b->bd.flags = a.flags;
+    b->bd.tail = a.tail;
+    b->routed = true;
+    b->route_pending = true;
+    b->rT = b->rR = b->rW = 0;
+    b->out_dev = conflict_out;
+    b->out_n = (int32_t)n_global;
+    b->out_ids.clear();
+    b->state = 1;
+    return FDBCS_OK;
+}
+
+// Sizes of a routed batch, once its route kernels are done (blocks until then).
+static int finish_route(fdbcs_batch* b) {
+    if (!b->route_pending) return FDBCS_OK;
+    BatchSlot* sl = b->slot;
+    HIPOK(hipEventSynchronize(sl->ev_up));
+    std::atomic_thread_fence(std::memory_order_acquire);
+    RouteResult r;
+    memcpy(&r, (const void*)sl->rt_res.p, sizeof(r));
+    if (r.error != 0) return r.error < 0 ? FDBCS_E_DEVICE : FDBCS_E_NOMEM;
+    b->rT = r.T;
+    b->rR = r.R;
+    b->rW = r.W;
+    b->r_tail = (size_t)r.tail_bytes;
+    b->tail_bytes = b->r_tail;
+    b->bd.T = r.T;
+    b->bd.R = r.R;
+    b->bd.W = r.W;
+    // history tail bytes the batch's write endpoints can add, each tail padded to 8 (a bound: the
+    // kept tails plus 7 bytes of padding per write endpoint)
+    b->wtail = r.tail_bytes + 14 * (int64_t)r.W;
+    b->max_len = r.n_gt24 ? 25 : (r.n_gt19 ? 20 : 16);
+    b->any_report = r.reports > 0;
+    b->route_pending = false;
+    return FDBCS_OK;
+}
+
+int fdbcs_batch_routed_info(fdbcs_batch* b, int32_t* T, int32_t* R, int32_t* W, void** inv_dev, void** read_ids_dev) {
+    if (!b) return FDBCS_E_INVALID;
+    if (!b->routed) return FDBCS_E_STATE;
+    if (int rc = finish_route(b)) return rc;
+    if (T) *T = b->rT;
+    if (R) *R = b->rR;
+    if (W) *W = b->rW;
+    if (inv_dev) *inv_dev = b->slot->rt_inv.p;
+    if (read_ids_dev) *read_ids_dev = b->slot->rt_rids.p;
+    return FDBCS_OK;
+}
+
 int fdbcs_batch_upload(fdbcs_batch* b) {
     if (!b) return FDBCS_E_INVALID;
     if (!b->cs) return FDBCS_E_STATE;
@@ -1547,6 +1817,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const auto t_begin = std::chrono::steady_clock::now();
     HIPOK(hipSetDevice(cs->device));
     if (now < cs->max_written) return FDBCS_E_VERSION;
+    if (int rc0 = finish_route(b)) return rc0;  // a routed batch's sizes (its route ran ahead)
     if (b->T() > kMaxTxnLds) return FDBCS_E_INVALID;
     // tail offsets are 32-bit: refuse a batch that could overflow the arena (GC repacks it long before)
     // history tail bytes this batch can append (each inserted tail padded to 8 bytes)
@@ -1583,7 +1854,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     b->h_hist = (uint8_t*)(ho + o_hc);
     b->h_first = (int32_t*)(ho + o_fc);
     if ((rc = sl->dverdict.ensure(T + 64))) return rc;
-    if (b->out_dev && b->out_n > 0) {
+    if (b->out_dev && b->out_n > 0 && !b->routed) {
         // global -> batch transaction map, read by k_conflict_output straight from host-mapped
         // memory (n_global * 4 bytes; the slot's previous batch finished with it: its flag was seen)
         if ((int64_t)b->out_ids.size() != T) return FDBCS_E_STATE;  // transactions added after the call
@@ -1592,8 +1863,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         std::fill(inv, inv + b->out_n, -1);
         for (int32_t t = 0; t < (int32_t)T; t++) inv[b->out_ids[t]] = t;
     }
-    b->any_report = false;
-    for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
+    if (!b->routed) {  // (a routed batch's count came with its sizes)
+        b->any_report = false;
+        for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
+    }
     b->seq = ++cs->seq;
     if (b->seq == 0) b->seq = ++cs->seq;  // 0 means "not done"
     *b->h_flag = 0;
@@ -1746,7 +2019,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp, sc);
     if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
-        launch_conflict_output(s, bd, w, (const int32_t*)sl->pin_inv.dp, b->out_n, b->out_dev);
+        launch_conflict_output(s, bd, w, b->routed ? (const int32_t*)sl->rt_inv.p : (const int32_t*)sl->pin_inv.dp,
+                               b->out_n, b->out_dev);
     if (b->any_report) {  // before the epilogue re-zeroes hist_conf (into the host-mapped results)
         char* hdv = (char*)sl->pin_out.dp;
         if (R) launch_copy_bytes(s, hdv + o_rc, w.rconf, R);

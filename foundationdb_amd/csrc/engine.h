@@ -241,6 +241,60 @@ __device__ __forceinline__ void trace_max(unsigned long long* tr, int slot) {
 // Byte offset of the Scalars copy that follows the verdicts in a batch's result buffer.
 __host__ __device__ inline int64_t verdict_scalars_offset(int64_t T) { return (T + 64) / 64 * 64; }
 
+// ---- multi-resolver routing on the device (the commit proxy's step, CommitProxyServer.actor.cpp:
+// 118-187, for a static key-range split).  Every rank is the proxy of one share of the global
+// batch: it packs its share in the wire layout below (fdbcs_share_pack), the shares are
+// all-gathered over xGMI (RCCL), and each resolver keeps the ranges that meet its key range
+// (k_scan<RouteScan> + k_route_move) as a batch in the upload layout.
+// Wire layout of a share: ShareHeader, then DKey keys[2(R+W)] (tail = byte offset in the share's
+// tail region), int64 snap[T], int32 roff[T+1], int32 woff[T+1], uint8 report[T], tail bytes; every
+// region 64-byte aligned, the whole share <= the all-gather stride.
+struct ShareHeader {
+    int32_t T, R, W, pad0;
+    int64_t bytes;       // the share, header included
+    int64_t off_keys, off_snap, off_roff, off_woff, off_report, off_tail;
+    int64_t tail_bytes;
+    int64_t pad[6];
+};
+static_assert(sizeof(ShareHeader) == 128, "ShareHeader is 128 bytes");
+// Totals of a routed batch (host-mapped copy for the host, device copy for k_route_move).
+struct RouteResult {
+    int32_t T, R, W, reports;
+    int32_t n_gt19, n_gt24;  // kept keys longer than 19 / 24 bytes (sort tail windows, long-key probes)
+    int64_t tail_bytes;
+    int32_t error;           // 1: a capacity bound was exceeded (nothing past it was written)
+    int32_t pad;
+};
+struct RouteArgs {
+    const uint8_t* shares;  // n_shares shares, `stride` bytes apart
+    int64_t stride;
+    int32_t n_shares, tcap;  // tcap: bound on any share's T (global element i = share i / tcap)
+    int32_t has_lo, has_hi;  // this resolver owns [lo, hi): lo absent for the first, hi for the last
+    DKey lo, hi;
+    const uint8_t* btail;    // tails of lo / hi
+    int64_t oldest;          // TooOld test (SkipList.cpp:770) at add time
+    int32_t report_enabled;
+    int32_t cap_T, cap_R, cap_W;  // capacity of the output layout
+    int64_t cap_tail;
+    // outputs: the routed batch at capacity offsets of the upload layout
+    DKey* keys;      // reads' endpoints [2R'] (writes' follow at 2R' after k_route_move)
+    DKey* wstage;    // writes' endpoints [2 cap_W] before the move
+    int32_t *rown, *wown, *roff, *woff;
+    int64_t* snap;
+    uint8_t* flags;
+    uint8_t* tail;
+    int32_t* inv;       // [global T] batch index of each global transaction, -1 if not routed here
+    int32_t* read_ids;  // [R'] index of each kept read in its transaction (txReadConflictRangeIndexMap)
+    uint8_t* out_zero;  // conflict output to zero for this batch (or null), out_n global transactions
+    int64_t out_n;
+    RouteResult* res;   // host-mapped
+    RouteResult* dres;  // device copy
+};
+// Route the all-gathered shares into this resolver's batch (two launches on `s`).  grid_n: bound
+// on n_shares * tcap (global elements); the scan state's granules are zeroed by the caller.
+void launch_route(hipStream_t s, const RouteArgs& a, ScanState st);
+int64_t route_scan_words(int64_t n_elems);
+
 // ---- launchers (kernels.hip); all enqueue on `s` and never synchronize.
 // A history tier as the read check sees it.
 struct Tier {

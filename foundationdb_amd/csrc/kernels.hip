@@ -2883,6 +2883,181 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     w.scan_words = g - a;
 }
 
+// ------------------------------------------------------------------ multi-resolver routing
+//
+// The commit proxy's split of a batch across resolvers (CommitProxyServer.actor.cpp:118-187,
+// static keyResolvers): a read range goes, unclipped, to every resolver whose key range it meets
+// (intersectingRanges = [rangeContaining(begin), lower_bound(end)), fdbrpc/RangeMap.h:126-129; an
+// empty range to rangeContaining(begin)), a write range to every owner it meets; a transaction
+// gets a sub-transaction only on resolvers that received one of its ranges (:107-116), with its
+// snapshot and report flag (:181-186).  Here every resolver routes the all-gathered shares for
+// itself: one scan over the global transactions (one element each, its ranges visited by its
+// thread) counts what this resolver keeps and its store places it; TooOld (SkipList.cpp:770) is
+// applied to the sub-transaction as addTransaction would (its ranges are dropped).
+
+__device__ __forceinline__ const ShareHeader* share_at(const RouteArgs& a, int p) {
+    return (const ShareHeader*)(a.shares + (int64_t)p * a.stride);
+}
+
+struct RouteScan {
+    RouteArgs a;
+    // does [b, e) (keys of a share with tail region tb) meet [lo, hi)?
+    __device__ bool mine(const uint8_t* tb, const DKey& b, const DKey& e) const {
+        if (a.has_hi && dkey_cmp(b, tb, a.hi, a.btail) >= 0) return false;
+        if (!a.has_lo) return true;
+        return dkey_cmp(e, tb, a.lo, a.btail) > 0 || dkey_cmp(b, tb, a.lo, a.btail) >= 0;
+    }
+    __device__ static uint32_t tail_len(const DKey& k) { return k.len > 16u ? k.len - 16u : 0u; }
+    // element i = share i / tcap, transaction i % tcap of it (past the share's T: padding)
+    __device__ const ShareHeader* at(int64_t i, int& t, int64_t& gid) const {
+        const int p = (int)(i / a.tcap);
+        t = (int)(i - (int64_t)p * a.tcap);
+        const ShareHeader* h = share_at(a, p);
+        if (t >= h->T) return nullptr;
+        gid = t;
+        for (int q = 0; q < p; q++) gid += share_at(a, q)->T;
+        return h;
+    }
+    // counts: sub-transaction, kept reads, kept writes, kept tail bytes, report flag, keys > 19 and > 24 bytes
+    __device__ void load(int64_t i, uint32_t (&v)[7]) const {
+        int t;
+        int64_t gid;
+        const ShareHeader* h = at(i, t, gid);
+        if (!h) return;
+        const uint8_t* base = (const uint8_t*)h;
+        const DKey* keys = (const DKey*)(base + h->off_keys);
+        const int32_t* roff = (const int32_t*)(base + h->off_roff);
+        const int32_t* woff = (const int32_t*)(base + h->off_woff);
+        const uint8_t* tb = base + h->off_tail;
+        uint32_t nr = 0, nw = 0, tl = 0, g19 = 0, g24 = 0;
+        for (int r = roff[t]; r < roff[t + 1]; r++) {
+            const DKey kb = keys[2 * r], ke = keys[2 * r + 1];
+            if (!mine(tb, kb, ke)) continue;
+            nr++;
+            tl += tail_len(kb) + tail_len(ke);
+            g19 += (kb.len > 19u) + (ke.len > 19u);
+            g24 += (kb.len > 24u) + (ke.len > 24u);
+        }
+        for (int w = woff[t]; w < woff[t + 1]; w++) {
+            const DKey kb = keys[2 * (h->R + w)], ke = keys[2 * (h->R + w) + 1];
+            if (!mine(tb, kb, ke)) continue;
+            nw++;
+            tl += tail_len(kb) + tail_len(ke);
+            g19 += (kb.len > 19u) + (ke.len > 19u);
+            g24 += (kb.len > 24u) + (ke.len > 24u);
+        }
+        if (nr + nw == 0) return;
+        const int64_t* snap = (const int64_t*)(base + h->off_snap);
+        v[0] = 1;
+        if (snap[t] < a.oldest && nr > 0) return;  // TooOld: a sub-transaction without ranges
+        v[1] = nr;
+        v[2] = nw;
+        v[3] = tl;
+        v[4] = (a.report_enabled && base[h->off_report + t]) ? 1u : 0u;
+        v[5] = g19;
+        v[6] = g24;
+    }
+    __device__ void put_key(const uint8_t* tb, const DKey& k, DKey* out, uint32_t& cur) const {
+        DKey o = k;
+        o.tail = 0;
+        const uint32_t n = tail_len(k);
+        if (n) {
+            o.tail = cur;
+            if ((int64_t)cur + n <= a.cap_tail)
+                for (uint32_t j = 0; j < n; j++) a.tail[cur + j] = tb[k.tail + j];
+            cur += n;
+        }
+        *out = o;
+    }
+    __device__ void store(int64_t i, const uint32_t (&ex)[7]) const {
+        int t;
+        int64_t gid;
+        const ShareHeader* h = at(i, t, gid);
+        if (!h) return;
+        if (a.out_zero) a.out_zero[gid] = 0;
+        const uint8_t* base = (const uint8_t*)h;
+        const DKey* keys = (const DKey*)(base + h->off_keys);
+        const int32_t* roff = (const int32_t*)(base + h->off_roff);
+        const int32_t* woff = (const int32_t*)(base + h->off_woff);
+        const int64_t* snap = (const int64_t*)(base + h->off_snap);
+        const uint8_t* tb = base + h->off_tail;
+        // whether this transaction has a sub-transaction here, and whether it is TooOld, again
+        bool any = false, anyr = false;
+        for (int r = roff[t]; r < roff[t + 1] && !anyr; r++) anyr = mine(tb, keys[2 * r], keys[2 * r + 1]);
+        any = anyr;
+        for (int w = woff[t]; w < woff[t + 1] && !any; w++)
+            any = mine(tb, keys[2 * (h->R + w)], keys[2 * (h->R + w) + 1]);
+        const int lt = (int)ex[0];
+        a.inv[gid] = any && lt < a.cap_T ? lt : -1;
+        if (!any || lt >= a.cap_T) return;
+        const bool too_old = snap[t] < a.oldest && anyr;
+        uint8_t fl = (a.report_enabled && base[h->off_report + t]) ? kFlagReport : 0;
+        if (too_old) fl |= kFlagTooOld;
+        a.snap[lt] = snap[t];
+        a.flags[lt] = fl;
+        a.roff[lt] = (int32_t)ex[1];
+        a.woff[lt] = (int32_t)ex[2];
+        if (too_old) return;
+        uint32_t rl = ex[1], wl = ex[2], cur = ex[3];
+        for (int r = roff[t], k = 0; r < roff[t + 1]; r++, k++) {
+            const DKey kb = keys[2 * r], ke = keys[2 * r + 1];
+            if (!mine(tb, kb, ke)) continue;
+            if ((int)rl < a.cap_R) {
+                put_key(tb, kb, &a.keys[2 * rl], cur);
+                put_key(tb, ke, &a.keys[2 * rl + 1], cur);
+                a.rown[rl] = lt;
+                if (a.read_ids) a.read_ids[rl] = k;
+            }
+            rl++;
+        }
+        for (int w = woff[t]; w < woff[t + 1]; w++) {
+            const DKey kb = keys[2 * (h->R + w)], ke = keys[2 * (h->R + w) + 1];
+            if (!mine(tb, kb, ke)) continue;
+            if ((int)wl < a.cap_W) {
+                put_key(tb, kb, &a.wstage[2 * wl], cur);
+                put_key(tb, ke, &a.wstage[2 * wl + 1], cur);
+                a.wown[wl] = lt;
+            }
+            wl++;
+        }
+    }
+    __device__ void finish(const uint32_t (&tot)[7]) const {
+        RouteResult r{};
+        r.T = (int32_t)tot[0];
+        r.R = (int32_t)tot[1];
+        r.W = (int32_t)tot[2];
+        r.tail_bytes = tot[3];
+        r.reports = (int32_t)tot[4];
+        r.n_gt19 = (int32_t)tot[5];
+        r.n_gt24 = (int32_t)tot[6];
+        r.error = (r.T > a.cap_T || r.R > a.cap_R || r.W > a.cap_W || (int64_t)tot[3] > a.cap_tail) ? 1 : 0;
+        if (!r.error) {
+            a.roff[r.T] = r.R;
+            a.woff[r.T] = r.W;
+        }
+        *a.dres = r;
+        *a.res = r;
+    }
+};
+
+// The writes' endpoints after the reads' (BatchDev: write w's keys at 2(R + w)).
+__global__ __launch_bounds__(kBlock) void k_route_move(RouteArgs a) {
+    const RouteResult r = *a.dres;
+    if (r.error) return;
+    const int64_t n = 2 * (int64_t)r.W;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        a.keys[2 * (int64_t)r.R + j] = a.wstage[j];
+}
+
+int64_t route_scan_words(int64_t n_elems) { return 1 + scan_granules(n_elems, 7) + 8; }
+
+void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
+    const int64_t n = (int64_t)a.n_shares * a.tcap;
+    launch_scan<7>(s, RouteScan{a}, nullptr, n, st);
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (2 * (int64_t)a.cap_W + kBlock - 1) / kBlock));
+    fdb_launch(k_route_move, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+}
+
 // ------------------------------------------------------------------ range-max hierarchy + epilogue
 //
 // One workgroup per 4096 boundaries: each wave reduces 16 blocks of 64 versions to level 1, wave 0

@@ -124,6 +124,23 @@ class PackedBatch:
             )
         return out
 
+    def slice_txns(self, lo: int, hi: int) -> "PackedBatch":
+        """Transactions [lo, hi) as a batch of their own (a commit proxy's share of a global batch)."""
+        R, T = self.n_reads, self.n_txn
+        assert 0 <= lo <= hi <= T
+        r0, r1 = int(self.read_offsets[lo]), int(self.read_offsets[hi])
+        w0, w1 = int(self.write_offsets[lo]), int(self.write_offsets[hi])
+        ko = self.key_offsets
+        # key arena: the reads' key bytes then the writes' (each run contiguous in the source)
+        rk = self.key_bytes[ko[2 * r0]: ko[2 * r1]]
+        wk = self.key_bytes[ko[2 * (R + w0)]: ko[2 * (R + w1)]]
+        rofs = ko[2 * r0: 2 * r1 + 1] - ko[2 * r0]
+        wofs = ko[2 * (R + w0): 2 * (R + w1) + 1] - ko[2 * (R + w0)] + len(rk)
+        return PackedBatch(self.read_snapshot[lo:hi].copy(), self.report[lo:hi].copy(),
+                           (self.read_offsets[lo: hi + 1] - r0).astype(np.int32),
+                           (self.write_offsets[lo: hi + 1] - w0).astype(np.int32),
+                           np.concatenate([rk, wk]), np.concatenate([rofs, wofs[1:]]).astype(np.int64))
+
     def c_struct(self) -> _CPackedBatch:
         """ctypes view; the numpy arrays must outlive the returned struct."""
         return _CPackedBatch(

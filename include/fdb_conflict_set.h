@@ -210,6 +210,35 @@ int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr);
  * combine (CommitProxyServer.actor.cpp:764-780). */
 int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int32_t n_global, uint8_t* dev_out);
 
+/* Multi-resolver routing on the device: the commit proxy's split of a batch across resolvers
+ * (CommitProxyServer.actor.cpp:118-187 with a static keyResolvers map; fdbrpc/RangeMap.h:126-129).
+ * Each GPU is the proxy of one share of the global batch and the resolver of one key range.
+ *   fdbcs_share_bytes / fdbcs_share_pack: the share in the engine's wire layout (host memory; no
+ *     TooOld test, which stays with the resolvers).  The shares of all ranks are then gathered
+ *     into one device buffer, `stride` bytes apart in rank order (an RCCL all-gather).
+ *   fdbcs_batch_add_routed: on a new batch (the addTransaction step, SkipList.cpp:763-794): once
+ *     `after_stream` (a hipStream_t, as an integer) reaches this point, the engine keeps, on the
+ *     device, every range of the gathered shares that meets [lo_key, hi_key) (lo_len < 0: no lower
+ *     bound, hi_len < 0: none above), unclipped, reads and writes alike; a transaction gets a
+ *     sub-transaction iff one of its ranges is kept (:107-116), its snapshot copied, TooOld tested
+ *     against this set's oldest version now (SkipList.cpp:770).  Sub-transactions keep the global
+ *     order.  cap_*: bounds on the routed batch (FDBCS_E_NOMEM at detect if passed).  conflict_out
+ *     (optional, n_global bytes of device memory): as fdbcs_batch_set_conflict_output, with the
+ *     global index of a sub-transaction = its position in the concatenated shares.  Conflicting-key
+ *     reports are not collected for routed batches.  Detect and wait as for any batch; detect
+ *     blocks until the routing kernels have run (issue the next batch's routing first).
+ *   fdbcs_batch_routed_info: the routed batch's sizes and device views of its global -> batch
+ *     transaction map (int32[n_shares * max_share_txns], -1 where not routed) and of each kept
+ *     read's index in its transaction (txReadConflictRangeIndexMap, :144-165). */
+int fdbcs_share_bytes(const fdbcs_packed_batch* pb, int64_t* bytes);
+int fdbcs_share_pack(const fdbcs_packed_batch* pb, void* out, int64_t cap, int64_t* used);
+int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, int32_t n_shares, int32_t max_share_txns,
+                           const uint8_t* lo_key, int32_t lo_len, const uint8_t* hi_key, int32_t hi_len,
+                           int32_t cap_txns, int32_t cap_reads, int32_t cap_writes, int64_t cap_tail,
+                           uint8_t* conflict_out, int64_t n_global, uint64_t after_stream);
+int fdbcs_batch_routed_info(fdbcs_batch* b, int32_t* n_txn, int32_t* n_reads, int32_t* n_writes, void** inv_dev,
+                            void** read_ids_dev);
+
 /* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
  * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the
  * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead); 1-2 = the
