@@ -753,11 +753,15 @@ def main():
             pass
         dist_info = {"world_size": world, "backend": args.backend, "rccl_version": rccl,
                      "routing": ("device: each rank packs its share of the global batch (proxy), H2D, all-gather of "
-                                 "the shares, fdbcs_batch_add_routed (k_scan<RouteScan> + k_route_move) per resolver, "
+                                 "the shares, fdbcs_batch_add_routed (k_route_mark, k_scan<RouteScan>, k_route_write) per resolver, "
                                  "inside the timed region" if droute else
                                  "host (balancing.BalancedRouting) before the timed region: a feature check, not a "
                                  "throughput figure"),
-                     "share_stride_bytes": stride or None}
+                     "share_stride_bytes": stride or None,
+                     # the routing kernels' device time and the host time of fdbcs_batch_add_routed per
+                     # batch, over the timed region (the all-gather is not included: RCCL's own kernels)
+                     "route_kernels_ms_per_batch": st["ms_route_kernels"] / max(1, st["routed_batches"]) if droute else None,
+                     "route_host_ms_per_batch": st["host_ms_route"] / max(1, st["routed_batches"]) if droute else None}
     out = {
         "metric": "resolved txns/sec (conflict ranges checked/sec) per batch; HBM GB/s vs peak",
         "value": gtxn / elapsed,

@@ -90,6 +90,9 @@ class Stats(ctypes.Structure):
         ("base_sum", ctypes.c_int64),
         ("segments_sum", ctypes.c_int64),
         ("sort_big_buckets", ctypes.c_int64),
+        ("routed_batches", ctypes.c_int64),
+        ("ms_route_kernels", ctypes.c_double),
+        ("host_ms_route", ctypes.c_double),
     ]
 
     def as_dict(self):

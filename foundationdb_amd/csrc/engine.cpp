@@ -263,9 +263,11 @@ struct BatchSlot {
     bool free_recorded = false;
     HBuf pin_inv;  // fdbcs_batch_set_conflict_output: global -> batch transaction map (host-mapped)
     // device routing (fdbcs_batch_add_routed): scan state, global -> batch map, read ids, totals
-    DBuf rt_scan, rt_inv, rt_rids, rt_dres;
+    DBuf rt_scan, rt_inv, rt_rids, rt_dres, rt_info, rt_txpre;
     HBuf rt_res;
     hipEvent_t ev_route_in = nullptr;  // the caller's stream reached the all-gathered shares
+    hipEvent_t ev_rt0 = nullptr, ev_rt1 = nullptr;  // around the routing kernels
+    bool rt_timed = false;
     // per-kernel events of the batch (timing level 3, or the timed kernel at level 1)
     std::vector<hipEvent_t> prof_pool;
     size_t prof_next = 0;
@@ -664,10 +666,14 @@ void release_slot(BatchSlot* sl) {
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
     if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
     if (sl->ev_route_in) (void)hipEventDestroy(sl->ev_route_in);
+    if (sl->ev_rt0) (void)hipEventDestroy(sl->ev_rt0);
+    if (sl->ev_rt1) (void)hipEventDestroy(sl->ev_rt1);
     sl->rt_scan.release();
     sl->rt_inv.release();
     sl->rt_rids.release();
     sl->rt_dres.release();
+    sl->rt_info.release();
+    sl->rt_txpre.release();
     sl->rt_res.release();
     for (hipEvent_t e : sl->prof_pool) (void)hipEventDestroy(e);
     sl->dev.release();
@@ -1561,6 +1567,8 @@ static size_t share_layout(int32_t T, int64_t R, int64_t W, int64_t tail, ShareH
     off = align_up(off + 4 * ((size_t)T + 1), 64);
     h->off_report = (int64_t)off;
     off = align_up(off + (size_t)T, 64);
+    h->off_owner = (int64_t)off;
+    off = align_up(off + 4 * (size_t)(R + W), 64);
     h->off_tail = (int64_t)off;
     h->tail_bytes = tail;
     off = align_up(off + (size_t)tail + 64, 64);  // slack for dkey.h tail_word
@@ -1636,6 +1644,11 @@ int fdbcs_share_pack(const fdbcs_packed_batch* pb, void* out, int64_t cap, int64
             memcpy(o + h.off_report, pb->report_conflicting_keys, (size_t)T);
         else
             memset(o + h.off_report, 0, (size_t)T);
+        int32_t* owner = (int32_t*)(o + h.off_owner);
+        for (int32_t t = 0; t < T; t++) {
+            for (int32_t r = pb->read_offsets[t]; r < pb->read_offsets[t + 1]; r++) owner[r] = t;
+            for (int32_t w = pb->write_offsets[t]; w < pb->write_offsets[t + 1]; w++) owner[R + w] = t;
+        }
     }
     if (used) *used = (int64_t)bytes;
     return FDBCS_OK;
@@ -1691,16 +1704,22 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     a.btail = (const uint8_t*)cs->route_btail.p;
     // the routed batch's layout at capacity offsets (upload layout)
     const UploadLayout L = upload_layout((size_t)cap_txns, (size_t)cap_reads, (size_t)cap_writes, (size_t)cap_tail);
-    if ((rc = ensure_slot(sl, L.total + sizeof(DKey) * 2 * ((size_t)cap_writes + 1), (size_t)cap_txns, (size_t)cap_reads)))
-        return rc;
+    if ((rc = ensure_slot(sl, L.total, (size_t)cap_txns, (size_t)cap_reads))) return rc;
     const int64_t n_elems = (int64_t)n_shares * max_share_txns;
+    // ranges of one share: each takes 48 bytes of endpoint records, so the stride bounds them
+    const int64_t rstride = std::max<int64_t>(1, (stride - (int64_t)sizeof(ShareHeader)) / (2 * (int64_t)sizeof(DKey)));
     if ((rc = sl->rt_scan.ensure(8 * (size_t)route_scan_words(n_elems)))) return rc;
+    if ((rc = sl->rt_info.ensure(4 * (size_t)(n_shares * rstride)))) return rc;
+    if ((rc = sl->rt_txpre.ensure(16 * (size_t)std::max<int64_t>(n_elems, 1)))) return rc;
     if ((rc = sl->rt_inv.ensure(4 * (size_t)std::max<int64_t>(n_elems, 1)))) return rc;
     if ((rc = sl->rt_rids.ensure(4 * ((size_t)cap_reads + 1)))) return rc;
     if ((rc = sl->rt_dres.ensure(sizeof(RouteResult)))) return rc;
     if ((rc = sl->rt_res.ensure(sizeof(RouteResult), true))) return rc;
     if ((rc = make_slot_events(sl))) return rc;
     if (!sl->ev_route_in) HIPOK(hipEventCreateWithFlags(&sl->ev_route_in, hipEventDisableTiming));
+    if (!sl->ev_rt0) HIPOK(hipEventCreate(&sl->ev_rt0));
+    if (!sl->ev_rt1) HIPOK(hipEventCreate(&sl->ev_rt1));
+    const auto t_host = std::chrono::steady_clock::now();
     char* d = (char*)sl->dev.p;
     a.shares = (const uint8_t*)shares;
     a.stride = stride;
@@ -1713,7 +1732,9 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     a.cap_W = cap_writes;
     a.cap_tail = cap_tail;
     a.keys = (DKey*)(d + L.keys);
-    a.wstage = (DKey*)(d + L.total);
+    a.info = (uint32_t*)sl->rt_info.p;
+    a.rstride = rstride;
+    a.txpre = (int4*)sl->rt_txpre.p;
     a.rown = (int32_t*)(d + L.rown);
     a.wown = (int32_t*)(d + L.wown);
     a.snap = (int64_t*)(d + L.snap);
@@ -1738,9 +1759,13 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     uint64_t* sw = (uint64_t*)sl->rt_scan.p;
     ScanState st{sw + 8, (int*)sw, (int*)(sw + 1)};
     t_record = nullptr;
+    HIPOK(hipEventRecord(sl->ev_rt0, us));
     launch_route(us, a, st);
     HIPOK(take_launch_error());
+    HIPOK(hipEventRecord(sl->ev_rt1, us));
+    sl->rt_timed = true;
     HIPOK(hipEventRecord(sl->ev_up, us));
+    cs->stats.host_ms_route += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host).count();
     b->bd.keys = a.keys;
     b->bd.rowner = a.rown;
     b->bd.wowner = a.wown;
@@ -2301,6 +2326,12 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         }
         st.gc_runs += b->gc_ran ? 1 : 0;
         st.sort_big_buckets += b->h_scal->sort_big;
+        if (b->routed && b->slot->rt_timed) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, b->slot->ev_rt0, b->slot->ev_rt1) == hipSuccess) st.ms_route_kernels += ms;
+            st.routed_batches += 1;
+            b->slot->rt_timed = false;
+        }
         if (b->compacted) {
             st.compactions += 1;
             // kept base boundaries read, delta boundaries inserted read, result written

@@ -245,19 +245,20 @@ __host__ __device__ inline int64_t verdict_scalars_offset(int64_t T) { return (T
 // 118-187, for a static key-range split).  Every rank is the proxy of one share of the global
 // batch: it packs its share in the wire layout below (fdbcs_share_pack), the shares are
 // all-gathered over xGMI (RCCL), and each resolver keeps the ranges that meet its key range
-// (k_scan<RouteScan> + k_route_move) as a batch in the upload layout.
+// (k_route_mark, k_scan<RouteScan>, k_route_write) as a batch in the upload layout.
 // Wire layout of a share: ShareHeader, then DKey keys[2(R+W)] (tail = byte offset in the share's
-// tail region), int64 snap[T], int32 roff[T+1], int32 woff[T+1], uint8 report[T], tail bytes; every
-// region 64-byte aligned, the whole share <= the all-gather stride.
+// tail region), int64 snap[T], int32 roff[T+1], int32 woff[T+1], uint8 report[T], int32 owner[R+W],
+// tail bytes; every region 64-byte aligned, the whole share <= the all-gather stride.
 struct ShareHeader {
     int32_t T, R, W, pad0;
     int64_t bytes;       // the share, header included
     int64_t off_keys, off_snap, off_roff, off_woff, off_report, off_tail;
     int64_t tail_bytes;
-    int64_t pad[6];
+    int64_t off_owner;   // int32 owner[R+W]: the transaction of each read, then of each write
+    int64_t pad[5];
 };
 static_assert(sizeof(ShareHeader) == 128, "ShareHeader is 128 bytes");
-// Totals of a routed batch (host-mapped copy for the host, device copy for k_route_move).
+// Totals of a routed batch (host-mapped copy for the host, device copy for k_route_write).
 struct RouteResult {
     int32_t T, R, W, reports;
     int32_t n_gt19, n_gt24;  // kept keys longer than 19 / 24 bytes (sort tail windows, long-key probes)
@@ -277,8 +278,10 @@ struct RouteArgs {
     int32_t cap_T, cap_R, cap_W;  // capacity of the output layout
     int64_t cap_tail;
     // outputs: the routed batch at capacity offsets of the upload layout
-    DKey* keys;      // reads' endpoints [2R'] (writes' follow at 2R' after k_route_move)
-    DKey* wstage;    // writes' endpoints [2 cap_W] before the move
+    DKey* keys;      // the routed endpoints: reads' [2R'], then writes'
+    uint32_t* info;  // [n_shares * rstride] per range: kept, long-key bits, tail bytes (k_route_mark)
+    int64_t rstride; // >= any share's R + W
+    int4* txpre;     // [n_shares * tcap] per transaction: batch index, read / write / tail prefixes
     int32_t *rown, *wown, *roff, *woff;
     int64_t* snap;
     uint8_t* flags;

@@ -2899,18 +2899,32 @@ __device__ __forceinline__ const ShareHeader* share_at(const RouteArgs& a, int p
     return (const ShareHeader*)(a.shares + (int64_t)p * a.stride);
 }
 
+// Per range of every share (one thread each): does it meet this resolver's [lo, hi)?  info =
+// kept | an endpoint longer than 19 bytes << 1 | longer than 24 << 2 | tail bytes of both
+// endpoints << 8.
+__global__ __launch_bounds__(kBlock) void k_route_mark(RouteArgs a) {
+    const int p = blockIdx.y;
+    const ShareHeader* h = share_at(a, p);
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= h->R + h->W) return;
+    const uint8_t* base = (const uint8_t*)h;
+    const DKey* keys = (const DKey*)(base + h->off_keys);
+    const uint8_t* tb = base + h->off_tail;
+    const DKey kb = keys[2 * j], ke = keys[2 * j + 1];
+    bool in = !a.has_hi || dkey_cmp(kb, tb, a.hi, a.btail) < 0;
+    if (in && a.has_lo) in = dkey_cmp(ke, tb, a.lo, a.btail) > 0 || dkey_cmp(kb, tb, a.lo, a.btail) >= 0;
+    const uint32_t tl = (kb.len > 16u ? kb.len - 16u : 0u) + (ke.len > 16u ? ke.len - 16u : 0u);
+    a.info[(int64_t)p * a.rstride + j] =
+        (in ? 1u : 0u) | ((kb.len > 19u || ke.len > 19u) ? 2u : 0u) | ((kb.len > 24u || ke.len > 24u) ? 4u : 0u) | (tl << 8);
+}
+
+// One element per transaction of every share (element i = share i / tcap, transaction i % tcap;
+// past the share's T: padding): what this resolver keeps of it, as counts; the store places the
+// sub-transaction and leaves its prefixes for k_route_write.
 struct RouteScan {
     RouteArgs a;
-    // does [b, e) (keys of a share with tail region tb) meet [lo, hi)?
-    __device__ bool mine(const uint8_t* tb, const DKey& b, const DKey& e) const {
-        if (a.has_hi && dkey_cmp(b, tb, a.hi, a.btail) >= 0) return false;
-        if (!a.has_lo) return true;
-        return dkey_cmp(e, tb, a.lo, a.btail) > 0 || dkey_cmp(b, tb, a.lo, a.btail) >= 0;
-    }
-    __device__ static uint32_t tail_len(const DKey& k) { return k.len > 16u ? k.len - 16u : 0u; }
-    // element i = share i / tcap, transaction i % tcap of it (past the share's T: padding)
-    __device__ const ShareHeader* at(int64_t i, int& t, int64_t& gid) const {
-        const int p = (int)(i / a.tcap);
+    __device__ const ShareHeader* at(int64_t i, int& p, int& t, int64_t& gid) const {
+        p = (int)(i / a.tcap);
         t = (int)(i - (int64_t)p * a.tcap);
         const ShareHeader* h = share_at(a, p);
         if (t >= h->T) return nullptr;
@@ -2918,118 +2932,79 @@ struct RouteScan {
         for (int q = 0; q < p; q++) gid += share_at(a, q)->T;
         return h;
     }
-    // counts: sub-transaction, kept reads, kept writes, kept tail bytes, report flag, keys > 19 and > 24 bytes
-    __device__ void load(int64_t i, uint32_t (&v)[7]) const {
-        int t;
-        int64_t gid;
-        const ShareHeader* h = at(i, t, gid);
-        if (!h) return;
+    // counts: sub-transaction, kept reads, kept writes, kept tail bytes, ranges with a key > 19 / > 24 bytes
+    __device__ bool visit(int64_t i, uint32_t (&v)[6], bool& any, bool& too_old, int& p, int& t, int64_t& gid,
+                          const ShareHeader*& h) const {
+        h = at(i, p, t, gid);
+        if (!h) return false;
         const uint8_t* base = (const uint8_t*)h;
-        const DKey* keys = (const DKey*)(base + h->off_keys);
         const int32_t* roff = (const int32_t*)(base + h->off_roff);
         const int32_t* woff = (const int32_t*)(base + h->off_woff);
-        const uint8_t* tb = base + h->off_tail;
+        const uint32_t* info = a.info + (int64_t)p * a.rstride;
         uint32_t nr = 0, nw = 0, tl = 0, g19 = 0, g24 = 0;
-        for (int r = roff[t]; r < roff[t + 1]; r++) {
-            const DKey kb = keys[2 * r], ke = keys[2 * r + 1];
-            if (!mine(tb, kb, ke)) continue;
+        const int r0 = roff[t], r1 = roff[t + 1], w0 = h->R + woff[t], w1 = h->R + woff[t + 1];
+        for (int j = r0; j < r1; j++) {
+            const uint32_t x = info[j];
+            if (!(x & 1u)) continue;
             nr++;
-            tl += tail_len(kb) + tail_len(ke);
-            g19 += (kb.len > 19u) + (ke.len > 19u);
-            g24 += (kb.len > 24u) + (ke.len > 24u);
+            tl += x >> 8;
+            g19 += (x >> 1) & 1u;
+            g24 += (x >> 2) & 1u;
         }
-        for (int w = woff[t]; w < woff[t + 1]; w++) {
-            const DKey kb = keys[2 * (h->R + w)], ke = keys[2 * (h->R + w) + 1];
-            if (!mine(tb, kb, ke)) continue;
+        for (int j = w0; j < w1; j++) {
+            const uint32_t x = info[j];
+            if (!(x & 1u)) continue;
             nw++;
-            tl += tail_len(kb) + tail_len(ke);
-            g19 += (kb.len > 19u) + (ke.len > 19u);
-            g24 += (kb.len > 24u) + (ke.len > 24u);
+            tl += x >> 8;
+            g19 += (x >> 1) & 1u;
+            g24 += (x >> 2) & 1u;
         }
-        if (nr + nw == 0) return;
-        const int64_t* snap = (const int64_t*)(base + h->off_snap);
+        any = nr + nw > 0;
+        too_old = any && nr > 0 && ((const int64_t*)(base + h->off_snap))[t] < a.oldest;
+        if (!any) return true;
         v[0] = 1;
-        if (snap[t] < a.oldest && nr > 0) return;  // TooOld: a sub-transaction without ranges
+        if (too_old) return true;  // TooOld (SkipList.cpp:770): a sub-transaction without ranges
         v[1] = nr;
         v[2] = nw;
         v[3] = tl;
-        v[4] = (a.report_enabled && base[h->off_report + t]) ? 1u : 0u;
-        v[5] = g19;
-        v[6] = g24;
+        v[4] = g19;
+        v[5] = g24;
+        return true;
     }
-    __device__ void put_key(const uint8_t* tb, const DKey& k, DKey* out, uint32_t& cur) const {
-        DKey o = k;
-        o.tail = 0;
-        const uint32_t n = tail_len(k);
-        if (n) {
-            o.tail = cur;
-            if ((int64_t)cur + n <= a.cap_tail)
-                for (uint32_t j = 0; j < n; j++) a.tail[cur + j] = tb[k.tail + j];
-            cur += n;
-        }
-        *out = o;
-    }
-    __device__ void store(int64_t i, const uint32_t (&ex)[7]) const {
-        int t;
+    __device__ void load(int64_t i, uint32_t (&v)[6]) const {
+        bool any, too_old;
+        int p, t;
         int64_t gid;
-        const ShareHeader* h = at(i, t, gid);
-        if (!h) return;
+        const ShareHeader* h;
+        visit(i, v, any, too_old, p, t, gid, h);
+    }
+    __device__ void store(int64_t i, const uint32_t (&ex)[6]) const {
+        uint32_t v[6] = {0, 0, 0, 0, 0, 0};
+        bool any, too_old;
+        int p, t;
+        int64_t gid;
+        const ShareHeader* h;
+        if (!visit(i, v, any, too_old, p, t, gid, h)) return;
         if (a.out_zero) a.out_zero[gid] = 0;
-        const uint8_t* base = (const uint8_t*)h;
-        const DKey* keys = (const DKey*)(base + h->off_keys);
-        const int32_t* roff = (const int32_t*)(base + h->off_roff);
-        const int32_t* woff = (const int32_t*)(base + h->off_woff);
-        const int64_t* snap = (const int64_t*)(base + h->off_snap);
-        const uint8_t* tb = base + h->off_tail;
-        // whether this transaction has a sub-transaction here, and whether it is TooOld, again
-        bool any = false, anyr = false;
-        for (int r = roff[t]; r < roff[t + 1] && !anyr; r++) anyr = mine(tb, keys[2 * r], keys[2 * r + 1]);
-        any = anyr;
-        for (int w = woff[t]; w < woff[t + 1] && !any; w++)
-            any = mine(tb, keys[2 * (h->R + w)], keys[2 * (h->R + w) + 1]);
         const int lt = (int)ex[0];
-        a.inv[gid] = any && lt < a.cap_T ? lt : -1;
-        if (!any || lt >= a.cap_T) return;
-        const bool too_old = snap[t] < a.oldest && anyr;
-        uint8_t fl = (a.report_enabled && base[h->off_report + t]) ? kFlagReport : 0;
-        if (too_old) fl |= kFlagTooOld;
-        a.snap[lt] = snap[t];
-        a.flags[lt] = fl;
+        const bool fits = any && lt < a.cap_T;
+        a.inv[gid] = fits ? lt : -1;
+        a.txpre[i] = make_int4(fits ? lt : -1, too_old ? -1 : (int)ex[1], (int)ex[2], (int)ex[3]);
+        if (!fits) return;
+        const uint8_t* base = (const uint8_t*)h;
+        a.snap[lt] = ((const int64_t*)(base + h->off_snap))[t];
+        a.flags[lt] = too_old ? kFlagTooOld : 0;
         a.roff[lt] = (int32_t)ex[1];
         a.woff[lt] = (int32_t)ex[2];
-        if (too_old) return;
-        uint32_t rl = ex[1], wl = ex[2], cur = ex[3];
-        for (int r = roff[t], k = 0; r < roff[t + 1]; r++, k++) {
-            const DKey kb = keys[2 * r], ke = keys[2 * r + 1];
-            if (!mine(tb, kb, ke)) continue;
-            if ((int)rl < a.cap_R) {
-                put_key(tb, kb, &a.keys[2 * rl], cur);
-                put_key(tb, ke, &a.keys[2 * rl + 1], cur);
-                a.rown[rl] = lt;
-                if (a.read_ids) a.read_ids[rl] = k;
-            }
-            rl++;
-        }
-        for (int w = woff[t]; w < woff[t + 1]; w++) {
-            const DKey kb = keys[2 * (h->R + w)], ke = keys[2 * (h->R + w) + 1];
-            if (!mine(tb, kb, ke)) continue;
-            if ((int)wl < a.cap_W) {
-                put_key(tb, kb, &a.wstage[2 * wl], cur);
-                put_key(tb, ke, &a.wstage[2 * wl + 1], cur);
-                a.wown[wl] = lt;
-            }
-            wl++;
-        }
     }
-    __device__ void finish(const uint32_t (&tot)[7]) const {
+    __device__ void finish(const uint32_t (&tot)[6]) const {
         RouteResult r{};
         r.T = (int32_t)tot[0];
         r.R = (int32_t)tot[1];
         r.W = (int32_t)tot[2];
         r.tail_bytes = tot[3];
-        r.reports = (int32_t)tot[4];
-        r.n_gt19 = (int32_t)tot[5];
-        r.n_gt24 = (int32_t)tot[6];
+        r.n_gt19 = (int32_t)tot[4];
+        r.n_gt24 = (int32_t)tot[5];
         r.error = (r.T > a.cap_T || r.R > a.cap_R || r.W > a.cap_W || (int64_t)tot[3] > a.cap_tail) ? 1 : 0;
         if (!r.error) {
             a.roff[r.T] = r.R;
@@ -3040,22 +3015,69 @@ struct RouteScan {
     }
 };
 
-// The writes' endpoints after the reads' (BatchDev: write w's keys at 2(R + w)).
-__global__ __launch_bounds__(kBlock) void k_route_move(RouteArgs a) {
-    const RouteResult r = *a.dres;
-    if (r.error) return;
-    const int64_t n = 2 * (int64_t)r.W;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
-        a.keys[2 * (int64_t)r.R + j] = a.wstage[j];
+// Per range of every share again: a kept range of a sub-transaction that is not TooOld goes to
+// its place (the transaction's prefix plus the kept ranges before it in the transaction; reads
+// before writes, as addTransaction registers them, SkipList.cpp:779-789), its tails appended.
+__global__ __launch_bounds__(kBlock) void k_route_write(RouteArgs a) {
+    const RouteResult res = *a.dres;
+    if (res.error) return;
+    const int p = blockIdx.y;
+    const ShareHeader* h = share_at(a, p);
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= h->R + h->W) return;
+    const uint32_t* info = a.info + (int64_t)p * a.rstride;
+    const uint32_t x = info[j];
+    if (!(x & 1u)) return;
+    const uint8_t* base = (const uint8_t*)h;
+    const int t = ((const int32_t*)(base + h->off_owner))[j];
+    const int4 pre = a.txpre[(int64_t)p * a.tcap + t];
+    if (pre.x < 0 || pre.y < 0) return;  // not placed, or TooOld
+    const int32_t* roff = (const int32_t*)(base + h->off_roff);
+    const int32_t* woff = (const int32_t*)(base + h->off_woff);
+    const bool is_read = j < h->R;
+    const int first = is_read ? roff[t] : h->R + woff[t];
+    // kept ranges of the transaction before this one (its kept reads all precede a write's tails)
+    uint32_t rank = 0, tail = (uint32_t)pre.w;
+    if (!is_read)
+        for (int q = roff[t]; q < roff[t + 1]; q++) tail += (info[q] & 1u) ? info[q] >> 8 : 0u;
+    for (int q = first; q < j; q++) {
+        const uint32_t y = info[q];
+        if (!(y & 1u)) continue;
+        rank++;
+        tail += y >> 8;
+    }
+    const DKey* keys = (const DKey*)(base + h->off_keys);
+    const uint8_t* tb = base + h->off_tail;
+    const int64_t slot = is_read ? (int64_t)pre.y + rank : (int64_t)res.R + pre.z + rank;
+    if (is_read) {
+        a.rown[pre.y + rank] = pre.x;
+        if (a.read_ids) a.read_ids[pre.y + rank] = j - roff[t];
+    } else {
+        a.wown[pre.z + rank] = pre.x;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        DKey k = keys[2 * j + e];
+        const uint32_t n = k.len > 16u ? k.len - 16u : 0u;
+        if (n) {
+            const uint8_t* src = tb + k.tail;
+            for (uint32_t q = 0; q < n; q++) a.tail[tail + q] = src[q];
+            k.tail = tail;
+            tail += n;
+        } else {
+            k.tail = 0;
+        }
+        a.keys[2 * slot + e] = k;
+    }
 }
 
-int64_t route_scan_words(int64_t n_elems) { return 1 + scan_granules(n_elems, 7) + 8; }
+int64_t route_scan_words(int64_t n_elems) { return 8 + scan_granules(n_elems, 6); }
 
 void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
-    const int64_t n = (int64_t)a.n_shares * a.tcap;
-    launch_scan<7>(s, RouteScan{a}, nullptr, n, st);
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (2 * (int64_t)a.cap_W + kBlock - 1) / kBlock));
-    fdb_launch(k_route_move, dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+    const dim3 grid((unsigned)std::max<int64_t>(1, (a.rstride + kBlock - 1) / kBlock), (unsigned)a.n_shares);
+    fdb_launch(k_route_mark, grid, dim3(kBlock), 0, s, a);
+    launch_scan<6>(s, RouteScan{a}, nullptr, (int64_t)a.n_shares * a.tcap, st);
+    fdb_launch(k_route_write, grid, dim3(kBlock), 0, s, a);
 }
 
 // ------------------------------------------------------------------ range-max hierarchy + epilogue

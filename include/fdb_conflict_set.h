@@ -125,6 +125,11 @@ typedef struct fdbcs_stats {
     int64_t base_sum;          /* base-tier boundaries after each batch, summed */
     int64_t segments_sum;      /* union segments of committed writes, summed */
     int64_t sort_big_buckets;  /* sort buckets past the per-wave capacity (ranked by their workgroup) */
+    /* Device routing (fdbcs_batch_add_routed): batches, device time of their routing kernels
+     * (events around them, every routed batch) and host time inside the call. */
+    int64_t routed_batches;
+    double ms_route_kernels;
+    double host_ms_route;
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */

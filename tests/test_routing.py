@@ -20,8 +20,8 @@ def _header(buf):
     h = np.frombuffer(buf[:128].tobytes(), dtype=np.int64)
     T, R = np.frombuffer(buf[:8].tobytes(), dtype=np.int32)
     Wn = int(np.frombuffer(buf[8:12].tobytes(), dtype=np.int32)[0])
-    names = ["bytes", "off_keys", "off_snap", "off_roff", "off_woff", "off_report", "off_tail", "tail_bytes"]
-    return int(T), int(R), Wn, dict(zip(names, (int(x) for x in h[2:10])))
+    names = ["bytes", "off_keys", "off_snap", "off_roff", "off_woff", "off_report", "off_tail", "tail_bytes", "off_owner"]
+    return int(T), int(R), Wn, dict(zip(names, (int(x) for x in h[2:11])))
 
 
 def _dkey(buf, off, k):
@@ -57,6 +57,9 @@ def test_share_pack_layout(lib, long_keys):
         if len(key) > 16:
             assert tails[tail: tail + len(key) - 16].tobytes() == key[16:]
     assert sum(max(0, len(pb.key(k)) - 16) for k in range(2 * (R + Wn))) == h["tail_bytes"]
+    owner = np.frombuffer(buf[h["off_owner"]: h["off_owner"] + 4 * (R + Wn)].tobytes(), np.int32)
+    np.testing.assert_array_equal(owner[:R], np.repeat(np.arange(T), np.diff(pb.read_offsets)))
+    np.testing.assert_array_equal(owner[R:], np.repeat(np.arange(T), np.diff(pb.write_offsets)))
 
 
 def test_share_pack_rejects_inverted_range_and_small_buffer(lib):
