@@ -1,40 +1,51 @@
-"""Per-launch HBM bytes of the roofline kernels (roofline.py) from rocprofv3 --pmc CSVs.
+"""Per-launch HBM bytes of every pipeline kernel from rocprofv3 --pmc CSVs (FETCH_SIZE and
+WRITE_SIZE, each from its own pass; MI355X_MICROARCH.md: PMC slots, gfx950 corrections).
 
-k_check_reads is the read check, k_bucket_sort the endpoint sort, k_merge_copy<BatchIns> merges a
-batch into the delta tier, k_merge_copy<CompactIns> folds the delta into the base tier.
-FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
-the bytes of a wide (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md, HBM); the copy
-reads 16-B keys and 8-B length/version words, so both the raw and the x2-corrected fetch figures
-are reported.
+FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half the bytes of a wide
+(16 B/lane) coalesced streaming read, so `bytes_per_launch` uses 2 x FETCH_SIZE + WRITE_SIZE and
+`bytes_per_launch_raw` the counters as read.  Kernel names are the engine's (fdbcs_kernel_profile:
+no `void`, no leading namespace, no parameter list), the key roofline.pmc_traffic reads.
+Usage: pmc_summary.py <dir with FETCH_SIZE/ and WRITE_SIZE/> [workload txns history]
 """
 import csv
 import glob
 import json
 import os
 import sys
+from collections import defaultdict
 
-# the read check: k_check_reads over both tiers (default over a base tier < 16M boundaries) or the
-# split check's base-tier launch k_check_tier<true, ...>
-KERNELS = {"check": ("k_check_tier<true", "k_check_reads"), "sort": ("k_bucket_sort",),
-           "merge": ("k_merge_copy<fdbcs::BatchIns",), "compact": ("k_merge_copy<fdbcs::CompactIns",)}
+
+def engine_name(n: str) -> str:
+    n = n.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    depth = 0
+    for i, ch in enumerate(n):  # cut the parameter list: the first '(' outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            n = n[:i]
+            break
+    return n[len("fdbcs::"):] if n.startswith("fdbcs::") else n
+
 
 root = sys.argv[1]
-out = {}
-for key, tag in KERNELS.items():
-    per = {}
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        files = glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True)
-        vals = []
-        for f in files:
-            for r in csv.DictReader(open(f)):
-                name = r.get("Kernel_Name", "")
-                if any(t in name for t in tag) and r.get("Counter_Name") == c:
-                    vals.append(float(r["Counter_Value"]))
-        per[c] = sum(vals) / len(vals) if vals else None
-        out[f"{key}_{c}_kib_per_launch"] = per[c]
-        out[f"{key}_{c}_launches"] = len(vals)
-    f, w = per["FETCH_SIZE"], per["WRITE_SIZE"]
-    if f is not None and w is not None:
-        out[f"{key}_bytes_per_launch_raw"] = (f + w) * 1024
-        out[f"{key}_bytes_per_launch"] = (2 * f + w) * 1024  # gfx950 FETCH_SIZE half-count correction
+per = {c: defaultdict(list) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+for c in per:
+    for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == c:
+                per[c][engine_name(r.get("Kernel_Name", ""))].append(float(r["Counter_Value"]))
+out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; bytes = (2 x FETCH + WRITE) x 1024",
+       "bytes_per_launch": {}, "bytes_per_launch_raw": {}, "launches": {}}
+if len(sys.argv) >= 5:
+    out["config"] = {"workload": sys.argv[2], "txns": int(sys.argv[3]), "history": int(sys.argv[4])}
+for k in sorted(set(per["FETCH_SIZE"]) & set(per["WRITE_SIZE"])):
+    f = sum(per["FETCH_SIZE"][k]) / len(per["FETCH_SIZE"][k])
+    w = sum(per["WRITE_SIZE"][k]) / len(per["WRITE_SIZE"][k])
+    out["bytes_per_launch"][k] = (2 * f + w) * 1024
+    out["bytes_per_launch_raw"][k] = (f + w) * 1024
+    out["launches"][k] = len(per["FETCH_SIZE"][k])
 print(json.dumps(out, indent=1))
