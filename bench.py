@@ -60,6 +60,7 @@ WINDOW = 8  # batches in flight (submitted, not yet waited) in the timed loops
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--window", type=int, default=8, help="batches in flight in the timed loops")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--txns", type=int, default=0, help="transactions per batch per GPU; 0 = the workload's")
@@ -322,6 +323,8 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank, n_
 
 def main():
     args = parse()
+    global WINDOW
+    WINDOW = max(1, args.window)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

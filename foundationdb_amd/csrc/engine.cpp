@@ -1902,7 +1902,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // Stage A (sort, positions, candidate edges) depends only on this batch: it runs on its own
     // stream and overlaps stage B of the previous batch.  Phase timing (level 2) runs both stages on
     // one stream so the phases are measured one after another.
-    hipStream_t sa = (timing >= 2 || cs->serial) ? s : cs->astream;
+    hipStream_t sa = (timing == 2 || cs->serial) ? s : cs->astream;  // level 3 keeps the timed layout
     const int wp = cs->wpar;
     cs->wpar = (wp + 1) % kNumWork;
     b->wp = wp;
@@ -1944,7 +1944,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // on the stream its half of D.CheckRead runs beside stage A on its own stream; stage B keeps the
     // delta half.
     const bool split = (cs->split_check == 1 || (cs->split_check == 2 && cs->n_ub >= kSplitCheckMinBase)) &&
-                       !cs->serial && timing < 2;
+                       !cs->serial && timing != 2;
     // two submitting threads: this batch's stage A and check go out from the helper, stage B on the
     // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it
     // records cannot be queried here: waits on its events are kept unconditionally.
@@ -1954,7 +1954,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- upload (issued now) and record stage A: D.Sort and the candidate edges of D.CheckIntraBatch
     // The upload runs on its own stream unless the phases are timed one after another (then on
     // stage A's stream, bracketed by the upload phase's events).
-    const bool own_upload = timing < 2 && !cs->serial;
+    const bool own_upload = timing != 2 && !cs->serial;
     if (hipEvent_t e = rec(kPhStart, 2)) HIPOK(hipEventRecord(e, sa));
     if (b->state == 0 && (rc = do_upload(b, own_upload ? cs->ustream : sa))) return rc;
     if (hipEvent_t e = rec(kPhUpload, 2)) HIPOK(hipEventRecord(e, sa));
@@ -2029,7 +2029,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- record stage B: D.CheckRead against the history the previous batch left, then batch order
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
-    const bool graphs = cs->stage_graphs && timing < 2;
+    const bool graphs = cs->stage_graphs && timing != 2;
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
         launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax);
