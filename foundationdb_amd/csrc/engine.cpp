@@ -134,6 +134,18 @@ struct fdbcs_conflict_set {
                                     // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
     hipEvent_t ev_b[kNumWork] = {}; // stage B (epilogue) of the batch using workspace k is done
+    // Stage B in two halves on two streams: X (`stream`: read check, resolution, D.Combine) and Y
+    // (`ystream`: merge into the delta, compaction / GC, epilogue).  The check of batch i + 1 runs
+    // against the delta before batch i's merge plus batch i's union segments (PrevSegs), so it does
+    // not wait for that merge: Y(i) overlaps X(i + 1).
+    hipStream_t ystream = nullptr;
+    hipEvent_t ev_res[kNumWork] = {};   // X of the batch using workspace k is done (Y waits for it)
+    hipEvent_t ev_xfree[kNumWork] = {}; // the next batch's check is done with workspace k's segments
+    bool prev_segs = false;             // the last batch's segments are not merged when the next check runs
+    int prev_wp = 0;
+    int64_t prev_now = 0;
+    int last_wp = -1, prev2_wp = -1;    // workspaces of the last two batches submitted (their Y events)
+    bool xfree_rec[kNumWork] = {};      // ev_xfree[k] recorded since workspace k's last use
     bool wused[kNumWork] = {};
     int wpar = 0;                   // workspace of the next batch
     int timing = 0;       // 0: no events; 1: the copy kernels; 2: every phase (fdbcs_set_timing)
@@ -151,8 +163,8 @@ struct fdbcs_conflict_set {
     DBuf hkey[2], hlt[2], hver[2];
     DBuf lvl[kMaxLevels];  // lvl[0]: sampled key index (the level-0 versions are hver[cur])
     DBuf dir;              // radix directory over the base tier's level-0 samples (k_directory)
-    DBuf edir;             // the delta tier's directory (epoch-tagged entries, filled by k_epilogue)
-    uint32_t ddir_epoch = 0;    // epoch of the delta tier's current directory (0: none)
+    DBuf edir[2];          // each delta buffer's directory (epoch-tagged entries, filled by k_epilogue)
+    uint32_t ddir_epoch[2] = {0, 0};  // epoch of each delta buffer's directory (0: none)
     uint32_t ddir_counter = 0;  // last epoch handed out
     int cur = 0;
     int64_t hist_cap = 0;  // elements per buffer set
@@ -160,7 +172,7 @@ struct fdbcs_conflict_set {
     int64_t lvl3_n = 0;
     // delta tier: the same layout, small
     DBuf dkey[2], dlt[2], dver[2];
-    DBuf dlvl[kMaxLevels];
+    DBuf dlvl[2][kMaxLevels];  // per delta buffer: the next batch's check reads one while the epilogue builds the other
     int dcur = 0;
     int64_t delta_cap = 0;
     int64_t nd_ub = 0;
@@ -175,6 +187,7 @@ struct fdbcs_conflict_set {
     std::vector<uint8_t> route_bounds; // the bounds route_btail holds (lo | hi bytes), to skip re-uploads
     // batch workspaces (rotating)
     DBuf ws[kNumWork][56];  // [0, kWsScanSlot): TAKE slots of ensure_workspace
+    DBuf wbtail[kNumWork];  // Work::btail of each workspace (ensure_btail)
     int64_t ws_T = -1, ws_R = -1, ws_W = -1;
     Work work[kNumWork]{};
     int64_t edge_cap = 0;
@@ -241,7 +254,8 @@ struct fdbcs_conflict_set {
     LaunchList work_a, work_c;          // the helper's lists
     hipStream_t work_sa = nullptr;
     uint32_t work_need_b = 0;           // the check goes out once b_issued >= this
-    LaunchList rec_a, rec_b, rec_c, pending_b;
+    LaunchList rec_a, rec_b, rec_c, rec_y, pending_b, pending_y;
+    hipStream_t pending_ys = nullptr;  // the stream of pending_y
     fdbcs_batch* pending_batch = nullptr;
     int64_t graph_launches = 0;
     std::unordered_set<fdbcs_batch*> live;  // batches not yet destroyed (detached if the set goes first)
@@ -377,6 +391,20 @@ int sync_all(fdbcs_conflict_set* cs) {
     HIPOK(hipStreamSynchronize(cs->cstream));
     HIPOK(hipStreamSynchronize(cs->astream));
     HIPOK(hipStreamSynchronize(cs->stream));
+    HIPOK(hipStreamSynchronize(cs->ystream));
+    cs->prev_segs = false;  // everything submitted is merged: the next check reads the current delta
+    return FDBCS_OK;
+}
+
+// Each workspace's copy of a batch tail region (Work::btail) for `bytes`.
+int ensure_btail(fdbcs_conflict_set* cs, int64_t bytes) {
+    const size_t need = (size_t)bytes + 64;
+    if (cs->wbtail[0].p && need <= cs->wbtail[0].cap) return FDBCS_OK;
+    if (int rc = sync_all(cs)) return rc;
+    for (int k = 0; k < kNumWork; k++) {
+        if (int rc = cs->wbtail[k].ensure(std::max<size_t>(need, 1 << 16))) return rc;
+        cs->work[k].btail = (uint8_t*)cs->wbtail[k].p;
+    }
     return FDBCS_OK;
 }
 
@@ -426,6 +454,8 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(crb, 4 * (E + 1));
     TAKE(cwe, 4 * (E + 1));
     TAKE(wends, 8 * (2 * W + 1));
+    TAKE(wkeys, sizeof(DKey) * (2 * W + 1));
+    TAKE(segk, sizeof(DKey) * (2 * W + 2));
     TAKE(wbpos, 4 * W);
     TAKE(wlead, 4 * (W + 1));
     TAKE(wtxn, 4 * (W + 1));
@@ -472,6 +502,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     }
     }
     cs->edge_cap = edge_cap;
+    cs->prev_segs = false;  // the last batch's segments were in the old arrays (and are merged: synced)
     cs->ws_T = T;
     cs->ws_R = R;
     cs->ws_W = W;
@@ -531,17 +562,17 @@ Hist delta_of(fdbcs_conflict_set* cs, int k) {
 MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     MaxLevels m;
     m.lvl[0] = (int64_t*)cs->dver[k].p;
-    for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->dlvl[L].p;
+    for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->dlvl[k][L].p;
     m.keys = (const ulonglong2*)cs->dkey[k].p;
-    carve_index(m, (ulonglong2*)cs->dlvl[0].p, cs->delta_cap);
-    m.edir = (uint64_t*)cs->edir.p;
-    m.edir_epoch = cs->edir.p ? cs->ddir_epoch : 0;
+    carve_index(m, (ulonglong2*)cs->dlvl[k][0].p, cs->delta_cap);
+    m.edir = (uint64_t*)cs->edir[k].p;
+    m.edir_epoch = cs->edir[k].p ? cs->ddir_epoch[k] : 0;
     return m;
 }
 
 // Read the exact history size/tail usage back (synchronizes the stream).
 int sync_sizes(fdbcs_conflict_set* cs) {
-    if (int rc = flush_pending(cs)) return rc;
+    if (int rc = sync_all(cs)) return rc;  // both halves of stage B
     Scalars s;
     HIPOK(hipMemcpyAsync(&s, cs->scal.p, sizeof(s), hipMemcpyDeviceToHost, cs->stream));
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -607,9 +638,12 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
         for (int k = 0; k < 5; k++) *c64[k] = (int64_t*)cs->cws[k].p;
         w.c_exact = (uint8_t*)cs->cws[5].p;
     }
-    if ((rc = alloc_levels(cs->dlvl, cap, &cs->dlvl3_n))) return rc;
+    for (int k = 0; k < 2; k++)
+        if ((rc = alloc_levels(cs->dlvl[k], cap, &cs->dlvl3_n))) return rc;
     cs->delta_cap = cap;
-    launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->nd,
+    cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;  // the current delta's levels are rebuilt, its directory not
+    cs->prev_segs = false;                      // (sync_sizes drained every stream)
+    launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->ndb[cs->dcur],
                     cs->dlvl3_n, std::max<int64_t>(cs->nd_ub, 1));
     HIPOK(take_launch_error());
     HIPOK(hipStreamSynchronize(cs->stream));
@@ -970,8 +1004,10 @@ int flush_pending(fdbcs_conflict_set* cs) {
     cs->pending_batch = nullptr;
     int rc = FDBCS_OK;
     if (cs->pending_b.replay(cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
+    if (cs->pending_y.replay(cs->pending_ys) != hipSuccess) rc = FDBCS_E_DEVICE;
     cs->b_issued.fetch_add(1, std::memory_order_release);
     cs->pending_b.clear();
+    cs->pending_y.clear();
     return rc;
 }
 
@@ -1027,6 +1063,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     static std::once_flag attr_once;
     std::call_once(attr_once, init_kernel_attributes);
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&cs->ystream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->cstream, hipStreamNonBlocking) == hipSuccess &&
@@ -1034,7 +1071,9 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     for (int k = 0; k < kNumWork && ok; k++)
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_c[k], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&cs->ev_b[k], hipEventDisableTiming) == hipSuccess;
+             hipEventCreateWithFlags(&cs->ev_b[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&cs->ev_res[k], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&cs->ev_xfree[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fdbcs_destroy_conflict_set(cs);
         return FDBCS_E_DEVICE;
@@ -1043,14 +1082,15 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = cs->quant.ensure(2 * sizeof(SplitKey) * kQuant);
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
-    if (!rc && cs->directory) {  // zeroed: epoch 0 entries are never trusted
-        rc = cs->edir.ensure(8 * ((size_t)kDirSlots + 1));
-        if (!rc && hipMemsetAsync(cs->edir.p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream) != hipSuccess)
+    for (int k = 0; k < 2 && !rc && cs->directory; k++) {  // zeroed: epoch 0 entries are never trusted
+        rc = cs->edir[k].ensure(8 * ((size_t)kDirSlots + 1));
+        if (!rc && hipMemsetAsync(cs->edir[k].p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream) != hipSuccess)
             rc = FDBCS_E_DEVICE;
     }
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
     if (!rc) rc = ensure_delta(cs, 1 << 14);
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
+    if (!rc) rc = ensure_btail(cs, 0);
     if (!rc && cs->trace) rc = cs->trace_buf.ensure(8 * kTrSlots);
     if (rc) {
         fdbcs_destroy_conflict_set(cs);
@@ -1069,6 +1109,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (cs->cstream) (void)hipStreamSynchronize(cs->cstream);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
     if (cs->stream) (void)hipStreamSynchronize(cs->stream);
+    if (cs->ystream) (void)hipStreamSynchronize(cs->ystream);
     for (int k = 0; k < 2; k++) {
         cs->hkey[k].release();
         cs->hlt[k].release();
@@ -1081,11 +1122,13 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->htail[1].release();
     for (auto& l : cs->lvl) l.release();
     cs->dir.release();
-    cs->edir.release();
-    for (auto& l : cs->dlvl) l.release();
+    for (auto& e : cs->edir) e.release();
+    for (auto& set : cs->dlvl)
+        for (auto& l : set) l.release();
     for (auto& x : cs->cws) x.release();
     for (auto& set : cs->ws)
         for (auto& x : set) x.release();
+    for (auto& x : cs->wbtail) x.release();
     cs->scal.release();
     cs->quant.release();
     cs->trace_buf.release();
@@ -1105,12 +1148,15 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         if (cs->ev_a[k]) (void)hipEventDestroy(cs->ev_a[k]);
         if (cs->ev_c[k]) (void)hipEventDestroy(cs->ev_c[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
+        if (cs->ev_res[k]) (void)hipEventDestroy(cs->ev_res[k]);
+        if (cs->ev_xfree[k]) (void)hipEventDestroy(cs->ev_xfree[k]);
     }
     if (cs->ustream) (void)hipStreamDestroy(cs->ustream);
     if (cs->cstream) (void)hipStreamDestroy(cs->cstream);
     if (cs->ev_cmp) (void)hipEventDestroy(cs->ev_cmp);
     if (cs->astream) (void)hipStreamDestroy(cs->astream);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
+    if (cs->ystream) (void)hipStreamDestroy(cs->ystream);
     delete cs;
 }
 
@@ -1123,7 +1169,8 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = version;
     cs->max_written = version;
-    cs->ddir_epoch = 0;
+    cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;
+    cs->prev_segs = false;
     cs->n_ub = 0;
     cs->nd_ub = 0;
     cs->tail_ub = 0;
@@ -1852,15 +1899,16 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const int64_t T = b->T(), R = b->R(), W = b->W();
     int rc;
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
+    if ((rc = ensure_btail(cs, (int64_t)b->tail_size()))) return rc;
     if ((rc = ensure_delta(cs, cs->nd_ub + 2 * W + 1))) return rc;
     if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + tail_add + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
-    if (cs->ddir_counter == UINT32_MAX && cs->edir.p) {
+    if (cs->ddir_counter == UINT32_MAX && cs->edir[0].p) {
         // the delta directory's 32-bit epoch tag is about to wrap: clear every entry (once per 2^32
         // batches) so that no entry left by an old fill can carry the reused epoch value
         if ((rc = sync_all(cs))) return rc;
-        HIPOK(hipMemsetAsync(cs->edir.p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream));
+        for (int k = 0; k < 2; k++) HIPOK(hipMemsetAsync(cs->edir[k].p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream));
         HIPOK(hipStreamSynchronize(cs->stream));
         cs->ddir_counter = 0;
     }
@@ -1928,15 +1976,17 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     LaunchList& la = cs->rec_a;
     LaunchList& lb = cs->rec_b;
     LaunchList& lc = cs->rec_c;
+    LaunchList& ly = cs->rec_y;
     la.clear();
     lb.clear();
     lc.clear();
+    ly.clear();
     // per-kernel events: every kernel at level 3, the kernel fdbcs_set_timed_kernel named at level 1
     // (sampled batches)
     sl->prof_next = 0;
     sl->prof_spans.clear();
     const bool kprof = timing == 3 || (timing == 1 && sampled && cs->timed_func);
-    for (LaunchList* L : {&la, &lb, &lc}) {
+    for (LaunchList* L : {&la, &lb, &lc, &ly}) {
         L->prof = kprof ? &sl->prof : nullptr;
         L->timed_func = timing == 3 ? nullptr : cs->timed_func;
     }
@@ -1965,6 +2015,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // flight included).
     const bool ws_busy = cs->wused[wp] && (threaded || hipEventQuery(cs->ev_b[wp]) != hipSuccess);
     if (ws_busy && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
+    // and the check after that batch may still read its union segments and their tails
+    if (cs->xfree_rec[wp] && sa != s && (threaded || hipEventQuery(cs->ev_xfree[wp]) != hipSuccess))
+        fdb_event(LaunchList::kSyncWait, cs->ev_xfree[wp], sa);
+    cs->xfree_rec[wp] = false;
     cs->wused[wp] = true;
     // stage A reads the batch: wait for the upload stream
     if (own_upload || (was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess))
@@ -1975,8 +2029,23 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const bool long_keys = cs->long_probe && b->max_len > 24;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
+    // Stage B in two halves (fdbcs_conflict_set::ystream): X = check, resolution, D.Combine on
+    // `stream`; Y = merge, compaction / GC, epilogue on `ystream`.  Unless the previous batch
+    // compacted, this batch's check reads the delta before the previous batch's merge (buffer
+    // dsrc ^ 1, complete once the batch before it finished Y) plus the previous batch's union
+    // segments at its `now` (PrevSegs): the same history, so the check need not wait for that merge.
+    const bool pipe = !(timing == 2 || cs->serial || cs->check_version != 6);
+    hipStream_t ys = pipe ? cs->ystream : s;
+    const bool use_prev = pipe && cs->prev_segs;
+    const int dchk = use_prev ? dsrc ^ 1 : dsrc;
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
-    const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->nd, kHole};
+    const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->ndb[dsrc], kHole};
+    const Tier cdelta{delta_of(cs, dchk), dlevels_of(cs, dchk), &sc->ndb[dchk], kHole};  // what the check reads
+    PrevSegs ps{};
+    if (use_prev) {
+        const Work& pw = cs->work[cs->prev_wp];
+        ps = PrevSegs{pw.segk, pw.btail, &pw.bsc->n_segments, cs->prev_now};
+    }
     uint8_t* htail = (uint8_t*)cs->htail[cs->tcur].p;
 
     w.trace = cs->trace ? (unsigned long long*)cs->trace_buf.p : nullptr;
@@ -2026,18 +2095,28 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
-    // ---- record stage B: D.CheckRead against the history the previous batch left, then batch order
+    // ---- record stage B, half X: D.CheckRead, then batch order
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
+    if (pipe && cs->last_wp >= 0) {
+        // the delta the check reads is complete: Y of the batch before the previous one (with the
+        // previous batch's segments), or of the previous batch (it compacted, or nothing pending)
+        const int wy = use_prev ? cs->prev2_wp : cs->last_wp;
+        if (wy >= 0 && (threaded || hipEventQuery(cs->ev_b[wy]) != hipSuccess)) fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
+    }
     const bool graphs = cs->stage_graphs && timing != 2;
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        launch_check_tier(s, bd, w, delta, false, htail, long_keys, !cs->group_rmax);
+        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, !cs->group_rmax, ps);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-        launch_check(s, bd, w, base, delta, htail, cs->check_version);
+        launch_check(s, bd, w, base, cdelta, htail, cs->check_version, ps);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
+    }
+    if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
+        fdb_event(LaunchList::kSyncRecord, cs->ev_xfree[cs->prev_wp], s);
+        cs->xfree_rec[cs->prev_wp] = true;
     }
     mark(kPhCheck);
     if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
@@ -2054,6 +2133,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     mark(kPhIntra);
     mark(kPhCombine);
+    // ---- half Y: D.MergeWrite, compaction / GC, epilogue, after X
+    fdb_event(LaunchList::kSyncRecord, cs->ev_res[wp], s);
+    t_record = &ly;
+    if (ys != s) fdb_event(LaunchList::kSyncWait, cs->ev_res[wp], ys);
     const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
@@ -2064,14 +2147,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (cs->tail_ub > cs->tail_reclaim) compact = true;
     // D.MergeWrite into the delta tier
     char* hd = (char*)sl->pin_out.dp;
-    launch_merge(s, bd, w, delta.h, delta.m, delta_of(cs, dsrc ^ 1), htail, sc, now, cs->dlvl3_n, cs->nd_ub + 1,
-                 rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
+    launch_merge(ys, bd, w, delta.h, delta.m, delta_of(cs, dnew), dlevels_of(cs, dnew), &sc->ndb[dsrc], htail, sc, now,
+                 cs->dlvl3_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;
     const int64_t base_hint = cs->n_ub + nd_after + 1;
     if (compact) {
-        launch_compact(s, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
+        launch_compact(ys, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
                        cs->header_version, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
                        rec(kPhCompEnd, 1));
         final_base = bsrc ^ 1;
@@ -2088,7 +2171,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     mark(kPhCompact);
     if (gc) {
-        launch_gc(s, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), htail,
+        launch_gc(ys, w, hist_of(cs, final_base), hist_of(cs, final_base ^ 1), htail,
                   (uint8_t*)cs->htail[cs->tcur ^ 1].p, sc, std::max(new_oldest, cs->gc_applied), cs->header_version,
                   base_hint);
         cs->tcur ^= 1;
@@ -2101,18 +2184,18 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // the epilogue that rebuilds the delta tier's index also fills its directory under a new epoch
     // (a compaction leaves none).  The epoch tag is 32 bits: before it wraps, every entry is
     // cleared (ensure_delta_directory), so a slot an old fill left behind is never trusted.
-    if (compact || !cs->edir.p) {
-        cs->ddir_epoch = 0;
+    if (compact || !cs->edir[dnew].p) {
+        cs->ddir_epoch[dnew] = 0;
     } else {
-        cs->ddir_epoch = ++cs->ddir_counter;
+        cs->ddir_epoch[dnew] = ++cs->ddir_counter;
     }
-    launch_epilogue(s, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
+    launch_epilogue(ys, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
                     gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
-                    compact ? base_hint : nd_after + 1);
-    fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], s);
-    fdb_event(LaunchList::kSyncRecord, sl->ev_free, s);
+                    compact ? base_hint : nd_after + 1, &sc->ndb[dnew]);
+    fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], ys);
+    fdb_event(LaunchList::kSyncRecord, sl->ev_free, ys);
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
-        fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, s);
+        fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, ys);
         cs->cmp_recorded = true;
     }
     sl->free_recorded = true;
@@ -2134,11 +2217,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         worker_start_job(cs);
         if (prev) {
             cs->pending_batch = nullptr;
-            const hipError_t e = cs->pending_b.replay(s);
+            hipError_t e = cs->pending_b.replay(s);
+            const hipError_t e2 = cs->pending_y.replay(cs->pending_ys);
             cs->b_issued.fetch_add(1, std::memory_order_release);
-            if (e != hipSuccess) return FDBCS_E_DEVICE;
+            if (e != hipSuccess || e2 != hipSuccess) return FDBCS_E_DEVICE;
         }
         std::swap(cs->pending_b, lb);
+        std::swap(cs->pending_y, ly);
+        cs->pending_ys = ys;
         cs->b_recorded++;
         cs->pending_batch = b;
     } else if (flush_pending(cs)) {
@@ -2147,16 +2233,24 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if ((rc = launch_stage(cs, la, sa))) return rc;
         if (split && (rc = launch_stage(cs, lc, cs->cstream))) return rc;
         if ((rc = launch_stage(cs, lb, s))) return rc;
+        if ((rc = launch_stage(cs, ly, ys))) return rc;
     } else {
         HIPOK(la.replay(sa));
         if (split) HIPOK(lc.replay(cs->cstream));
         HIPOK(lb.replay(s));
+        HIPOK(ly.replay(ys));
     }
     HIPOK(take_launch_error());
     cs->stats.host_ms_submit += host_ms_since(t_sub);
     cs->stats.graph_launches = cs->graph_launches;
     cs->cur = final_base;
     cs->dcur = dnew;
+    // the next batch's check: this batch's segments stand in for its merge unless it compacted
+    cs->prev_segs = pipe && !compact;
+    cs->prev2_wp = cs->last_wp;
+    cs->last_wp = wp;
+    cs->prev_wp = wp;
+    cs->prev_now = now;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
     if (W) cs->max_written = std::max(cs->max_written, now);
     if (compact) {
@@ -2415,7 +2509,7 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     Work& w = cs->work[cs->wpar];
     Scalars* sc = (Scalars*)cs->scal.p;
     const Tier base{hist_of(cs, cs->cur), levels_of(cs, cs->cur), &sc->n, cs->header_version};
-    const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->nd, kHole};
+    const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->ndb[cs->dcur], kHole};
     if (which >= 1) {  // the sort kernels
         if (!cs->quant_valid) return FDBCS_E_STATE;  // warm splitters only: detect a batch first
         HIPOK(debug_time_sort(cs->stream, b->bd, w, (SplitKey*)cs->quant.p + cs->qcur * kQuant, cs->bucket_target,

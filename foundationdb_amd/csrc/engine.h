@@ -80,6 +80,9 @@ struct Scalars {
     int64_t intra_edges;   // copied from BatchScalars::n_edges (host view only; overflow -> -1)
     int32_t sort_big;      // copied from BatchScalars::sort_big (host view only)
     int32_t sort_pad;
+    int64_t ndb[2];        // delta boundaries held by delta buffer k (read checks and merges address
+                           // the buffer they use: the next batch's check reads the buffer before
+                           // this batch's merge while the merge writes the other one)
 };
 
 // Device scalars of one batch workspace (two workspaces alternate, so batch i+1's history-
@@ -91,6 +94,7 @@ struct BatchScalars {
     int32_t debug_error;   // FDBCS_VALIDATE: invariant violated; bit 1: scan look-back timed out
     int32_t ovf_n;         // sort: endpoints past their bucket's slab (reset by the epilogue)
     int32_t sort_big;      // sort: buckets past the slab, sorted by the workgroup path (reset by the epilogue)
+    int64_t n_segments;    // union segments of committed writes (D.Combine, k_resolve)
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -175,6 +179,10 @@ struct Work {
     int32_t* crb;          // [E+1] read-begins before each position
     int32_t* cwe;          // [E+1] write-ends before each position
     int2* wends;           // [2W] write endpoints in sorted order: (position, 2 owner + is-end; -1 empty write)
+    DKey* wkeys;           // [2W] their keys (tails in the batch's tail region)
+    DKey* segk;            // [2W] union segment j: begin key 2j, end key 2j + 1 (D.Combine)
+    uint8_t* btail;        // [btail_cap] copy of the batch's tail region (k_sort_partition): the next
+                           // batch's read check reads segk's tails here, after the batch is waited
     int32_t* wbpos;        // [W] positions of write-begins in order
     int32_t* rbpos;        // [R] positions of read-begins in order
     int32_t* eoff;         // [R+1] first edge slot of each read
@@ -306,6 +314,15 @@ struct Tier {
     const int64_t* n;  // device size
     int64_t hdr;       // version below the first boundary (kHole for the delta)
 };
+// The previous batch's union segments (its committed writes' union, at version `version`), for
+// a read check that runs before that batch's merge into the delta tier (stage B's merge half runs
+// on its own stream, beside the next batch's check).  n == nullptr: none.
+struct PrevSegs {
+    const DKey* segk;     // begin / end keys of segment j at 2j / 2j + 1
+    const uint8_t* tail;  // their tails (the previous batch's workspace copy)
+    const int64_t* n;     // segments
+    int64_t version;      // the previous batch's `now`
+};
 // Per batch, two stages on two streams:
 //   A (history-independent): launch_sort (D.Sort + positions), launch_edges;
 //   B (reads/writes the history, in batch order): launch_check, launch_resolve (+ D.Combine),
@@ -322,12 +339,13 @@ int sort_bucket_count(int64_t E, int target, int slab_buckets);
 // D.CheckRead against the history the previous batch left.
 // check_version: 6 = base and delta lookups in separate waves (default), 1 = in one wave.
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, int check_version = 6);
+                  const uint8_t* htail, int check_version = 6, const PrevSegs& ps = PrevSegs{});
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
 // delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
 // long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys = false, bool lead_rmax = false);
+                       const uint8_t* htail, bool long_keys = false, bool lead_rmax = false,
+                       const PrevSegs& ps = PrevSegs{});
 // Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
 // k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,
@@ -340,9 +358,11 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
 // Union segments of the batch into the delta tier (src -> dst), new boundaries at `now`.
 // `srcm` are the source tier's levels: its key index is searched, its top level reset for the
 // epilogue's rebuild.
+// nd_src: the source buffer's size; dstm: the destination's levels (top level reset for the epilogue).
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
-                  const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end, bool long_keys = false);
+                  const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
+                  int64_t now, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end,
+                  bool long_keys = false);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
@@ -369,8 +389,9 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 // the tier that changed (the base after a compaction, else the delta).  k_resolve already wrote the
 // verdict bytes into the host-mapped result; the epilogue publishes the scalars after them and
 // then the completion flag (the host waits for *flag == seq instead of an event).
+// nd_out: the size word of the delta buffer the batch leaves current (Scalars::ndb).
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
-                     uint32_t seq, int64_t grid_hint_n);
+                     uint32_t seq, int64_t grid_hint_n, int64_t* nd_out);
 
 }  // namespace fdbcs

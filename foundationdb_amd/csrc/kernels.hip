@@ -585,6 +585,34 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
     return range_max(m, ub - 1, j, snap) > snap;
 }
 
+// Does the read [kb, ke) (degenerate: [kb, kb)) meet a union segment of the previous batch, i.e.
+// would the merge of that batch (SkipList.cpp:899-924: [B, E) set to its `now`, E keeping its old
+// version) put a boundary the read counts at `now`?  Segments are disjoint and sorted, so the last
+// one whose begin lies below the read's end decides (below its begin for a degenerate read, which
+// looks at the greatest boundary < b): it meets the read iff its end lies past the read's begin (at
+// or past it for a degenerate read).  The kArity lanes of one group call this with the same read
+// (ballots and shuffles stay inside the group): a kArity-ary search over the U begin keys.
+__device__ __forceinline__ bool prev_seg_hit(const PrevSegs& ps, int64_t U, const DKey& kb, const DKey& ke,
+                                             bool degenerate, const uint8_t* qtail) {
+    const DKey& target = degenerate ? kb : ke;
+    const int lane = threadIdx.x & 63;
+    const int gl = lane & (kArity - 1), gbase = lane & ~(kArity - 1);
+    int64_t lo = 0, hi = U;  // begins below the target: all of [0, lo), none of [hi, U)
+    while (lo < hi) {
+        const int64_t idx = lo + ((hi - lo) * (gl + 1)) / (kArity + 1);
+        const bool below = dkey_cmp(ps.segk[2 * idx], ps.tail, target, qtail) < 0;
+        const uint32_t m = (uint32_t)(__ballot(below) >> gbase) & ((1u << kArity) - 1);
+        const int c = __popc(m);  // the probes below form a prefix (begins ascend with idx)
+        const int64_t nlo = c > 0 ? __shfl(idx, gbase + c - 1, 64) + 1 : lo;
+        const int64_t nhi = c < kArity ? __shfl(idx, gbase + c, 64) : hi;
+        lo = nlo;
+        hi = nhi;
+    }
+    if (lo == 0) return false;
+    const int cmp = dkey_cmp(ps.segk[2 * lo - 1], ps.tail, kb, qtail);  // end of segment lo - 1 vs b
+    return degenerate ? cmp >= 0 : cmp > 0;
+}
+
 // kArity lanes per lookup, four lookups per read range (SkipList.cpp:426-458 + CheckMax :619-706,
 // as the step-function rule of SURVEY A.2): lane groups 0/1 of a read locate its begin/end key in
 // the base tier, groups 2/3 in the delta tier, all concurrently.  The history is the base tier
@@ -631,7 +659,8 @@ __device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, 
 // radix directory and a delta lookup descending its tree run one after the other (divergent
 // branches of one wave); here each wave runs one of them.
 __device__ __forceinline__ void check_read_tier_waves(const BatchDev& b, const Tier& base, const Tier& delta,
-                                                      const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf) {
+                                                      const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
+                                                      const PrevSegs& ps) {
     constexpr int kPerWave = 64 / (2 * kArity);               // reads per wave (16 lanes each)
     constexpr int kHalf = kBlock / 64 / 2;                    // waves per tier
     constexpr int kReadsPerBlock = kHalf * kPerWave;          // == kBlock / kReadLanes
@@ -657,6 +686,12 @@ __device__ __forceinline__ void check_read_tier_waves(const BatchDev& b, const T
     bool conf = false;
     if (live && leader && (!is_delta || n > 0))
         conf = tier_conflict(tier.h, tier.m, is_delta ? kHole : tier.hdr, lb, eq, j, degenerate, snap);
+    if (is_delta && ps.n) {  // the previous batch's union segments, not merged into the delta yet
+        const int64_t U = *ps.n;
+        bool hit = false;
+        if (live && grp == 1 && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
+        conf = conf || __shfl((int)hit, (lane + kArity) & 63, 64);
+    }
     if (leader && is_delta) sconf[local] = conf ? 1 : 0;
     __syncthreads();
     if (live && leader && !is_delta) {
@@ -713,7 +748,8 @@ __device__ __forceinline__ int64_t group_range_max(const MaxLevels& m, int64_t l
 
 template <bool LONG = false>
 __device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& tier, bool is_base, const uint8_t* htail,
-                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot, int lead_rmax) {
+                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot, int lead_rmax,
+                                                const PrevSegs& ps) {
     const int lane = threadIdx.x & 63;
     const int k = (int)(slot / kTierLanes);
     const int grp = (lane / kArity) & 1;
@@ -735,6 +771,15 @@ __device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& t
     const int eqb = __shfl((int)eq, lead, 64);
     const int64_t j = __shfl(lb, lead + kArity, 64);
     bool conf = false;
+    if (!is_base && ps.n) {  // the previous batch's union segments, not merged into the delta yet
+        const int64_t U = *ps.n;
+        bool hit = false;
+        if (live && grp == 1 && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
+        if (__shfl((int)hit, lead + kArity, 64) && live && lane == lead) {
+            rconf[r] = 1;
+            hist_conf[b.rowner[r]] = 1;
+        }
+    }
     if (lead_rmax) {  // FDBCS_GROUP_RMAX=0 (A/B): the range max by the read's first lane alone
         if (active && lane == lead && tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
             rconf[r] = 1;
@@ -900,6 +945,7 @@ struct CheckReads {
     const uint8_t* htail;
     uint8_t *hist_conf, *rconf;
     unsigned long long* trace;
+    PrevSegs ps;  // FDBCS_CHECK=6 only (the one-wave variant runs after the previous batch's merge)
 };
 
 // Split check: base tier (stage A, own stream) or delta tier (stage B); two instantiations so
@@ -907,18 +953,19 @@ struct CheckReads {
 // LONG: the batch has keys over 16 bytes (long-key probes, group_lower_bound<true>).
 template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const uint8_t* htail, uint8_t* hist_conf,
-                                                       uint8_t* rconf, int lead_rmax) {
+                                                       uint8_t* rconf, int lead_rmax, PrevSegs ps) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax);
+    check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax, ps);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys, bool lead_rmax) {
+                       const uint8_t* htail, bool long_keys, bool lead_rmax, const PrevSegs& ps) {
     if (b.R == 0) return;
     const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
     auto k = is_base ? (long_keys ? k_check_tier<true, true> : k_check_tier<true, false>)
                      : (long_keys ? k_check_tier<false, true> : k_check_tier<false, false>);
-    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, lead_rmax ? 1 : 0);
+    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, lead_rmax ? 1 : 0,
+               is_base ? PrevSegs{} : ps);
 }
 
 template <bool TIER_WAVES>
@@ -926,7 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c
     if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if constexpr (TIER_WAVES)
-        check_read_tier_waves(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf);
+        check_read_tier_waves(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
     else
         check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
     __syncthreads();
@@ -934,10 +981,10 @@ __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, int check_version) {
+                  const uint8_t* htail, int check_version, const PrevSegs& ps) {
     if (b.R == 0) return;
     // four lookups per read: 6 = the base and delta lookups in separate waves, 1 = in one wave
-    CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace};
+    CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps};
     const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
     if (check_version == 6)
         fdb_launch(k_check_reads<true>, dim3(grid), dim3(kBlock), 0, s, b, c);
@@ -1039,6 +1086,7 @@ __device__ __forceinline__ int split_cmp_rest(const uint64_t (&a)[kSplitWords], 
 // read-begins | write-ends << 32, one bucket per 128-byte line: the atomics of different buckets
 // never share a line (device-scope atomics on one line serialize at the memory side).
 struct SortArgs {
+    uint8_t* btail;  // the workspace's copy of the batch tail region (see Work::btail)
     const SplitKey* quant;
     uint64_t* cnt;
     SortItem* slab;
@@ -1067,6 +1115,8 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
         if (a.trace) trace_max(a.trace, kTrPartEnd);
         return;
     }
+    if (it.len > 16u && a.btail)  // this endpoint's tail into the workspace copy (same offset)
+        for (uint32_t q = 0; q < it.len - 16u; q++) a.btail[it.tail + q] = b.tail[it.tail + q];
     // splitters below my first two words: [0, lo); equal to them: [lo, up)
     int lo = 0, hi = ns;
     while (lo < hi) {
@@ -1502,7 +1552,7 @@ int sort_bucket_count(int64_t E, int target, int slab_buckets) {
 }
 
 static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb) {
-    return SortArgs{quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
+    return SortArgs{w.btail, quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
 }
 
 void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
@@ -1629,6 +1679,7 @@ struct EdgePairScan {
     Work w;
     int32_t R, G;
     const int32_t* wowner;
+    const DKey* keys;
     __device__ void counts(int64_t g, uint32_t& slots, uint32_t& pairs, uint32_t& a) const {
         slots = pairs = a = 0;
         if (g >= R) {
@@ -1636,8 +1687,11 @@ struct EdgePairScan {
             // endpoints before its position), read by D.Combine at the end of k_resolve
             const int pb = w.pos[2 * g], pe = w.pos[2 * g + 1];
             const int code = pb < pe ? 2 * wowner[g - R] : -1;
-            w.wends[w.cwb[pb] + w.cwe[pb]] = make_int2(pb, code);
-            w.wends[w.cwb[pe] + w.cwe[pe]] = make_int2(pe, code < 0 ? -1 : code + 1);
+            const int ib = w.cwb[pb] + w.cwe[pb], ie = w.cwb[pe] + w.cwe[pe];
+            w.wends[ib] = make_int2(pb, code);
+            w.wends[ie] = make_int2(pe, code < 0 ? -1 : code + 1);
+            w.wkeys[ib] = keys[2 * g];
+            w.wkeys[ie] = keys[2 * g + 1];
         }
         if (g >= R && w.groups) {
             // write-begin index j of this write; it leads a group unless the write before it in
@@ -1770,7 +1824,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
 
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    launch_scan<2>(s, EdgePairScan{w, b.R, G, b.wowner}, nullptr, G, w.scan[kScanEdges]);
+    launch_scan<2>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
         const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
         fdb_launch(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
@@ -1885,8 +1939,14 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
         int j = soff + bex;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
-            if (bm & (1u << k)) w.seg_b[j++] = e[k].x;
-            if (em & (1u << k)) w.seg_e[j - 1] = e[k].x;
+            if (bm & (1u << k)) {
+                w.segk[2 * j] = w.wkeys[i0 + k];
+                w.seg_b[j++] = e[k].x;
+            }
+            if (em & (1u << k)) {
+                w.segk[2 * j - 1] = w.wkeys[i0 + k];
+                w.seg_e[j - 1] = e[k].x;
+            }
         }
         if (c0 == 0 && threadIdx.x == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1896,7 +1956,8 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
         nseg += stot;
         __syncthreads();  // s_wsum is rewritten by the next chunk
     }
-    if (threadIdx.x == 0) hs->n_segments = nseg;
+    if (threadIdx.x == 0) w.bsc->n_segments = nseg;
+    (void)hs;
 }
 
 // Pre-pass of the resolution, one wave per transaction across the chip (k_resolve_pre), then the
@@ -2327,7 +2388,7 @@ void init_kernel_attributes() {
 
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out, Scalars* sc) {
     if (b.T == 0) {  // no transactions, no writes: no union segments
-        fdb_launch(k_set_i64, dim3(1), dim3(64), 0, s, &sc->n_segments, (int64_t)0);
+        fdb_launch(k_set_i64, dim3(1), dim3(64), 0, s, &w.bsc->n_segments, (int64_t)0);
         return;
     }
     // one wave per transaction for the pre-pass, then the rounds in one workgroup
@@ -2368,6 +2429,7 @@ struct Epilogue {
     uint64_t* zero_bc;  // sort bucket counters [kCntStride kSortMaxBuckets] (two words of each line used)
     int32_t* zero_rank;  // cold-start sample ranks [kMaxSample + 64]
     BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
+    int64_t* nd_out;     // Scalars::ndb of the delta buffer the batch leaves current
 };
 
 // The scalars after the verdicts in the host-mapped result (word by word: a local Scalars copy
@@ -2383,6 +2445,7 @@ __device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogu
     out->intra_rounds = ep.bsc->rounds;
     out->intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
     out->sort_big = ep.bsc->sort_big;
+    out->n_segments = ep.bsc->n_segments;
     ep.bsc->debug_error = 0;
     ep.bsc->ovf_n = 0;     // the sort's overflow list and big-bucket count (this batch's sort is done)
     ep.bsc->sort_big = 0;
@@ -2433,13 +2496,13 @@ __global__ __launch_bounds__(kWG) void k_seg_prep(BatchDev b, Work w, Hist h, Ma
     __shared__ uint32_t s_base[3];
     __shared__ int s_tile;
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the history check of this batch is done with the old hierarchy: reset its top level for the
-    // epilogue's atomicMax build
+    // the destination tier's top level, reset for the epilogue's atomicMax build (its previous
+    // contents belonged to the history two batches back, which no check reads any more)
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
     if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanSegSum].counter, 1);
     __syncthreads();
     const int tile = s_tile;
-    const int U = (int)sc->n_segments;
+    const int U = (int)w.bsc->n_segments;
     const int ntiles = U > 0 ? (U + kSegPer - 1) / kSegPer : 1;
     if (tile >= ntiles) return;  // spare workgroup: nobody waits on it
     const int64_t n = *io.n_in;
@@ -2695,11 +2758,14 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 }
 
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
-                  const Hist& dst, uint8_t* htail, Scalars* sc, int64_t now, int64_t lvl3_n, int64_t grid_hint_n,
-                  hipEvent_t copy_begin, hipEvent_t copy_end, bool long_keys) {
-    const TierIO io{&sc->nd, &sc->nd_next, &sc->d_before, &sc->d_rem};
+                  const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
+                  int64_t now, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end,
+                  bool long_keys) {
+    const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
+    // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
+    // stay intact: the next batch's read check may still search them)
     fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_prep_tiles(b.W)), dim3(kWG), 0, s, b,
-               w, src, srcm, htail, sc, io, srcm.lvl[3], lvl3_n);
+               w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
     ins.b = b;
@@ -2713,7 +2779,7 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     ins.sc = sc;
     ins.now = now;
     fdb_launch((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile)), dim3(kBlock), 0,
-               s, batch_segs(w), src, dst, &sc->nd, &sc->n_segments, ins);
+               s, batch_segs(w), src, dst, nd_src, &w.bsc->n_segments, ins);
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 
@@ -3208,6 +3274,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
         } else {
             sc->nd = sc->nd_next;
         }
+        if (ep.nd_out) *ep.nd_out = sc->nd;
         sc->tail_used = ep.gc_ran ? sc->tail_gc : sc->tail_next;
         publish_scalars(sc, ep);
     }
@@ -3322,8 +3389,9 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
-                     uint32_t seq, int64_t grid_hint_n) {
-    const Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq);
+                     uint32_t seq, int64_t grid_hint_n, int64_t* nd_out) {
+    Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq);
+    ep.nd_out = nd_out;
     if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
     int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
     extra = extra > b.T ? extra : b.T;
