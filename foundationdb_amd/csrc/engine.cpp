@@ -139,6 +139,7 @@ struct fdbcs_conflict_set {
     // against the delta before batch i's merge plus batch i's union segments (PrevSegs), so it does
     // not wait for that merge: Y(i) overlaps X(i + 1).
     hipStream_t ystream = nullptr;
+    bool split_stage_b = true;          // FDBCS_SPLIT_B=0: both halves on `stream`, checks after the merge
     hipEvent_t ev_res[kNumWork] = {};   // X of the batch using workspace k is done (Y waits for it)
     hipEvent_t ev_xfree[kNumWork] = {}; // the next batch's check is done with workspace k's segments
     bool prev_segs = false;             // the last batch's segments are not merged when the next check runs
@@ -1059,6 +1060,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : 6;
+    if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     static std::once_flag attr_once;
     std::call_once(attr_once, init_kernel_attributes);
@@ -1279,6 +1281,7 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
     cs->max_written = maxv;
+    cs->prev_segs = false;
     cs->n_ub = n;
     cs->nd_ub = 0;
     cs->tail_ub = (int64_t)tail.size();
@@ -1403,6 +1406,7 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
         (void)hipStreamSynchronize(b->cs->cstream);
         (void)hipStreamSynchronize(b->cs->astream);
         (void)hipStreamSynchronize(b->cs->stream);
+        (void)hipStreamSynchronize(b->cs->ystream);
         b->cs->inflight--;
     } else if (b->state == 1) {  // uploaded, never submitted: the copy may still be in flight
         (void)hipSetDevice(b->cs->device);
@@ -2034,7 +2038,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // compacted, this batch's check reads the delta before the previous batch's merge (buffer
     // dsrc ^ 1, complete once the batch before it finished Y) plus the previous batch's union
     // segments at its `now` (PrevSegs): the same history, so the check need not wait for that merge.
-    const bool pipe = !(timing == 2 || cs->serial || cs->check_version != 6);
+    const bool pipe = cs->split_stage_b && !(timing == 2 || cs->serial || cs->check_version != 6);
     hipStream_t ys = pipe ? cs->ystream : s;
     const bool use_prev = pipe && cs->prev_segs;
     const int dchk = use_prev ? dsrc ^ 1 : dsrc;
@@ -2276,8 +2280,11 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         // the epilogue's last workgroup publishes b->seq; poll it (checking the stream for errors)
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
             if ((spin & 1023) == 1023) {
+                // the flag comes from the epilogue (stage B's Y half): done or failing once both
+                // halves are idle
                 hipError_t e = hipStreamQuery(cs->astream);
                 if (e == hipSuccess || e == hipErrorNotReady) e = hipStreamQuery(cs->stream);
+                if (e == hipSuccess) e = hipStreamQuery(cs->ystream);
                 if (e != hipSuccess && e != hipErrorNotReady) {
                     fprintf(stderr, "fdbcs: stream error while waiting: %s\n", hipGetErrorString(e));
                     return FDBCS_E_DEVICE;
