@@ -457,6 +457,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(wends, 8 * (2 * W + 1));
     TAKE(wkeys, sizeof(DKey) * (2 * W + 1));
     TAKE(segk, sizeof(DKey) * (2 * W + 2));
+    TAKE(cflag, 2 * W + 2);
     TAKE(wbpos, 4 * W);
     TAKE(wlead, 4 * (W + 1));
     TAKE(wtxn, 4 * (W + 1));

@@ -116,7 +116,7 @@ struct Segs {
 };
 
 // Scans of one batch (each owns a slice of the per-batch zeroed scan arena).
-enum ScanKind { kScanEdges, kScanSegSum, kScanCompact, kScanGc, kNumScans };
+enum ScanKind { kScanEdges, kScanSegSum, kScanCompact, kScanGc, kScanCover, kScanSegNum, kNumScans };
 
 // Device copy of one batch's packed input (tooOld transactions carry no ranges,
 // as in addTransaction, SkipList.cpp:770-790).
@@ -181,6 +181,7 @@ struct Work {
     int2* wends;           // [2W] write endpoints in sorted order: (position, 2 owner + is-end; -1 empty write)
     DKey* wkeys;           // [2W] their keys (tails in the batch's tail region)
     DKey* segk;            // [2W] union segment j: begin key 2j, end key 2j + 1 (D.Combine)
+    uint8_t* cflag;        // [2W] D.Combine across workgroups: write endpoint opens (1) / closes (2) a segment
     uint8_t* btail;        // [btail_cap] copy of the batch's tail region (k_sort_partition): the next
                            // batch's read check reads segk's tails here, after the batch is waited
     int32_t* wbpos;        // [W] positions of write-begins in order

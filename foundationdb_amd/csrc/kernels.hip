@@ -1960,6 +1960,46 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
     (void)hs;
 }
 
+// D.Combine across the pre-pass workgroups when no transaction has a candidate writer (a
+// transaction commits iff it has no history conflict and is not TooOld, so every status is known
+// from the check's flags): the coverage of committed writes over the sorted write endpoints by one
+// look-back scan, the union segments numbered by a second one chained in the same tile (k_scan2's
+// scheme), instead of one workgroup walking all 2W endpoints after the statuses.
+struct CoverScan {
+    Work w;
+    BatchDev b;
+    __device__ int delta(int64_t i) const {
+        const int2 e = w.wends[i];
+        if (e.y < 0) return 0;
+        const int t = e.y >> 1;
+        const bool committed = !w.hist_conf[t] && !(b.flags[t] & kFlagTooOld);
+        return committed ? ((e.y & 1) ? -1 : 1) : 0;
+    }
+    __device__ void load(int64_t i, uint32_t (&v)[1]) const { v[0] = (uint32_t)delta(i); }
+    __device__ void store(int64_t i, const uint32_t (&ex)[1]) const {
+        const int d = delta(i), c = (int)ex[0];  // coverage before endpoint i
+        w.cflag[i] = (d == 1 && c == 0) ? 1 : ((d == -1 && c == 1) ? 2 : 0);
+    }
+    __device__ void finish(const uint32_t (&)[1]) const {}
+};
+struct SegNumScan {
+    Work w;
+    __device__ void load(int64_t i, uint32_t (&v)[1]) const { v[0] = w.cflag[i] == 1 ? 1u : 0u; }
+    __device__ void store(int64_t i, const uint32_t (&ex)[1]) const {
+        const uint8_t f = w.cflag[i];
+        if (!f) return;
+        const int x = w.wends[i].x;
+        if (f == 1) {  // segment ex opens here
+            w.seg_b[ex[0]] = x;
+            w.segk[2 * ex[0]] = w.wkeys[i];
+        } else {       // the segment opened last (ex - 1) closes here
+            w.seg_e[ex[0] - 1] = x;
+            w.segk[2 * ex[0] - 1] = w.wkeys[i];
+        }
+    }
+    __device__ void finish(const uint32_t (&tot)[1]) const { w.bsc->n_segments = tot[0]; }
+};
+
 // Pre-pass of the resolution, one wave per transaction across the chip (k_resolve_pre), then the
 // batch-order rounds and D.Combine in one workgroup (k_resolve).  Two launches: the rounds keep the
 // status bytes, group minima and members in up to 159 KiB of LDS, and a single kernel would ask
@@ -1976,6 +2016,19 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
             w.status[t] = st;
             w.first_conf[t] = INT_MAX;
             vout[t] = verdict_byte(b, t, st);
+        }
+        // D.Combine: tiles of kScanTile write endpoints, ids in launch order
+        __shared__ uint32_t sv[1][kScanPad];
+        __shared__ uint32_t swave[1][kScanThreads / 64];
+        __shared__ uint32_t sbase[1];
+        __shared__ int s_tile;
+        if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanCover].counter, 1);
+        __syncthreads();
+        const int64_t n = 2 * (int64_t)b.W;
+        const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+        if (s_tile < ntiles) {
+            scan_tile<1>(CoverScan{w, b}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
+            scan_tile<1>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave, sbase);
         }
         if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
         return;
@@ -2062,14 +2115,11 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
     __shared__ int s_more;
     const int T = b.T;
     if (threadIdx.x == 0) trace_max(w.trace, kTrResWait);
-    if (sc->n_edges == 0 && !sc->edge_overflow) {
-        // k_resolve_pre decided every transaction: the statuses into LDS (coalesced) for D.Combine
-        for (int t = threadIdx.x; t < T; t += blockDim.x) st[t] = w.status[t];
-        if (threadIdx.x == 0) sc->rounds = 0;
-        __syncthreads();
-        if (threadIdx.x == 0) trace_max(w.trace, kTrResRounds);
-        combine_segments(w, b.W, hs, [&](int t) { return st[t] == kCommitted; });
-        if (threadIdx.x == 0) trace_max(w.trace, kTrResEnd);
+    if (sc->n_edges == 0 && !sc->edge_overflow) {  // k_resolve_pre decided everything and combined
+        if (threadIdx.x == 0) {
+            sc->rounds = 0;
+            trace_max(w.trace, kTrResEnd);
+        }
         return;
     }
     const bool use_pre = !sc->edge_overflow && !w.no_prepass;
@@ -2392,8 +2442,10 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
         return;
     }
     // one wave per transaction for the pre-pass, then the rounds in one workgroup
-    fdb_launch(k_resolve_pre, dim3((unsigned)(((int64_t)b.T * 64 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, b, w,
-               verdict_out);
+    // (at least one workgroup per D.Combine tile of the no-edge case)
+    const int64_t pre_grid = std::max<int64_t>(((int64_t)b.T * 64 + kBlock - 1) / kBlock,
+                                               (2 * (int64_t)b.W + kScanTile - 1) / kScanTile);
+    fdb_launch(k_resolve_pre, dim3((unsigned)pre_grid), dim3(kBlock), 0, s, b, w, verdict_out);
     size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
     Work wl = w;
     wl.member_lds = 0;
@@ -2930,7 +2982,8 @@ int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int6
     (void)T;
     const int64_t E = 2 * (R + W);
     (void)E;
-    return kNumScans + scan_granules(R + W, 2) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) + scan_granules(hist_cap, 2);
+    return kNumScans + scan_granules(R + W, 2) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) +
+           scan_granules(hist_cap, 2) + 2 * scan_granules(2 * W, 1);
 }
 
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
@@ -2939,7 +2992,8 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     uint64_t* a = w.scan_arena;
     (void)E;
     const int64_t gran[kNumScans] = {scan_granules(R + W, 2), 3 * seg_prep_tiles(W),
-                                     scan_granules(delta_cap + 1, 2), scan_granules(hist_cap, 2)};
+                                     scan_granules(delta_cap + 1, 2), scan_granules(hist_cap, 2),
+                                     scan_granules(2 * W, 1), scan_granules(2 * W, 1)};
     uint64_t* g = a + kNumScans;
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);
