@@ -96,10 +96,16 @@ def kernel_bytes(name: str, s: dict):
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
     if name == "k_resolve_pre":
-        return (T * (1 + 1 + 4 + 1 + 4) + X * (4 + 1 + 1 + 4) + T * 12,
-                "statuses (hist flag, tooOld flag, verdict, first conflict) or the pre-pass: edges, their writers' "
-                "flags, packed live writers, resume pointers")
+        if X > 0:
+            return (T * (1 + 1 + 4 + 1 + 4) + X * (4 + 1 + 1 + 4) + T * 12,
+                    "pre-pass: per transaction its flags and edge runs, per edge the writer and its flags, packed live "
+                    "writers, resume pointers")
+        return (T * (1 + 1 + 1 + 4 + 1) + 2 * W * (8 + 1 + 1 + 1) + U * (2 * D + 8),
+                "statuses (hist flag, tooOld flag, status, first conflict, verdict); D.Combine: per write endpoint its "
+                "record, owner's flags, segment flag; per segment 2 keys and 2 positions")
     if name == "k_resolve":
+        if X == 0:
+            return 8, "no candidate edges: the pre-pass decided and combined; one scalar"
         return (T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16 + 2 * W * 8 + U * 8,
                 "statuses, flags, offsets, edges and writer states, verdicts; D.Combine: 2W write endpoints, U segments")
     if name == "k_intra_report":
