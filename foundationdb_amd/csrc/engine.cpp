@@ -858,6 +858,7 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     b->bd.flags = (uint8_t*)(d + L.flags);
     b->bd.tail = (uint8_t*)(d + L.tail);
     b->tail_bytes = b->tail_size();
+    b->bd.tail_n = (int64_t)b->tail_bytes;
     b->state = 1;
     return FDBCS_OK;
 }
@@ -1850,6 +1851,7 @@ static int finish_route(fdbcs_batch* b) {
     b->rW = r.W;
     b->r_tail = (size_t)r.tail_bytes;
     b->tail_bytes = b->r_tail;
+    b->bd.tail_n = r.tail_bytes;
     b->bd.T = r.T;
     b->bd.R = r.R;
     b->bd.W = r.W;

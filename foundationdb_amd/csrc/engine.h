@@ -130,6 +130,7 @@ struct BatchDev {
     int32_t* wowner;     // [W]
     DKey* keys;          // [2(R+W)]
     uint8_t* tail;       // key bytes beyond 16
+    int64_t tail_n;      // bytes of `tail` in use
 };
 
 // D.Sort geometry (kernels.hip): a bucket holds kSortTarget endpoints on average and is sorted in

@@ -1087,6 +1087,7 @@ __device__ __forceinline__ int split_cmp_rest(const uint64_t (&a)[kSplitWords], 
 // never share a line (device-scope atomics on one line serialize at the memory side).
 struct SortArgs {
     uint8_t* btail;  // the workspace's copy of the batch tail region (see Work::btail)
+    int64_t btail_n; // bytes of the batch tail region
     const SplitKey* quant;
     uint64_t* cnt;
     SortItem* slab;
@@ -1115,8 +1116,12 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
         if (a.trace) trace_max(a.trace, kTrPartEnd);
         return;
     }
-    if (it.len > 16u && a.btail)  // this endpoint's tail into the workspace copy (same offset)
-        for (uint32_t q = 0; q < it.len - 16u; q++) a.btail[it.tail + q] = b.tail[it.tail + q];
+    if (a.btail) {  // the batch tail region into the workspace copy, 8-byte words, grid-strided
+        const int64_t nw = (a.btail_n + 7) / 8;
+        const uint64_t* src = (const uint64_t*)b.tail;
+        uint64_t* dst = (uint64_t*)a.btail;
+        for (int64_t q = p; q < nw; q += (int64_t)gridDim.x * blockDim.x) dst[q] = src[q];
+    }
     // splitters below my first two words: [0, lo); equal to them: [lo, up)
     int lo = 0, hi = ns;
     while (lo < hi) {
@@ -1551,8 +1556,8 @@ int sort_bucket_count(int64_t E, int target, int slab_buckets) {
     return (int)std::max<int64_t>(1, std::min(nb, cap));
 }
 
-static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb) {
-    return SortArgs{w.btail, quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
+static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb, int64_t btail_n) {
+    return SortArgs{w.btail, btail_n, quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
 }
 
 void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
@@ -1572,7 +1577,7 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
         fdb_launch(k_quant_cold, dim3(1), dim3(kWG), 0, s, b, (const SortItem*)w.samples, (const int32_t*)w.srank,
                    c.S, quant);
     }
-    const SortArgs a = sort_args(w, quant, nb);
+    const SortArgs a = sort_args(w, quant, nb, b.tail_n);
     fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
     SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, validate ? w.items : nullptr,
               quant_out, w.big, w.big_p};
@@ -1595,7 +1600,7 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
     hipEvent_t e0, e1;
     hipError_t err;
     if ((err = hipEventCreate(&e0)) || (err = hipEventCreate(&e1))) return err;
-    const SortArgs a = sort_args(w, quant, nb);
+    const SortArgs a = sort_args(w, quant, nb, b.tail_n);
     SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, nullptr, nullptr, w.big, w.big_p};
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     double total = 0;
