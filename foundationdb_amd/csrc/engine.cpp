@@ -147,6 +147,7 @@ struct fdbcs_conflict_set {
     int64_t prev_now = 0;
     int last_wp = -1, prev2_wp = -1;    // workspaces of the last two batches submitted (their Y events)
     bool xfree_rec[kNumWork] = {};      // ev_xfree[k] recorded since workspace k's last use
+    bool y_async[kNumWork] = {};        // Y of workspace k's last batch ran on ystream (not in `stream` order)
     bool wused[kNumWork] = {};
     int wpar = 0;                   // workspace of the next batch
     int timing = 0;       // 0: no events; 1: the copy kernels; 2: every phase (fdbcs_set_timing)
@@ -2021,7 +2022,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // never answered by a stale or never-recorded event (a timing-level change with batches in
     // flight included).
     const bool ws_busy = cs->wused[wp] && (threaded || hipEventQuery(cs->ev_b[wp]) != hipSuccess);
-    if (ws_busy && sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
+    if (ws_busy && (sa != s || cs->y_async[wp])) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     // and the check after that batch may still read its union segments and their tails
     if (cs->xfree_rec[wp] && sa != s && (threaded || hipEventQuery(cs->ev_xfree[wp]) != hipSuccess))
         fdb_event(LaunchList::kSyncWait, cs->ev_xfree[wp], sa);
@@ -2105,11 +2106,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ---- record stage B, half X: D.CheckRead, then batch order
     t_record = &lb;
     if (sa == s || !was_uploaded || hipEventQuery(sl->ev_up) != hipSuccess) fdb_event(LaunchList::kSyncWait, sl->ev_up, s);
-    if (pipe && cs->last_wp >= 0) {
+    {
         // the delta the check reads is complete: Y of the batch before the previous one (with the
-        // previous batch's segments), or of the previous batch (it compacted, or nothing pending)
+        // previous batch's segments), or of the previous batch (it compacted, or nothing pending).
+        // Only a Y on ystream needs the event (a timing-level change may switch layouts mid-flight).
         const int wy = use_prev ? cs->prev2_wp : cs->last_wp;
-        if (wy >= 0 && (threaded || hipEventQuery(cs->ev_b[wy]) != hipSuccess)) fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
+        if (wy >= 0 && cs->y_async[wy] && (threaded || hipEventQuery(cs->ev_b[wy]) != hipSuccess))
+            fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
     }
     const bool graphs = cs->stage_graphs && timing != 2;
     if (split) {
@@ -2256,6 +2259,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->prev_segs = pipe && !compact;
     cs->prev2_wp = cs->last_wp;
     cs->last_wp = wp;
+    cs->y_async[wp] = ys != s;
     cs->prev_wp = wp;
     cs->prev_now = now;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
