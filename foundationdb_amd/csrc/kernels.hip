@@ -1851,119 +1851,14 @@ __device__ __forceinline__ uint8_t verdict_byte(const BatchDev& b, int t, uint8_
     return status == kCommitted ? 2 : 0;     // TransactionCommitted : TransactionConflict
 }
 
-// D.Combine (combineWriteConflictRanges, SkipList.cpp:926-939), run by workgroup 0 of k_resolve
-// once every status is final: +1 at the begin and -1 at the end of every committed non-empty write,
-// summed over the write endpoints in sorted order (wends, from stage A), gives the coverage before
-// each; a union segment [key(begin), key(end)) starts where coverage leaves 0 and ends where it
-// returns.  Positions that are not write endpoints add nothing, so this equals the coverage over
-// all E positions.  `committed(t)` reads the final status of transaction t.
+// D.Combine (combineWriteConflictRanges, SkipList.cpp:926-939): +1 at the begin and -1 at the end
+// of every committed non-empty write, summed over the write endpoints in sorted order (wends, from
+// stage A), gives the coverage before each; a union segment [key(begin), key(end)) starts where
+// coverage leaves 0 and ends where it returns (CoverScan / SegNumScan below).
 __global__ void k_set_i64(int64_t* p, int64_t v) {
     if (threadIdx.x == 0) *p = v;
 }
 
-template <class Committed>
-__device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed committed) {
-    // each lane owns kPer consecutive write endpoints (one 128-byte run, vector loads), a wave
-    // 64 kPer, the workgroup kPer * blockDim.x per chunk: coverage and segment counts are summed
-    // along the lane's run in registers, so a chunk costs two wave scans (coverage, then segment
-    // begins) plus two cross-wave LDS steps instead of one shuffle scan per slot
-    __shared__ int32_t s_wsum[2][kWG / 64];
-    constexpr int kPer = 24;  // one chunk covers 2W <= 24576 (C2: 20000 write endpoints)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int n = 2 * W;
-    auto wave_excl = [&](int x, int& total) {
-        int v = x;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(v, o, 64);
-            if (lane >= o) v += y;
-        }
-        total = __shfl(v, 63, 64);
-        return v - x;
-    };
-    int32_t cov = 0, nseg = 0;  // carried over chunks (uniform)
-    for (int c0 = 0; c0 < n; c0 += kPer * (int)blockDim.x) {
-        const int i0 = c0 + (wid * 64 + lane) * kPer;
-        int2 e[kPer];
-        if (i0 + kPer <= n) {
-            const int4* src = (const int4*)(w.wends + i0);
-#pragma unroll
-            for (int k = 0; k < kPer / 2; k++) {
-                const int4 v = src[k];
-                e[2 * k] = make_int2(v.x, v.y);
-                e[2 * k + 1] = make_int2(v.z, v.w);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kPer; k++) e[k] = i0 + k < n ? w.wends[i0 + k] : make_int2(0, -1);
-        }
-        // +1 at a committed write's begin, -1 at its end; coverage before each endpoint
-        int d[kPer], lsum = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            d[k] = e[k].y >= 0 && committed(e[k].y >> 1) ? ((e[k].y & 1) ? -1 : 1) : 0;
-            lsum += d[k];
-        }
-        if (c0 == 0 && threadIdx.x == 0) trace_max(w.trace, kTrCmbLoad);
-        int wtot;
-        const int lex = wave_excl(lsum, wtot);
-        if (lane == 0) s_wsum[0][wid] = wtot;
-        __syncthreads();
-        int off = cov, tot = 0;
-        for (int q = 0; q < nw; q++) {
-            const int v = s_wsum[0][q];
-            if (q < wid) off += v;
-            tot += v;
-        }
-        if (c0 == 0 && threadIdx.x == 0) trace_max(w.trace, kTrCmbScan1);
-        // a segment begins where coverage leaves 0 and ends where it returns to 0
-        uint32_t bm = 0, em = 0;
-        int c = off + lex, nb = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            if (d[k] == 1 && c == 0) {
-                bm |= 1u << k;
-                nb++;
-            }
-            if (d[k] == -1 && c == 1) em |= 1u << k;
-            c += d[k];
-        }
-        int btot;
-        const int bex = wave_excl(nb, btot);
-        if (lane == 0) s_wsum[1][wid] = btot;
-        __syncthreads();
-        int soff = nseg, stot = 0;
-        for (int q = 0; q < nw; q++) {
-            const int v = s_wsum[1][q];
-            if (q < wid) soff += v;
-            stot += v;
-        }
-        // segment j's begin and end: the lane's begins are numbered in order; an end closes the
-        // segment opened last (begins before it in the chunk, plus those before the chunk)
-        if (c0 == 0 && threadIdx.x == 0) trace_max(w.trace, kTrCmbScan2);
-        int j = soff + bex;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            if (bm & (1u << k)) {
-                w.segk[2 * j] = w.wkeys[i0 + k];
-                w.seg_b[j++] = e[k].x;
-            }
-            if (em & (1u << k)) {
-                w.segk[2 * j - 1] = w.wkeys[i0 + k];
-                w.seg_e[j - 1] = e[k].x;
-            }
-        }
-        if (c0 == 0 && threadIdx.x == 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            trace_max(w.trace, kTrCmbStore);
-        }
-        cov += tot;
-        nseg += stot;
-        __syncthreads();  // s_wsum is rewritten by the next chunk
-    }
-    if (threadIdx.x == 0) w.bsc->n_segments = nseg;
-    (void)hs;
-}
 
 // D.Combine across the pre-pass workgroups when no transaction has a candidate writer (a
 // transaction commits iff it has no history conflict and is not TooOld, so every status is known
@@ -1973,11 +1868,13 @@ __device__ void combine_segments(const Work& w, int W, Scalars* hs, Committed co
 struct CoverScan {
     Work w;
     BatchDev b;
+    int use_status;  // 1: the resolution's final statuses (candidate edges existed); 0: the check's flags
     __device__ int delta(int64_t i) const {
         const int2 e = w.wends[i];
         if (e.y < 0) return 0;
         const int t = e.y >> 1;
-        const bool committed = !w.hist_conf[t] && !(b.flags[t] & kFlagTooOld);
+        const bool committed = use_status ? w.status[t] == kCommitted
+                                          : (!w.hist_conf[t] && !(b.flags[t] & kFlagTooOld));
         return committed ? ((e.y & 1) ? -1 : 1) : 0;
     }
     __device__ void load(int64_t i, uint32_t (&v)[1]) const { v[0] = (uint32_t)delta(i); }
@@ -2032,7 +1929,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
         const int64_t n = 2 * (int64_t)b.W;
         const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
         if (s_tile < ntiles) {
-            scan_tile<1>(CoverScan{w, b}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
+            scan_tile<1>(CoverScan{w, b, 0}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
             scan_tile<1>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave, sbase);
         }
         if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
@@ -2411,8 +2308,25 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         vout[t] = verdict_byte(b, t, st[t]);
     }
     if (threadIdx.x == 0) sc->rounds = rounds;
-    combine_segments(w, b.W, hs, [&](int t) { return st[t] == kCommitted; });
+    (void)hs;  // D.Combine: k_combine, across workgroups, after this launch
     if (threadIdx.x == 0) trace_max(w.trace, kTrResEnd);
+}
+
+// D.Combine after batch-order rounds (candidate edges existed): the same two chained look-back
+// scans as the no-edge case, over the final statuses; exits at once when k_resolve_pre combined.
+__global__ __launch_bounds__(kScanThreads) void k_combine(BatchDev b, Work w) {
+    __shared__ uint32_t sv[1][kScanPad];
+    __shared__ uint32_t swave[1][kScanThreads / 64];
+    __shared__ uint32_t sbase[1];
+    __shared__ int s_tile;
+    if (w.bsc->n_edges == 0 && !w.bsc->edge_overflow) return;
+    if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanCover].counter, 1);
+    __syncthreads();
+    const int64_t n = 2 * (int64_t)b.W;
+    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+    if (s_tile >= ntiles) return;
+    scan_tile<1>(CoverScan{w, b, 1}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
+    scan_tile<1>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave, sbase);
 }
 
 // First conflicting read index of intra-batch aborts that report conflicting keys
@@ -2460,6 +2374,8 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
         lds += 8 * (size_t)wl.member_lds;
     }
     fdb_launch(k_resolve, dim3(1), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out, sc);
+    fdb_launch(k_combine, dim3((unsigned)std::max<int64_t>(1, (2 * (int64_t)b.W + kScanTile - 1) / kScanTile)),
+               dim3(kScanThreads), 0, s, b, w);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
 

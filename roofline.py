@@ -106,8 +106,13 @@ def kernel_bytes(name: str, s: dict):
     if name == "k_resolve":
         if X == 0:
             return 8, "no candidate edges: the pre-pass decided and combined; one scalar"
-        return (T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16 + 2 * W * 8 + U * 8,
-                "statuses, flags, offsets, edges and writer states, verdicts; D.Combine: 2W write endpoints, U segments")
+        return (T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16,
+                "statuses, flags, resume pointers, edges and writer states, write-group members, verdicts")
+    if name == "k_combine":
+        if X == 0:
+            return 8, "no candidate edges: the pre-pass combined; one scalar"
+        return (2 * W * (8 + 1 + 1 + 1) + U * (2 * D + 8),
+                "D.Combine: per write endpoint its record, owner's status, segment flag; per segment 2 keys and 2 positions")
     if name == "k_intra_report":
         return R * 12, "per read: edge range, first conflict"
     if name.startswith("k_seg_prep"):
