@@ -2,20 +2,20 @@
 //
 // The reference resolves a batch on one CPU thread with a versioned skip list
 // (fdbserver/SkipList.cpp:844-890).  Here the history is a sorted boundary array
-// in HBM (structure of arrays) with a 64-ary range-max hierarchy, and every phase
-// of ConflictBatch::detectConflicts is a data-parallel kernel:
+// in HBM (structure of arrays, a base and a delta tier) with a 64-ary range-max
+// hierarchy, and every phase of ConflictBatch::detectConflicts is a data-parallel
+// kernel.  Per batch, three chains on three streams (engine.cpp):
 //
-//   D.CheckRead        k_check_reads<tier waves> (both tiers) or k_check_tier<base / delta> (split check):
-//                      per read range two cooperative tree searches + range max; k_directory:
-//                      the base tier's radix directory (first two key bytes -> level-0 samples)
-//   D.Sort             k_sample, k_bucket_count, k_bucket_scatter, k_bucket_sort: sample sort of
-//                      the endpoints by (key, class, id)
-//   D.CheckIntraBatch  k_scan<PosScan>, k_scan<EdgePairScan>, k_edge_fill, k_resolve: candidate
-//                      edges (one per write group) + batch-order rounds
-//   D.Combine          k_scan2<CoverScan, SegmentScan>: union segments of committed writes
-//   D.MergeWrite       k_seg_search, k_scan<SegSumScan>, k_merge_copy<BatchIns>; compaction:
-//                      k_compact_search, k_scan<CompactSumScan>, k_merge_copy<CompactIns>
-//   D.RemoveBefore     k_scan<GcScan> (with a compaction); k_epilogue: levels, index, scalars
+//   stage A   D.Sort             k_sort_partition, k_sort_bucket (cold start: k_sample, k_quant_cold)
+//             D.CheckIntraBatch  k_scan<EdgePairScan>, k_edge_fill: candidate edges (one per write group)
+//   stage B X D.CheckRead        k_check_reads<tier waves> (both tiers, plus the previous batch's union
+//                                segments: prev_seg_hit) or k_check_tier<base / delta> (split check)
+//             D.CheckIntraBatch  k_resolve_pre (statuses, or the pre-pass), k_resolve (batch-order rounds)
+//             D.Combine          in k_resolve_pre without candidate edges, else k_combine
+//   stage B Y D.MergeWrite       k_seg_prep, k_merge_copy<BatchIns>; compaction: k_compact_search,
+//                                k_scan<CompactSumScan>, k_merge_copy<CompactIns>
+//             D.RemoveBefore     k_scan<GcScan> (with a compaction); k_epilogue: levels, index, scalars
+//   routing   (multi-resolver)   k_route_mark, k_scan<RouteScan>, k_route_write
 //
 // Memory-bound integer/byte work: no MFMA anywhere (BASELINE.json north_star).
 #include <hip/hip_runtime.h>
