@@ -432,6 +432,10 @@ def main():
         stride = (int(tb.item()) * 5 // 4 + 4095) // 4096 * 4096  # headroom over the sampled batches
         share_dev = [torch.empty(stride, dtype=torch.uint8, device=cdev) for _ in range(RING)]
         gathered = [torch.empty(world * stride, dtype=torch.uint8, device=cdev) for _ in range(RING)]
+        # torch's collectives run in their own HIP runtime: the engine cannot wait on their streams,
+        # so the current stream sets ready[k] = i + 1 once batch i's shares are gathered and the
+        # engine's first routing kernel polls it
+        ready = torch.zeros(RING, dtype=torch.int32, device=cdev)
         caps = (maxT, maxR, maxW, maxTail)
 
         def pack_share(i):
@@ -447,9 +451,10 @@ def main():
                 dist.all_gather_into_tensor(gathered[k], share_dev[k])
             else:  # gloo (one-GPU rehearsals): list form
                 dist.all_gather(list(gathered[k].view(world, stride).unbind(0)), share_dev[k])
+            ready[k].fill_(i + 1)
             o = C.ConflictBatch(cs)
             o.add_routed(gathered[k].data_ptr(), stride, world, p.txns, lo_key, hi_key, caps, outbuf[i].data_ptr(),
-                         gbatches[i][0].n_txn, torch.cuda.current_stream().cuda_stream)
+                         gbatches[i][0].n_txn, ready[k:k + 1].data_ptr(), i + 1)
             return o
 
     def attach(i, o):

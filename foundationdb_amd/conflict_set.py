@@ -136,7 +136,7 @@ SIGNATURES = {
     "fdbcs_share_bytes": (ctypes.c_int, [ctypes.POINTER(_CPackedBatch), ctypes.POINTER(_I64)]),
     "fdbcs_share_pack": (ctypes.c_int, [ctypes.POINTER(_CPackedBatch), _VP, _I64, ctypes.POINTER(_I64)]),
     "fdbcs_batch_add_routed": (ctypes.c_int, [_VP, _VP, _I64, _I32, _I32, _VP, _I32, _VP, _I32, _I32, _I32, _I32, _I64,
-                                              _VP, _I64, ctypes.c_uint64]),
+                                              _VP, _I64, _VP, ctypes.c_uint32]),
     "fdbcs_batch_routed_info": (ctypes.c_int, [_VP, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32),
                                                ctypes.POINTER(_VP), ctypes.POINTER(_VP)]),
     "fdbcs_debug_kernel_time": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
@@ -389,10 +389,12 @@ class ConflictBatch:
 
     def add_routed(self, shares_ptr: int, stride: int, n_shares: int, max_share_txns: int, lo: Optional[bytes],
                    hi: Optional[bytes], caps: Tuple[int, int, int, int], conflict_out: int = 0, n_global: int = 0,
-                   stream: int = 0) -> None:
+                   ready_ptr: int = 0, ready_value: int = 0) -> None:
         """fdbcs_batch_add_routed: this resolver's part ([lo, hi); None = unbounded) of the shares
         gathered at device address `shares_ptr` (`stride` bytes apart), routed on the device once
-        `stream` (a hipStream_t handle, e.g. torch.cuda.current_stream().cuda_stream) gets there.
+        the uint32 at device address `ready_ptr` equals `ready_value` (the caller's stream sets it
+        after the all-gather: torch's collectives run in their own HIP runtime, whose stream
+        handles this engine cannot wait on; 0 = the shares are complete already).
         caps = (txns, reads, writes, tail bytes) bounds of the routed batch."""
         lo_b = bytes(lo) if lo is not None else b""
         hi_b = bytes(hi) if hi is not None else b""
@@ -402,7 +404,7 @@ class ConflictBatch:
             self._h, _VP(shares_ptr), int(stride), int(n_shares), int(max_share_txns), ctypes.cast(lo_buf, _VP),
             len(lo_b) if lo is not None else -1, ctypes.cast(hi_buf, _VP), len(hi_b) if hi is not None else -1,
             int(caps[0]), int(caps[1]), int(caps[2]), int(caps[3]), _VP(conflict_out or None), int(n_global),
-            int(stream)), "addRouted")
+            _VP(ready_ptr or None), int(ready_value) & 0xFFFFFFFF), "addRouted")
         self._routed = True
 
     def routed_info(self) -> Tuple[int, int, int, int, int]:

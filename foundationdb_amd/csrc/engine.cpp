@@ -281,7 +281,6 @@ struct BatchSlot {
     // device routing (fdbcs_batch_add_routed): scan state, global -> batch map, read ids, totals
     DBuf rt_scan, rt_inv, rt_rids, rt_dres, rt_info, rt_txpre;
     HBuf rt_res;
-    hipEvent_t ev_route_in = nullptr;  // the caller's stream reached the all-gathered shares
     hipEvent_t ev_rt0 = nullptr, ev_rt1 = nullptr;  // around the routing kernels
     bool rt_timed = false;
     // per-kernel events of the batch (timing level 3, or the timed kernel at level 1)
@@ -702,7 +701,6 @@ void release_slot(BatchSlot* sl) {
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
     if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
-    if (sl->ev_route_in) (void)hipEventDestroy(sl->ev_route_in);
     if (sl->ev_rt0) (void)hipEventDestroy(sl->ev_rt0);
     if (sl->ev_rt1) (void)hipEventDestroy(sl->ev_rt1);
     sl->rt_scan.release();
@@ -1711,7 +1709,7 @@ int fdbcs_share_pack(const fdbcs_packed_batch* pb, void* out, int64_t cap, int64
 int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, int32_t n_shares, int32_t max_share_txns,
                            const uint8_t* lo_key, int32_t lo_len, const uint8_t* hi_key, int32_t hi_len, int32_t cap_txns,
                            int32_t cap_reads, int32_t cap_writes, int64_t cap_tail, uint8_t* conflict_out,
-                           int64_t n_global, uint64_t after_stream) {
+                           int64_t n_global, const uint32_t* ready_flag, uint32_t ready_value) {
     if (!b || !shares || stride <= (int64_t)sizeof(ShareHeader) || n_shares <= 0 || max_share_txns < 0 || cap_txns < 0 ||
         cap_reads < 0 || cap_writes < 0 || cap_tail < 0 || (lo_len > 0 && !lo_key) || (hi_len > 0 && !hi_key) ||
         n_global < 0 || (conflict_out && n_global > (int64_t)n_shares * max_share_txns))
@@ -1770,7 +1768,6 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     if ((rc = sl->rt_dres.ensure(sizeof(RouteResult)))) return rc;
     if ((rc = sl->rt_res.ensure(sizeof(RouteResult), true))) return rc;
     if ((rc = make_slot_events(sl))) return rc;
-    if (!sl->ev_route_in) HIPOK(hipEventCreateWithFlags(&sl->ev_route_in, hipEventDisableTiming));
     if (!sl->ev_rt0) HIPOK(hipEventCreate(&sl->ev_rt0));
     if (!sl->ev_rt1) HIPOK(hipEventCreate(&sl->ev_rt1));
     const auto t_host = std::chrono::steady_clock::now();
@@ -1804,10 +1801,11 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     a.dres = (RouteResult*)sl->rt_dres.p;
     ((RouteResult*)sl->rt_res.p)->error = -1;  // not written yet
     hipStream_t us = cs->ustream;
-    // the shares are complete on the caller's stream (the all-gather); the slot's previous batch
-    // may still read its device buffer
-    HIPOK(hipEventRecord(sl->ev_route_in, (hipStream_t)(uintptr_t)after_stream));
-    HIPOK(hipStreamWaitEvent(us, sl->ev_route_in, 0));
+    // the shares are complete once *ready_flag == ready_value (k_route_wait); the slot's previous
+    // batch may still read its device buffer
+    a.ready = ready_flag;
+    a.ready_value = ready_value;
+    a.wait_err = (uint32_t*)((uint64_t*)sl->rt_scan.p + 2);
     if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
     HIPOK(hipMemsetAsync(sl->rt_scan.p, 0, 8 * (size_t)route_scan_words(n_elems), us));
     uint64_t* sw = (uint64_t*)sl->rt_scan.p;
@@ -1846,7 +1844,10 @@ static int finish_route(fdbcs_batch* b) {
     std::atomic_thread_fence(std::memory_order_acquire);
     RouteResult r;
     memcpy(&r, (const void*)sl->rt_res.p, sizeof(r));
-    if (r.error != 0) return r.error < 0 ? FDBCS_E_DEVICE : FDBCS_E_NOMEM;
+    if (r.error != 0) {
+        if (r.error == 2) fprintf(stderr, "fdbcs: routed batch: the shares' ready flag was never set\n");
+        return r.error == 1 ? FDBCS_E_NOMEM : FDBCS_E_DEVICE;
+    }
     b->rT = r.T;
     b->rR = r.R;
     b->rW = r.W;

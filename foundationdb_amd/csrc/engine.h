@@ -302,6 +302,9 @@ struct RouteArgs {
     int64_t out_n;
     RouteResult* res;   // host-mapped
     RouteResult* dres;  // device copy
+    const uint32_t* ready;  // device word the caller's stream sets to ready_value once the shares are
+    uint32_t ready_value;   // gathered (null: already complete); k_route_wait spins on it
+    uint32_t* wait_err;     // set when that wait timed out (the routed batch then reports an error)
 };
 // Route the all-gathered shares into this resolver's batch (two launches on `s`).  grid_n: bound
 // on n_shares * tcap (global elements); the scan state's granules are zeroed by the caller.

@@ -2940,14 +2940,35 @@ __device__ __forceinline__ const ShareHeader* share_at(const RouteArgs& a, int p
     return (const ShareHeader*)(a.shares + (int64_t)p * a.stride);
 }
 
+// The shares are written by another HIP runtime (torch's collectives load their own), whose
+// streams this engine cannot wait on: the caller's stream sets a device word once the all-gather
+// is complete, and one wave here polls it (agent scope, bounded) before the routing kernels.
+__global__ void k_route_wait(const uint32_t* ready, uint32_t value, uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    if (ready) {
+        for (uint32_t spin = 0; spin < (1u << 24); spin++) {
+            if (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == value) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                *err = 0;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        *err = 1;  // bounded: never hang the GPU
+        return;
+    }
+    *err = 0;
+}
+
 // Per range of every share (one thread each): does it meet this resolver's [lo, hi)?  info =
 // kept | an endpoint longer than 19 bytes << 1 | longer than 24 << 2 | tail bytes of both
 // endpoints << 8.
 __global__ __launch_bounds__(kBlock) void k_route_mark(RouteArgs a) {
+    if (*a.wait_err) return;
     const int p = blockIdx.y;
     const ShareHeader* h = share_at(a, p);
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= h->R + h->W) return;
+    if (j >= h->R + h->W || j >= a.rstride) return;
     const uint8_t* base = (const uint8_t*)h;
     const DKey* keys = (const DKey*)(base + h->off_keys);
     const uint8_t* tb = base + h->off_tail;
@@ -2967,6 +2988,7 @@ struct RouteScan {
     __device__ const ShareHeader* at(int64_t i, int& p, int& t, int64_t& gid) const {
         p = (int)(i / a.tcap);
         t = (int)(i - (int64_t)p * a.tcap);
+        if (*a.wait_err) return nullptr;  // the shares never arrived: read nothing of them
         const ShareHeader* h = share_at(a, p);
         if (t >= h->T) return nullptr;
         gid = t;
@@ -3047,6 +3069,7 @@ struct RouteScan {
         r.n_gt19 = (int32_t)tot[4];
         r.n_gt24 = (int32_t)tot[5];
         r.error = (r.T > a.cap_T || r.R > a.cap_R || r.W > a.cap_W || (int64_t)tot[3] > a.cap_tail) ? 1 : 0;
+        if (*a.wait_err) r.error = 2;
         if (!r.error) {
             a.roff[r.T] = r.R;
             a.woff[r.T] = r.W;
@@ -3116,6 +3139,7 @@ int64_t route_scan_words(int64_t n_elems) { return 8 + scan_granules(n_elems, 6)
 
 void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
     const dim3 grid((unsigned)std::max<int64_t>(1, (a.rstride + kBlock - 1) / kBlock), (unsigned)a.n_shares);
+    fdb_launch(k_route_wait, dim3(1), dim3(64), 0, s, a.ready, a.ready_value, a.wait_err);
     fdb_launch(k_route_mark, grid, dim3(kBlock), 0, s, a);
     launch_scan<6>(s, RouteScan{a}, nullptr, (int64_t)a.n_shares * a.tcap, st);
     fdb_launch(k_route_write, grid, dim3(kBlock), 0, s, a);

@@ -222,7 +222,8 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
  *     TooOld test, which stays with the resolvers).  The shares of all ranks are then gathered
  *     into one device buffer, `stride` bytes apart in rank order (an RCCL all-gather).
  *   fdbcs_batch_add_routed: on a new batch (the addTransaction step, SkipList.cpp:763-794): once
- *     `after_stream` (a hipStream_t, as an integer) reaches this point, the engine keeps, on the
+ *     the device word *ready_flag equals ready_value (the caller's stream sets it after the
+ *     all-gather; NULL: the shares are already complete), the engine keeps, on the
  *     device, every range of the gathered shares that meets [lo_key, hi_key) (lo_len < 0: no lower
  *     bound, hi_len < 0: none above), unclipped, reads and writes alike; a transaction gets a
  *     sub-transaction iff one of its ranges is kept (:107-116), its snapshot copied, TooOld tested
@@ -240,7 +241,8 @@ int fdbcs_share_pack(const fdbcs_packed_batch* pb, void* out, int64_t cap, int64
 int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, int32_t n_shares, int32_t max_share_txns,
                            const uint8_t* lo_key, int32_t lo_len, const uint8_t* hi_key, int32_t hi_len,
                            int32_t cap_txns, int32_t cap_reads, int32_t cap_writes, int64_t cap_tail,
-                           uint8_t* conflict_out, int64_t n_global, uint64_t after_stream);
+                           uint8_t* conflict_out, int64_t n_global, const uint32_t* ready_flag,
+                           uint32_t ready_value);
 int fdbcs_batch_routed_info(fdbcs_batch* b, int32_t* n_txn, int32_t* n_reads, int32_t* n_writes, void** inv_dev,
                             void** read_ids_dev);
 

@@ -35,6 +35,7 @@ for G in Gs:
         host[g * stride: g * stride + len(x)] = x
     dev = torch.from_numpy(host).cuda()
     out = torch.empty(pb.n_txn, dtype=torch.uint8, device="cuda")
+    ready = torch.ones(1, dtype=torch.int32, device="cuda")  # set by torch's stream; polled by the engine
     tail = int(np.maximum(np.diff(pb.key_offsets) - 16, 0).sum())
     routes = sh.route(pb)
     res = []
@@ -47,7 +48,7 @@ for G in Gs:
                 cs.reset_stats()
             b = C.ConflictBatch(cs)
             b.add_routed(dev.data_ptr(), stride, G, 5000, lo, hi, (pb.n_txn, pb.n_reads, pb.n_writes, tail),
-                         out.data_ptr(), pb.n_txn, torch.cuda.current_stream().cuda_stream)
+                         out.data_ptr(), pb.n_txn, ready.data_ptr(), 1)
             T, R, Wn, _, _ = b.routed_info()
             sub = routes[r].batch
             assert (T, R, Wn) == (sub.n_txn, sub.n_reads, sub.n_writes), (T, R, Wn, sub.n_txn)

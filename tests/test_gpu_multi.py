@@ -88,6 +88,13 @@ def test_device_routing_matches_host_routing(engine, G, alphabet, max_len, long_
         for g, x in enumerate(shares):
             host[g * stride: g * stride + len(x)] = x
         dev = torch.from_numpy(host).cuda()
+        # the gathered shares' ready flag, set on torch's stream (another HIP runtime) after the
+        # copy; odd steps pass none, the shares being complete once torch has synchronised
+        ready = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ready.fill_(step + 1)
+        if step % 2:
+            torch.cuda.synchronize()
+        flag = (ready.data_ptr(), step + 1) if step % 2 == 0 else (0, 0)
         routes = sh.route(pb)
         tail = int(np.maximum(np.diff(pb.key_offsets) - 16, 0).sum())
         out = [torch.full((pb.n_txn,), 7, dtype=torch.uint8, device="cuda") for _ in range(G)]
@@ -96,7 +103,7 @@ def test_device_routing_matches_host_routing(engine, G, alphabet, max_len, long_
             hi = splits[g] if g < G - 1 else None
             b = engine.ConflictBatch(sets[g])
             b.add_routed(dev.data_ptr(), stride, G, Tshare, lo, hi, (pb.n_txn, pb.n_reads, pb.n_writes, tail),
-                         out[g].data_ptr(), pb.n_txn, torch.cuda.current_stream().cuda_stream)
+                         out[g].data_ptr(), pb.n_txn, *flag)
             sub = routes[g].batch
             T, R, Wn, _, _ = b.routed_info()
             # TooOld sub-transactions (SkipList.cpp:770, at add time) keep no ranges
