@@ -1680,6 +1680,13 @@ __device__ __forceinline__ uint2 write_rb_interval(const Work& w, int g) {
     return hi > lo ? make_uint2((uint32_t)lo, (uint32_t)hi) : make_uint2(0, 0);
 }
 
+// Elements per thread of the scans whose visits are chains of dependent gathers (scan.h): one,
+// so every chain has its own lane and the small batch-sized scans still span many workgroups.
+constexpr int kEdgeScanP = 1;
+constexpr int kCombineP = 1;
+constexpr int kCombineTile = kScanThreads * kCombineP;
+constexpr int kRouteScanP = 1;
+
 struct EdgePairScan {
     Work w;
     int32_t R, G;
@@ -1829,7 +1836,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
 
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    launch_scan<2>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys}, nullptr, G, w.scan[kScanEdges]);
+    launch_scan<2, kEdgeScanP>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
         const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
         fdb_launch(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
@@ -1919,18 +1926,26 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
             w.first_conf[t] = INT_MAX;
             vout[t] = verdict_byte(b, t, st);
         }
-        // D.Combine: tiles of kScanTile write endpoints, ids in launch order
-        __shared__ uint32_t sv[1][kScanPad];
+        // D.Combine: tiles of kCombineTile write endpoints, ids in launch order.  Only the first
+        // ntiles workgroups take an id: the grid is sized for the waves of the edge case, and
+        // every id taken is one more atomic on the same counter word
+        __shared__ uint32_t sv[1][scan_pad(kCombineP)];
         __shared__ uint32_t swave[1][kScanThreads / 64];
         __shared__ uint32_t sbase[1];
         __shared__ int s_tile;
+        const int64_t n = 2 * (int64_t)b.W;
+        const int64_t ntiles = n > 0 ? (n + kCombineTile - 1) / kCombineTile : 1;
+        if (blockIdx.x >= ntiles) {
+            if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
+            return;
+        }
         if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanCover].counter, 1);
         __syncthreads();
-        const int64_t n = 2 * (int64_t)b.W;
-        const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
         if (s_tile < ntiles) {
-            scan_tile<1>(CoverScan{w, b, 0}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
-            scan_tile<1>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave, sbase);
+            scan_tile<1, CoverScan, kCombineP>(CoverScan{w, b, 0}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave,
+                                               sbase);
+            scan_tile<1, SegNumScan, kCombineP>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave,
+                                                sbase);
         }
         if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
         return;
@@ -2315,7 +2330,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
 // D.Combine after batch-order rounds (candidate edges existed): the same two chained look-back
 // scans as the no-edge case, over the final statuses; exits at once when k_resolve_pre combined.
 __global__ __launch_bounds__(kScanThreads) void k_combine(BatchDev b, Work w) {
-    __shared__ uint32_t sv[1][kScanPad];
+    __shared__ uint32_t sv[1][scan_pad(kCombineP)];
     __shared__ uint32_t swave[1][kScanThreads / 64];
     __shared__ uint32_t sbase[1];
     __shared__ int s_tile;
@@ -2323,10 +2338,10 @@ __global__ __launch_bounds__(kScanThreads) void k_combine(BatchDev b, Work w) {
     if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanCover].counter, 1);
     __syncthreads();
     const int64_t n = 2 * (int64_t)b.W;
-    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+    const int64_t ntiles = n > 0 ? (n + kCombineTile - 1) / kCombineTile : 1;
     if (s_tile >= ntiles) return;
-    scan_tile<1>(CoverScan{w, b, 1}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
-    scan_tile<1>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave, sbase);
+    scan_tile<1, CoverScan, kCombineP>(CoverScan{w, b, 1}, n, s_tile, ntiles, w.scan[kScanCover], sv, swave, sbase);
+    scan_tile<1, SegNumScan, kCombineP>(SegNumScan{w}, n, s_tile, ntiles, w.scan[kScanSegNum], sv, swave, sbase);
 }
 
 // First conflicting read index of intra-batch aborts that report conflicting keys
@@ -2363,7 +2378,7 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
     // one wave per transaction for the pre-pass, then the rounds in one workgroup
     // (at least one workgroup per D.Combine tile of the no-edge case)
     const int64_t pre_grid = std::max<int64_t>(((int64_t)b.T * 64 + kBlock - 1) / kBlock,
-                                               (2 * (int64_t)b.W + kScanTile - 1) / kScanTile);
+                                               (2 * (int64_t)b.W + kCombineTile - 1) / kCombineTile);
     fdb_launch(k_resolve_pre, dim3((unsigned)pre_grid), dim3(kBlock), 0, s, b, w, verdict_out);
     size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
     Work wl = w;
@@ -2374,7 +2389,7 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
         lds += 8 * (size_t)wl.member_lds;
     }
     fdb_launch(k_resolve, dim3(1), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out, sc);
-    fdb_launch(k_combine, dim3((unsigned)std::max<int64_t>(1, (2 * (int64_t)b.W + kScanTile - 1) / kScanTile)),
+    fdb_launch(k_combine, dim3((unsigned)std::max<int64_t>(1, (2 * (int64_t)b.W + kCombineTile - 1) / kCombineTile)),
                dim3(kScanThreads), 0, s, b, w);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
 }
@@ -2903,8 +2918,8 @@ int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int6
     (void)T;
     const int64_t E = 2 * (R + W);
     (void)E;
-    return kNumScans + scan_granules(R + W, 2) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) +
-           scan_granules(hist_cap, 2) + 2 * scan_granules(2 * W, 1);
+    return kNumScans + scan_granules(R + W, 2, kEdgeScanP) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) +
+           scan_granules(hist_cap, 2) + 2 * scan_granules(2 * W, 1, kCombineP);
 }
 
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
@@ -2912,9 +2927,9 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     const int64_t E = 2 * (R + W);
     uint64_t* a = w.scan_arena;
     (void)E;
-    const int64_t gran[kNumScans] = {scan_granules(R + W, 2), 3 * seg_prep_tiles(W),
+    const int64_t gran[kNumScans] = {scan_granules(R + W, 2, kEdgeScanP), 3 * seg_prep_tiles(W),
                                      scan_granules(delta_cap + 1, 2), scan_granules(hist_cap, 2),
-                                     scan_granules(2 * W, 1), scan_granules(2 * W, 1)};
+                                     scan_granules(2 * W, 1, kCombineP), scan_granules(2 * W, 1, kCombineP)};
     uint64_t* g = a + kNumScans;
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);
@@ -3135,13 +3150,13 @@ __global__ __launch_bounds__(kBlock) void k_route_write(RouteArgs a) {
     }
 }
 
-int64_t route_scan_words(int64_t n_elems) { return 8 + scan_granules(n_elems, 6); }
+int64_t route_scan_words(int64_t n_elems) { return 8 + scan_granules(n_elems, 6, kRouteScanP); }
 
 void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
     const dim3 grid((unsigned)std::max<int64_t>(1, (a.rstride + kBlock - 1) / kBlock), (unsigned)a.n_shares);
     fdb_launch(k_route_wait, dim3(1), dim3(64), 0, s, a.ready, a.ready_value, a.wait_err);
     fdb_launch(k_route_mark, grid, dim3(kBlock), 0, s, a);
-    launch_scan<6>(s, RouteScan{a}, nullptr, (int64_t)a.n_shares * a.tcap, st);
+    launch_scan<6, kRouteScanP>(s, RouteScan{a}, nullptr, (int64_t)a.n_shares * a.tcap, st);
     fdb_launch(k_route_write, grid, dim3(kBlock), 0, s, a);
 }
 

@@ -24,6 +24,9 @@ constexpr int kScanThreads = 256;
 constexpr int kScanPer = 4;
 constexpr int kScanTile = kScanThreads * kScanPer;  // 1024: many workgroups even for small scans
 constexpr int kScanPad = kScanTile + kScanTile / 4;
+// elements per thread P: 4 by default; 1 for scans whose visits are chains of dependent gathers
+// (a thread's P visits run one after another, so P = 1 spreads the chains over 4x the waves)
+constexpr int scan_pad(int P) { return kScanThreads * P + kScanThreads * P / 4; }
 
 __device__ __forceinline__ int scan_slot(int e) { return e + (e >> 2); }  // one pad word per thread run
 
@@ -94,15 +97,15 @@ __device__ __forceinline__ void tile_lookback(ScanState st, int64_t tile, const 
 
 // One tile of a scan (tile ids come from the caller, in launch order).  Ends with a barrier, so
 // the LDS arrays can be reused by a following stage.
-template <int K, class F>
+template <int K, class F, int P = kScanPer>
 __device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64_t ntiles, ScanState st,
-                                          uint32_t (&sv)[K][kScanPad], uint32_t (&swave)[K][kScanThreads / 64],
+                                          uint32_t (&sv)[K][scan_pad(P)], uint32_t (&swave)[K][kScanThreads / 64],
                                           uint32_t (&sbase)[K]) {
-    const int64_t base = (int64_t)tile * kScanTile;
+    const int64_t base = (int64_t)tile * (kScanThreads * P);
 
     // phase 1: coalesced visits
 #pragma unroll
-    for (int k = 0; k < kScanPer; k++) {
+    for (int k = 0; k < P; k++) {
         const int e = k * kScanThreads + threadIdx.x;
         const int64_t i = base + e;
         uint32_t v[K];
@@ -119,8 +122,8 @@ __device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64
     for (int c = 0; c < K; c++) {
         uint32_t s = 0;
 #pragma unroll
-        for (int j = 0; j < kScanPer; j++) {
-            const int slot = scan_slot(threadIdx.x * kScanPer + j);
+        for (int j = 0; j < P; j++) {
+            const int slot = scan_slot(threadIdx.x * P + j);
             const uint32_t x = sv[c][slot];
             sv[c][slot] = s;
             s += x;
@@ -161,12 +164,12 @@ __device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64
     for (int c = 0; c < K; c++) {
         const uint32_t add = sbase[c] + texcl[c];
 #pragma unroll
-        for (int j = 0; j < kScanPer; j++) sv[c][scan_slot(threadIdx.x * kScanPer + j)] += add;
+        for (int j = 0; j < P; j++) sv[c][scan_slot(threadIdx.x * P + j)] += add;
     }
     __syncthreads();
     // phase 4: coalesced stores
 #pragma unroll
-    for (int k = 0; k < kScanPer; k++) {
+    for (int k = 0; k < P; k++) {
         const int e = k * kScanThreads + threadIdx.x;
         const int64_t i = base + e;
         if (i < n) {
@@ -185,9 +188,9 @@ __device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64
     __syncthreads();
 }
 
-template <int K, class F>
+template <int K, class F, int P = kScanPer>
 __global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr, int64_t n_host, ScanState st) {
-    __shared__ uint32_t sv[K][kScanPad];
+    __shared__ uint32_t sv[K][scan_pad(P)];
     __shared__ uint32_t swave[K][kScanThreads / 64];
     __shared__ uint32_t sbase[K];
     __shared__ int s_tile;
@@ -195,9 +198,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(F f, const int64_t* n_ptr
     if (threadIdx.x == 0) s_tile = atomicAdd(st.counter, 1);
     __syncthreads();
     const int tile = s_tile;
-    const int64_t ntiles = n > 0 ? (n + kScanTile - 1) / kScanTile : 1;
+    const int64_t ntiles = n > 0 ? (n + kScanThreads * P - 1) / (kScanThreads * P) : 1;
     if (tile >= ntiles) return;  // spare tile of a device-sized launch: nobody waits on it
-    scan_tile<K>(f, n, tile, ntiles, st, sv, swave, sbase);
+    scan_tile<K, F, P>(f, n, tile, ntiles, st, sv, swave, sbase);
 }
 
 // Two chained scans over the same n elements in one launch: stage 2's load(i) may read what
@@ -223,8 +226,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan2(F1 f1, F2 f2, int64_t n,
                   reinterpret_cast<uint32_t(&)[K2][kScanThreads / 64]>(swave), reinterpret_cast<uint32_t(&)[K2]>(sbase));
 }
 
-// Granules needed for a scan of up to n elements with K components.
-inline int64_t scan_granules(int64_t n, int K) { return ((n > 0 ? n : 1) + kScanTile - 1) / kScanTile * K; }
+// Granules needed for a scan of up to n elements with K components (P elements per thread).
+inline int64_t scan_granules(int64_t n, int K, int P = kScanPer) {
+    return ((n > 0 ? n : 1) + kScanThreads * P - 1) / (kScanThreads * P) * K;
+}
 
 template <int K1, class F1, int K2, class F2>
 void launch_scan2(hipStream_t s, const F1& f1, const F2& f2, int64_t n, ScanState st1, ScanState st2) {
@@ -233,11 +238,11 @@ void launch_scan2(hipStream_t s, const F1& f1, const F2& f2, int64_t n, ScanStat
     fdb_launch((k_scan2<K1, F1, K2, F2>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f1, f2, n, st1, st2);
 }
 
-template <int K, class F>
+template <int K, int P = kScanPer, class F>
 void launch_scan(hipStream_t s, const F& f, const int64_t* n_dev, int64_t n_max, ScanState st) {
-    int64_t tiles = (n_max + kScanTile - 1) / kScanTile;
+    int64_t tiles = (n_max + kScanThreads * P - 1) / (kScanThreads * P);
     if (tiles < 1) tiles = 1;
-    fdb_launch((k_scan<K, F>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f, n_dev, n_max, st);
+    fdb_launch((k_scan<K, F, P>), dim3((unsigned)tiles), dim3(kScanThreads), 0, s, f, n_dev, n_max, st);
 }
 
 }  // namespace fdbcs
