@@ -232,7 +232,11 @@ struct fdbcs_conflict_set {
     // cross-stream event waits and records around it issued directly, so the stages still overlap
     // across streams as in direct mode while the submitting thread makes ~3 graph launches instead
     // of ~20 kernel launches per batch.
-    bool stage_graphs = false;
+    // FDBCS_GRAPH=3: whole-stage graphs.  Each stage list of a batch (A, the check / resolution
+    // half X, the merge / epilogue half Y) goes out as ONE cached graph on its stream, its
+    // cross-stream waits and records included as event wait / record nodes, so the stream
+    // layout and every dependency stay those of direct mode at three graph launches per batch.
+    int stage_graphs = 0;  // 1: runs between sync points (FDBCS_GRAPH=2); 2: whole lists (=3)
     struct StageGraph {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
@@ -871,7 +875,8 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
     uint64_t key = 1469598103934665603ull;
     for (size_t i = i0; i < i1; i++) {
         const LaunchList::Rec& r = L.recs[i];
-        key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u)) * 1099511628211ull;
+        key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u + r.kind)) *
+              1099511628211ull;
     }
     fdbcs_conflict_set::StageGraph* sg = nullptr;
     for (auto& kv : cs->stage_cache)
@@ -895,6 +900,8 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
             if (r.kind == LaunchList::kKernel) {
                 const hipKernelNodeParams p = params(r);
                 HIPOK(hipGraphAddKernelNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, &p));
+            } else if (r.kind == LaunchList::kSyncWait) {
+                HIPOK(hipGraphAddEventWaitNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
             } else {
                 HIPOK(hipGraphAddEventRecordNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
             }
@@ -911,6 +918,8 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
             if (r.kind == LaunchList::kKernel) {
                 const hipKernelNodeParams p = params(r);
                 HIPOK(hipGraphExecKernelNodeSetParams(sg->exec, sg->nodes[k++], &p));
+            } else if (r.kind == LaunchList::kSyncWait) {
+                HIPOK(hipGraphExecEventWaitNodeSetEvent(sg->exec, sg->nodes[k++], r.event));
             } else {
                 HIPOK(hipGraphExecEventRecordNodeSetEvent(sg->exec, sg->nodes[k++], r.event));
             }
@@ -927,6 +936,13 @@ int launch_stage(fdbcs_conflict_set* cs, LaunchList& L, hipStream_t st) {
     };
     L.finalize();
     const size_t n = L.recs.size();
+    if (cs->stage_graphs == 2) {  // the whole list, its waits and records included, as one graph
+        size_t kernels = 0;
+        for (const LaunchList::Rec& r : L.recs) kernels += r.kind == LaunchList::kKernel ? 1 : 0;
+        if (kernels >= 1 && n >= 2) return launch_graph_run(cs, L, 0, n, st);
+        for (const LaunchList::Rec& r : L.recs) HIPOK(L.issue(r, st));
+        return FDBCS_OK;
+    }
     size_t i = 0;
     while (i < n) {
         if (is_sync(L.recs[i])) {
@@ -1053,7 +1069,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
-    if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2';
+    if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2' ? 1 : (v[0] == '3' ? 2 : 0);
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';

@@ -545,6 +545,7 @@ def test_empty_batches(engine, oracle_mod):
                                    {"FDBCS_SORT_COLD": "1"},
                                    {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
+                                   {"FDBCS_GRAPH": "3"}, {"FDBCS_GRAPH": "3", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
                                    {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"}])
