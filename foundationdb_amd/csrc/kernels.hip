@@ -1112,15 +1112,16 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     }
     __syncthreads();
     if (threadIdx.x == 0) trace_max(a.trace, kTrPartFill);
-    if (p >= E) {
-        if (a.trace) trace_max(a.trace, kTrPartEnd);
-        return;
-    }
-    if (a.btail) {  // the batch tail region into the workspace copy, 8-byte words, grid-strided
+    if (a.btail) {  // the batch tail region into the workspace copy, 8-byte words, strided over
+        // EVERY thread of the grid (the tail region can hold many more words than endpoints)
         const int64_t nw = (a.btail_n + 7) / 8;
         const uint64_t* src = (const uint64_t*)b.tail;
         uint64_t* dst = (uint64_t*)a.btail;
         for (int64_t q = p; q < nw; q += (int64_t)gridDim.x * blockDim.x) dst[q] = src[q];
+    }
+    if (p >= E) {
+        if (a.trace) trace_max(a.trace, kTrPartEnd);
+        return;
     }
     // splitters below my first two words: [0, lo); equal to them: [lo, up)
     int lo = 0, hi = ns;

@@ -75,6 +75,37 @@ def test_random_vs_oracle(engine, oracle_mod, alphabet, max_len):
         run_pair(engine, oracle_mod, seq, gc_interval=gc, delta_limit=dl, clear=(5 if trial % 5 == 0 else None))
 
 
+def _prefixed(pb, prefix: bytes):
+    """The batch with `prefix` before every key: the same verdicts, every comparison in the tails."""
+    n = len(pb.key_offsets) - 1
+    lens = np.diff(pb.key_offsets)
+    parts = []
+    for k in range(n):
+        parts.append(prefix)
+        parts.append(pb.key_bytes[pb.key_offsets[k]:pb.key_offsets[k + 1]].tobytes())
+    offs = np.concatenate([[0], np.cumsum(lens + len(prefix))]).astype(np.int64)
+    return PackedBatch(pb.read_snapshot, pb.report, pb.read_offsets, pb.write_offsets,
+                         np.frombuffer(b"".join(parts), np.uint8).copy(), offs)
+
+
+@pytest.mark.parametrize("gc_interval,delta_limit", [(0, 0), (0, 40), (3, 0)])
+def test_long_shared_prefix_tails(engine, oracle_mod, gc_interval, delta_limit):
+    """Keys behind a 60-byte shared prefix: every order decision is made in the tails, and a batch's
+    tail region holds several words per endpoint.  The next batch's check reads the previous
+    batch's union segments with their tails from the workspace copy (PrevSegs), so a short copy
+    shows up as wrong verdicts."""
+    rng = np.random.default_rng(77 + gc_interval + delta_limit)
+    prefix = bytes(rng.integers(0, 256, 60, dtype=np.uint8))
+    seq = []
+    now = 10
+    for _ in range(24):
+        pb = W.random_small_batch(rng, int(rng.integers(20, 200)), alphabet=3, max_len=5, now=now, staleness=12,
+                                  max_reads=4, max_writes=3)
+        seq.append((_prefixed(pb, prefix), now, now - int(rng.integers(0, 10))))
+        now += int(rng.integers(1, 4))
+    run_pair(engine, oracle_mod, seq, gc_interval=gc_interval, delta_limit=delta_limit)
+
+
 @pytest.mark.parametrize("gc_interval,delta_limit", [(1, 0), (0, 0), (0, 25), (4, 0)])
 def test_delta_tier_configurations(engine, oracle_mod, gc_interval, delta_limit):
     """The two-tier history (delta merges, compaction, GC at compaction) is verdict- and
