@@ -89,9 +89,9 @@ def kernel_bytes(name: str, s: dict):
     if name.startswith("k_sort_bucket"):
         return (E * (I + 4 + 4 + 12) + G * 4 + nb * 16,
                 "E slab items read; position, meta and 3 class prefixes written per endpoint; R+W begin lists")
-    if name.startswith("k_scan<3, fdbcs::PosScan>"):
+    if name.startswith("k_scan<3, fdbcs::PosScan"):
         return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
-    if name.startswith("k_scan<2, fdbcs::EdgePairScan>"):
+    if name.startswith("k_scan<2, fdbcs::EdgePairScan"):
         return G * (8 + 24 + 8) + W * 8, "per range: 2 positions, class prefixes at both, slot/pair offsets"
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
@@ -124,9 +124,9 @@ def kernel_bytes(name: str, s: dict):
         return s["compact_bytes"], "32 B per kept base / inserted delta boundary read and per result boundary written"
     if name == "k_compact_search":
         return Nd * (P + 8 + lookup_bytes(N, s["dir_share"]) + 17), "per delta boundary: key + lookup in the base, 2 words"
-    if name.startswith("k_scan<2, fdbcs::CompactSumScan>"):
+    if name.startswith("k_scan<2, fdbcs::CompactSumScan"):
         return Nd * (8 + 8 + 1 + 24), "per delta boundary: lo, version, exact flag; 3 words written"
-    if name.startswith("k_scan<2, fdbcs::GcScan>"):
+    if name.startswith("k_scan<2, fdbcs::GcScan"):
         return N * (2 * V + 8) + N * 32, "versions (own + predecessor) and lengths read, kept boundaries rewritten"
     if name == "k_epilogue":
         n = Nd if Nd > 0 else N
