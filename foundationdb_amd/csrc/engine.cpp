@@ -141,12 +141,14 @@ struct fdbcs_conflict_set {
     hipStream_t ystream = nullptr;
     bool split_stage_b = true;          // FDBCS_SPLIT_B=0: both halves on `stream`, checks after the merge
     hipEvent_t ev_res[kNumWork] = {};   // X of the batch using workspace k is done (Y waits for it)
-    hipEvent_t ev_xfree[kNumWork] = {}; // the next batch's check is done with workspace k's segments
+    // the next batch's check is done with workspace k's segments: that batch's ev_res (the end of
+    // its half X, recorded anyway, and not re-recorded before workspace k's next user records)
+    hipEvent_t xfree_ev[kNumWork] = {};
     bool prev_segs = false;             // the last batch's segments are not merged when the next check runs
     int prev_wp = 0;
     int64_t prev_now = 0;
     int last_wp = -1, prev2_wp = -1;    // workspaces of the last two batches submitted (their Y events)
-    bool xfree_rec[kNumWork] = {};      // ev_xfree[k] recorded since workspace k's last use
+    bool xfree_rec[kNumWork] = {};      // xfree_ev[k] set since workspace k's last use
     bool y_async[kNumWork] = {};        // Y of workspace k's last batch ran on ystream (not in `stream` order)
     bool wused[kNumWork] = {};
     int wpar = 0;                   // workspace of the next batch
@@ -1091,8 +1093,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_c[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_b[k], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&cs->ev_res[k], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&cs->ev_xfree[k], hipEventDisableTiming) == hipSuccess;
+             hipEventCreateWithFlags(&cs->ev_res[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         fdbcs_destroy_conflict_set(cs);
         return FDBCS_E_DEVICE;
@@ -1168,7 +1169,6 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         if (cs->ev_c[k]) (void)hipEventDestroy(cs->ev_c[k]);
         if (cs->ev_b[k]) (void)hipEventDestroy(cs->ev_b[k]);
         if (cs->ev_res[k]) (void)hipEventDestroy(cs->ev_res[k]);
-        if (cs->ev_xfree[k]) (void)hipEventDestroy(cs->ev_xfree[k]);
     }
     if (cs->ustream) (void)hipStreamDestroy(cs->ustream);
     if (cs->cstream) (void)hipStreamDestroy(cs->cstream);
@@ -2041,8 +2041,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const bool ws_busy = cs->wused[wp] && (threaded || hipEventQuery(cs->ev_b[wp]) != hipSuccess);
     if (ws_busy && (sa != s || cs->y_async[wp])) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     // and the check after that batch may still read its union segments and their tails
-    if (cs->xfree_rec[wp] && sa != s && (threaded || hipEventQuery(cs->ev_xfree[wp]) != hipSuccess))
-        fdb_event(LaunchList::kSyncWait, cs->ev_xfree[wp], sa);
+    if (cs->xfree_rec[wp] && sa != s && (threaded || hipEventQuery(cs->xfree_ev[wp]) != hipSuccess))
+        fdb_event(LaunchList::kSyncWait, cs->xfree_ev[wp], sa);
     cs->xfree_rec[wp] = false;
     cs->wused[wp] = true;
     // stage A reads the batch: wait for the upload stream
@@ -2142,7 +2142,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
-        fdb_event(LaunchList::kSyncRecord, cs->ev_xfree[cs->prev_wp], s);
+        cs->xfree_ev[cs->prev_wp] = cs->ev_res[wp];  // recorded at the end of this half X
         cs->xfree_rec[cs->prev_wp] = true;
     }
     mark(kPhCheck);
