@@ -472,6 +472,8 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(rbpos, 4 * R);
     TAKE(eoff, 4 * (R + 1));
     TAKE(poff, 4 * (R + W + 1));
+    TAKE(pcg, 4 * (R + W + 1));
+    TAKE(pcoff, 4 * (R + W + 1));
     TAKE(ecur, 4 * R);
     TAKE(edges, 4 * edge_cap);
     TAKE(eptr, 4 * T);
@@ -2333,9 +2335,10 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                     us(kTrEpiHost, kTrEpiFence));
             fprintf(stderr,
                     "fdbcs trace: sort partition fill %.2f, search %.2f, end %.2f us; bucket prologue %.2f, "
-                    "sorted %.2f, end %.2f us (partition start to bucket start %.2f us)\n",
+                    "sorted %.2f, ties %.2f, end %.2f us (partition start to bucket start %.2f us)\n",
                     us(kTrPartBegin, kTrPartFill), us(kTrPartBegin, kTrPartSearch), us(kTrPartBegin, kTrPartEnd),
-                    us(kTrBktBegin, kTrBktPrologue), us(kTrBktBegin, kTrBktSorted), us(kTrBktBegin, kTrBktEnd),
+                    us(kTrBktBegin, kTrBktPrologue), us(kTrBktBegin, kTrBktSorted), us(kTrBktBegin, kTrBktTies),
+                    us(kTrBktBegin, kTrBktEnd),
                     us(kTrPartBegin, kTrBktBegin));
             fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
                     us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),

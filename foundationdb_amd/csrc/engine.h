@@ -95,6 +95,7 @@ struct BatchScalars {
     int32_t ovf_n;         // sort: endpoints past their bucket's slab (reset by the epilogue)
     int32_t sort_big;      // sort: buckets past the slab, sorted by the workgroup path (reset by the epilogue)
     int64_t n_segments;    // union segments of committed writes (D.Combine, k_resolve)
+    int64_t n_pranges;     // ranges with candidate pairs (k_scan<EdgePairScan>)
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -189,6 +190,8 @@ struct Work {
     int32_t* rbpos;        // [R] positions of read-begins in order
     int32_t* eoff;         // [R+1] first edge slot of each read
     int32_t* poff;         // [R+W+1] first candidate pair of each range
+    int32_t* pcg;          // [R+W+1] the ranges with candidate pairs, in order (then G)
+    int32_t* pcoff;        // [R+W+1] their first pairs (then the pair count): k_edge_fill's index
     int32_t* ecur;         // [R] edges of each read (slots taken; zeroed by the epilogue)
     // write groups (groups != 0): consecutive write-begins (in sorted order) whose writes contain
     // exactly the same read-begins are one group; a read gets one edge T + j per group j (j = the
@@ -237,7 +240,7 @@ enum TraceSlot {
     kTrEpiBegin, kTrEpiLevels, kTrEpiZero, kTrEpiHost, kTrEpiFence, kTrEpiEnd,
     kTrResBegin, kTrResPre, kTrResWait, kTrResRounds, kTrResEnd,
     kTrPartBegin, kTrPartFill, kTrPartSearch, kTrPartEnd,
-    kTrBktBegin, kTrBktPrologue, kTrBktSorted, kTrBktEnd,
+    kTrBktBegin, kTrBktPrologue, kTrBktSorted, kTrBktTies, kTrBktEnd,
     kTrCmbLoad, kTrCmbScan1, kTrCmbScan2, kTrCmbStore,
     kTrSlots
 };

@@ -1427,10 +1427,29 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                     int st = k, en = k;
                     while (st > 0 && s_tie[wave][st - 1]) st--;
                     while (s_tie[wave][en]) en++;
-                    const SortItem me = make_item(b, ps[s]);
+                    // The two endpoints of one range (a point range [k, k\0], a prefix range):
+                    // begin <= end holds for every admitted range, so keys of different lengths
+                    // order begin first without reading their tails; other pairs compare whole
+                    // keys.
+                    const int pm = ps[s];
+                    const uint32_t lme = b.keys[pm].len;
                     int rank = 0;
-                    for (int j = st; j <= en; j++)
-                        if (j != k) rank += item_less_total(make_item(b, s_p[wave][j]), me, b.tail) ? 1 : 0;
+                    bool need_me = false;
+                    for (int j = st; j <= en; j++) {
+                        if (j == k) continue;
+                        const int po = s_p[wave][j];
+                        if ((po >> 1) == (pm >> 1) && b.keys[po].len != lme) rank += (po & 1) ? 0 : 1;
+                        else need_me = true;
+                    }
+                    if (need_me) {
+                        const SortItem me = make_item(b, pm);
+                        for (int j = st; j <= en; j++) {
+                            if (j == k) continue;
+                            const int po = s_p[wave][j];
+                            if ((po >> 1) == (pm >> 1) && b.keys[po].len != lme) continue;
+                            rank += item_less_total(make_item(b, po), me, b.tail) ? 1 : 0;
+                        }
+                    }
                     fin[s] = st + rank;
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1449,6 +1468,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                 }
             }
         }
+        if (lane == 0) trace_max(a.trace, kTrBktTies);
         // positions, class counts before them, begin lists; quantiles for the next batch
         uint32_t carry[3] = {s_base[wave][1], s_base[wave][2], s_base[wave][3]};
 #pragma unroll
@@ -1736,62 +1756,90 @@ struct EdgePairScan {
             pairs = (uint32_t)(w.crb[e] - w.crb[b]);
         }
     }
-    __device__ void load(int64_t g, uint32_t (&v)[2]) const {
+    static constexpr bool kOwn = true;
+    // counts: edge slots, candidate pairs, has pairs (the compacted index k_edge_fill searches)
+    __device__ void load(int64_t g, uint32_t (&v)[3]) const {
         uint32_t a;
         counts(g, v[0], v[1], a);
+        v[2] = v[1] > 0 ? 1u : 0u;
     }
-    __device__ void store(int64_t g, const uint32_t (&ex)[2]) const {
+    __device__ void store(int64_t g, const uint32_t (&ex)[3], const uint32_t (&own)[3]) const {
         if (g < R) w.eoff[g] = (int32_t)ex[0];
         w.poff[g] = (int32_t)ex[1];
+        if (own[2]) {
+            w.pcg[ex[2]] = (int32_t)g;
+            w.pcoff[ex[2]] = (int32_t)ex[1];
+        }
     }
-    __device__ void finish(const uint32_t (&tot)[2]) const {
+    __device__ void finish(const uint32_t (&tot)[3]) const {
         w.eoff[R] = (int32_t)tot[0];
         w.poff[G] = (int32_t)tot[1];
+        w.pcg[tot[2]] = G;
+        w.pcoff[tot[2]] = (int32_t)tot[1];
+        w.bsc->n_pranges = tot[2];
         w.bsc->n_edges = tot[0];
         w.bsc->edge_overflow = (int64_t)tot[0] > w.edge_cap || tot[0] > 0x7fffffffu || tot[1] > 0x7fffffffu ? 1 : 0;
     }
 };
 
 constexpr int kPairsPerThread = 4;
+constexpr int kFillPairs = kBlock * kPairsPerThread;  // pairs per workgroup step of k_edge_fill
+
+// Last index c in [lo, hi) with a[c] <= x, given a[lo] <= x < a[hi] (a non-decreasing), by one
+// whole wave: 64 probes per step, so ~3 dependent loads for 10^5 entries instead of ~17.
+__device__ __forceinline__ int wave_last_le(const int32_t* a, int lo, int hi, int x) {
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 1) {
+        const int idx = lo + 1 + (int)(((int64_t)lane * (hi - lo - 1)) / 64);  // inside (lo, hi)
+        const uint64_t le = __ballot(a[idx] <= x);  // a prefix of the lanes
+        const int c = __popcll(le);
+        const int nlo = c > 0 ? __shfl(idx, c - 1, 64) : lo;
+        const int nhi = c < 64 ? __shfl(idx, c, 64) : hi;
+        lo = nlo;
+        hi = nhi;
+    }
+    return lo;
+}
 
 __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
+    __shared__ int32_t s_off[kFillPairs + 2], s_g[kFillPairs + 1];
+    __shared__ int s_c[2];
     if (w.bsc->edge_overflow) return;
-    const int R = b.R, G = b.R + b.W;
-    const int P = w.poff[G];
-    const int stride = gridDim.x * blockDim.x * kPairsPerThread;
-    for (int q0 = (blockIdx.x * blockDim.x + threadIdx.x) * kPairsPerThread; q0 < P; q0 += stride) {
-        // range owning pair q0: last g with poff[g] <= q0
-        int lo = 0, hi = G;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (w.poff[mid] <= q0) lo = mid; else hi = mid;
+    const int R = b.R;
+    const int M = (int)w.bsc->n_pranges;  // ranges with pairs: pcg / pcoff[0, M), pcoff[M] = P
+    const int P = w.pcoff[M];
+    const int wave = threadIdx.x >> 6;
+    for (int Q0 = blockIdx.x * kFillPairs; Q0 < P; Q0 += gridDim.x * kFillPairs) {
+        // the compacted ranges holding this step's first and last pair (each range there has at
+        // least one pair, so at most kFillPairs of them), found by waves 0 and 1 side by side,
+        // then their first pairs and range ids staged in LDS
+        const int Q1 = min(P, Q0 + kFillPairs) - 1;
+        if (wave < 2) {
+            const int c = wave_last_le(w.pcoff, 0, M, wave == 0 ? Q0 : Q1);
+            if ((threadIdx.x & 63) == 0) s_c[wave] = c;
         }
-        int g = lo;
-        // the ranges of the thread's pairs first (consecutive pairs mostly share one range), then
-        // each dependent step of the pair filter for all of them at once: four chains of gathers
-        // in flight per thread instead of one after another (C3: 1.85M pairs per batch)
+        __syncthreads();
+        const int c0 = s_c[0], nc = s_c[1] - s_c[0] + 1;
+        for (int i = threadIdx.x; i <= nc; i += blockDim.x) {
+            s_off[i] = w.pcoff[c0 + i];
+            if (i < nc) s_g[i] = w.pcg[c0 + i];
+        }
+        __syncthreads();
+        // each dependent step of the pair filter for the thread's four pairs at once: four chains
+        // of gathers in flight per thread instead of one after another (C3: 1.85M pairs per batch)
         int gq[kPairsPerThread], kq[kPairsPerThread];
 #pragma unroll
         for (int u = 0; u < kPairsPerThread; u++) {
-            const int q = q0 + u;
+            const int q = Q0 + threadIdx.x * kPairsPerThread + u;
             gq[u] = -1;
             if (q >= P) continue;
-            if (w.poff[g + 1] <= q) {
-                // next range with pairs: gallop forward (ranges without pairs can run for thousands)
-                int step = 1, lo2 = g + 1, hi2 = g + 2;  // poff[lo2] <= q; find hi2 with poff[hi2] > q
-                while (hi2 < G && w.poff[hi2] <= q) {
-                    lo2 = hi2;
-                    step *= 2;
-                    hi2 = min(G, hi2 + step);
-                }
-                while (hi2 - lo2 > 1) {
-                    const int mid = (lo2 + hi2) >> 1;
-                    if (w.poff[mid] <= q) lo2 = mid; else hi2 = mid;
-                }
-                g = lo2;
+            int lo = 0, hi = nc;  // s_off[lo] <= q < s_off[hi]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_off[mid] <= q) lo = mid; else hi = mid;
             }
-            gq[u] = g;
-            kq[u] = q - w.poff[g];
+            gq[u] = s_g[lo];
+            kq[u] = q - s_off[lo];
         }
         // partner endpoint: read g's k-th write-begin inside it, or write g's k-th read-begin
         int part[kPairsPerThread];
@@ -1832,12 +1880,13 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
             const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
             if (slot < w.eoff[r + 1]) w.edges[slot] = tw[u];
         }
+        __syncthreads();  // the next step restages s_c / s_off / s_g
     }
 }
 
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    launch_scan<2, kEdgeScanP>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys}, nullptr, G, w.scan[kScanEdges]);
+    launch_scan<3, kEdgeScanP>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
         const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
         fdb_launch(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
@@ -2919,7 +2968,7 @@ int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int6
     (void)T;
     const int64_t E = 2 * (R + W);
     (void)E;
-    return kNumScans + scan_granules(R + W, 2, kEdgeScanP) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) +
+    return kNumScans + scan_granules(R + W, 3, kEdgeScanP) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) +
            scan_granules(hist_cap, 2) + 2 * scan_granules(2 * W, 1, kCombineP);
 }
 
@@ -2928,7 +2977,7 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     const int64_t E = 2 * (R + W);
     uint64_t* a = w.scan_arena;
     (void)E;
-    const int64_t gran[kNumScans] = {scan_granules(R + W, 2, kEdgeScanP), 3 * seg_prep_tiles(W),
+    const int64_t gran[kNumScans] = {scan_granules(R + W, 3, kEdgeScanP), 3 * seg_prep_tiles(W),
                                      scan_granules(delta_cap + 1, 2), scan_granules(hist_cap, 2),
                                      scan_granules(2 * W, 1, kCombineP), scan_granules(2 * W, 1, kCombineP)};
     uint64_t* g = a + kNumScans;

@@ -12,9 +12,13 @@
 //   __device__ void store(int64_t i, const uint32_t (&excl)[K]);   // exclusive prefixes of i
 //   __device__ void finish(const uint32_t (&total)[K]);            // once, by the last tile
 // Both visits of an element run on the same thread.  Sums are modulo 2^32, so +/-1 deltas work.
+// An F that declares `static constexpr bool kOwn = true` gets store(i, excl, own) instead, own =
+// element i's own counts (its inclusive minus exclusive prefixes).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "launch.h"
 
@@ -36,6 +40,11 @@ __device__ __forceinline__ void granule_store(uint64_t* g, uint32_t status, uint
 __device__ __forceinline__ uint64_t granule_load(const uint64_t* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+template <class F, class = void>
+struct scan_wants_own : std::false_type {};
+template <class F>
+struct scan_wants_own<F, std::void_t<decltype(F::kOwn)>> : std::true_type {};
 
 // Scan state for one launch: K granules per tile + the tile counter + an error word, zeroed
 // before the launch (one hipMemsetAsync covers every scan of a batch).
@@ -176,7 +185,15 @@ __device__ __forceinline__ void scan_tile(const F& f, int64_t n, int tile, int64
             uint32_t ex[K];
 #pragma unroll
             for (int c = 0; c < K; c++) ex[c] = sv[c][scan_slot(e)];
-            f.store(i, ex);
+            if constexpr (scan_wants_own<F>::value) {
+                uint32_t own[K];  // the next element's exclusive prefix (the tile's end for the last)
+#pragma unroll
+                for (int c = 0; c < K; c++)
+                    own[c] = (e + 1 < kScanThreads * P ? sv[c][scan_slot(e + 1)] : sbase[c] + btot[c]) - ex[c];
+                f.store(i, ex, own);
+            } else {
+                f.store(i, ex);
+            }
         }
     }
     if (tile == ntiles - 1 && threadIdx.x == 0) {

@@ -91,8 +91,8 @@ def kernel_bytes(name: str, s: dict):
                 "E slab items read; position, meta and 3 class prefixes written per endpoint; R+W begin lists")
     if name.startswith("k_scan<3, fdbcs::PosScan"):
         return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
-    if name.startswith("k_scan<2, fdbcs::EdgePairScan"):
-        return G * (8 + 24 + 8) + W * 8, "per range: 2 positions, class prefixes at both, slot/pair offsets"
+    if name.startswith("k_scan<3, fdbcs::EdgePairScan"):
+        return G * (8 + 24 + 8) + W * 8, "per range: 2 positions, class prefixes at both, slot/pair offsets (+ index of ranges with pairs)"
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
     if name == "k_resolve_pre":
