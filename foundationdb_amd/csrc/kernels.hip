@@ -827,6 +827,18 @@ __device__ __forceinline__ SortItem make_item(const BatchDev& b, int p) {
     return it;
 }
 
+// The last (up to) 8 bytes of a tail of tl bytes, big-endian.
+__device__ __forceinline__ uint64_t tail_last(const uint8_t* t, uint32_t tl) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (tl >= 8) return tail_word(t + tl - 8);
+    return tl ? tail_word(t) & (~0ull << (64 - 8 * tl)) : 0ull;
+#else
+    (void)t;
+    (void)tl;
+    return 0;
+#endif
+}
+
 // Total order used by the sort: KeyInfo::operator< (key, then class; SkipList.cpp:114-128) with the
 // endpoint id as a final tie-break.  Endpoints equal in (key, class) are interchangeable for every
 // later use, so the tie-break changes nothing observable; it makes every item distinct,
@@ -1427,26 +1439,36 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                     int st = k, en = k;
                     while (st > 0 && s_tie[wave][st - 1]) st--;
                     while (s_tie[wave][en]) en++;
-                    // The two endpoints of one range (a point range [k, k\0], a prefix range):
-                    // begin <= end holds for every admitted range, so keys of different lengths
-                    // order begin first without reading their tails; other pairs compare whole
-                    // keys.
+                    // The two endpoints of one range (a point range [k, k\0], a prefix range
+                    // [p\0, p\xff]): begin <= end holds for every admitted range, so keys that
+                    // differ at all order begin first — different lengths, or (equality needs no
+                    // order) different last tail words, one load each instead of the whole
+                    // tails.  Other pairs compare whole keys.
                     const int pm = ps[s];
-                    const uint32_t lme = b.keys[pm].len;
+                    const DKey kme = b.keys[pm];
                     int rank = 0;
                     bool need_me = false;
+                    uint32_t differ = 0;  // bit j - st: the same range's other endpoint, keys differ
                     for (int j = st; j <= en; j++) {
                         if (j == k) continue;
                         const int po = s_p[wave][j];
-                        if ((po >> 1) == (pm >> 1) && b.keys[po].len != lme) rank += (po & 1) ? 0 : 1;
-                        else need_me = true;
+                        if ((po >> 1) == (pm >> 1)) {
+                            const DKey ko = b.keys[po];
+                            const uint32_t tl = kme.len - 16u;  // tied keys are longer than 19 bytes
+                            if (ko.len != kme.len ||
+                                tail_last(b.tail + ko.tail, tl) != tail_last(b.tail + kme.tail, tl)) {
+                                rank += (po & 1) ? 0 : 1;
+                                if (j - st < 32) differ |= 1u << (j - st);
+                                continue;
+                            }
+                        }
+                        need_me = true;
                     }
                     if (need_me) {
                         const SortItem me = make_item(b, pm);
                         for (int j = st; j <= en; j++) {
-                            if (j == k) continue;
+                            if (j == k || (j - st < 32 && ((differ >> (j - st)) & 1u))) continue;
                             const int po = s_p[wave][j];
-                            if ((po >> 1) == (pm >> 1) && b.keys[po].len != lme) continue;
                             rank += item_less_total(make_item(b, po), me, b.tail) ? 1 : 0;
                         }
                     }
