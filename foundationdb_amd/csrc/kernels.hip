@@ -1448,7 +1448,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                     const DKey kme = b.keys[pm];
                     int rank = 0;
                     bool need_me = false;
-                    uint32_t differ = 0;  // bit j - st: the same range's other endpoint, keys differ
+                    int differ = -1;  // position of the same range's other endpoint when its key differs
                     for (int j = st; j <= en; j++) {
                         if (j == k) continue;
                         const int po = s_p[wave][j];
@@ -1458,7 +1458,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                             if (ko.len != kme.len ||
                                 tail_last(b.tail + ko.tail, tl) != tail_last(b.tail + kme.tail, tl)) {
                                 rank += (po & 1) ? 0 : 1;
-                                if (j - st < 32) differ |= 1u << (j - st);
+                                differ = j;  // (a range has one other endpoint)
                                 continue;
                             }
                         }
@@ -1467,7 +1467,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                     if (need_me) {
                         const SortItem me = make_item(b, pm);
                         for (int j = st; j <= en; j++) {
-                            if (j == k || (j - st < 32 && ((differ >> (j - st)) & 1u))) continue;
+                            if (j == k || j == differ) continue;
                             const int po = s_p[wave][j];
                             rank += item_less_total(make_item(b, po), me, b.tail) ? 1 : 0;
                         }
