@@ -761,7 +761,7 @@ def main():
             pass
         dist_info = {"world_size": world, "backend": args.backend, "rccl_version": rccl,
                      "routing": ("device: each rank packs its share of the global batch (proxy), H2D, all-gather of "
-                                 "the shares, fdbcs_batch_add_routed (k_route_mark, k_scan<RouteScan>, k_route_write) per resolver, "
+                                 "the shares, fdbcs_batch_add_routed (k_route_wait, k_route_mark, k_scan<RouteScan>, k_route_write) per resolver, "
                                  "inside the timed region" if droute else
                                  "host (balancing.BalancedRouting) before the timed region: a feature check, not a "
                                  "throughput figure"),
