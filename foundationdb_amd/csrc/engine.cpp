@@ -2340,6 +2340,13 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                     us(kTrBktBegin, kTrBktPrologue), us(kTrBktBegin, kTrBktSorted), us(kTrBktBegin, kTrBktTies),
                     us(kTrBktBegin, kTrBktEnd),
                     us(kTrPartBegin, kTrBktBegin));
+            {
+                const double nw = tr[kTrBktWaves] ? (double)tr[kTrBktWaves] : 1.0;
+                fprintf(stderr,
+                        "fdbcs trace: bucket per wave (%llu waves): load %.2f, sort %.2f, ties %.2f, put %.2f us\n",
+                        tr[kTrBktWaves], tr[kTrBktSumLoad] / nw / 100.0, tr[kTrBktSumSort] / nw / 100.0,
+                        tr[kTrBktSumTies] / nw / 100.0, tr[kTrBktSumPut] / nw / 100.0);
+            }
             fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
                     us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),
                     us(kTrResRounds, kTrResEnd));

@@ -241,6 +241,7 @@ enum TraceSlot {
     kTrResBegin, kTrResPre, kTrResWait, kTrResRounds, kTrResEnd,
     kTrPartBegin, kTrPartFill, kTrPartSearch, kTrPartEnd,
     kTrBktBegin, kTrBktPrologue, kTrBktSorted, kTrBktTies, kTrBktEnd,
+    kTrBktWaves, kTrBktSumLoad, kTrBktSumSort, kTrBktSumTies, kTrBktSumPut,  // per-wave sums (ticks)
     kTrCmbLoad, kTrCmbScan1, kTrCmbScan2, kTrCmbStore,
     kTrSlots
 };

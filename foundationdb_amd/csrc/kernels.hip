@@ -1370,6 +1370,8 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
     const int64_t base = s_base[wave][0];
     if (lane == 0) s_big[wave] = n > kSlab ? 1 : 0;
     if (bk < nb && n > 0 && n <= kSlab) {
+        const unsigned long long tw0 = a.trace ? wall_clock64() : 0ull;
+        unsigned long long tw1 = 0, tw2 = 0;
         // bytes every key of the bucket shares: those its bounding splitters share (none at the ends)
         // (batches of keys up to kSortNxLen bytes sort exactly on their first 19 bytes: no strip)
         uint32_t c = 0;
@@ -1395,10 +1397,12 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                 }
             }
         }
+        if (a.trace) tw1 = wall_clock64();
         if (S == 1) wave_bitonic<1>(kh, kl, ka);
         else if (S == 2) wave_bitonic<2>(kh, kl, ka);
         else wave_bitonic<4>(kh, kl, ka);
         if (lane == 0) trace_max(a.trace, kTrBktSorted);
+        if (a.trace) tw2 = wall_clock64();
         int ps[4];  // endpoint at each position (id bits of the tie-break word)
 #pragma unroll
         for (int s = 0; s < 4; s++) ps[s] = (int)(ka[s] & 0x3fffffffull);
@@ -1491,6 +1495,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             }
         }
         if (lane == 0) trace_max(a.trace, kTrBktTies);
+        const unsigned long long tw3 = a.trace ? wall_clock64() : 0ull;
         // positions, class counts before them, begin lists; quantiles for the next batch
         uint32_t carry[3] = {s_base[wave][1], s_base[wave][2], s_base[wave][3]};
 #pragma unroll
@@ -1516,6 +1521,15 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                 put_position(b, o, ps[s], base + k, (int32_t)ex[0], (int32_t)ex[1], (int32_t)ex[2]);
                 if (o.quant) put_quantiles(b, o.quant, base + k, E, ps[s]);
             }
+        }
+        if (a.trace && lane == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned long long tw4 = wall_clock64();
+            atomicAdd(&a.trace[kTrBktWaves], 1ull);
+            atomicAdd(&a.trace[kTrBktSumLoad], tw1 - tw0);
+            atomicAdd(&a.trace[kTrBktSumSort], tw2 - tw1);
+            atomicAdd(&a.trace[kTrBktSumTies], tw3 - tw2);
+            atomicAdd(&a.trace[kTrBktSumPut], tw4 - tw3);
         }
     }
     // ---- buckets past kSlab: ranked by the whole workgroup, one after another
