@@ -2346,6 +2346,12 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                         "fdbcs trace: bucket per wave (%llu waves): load %.2f, sort %.2f, ties %.2f, put %.2f us\n",
                         tr[kTrBktWaves], tr[kTrBktSumLoad] / nw / 100.0, tr[kTrBktSumSort] / nw / 100.0,
                         tr[kTrBktSumTies] / nw / 100.0, tr[kTrBktSumPut] / nw / 100.0);
+                const double np = tr[kTrPartWaves] ? (double)tr[kTrPartWaves] : 1.0;
+                fprintf(stderr,
+                        "fdbcs trace: partition per wave (%llu waves): fill %.2f, tail copy %.2f, search %.2f, "
+                        "place %.2f us\n",
+                        tr[kTrPartWaves], tr[kTrPartSumFill] / np / 100.0, tr[kTrPartSumCopy] / np / 100.0,
+                        tr[kTrPartSumSearch] / np / 100.0, tr[kTrPartSumPlace] / np / 100.0);
             }
             fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
                     us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),

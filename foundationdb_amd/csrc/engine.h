@@ -242,6 +242,7 @@ enum TraceSlot {
     kTrPartBegin, kTrPartFill, kTrPartSearch, kTrPartEnd,
     kTrBktBegin, kTrBktPrologue, kTrBktSorted, kTrBktTies, kTrBktEnd,
     kTrBktWaves, kTrBktSumLoad, kTrBktSumSort, kTrBktSumTies, kTrBktSumPut,  // per-wave sums (ticks)
+    kTrPartWaves, kTrPartSumFill, kTrPartSumCopy, kTrPartSumSearch, kTrPartSumPlace,
     kTrCmbLoad, kTrCmbScan1, kTrCmbScan2, kTrCmbStore,
     kTrSlots
 };

@@ -1115,6 +1115,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     const int E = 2 * (b.R + b.W), nb = a.nb, ns = nb - 1;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) trace_min(a.trace, kTrPartBegin);
+    const unsigned long long tp0 = a.trace ? wall_clock64() : 0ull;
     SortItem it{};
     if (p < E) it = make_item(b, p);  // in flight during the splitter fill
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
@@ -1124,6 +1125,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     }
     __syncthreads();
     if (threadIdx.x == 0) trace_max(a.trace, kTrPartFill);
+    const unsigned long long tp1 = a.trace ? wall_clock64() : 0ull;
     if (a.btail) {  // the batch tail region into the workspace copy, 8-byte words, strided over
         // EVERY thread of the grid (the tail region can hold many more words than endpoints)
         const int64_t nw = (a.btail_n + 7) / 8;
@@ -1134,6 +1136,11 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     if (p >= E) {
         if (a.trace) trace_max(a.trace, kTrPartEnd);
         return;
+    }
+    unsigned long long tp2 = 0;
+    if (a.trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tp2 = wall_clock64();
     }
     // splitters below my first two words: [0, lo); equal to them: [lo, up)
     int lo = 0, hi = ns;
@@ -1164,6 +1171,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
         bk = l;
     }
     if (a.trace) trace_max(a.trace, kTrPartSearch);
+    const unsigned long long tp3 = a.trace ? wall_clock64() : 0ull;
     const uint32_t cls = item_class(it.meta);
     const unsigned long long old =
         atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
@@ -1180,6 +1188,14 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     if (a.trace) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         trace_max(a.trace, kTrPartEnd);
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned long long tp4 = wall_clock64();
+            atomicAdd(&a.trace[kTrPartWaves], 1ull);
+            atomicAdd(&a.trace[kTrPartSumFill], tp1 - tp0);
+            atomicAdd(&a.trace[kTrPartSumCopy], tp2 - tp1);
+            atomicAdd(&a.trace[kTrPartSumSearch], tp3 - tp2);
+            atomicAdd(&a.trace[kTrPartSumPlace], tp4 - tp3);
+        }
     }
 }
 
