@@ -1110,100 +1110,10 @@ struct SortArgs {
     unsigned long long* trace;
 };
 
-__global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_spl[];  // [2 (nb - 1)]: first two key words
-    const int E = 2 * (b.R + b.W), nb = a.nb, ns = nb - 1;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (threadIdx.x == 0) trace_min(a.trace, kTrPartBegin);
-    const unsigned long long tp0 = a.trace ? wall_clock64() : 0ull;
-    SortItem it{};
-    if (p < E) it = make_item(b, p);  // in flight during the splitter fill
-    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
-        const SplitKey* sk = &a.quant[split_index(k, nb)];
-        s_spl[2 * k] = sk->w[0];
-        s_spl[2 * k + 1] = sk->w[1];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) trace_max(a.trace, kTrPartFill);
-    const unsigned long long tp1 = a.trace ? wall_clock64() : 0ull;
-    if (a.btail) {  // the batch tail region into the workspace copy, 8-byte words, strided over
-        // EVERY thread of the grid (the tail region can hold many more words than endpoints)
-        const int64_t nw = (a.btail_n + 7) / 8;
-        const uint64_t* src = (const uint64_t*)b.tail;
-        uint64_t* dst = (uint64_t*)a.btail;
-        for (int64_t q = p; q < nw; q += (int64_t)gridDim.x * blockDim.x) dst[q] = src[q];
-    }
-    if (p >= E) {
-        if (a.trace) trace_max(a.trace, kTrPartEnd);
-        return;
-    }
-    unsigned long long tp2 = 0;
-    if (a.trace) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        tp2 = wall_clock64();
-    }
-    // splitters below my first two words: [0, lo); equal to them: [lo, up)
-    int lo = 0, hi = ns;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
-        if (h < it.hi || (h == it.hi && l < it.lo)) lo = mid + 1; else hi = mid;
-    }
-    int up = lo;
-    hi = ns;
-    while (up < hi) {
-        const int mid = (up + hi) >> 1;
-        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
-        if (h < it.hi || (h == it.hi && l <= it.lo)) up = mid + 1; else hi = mid;
-    }
-    int bk = lo;
-    if (up > lo) {  // ties on 16 bytes (hot keys, shared prefixes): the rest of the window
-        uint64_t wv[kSplitWords];
-        wv[0] = it.hi;
-        wv[1] = it.lo;
-#pragma unroll
-        for (int i = 2; i < kSplitWords; i++) wv[i] = key_word(it.hi, it.lo, b.tail + it.tail, it.len, 8 * i);
-        int l = lo, h = up;  // splitters in [lo, up) not above my projection
-        while (l < h) {
-            const int mid = (l + h) >> 1;
-            if (split_cmp_rest(wv, it.len, it.meta, a.quant[split_index(mid, nb)]) >= 0) l = mid + 1; else h = mid;
-        }
-        bk = l;
-    }
-    if (a.trace) trace_max(a.trace, kTrPartSearch);
-    const unsigned long long tp3 = a.trace ? wall_clock64() : 0ull;
-    const uint32_t cls = item_class(it.meta);
-    const unsigned long long old =
-        atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
-    if (cls == kReadBegin || cls == kWriteEnd)
-        atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk + 1], cls == kReadBegin ? 1ull : 1ull << 32);
-    const uint32_t slot = (uint32_t)old;
-    if (slot < (uint32_t)kSlab) {
-        a.slab[(size_t)bk * kSlab + slot] = it;
-    } else {
-        const int o = atomicAdd(&a.bsc->ovf_n, 1);
-        a.ovf[o] = it;
-        a.ovf_b[o] = bk;
-    }
-    if (a.trace) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        trace_max(a.trace, kTrPartEnd);
-        if ((threadIdx.x & 63) == 0) {
-            const unsigned long long tp4 = wall_clock64();
-            atomicAdd(&a.trace[kTrPartWaves], 1ull);
-            atomicAdd(&a.trace[kTrPartSumFill], tp1 - tp0);
-            atomicAdd(&a.trace[kTrPartSumCopy], tp2 - tp1);
-            atomicAdd(&a.trace[kTrPartSumSearch], tp3 - tp2);
-            atomicAdd(&a.trace[kTrPartSumPlace], tp4 - tp3);
-        }
-    }
-}
-
-// k_sort_partition with PER endpoints per thread (coalesced: endpoint blockIdx.x * kBlock * PER +
-// u * kBlock + tid):
+// PER endpoints per thread (coalesced: endpoint blockIdx.x * kBlock * PER + u * kBlock + tid):
 // one splitter fill per workgroup serves PER x 256 endpoints (FDBCS_SORT_PART4=1: PER = 4).
 template <int PER>
-__global__ __launch_bounds__(kBlock) void k_sort_partition_n(BatchDev b, SortArgs a) {
+__global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_spl[];  // [2 (nb - 1)]: first two key words
     const int E = 2 * (b.R + b.W), nb = a.nb, ns = nb - 1;
     const int p0 = blockIdx.x * blockDim.x * PER + threadIdx.x;
@@ -1769,10 +1679,10 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
     }
     const SortArgs a = sort_args(w, quant, nb, b.tail_n);
     if (part4)
-        fdb_launch(k_sort_partition_n<4>, dim3((E + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), (uint32_t)(16 * (nb - 1)),
+        fdb_launch(k_sort_partition<4>, dim3((E + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), (uint32_t)(16 * (nb - 1)),
                    s, b, a);
     else
-        fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
+        fdb_launch(k_sort_partition<1>, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
     SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, validate ? w.items : nullptr,
               quant_out, w.big, w.big_p};
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
@@ -1803,10 +1713,10 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
         (void)hipMemsetAsync(&w.bsc->ovf_n, 0, 4, s);
         if (which == 1) (void)hipEventRecord(e0, s);
         if (part4)
-            fdb_launch(k_sort_partition_n<4>, dim3((E + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock),
+            fdb_launch(k_sort_partition<4>, dim3((E + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock),
                        (uint32_t)(16 * (nb - 1)), s, b, a);
         else
-            fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s,
+            fdb_launch(k_sort_partition<1>, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s,
                        b, a);
         if (which == 1) (void)hipEventRecord(e1, s);
         if (which == 2) (void)hipEventRecord(e0, s);
