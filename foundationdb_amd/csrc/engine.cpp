@@ -200,7 +200,6 @@ struct fdbcs_conflict_set {
     bool validate = false;  // FDBCS_VALIDATE=1: device-side invariant checks (tests)
     int bucket_target = 0;  // FDBCS_SORT_BUCKET: endpoints per sort bucket on average (0 = kSortTarget)
     bool sort_cold = false; // FDBCS_SORT_COLD=1: splitters from every batch's own samples (tests)
-    bool sort_part4 = false; // FDBCS_SORT_PART4=1: the partition takes 4 endpoints per thread
     DBuf quant;             // the sort's splitter source, two tables: quantiles of the last batch of
     int qcur = 0;           // >= kQuantMinE endpoints in table qcur; the next such batch writes the other
     bool quant_valid = false;
@@ -1070,7 +1069,6 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_VALIDATE")) cs->validate = v[0] == '1';
     if (const char* v = getenv("FDBCS_SORT_BUCKET")) cs->bucket_target = atoi(v);
     if (const char* v = getenv("FDBCS_SORT_COLD")) cs->sort_cold = v[0] == '1';
-    if (const char* v = getenv("FDBCS_SORT_PART4")) cs->sort_part4 = v[0] == '1';
     if (const char* v = getenv("FDBCS_TRACE")) cs->trace = v[0] == '1';
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
@@ -2101,7 +2099,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         SplitKey* qt = (SplitKey*)cs->quant.p;
         launch_sort(sa, bd, w, qt + cs->qcur * kQuant, write_quant ? qt + (cs->qcur ^ 1) * kQuant : nullptr, cold,
                     cs->bucket_target, b->max_len > (int32_t)kSortNxLen, cs->validate, rec(kPhSortBegin, 1),
-                    rec(kPhSortEnd, 1), cs->sort_part4);
+                    rec(kPhSortEnd, 1));
         if (write_quant) {
             cs->qcur ^= 1;
             cs->quant_valid = true;
@@ -2562,7 +2560,7 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     if (which >= 1) {  // the sort kernels
         if (!cs->quant_valid) return FDBCS_E_STATE;  // warm splitters only: detect a batch first
         HIPOK(debug_time_sort(cs->stream, b->bd, w, (SplitKey*)cs->quant.p + cs->qcur * kQuant, cs->bucket_target,
-                              b->max_len > (int32_t)kSortNxLen, which, reps, us_per_launch, cs->sort_part4));
+                              b->max_len > (int32_t)kSortNxLen, which, reps, us_per_launch));
         return FDBCS_OK;
     }
     hipEvent_t e0, e1;

@@ -343,8 +343,7 @@ struct PrevSegs {
 // receives this batch's quantiles for the next batch (null: keep).  long_keys: the batch has keys
 // longer than kSortNxLen (tail comparisons possible).
 void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
-                 int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end,
-                 bool part4 = false);
+                 int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end);
 // Buckets of a batch of E endpoints (target 0 = kSortTarget), within the workspace slab.
 int sort_bucket_count(int64_t E, int target, int slab_buckets);
 // D.CheckRead against the history the previous batch left.
@@ -360,7 +359,7 @@ void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Ti
 // Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
 // k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,
-                           bool long_keys, int which, int reps, double* us, bool part4 = false);
+                           bool long_keys, int which, int reps, double* us);
 // FDBCS_VALIDATE: the sorted endpoints are in order and the positions invert the permutation.
 void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w);
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w);

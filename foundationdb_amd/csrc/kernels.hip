@@ -1110,21 +1110,14 @@ struct SortArgs {
     unsigned long long* trace;
 };
 
-// PER endpoints per thread (coalesced: endpoint blockIdx.x * kBlock * PER + u * kBlock + tid):
-// one splitter fill per workgroup serves PER x 256 endpoints (FDBCS_SORT_PART4=1: PER = 4).
-template <int PER>
 __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_spl[];  // [2 (nb - 1)]: first two key words
     const int E = 2 * (b.R + b.W), nb = a.nb, ns = nb - 1;
-    const int p0 = blockIdx.x * blockDim.x * PER + threadIdx.x;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) trace_min(a.trace, kTrPartBegin);
     const unsigned long long tp0 = a.trace ? wall_clock64() : 0ull;
-    SortItem its[PER];
-#pragma unroll
-    for (int u = 0; u < PER; u++) {
-        its[u] = SortItem{};
-        if (p0 + u * (int)blockDim.x < E) its[u] = make_item(b, p0 + u * (int)blockDim.x);  // in flight during the fill
-    }
+    SortItem it{};
+    if (p < E) it = make_item(b, p);  // in flight during the splitter fill
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
         const SplitKey* sk = &a.quant[split_index(k, nb)];
         s_spl[2 * k] = sk->w[0];
@@ -1138,10 +1131,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
         const int64_t nw = (a.btail_n + 7) / 8;
         const uint64_t* src = (const uint64_t*)b.tail;
         uint64_t* dst = (uint64_t*)a.btail;
-        for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += (int64_t)gridDim.x * blockDim.x)
-            dst[q] = src[q];
+        for (int64_t q = p; q < nw; q += (int64_t)gridDim.x * blockDim.x) dst[q] = src[q];
     }
-    if (p0 >= E) {
+    if (p >= E) {
         if (a.trace) trace_max(a.trace, kTrPartEnd);
         return;
     }
@@ -1150,66 +1142,48 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         tp2 = wall_clock64();
     }
-    int bks[PER];
+    // splitters below my first two words: [0, lo); equal to them: [lo, up)
+    int lo = 0, hi = ns;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
+        if (h < it.hi || (h == it.hi && l < it.lo)) lo = mid + 1; else hi = mid;
+    }
+    int up = lo;
+    hi = ns;
+    while (up < hi) {
+        const int mid = (up + hi) >> 1;
+        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
+        if (h < it.hi || (h == it.hi && l <= it.lo)) up = mid + 1; else hi = mid;
+    }
+    int bk = lo;
+    if (up > lo) {  // ties on 16 bytes (hot keys, shared prefixes): the rest of the window
+        uint64_t wv[kSplitWords];
+        wv[0] = it.hi;
+        wv[1] = it.lo;
 #pragma unroll
-    for (int u = 0; u < PER; u++) {
-        const SortItem& it = its[u];
-        bks[u] = -1;
-        if (p0 + u * (int)blockDim.x >= E) continue;
-        // splitters below my first two words: [0, lo); equal to them: [lo, up)
-        int lo = 0, hi = ns;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
-            if (h < it.hi || (h == it.hi && l < it.lo)) lo = mid + 1; else hi = mid;
+        for (int i = 2; i < kSplitWords; i++) wv[i] = key_word(it.hi, it.lo, b.tail + it.tail, it.len, 8 * i);
+        int l = lo, h = up;  // splitters in [lo, up) not above my projection
+        while (l < h) {
+            const int mid = (l + h) >> 1;
+            if (split_cmp_rest(wv, it.len, it.meta, a.quant[split_index(mid, nb)]) >= 0) l = mid + 1; else h = mid;
         }
-        int up = lo;
-        hi = ns;
-        while (up < hi) {
-            const int mid = (up + hi) >> 1;
-            const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
-            if (h < it.hi || (h == it.hi && l <= it.lo)) up = mid + 1; else hi = mid;
-        }
-        int bk = lo;
-        if (up > lo) {  // ties on 16 bytes (hot keys, shared prefixes): the rest of the window
-            uint64_t wv[kSplitWords];
-            wv[0] = it.hi;
-            wv[1] = it.lo;
-#pragma unroll
-            for (int i = 2; i < kSplitWords; i++) wv[i] = key_word(it.hi, it.lo, b.tail + it.tail, it.len, 8 * i);
-            int l = lo, h = up;  // splitters in [lo, up) not above my projection
-            while (l < h) {
-                const int mid = (l + h) >> 1;
-                if (split_cmp_rest(wv, it.len, it.meta, a.quant[split_index(mid, nb)]) >= 0) l = mid + 1; else h = mid;
-            }
-            bk = l;
-        }
-        bks[u] = bk;
+        bk = l;
     }
     if (a.trace) trace_max(a.trace, kTrPartSearch);
     const unsigned long long tp3 = a.trace ? wall_clock64() : 0ull;
-    unsigned long long olds[PER];
-#pragma unroll
-    for (int u = 0; u < PER; u++) {  // the slot reservations of the thread's endpoints in flight together
-        olds[u] = 0;
-        if (bks[u] < 0) continue;
-        const uint32_t cls = item_class(its[u].meta);
-        olds[u] = atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bks[u]],
-                            1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
-        if (cls == kReadBegin || cls == kWriteEnd)
-            atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bks[u] + 1], cls == kReadBegin ? 1ull : 1ull << 32);
-    }
-#pragma unroll
-    for (int u = 0; u < PER; u++) {
-        if (bks[u] < 0) continue;
-        const uint32_t slot = (uint32_t)olds[u];
-        if (slot < (uint32_t)kSlab) {
-            a.slab[(size_t)bks[u] * kSlab + slot] = its[u];
-        } else {
-            const int o = atomicAdd(&a.bsc->ovf_n, 1);
-            a.ovf[o] = its[u];
-            a.ovf_b[o] = bks[u];
-        }
+    const uint32_t cls = item_class(it.meta);
+    const unsigned long long old =
+        atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
+    if (cls == kReadBegin || cls == kWriteEnd)
+        atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk + 1], cls == kReadBegin ? 1ull : 1ull << 32);
+    const uint32_t slot = (uint32_t)old;
+    if (slot < (uint32_t)kSlab) {
+        a.slab[(size_t)bk * kSlab + slot] = it;
+    } else {
+        const int o = atomicAdd(&a.bsc->ovf_n, 1);
+        a.ovf[o] = it;
+        a.ovf_b[o] = bk;
     }
     if (a.trace) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1660,8 +1634,7 @@ static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb, int64_t 
 }
 
 void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
-                 int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end,
-                 bool part4) {
+                 int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end) {
     const int E = 2 * (b.R + b.W);
     if (E == 0) return;
     const int nb = sort_bucket_count(E, bucket_target, w.slab_buckets);
@@ -1678,11 +1651,7 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
                    c.S, quant);
     }
     const SortArgs a = sort_args(w, quant, nb, b.tail_n);
-    if (part4)
-        fdb_launch(k_sort_partition<4>, dim3((E + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock), (uint32_t)(16 * (nb - 1)),
-                   s, b, a);
-    else
-        fdb_launch(k_sort_partition<1>, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
+    fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
     SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, validate ? w.items : nullptr,
               quant_out, w.big, w.big_p};
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
@@ -1697,7 +1666,7 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
 // k_sort_bucket (warm splitters) over `reps` runs of the sort on an idle stream; the zeroed
 // scratch is reset before each run, outside the timing.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,
-                           bool long_keys, int which, int reps, double* us, bool part4) {
+                           bool long_keys, int which, int reps, double* us) {
     const int E = 2 * (b.R + b.W);
     if (E == 0) return hipErrorInvalidValue;
     const int nb = sort_bucket_count(E, bucket_target, w.slab_buckets);
@@ -1712,12 +1681,7 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
         (void)hipMemsetAsync(w.scnt, 0, 8 * kCntStride * (size_t)kSortMaxBuckets, s);
         (void)hipMemsetAsync(&w.bsc->ovf_n, 0, 4, s);
         if (which == 1) (void)hipEventRecord(e0, s);
-        if (part4)
-            fdb_launch(k_sort_partition<4>, dim3((E + 4 * kBlock - 1) / (4 * kBlock)), dim3(kBlock),
-                       (uint32_t)(16 * (nb - 1)), s, b, a);
-        else
-            fdb_launch(k_sort_partition<1>, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s,
-                       b, a);
+        fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
         if (which == 1) (void)hipEventRecord(e1, s);
         if (which == 2) (void)hipEventRecord(e0, s);
         if (long_keys)

@@ -84,7 +84,7 @@ def kernel_bytes(name: str, s: dict):
         return E * (2 + D + I) + nb * 8, "E (bucket id + key) read, E items written"
     if name.startswith("k_bucket_sort"):
         return 2 * I * E, "one read and one write of every 32-byte item"
-    if name.startswith("k_sort_partition"):
+    if name == "k_sort_partition":
         return E * (D + I + 8) + nb * 16, "E keys read, E 32-byte items written to their bucket slabs, a counter word each"
     if name.startswith("k_sort_bucket"):
         return (E * (I + 4 + 4 + 12) + G * 4 + nb * 16,

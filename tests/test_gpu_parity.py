@@ -573,7 +573,7 @@ def test_empty_batches(engine, oracle_mod):
 # Every engine knob that selects a different kernel or submission path (DESIGN.md §5 "Engine knobs")
 # is parity-tested here; knobs measured slower and not kept were deleted with their code.
 @pytest.mark.parametrize("knobs", [{"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
-                                   {"FDBCS_SORT_COLD": "1"}, {"FDBCS_SORT_PART4": "1"},
+                                   {"FDBCS_SORT_COLD": "1"},
                                    {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
                                    {"FDBCS_GRAPH": "3"}, {"FDBCS_GRAPH": "3", "FDBCS_SPLIT_CHECK": "1"},
