@@ -32,6 +32,7 @@ FDBCS_E_NOMEM = -3
 FDBCS_E_VERSION = -4
 FDBCS_E_STATE = -5
 FDBCS_E_NODEVICE = -6
+FDBCS_E_TIMEOUT = -7
 
 TransactionConflict = 0
 TransactionTooOld = 1
@@ -197,6 +198,19 @@ def _check(rc: int, what: str) -> None:
 
 def _p(a: np.ndarray):
     return ctypes.c_void_p(a.ctypes.data if a.size else 0)
+
+
+def fill_verdict_lists(verdicts: np.ndarray, non_conflicting: Optional[List[int]],
+                       too_old_transactions: Optional[List[int]]) -> None:
+    """The verdict lists of detectConflicts (SkipList.cpp:869-876) from the verdict bytes.
+
+    A TooOld transaction's conflict status is set to true (`conflict = tr.tooOld`,
+    SkipList.cpp:820,830), so without a tooOld list it lands in neither list."""
+    v = np.asarray(verdicts)
+    if too_old_transactions is not None:
+        too_old_transactions.extend(np.flatnonzero(v == TransactionTooOld).tolist())
+    if non_conflicting is not None:
+        non_conflicting.extend(np.flatnonzero(v == TransactionCommitted).tolist())
 
 
 class ConflictSet:
@@ -441,13 +455,7 @@ class ConflictBatch:
         rc = load_library().fdbcs_batch_detect_conflicts(self._h, now, new_oldest_version, _p(v), None, None)
         _check(rc, "detectConflicts")
         self.verdicts = v
-        for t in range(self.transaction_count):
-            if too_old_transactions is not None and v[t] == TransactionTooOld:
-                too_old_transactions.append(t)
-            elif v[t] != TransactionConflict and non_conflicting is not None:
-                # a TooOld transaction registered no ranges, so its conflict status is false: without
-                # a tooOld list the reference counts it as non-conflicting (SkipList.cpp:869-876)
-                non_conflicting.append(t)
+        fill_verdict_lists(v, non_conflicting, too_old_transactions)
         self._collect_conflicting_keys()
         return v
 

@@ -187,6 +187,7 @@ struct fdbcs_conflict_set {
     int64_t tail_ub = 0;
     int64_t tail_cap = 0;
     DBuf scal;  // Scalars
+    int64_t route_timeout_ms = 60000;  // FDBCS_ROUTE_TIMEOUT_MS: bound of a routed batch's wait for its shares
     DBuf route_btail;                  // device routing: tails of this resolver's key-range bounds
     std::vector<uint8_t> route_bounds; // the bounds route_btail holds (lo | hi bytes), to skip re-uploads
     // batch workspaces (rotating)
@@ -203,6 +204,10 @@ struct fdbcs_conflict_set {
     DBuf quant;             // the sort's splitter source, two tables: quantiles of the last batch of
     int qcur = 0;           // >= kQuantMinE endpoints in table qcur; the next such batch writes the other
     bool quant_valid = false;
+    // the stream of the last stage A (its sort read one splitter table and wrote the other): a batch
+    // whose stage A runs on another stream (a timing-level change) waits for ev_quant recorded there
+    hipStream_t quant_sa = nullptr;
+    hipEvent_t ev_quant = nullptr;
     int64_t sort_big_buckets = 0;  // buckets past kSlab so far (host view, from the published scalars)
     bool trace = false;     // FDBCS_TRACE=1: device timestamps of kernel sections printed per batch
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
@@ -329,7 +334,7 @@ struct fdbcs_batch {
     bool any_report = false;
     int64_t check_hist = 0;  // boundaries (both tiers, upper bound) the read check searched
     std::vector<int32_t> out_ids;  // fdbcs_batch_set_conflict_output: global index per transaction
-    int32_t out_n = 0;
+    int64_t out_n = 0;
     uint8_t* out_dev = nullptr;
     int wp = 0;           // the workspace this batch's detect used
     int32_t max_len = 0;  // longest key added (the sort stages tail windows only past kSortNxLen)
@@ -1052,6 +1057,7 @@ const char* fdbcs_strerror(int s) {
         case FDBCS_E_VERSION: return "version below the history's newest version";
         case FDBCS_E_STATE: return "call out of order";
         case FDBCS_E_NODEVICE: return "no HIP device";
+        case FDBCS_E_TIMEOUT: return "routed batch: the shares were never ready";
         default: return "unknown status";
     }
 }
@@ -1083,6 +1089,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : 6;
     if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
+    if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));
     static std::once_flag attr_once;
     std::call_once(attr_once, init_kernel_attributes);
     bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
@@ -1090,7 +1097,8 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
               hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&cs->cstream, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&cs->ev_quant, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < kNumWork && ok; k++)
         ok = hipEventCreateWithFlags(&cs->ev_a[k], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&cs->ev_c[k], hipEventDisableTiming) == hipSuccess &&
@@ -1175,6 +1183,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     if (cs->ustream) (void)hipStreamDestroy(cs->ustream);
     if (cs->cstream) (void)hipStreamDestroy(cs->cstream);
     if (cs->ev_cmp) (void)hipEventDestroy(cs->ev_cmp);
+    if (cs->ev_quant) (void)hipEventDestroy(cs->ev_quant);
     if (cs->astream) (void)hipStreamDestroy(cs->astream);
     if (cs->stream) (void)hipStreamDestroy(cs->stream);
     if (cs->ystream) (void)hipStreamDestroy(cs->ystream);
@@ -1794,7 +1803,6 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     a.stride = stride;
     a.n_shares = n_shares;
     a.tcap = std::max(1, max_share_txns);
-    a.oldest = cs->oldest;  // addTransaction's TooOld test (SkipList.cpp:770) at add time
     a.report_enabled = 0;  // conflicting-key reports go through the host-routed path (sharding.py)
     a.cap_T = cap_txns;
     a.cap_R = cap_reads;
@@ -1812,6 +1820,7 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     a.flags = (uint8_t*)(d + L.flags);
     a.tail = (uint8_t*)(d + L.tail);
     a.inv = (int32_t*)sl->rt_inv.p;
+    a.inv_n = std::max<int64_t>(n_elems, 1);
     a.read_ids = (int32_t*)sl->rt_rids.p;
     a.out_zero = conflict_out;
     a.out_n = n_global;
@@ -1823,9 +1832,12 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     // batch may still read its device buffer
     a.ready = ready_flag;
     a.ready_value = ready_value;
+    a.wait_ticks = (uint64_t)cs->route_timeout_ms * 100000ull;  // 100 MHz wall clock
     a.wait_err = (uint32_t*)((uint64_t*)sl->rt_scan.p + 2);
     if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
     HIPOK(hipMemsetAsync(sl->rt_scan.p, 0, 8 * (size_t)route_scan_words(n_elems), us));
+    // global indices past the shares' transactions stay "not routed here"
+    HIPOK(hipMemsetAsync(sl->rt_inv.p, 0xFF, 4 * (size_t)a.inv_n, us));
     uint64_t* sw = (uint64_t*)sl->rt_scan.p;
     ScanState st{sw + 8, (int*)sw, (int*)(sw + 1)};
     t_record = nullptr;
@@ -1848,7 +1860,7 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     b->route_pending = true;
     b->rT = b->rR = b->rW = 0;
     b->out_dev = conflict_out;
-    b->out_n = (int32_t)n_global;
+    b->out_n = n_global;
     b->out_ids.clear();
     b->state = 1;
     return FDBCS_OK;
@@ -1863,8 +1875,15 @@ static int finish_route(fdbcs_batch* b) {
     RouteResult r;
     memcpy(&r, (const void*)sl->rt_res.p, sizeof(r));
     if (r.error != 0) {
-        if (r.error == 2) fprintf(stderr, "fdbcs: routed batch: the shares' ready flag was never set\n");
-        return r.error == 1 ? FDBCS_E_NOMEM : FDBCS_E_DEVICE;
+        if (r.error == 2) {  // the shares never arrived: nothing was placed, the batch can be routed again
+            fprintf(stderr, "fdbcs: routed batch: the shares' ready flag was never set\n");
+            b->routed = b->route_pending = false;
+            b->out_dev = nullptr;
+            b->out_n = 0;
+            b->state = 0;
+            return FDBCS_E_TIMEOUT;
+        }
+        return r.error == 1 ? FDBCS_E_NOMEM : r.error == 3 ? FDBCS_E_INVALID : FDBCS_E_DEVICE;
     }
     b->rT = r.T;
     b->rR = r.R;
@@ -2051,6 +2070,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (own_upload || (was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess))
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sa);
     const BatchDev& bd = b->bd;
+    // a routed batch's TooOld test (SkipList.cpp:770) against the oldest version every earlier
+    // detect left (its routing may have run before the previous batch's detect): stage A, ahead
+    // of every kernel that reads the flags (stage B)
+    if (b->routed) launch_route_too_old(sa, bd, cs->oldest);
     // long-key probes pay off once tails run past a word (a 17-byte end key k\0 of a 16-byte key
     // ties on the prefix with k only, and the length decides)
     const bool long_keys = cs->long_probe && b->max_len > 24;
@@ -2097,6 +2120,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         const bool cold = nbk > 1 && (cs->sort_cold || !cs->quant_valid);
         const bool write_quant = E >= kQuantMinE;
         SplitKey* qt = (SplitKey*)cs->quant.p;
+        if (cs->quant_sa && cs->quant_sa != sa) {
+            // the splitter tables were last read and written by a sort on another stream: order
+            // this sort after it (every stage A before this one has been issued: flush the helper)
+            if ((rc = flush_pending(cs))) return rc;
+            HIPOK(hipEventRecord(cs->ev_quant, cs->quant_sa));
+            fdb_event(LaunchList::kSyncWait, cs->ev_quant, sa);
+        }
+        cs->quant_sa = sa;
         launch_sort(sa, bd, w, qt + cs->qcur * kQuant, write_quant ? qt + (cs->qcur ^ 1) * kQuant : nullptr, cold,
                     cs->bucket_target, b->max_len > (int32_t)kSortNxLen, cs->validate, rec(kPhSortBegin, 1),
                     rec(kPhSortEnd, 1));

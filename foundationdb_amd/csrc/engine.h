@@ -278,8 +278,10 @@ struct RouteResult {
     int32_t T, R, W, reports;
     int32_t n_gt19, n_gt24;  // kept keys longer than 19 / 24 bytes (sort tail windows, long-key probes)
     int64_t tail_bytes;
-    int32_t error;           // 1: a capacity bound was exceeded (nothing past it was written)
+    int32_t error;           // 1: a capacity bound was exceeded (nothing past it was written); 2: the
+                             // shares' ready flag was never set; 3: conflict output size != global T
     int32_t pad;
+    int64_t global_T;        // transactions of all shares
 };
 struct RouteArgs {
     const uint8_t* shares;  // n_shares shares, `stride` bytes apart
@@ -288,7 +290,6 @@ struct RouteArgs {
     int32_t has_lo, has_hi;  // this resolver owns [lo, hi): lo absent for the first, hi for the last
     DKey lo, hi;
     const uint8_t* btail;    // tails of lo / hi
-    int64_t oldest;          // TooOld test (SkipList.cpp:770) at add time
     int32_t report_enabled;
     int32_t cap_T, cap_R, cap_W;  // capacity of the output layout
     int64_t cap_tail;
@@ -301,7 +302,8 @@ struct RouteArgs {
     int64_t* snap;
     uint8_t* flags;
     uint8_t* tail;
-    int32_t* inv;       // [global T] batch index of each global transaction, -1 if not routed here
+    int32_t* inv;       // [inv_n] batch index of each global transaction, -1 if not routed here
+    int64_t inv_n;      // n_shares * tcap (every global index fits)
     int32_t* read_ids;  // [R'] index of each kept read in its transaction (txReadConflictRangeIndexMap)
     uint8_t* out_zero;  // conflict output to zero for this batch (or null), out_n global transactions
     int64_t out_n;
@@ -310,11 +312,14 @@ struct RouteArgs {
     const uint32_t* ready;  // device word the caller's stream sets to ready_value once the shares are
     uint32_t ready_value;   // gathered (null: already complete); k_route_wait spins on it
     uint32_t* wait_err;     // set when that wait timed out (the routed batch then reports an error)
+    uint64_t wait_ticks;    // bound of that wait, in 100 MHz wall-clock ticks
 };
 // Route the all-gathered shares into this resolver's batch (two launches on `s`).  grid_n: bound
 // on n_shares * tcap (global elements); the scan state's granules are zeroed by the caller.
 void launch_route(hipStream_t s, const RouteArgs& a, ScanState st);
 int64_t route_scan_words(int64_t n_elems);
+// TooOld (SkipList.cpp:770) of a routed batch against the oldest version at detect time.
+void launch_route_too_old(hipStream_t s, const BatchDev& b, int64_t oldest);
 
 // ---- launchers (kernels.hip); all enqueue on `s` and never synchronize.
 // A history tier as the read check sees it.

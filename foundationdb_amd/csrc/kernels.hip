@@ -3050,8 +3050,10 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
 // gets a sub-transaction only on resolvers that received one of its ranges (:107-116), with its
 // snapshot and report flag (:181-186).  Here every resolver routes the all-gathered shares for
 // itself: one scan over the global transactions (one element each, its ranges visited by its
-// thread) counts what this resolver keeps and its store places it; TooOld (SkipList.cpp:770) is
-// applied to the sub-transaction as addTransaction would (its ranges are dropped).
+// thread) counts what this resolver keeps and its store places it.  TooOld (SkipList.cpp:770) is
+// decided when the batch is detected (k_route_too_old), against the oldest version every earlier
+// detect left: routing runs ahead of the previous batch's detect, and the Resolver adds a batch only
+// after the previous one is resolved (Resolver.actor.cpp:139-150, 179-194).
 
 __device__ __forceinline__ const ShareHeader* share_at(const RouteArgs& a, int p) {
     return (const ShareHeader*)(a.shares + (int64_t)p * a.stride);
@@ -3060,18 +3062,22 @@ __device__ __forceinline__ const ShareHeader* share_at(const RouteArgs& a, int p
 // The shares are written by another HIP runtime (torch's collectives load their own), whose
 // streams this engine cannot wait on: the caller's stream sets a device word once the all-gather
 // is complete, and one wave here polls it (agent scope, bounded) before the routing kernels.
-__global__ void k_route_wait(const uint32_t* ready, uint32_t value, uint32_t* err) {
+// The wait is bounded by `timeout_ticks` of the 100 MHz constant clock (wall_clock64): never hang
+// the GPU, but outlast a slow all-gather (the communicator's first call, a straggler rank).
+__global__ void k_route_wait(const uint32_t* ready, uint32_t value, uint32_t* err, uint64_t timeout_ticks) {
     if (threadIdx.x != 0) return;
     if (ready) {
-        for (uint32_t spin = 0; spin < (1u << 24); spin++) {
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
             if (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == value) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 *err = 0;
                 return;
             }
-            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > timeout_ticks) break;
+            __builtin_amdgcn_s_sleep(16);
         }
-        *err = 1;  // bounded: never hang the GPU
+        *err = 1;
         return;
     }
     *err = 0;
@@ -3113,7 +3119,7 @@ struct RouteScan {
         return h;
     }
     // counts: sub-transaction, kept reads, kept writes, kept tail bytes, ranges with a key > 19 / > 24 bytes
-    __device__ bool visit(int64_t i, uint32_t (&v)[6], bool& any, bool& too_old, int& p, int& t, int64_t& gid,
+    __device__ bool visit(int64_t i, uint32_t (&v)[6], bool& any, int& p, int& t, int64_t& gid,
                           const ShareHeader*& h) const {
         h = at(i, p, t, gid);
         if (!h) return false;
@@ -3140,10 +3146,8 @@ struct RouteScan {
             g24 += (x >> 2) & 1u;
         }
         any = nr + nw > 0;
-        too_old = any && nr > 0 && ((const int64_t*)(base + h->off_snap))[t] < a.oldest;
         if (!any) return true;
         v[0] = 1;
-        if (too_old) return true;  // TooOld (SkipList.cpp:770): a sub-transaction without ranges
         v[1] = nr;
         v[2] = nw;
         v[3] = tl;
@@ -3152,33 +3156,35 @@ struct RouteScan {
         return true;
     }
     __device__ void load(int64_t i, uint32_t (&v)[6]) const {
-        bool any, too_old;
+        bool any;
         int p, t;
         int64_t gid;
         const ShareHeader* h;
-        visit(i, v, any, too_old, p, t, gid, h);
+        visit(i, v, any, p, t, gid, h);
     }
     __device__ void store(int64_t i, const uint32_t (&ex)[6]) const {
         uint32_t v[6] = {0, 0, 0, 0, 0, 0};
-        bool any, too_old;
+        bool any;
         int p, t;
         int64_t gid;
         const ShareHeader* h;
-        if (!visit(i, v, any, too_old, p, t, gid, h)) return;
-        if (a.out_zero) a.out_zero[gid] = 0;
+        if (!visit(i, v, any, p, t, gid, h)) return;
+        if (a.out_zero && gid < a.out_n) a.out_zero[gid] = 0;
         const int lt = (int)ex[0];
         const bool fits = any && lt < a.cap_T;
-        a.inv[gid] = fits ? lt : -1;
-        a.txpre[i] = make_int4(fits ? lt : -1, too_old ? -1 : (int)ex[1], (int)ex[2], (int)ex[3]);
+        if (gid < a.inv_n) a.inv[gid] = fits ? lt : -1;
+        a.txpre[i] = make_int4(fits ? lt : -1, (int)ex[1], (int)ex[2], (int)ex[3]);
         if (!fits) return;
         const uint8_t* base = (const uint8_t*)h;
         a.snap[lt] = ((const int64_t*)(base + h->off_snap))[t];
-        a.flags[lt] = too_old ? kFlagTooOld : 0;
+        a.flags[lt] = 0;  // TooOld is decided when the batch is detected (k_route_too_old)
         a.roff[lt] = (int32_t)ex[1];
         a.woff[lt] = (int32_t)ex[2];
     }
     __device__ void finish(const uint32_t (&tot)[6]) const {
         RouteResult r{};
+        if (!*a.wait_err)
+            for (int q = 0; q < a.n_shares; q++) r.global_T += share_at(a, q)->T;
         r.T = (int32_t)tot[0];
         r.R = (int32_t)tot[1];
         r.W = (int32_t)tot[2];
@@ -3187,6 +3193,7 @@ struct RouteScan {
         r.n_gt24 = (int32_t)tot[5];
         r.error = (r.T > a.cap_T || r.R > a.cap_R || r.W > a.cap_W || (int64_t)tot[3] > a.cap_tail) ? 1 : 0;
         if (*a.wait_err) r.error = 2;
+        if (!r.error && a.out_zero && r.global_T != a.out_n) r.error = 3;  // conflict bytes for every global txn
         if (!r.error) {
             a.roff[r.T] = r.R;
             a.woff[r.T] = r.W;
@@ -3212,7 +3219,7 @@ __global__ __launch_bounds__(kBlock) void k_route_write(RouteArgs a) {
     const uint8_t* base = (const uint8_t*)h;
     const int t = ((const int32_t*)(base + h->off_owner))[j];
     const int4 pre = a.txpre[(int64_t)p * a.tcap + t];
-    if (pre.x < 0 || pre.y < 0) return;  // not placed, or TooOld
+    if (pre.x < 0) return;  // not placed
     const int32_t* roff = (const int32_t*)(base + h->off_roff);
     const int32_t* woff = (const int32_t*)(base + h->off_woff);
     const bool is_read = j < h->R;
@@ -3252,11 +3259,27 @@ __global__ __launch_bounds__(kBlock) void k_route_write(RouteArgs a) {
     }
 }
 
+// TooOld of a routed batch's sub-transactions (SkipList.cpp:770: snapshot below the oldest version
+// with at least one read), decided at detect time in stage A; every kernel that reads the flags
+// runs in stage B.  A TooOld sub-transaction keeps its ranges here, unlike addTransaction's: its
+// status is aborted from the start, so its writes never enter the MiniConflictSet or the history,
+// and its endpoints do not change any other range's answer (overlap is a key-order question).
+__global__ __launch_bounds__(kBlock) void k_route_too_old(BatchDev b, int64_t oldest) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.T) return;
+    if (b.roff[t + 1] > b.roff[t] && b.snap[t] < oldest) b.flags[t] |= kFlagTooOld;
+}
+
+void launch_route_too_old(hipStream_t s, const BatchDev& b, int64_t oldest) {
+    if (b.T <= 0) return;
+    fdb_launch(k_route_too_old, dim3((unsigned)((b.T + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, b, oldest);
+}
+
 int64_t route_scan_words(int64_t n_elems) { return 8 + scan_granules(n_elems, 6, kRouteScanP); }
 
 void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
     const dim3 grid((unsigned)std::max<int64_t>(1, (a.rstride + kBlock - 1) / kBlock), (unsigned)a.n_shares);
-    fdb_launch(k_route_wait, dim3(1), dim3(64), 0, s, a.ready, a.ready_value, a.wait_err);
+    fdb_launch(k_route_wait, dim3(1), dim3(64), 0, s, a.ready, a.ready_value, a.wait_err, a.wait_ticks);
     fdb_launch(k_route_mark, grid, dim3(kBlock), 0, s, a);
     launch_scan<6, kRouteScanP>(s, RouteScan{a}, nullptr, (int64_t)a.n_shares * a.tcap, st);
     fdb_launch(k_route_write, grid, dim3(kBlock), 0, s, a);

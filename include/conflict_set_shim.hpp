@@ -111,11 +111,14 @@ struct ConflictBatchT {
         verdicts.assign(report.size(), 0);
         fdbcs_shim::check(fdbcs_batch_detect_conflicts(b, now, newOldestVersion, verdicts.data(), nullptr, nullptr),
                           "detectConflicts");
+        // A TooOld transaction's conflict status is set to true (`conflict = tr.tooOld`,
+        // SkipList.cpp:820,830), so without a tooOld list it lands in neither list (:869-876).
         for (int i = 0; i < (int)verdicts.size(); i++) {
-            if (tooOldTransactions && verdicts[i] == TransactionTooOld)
-                tooOldTransactions->push_back(i);
-            else if (verdicts[i] != TransactionConflict)  // TooOld lands here without a tooOld list:
-                nonConflicting.push_back(i);               // its conflict status stays false (:869-876)
+            if (verdicts[i] == TransactionTooOld) {
+                if (tooOldTransactions) tooOldTransactions->push_back(i);
+            } else if (verdicts[i] == TransactionCommitted) {
+                nonConflicting.push_back(i);
+            }
         }
         if (map) {
             std::vector<int32_t> idx;

@@ -44,6 +44,7 @@ extern "C" {
 #define FDBCS_E_VERSION (-4)   /* `now` below a version already present in the history */
 #define FDBCS_E_STATE (-5)     /* call out of order (e.g. add after detect) */
 #define FDBCS_E_NODEVICE (-6)  /* no HIP device / extension unusable: the product never falls back to the CPU */
+#define FDBCS_E_TIMEOUT (-7)   /* a routed batch's shares never became ready (fdbcs_batch_add_routed) */
 
 /* Verdict bytes: ConflictBatch::TransactionCommitResult (ConflictSet.h:40-44). */
 #define FDBCS_TRANSACTION_CONFLICT 0
@@ -226,13 +227,19 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
  *     all-gather; NULL: the shares are already complete), the engine keeps, on the
  *     device, every range of the gathered shares that meets [lo_key, hi_key) (lo_len < 0: no lower
  *     bound, hi_len < 0: none above), unclipped, reads and writes alike; a transaction gets a
- *     sub-transaction iff one of its ranges is kept (:107-116), its snapshot copied, TooOld tested
- *     against this set's oldest version now (SkipList.cpp:770).  Sub-transactions keep the global
- *     order.  cap_*: bounds on the routed batch (FDBCS_E_NOMEM at detect if passed).  conflict_out
- *     (optional, n_global bytes of device memory): as fdbcs_batch_set_conflict_output, with the
+ *     sub-transaction iff one of its ranges is kept (:107-116), its snapshot copied.  Its TooOld
+ *     test (SkipList.cpp:770) is made when the batch is detected, against the oldest version every
+ *     earlier detect of this set left: the value addTransaction sees in the Resolver's order
+ *     (Resolver.actor.cpp:139-150, 179-194), whether the routing was issued before or after the
+ *     previous batch's detect.  Sub-transactions keep the global order.  cap_*: bounds on the
+ *     routed batch, TooOld sub-transactions' ranges included (FDBCS_E_NOMEM at detect if passed).
+ *     conflict_out (optional, n_global bytes of device memory, n_global = the transactions of all
+ *     shares, FDBCS_E_INVALID at detect otherwise): as fdbcs_batch_set_conflict_output, with the
  *     global index of a sub-transaction = its position in the concatenated shares.  Conflicting-key
  *     reports are not collected for routed batches.  Detect and wait as for any batch; detect
- *     blocks until the routing kernels have run (issue the next batch's routing first).
+ *     blocks until the routing kernels have run (issue the next batch's routing first).  The wait
+ *     for the ready flag is bounded by FDBCS_ROUTE_TIMEOUT_MS (default 60000): past it detect
+ *     returns FDBCS_E_TIMEOUT and the batch is empty again, to be routed anew.
  *   fdbcs_batch_routed_info: the routed batch's sizes and device views of its global -> batch
  *     transaction map (int32[n_shares * max_share_txns], -1 where not routed) and of each kept
  *     read's index in its transaction (txReadConflictRangeIndexMap, :144-165). */

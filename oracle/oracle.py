@@ -84,6 +84,7 @@ class _CSBase:
             f.argtypes = args
             self._fn[n] = f
         self._h = self._fn["new"]()
+        self._last_T = 0
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -128,6 +129,7 @@ class _CSBase:
         )
         if n < 0:
             raise RuntimeError("oracle detect failed")
+        self._last_T = T
         # conflictingKeyRangeMap as the reference fills it: an entry for every reporting transaction
         # that was admitted with at least one read range (created in addTransaction,
         # SkipList.cpp:777-784), holding the conflicting read indices (empty if it committed)
@@ -148,6 +150,19 @@ class OracleConflictSet(_CSBase):
         f.restype = ctypes.c_int64
         f.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
         return f(self._h, key, len(key))
+
+    def last_lists(self, with_too_old: bool):
+        """(nonConflicting, tooOld) of the last detect, as SkipList.cpp:869-876 fills them when the
+        caller passes a tooOld list (with_too_old) or nullptr; tooOld is None in the second case."""
+        f = self._L.oracle_last_lists
+        f.restype = None
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                      ctypes.c_void_p]
+        cap = max(1, self._last_T)
+        nc, to = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+        n_nc, n_to = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        f(self._h, int(bool(with_too_old)), _p(nc), _p(n_nc), _p(to), _p(n_to))
+        return nc[: n_nc[0]].tolist(), (to[: n_to[0]].tolist() if with_too_old else None)
 
     def dump_history(self):
         n = self.history_size()

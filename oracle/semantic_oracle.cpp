@@ -51,6 +51,9 @@ struct OracleSet {
     std::map<Key, int64_t, KeyLess> history;  // boundary -> version of its segment
     int64_t headerVersion = 0;                // SkipList(Version) header, SkipList.cpp:398-404
     int64_t oldestVersion = 0;                // ConflictSet::oldestVersion, SkipList.cpp:731-736
+    // The last batch's TransactionInfo::tooOld flags and transactionConflictStatus, from which
+    // oracle_last_lists restates the verdict-list loop (SkipList.cpp:869-876).
+    std::vector<char> lastTooOld, lastStatus;
 };
 
 // Version of the segment containing `k` (greatest boundary <= k, else header).
@@ -266,8 +269,12 @@ int64_t oracle_detect(void* p, const fdbcs_packed_batch* pb, int64_t now, int64_
         cs->history[b] = now;
     }
 
-    // ---- verdict lists (SkipList.cpp:869-876) in reply.committed encoding (Resolver.actor.cpp:196-204)
+    // ---- verdict lists (SkipList.cpp:869-876) in reply.committed encoding (Resolver.actor.cpp:196-204);
+    // the lists themselves are restated by oracle_last_lists from the flags kept here
+    cs->lastTooOld.assign(T, 0);
+    cs->lastStatus.assign(status.begin(), status.end());
     for (int t = 0; t < T; t++) {
+        cs->lastTooOld[t] = info[t].tooOld;
         if (info[t].tooOld)
             verdicts[t] = FDBCS_TRANSACTION_TOO_OLD;
         else
@@ -301,6 +308,24 @@ int64_t oracle_detect(void* p, const fdbcs_packed_batch* pb, int64_t now, int64_
         conf_off[t + 1] = (int32_t)n;
     }
     return n;
+}
+
+// The verdict lists of the last detect, built exactly as SkipList.cpp:869-876 builds them from
+// TransactionInfo::tooOld and transactionConflictStatus (a TooOld transaction's status is true,
+// :820,830): with_too_old != 0 passes a tooOld list, 0 passes nullptr.  Both outputs hold up to
+// T entries; the counts are returned through n_nc / n_to.
+void oracle_last_lists(void* p, int with_too_old, int32_t* non_conflicting, int32_t* n_nc, int32_t* too_old,
+                       int32_t* n_to) {
+    OracleSet* cs = static_cast<OracleSet*>(p);
+    int32_t a = 0, b = 0;
+    for (size_t i = 0; i < cs->lastTooOld.size(); i++) {
+        if (with_too_old && cs->lastTooOld[i])
+            too_old[b++] = (int32_t)i;
+        else if (!cs->lastStatus[i])
+            non_conflicting[a++] = (int32_t)i;
+    }
+    *n_nc = a;
+    *n_to = b;
 }
 
 // The four ordering known-answer tests of operatorLessThanTest (SkipList.cpp:973-1005),

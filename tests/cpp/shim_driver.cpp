@@ -2,6 +2,7 @@
 // CommitTransactionRef/KeyRangeRef types, the way Resolver.actor.cpp:179-194 does.
 // Prints one verdict digit per transaction per batch.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -34,7 +35,86 @@ struct Txn {
     bool report_conflicting_keys = false;
 };
 
-int main() {
+static std::string unhex(const std::string& h) {
+    std::string out;
+    if (h == "-") return out;
+    for (size_t i = 0; i + 1 < h.size(); i += 2) out.push_back((char)strtol(h.substr(i, 2).c_str(), nullptr, 16));
+    return out;
+}
+
+static void print_list(const char* name, const std::vector<int>& v) {
+    printf(" %s=", name);
+    for (size_t i = 0; i < v.size(); i++) printf(i ? ",%d" : "%d", v[i]);
+}
+
+// --lists FILE: replays the batches of FILE through two conflict sets, calling detectConflicts
+// with a tooOld list on one and without it (nullptr, skipListTest's call shape, SkipList.cpp:1077)
+// on the other, and prints both sets of lists per batch.  FILE lines:
+//   S                         new scenario (fresh conflict sets)
+//   C <version>               clearConflictSet on both
+//   B <now> <newOldest> <T>   a batch of T transactions, each on a line:
+//   T <snapshot> <report> <nr> <nw> <hex key> x 2(nr+nw)   ("-" = empty key)
+static int run_lists(const char* path) {
+    FILE* f = fopen(path, "r");
+    if (!f) return 2;
+    ConflictSet *with = nullptr, *without = nullptr;
+    char tok[8];
+    int batch = 0;
+    while (fscanf(f, "%7s", tok) == 1) {
+        if (tok[0] == 'S') {
+            if (with) destroyConflictSet(with), destroyConflictSet(without);
+            with = newConflictSet();
+            without = newConflictSet();
+            batch = 0;
+        } else if (tok[0] == 'C') {
+            long long v;
+            if (fscanf(f, "%lld", &v) != 1) return 3;
+            clearConflictSet(with, v);
+            clearConflictSet(without, v);
+        } else if (tok[0] == 'B') {
+            long long now, oldest;
+            int T;
+            if (fscanf(f, "%lld %lld %d", &now, &oldest, &T) != 3) return 3;
+            std::vector<Txn> txns(T);
+            for (int t = 0; t < T; t++) {
+                long long snap;
+                int rep, nr, nw;
+                if (fscanf(f, "%7s %lld %d %d %d", tok, &snap, &rep, &nr, &nw) != 5) return 3;
+                txns[t].read_snapshot = snap;
+                txns[t].report_conflicting_keys = rep != 0;
+                char buf[4096];
+                for (int r = 0; r < nr + nw; r++) {
+                    Range rg;
+                    if (fscanf(f, "%4095s", buf) != 1) return 3;
+                    rg.begin.s = unhex(buf);
+                    if (fscanf(f, "%4095s", buf) != 1) return 3;
+                    rg.end.s = unhex(buf);
+                    (r < nr ? txns[t].read_conflict_ranges : txns[t].write_conflict_ranges).push_back(rg);
+                }
+            }
+            ConflictBatch a(with), b(without);
+            for (auto& t : txns) a.addTransaction(t), b.addTransaction(t);
+            std::vector<int> nc, to, nc2;
+            a.detectConflicts(now, oldest, nc, &to);
+            b.detectConflicts(now, oldest, nc2);
+            printf("L %d with", batch);
+            print_list("nc", nc);
+            print_list("to", to);
+            printf("\nL %d without", batch);
+            print_list("nc", nc2);
+            printf("\n");
+            batch++;
+        } else {
+            return 3;
+        }
+    }
+    if (with) destroyConflictSet(with), destroyConflictSet(without);
+    fclose(f);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc == 3 && strcmp(argv[1], "--lists") == 0) return run_lists(argv[2]);
     ConflictSet* cs = newConflictSet();
     // batch 1: T0 writes [k, k\0); T1 reads it (intra-batch conflict); T2 reads [a, b)
     {
@@ -110,8 +190,8 @@ int main() {
         printf("b5 commit=%zu tooold=%zu late=%zu late0=%d entries=%zu\n", ok.size(), tooOld.size(), late.size(),
                late.empty() ? -1 : late[0], ckr.size());
     }
-    // batch 6: without a tooOld list the reference files a TooOld transaction as non-conflicting
-    // (its conflict status is never set, SkipList.cpp:869-876)
+    // batch 6: without a tooOld list a TooOld transaction lands in neither list: its conflict status
+    // is set to true (`conflict = tr.tooOld`, SkipList.cpp:820,830) and :873 skips it
     {
         ConflictBatch batch(cs);
         Txn a;

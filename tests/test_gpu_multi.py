@@ -22,26 +22,32 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("workload,extra", [("c2", []), ("c3", []), ("c3", ["--reshard", "--reshard-preroll", "60"])])
-def test_two_rank_bench_parity(engine, workload, extra):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,workload,extra", [(2, "c2", []), (2, "c3", []),
+                                                  (2, "c3", ["--reshard", "--reshard-preroll", "60"]),
+                                                  (8, "c2", [])])
+def test_multi_rank_bench_parity(engine, world, workload, extra):
+    """bench.py's N-rank path rehearsed on one GPU over gloo (RCCL refuses several ranks on one
+    card): 2 ranks, and the 8-way split of C5 with 500-transaction shares."""
+    txns, history = ("1000", "200000") if world == 2 else ("500", "50000")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--workload", workload, "--steps", "8", "--warmup", "2", "--txns", "1000",
-           "--history", "200000", "--resident-steps", "0", "--total-steps", "0", "--breakdown-steps", "0",
+           "--gpus", str(world), "--workload", workload, "--steps", "8", "--warmup", "2", "--txns", txns,
+           "--history", history, "--resident-steps", "0", "--total-steps", "0", "--breakdown-steps", "0",
            "--profile-steps", "4", "--sync-steps", "4", "--backend", "gloo", "--cpu-seconds", "20"] + extra
-    env = dict(os.environ, OMP_NUM_THREADS="2")
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    env = dict(os.environ, OMP_NUM_THREADS="1" if world > 2 else "2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280 if world > 2 else 110)
     assert r.returncode == 0, "\n".join([l for l in r.stderr.splitlines() if "[rank1]" in l][-30:]) + r.stderr[-1500:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert out["n_gpus"] == world and out["value"] > 0
     # warmup 2 + profile 4 + timed 8 + sync 4 batches, every one combined and replayed on each rank
-    assert out["parity"]["batches_checked"] >= 2 * 18 and out["parity"]["mismatched_batches"] == 0
+    assert out["parity"]["batches_checked"] >= world * 18 and out["parity"]["mismatched_batches"] == 0
     # the combine check covers the timed and later batches (timed 8 + sync 4)
     assert out["combine_check"]["mismatched"] == 0 and out["combine_check"]["batches"] == 12
-    # G resolvers on G cores: both ranks' restatements timed at once, over the slower one
-    assert out["cpu_baseline"]["cores"] == 2 and out["cpu_baseline"]["value"] > 0
-    assert out["distributed"]["world_size"] == 2 and out["distributed"]["backend"] == "gloo"
+    # G resolvers on G cores: every rank's restatement timed at once, over the slowest one
+    assert out["cpu_baseline"]["cores"] == world and out["cpu_baseline"]["value"] > 0
+    assert out["distributed"]["world_size"] == world and out["distributed"]["backend"] == "gloo"
     assert out["combine_check"]["path"].startswith("device conflict bytes")
     if extra:
         assert out["reshard"]["moves"] > 0  # the hot rank gave key ranges away
@@ -79,7 +85,6 @@ def test_device_routing_matches_host_routing(engine, G, alphabet, max_len, long_
     sets = [engine.ConflictSet(0) for _ in range(G)]
     oras = [O.OracleConflictSet() for _ in range(G)]
     now = 10
-    oldest = 0
     for step in range(10):
         pb = W.random_small_batch(rng, G * Tshare, alphabet=alphabet, max_len=max_len, now=now, staleness=12)
         shares = [engine.share_pack(pb.slice_txns(g * Tshare, (g + 1) * Tshare)) for g in range(G)]
@@ -106,10 +111,10 @@ def test_device_routing_matches_host_routing(engine, G, alphabet, max_len, long_
                          out[g].data_ptr(), pb.n_txn, *flag)
             sub = routes[g].batch
             T, R, Wn, _, _ = b.routed_info()
-            # TooOld sub-transactions (SkipList.cpp:770, at add time) keep no ranges
+            # every kept range is placed, TooOld sub-transactions' included (their TooOld test,
+            # SkipList.cpp:770, is made at detect time)
             nr, nw = np.diff(sub.read_offsets), np.diff(sub.write_offsets)
-            old = (sub.read_snapshot < oldest) & (nr > 0)
-            assert (T, R, Wn) == (sub.n_txn, int(nr[~old].sum()), int(nw[~old].sum()))
+            assert (T, R, Wn) == (sub.n_txn, int(nr.sum()), int(nw.sum()))
             b.detect_async(now, now - 9)
             got = b.wait()
             b.close()
@@ -119,7 +124,91 @@ def test_device_routing_matches_host_routing(engine, G, alphabet, max_len, long_
             ref = np.zeros(pb.n_txn, np.uint8)
             ref[ids] = 2 - want.astype(np.uint8)
             np.testing.assert_array_equal(out[g].cpu().numpy(), ref)
-        oldest = max(oldest, now - 9)
         now += 4
+    for cs in sets:
+        cs.close()
+
+
+def _route_and_gather(engine, torch, np, pb, G, Tshare):
+    shares = [engine.share_pack(pb.slice_txns(g * Tshare, (g + 1) * Tshare)) for g in range(G)]
+    stride = (max(len(x) for x in shares) + 255) // 256 * 256
+    host = np.zeros(G * stride, np.uint8)
+    for g, x in enumerate(shares):
+        host[g * stride: g * stride + len(x)] = x
+    return torch.from_numpy(host).cuda(), stride
+
+
+@pytest.mark.parametrize("G,workload", [(8, "c2"), (8, "c3"), (4, "c2")])
+def test_pipelined_device_routing_eight_resolvers(engine, G, workload):
+    """The 8-way key-range split on one card (C5 shape, CommitProxyServer.actor.cpp:107-187,
+    764-780): G resolvers route C2/C3-shaped global batches on the device in bench.py's order (batch
+    i+1 routed before batch i's detect), with snapshots straddling the oldest version as it moves.
+    Each resolver's verdicts equal its own restatement fed the host routing in the Resolver's
+    order (add after the previous detect: TooOld against the oldest that detect left,
+    SkipList.cpp:770, 880-882), and the device conflict bytes max-combined over the resolvers equal
+    the host combine (the proxy's min over verdicts)."""
+    import numpy as np
+    import torch
+
+    from foundationdb_amd import workloads as W
+    from foundationdb_amd.sharding import KeyRangeSharding
+    from oracle import oracle as O
+
+    O.build()
+    rng = np.random.default_rng(800 + G)
+    Tshare = 250
+    p = W.C2Params(txns=G * Tshare, staleness=60)
+    sh = KeyRangeSharding.uniform(G) if workload == "c2" else KeyRangeSharding(
+        [W.mako_keys(np.array([g * 1_000_000 // G]))[0].tobytes() for g in range(1, G)])
+    z = W.ZipfGenerator(1_000_000, 0.99) if workload == "c3" else None
+    sets = [engine.ConflictSet(0) for _ in range(G)]
+    oras = [O.OracleConflictSet() for _ in range(G)]
+    now = 1000
+    pending = None
+    saw_too_old = 0
+    too_old_window = 0
+
+    def finish(pend):
+        pb_, now_, no_, objs, outs = pend
+        routes = sh.route(pb_)
+        comb = np.zeros(pb_.n_txn, np.uint8)
+        want_comb = np.zeros(pb_.n_txn, np.uint8)
+        nonlocal saw_too_old, too_old_window
+        for g in range(G):
+            objs[g].detect_async(now_, no_)
+        for g in range(G):
+            got = objs[g].wait()
+            objs[g].close()
+            sub = routes[g].batch
+            old_before = oras[g].oldest_version
+            want, _ = oras[g].detect(sub, now_, no_)
+            np.testing.assert_array_equal(got, want, err_msg=f"resolver {g}")
+            saw_too_old += int((want == 1).sum())
+            # TooOld only because the previous detect raised the oldest version
+            too_old_window += int(((want == 1) & (sub.read_snapshot >= old_before - 4)).sum())
+            comb = np.maximum(comb, outs[g].cpu().numpy())
+            want_comb = np.maximum(want_comb, KeyRangeSharding.conflict_bytes(pb_.n_txn, routes[g], want))
+        np.testing.assert_array_equal(comb, want_comb)
+
+    for step in range(8):
+        now += 4
+        pb = W.c3_batch(p, rng, now, z) if z else W.c2_batch(p, rng, now)
+        dev, stride = _route_and_gather(engine, torch, np, pb, G, Tshare)
+        tail = int(np.maximum(np.diff(pb.key_offsets) - 16, 0).sum())
+        objs, outs = [], []
+        for g in range(G):
+            lo = sh.splits[g - 1] if g > 0 else None
+            hi = sh.splits[g] if g < G - 1 else None
+            out = torch.full((pb.n_txn,), 7, dtype=torch.uint8, device="cuda")
+            b = engine.ConflictBatch(sets[g])
+            b.add_routed(dev.data_ptr(), stride, G, Tshare, lo, hi, (pb.n_txn, pb.n_reads, pb.n_writes, tail),
+                         out.data_ptr(), pb.n_txn)
+            objs.append(b)
+            outs.append(out)
+        if pending is not None:  # the previous batch's detect after this batch's routing
+            finish(pending)
+        pending = (pb, now, now - 30, objs, outs)
+    finish(pending)
+    assert saw_too_old > 0 and too_old_window > 0
     for cs in sets:
         cs.close()

@@ -500,7 +500,7 @@ def test_cpp_shim_driver(tmp_path):
     assert "b2 commit=1 first=1" in out, out
     assert "b3 commit=0 report0=1 idx=1 arena=1" in out, out
     assert "b5 commit=2 tooold=1 late=1 late0=0 entries=0" in out, out
-    assert "b6 commit=1 first=0" in out, out
+    assert "b6 commit=0 first=-1" in out, out
 
 
 def test_sharded_engines_match_sharded_oracles(engine, oracle_mod):
@@ -579,7 +579,8 @@ def test_empty_batches(engine, oracle_mod):
                                    {"FDBCS_GRAPH": "3"}, {"FDBCS_GRAPH": "3", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
-                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"}])
+                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"},
+                                   {"FDBCS_SPLIT_B": "0"}, {"FDBCS_SPLIT_B": "0", "FDBCS_SPLIT_CHECK": "1"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the unsplit and
     split read checks, the one-wave check, long-key sorting without LDS windows, stage graphs, the
@@ -649,3 +650,48 @@ def test_conflict_output_rejects_duplicate_ids(engine):
         b.set_conflict_output(np.array([0, 2, 0], np.int32), 4, 1 << 20)
     b.close()
     cs.close()
+
+
+def test_verdict_lists_match_oracle_lists(engine, oracle_mod, tmp_path):
+    """Both host adapters over the HIP engine fill nonConflicting / tooOld exactly as the oracle's
+    restatement of SkipList.cpp:869-876, with a tooOld list (Resolver.actor.cpp:194) and without one
+    (skipListTest's call shape, SkipList.cpp:1077): the Python ConflictBatch and the C++ shim
+    (tests/cpp/shim_driver.cpp --lists) on the KAT scenarios and random TooOld-heavy sequences."""
+    import subprocess
+
+    from tests.helpers import list_scenarios, oracle_scenario_lists, write_list_file
+    from tests.test_abi import build_shim_driver
+
+    scenarios = list_scenarios()
+    want = oracle_scenario_lists(oracle_mod, scenarios)
+    lines = []
+    for steps, res in zip(scenarios, want):
+        with_cs, without_cs = engine.ConflictSet(0), engine.ConflictSet(0)
+        batches = iter(res)
+        for st in steps:
+            if st[0] == "clear":
+                with_cs.clear(st[1])
+                without_cs.clear(st[1])
+                continue
+            _, pb, now, no = st
+            v, nc, to, nc2 = next(batches)
+            got_nc, got_to, got_nc2 = [], [], []
+            b = engine.ConflictBatch(with_cs)
+            b.add_packed(pb)
+            b.detect_conflicts(now, no, got_nc, got_to)
+            b.close()
+            b = engine.ConflictBatch(without_cs)
+            b.add_packed(pb)
+            b.detect_conflicts(now, no, got_nc2)
+            b.close()
+            assert (got_nc, got_to, got_nc2) == (nc, to, nc2)
+        with_cs.close()
+        without_cs.close()
+        for i, (v, nc, to, nc2) in enumerate(res):
+            lines.append(f"L {i} with nc={','.join(map(str, nc))} to={','.join(map(str, to))}")
+            lines.append(f"L {i} without nc={','.join(map(str, nc2))}")
+    path = str(tmp_path / "lists.txt")
+    write_list_file(scenarios, path)
+    exe = build_shim_driver(str(tmp_path / "shim_driver"))
+    out = subprocess.check_output([exe, "--lists", path], text=True, timeout=120)
+    assert out.split("\n")[:-1] == lines

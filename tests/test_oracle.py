@@ -238,3 +238,25 @@ def test_conflicting_key_map_entries_follow_add_transaction(oracle_built):
     v, conf = cs.detect(pb, 10, 5)
     assert v.tolist() == [2, 2, 0, 1]
     assert conf == {1: [], 2: [0]}
+
+
+def test_verdict_lists_follow_reference_loop(oracle_built):
+    """The host adapters' list filling (conflict_set.fill_verdict_lists, mirrored in
+    conflict_set_shim.hpp) equals the oracle's restatement of SkipList.cpp:869-876, with and
+    without a tooOld list; without one a TooOld transaction lands in neither list (:820,830)."""
+    from foundationdb_amd.conflict_set import fill_verdict_lists
+    from tests.helpers import list_scenarios, oracle_scenario_lists
+
+    saw_too_old = 0
+    for res in oracle_scenario_lists(oracle_built, list_scenarios()):
+        for v, nc, to, nc2 in res:
+            a, b = [], []
+            fill_verdict_lists(v, a, b)
+            assert (a, b) == (nc, to)
+            c = []
+            fill_verdict_lists(v, c, None)
+            assert c == nc2
+            assert not set(to) & set(nc2)  # TooOld is in neither list without a tooOld list
+            assert sorted(nc2 + to + np.flatnonzero(v == 0).tolist()) == list(range(len(v)))
+            saw_too_old += len(to)
+    assert saw_too_old > 10
