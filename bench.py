@@ -76,8 +76,9 @@ def parse():
                     help="batches of the add+detect ('total') pass; -1 = --steps, 0 = skip")
     ap.add_argument("--resident-steps", type=int, default=20,
                     help="batches of the device-resident pass (uploaded before its timed region; diagnostic)")
-    ap.add_argument("--breakdown-steps", type=int, default=16,
-                    help="extra batches after the timed region with every phase timed (diagnostic)")
+    ap.add_argument("--breakdown-steps", type=int, default=128,
+                    help="extra batches after the timed region with every phase timed: the per-phase split and the "
+                    "compaction + GC cost amortized per batch (>= 128 batches hold several compactions and GC runs)")
     ap.add_argument("--profile-steps", type=int, default=16,
                     help="batches with events around every kernel (per-kernel table, dominant kernel)")
     ap.add_argument("--sync-steps", type=int, default=20,
@@ -579,6 +580,17 @@ def main():
         kprof = cs.kernel_profile()
         st_prof = cs.stats()
         dominant = max(kprof, key=lambda k: kprof[k]["ms"]) if kprof else None
+    # The dominant kernel by rocprofv3 kernel-trace time (dispatch to completion) when a summary of
+    # this configuration and build is committed: the profile pass's events also count the time a
+    # kernel waits for its stream's turn behind the other streams' kernels.
+    build = roofline.build_id(ROOT)
+    rp_kernels, rp_note = roofline.rocprof_kernels(ROOT, args.workload, p.txns, p.history, build)
+    dominant_source = "profile pass (events around every kernel)"
+    if rp_kernels:
+        ranked = [k for k in rp_kernels if k in kprof]
+        if ranked:
+            dominant = ranked[0]
+            dominant_source = "rocprofv3 kernel trace: " + rp_note
     cs.set_timing(args.timing)
     if dominant and args.timing >= 1:
         cs.set_timed_kernel(dominant)
@@ -661,6 +673,7 @@ def main():
     # diagnostic phase split: extra batches with every phase timed (each event costs queue time,
     # so these are outside the timed region)
     phase = None
+    amortized = None
     if args.breakdown_steps > 0:
         cs.set_timing(2)
         cs.reset_stats()
@@ -677,6 +690,27 @@ def main():
         phase["intra_edges"] = sb["intra_edges"] / max(1, sb["batches"] - sb["intra_fallbacks"])
         phase["intra_rounds"] = sb["intra_rounds"] / max(1, sb["batches"] - sb["intra_fallbacks"])
         phase["intra_fallbacks"] = sb["intra_fallbacks"]
+        phase["gc_runs"] = sb["gc_runs"]
+        # what the headline's short window may not hold: compaction (delta folded into the base) and
+        # removeBefore, amortized over the breakdown pass (the reference pays a bounded removeBefore
+        # every batch, SkipList.cpp:880-889)
+        amortized = {"compaction_ms_per_batch": phase["ms_compact"], "gc_ms_per_batch": phase["ms_gc"],
+                     "merge_ms_per_batch": phase["ms_merge"], "batches": sb["batches"],
+                     "compactions": sb["compactions"], "gc_runs": sb["gc_runs"],
+                     "timed_region_compactions": st["compactions"], "timed_region_gc_runs": st["gc_runs"]}
+    # The Resolver's verdict counters over the timed batches (Resolver.actor.cpp:206-208:
+    # TransactionsAccepted / TooOld / Conflicted), combined over resolvers at N > 1
+    mix = {"committed": 0, "conflict": 0, "too_old": 0}
+    for i in range(timed_lo, timed_hi):
+        v = combined[i].cpu().numpy() if (dist is not None and i in combined) else verdicts[i]
+        if v is None:
+            continue
+        v = np.asarray(v)
+        if dist is not None and i in combined:  # conflict bytes: 2 - min verdict, 0 = not routed anywhere
+            v = np.where(v == 0, 2, 2 - v.astype(np.int64))
+        mix["committed"] += int((v == 2).sum())
+        mix["conflict"] += int((v == 0).sum())
+        mix["too_old"] += int((v == 1).sum())
     gtxn = pass_txns("timed")
     granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(timed_lo, timed_hi))
     ttxn = pass_txns("total")
@@ -695,6 +729,11 @@ def main():
     if dominant and dominant in kprof_timed:
         k = kprof_timed[dominant]
         ent = roofline.entry(dominant, k["ms"], k["launches"], shape, st)
+        traffic, traffic_note = roofline.pmc_traffic(ROOT, args.workload, dominant, p.txns, p.history, build)
+        rp = (rp_kernels or {}).get(dominant)
+        rp_frac = None
+        if rp and ent["algorithmic_bytes_per_launch"]:
+            rp_frac = ent["algorithmic_bytes_per_launch"] / (rp["avg_us"] * 1e-6) / 1e9 / roofline.HBM_PEAK_GBS
         roof = {
             "kernel": dominant,
             "bound": "hbm",
@@ -702,8 +741,15 @@ def main():
             "peak": roofline.HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": ent["frac"],
-            "traffic": roofline.pmc_traffic(ROOT, args.workload, dominant, p.txns, p.history),
+            "traffic": traffic,
+            "traffic_source": traffic_note,
+            "dominant_source": dominant_source,
+            "build_id": build,
             "avg_launch_ms": ent["avg_launch_ms"],
+            # the same kernel's rocprofv3 average (committed summary of this build and configuration)
+            "rocprof_avg_launch_ms": rp["avg_us"] / 1e3 if rp else None,
+            "frac_rocprof": rp_frac,
+            "rocprof_source": rp_note,
             "launches_timed": k["launches"],
             "algorithmic_bytes_per_launch": ent["algorithmic_bytes_per_launch"],
             "model": ent["model"],
@@ -807,6 +853,8 @@ def main():
         "reshard": reshard,
         "history_boundaries_end": hist_end,
         "phase_ms_per_batch": phase,
+        "amortized_ms_per_batch": amortized,
+        "verdict_mix": mix,
         "compactions": st["compactions"],
         "kernels": table,
         "sort_phase": roofline.sort_phase(table),

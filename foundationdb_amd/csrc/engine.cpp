@@ -213,8 +213,9 @@ struct fdbcs_conflict_set {
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
-    int check_version = 6;    // FDBCS_CHECK: read-check kernel (1: the four lookups of a read in one wave;
-                              // 6: the base and delta lookups in separate waves)
+    int check_version = 7;    // FDBCS_CHECK: read-check kernel (7: one lane per lookup, for batches of keys
+                              // up to 24 bytes; 6: kArity lanes per lookup, the base and delta lookups in
+                              // separate waves, 1: kArity lanes per lookup, the four of a read in one wave)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
     bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
@@ -1086,7 +1087,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
-    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : 6;
+    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));
@@ -2077,6 +2078,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // long-key probes pay off once tails run past a word (a 17-byte end key k\0 of a 16-byte key
     // ties on the prefix with k only, and the length decides)
     const bool long_keys = cs->long_probe && b->max_len > 24;
+    // one lane per lookup unless tails run past a word (then the cooperative long-key probes)
+    const bool lanes = cs->check_version == 7 && b->max_len <= 24;
+    const int check_version = cs->check_version == 7 && !lanes ? 6 : cs->check_version;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     // Stage B in two halves (fdbcs_conflict_set::ystream): X = check, resolution, D.Combine on
@@ -2084,7 +2088,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // compacted, this batch's check reads the delta before the previous batch's merge (buffer
     // dsrc ^ 1, complete once the batch before it finished Y) plus the previous batch's union
     // segments at its `now` (PrevSegs): the same history, so the check need not wait for that merge.
-    const bool pipe = cs->split_stage_b && !(timing == 2 || cs->serial || cs->check_version != 6);
+    const bool pipe = cs->split_stage_b && !(timing == 2 || cs->serial || cs->check_version == 1);
     hipStream_t ys = pipe ? cs->ystream : s;
     const bool use_prev = pipe && cs->prev_segs;
     const int dchk = use_prev ? dsrc ^ 1 : dsrc;
@@ -2149,7 +2153,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
             fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
-        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax);
+        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, PrevSegs{}, lanes);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
@@ -2167,11 +2171,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const bool graphs = cs->stage_graphs && timing != 2;
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, !cs->group_rmax, ps);
+        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, !cs->group_rmax, ps, lanes);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-        launch_check(s, bd, w, base, cdelta, htail, cs->check_version, ps);
+        launch_check(s, bd, w, base, cdelta, htail, check_version, ps);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
@@ -2597,10 +2601,11 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     hipEvent_t e0, e1;
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));
-    launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version);
+    const int cv = cs->check_version == 7 && b->max_len > 24 ? 6 : cs->check_version;
+    launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cv);
     HIPOK(hipEventRecord(e0, cs->stream));
     for (int i = 0; i < reps; i++)
-        launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cs->check_version);
+        launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cv);
     HIPOK(hipEventRecord(e1, cs->stream));
     HIPOK(hipEventSynchronize(e1));
     *us_per_launch = ev_ms(e0, e1) * 1000.0 / reps;

@@ -352,15 +352,17 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
 // Buckets of a batch of E endpoints (target 0 = kSortTarget), within the workspace slab.
 int sort_bucket_count(int64_t E, int target, int slab_buckets);
 // D.CheckRead against the history the previous batch left.
-// check_version: 6 = base and delta lookups in separate waves (default), 1 = in one wave.
+// check_version: 7 = one lane per lookup (default for keys up to 24 bytes), 6 = kArity lanes per
+// lookup with the base and delta lookups in separate waves, 1 = kArity lanes per lookup in one wave.
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
                   const uint8_t* htail, int check_version = 6, const PrevSegs& ps = PrevSegs{});
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
 // delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
 // long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
+// lanes: one lane per lookup (FDBCS_CHECK=7 on keys up to 24 bytes).
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
                        const uint8_t* htail, bool long_keys = false, bool lead_rmax = false,
-                       const PrevSegs& ps = PrevSegs{});
+                       const PrevSegs& ps = PrevSegs{}, bool lanes = false);
 // Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
 // k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,

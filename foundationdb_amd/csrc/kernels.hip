@@ -803,6 +803,308 @@ __device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& t
     }
 }
 
+// ---- per-lane lookups (FDBCS_CHECK=7, the default for batches of keys up to 24 bytes)
+//
+// One lane per lookup.  The cooperative lookups above give each lookup kArity lanes that load one
+// node entry each, so a wave serves kArity lookups and the wave's instruction stream (ballots,
+// shuffles, 64-bit compares) is paid per kArity lookups: at C2 12,500 waves of ~350 VALU + ~260
+// SALU instructions each, 77 % of their life waiting on loads (rocprofv3 SQ counters), the chip
+// never holding all of them at once.  Here a lane issues a whole node's (or directory slot's)
+// entries itself, up to kLaneProbe independent 16-byte loads in flight, and counts them in
+// registers: the same dependent rounds per lookup, 64 lookups per wave, every wave of a C2 batch
+// resident at once.
+constexpr int kLaneProbe = 16;  // entries one lane loads per round (a directory slot of two groups)
+
+// Number of the first cnt (<= N) entries of a[base, ...) whose 16-byte prefix is below q's, and
+// whether the first entry not below it has q's prefix (eq_next; false if all are below).
+template <int N>
+__device__ __forceinline__ int lane_count(const ulonglong2* a, int64_t base, int cnt, const DKey& q, bool& eq_next) {
+    ulonglong2 k[N];
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (i < cnt) k[i] = a[base + i];
+    int c = 0;
+    eq_next = false;
+    bool stop = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (i < cnt && !stop) {
+            if (prefix_less(k[i], q)) {
+                c++;
+            } else {
+                stop = true;
+                eq_next = k[i].x == q.hi && k[i].y == q.lo;
+            }
+        }
+    }
+    return c;
+}
+
+// std::lower_bound of q over the n boundaries of a tier by one lane (the result and eq as
+// group_lower_bound's): the radix directory slot (at most kLaneProbe level-0 samples) or the
+// kArity-ary sample tree down to one 64-boundary block, then the block's eight group starts
+// (skey8) and the seven boundaries after the last start below q; prefix ties compare lengths and
+// tails against the boundary itself (probe_cmp_lean).  A run of boundaries sharing q's 16-byte
+// prefix over more than one block (tuple subspaces) falls back to a binary search.
+__device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
+                                                    const uint8_t* htail, const uint8_t* qtail, bool& eq) {
+    eq = false;
+    if (n <= 0) return 0;
+    int64_t sz[kIdxLevels];
+    sz[0] = (n + kFan - 1) / kFan;
+#pragma unroll
+    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + kArity - 1) / kArity;
+    int top = 0;
+    while (top + 1 < kIdxLevels && sz[top] > kArity) top++;
+    int64_t c = 0;      // level-0 samples whose prefix is below q
+    bool bknown = false;  // the sample at c (if any) is known not to share q's prefix
+    bool direct = false;
+    if (m.dir || m.edir_epoch) {
+        const uint32_t dv = (uint32_t)(q.hi >> 48);
+        int64_t d0, d1;
+        bool have = true;
+        if (m.dir) {
+            d0 = m.dir[dv];
+            d1 = m.dir[dv + 1];
+        } else {
+            const uint64_t x0 = m.edir[dv], x1 = m.edir[dv + 1];
+            have = (uint32_t)(x0 >> 32) == m.edir_epoch && (uint32_t)(x1 >> 32) == m.edir_epoch;
+            d0 = (uint32_t)x0;
+            d1 = (uint32_t)x1;
+        }
+        if (have && d1 - d0 <= kLaneProbe && d1 <= sz[0]) {
+            direct = true;
+            bool eqn;
+            const int cnt = (int)(d1 - d0);
+            const int k = lane_count<kLaneProbe>(m.skey[0], d0, cnt, q, eqn);
+            c = d0 + k;
+            // all of the slot below q: the next sample's first two bytes are greater
+            bknown = k < cnt ? !eqn : true;
+        }
+    }
+    if (!direct) {
+        for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
+            const int cnt = (int)min((int64_t)kArity, sz[top] - j0);
+            bool eqn;
+            const int k = lane_count<kArity>(m.skey[top], j0, cnt, q, eqn);
+            if (top == 0 && k < cnt) bknown = !eqn;
+            c += k;
+            if (k < cnt) break;
+        }
+        for (int L = top; L > 0; L--) {
+            if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
+            const int64_t base = (int64_t)kArity * (c - 1) + 1;
+            const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
+            bool eqn;
+            const int cnt = (int)(end - base);
+            const int k = lane_count<kArity>(m.skey[L - 1], base, cnt, q, eqn);
+            if (L == 1 && k < cnt) bknown = !eqn;
+            c = base + k;
+        }
+    }
+    // samples sharing q's prefix widen the block
+    int64_t b = c;
+    while (!bknown && b < sz[0]) {
+        const ulonglong2 k = m.skey[0][b];
+        if (k.x != q.hi || k.y != q.lo) break;
+        b++;
+    }
+    const int64_t hi = min(n, kFan * b);
+    if (b == c) {
+        // boundary 64(c-1) < q < boundary 64c: one 64-boundary block; its group starts, then the
+        // boundaries after the last start below q
+        const int64_t B = c > 0 ? kFan * (c - 1) : 0;
+        const int n8 = (int)min((int64_t)8, (hi - B + 7) / 8);  // group starts below hi
+        ulonglong2 s8[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            if (i < n8) s8[i] = m.skey8[B / 8 + i];
+        int r8[8];
+        int k8 = 0;
+        bool stop = false;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            r8[i] = 1;
+            if (i < n8 && !stop) {
+                r8[i] = probe_cmp_lean(h, B + 8 * i, s8[i], htail, q, qtail);
+                if (r8[i] < 0) k8++; else stop = true;
+            }
+        }
+        if (k8 == 0) {  // c == 0 and q <= boundary 0
+            eq = hi > 0 && r8[0] == 0;
+            return 0;
+        }
+        const int64_t g = B + 8 * (k8 - 1);  // boundary g < q; the answer lies in (g, min(g + 8, hi)]
+        const int64_t gend = min(g + 8, hi);
+        const int nk = (int)(gend - g - 1);
+        ulonglong2 kk[7];
+#pragma unroll
+        for (int i = 0; i < 7; i++)
+            if (i < nk) kk[i] = h.key[g + 1 + i];
+        int k1 = 0;
+        int r_stop = 1;
+        stop = false;
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            if (i < nk && !stop) {
+                const int r = probe_cmp_lean(h, g + 1 + i, kk[i], htail, q, qtail);
+                if (r < 0) {
+                    k1++;
+                } else {
+                    stop = true;
+                    r_stop = r;
+                }
+            }
+        }
+        const int64_t lb = g + 1 + k1;
+        if (lb < gend)
+            eq = r_stop == 0;
+        else if (lb < hi)
+            eq = k8 < 8 && r8[k8] == 0;  // lb = g + 8: the next group's start, probed above
+        return lb;
+    }
+    // a run of boundaries sharing q's prefix across blocks: binary search with full compares
+    int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0, hh = hi;
+    while (lo < hh) {
+        const int64_t mid = (lo + hh) >> 1;
+        const int r = hist_cmp(h, mid, htail, q, qtail);
+        if (r < 0) {
+            lo = mid + 1;
+        } else {
+            hh = mid;
+            eq = r == 0;
+        }
+    }
+    if (lo >= hi) eq = false;
+    return lo;
+}
+
+// The previous batch's union segments (prev_seg_hit) searched by the four lanes of one read
+// (lanes 4i..4i+3 call with the same read): 16 probes per round, four per lane.
+__device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U, const DKey& kb, const DKey& ke,
+                                                  bool degenerate, const uint8_t* qtail, bool active) {
+    const DKey& target = degenerate ? kb : ke;
+    const int ql = threadIdx.x & 3;
+    int64_t lo = 0, hi = active ? U : 0;  // begins below the target: all of [0, lo), none of [hi, U)
+    for (;;) {
+        const bool more = lo < hi;
+        // the quad's lanes share lo / hi: the loop runs while any read of the wave searches
+        if (!__ballot(more)) break;
+        int below = 0;
+        if (more) {
+            int64_t idx[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) idx[j] = lo + ((hi - lo) * (4 * ql + j + 1)) / 17;
+            DKey d[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) d[j] = ps.segk[2 * idx[j]];
+#pragma unroll
+            for (int j = 0; j < 4; j++) below += dkey_cmp(d[j], ps.tail, target, qtail) < 0 ? 1 : 0;
+        }
+        // probes below the target form a prefix of the 16 (begins ascend with the index)
+        below += __shfl_xor(below, 1, 64);
+        below += __shfl_xor(below, 2, 64);
+        if (more) {
+            const int64_t nlo = below > 0 ? lo + ((hi - lo) * below) / 17 + 1 : lo;
+            const int64_t nhi = below < 16 ? lo + ((hi - lo) * (below + 1)) / 17 : hi;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    if (!active || lo == 0) return false;
+    const int cmp = dkey_cmp(ps.segk[2 * lo - 1], ps.tail, kb, qtail);  // end of segment lo - 1 vs b
+    return degenerate ? cmp >= 0 : cmp > 0;
+}
+
+// D.CheckRead of one read by four lanes (both tiers): lane 4i + 0 / 1 locates its begin / end key
+// in the base tier, 4i + 2 / 3 in the delta tier; the begin lanes take the end's position by a
+// shuffle and decide their tier (tier_conflict); the previous batch's segments by the quad; the
+// quad's verdict goes to the read's flags from lane 4i.
+__device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& base, const Tier& delta,
+                                                 const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
+                                                 const PrevSegs& ps) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = t >> 2;
+    const int k = (int)(t & 3);
+    const bool live = r < b.R;
+    const int64_t rr = live ? r : 0;
+    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+    const int64_t snap = b.snap[b.rowner[rr]];
+    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+    const bool is_delta = k >= 2;
+    const Tier& tier = is_delta ? delta : base;
+    const int64_t n = *tier.n;
+    const bool active = live && (!is_delta || n > 0);
+    int64_t lb = 0;
+    bool eq = false;
+    if (active && !((k & 1) && degenerate))
+        lb = lane_lower_bound(tier.h, tier.m, n, (k & 1) ? ke : kb, htail, b.tail, eq);
+    const int64_t j = __shfl_xor(lb, 1, 64);  // the begin lane takes the end key's position
+    bool conf = false;
+    if (active && !(k & 1)) conf = tier_conflict(tier.h, tier.m, is_delta ? kHole : tier.hdr, lb, eq, j, degenerate, snap);
+    if (ps.n) {  // the previous batch's union segments, not merged into the delta yet (every lane
+                 // of the quad takes part in the search's shuffles)
+        const int64_t U = *ps.n;
+        const bool hit = prev_seg_hit_quad(ps, U, kb, ke, degenerate, b.tail, live && U > 0 && ps.version > snap);
+        conf = conf || hit;
+    }
+    int c = conf ? 1 : 0;
+    c |= __shfl_xor(c, 1, 64);
+    c |= __shfl_xor(c, 2, 64);
+    if (live && k == 0) {
+        rconf[r] = (uint8_t)c;
+        if (c) hist_conf[b.rowner[r]] = 1;
+    }
+}
+
+// One tier only (the split check) by two lanes per read: begin / end; conflicts OR into the
+// pre-zeroed flags like check_read_tier.
+__device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const Tier& tier, bool is_base,
+                                                      const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
+                                                      const PrevSegs& ps) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = t >> 1;
+    const int k = (int)(t & 1);
+    const bool live = r < b.R;
+    const int64_t rr = live ? r : 0;
+    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+    const int64_t snap = b.snap[b.rowner[rr]];
+    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+    const int64_t n = *tier.n;
+    const bool active = live && (is_base || n > 0);
+    int64_t lb = 0;
+    bool eq = false;
+    if (active && !(k && degenerate)) lb = lane_lower_bound(tier.h, tier.m, n, k ? ke : kb, htail, b.tail, eq);
+    const int64_t j = __shfl_xor(lb, 1, 64);
+    bool conf = false;
+    if (active && !k) conf = tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
+    if (!is_base && ps.n) {
+        // the pair of lanes runs the quad search with its neighbour pair (the same code path for
+        // every lane; each pair's read is its own, the quad shares no state but the shuffles)
+        const int64_t U = *ps.n;
+        const bool act = live && U > 0 && ps.version > snap;
+        // two reads per quad: search them one after the other so the quad's lanes agree on lo / hi
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const int src = (int)(threadIdx.x & ~3) + 2 * s;  // the first lane of read s of the quad
+            const DKey sb = {(uint64_t)__shfl((long long)kb.hi, src, 64), (uint64_t)__shfl((long long)kb.lo, src, 64),
+                             (uint32_t)__shfl((int)kb.len, src, 64), (uint32_t)__shfl((int)kb.tail, src, 64)};
+            const DKey se = {(uint64_t)__shfl((long long)ke.hi, src, 64), (uint64_t)__shfl((long long)ke.lo, src, 64),
+                             (uint32_t)__shfl((int)ke.len, src, 64), (uint32_t)__shfl((int)ke.tail, src, 64)};
+            const int sdeg = __shfl((int)degenerate, src, 64);
+            const int sact = __shfl((int)act, src, 64);
+            const bool hit = prev_seg_hit_quad(ps, U, sb, se, sdeg != 0, b.tail, sact != 0);
+            if (((threadIdx.x >> 1) & 1) == s) conf = conf || hit;
+        }
+    }
+    int c = conf ? 1 : 0;
+    c |= __shfl_xor(c, 1, 64);
+    if (live && !k && c) {
+        rconf[r] = 1;
+        hist_conf[b.rowner[r]] = 1;
+    }
+}
+
 // ------------------------------------------------------------------ D.Sort
 
 // Endpoint item p of the batch (KeyInfo, SkipList.cpp:77-87): range g = p / 2, end = p & 1.
@@ -970,9 +1272,25 @@ __global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const
     check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax, ps);
 }
 
+// Per-lane checks (FDBCS_CHECK=7): both tiers, four lanes per read; one tier, two lanes per read.
+__global__ __launch_bounds__(kBlock) void k_check_lanes(BatchDev b, CheckReads c) {
+    check_read_lanes(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
+}
+template <bool BASE>
+__global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t, const uint8_t* htail,
+                                                             uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps) {
+    check_read_lanes_tier(b, t, BASE, htail, hist_conf, rconf, ps);
+}
+
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys, bool lead_rmax, const PrevSegs& ps) {
+                       const uint8_t* htail, bool long_keys, bool lead_rmax, const PrevSegs& ps, bool lanes) {
     if (b.R == 0) return;
+    if (lanes) {
+        const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
+        fdb_launch(is_base ? k_check_lanes_tier<true> : k_check_lanes_tier<false>, dim3(grid), dim3(kBlock), 0, s, b,
+                   t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
+        return;
+    }
     const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
     auto k = is_base ? (long_keys ? k_check_tier<true, true> : k_check_tier<true, false>)
                      : (long_keys ? k_check_tier<false, true> : k_check_tier<false, false>);
@@ -995,8 +1313,14 @@ __global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
                   const uint8_t* htail, int check_version, const PrevSegs& ps) {
     if (b.R == 0) return;
-    // four lookups per read: 6 = the base and delta lookups in separate waves, 1 = in one wave
+    // four lookups per read: 7 = one lane each, 6 = kArity lanes each with the base and delta lookups
+    // in separate waves, 1 = kArity lanes each in one wave
     CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps};
+    if (check_version == 7) {
+        const int grid = (int)(((int64_t)b.R * 4 + kBlock - 1) / kBlock);
+        fdb_launch(k_check_lanes, dim3(grid), dim3(kBlock), 0, s, b, c);
+        return;
+    }
     const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
     if (check_version == 6)
         fdb_launch(k_check_reads<true>, dim3(grid), dim3(kBlock), 0, s, b, c);

@@ -69,12 +69,12 @@ def kernel_bytes(name: str, s: dict):
     S = min(E, max(1024.0, min(8192.0, 4 * math.ceil(E / 128))))
     nb = min(2048.0, math.ceil(E / 128))
     look_b, look_d = lookup_bytes(N, s["dir_share"]), lookup_bytes(Nd, 0.5)
-    if name.startswith("k_check_reads"):  # both tiers
+    if name == "k_check_lanes" or name.startswith("k_check_reads"):  # both tiers
         return (2 * R * (D + look_b + look_d) + R * (4 + V) + 2 * R * V + T,
                 "2R(D + base lookup + delta lookup) + R(owner + snapshot) + range-max ends 2RV + T")
-    if name.startswith("k_check_tier<true"):
+    if name.startswith("k_check_tier<true") or name.startswith("k_check_lanes_tier<true"):
         return (2 * R * (D + look_b) + R * (4 + V) + R * V + T, "base tier: 2R(D + lookup) + R(4+V) + RV + T")
-    if name.startswith("k_check_tier<false"):
+    if name.startswith("k_check_tier<false") or name.startswith("k_check_lanes_tier<false"):
         return (2 * R * (D + look_d) + R * (4 + V) + R * V + T, "delta tier: 2R(D + lookup) + R(4+V) + RV + T")
     if name == "k_sample":
         return S * (D + I + 4), "S samples: key read, item written, rank"
@@ -175,15 +175,54 @@ def sort_phase(table: dict) -> dict | None:
     return {"kernels": sorted(ks), "ms_per_batch": per_batch}
 
 
-def pmc_traffic(root: str, workload: str, kernel: str, txns: int, history: int):
-    """HBM bytes per launch of `kernel` from the PMC passes of the SAME configuration
-    (profiles/pmc_<workload>_<txns>_<history>.json, written by scripts/pmc_summary.py: FETCH_SIZE
-    x2 gfx950 correction + WRITE_SIZE, each in its own rocprofv3 pass), or None."""
-    f = os.path.join(root, "profiles", f"pmc_{workload}_{txns}_{history}.json")
+# Sources whose content defines the kernels a profile measured: a profile whose build id differs
+# from the running tree's describes other code and is not used.
+BUILD_SOURCES = ("foundationdb_amd/csrc/kernels.hip", "foundationdb_amd/csrc/engine.cpp",
+                 "foundationdb_amd/csrc/engine.h", "foundationdb_amd/csrc/scan.h", "foundationdb_amd/csrc/launch.h",
+                 "foundationdb_amd/csrc/dkey.h", "include/fdb_conflict_set.h")
+
+
+def build_id(root: str) -> str:
+    """Content hash of the engine sources (the GPU box has no .git: the tree itself is the identity)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in BUILD_SOURCES:
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def _profile(root: str, prefix: str, workload: str, txns: int, history: int, build: str):
+    f = os.path.join(root, "profiles", f"{prefix}_{workload}_{txns}_{history}.json")
     if not os.path.exists(f):
-        return None
+        return None, f"no {os.path.basename(f)}"
     try:
         with open(f) as fh:
-            return json.load(fh).get("bytes_per_launch", {}).get(kernel)
-    except Exception:
-        return None
+            d = json.load(fh)
+    except Exception as e:  # noqa: BLE001
+        return None, f"{os.path.basename(f)} unreadable: {e}"
+    if d.get("build_id") != build:
+        return None, f"{os.path.basename(f)} measured build {d.get('build_id')}, running build {build}"
+    return d, f"profiles/{os.path.basename(f)} (build {build}, git {d.get('git_head')})"
+
+
+def pmc_traffic(root: str, workload: str, kernel: str, txns: int, history: int, build: str):
+    """(HBM bytes per launch of `kernel`, source note) from the PMC passes of the SAME configuration
+    and the SAME build (profiles/pmc_<workload>_<txns>_<history>.json, written by
+    scripts/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, each in its own
+    rocprofv3 pass); None when the file is absent or measured other code."""
+    d, note = _profile(root, "pmc", workload, txns, history, build)
+    if d is None:
+        return None, note
+    return d.get("bytes_per_launch", {}).get(kernel), note
+
+
+def rocprof_kernels(root: str, workload: str, txns: int, history: int, build: str):
+    """({kernel: {"calls", "avg_us", "total_ms"}}, source note) from the rocprofv3 kernel-trace
+    summary of the same configuration and build (profiles/rocprof_<workload>_<txns>_<history>.json,
+    scripts/rocprof_rank.py), or (None, why not)."""
+    d, note = _profile(root, "rocprof", workload, txns, history, build)
+    if d is None:
+        return None, note
+    return d.get("kernels"), note

@@ -17,6 +17,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $c rc=$rc" >&2
   [ $rc -ne 0 ] && exit $rc
 done
-python3 scripts/pmc_summary.py gpurun_out/pmc $W $TX $HI > gpurun_out/pmc/pmc_${W}_${TX}_${HI}.json
+GIT_HEAD=${GIT_HEAD:-} python3 scripts/pmc_summary.py gpurun_out/pmc $W $TX $HI > gpurun_out/pmc/pmc_${W}_${TX}_${HI}.json
 rm -rf gpurun_out/pmc/FETCH_SIZE gpurun_out/pmc/WRITE_SIZE
 head -c 1500 gpurun_out/pmc/pmc_${W}_${TX}_${HI}.json >&2

@@ -26,7 +26,7 @@ for w in ${WORKLOADS:-c2 c3 c4}; do
   step bench_$w 600 python bench.py --workload $w ${BENCH_ARGS:-} > $O/bench_$w.json 2> $O/bench_$w.err
   cat $O/bench_$w.json >&2
   if [ "${PROFILE:-1}" = "1" ]; then
-    OUT=$O/prof_$w BENCH_ARGS="--workload $w" step prof_$w 660 bash scripts/gpu_profile.sh
+    WORKLOAD=$w OUT=$O/prof_$w step prof_$w 660 bash scripts/gpu_profile.sh
     head -3 $O/prof_$w/timeline.txt >&2
   fi
 done

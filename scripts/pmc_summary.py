@@ -42,6 +42,11 @@ out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; byte
        "bytes_per_launch": {}, "bytes_per_launch_raw": {}, "launches": {}}
 if len(sys.argv) >= 5:
     out["config"] = {"workload": sys.argv[2], "txns": int(sys.argv[3]), "history": int(sys.argv[4])}
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import roofline  # noqa: E402
+
+out["build_id"] = roofline.build_id(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+out["git_head"] = os.environ.get("GIT_HEAD")
 for k in sorted(set(per["FETCH_SIZE"]) & set(per["WRITE_SIZE"])):
     f = sum(per["FETCH_SIZE"][k]) / len(per["FETCH_SIZE"][k])
     w = sum(per["WRITE_SIZE"][k]) / len(per["WRITE_SIZE"][k])

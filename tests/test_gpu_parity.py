@@ -163,17 +163,20 @@ def test_shared_long_prefixes(engine, oracle_mod):
 
 
 @pytest.mark.parametrize("split", ["1", "2"])
-def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split):
+@pytest.mark.parametrize("tail_max", [40, 8])
+def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split, tail_max):
     """Thousands of history boundaries behind one 16-byte prefix (a few huge tuple subspaces): the
     search must order them by their tail bytes over a run far longer than one 64-boundary block
-    (the cooperative probe rounds start at a stride of 512 or more)."""
+    (the cooperative probe rounds start at a stride of 512 or more; with keys of at most 24 bytes
+    the per-lane lookups' binary search over the run)."""
     monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
-    rng = np.random.default_rng(123)
-    prefixes = [b"\x15\x2a\x02huge-subspace-%d\x00" % i for i in range(3)]
+    rng = np.random.default_rng(123 + tail_max)
+    prefixes = [b"\x15\x2a\x02huge-subsp%d\x00" % i for i in range(3)]
+    assert all(len(x) == 16 for x in prefixes)
 
     def key():
         pre = prefixes[int(rng.integers(0, len(prefixes)))]
-        return pre + bytes(rng.integers(0, 256, size=int(rng.integers(0, 40))).astype(np.uint8))
+        return pre + bytes(rng.integers(0, 256, size=int(rng.integers(0, tail_max + 1))).astype(np.uint8))
 
     hist = sorted({key() for _ in range(20000)})
     kb = np.frombuffer(b"".join(hist), np.uint8)
