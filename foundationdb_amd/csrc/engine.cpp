@@ -2118,10 +2118,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // D.Sort and the sorted positions.  Splitters: the quantiles the last batch of >= kQuantMinE
     // endpoints left (stage A runs in batch order on one stream), or this batch's ranked samples
     // when there are none yet (cold start)
+    int sort_nb = 0, sort_samples = 0;  // what the epilogue re-zeroes of the sort's scratch
     {
         const int64_t E = 2 * (R + W);
         const int nbk = sort_bucket_count(E, cs->bucket_target, w.slab_buckets);
         const bool cold = nbk > 1 && (cs->sort_cold || !cs->quant_valid);
+        sort_nb = E > 0 ? nbk : 0;
+        sort_samples = E > 0 && cold ? sort_cold_samples(E, nbk) : 0;
         const bool write_quant = E >= kQuantMinE;
         SplitKey* qt = (SplitKey*)cs->quant.p;
         if (cs->quant_sa && cs->quant_sa != sa) {
@@ -2255,7 +2258,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     launch_epilogue(ys, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
                     gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
-                    compact ? base_hint : nd_after + 1, &sc->ndb[dnew]);
+                    compact ? base_hint : nd_after + 1, &sc->ndb[dnew], sort_nb, sort_samples);
     fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], ys);
     fdb_event(LaunchList::kSyncRecord, sl->ev_free, ys);
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base

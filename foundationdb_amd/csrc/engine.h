@@ -223,6 +223,7 @@ struct Work {
     uint8_t* verdict;      // [T]
     BatchScalars* bsc;
     ScanState scan[kNumScans];
+    int64_t scan_gran[kNumScans];  // granules each scan's slice of the arena holds
     uint64_t* scan_arena;  // zeroed by the previous batch's epilogue (and at allocation)
     int64_t scan_words;
     int64_t cap_T, cap_R;  // workspace capacity (what the epilogue zeroes)
@@ -407,8 +408,12 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 // verdict bytes into the host-mapped result; the epilogue publishes the scalars after them and
 // then the completion flag (the host waits for *flag == seq instead of an event).
 // nd_out: the size word of the delta buffer the batch leaves current (Scalars::ndb).
+// sort_nb / sort_samples: the batch's sort buckets and cold-start samples (their counters and
+// ranks are re-zeroed; 0 samples on a warm start).
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
-                     uint32_t seq, int64_t grid_hint_n, int64_t* nd_out);
+                     uint32_t seq, int64_t grid_hint_n, int64_t* nd_out, int sort_nb, int sort_samples);
+// Cold-start samples of a sort over E endpoints in nb buckets (k_sample; ranks re-zeroed by the epilogue).
+int sort_cold_samples(int64_t E, int nb);
 
 }  // namespace fdbcs

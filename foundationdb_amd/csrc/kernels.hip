@@ -1946,6 +1946,8 @@ __global__ __launch_bounds__(kWG) void k_quant_cold(BatchDev b, const SortItem* 
     }
 }
 
+int sort_cold_samples(int64_t E, int nb) { return (int)std::min<int64_t>(E, std::min(kMaxSample, std::max(1024, 4 * nb))); }
+
 int sort_bucket_count(int64_t E, int target, int slab_buckets) {
     if (target <= 0) target = kSortTarget;
     int64_t nb = (E + target - 1) / target;
@@ -1965,7 +1967,7 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
     fdb_event(LaunchList::kTimingRecord, sort_begin, s);
     if (cold && nb > 1) {  // splitters from this batch's ranked samples
         SampleRank c{};
-        c.S = std::min(E, std::min(kMaxSample, std::max(1024, 4 * nb)));
+        c.S = sort_cold_samples(E, nb);
         c.n_slice = (c.S + kSampleSlice - 1) / kSampleSlice;
         c.srank = w.srank;
         c.samples = w.samples;
@@ -2832,16 +2834,21 @@ struct Epilogue {
     unsigned long long* trace;
     int32_t T;
     int compacted, gc_ran;
-    uint8_t* zero8;  // hist_conf
+    // Scratch the next batch on this workspace expects zeroed: exactly what this batch dirtied
+    // (everything else is still zero from the allocation or an earlier epilogue), not the
+    // workspace's capacity.
+    uint8_t* zero8;  // hist_conf [T]
     int64_t zero8_n;
-    uint8_t* zero8r;  // rconf (read-check variants that only set flags)
+    uint8_t* zero8r;  // rconf [R]
     int64_t zero8r_n;
-    int32_t* zero32b;  // ecur
+    int32_t* zero32b;  // ecur [R]
     int64_t zero32_n;
-    uint64_t* zero64;  // scan arena
-    int64_t zero64_n;
-    uint64_t* zero_bc;  // sort bucket counters [kCntStride kSortMaxBuckets] (two words of each line used)
-    int32_t* zero_rank;  // cold-start sample ranks [kMaxSample + 64]
+    uint64_t* zero64[kNumScans + 1];  // scan arena: the tile counters, then each scan's granules used
+    int64_t zero64_n[kNumScans + 1];
+    uint64_t* zero_bc;  // sort bucket counters of the batch's buckets (two words of each line used)
+    int64_t zero_bc_n;
+    int32_t* zero_rank;  // cold-start sample ranks
+    int64_t zero_rank_n;
     BatchScalars* bsc;   // the batch workspace's scalars (error bits reported, then cleared)
     int64_t* nd_out;     // Scalars::ndb of the delta buffer the batch leaves current
 };
@@ -3145,7 +3152,7 @@ static unsigned copy_tiles(int64_t grid_hint_n, int tile) {
 }
 
 static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, int gc_ran, uint8_t* verdict_out,
-                              uint8_t* verdict_dev, uint32_t* flag, uint32_t seq) {
+                              uint8_t* verdict_dev, uint32_t* flag, uint32_t seq, int sort_nb, int sort_samples) {
     Epilogue ep{};
     ep.verdict_dev = verdict_dev;
     ep.flag = flag;
@@ -3158,15 +3165,27 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
     ep.compacted = compacted;
     ep.gc_ran = gc_ran;
     ep.zero8 = w.hist_conf;
-    ep.zero8_n = w.cap_T;
+    ep.zero8_n = b.T;
     ep.zero8r = w.rconf;
-    ep.zero8r_n = w.cap_R;
+    ep.zero8r_n = b.R;
     ep.zero32b = w.ecur;
-    ep.zero32_n = w.cap_R;
-    ep.zero64 = w.scan_arena;
-    ep.zero64_n = w.scan_words;
+    ep.zero32_n = b.R;
+    // the scans' tile counters, then the granules of the tiles each scan of this batch ran
+    const int64_t G = (int64_t)b.R + b.W;
+    const int64_t used[kNumScans] = {scan_granules(G, 3, kEdgeScanP), 3 * seg_prep_tiles(b.W),
+                                     compacted ? w.scan_gran[kScanCompact] : 0, gc_ran ? w.scan_gran[kScanGc] : 0,
+                                     scan_granules(2 * (int64_t)b.W, 1, kCombineP),
+                                     scan_granules(2 * (int64_t)b.W, 1, kCombineP)};
+    ep.zero64[0] = w.scan_arena;
+    ep.zero64_n[0] = kNumScans;
+    for (int k = 0; k < kNumScans; k++) {
+        ep.zero64[k + 1] = w.scan[k].granules;
+        ep.zero64_n[k + 1] = std::min<int64_t>(used[k], w.scan_gran[k]);
+    }
     ep.zero_bc = w.scnt;
+    ep.zero_bc_n = sort_nb;
     ep.zero_rank = w.srank;
+    ep.zero_rank_n = sort_samples;
     ep.bsc = w.bsc;
     return ep;
 }
@@ -3360,6 +3379,7 @@ void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);
         w.scan[k].granules = g;
+        w.scan_gran[k] = gran[k];
         g += gran[k];
     }
     w.scan_words = g - a;
@@ -3718,12 +3738,14 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
     for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
     for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
-    for (int64_t i = tid; i < ep.zero64_n; i += stride) ep.zero64[i] = 0;
-    for (int64_t i = tid; i < kSortMaxBuckets; i += stride) {
+#pragma unroll
+    for (int k = 0; k <= kNumScans; k++)
+        for (int64_t i = tid; i < ep.zero64_n[k]; i += stride) ep.zero64[k][i] = 0;
+    for (int64_t i = tid; i < ep.zero_bc_n; i += stride) {
         ep.zero_bc[(size_t)kCntStride * i] = 0;
         ep.zero_bc[(size_t)kCntStride * i + 1] = 0;
     }
-    for (int64_t i = tid; i < kMaxSample + 64; i += stride) ep.zero_rank[i] = 0;
+    for (int64_t i = tid; i < ep.zero_rank_n; i += stride) ep.zero_rank[i] = 0;
     __syncthreads();
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiZero);
     if (blockIdx.x != 0) return;
@@ -3852,12 +3874,12 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
                      int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
-                     uint32_t seq, int64_t grid_hint_n, int64_t* nd_out) {
-    Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq);
+                     uint32_t seq, int64_t grid_hint_n, int64_t* nd_out, int sort_nb, int sort_samples) {
+    Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq, sort_nb, sort_samples);
     ep.nd_out = nd_out;
     if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
-    int64_t extra = w.cap_R > w.scan_words ? w.cap_R : w.scan_words;
-    extra = extra > b.T ? extra : b.T;
+    int64_t extra = std::max<int64_t>(b.R, b.T);
+    for (int k = 0; k <= kNumScans; k++) extra = std::max(extra, ep.zero64_n[k]);
     fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
                        (const int64_t*)nullptr, ep);
 }
