@@ -171,7 +171,7 @@ def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split, tail_ma
     the per-lane lookups' binary search over the run)."""
     monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(123 + tail_max)
-    prefixes = [b"\x15\x2a\x02huge-subsp%d\x00" % i for i in range(3)]
+    prefixes = [b"\x15\x2a\x02huge-subspa%d\x00" % i for i in range(3)]
     assert all(len(x) == 16 for x in prefixes)
 
     def key():
