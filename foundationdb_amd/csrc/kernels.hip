@@ -2903,15 +2903,21 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 // boundary of its own (no exact match, not glued to the next segment's B) and the version it
 // inherits, then the exclusive prefixes of removed boundaries, inserted boundaries and tail units
 // with one decoupled look-back across tiles, and tile_first for the copy.  One workgroup per tile
-// of kSegPer segments, 16 lanes each (8 locate B, 8 locate E, cooperatively), plus 8 lanes that
-// locate the B of the segment before the tile, whose lo bounds the tile's first copy tiles.
+// of kSegPer segments: 2 lookups each (B and E) plus one for the B of the segment before the tile,
+// whose lo bounds the tile's first copy tiles; one lane per lookup (lane_lower_bound, 128-thread
+// workgroups), or kArity cooperating lanes for batches of keys over 24 bytes (long-key probes).
 constexpr int kSegPer = kWG / (2 * kArity) - 1;  // 63
 
 inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / kSegPer + 1; }
+// lanes per lookup and workgroup size of k_seg_prep
+constexpr int seg_lanes(bool long_keys) { return long_keys ? kArity : 1; }
+constexpr int seg_threads(bool long_keys) { return 2 * seg_lanes(long_keys) * (kSegPer + 1); }
 
 template <bool LONG>
-__global__ __launch_bounds__(kWG) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm, const uint8_t* htail,
-                                                  Scalars* sc, TierIO io, int64_t* lvl3, int64_t lvl3_n) {
+__global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
+                                                                const uint8_t* htail, Scalars* sc, TierIO io,
+                                                                int64_t* lvl3, int64_t lvl3_n) {
+    constexpr int LL = seg_lanes(LONG);
     __shared__ int64_t s_lo[kSegPer + 1];       // lo of the segment before the tile, then the tile's
     __shared__ uint32_t s_val[3][kSegPer + 1];  // removed, inserted, tail units per segment
     __shared__ uint32_t s_base[3];
@@ -2927,7 +2933,7 @@ __global__ __launch_bounds__(kWG) void k_seg_prep(BatchDev b, Work w, Hist h, Ma
     const int ntiles = U > 0 ? (U + kSegPer - 1) / kSegPer : 1;
     if (tile >= ntiles) return;  // spare workgroup: nobody waits on it
     const int64_t n = *io.n_in;
-    const int q = threadIdx.x / (2 * kArity), role = (threadIdx.x / kArity) & 1;
+    const int q = threadIdx.x / (2 * LL), role = (threadIdx.x / LL) & 1;
     const int sg = tile * kSegPer + (q < kSegPer ? q : -1);  // slot kSegPer: the segment before
     const bool live = sg >= 0 && sg < U && (q < kSegPer || role == 0);
     int64_t pos = 0;
@@ -2936,12 +2942,15 @@ __global__ __launch_bounds__(kWG) void k_seg_prep(BatchDev b, Work w, Hist h, Ma
     if (live) {
         kb = seg_key(b, w, w.seg_b[sg], 0);
         ke = seg_key(b, w, w.seg_e[sg], 1);
-        pos = group_lower_bound<LONG>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        if constexpr (LONG)
+            pos = group_lower_bound<true>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        else
+            pos = lane_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
     }
     const int lane = threadIdx.x & 63;
-    const int64_t hi = __shfl(pos, (lane + kArity) & 63, 64);
-    const int exact = __shfl((int)eq, (lane + kArity) & 63, 64);
-    if (threadIdx.x % (2 * kArity) == 0) {
+    const int64_t hi = __shfl(pos, (lane + LL) & 63, 64);
+    const int exact = __shfl((int)eq, (lane + LL) & 63, 64);
+    if (threadIdx.x % (2 * LL) == 0) {
         if (q == kSegPer) {
             s_lo[0] = live ? pos : 0;
         } else if (live) {
@@ -3011,7 +3020,10 @@ constexpr int kSegLds = 1024;
 // Copy surviving old boundaries to their new positions and write each segment's inserts.  Per
 // tile, the segments that can affect it are staged in LDS; element i is removed iff
 // lo_j <= i < hi_j for the last segment j with lo_j <= i, else it moves to i - rem_before +
-// ins_before.  `Ins` writes segment s's new boundaries starting at output position o.
+// ins_before.  `Ins` writes segment s's new boundaries starting at output position o; the inserts
+// are spread over the whole grid (grid-stride over the segments), not over the copy tiles that own
+// their positions: right after a compaction the delta is nearly empty and one copy tile owns every
+// segment of the batch (at the reference's 32768-transaction cap, ~60k inserts by one workgroup).
 template <class Ins, int TILE>
 __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist dst, const int64_t* n_in,
                                                        const int64_t* U_ptr, Ins ins) {
@@ -3097,10 +3109,10 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                 dst.ver[o] = src.ver[i];
             }
         }
-        for (int sg = s_ins0 + threadIdx.x; sg < s_ins1; sg += blockDim.x)
-            ins(sg, dst, g.lo[sg] - g.rem[sg] + g.ins[sg]);
         __syncthreads();
     }
+    for (int64_t sg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sg < U; sg += (int64_t)gridDim.x * blockDim.x)
+        ins((int)sg, dst, g.lo[sg] - g.rem[sg] + g.ins[sg]);
 }
 
 // Inserts of a union segment: B at `now`, E (when needed) at the version it had.
@@ -3144,8 +3156,11 @@ struct BatchIns {
 
 static Segs batch_segs(const Work& w) { return Segs{w.seg_lo, w.seg_hi, w.seg_rem, w.seg_ins, w.tile_first}; }
 
-static unsigned copy_tiles(int64_t grid_hint_n, int tile) {
+// Workgroups of a merge copy: the copy tiles of a source of about grid_hint_n boundaries, and at
+// least one thread per insert of up to max_inserts segments.
+static unsigned copy_tiles(int64_t grid_hint_n, int tile, int64_t max_inserts = 0) {
     int64_t tiles = (grid_hint_n + 1 + tile - 1) / tile;
+    tiles = std::max<int64_t>(tiles, (max_inserts + kBlock - 1) / kBlock);
     if (tiles < 1) tiles = 1;
     if (tiles > 8192) tiles = 8192;
     return (unsigned)tiles;
@@ -3197,8 +3212,8 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
-    fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_prep_tiles(b.W)), dim3(kWG), 0, s, b,
-               w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n);
+    fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_prep_tiles(b.W)),
+               dim3(seg_threads(long_keys)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
     ins.b = b;
@@ -3211,7 +3226,7 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     ins.htail = htail;
     ins.sc = sc;
     ins.now = now;
-    fdb_launch((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile)), dim3(kBlock), 0,
+    fdb_launch((k_merge_copy<BatchIns, kDeltaTile>), dim3(copy_tiles(grid_hint_n, kDeltaTile, b.W)), dim3(kBlock), 0,
                s, batch_segs(w), src, dst, nd_src, &w.bsc->n_segments, ins);
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
@@ -3305,7 +3320,8 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
     launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
                    w.scan[kScanCompact]);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
-    fdb_launch((k_merge_copy<CompactIns, kBaseTile>), dim3(copy_tiles(grid_hint_n, kBaseTile)), dim3(kBlock), 0,
+    fdb_launch((k_merge_copy<CompactIns, kBaseTile>), dim3(copy_tiles(grid_hint_n, kBaseTile, delta_hint_n + 1)),
+                       dim3(kBlock), 0,
                        s, g, base, dst,
                        &sc->n, &sc->nd_next, CompactIns{delta, w.c_val, w.c_ins});
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
@@ -3642,7 +3658,14 @@ void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
 // Range-max levels over lvl[0][0, n0) (lvl[3] reset beforehand); with a batch attached, also the
 // verdicts and the scalar roll-over.  n0 comes from `n_levels` or, for a batch, from the tier
 // that changed.
-__global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, const int64_t* n_levels, Epilogue ep) {
+// kEpiWaves waves per workgroup of 4096 boundaries, kFan / kEpiWaves level-1 blocks per wave: the
+// loads of a block's 64 versions are one wave instruction, and the more waves share the 4096
+// boundaries, the shorter each wave's chain of loads, reductions and stores.
+constexpr int kEpiWaves = 16;
+constexpr int kEpiThreads = 64 * kEpiWaves;
+constexpr int kEpiBlocks = kFan / kEpiWaves;  // level-1 blocks per wave
+
+__global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* sc, const int64_t* n_levels, Epilogue ep) {
     __shared__ int64_t l1[kFan];
     if (threadIdx.x == 0) trace_min(ep.trace, kTrEpiBegin);
     int64_t n0;
@@ -3655,30 +3678,30 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
     const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int64_t b2 = blockIdx.x; b2 < n2; b2 += gridDim.x) {
-        // each wave reduces 16 blocks of 64 versions: all 16 loads first, then the reductions
-        const int64_t b1_0 = b2 * kFan + wid * (kFan / 4);
-        int64_t v[kFan / 4];
+        // each wave reduces kEpiBlocks blocks of 64 versions: all loads first, then the reductions
+        const int64_t b1_0 = b2 * kFan + wid * kEpiBlocks;
+        int64_t v[kEpiBlocks];
 #pragma unroll
-        for (int q = 0; q < kFan / 4; q++) {
+        for (int q = 0; q < kEpiBlocks; q++) {
             const int64_t i = (b1_0 + q) * kFan + lane;
             v[q] = i < n0 ? m.lvl[0][i] : LLONG_MIN;
         }
-        const int64_t b1l = b1_0 + lane;  // lane q < 16 owns block b1_0 + q
+        const int64_t b1l = b1_0 + lane;  // lane q < kEpiBlocks owns block b1_0 + q
         ulonglong2 sk = make_ulonglong2(0, 0);
         uint64_t prev_hi = 0;  // the previous block's sampled key (delta directory fill)
-        if (lane < kFan / 4 && b1l < n1) {
+        if (lane < kEpiBlocks && b1l < n1) {
             sk = m.keys[b1l * kFan];  // sampled key of the block
             if (m.edir_epoch && b1l > 0) prev_hi = m.keys[(b1l - 1) * kFan].x;
         }
-        // every 8th boundary of the wave's 16 blocks (128 entries of skey8, two per lane)
-#pragma unroll
-        for (int h8 = 0; h8 < 2; h8++) {
-            const int64_t e8 = b1_0 * (kFan / 8) + h8 * 64 + lane;
-            if (e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
+        // every 8th boundary of the wave's blocks (8 entries of skey8 per block)
+        static_assert(kEpiBlocks * kFan / 8 <= 64, "one skey8 entry per lane");
+        {
+            const int64_t e8 = b1_0 * (kFan / 8) + lane;
+            if (lane < kEpiBlocks * kFan / 8 && e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
         }
         int64_t mine = LLONG_MIN;
 #pragma unroll
-        for (int q = 0; q < kFan / 4; q++) {
+        for (int q = 0; q < kEpiBlocks; q++) {
             int64_t x = v[q];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
@@ -3687,7 +3710,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
             }
             if (lane == q) mine = x;
         }
-        if (lane < kFan / 4) {
+        if (lane < kEpiBlocks) {
             if (b1l < n1) {
                 m.lvl[1][b1l] = mine;
                 m.skey[0][b1l] = sk;
@@ -3711,7 +3734,7 @@ __global__ __launch_bounds__(kBlock) void k_epilogue(MaxLevels m, Scalars* sc, c
                         for (int64_t v = c + 1; v <= kDirSlots && v <= c + kDirRun; v++) m.edir[v] = tag | (uint64_t)n1;
                 }
             }
-            l1[wid * (kFan / 4) + lane] = mine;
+            l1[wid * kEpiBlocks + lane] = mine;
         }
         __syncthreads();
         if (wid == 0) {
@@ -3830,7 +3853,7 @@ __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
 
 static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
     int64_t g = (hint_n + (int64_t)kFan * kFan - 1) / ((int64_t)kFan * kFan);
-    const int64_t ge = (extra + kBlock - 1) / kBlock;
+    const int64_t ge = (extra + kEpiThreads - 1) / kEpiThreads;
     g = g > ge ? g : ge;
     g = g < 1 ? 1 : g;
     return g > 4096 ? 4096 : g;
@@ -3869,7 +3892,7 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
     fdb_launch(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
     Epilogue ep{};
     ep.trace = nullptr;
-    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kBlock), 0, s, m, sc, n, ep);
+    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kEpiThreads), 0, s, m, sc, n, ep);
 }
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
@@ -3880,7 +3903,7 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
     int64_t extra = std::max<int64_t>(b.R, b.T);
     for (int k = 0; k <= kNumScans; k++) extra = std::max(extra, ep.zero64_n[k]);
-    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kBlock), 0, s, m, sc,
+    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kEpiThreads), 0, s, m, sc,
                        (const int64_t*)nullptr, ep);
 }
 
