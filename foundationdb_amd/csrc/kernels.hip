@@ -2904,13 +2904,14 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 // inherits, then the exclusive prefixes of removed boundaries, inserted boundaries and tail units
 // with one decoupled look-back across tiles, and tile_first for the copy.  One workgroup per tile
 // of kSegPer segments: 2 lookups each (B and E) plus one for the B of the segment before the tile,
-// whose lo bounds the tile's first copy tiles; one lane per lookup (lane_lower_bound, 128-thread
-// workgroups), or kArity cooperating lanes for batches of keys over 24 bytes (long-key probes).
+// whose lo bounds the tile's first copy tiles, kArity cooperating lanes per lookup.  (One lane per
+// lookup in 128-thread workgroups, as the read check does, measured slower here: 19.7 vs 18.0 us
+// per launch at C2 on one box; the tiles' look-back chain, not the lookups, sets the pace.)
 constexpr int kSegPer = kWG / (2 * kArity) - 1;  // 63
 
 inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / kSegPer + 1; }
 // lanes per lookup and workgroup size of k_seg_prep
-constexpr int seg_lanes(bool long_keys) { return long_keys ? kArity : 1; }
+constexpr int seg_lanes(bool long_keys) { return (void)long_keys, kArity; }
 constexpr int seg_threads(bool long_keys) { return 2 * seg_lanes(long_keys) * (kSegPer + 1); }
 
 template <bool LONG>
@@ -2942,10 +2943,7 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
     if (live) {
         kb = seg_key(b, w, w.seg_b[sg], 0);
         ke = seg_key(b, w, w.seg_e[sg], 1);
-        if constexpr (LONG)
-            pos = group_lower_bound<true>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
-        else
-            pos = lane_lower_bound(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        pos = group_lower_bound<LONG>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
     }
     const int lane = threadIdx.x & 63;
     const int64_t hi = __shfl(pos, (lane + LL) & 63, 64);
@@ -3659,9 +3657,9 @@ void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
 // verdicts and the scalar roll-over.  n0 comes from `n_levels` or, for a batch, from the tier
 // that changed.
 // kEpiWaves waves per workgroup of 4096 boundaries, kFan / kEpiWaves level-1 blocks per wave: the
-// loads of a block's 64 versions are one wave instruction, and the more waves share the 4096
-// boundaries, the shorter each wave's chain of loads, reductions and stores.
-constexpr int kEpiWaves = 16;
+// loads of a block's 64 versions are one wave instruction.  16 waves per workgroup (4 blocks each)
+// measured slower than 4 (C2, same box: 22.6 vs 18.6 us per launch).
+constexpr int kEpiWaves = 4;
 constexpr int kEpiThreads = 64 * kEpiWaves;
 constexpr int kEpiBlocks = kFan / kEpiWaves;  // level-1 blocks per wave
 
@@ -3694,10 +3692,10 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             if (m.edir_epoch && b1l > 0) prev_hi = m.keys[(b1l - 1) * kFan].x;
         }
         // every 8th boundary of the wave's blocks (8 entries of skey8 per block)
-        static_assert(kEpiBlocks * kFan / 8 <= 64, "one skey8 entry per lane");
-        {
-            const int64_t e8 = b1_0 * (kFan / 8) + lane;
-            if (lane < kEpiBlocks * kFan / 8 && e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
+#pragma unroll
+        for (int h8 = 0; h8 < (kEpiBlocks * kFan / 8 + 63) / 64; h8++) {
+            const int64_t e8 = b1_0 * (kFan / 8) + h8 * 64 + lane;
+            if (h8 * 64 + lane < kEpiBlocks * kFan / 8 && e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
         }
         int64_t mine = LLONG_MIN;
 #pragma unroll
