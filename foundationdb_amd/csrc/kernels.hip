@@ -1141,11 +1141,52 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
 //   * the tier's deepest sample level of at most kStageMax entries is staged in LDS by the
 //     workgroup (one coalesced fill beside the key loads), so a lookup starts below it: C4's base
 //     tier (50M boundaries) skips four global levels of its seven;
-//   * a single-key read [k, k\0) (FDBTypes.h:499-505; C4's point reads) needs no lookup of its
-//     end: no key lies between k and k\0, so it ends right after k (or at k's own position).
-// (One group per read with the end searched from the begin's position measured no faster: the
-// wide reads' chains got longer, and they set the kernel's length.)
+//   * a read's end key is found from its begin key's position, not by a lookup of its own: a
+//     single-key read [k, k\0) (FDBTypes.h:499-505; C4's point reads) ends right after k, since no
+//     key lies between k and k\0, and any other read first searches the 512 boundaries after its
+//     begin (a Tuple.range() read covers one user's few dozen), falling back to a lookup;
+//   * one group per read instead of two halves the waves.
 constexpr int kStageMax = 2048;  // entries of the LDS-staged sample level (32 KiB)
+
+// lower_bound of q in [lo, hi) (q above every boundary before lo): rounds of kArity probes at a
+// shrinking stride (the span search of group_lower_bound).
+template <bool LONG>
+__device__ __forceinline__ int64_t group_span_lower_bound(const Hist& h, int64_t lo, int64_t hi, const DKey& q,
+                                                          const uint8_t* htail, const uint8_t* qtail, bool& eq) {
+    const int gl = threadIdx.x & (kArity - 1);
+    const int g0 = threadIdx.x & 63 & ~(kArity - 1);
+    QTail qt;
+    if constexpr (LONG) load_qtail(qt, q, qtail);
+    auto probe = [&](int64_t p) -> int {
+        if constexpr (LONG) {
+            const ulonglong2 k = h.key[p];
+            const uint2 lt = h.lt[p];
+            return probe_cmp_long(k, lt, htail, q, qt, qtail);
+        } else {
+            return probe_cmp(h, p, h.key[p], htail, q, qtail);
+        }
+    };
+    eq = false;
+    int64_t span = hi - lo;
+    int64_t stride0 = kFan / kArity;
+    while (stride0 * kArity < span) stride0 *= kArity;
+    bool eq_cand = false;
+    for (int64_t stride = stride0; span > 0; stride = stride > kArity ? stride / kArity : 1) {
+        const int64_t p = lo + stride * (gl + 1) - 1;
+        const bool v = stride * (gl + 1) <= span && p < hi;
+        int r = 1;
+        if (v) r = probe(p);
+        const uint32_t valid = gmask(v);
+        const int cnt = __popc(gmask(v && r < 0));
+        const int stop = __shfl(r, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
+        if (cnt < __popc(valid)) eq_cand = stop == 0;
+        lo += stride * cnt;
+        span = cnt < __popc(valid) ? stride - 1 : span - stride * cnt;
+        if (stride == 1) break;
+    }
+    if (lo < hi) eq = eq_cand;
+    return lo;
+}
 
 // Is ke = kb + "\0", i.e. is [kb, ke) a single-key range (keyAfter, FDBTypes.h:499-505)?
 __device__ __forceinline__ bool is_key_after(const DKey& kb, const DKey& ke, const uint8_t* tail) {
@@ -1171,44 +1212,48 @@ __global__ __launch_bounds__(kBlock) void k_check_tier_long(BatchDev b, Tier t, 
     for (int64_t i = threadIdx.x; i < stage_n; i += blockDim.x) s_stage[i] = stage_src[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int lead = lane & ~(kTierLanes - 1);  // first lane of the read (its begin group)
-    const int grp = (lane / kArity) & 1;       // 0: begin key, 1: end key
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTierLanes;
+    const int g0 = lane & ~(kArity - 1);
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kArity;
     const bool live = r < b.R;
     const int64_t rr = live ? r : 0;
     const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
     const int64_t snap = b.snap[b.rowner[rr]];
     const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
     const bool active = live && (BASE || n > 0);
-    // a single-key read [k, k\0) needs no lookup of its end (the end group idles)
-    const bool point = !degenerate && is_key_after(kb, ke, b.tail);
     const ulonglong2* st = stage_n > 0 ? s_stage : nullptr;
-    int64_t lb = 0;
+    int64_t lb = 0, j = 0;
     bool eq = false;
-    if (active && (grp == 0 || !(degenerate || point)))
-        lb = group_lower_bound<true>(t.h, t.m, n, grp ? ke : kb, htail, b.tail, eq, st, stage_level, stage_n);
-    const int64_t lbb = __shfl(lb, lead, 64);
-    const int eqb = __shfl((int)eq, lead, 64);
-    int64_t j = __shfl(lb, lead + kArity, 64);
-    if (point) j = lbb + (eqb ? 1 : 0);  // the boundary k itself, if any, is the only one in [k, k\0)
+    if (active) {
+        lb = group_lower_bound<true>(t.h, t.m, n, kb, htail, b.tail, eq, st, stage_level, stage_n);
+        if (!degenerate) {
+            if (is_key_after(kb, ke, b.tail)) {
+                j = lb + (eq ? 1 : 0);  // the boundary k itself, if there is one, is the only one in [k, k\0)
+            } else {
+                const int64_t hi = min(n, lb + (int64_t)8 * kFan);
+                bool eqe;
+                j = group_span_lower_bound<true>(t.h, lb, hi, ke, htail, b.tail, eqe);
+                if (j == hi && hi < n) j = group_lower_bound<true>(t.h, t.m, n, ke, htail, b.tail, eqe, st, stage_level, stage_n);
+            }
+        }
+    }
     bool conf = false;
     if (active) {
         const int64_t hdr = BASE ? t.hdr : kHole;
         if (degenerate) {
-            conf = (lbb > 0 ? t.h.ver[lbb - 1] : hdr) > snap;
+            conf = (lb > 0 ? t.h.ver[lb - 1] : hdr) > snap;
         } else {
-            const int64_t ub = lbb + (eqb ? 1 : 0);
+            const int64_t ub = lb + (eq ? 1 : 0);
             // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
-            conf = (ub == 0 && hdr > snap) || group_range_max(t.m, ub > 0 ? ub - 1 : 0, j, snap) > snap;
+            conf = (ub == 0 && hdr > snap) || group_range_max<kArity>(t.m, ub > 0 ? ub - 1 : 0, j, snap) > snap;
         }
     }
     if (!BASE && ps.n) {  // the previous batch's union segments, not merged into the delta yet
         const int64_t U = *ps.n;
         bool hit = false;
-        if (live && grp == 1 && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
-        conf = conf || __shfl((int)hit, lead + kArity, 64);
+        if (live && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
+        conf = conf || hit;
     }
-    if (live && lane == lead && conf) {
+    if (live && lane == g0 && conf) {
         rconf[r] = 1;
         hist_conf[b.rowner[r]] = 1;
     }
@@ -1412,7 +1457,7 @@ void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Ti
         return;
     }
     if (long_keys && stage_level >= 0) {
-        const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
+        const int grid = (int)(((int64_t)b.R * kArity + kBlock - 1) / kBlock);
         fdb_launch(is_base ? k_check_tier_long<true> : k_check_tier_long<false>, dim3(grid), dim3(kBlock), 0, s, b, t,
                    htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps,
                    (const ulonglong2*)t.m.skey[stage_level], stage_level);
