@@ -218,8 +218,6 @@ struct fdbcs_conflict_set {
                               // separate waves, 1: kArity lanes per lookup, the four of a read in one wave)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
-    bool long_check = true;   // FDBCS_LONG_CHECK=0: the split check's long-key batches use the two-group
-                              // cooperative k_check_tier instead of k_check_tier_long (A/B)
     bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
                               // even for batches with keys over 16 bytes (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
@@ -1085,7 +1083,6 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2' ? 1 : (v[0] == '3' ? 2 : 0);
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
-    if (const char* v = getenv("FDBCS_LONG_CHECK")) cs->long_check = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
@@ -2159,8 +2156,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
             fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
-        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, PrevSegs{}, lanes,
-                          long_keys && cs->long_check ? stage_level_for(cs->n_ub) : -1);
+        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, PrevSegs{}, lanes);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
@@ -2178,8 +2174,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const bool graphs = cs->stage_graphs && timing != 2;
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, !cs->group_rmax, ps, lanes,
-                          long_keys && cs->long_check ? stage_level_for(std::max<int64_t>(cs->nd_ub, 1)) : -1);
+        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, !cs->group_rmax, ps, lanes);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);

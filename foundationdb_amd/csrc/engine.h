@@ -360,14 +360,10 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
 // delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
 // long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
-// lanes: one lane per lookup (FDBCS_CHECK=7 on keys up to 24 bytes).  stage_level >= 0 with
-// long_keys: k_check_tier_long, one group per read, that sample level staged in LDS
-// (stage_level_for(a bound on the tier's size); -1: the cooperative k_check_tier).
+// lanes: one lane per lookup (FDBCS_CHECK=7 on keys up to 24 bytes).
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
                        const uint8_t* htail, bool long_keys = false, bool lead_rmax = false,
-                       const PrevSegs& ps = PrevSegs{}, bool lanes = false, int stage_level = -1);
-// The deepest sample level of a tier of at most n_bound boundaries that fits the LDS stage (-1: none).
-int stage_level_for(int64_t n_bound);
+                       const PrevSegs& ps = PrevSegs{}, bool lanes = false);
 // Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
 // k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,

@@ -330,31 +330,10 @@ __device__ __forceinline__ uint32_t gmask(bool pred) {
     return (uint32_t)(m >> (threadIdx.x & 63 & ~(kArity - 1))) & ((1u << kArity) - 1u);
 }
 
-// Entries of an LDS-staged sample level lds[0, n) whose prefix is below q's, by the kArity lanes of
-// a group: (kArity + 1)-ary search, each step one LDS read per lane (four steps for 2048 entries
-// instead of one global round trip per tree level above the staged one).
-__device__ __forceinline__ int64_t group_count_lds(const ulonglong2* lds, int64_t n, const DKey& q) {
-    const int gl = threadIdx.x & (kArity - 1);
-    int64_t lo = 0, hi = n;  // entries [0, lo) are below q, [hi, n) are not
-    while (lo < hi) {
-        const int64_t idx = lo + ((hi - lo) * (gl + 1)) / (kArity + 1);
-        const int c = __popc(gmask(prefix_less(lds[idx], q)));  // the probes below q form a prefix
-        const int64_t nlo = c > 0 ? lo + ((hi - lo) * c) / (kArity + 1) + 1 : lo;
-        const int64_t nhi = c < kArity ? lo + ((hi - lo) * (c + 1)) / (kArity + 1) : hi;
-        lo = nlo;
-        hi = nhi;
-    }
-    return lo;
-}
-
 // LONG: the long-key probes above (the batch has keys over 16 bytes); same result.
-// stage: the tier's sample level stage_level copied to LDS by the caller's workgroup (stage_n
-// entries, the whole level): the descent starts below it (null: from the top of the tree).
 template <bool LONG = false>
 __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
-                                                     const uint8_t* htail, const uint8_t* qtail, bool& eq,
-                                                     const ulonglong2* stage = nullptr, int stage_level = 0,
-                                                     int64_t stage_n = 0) {
+                                                     const uint8_t* htail, const uint8_t* qtail, bool& eq) {
     const int gl = threadIdx.x & (kArity - 1);
     const int g0 = threadIdx.x & 63 & ~(kArity - 1);  // first lane of the group
     eq = false;
@@ -420,22 +399,15 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
         }
     }
     if (!direct) {
-        int start = top;
-        if (stage && stage_level < top) {
-            start = stage_level;
-            c = group_count_lds(stage, stage_n, q);
-            if (stage_level == 0 && c < stage_n) bknown = !prefix_eq(stage[c]);
-        } else {
-            for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
-                const bool v = j0 == 0 ? v_top : j0 + gl < sz[top];
-                const ulonglong2 e = j0 == 0 ? e_top : m.skey[top][v ? j0 + gl : 0];
-                const int k = __popc(gmask(v && prefix_less(e, q)));
-                if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
-                c += k;
-                if (k < kArity) break;
-            }
+        for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
+            const bool v = j0 == 0 ? v_top : j0 + gl < sz[top];
+            const ulonglong2 e = j0 == 0 ? e_top : m.skey[top][v ? j0 + gl : 0];
+            const int k = __popc(gmask(v && prefix_less(e, q)));
+            if (top == 0 && k < __popc(gmask(v))) bknown = !((gmask(v && prefix_eq(e)) >> k) & 1u);
+            c += k;
+            if (k < kArity) break;
         }
-        for (int L = start; L > 0; L--) {
+        for (int L = top; L > 0; L--) {
             if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
             // entries of level L-1 below q: [0, c') with c' in [A(c-1)+1, Ac]
             const int64_t base = (int64_t)kArity * (c - 1) + 1;
@@ -742,9 +714,7 @@ constexpr int kTierLanes = 2 * kArity;
 // max-reduced across the lanes; stops after a level once above `snap`.  A wide read (C4's
 // Tuple.range() over a user's ~50 boundaries) costs one round of loads instead of a dependent scan
 // by one lane.
-template <int GL = kTierLanes>
 __device__ __forceinline__ int64_t group_range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
-    constexpr int kTierLanes = GL;  // lanes sharing the range max
     const int sl = threadIdx.x & (kTierLanes - 1);
     int64_t best = LLONG_MIN;
     for (int L = 0; L < kMaxLevels; L++) {
@@ -1135,130 +1105,6 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
     }
 }
 
-// ---- long-key split check (keys over 24 bytes, C4): one kArity-lane group per read
-//
-// The cooperative long-key lookups, with three changes for tuple keys:
-//   * the tier's deepest sample level of at most kStageMax entries is staged in LDS by the
-//     workgroup (one coalesced fill beside the key loads), so a lookup starts below it: C4's base
-//     tier (50M boundaries) skips four global levels of its seven;
-//   * a read's end key is found from its begin key's position, not by a lookup of its own: a
-//     single-key read [k, k\0) (FDBTypes.h:499-505; C4's point reads) ends right after k, since no
-//     key lies between k and k\0, and any other read first searches the 512 boundaries after its
-//     begin (a Tuple.range() read covers one user's few dozen), falling back to a lookup;
-//   * one group per read instead of two halves the waves.
-constexpr int kStageMax = 2048;  // entries of the LDS-staged sample level (32 KiB)
-
-// lower_bound of q in [lo, hi) (q above every boundary before lo): rounds of kArity probes at a
-// shrinking stride (the span search of group_lower_bound).
-template <bool LONG>
-__device__ __forceinline__ int64_t group_span_lower_bound(const Hist& h, int64_t lo, int64_t hi, const DKey& q,
-                                                          const uint8_t* htail, const uint8_t* qtail, bool& eq) {
-    const int gl = threadIdx.x & (kArity - 1);
-    const int g0 = threadIdx.x & 63 & ~(kArity - 1);
-    QTail qt;
-    if constexpr (LONG) load_qtail(qt, q, qtail);
-    auto probe = [&](int64_t p) -> int {
-        if constexpr (LONG) {
-            const ulonglong2 k = h.key[p];
-            const uint2 lt = h.lt[p];
-            return probe_cmp_long(k, lt, htail, q, qt, qtail);
-        } else {
-            return probe_cmp(h, p, h.key[p], htail, q, qtail);
-        }
-    };
-    eq = false;
-    int64_t span = hi - lo;
-    int64_t stride0 = kFan / kArity;
-    while (stride0 * kArity < span) stride0 *= kArity;
-    bool eq_cand = false;
-    for (int64_t stride = stride0; span > 0; stride = stride > kArity ? stride / kArity : 1) {
-        const int64_t p = lo + stride * (gl + 1) - 1;
-        const bool v = stride * (gl + 1) <= span && p < hi;
-        int r = 1;
-        if (v) r = probe(p);
-        const uint32_t valid = gmask(v);
-        const int cnt = __popc(gmask(v && r < 0));
-        const int stop = __shfl(r, g0 + (cnt < kArity ? cnt : kArity - 1), 64);
-        if (cnt < __popc(valid)) eq_cand = stop == 0;
-        lo += stride * cnt;
-        span = cnt < __popc(valid) ? stride - 1 : span - stride * cnt;
-        if (stride == 1) break;
-    }
-    if (lo < hi) eq = eq_cand;
-    return lo;
-}
-
-// Is ke = kb + "\0", i.e. is [kb, ke) a single-key range (keyAfter, FDBTypes.h:499-505)?
-__device__ __forceinline__ bool is_key_after(const DKey& kb, const DKey& ke, const uint8_t* tail) {
-    if (ke.len != kb.len + 1u || ke.hi != kb.hi || ke.lo != kb.lo) return false;
-    if (kb.len < 16u) return true;  // the zero-padded prefixes agree: ke's byte at kb.len is 0
-    // bytes [16, kb.len) equal, and ke's byte kb.len is 0
-    return tail_cmp(tail + kb.tail, kb.len, tail + ke.tail, kb.len) == 0 && tail[ke.tail + (kb.len - 16u)] == 0;
-}
-
-template <bool BASE>
-__global__ __launch_bounds__(kBlock) void k_check_tier_long(BatchDev b, Tier t, const uint8_t* htail,
-                                                            uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps,
-                                                            const ulonglong2* stage_src, int stage_level) {
-    __shared__ ulonglong2 s_stage[kStageMax];
-    const int64_t n = *t.n;
-    // entries of the staged level for this tier size (the host picked a level that fits its bound)
-    int64_t stage_n = 0;
-    if (stage_src && n > 0) {
-        stage_n = (n + kFan - 1) / kFan;
-        for (int L = 0; L < stage_level; L++) stage_n = (stage_n + kArity - 1) / kArity;
-        if (stage_n > kStageMax) stage_n = 0;  // (a bound the host got wrong: no staging)
-    }
-    for (int64_t i = threadIdx.x; i < stage_n; i += blockDim.x) s_stage[i] = stage_src[i];
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int g0 = lane & ~(kArity - 1);
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kArity;
-    const bool live = r < b.R;
-    const int64_t rr = live ? r : 0;
-    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
-    const int64_t snap = b.snap[b.rowner[rr]];
-    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    const bool active = live && (BASE || n > 0);
-    const ulonglong2* st = stage_n > 0 ? s_stage : nullptr;
-    int64_t lb = 0, j = 0;
-    bool eq = false;
-    if (active) {
-        lb = group_lower_bound<true>(t.h, t.m, n, kb, htail, b.tail, eq, st, stage_level, stage_n);
-        if (!degenerate) {
-            if (is_key_after(kb, ke, b.tail)) {
-                j = lb + (eq ? 1 : 0);  // the boundary k itself, if there is one, is the only one in [k, k\0)
-            } else {
-                const int64_t hi = min(n, lb + (int64_t)8 * kFan);
-                bool eqe;
-                j = group_span_lower_bound<true>(t.h, lb, hi, ke, htail, b.tail, eqe);
-                if (j == hi && hi < n) j = group_lower_bound<true>(t.h, t.m, n, ke, htail, b.tail, eqe, st, stage_level, stage_n);
-            }
-        }
-    }
-    bool conf = false;
-    if (active) {
-        const int64_t hdr = BASE ? t.hdr : kHole;
-        if (degenerate) {
-            conf = (lb > 0 ? t.h.ver[lb - 1] : hdr) > snap;
-        } else {
-            const int64_t ub = lb + (eq ? 1 : 0);
-            // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
-            conf = (ub == 0 && hdr > snap) || group_range_max<kArity>(t.m, ub > 0 ? ub - 1 : 0, j, snap) > snap;
-        }
-    }
-    if (!BASE && ps.n) {  // the previous batch's union segments, not merged into the delta yet
-        const int64_t U = *ps.n;
-        bool hit = false;
-        if (live && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
-        conf = conf || hit;
-    }
-    if (live && lane == g0 && conf) {
-        rconf[r] = 1;
-        hist_conf[b.rowner[r]] = 1;
-    }
-}
-
 // ------------------------------------------------------------------ D.Sort
 
 // Endpoint item p of the batch (KeyInfo, SkipList.cpp:77-87): range g = p / 2, end = p & 1.
@@ -1436,31 +1282,13 @@ __global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t,
     check_read_lanes_tier(b, t, BASE, htail, hist_conf, rconf, ps);
 }
 
-int stage_level_for(int64_t n_bound) {
-    int64_t sz = (n_bound + kFan - 1) / kFan;
-    int L = 0;
-    while (sz > kStageMax && L + 1 < kIdxLevels) {
-        sz = (sz + kArity - 1) / kArity;
-        L++;
-    }
-    return sz <= kStageMax ? L : -1;
-}
-
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys, bool lead_rmax, const PrevSegs& ps, bool lanes,
-                       int stage_level) {
+                       const uint8_t* htail, bool long_keys, bool lead_rmax, const PrevSegs& ps, bool lanes) {
     if (b.R == 0) return;
     if (lanes) {
         const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
         fdb_launch(is_base ? k_check_lanes_tier<true> : k_check_lanes_tier<false>, dim3(grid), dim3(kBlock), 0, s, b,
                    t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
-        return;
-    }
-    if (long_keys && stage_level >= 0) {
-        const int grid = (int)(((int64_t)b.R * kArity + kBlock - 1) / kBlock);
-        fdb_launch(is_base ? k_check_tier_long<true> : k_check_tier_long<false>, dim3(grid), dim3(kBlock), 0, s, b, t,
-                   htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps,
-                   (const ulonglong2*)t.m.skey[stage_level], stage_level);
         return;
     }
     const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
