@@ -7,7 +7,7 @@ O=gpurun_out/${TAG:-iter}
 mkdir -p $O
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
-    ${TEST_ARGS:-} > $O/gpu_tests.log 2>&1
+    -k "${TEST_K:-}" > $O/gpu_tests.log 2>&1
   rc=$?
   tail -3 $O/gpu_tests.log
   [ $rc -ne 0 ] && { grep -E "FAILED|Error|error" $O/gpu_tests.log | head -20; exit $rc; }

@@ -339,12 +339,14 @@ def test_c3_zipf_heavy_contention(engine, oracle_mod, monkeypatch, prepass):
     e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
 
 
-@pytest.mark.parametrize("gc_interval,delta_limit", [(1, 0), (0, 3000)])
-def test_c4_tuple_keys_window_gc(engine, oracle_mod, gc_interval, delta_limit):
+@pytest.mark.parametrize("gc_interval,delta_limit,split", [(1, 0, "2"), (0, 3000, "2"), (1, 0, "1"), (0, 3000, "1")])
+def test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, gc_interval, delta_limit, split):
     """BASELINE config C4, reduced: tuple-encoded keys up to ~100 B whose 16-byte prefixes are
     shared by every key of a user (comparisons go to the tail bytes), wide Tuple.range() reads, and
     the window sliding with newOldest = now - window every batch (GC), against the skip-list
-    restatement; after a compaction with GC both hold the same boundary count."""
+    restatement; after a compaction with GC both hold the same boundary count.  split "1": the
+    split check (the base tier's long-key lookups on their own launch)."""
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     p = W.C4Params(txns=1500, users=3000, items=400, history=80_000, window=12_000, staleness=4_000)
     kb, ko, vers = W.c4_history(p, seed=4, start_version=100_000)
     e = EngineDriver(engine, gc_interval=gc_interval, delta_limit=delta_limit)
