@@ -59,6 +59,7 @@ def shape_of(batches, st: dict, history: int, dir_share: float = 1.0) -> dict:
         "X": st.get("intra_edges", 0) / max(1, b - st.get("intra_fallbacks", 0)),
         "merge_bytes": st.get("merge_bytes_all", 0) / b,
         "compact_bytes": st.get("compact_bytes_all", 0) / max(1, st.get("compactions", 0)),
+        "fc": st.get("compactions", 0) / b,  # share of batches that compact (their epilogue rebuilds the base)
         "dir_share": dir_share,
     }
 
@@ -85,10 +86,16 @@ def kernel_bytes(name: str, s: dict):
     if name.startswith("k_bucket_sort"):
         return 2 * I * E, "one read and one write of every 32-byte item"
     if name == "k_sort_partition":
-        return E * (D + I + 8) + nb * 16, "E keys read, E 32-byte items written to their bucket slabs, a counter word each"
+        # the slot and class-count atomics execute at the memory side (1 + 1/2 per endpoint): PMC
+        # counts ~32 bytes each beyond the item traffic (profiles/pmc_c2_*: 4.1 MB for 105k atomics)
+        return (E * (D + I) + 1.5 * E * 32 + nb * 16,
+                "E keys read, E 32-byte items written to their bucket slabs; 1.5 memory-side atomics per endpoint "
+                "(~32 bytes each)")
     if name.startswith("k_sort_bucket"):
-        return (E * (I + 4 + 4 + 12) + G * 4 + nb * 16,
-                "E slab items read; position, meta and 3 class prefixes written per endpoint; R+W begin lists")
+        # pos[p] is a scattered 4-byte store: one 64-byte line written per endpoint
+        return (E * (I + 64 + 4 + 12) + G * 4 + nb * 16,
+                "E slab items read; meta and 3 class prefixes written by position, pos[] by endpoint (a scattered "
+                "store: a 64-byte line each); R+W begin lists")
     if name.startswith("k_scan<3, fdbcs::PosScan"):
         return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
     if name.startswith("k_scan<3, fdbcs::EdgePairScan"):
@@ -129,8 +136,14 @@ def kernel_bytes(name: str, s: dict):
     if name.startswith("k_scan<2, fdbcs::GcScan"):
         return N * (2 * V + 8) + N * 32, "versions (own + predecessor) and lengths read, kept boundaries rewritten"
     if name == "k_epilogue":
-        n = Nd if Nd > 0 else N
-        return n * V + n / 8 * P * 2 + T * 2 + E * 2, "levels over the tier's versions, sampled keys, verdicts, scratch zeroing"
+        # the levels and sample index of the tier that changed: the delta after a merge, the whole
+        # base after a compaction (a share fc of the launches); per boundary its version, and per 8
+        # boundaries the 64-byte line holding the sampled key plus the skey8 entry written
+        fc = s.get("fc", 0.0)
+        n = (1 - fc) * Nd + fc * N if (Nd > 0 or fc > 0) else N
+        return (n * (V + 64 / 8 + P / 8) + T * 2 + R * 6,
+                "levels and sample index of the changed tier (the base on the compacting share of the launches): "
+                "versions, one key line and one skey8 entry per 8 boundaries; verdicts; re-zeroed flags and edge counts")
     if name == "k_directory":
         return 65537 * (4 + 17 * P), "65537 slots: binary search over level-0 samples"
     if name == "k_conflict_output":
