@@ -1473,12 +1473,17 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
         const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
         if (h < it.hi || (h == it.hi && l < it.lo)) lo = mid + 1; else hi = mid;
     }
+    // the splitters equal to my first two words, [lo, up): searched only when the first one not
+    // below me is equal (hot keys, shared prefixes), one LDS probe otherwise
     int up = lo;
-    hi = ns;
-    while (up < hi) {
-        const int mid = (up + hi) >> 1;
-        const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
-        if (h < it.hi || (h == it.hi && l <= it.lo)) up = mid + 1; else hi = mid;
+    if (lo < ns && s_spl[2 * lo] == it.hi && s_spl[2 * lo + 1] == it.lo) {
+        up = lo + 1;
+        hi = ns;
+        while (up < hi) {
+            const int mid = (up + hi) >> 1;
+            const uint64_t h = s_spl[2 * mid], l = s_spl[2 * mid + 1];
+            if (h < it.hi || (h == it.hi && l <= it.lo)) up = mid + 1; else hi = mid;
+        }
     }
     int bk = lo;
     if (up > lo) {  // ties on 16 bytes (hot keys, shared prefixes): the rest of the window
