@@ -2473,6 +2473,22 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         return;
     }
     const bool use_pre = !sc->edge_overflow && !w.no_prepass;
+    constexpr int kTPer = 8;  // transactions per thread held in registers (T <= 8 * kWG)
+    const bool in_regs = use_pre && T <= kTPer * (int)blockDim.x;
+    // Register rounds: each thread's transactions' resume pointers and the writer at each pointer,
+    // loaded here so that their two dependent loads overlap the status and member loads below
+    // (only a transaction the pre-pass left undecided has writers: ep < en)
+    int ep[kTPer], en[kTPer], cur[kTPer];
+    if (in_regs) {
+#pragma unroll
+        for (int k = 0; k < kTPer; k++) {
+            const int t = threadIdx.x + k * blockDim.x;
+            ep[k] = t < T ? w.pre_ep[t] : 0;
+            en[k] = t < T ? w.pre_end[t] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kTPer; k++) cur[k] = ep[k] < en[k] ? w.tedges[ep[k]] : -1;
+    }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         st[t] = use_pre ? w.pre_st[t] : ((w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided);
         w.first_conf[t] = INT_MAX;
@@ -2569,30 +2585,22 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         if (minLive[j] < t) return kUndecided;
         return kAborted;
     };
-    constexpr int kTPer = 8;  // transactions per thread held in registers (T <= 8 * kWG)
-    if (!sc->edge_overflow && use_pre && T <= kTPer * (int)blockDim.x) {
-        // Rounds with each thread's transactions' resume pointers in registers, and the first
-        // writer of every undecided transaction loaded together at the start of a round (the
-        // walk's further steps, skipping writers aborted since, are the rare case).
-        int ep[kTPer], en[kTPer];
-#pragma unroll
-        for (int k = 0; k < kTPer; k++) {
-            const int t = threadIdx.x + k * blockDim.x;
-            ep[k] = t < T ? w.pre_ep[t] : 0;
-            en[k] = t < T ? w.pre_end[t] : 0;
-        }
+    if (in_regs) {
+        // Rounds with each thread's transactions' resume pointers and current writers in
+        // registers: a round reads only LDS unless a walk steps past writers aborted since (the
+        // rare case), so the rounds run at LDS and barrier speed.
         volatile uint8_t* vst = st;
+        // "more" flags of alternate rounds: round r's is set during r and read after its closing
+        // barrier; the other one, read last after round r-1's closing barrier, is reset during r
+        // (past at least one barrier since that read), so a round needs two barriers, not three
+        __shared__ int s_more2[2];
+        if (threadIdx.x == 0) s_more2[0] = s_more2[1] = 0;
+        __syncthreads();
         for (;;) {
-            if (threadIdx.x == 0) s_more = 0;
             if (NW) group_minima(vst);
             __syncthreads();
+            if (threadIdx.x == 0) s_more2[(rounds + 1) & 1] = 0;
             int more = 0;
-            int e0[kTPer];
-#pragma unroll
-            for (int k = 0; k < kTPer; k++) {
-                const int t = threadIdx.x + k * blockDim.x;
-                e0[k] = t < T && vst[t] == kUndecided && ep[k] < en[k] ? w.tedges[ep[k]] : -1;
-            }
 #pragma unroll
             for (int k = 0; k < kTPer; k++) {
                 const int t = threadIdx.x + k * blockDim.x;
@@ -2600,7 +2608,7 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
                 int p = ep[k];
                 const int end = en[k];
                 uint8_t res = kUndecided;
-                int e = e0[k];
+                int e = cur[k];
                 while (p < end) {
                     const uint8_t sp = e >= T ? group_status(e, t) : vst[e];
                     if (sp == kAborted) {
@@ -2612,16 +2620,17 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
                 }
                 if (p == end) res = kCommitted;
                 ep[k] = p;
+                cur[k] = e;
                 if (res != kUndecided)
                     vst[t] = res;
                 else
                     more = 1;
             }
-            if (more) s_more = 1;
+            if (more) s_more2[rounds & 1] = 1;
             __syncthreads();
+            const int again = s_more2[rounds & 1];
             rounds++;
-            if (!s_more) break;
-            __syncthreads();
+            if (!again) break;
         }
     } else if (!sc->edge_overflow) {
         for (int t = threadIdx.x; t < T; t += blockDim.x)
