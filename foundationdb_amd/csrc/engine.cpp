@@ -174,6 +174,7 @@ struct fdbcs_conflict_set {
     int64_t hist_cap = 0;  // elements per buffer set
     int64_t n_ub = 0;      // upper bound of live base boundaries (exact after a wait)
     int64_t lvl3_n = 0;
+    int64_t lvl2_n = 0;
     // delta tier: the same layout, small
     DBuf dkey[2], dlt[2], dver[2];
     DBuf dlvl[2][kMaxLevels];  // per delta buffer: the next batch's check reads one while the epilogue builds the other
@@ -181,6 +182,7 @@ struct fdbcs_conflict_set {
     int64_t delta_cap = 0;
     int64_t nd_ub = 0;
     int64_t dlvl3_n = 0;
+    int64_t dlvl2_n = 0;
     DBuf cws[6];  // compaction arrays (per delta boundary)
     DBuf htail[2];  // tail arenas (bytes [16, len) of long keys): append-only between GCs; each GC
     int tcur = 0;   // repacks the live tails into the other one, reclaiming the rest
@@ -600,7 +602,7 @@ int sync_sizes(fdbcs_conflict_set* cs) {
 
 // Range-max hierarchy buffers (and the sampled key index in lv[0]) for `cap` elements; returns the
 // top level's length.
-int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n) {
+int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n, int64_t* l2_n) {
     lv[0].release();
     if (int rc = lv[0].ensure(index_bytes(cap))) return rc;
     int64_t m = cap;
@@ -608,6 +610,7 @@ int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n) {
         m = (m + kFan - 1) / kFan + 1;
         lv[L].release();
         if (int rc = lv[L].ensure(8 * m)) return rc;
+        if (L == 2) *l2_n = m;
     }
     *top_n = m;
     return FDBCS_OK;
@@ -655,12 +658,12 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
         w.c_exact = (uint8_t*)cs->cws[5].p;
     }
     for (int k = 0; k < 2; k++)
-        if ((rc = alloc_levels(cs->dlvl[k], cap, &cs->dlvl3_n))) return rc;
+        if ((rc = alloc_levels(cs->dlvl[k], cap, &cs->dlvl3_n, &cs->dlvl2_n))) return rc;
     cs->delta_cap = cap;
     cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;  // the current delta's levels are rebuilt, its directory not
     cs->prev_segs = false;                      // (sync_sizes drained every stream)
     launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->ndb[cs->dcur],
-                    cs->dlvl3_n, std::max<int64_t>(cs->nd_ub, 1));
+                    cs->dlvl3_n, cs->dlvl2_n, std::max<int64_t>(cs->nd_ub, 1));
     HIPOK(take_launch_error());
     HIPOK(hipStreamSynchronize(cs->stream));
     return ensure_scan_arena(cs);
@@ -676,11 +679,11 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
         int64_t cap = std::max<int64_t>(need, cs->hist_cap);
         cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
         if ((rc = grow_sets(cs, cs->hkey, cs->hlt, cs->hver, cs->cur, cs->n_ub, cap))) return rc;
-        if ((rc = alloc_levels(cs->lvl, cap, &cs->lvl3_n))) return rc;
+        if ((rc = alloc_levels(cs->lvl, cap, &cs->lvl3_n, &cs->lvl2_n))) return rc;
         if (cs->directory && (rc = cs->dir.ensure(4 * ((size_t)kDirSlots + 1)))) return rc;
         cs->hist_cap = cap;
         launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n,
-                        cs->lvl3_n, std::max<int64_t>(cs->n_ub, 1));
+                        cs->lvl3_n, cs->lvl2_n, std::max<int64_t>(cs->n_ub, 1));
         HIPOK(take_launch_error());
     }
     if (tail_need > cs->tail_cap) {
@@ -1305,7 +1308,7 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     s.tail_used = (int64_t)tail.size();
     HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
     launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n, cs->lvl3_n,
-                    std::max<int64_t>(n, 1));
+                    cs->lvl2_n, std::max<int64_t>(n, 1));
     HIPOK(take_launch_error());
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
@@ -2215,14 +2218,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // D.MergeWrite into the delta tier
     char* hd = (char*)sl->pin_out.dp;
     launch_merge(ys, bd, w, delta.h, delta.m, delta_of(cs, dnew), dlevels_of(cs, dnew), &sc->ndb[dsrc], htail, sc, now,
-                 cs->dlvl3_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
+                 cs->dlvl3_n, cs->dlvl2_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;
     const int64_t base_hint = cs->n_ub + nd_after + 1;
     if (compact) {
         launch_compact(ys, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
-                       cs->header_version, cs->lvl3_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
+                       cs->header_version, cs->lvl3_n, cs->lvl2_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
                        rec(kPhCompEnd, 1));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;

@@ -379,12 +379,13 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
 // nd_src: the source buffer's size; dstm: the destination's levels (top level reset for the epilogue).
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
-                  int64_t now, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end,
-                  bool long_keys = false);
+                  int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
+                  hipEvent_t copy_end, bool long_keys = false);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
-                    int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end);
+                    int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
+                    hipEvent_t copy_end);
 // removeBefore over the whole base (src -> dst); the live tails are repacked from arena tsrc into
 // the empty arena tdst (reclaiming the bytes of removed and overwritten boundaries).
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
@@ -400,9 +401,9 @@ void launch_conflict_output(hipStream_t s, const BatchDev& b, const Work& w, con
                             uint8_t* out);
 int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
-// Range-max levels of a tier whose size is *n (lvl[3] reset first).
+// Range-max levels of a tier whose size is *n (lvl[2] and lvl[3] reset first).
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
-                     int64_t grid_hint_n);
+                     int64_t lvl2_n, int64_t grid_hint_n);
 // Scalar roll-over, the device copy of the verdicts, scratch zeroing and the range-max levels of
 // the tier that changed (the base after a compaction, else the delta).  k_resolve already wrote the
 // verdict bytes into the host-mapped result; the epilogue publishes the scalars after them and

@@ -2867,24 +2867,6 @@ struct Epilogue {
     int64_t* nd_out;     // Scalars::ndb of the delta buffer the batch leaves current
 };
 
-// The scalars after the verdicts in the host-mapped result (word by word: a local Scalars copy
-// would live in scratch), with the workspace's batch statistics; resets the workspace counters.
-__device__ __forceinline__ void publish_scalars(const Scalars* sc, const Epilogue& ep) {
-    static_assert(sizeof(Scalars) % 8 == 0, "Scalars is copied in 8-byte words");
-    Scalars* out = (Scalars*)(ep.verdict_out + verdict_scalars_offset(ep.T));
-    const uint64_t* from = (const uint64_t*)sc;
-    uint64_t* to = (uint64_t*)out;
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(Scalars) / 8); i++) to[i] = from[i];
-    out->debug_error = ep.bsc->debug_error;
-    out->intra_rounds = ep.bsc->rounds;
-    out->intra_edges = ep.bsc->edge_overflow ? -1 : ep.bsc->n_edges;
-    out->sort_big = ep.bsc->sort_big;
-    out->n_segments = ep.bsc->n_segments;
-    ep.bsc->debug_error = 0;
-    ep.bsc->ovf_n = 0;     // the sort's overflow list and big-bucket count (this batch's sort is done)
-    ep.bsc->sort_big = 0;
-}
 // ------------------------------------------------------------------ D.MergeWrite
 //
 // mergeWriteConflictRanges (SkipList.cpp:899-924, 414-424): for each union segment [B, E):
@@ -2931,16 +2913,18 @@ constexpr int seg_threads(bool long_keys) { return 2 * seg_lanes(long_keys) * (k
 template <bool LONG>
 __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
                                                                 const uint8_t* htail, Scalars* sc, TierIO io,
-                                                                int64_t* lvl3, int64_t lvl3_n) {
+                                                                int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
+                                                                int64_t lvl2_n) {
     constexpr int LL = seg_lanes(LONG);
     __shared__ int64_t s_lo[kSegPer + 1];       // lo of the segment before the tile, then the tile's
     __shared__ uint32_t s_val[3][kSegPer + 1];  // removed, inserted, tail units per segment
     __shared__ uint32_t s_base[3];
     __shared__ int s_tile;
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the destination tier's top level, reset for the epilogue's atomicMax build (its previous
-    // contents belonged to the history two batches back, which no check reads any more)
+    // the destination tier's top two levels, reset for the epilogue's atomicMax build (their
+    // previous contents belonged to the history two batches back, which no check reads any more)
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = gt; i < lvl2_n; i += (int64_t)gridDim.x * blockDim.x) lvl2[i] = LLONG_MIN;
     if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanSegSum].counter, 1);
     __syncthreads();
     const int tile = s_tile;
@@ -3219,13 +3203,14 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
-                  int64_t now, int64_t lvl3_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end,
-                  bool long_keys) {
+                  int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
+                  hipEvent_t copy_end, bool long_keys) {
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
     fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_prep_tiles(b.W)),
-               dim3(seg_threads(long_keys)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n);
+               dim3(seg_threads(long_keys)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
+               dstm.lvl[2], lvl2_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
     ins.b = b;
@@ -3253,9 +3238,10 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
 __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels basem, Hist delta,
                                                            const uint8_t* htail, const int64_t* nb_ptr,
                                                            const int64_t* nd_ptr, int64_t hdr, Work w, int64_t* lvl3,
-                                                           int64_t lvl3_n) {
+                                                           int64_t lvl3_n, int64_t* lvl2, int64_t lvl2_n) {
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = gt; i < lvl2_n; i += (int64_t)gridDim.x * blockDim.x) lvl2[i] = LLONG_MIN;
     const int64_t j = gt / kArity;  // kArity lanes per delta boundary (cooperative search)
     const int64_t nd = *nd_ptr;
     if (j >= nd) return;  // whole groups leave together
@@ -3322,11 +3308,12 @@ struct CompactIns {
 
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
-                    int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin, hipEvent_t copy_end) {
+                    int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
+                    hipEvent_t copy_end) {
     int64_t blocks = (kArity * delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     fdb_launch(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
-                       &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n);
+                       &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
     const Segs g{w.c_lo, w.c_hi, w.c_rem, w.c_ins, w.tile_first};
     const TierIO io{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem};
     launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
@@ -3659,27 +3646,47 @@ void launch_route(hipStream_t s, const RouteArgs& a, ScanState st) {
 
 // ------------------------------------------------------------------ range-max hierarchy + epilogue
 //
-// One workgroup per 4096 boundaries: each wave reduces 16 blocks of 64 versions to level 1, wave 0
-// reduces the 64 level-1 values to level 2, and level 3 is built by atomicMax (reset beforehand).
-// With a batch attached the same launch writes the device copy of the verdicts (k_resolve already
-// wrote the host-mapped bytes), publishes the scalars after them and then the completion flag, and
-// zeroes the scratch the next batch on the workspace expects zeroed.
+// Each wave reduces kEpiBlocks blocks of 64 versions to level 1 on its own (no barrier, no LDS);
+// levels 2 and 3 are built by atomicMax (both reset beforehand).  With a batch attached the same
+// launch writes the device copy of the verdicts (k_resolve already wrote the host-mapped bytes),
+// publishes the scalars after them and then the completion flag, and zeroes the scratch the next
+// batch on the workspace expects zeroed.
 
-
-
-// Range-max levels over lvl[0][0, n0) (lvl[3] reset beforehand); with a batch attached, also the
-// verdicts and the scalar roll-over.  n0 comes from `n_levels` or, for a batch, from the tier
-// that changed.
-// kEpiWaves waves per workgroup of 4096 boundaries, kFan / kEpiWaves level-1 blocks per wave: the
-// loads of a block's 64 versions are one wave instruction.  16 waves per workgroup (4 blocks each)
-// measured slower than 4 (C2, same box: 22.6 vs 18.6 us per launch).
+// Range-max levels over lvl[0][0, n0) (lvl[2] and lvl[3] reset beforehand); with a batch attached,
+// also the verdicts and the scalar roll-over.  n0 comes from `n_levels` or, for a batch, from the
+// tier that changed.
+// Round 3 gave each workgroup 4096 boundaries, its waves 16 blocks each and wave 0 the level-2
+// reduce behind a barrier: at C2 (~150k delta boundaries) ~40 workgroups, each wave issuing ~40
+// dependent-free loads one after another, 10 us for the levels (device trace).  Here a wave owns 4
+// blocks, so the same tier spreads over 4x the waves, and level 2 takes one atomic per wave (16 per
+// word).  (16 waves per 4096-boundary workgroup with the barrier: slower, 22.6 vs 18.6 us per
+// launch at C2 on one box.)
 constexpr int kEpiWaves = 4;
 constexpr int kEpiThreads = 64 * kEpiWaves;
-constexpr int kEpiBlocks = kFan / kEpiWaves;  // level-1 blocks per wave
+constexpr int kEpiBlocks = 4;  // level-1 blocks (64 boundaries each) per wave
+constexpr int64_t kEpiSpan = (int64_t)kEpiWaves * kEpiBlocks * kFan;  // boundaries per workgroup step
+static_assert(kFan % kEpiBlocks == 0, "a wave's blocks share one level-2 entry");
+
+// Words of Scalars / BatchScalars, prefetched by the publishing wave at the start of the launch.
+constexpr int kScWords = (int)(sizeof(Scalars) / 8);
+constexpr int kBscWords = (int)(sizeof(BatchScalars) / 8);
+static_assert(sizeof(Scalars) % 8 == 0 && sizeof(BatchScalars) % 8 == 0, "scalars move in 8-byte words");
+static_assert(kScWords <= 32 && kBscWords <= 32, "one lane per word, Scalars in lanes 0-31, BatchScalars in 32-63");
+constexpr int sc_word(size_t off) { return (int)(off / 8); }
 
 __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* sc, const int64_t* n_levels, Epilogue ep) {
-    __shared__ int64_t l1[kFan];
     if (threadIdx.x == 0) trace_min(ep.trace, kTrEpiBegin);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // the publishing wave loads the scalars it will publish now, while the levels are built: this
+    // launch is the only writer of them until it publishes (every kernel that sets them ran
+    // earlier on this stream)
+    uint64_t pre = 0;
+    if (ep.verdict_out && blockIdx.x == 0 && wid == 0) {
+        if (lane < kScWords)
+            pre = reinterpret_cast<const uint64_t*>(sc)[lane];
+        else if (lane >= 32 && lane < 32 + kBscWords)
+            pre = reinterpret_cast<const uint64_t*>(ep.bsc)[lane - 32];
+    }
     int64_t n0;
     if (n_levels)
         n0 = *n_levels;
@@ -3687,11 +3694,10 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         n0 = ep.gc_ran ? sc->n_gc : sc->n_next;
     else
         n0 = sc->nd_next;
-    const int64_t n1 = (n0 + kFan - 1) / kFan, n2 = (n1 + kFan - 1) / kFan;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t b2 = blockIdx.x; b2 < n2; b2 += gridDim.x) {
-        // each wave reduces kEpiBlocks blocks of 64 versions: all loads first, then the reductions
-        const int64_t b1_0 = b2 * kFan + wid * kEpiBlocks;
+    const int64_t n1 = (n0 + kFan - 1) / kFan, nwv = (n1 + kEpiBlocks - 1) / kEpiBlocks;
+    for (int64_t wv = (int64_t)blockIdx.x * kEpiWaves + wid; wv < nwv; wv += (int64_t)gridDim.x * kEpiWaves) {
+        // the wave's kEpiBlocks blocks of 64 versions: all loads first, then the reductions
+        const int64_t b1_0 = wv * kEpiBlocks;
         int64_t v[kEpiBlocks];
 #pragma unroll
         for (int q = 0; q < kEpiBlocks; q++) {
@@ -3706,10 +3712,10 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             if (m.edir_epoch && b1l > 0) prev_hi = m.keys[(b1l - 1) * kFan].x;
         }
         // every 8th boundary of the wave's blocks (8 entries of skey8 per block)
-#pragma unroll
-        for (int h8 = 0; h8 < (kEpiBlocks * kFan / 8 + 63) / 64; h8++) {
-            const int64_t e8 = b1_0 * (kFan / 8) + h8 * 64 + lane;
-            if (h8 * 64 + lane < kEpiBlocks * kFan / 8 && e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
+        static_assert(kEpiBlocks * kFan / 8 <= 64, "one skey8 entry per lane");
+        {
+            const int64_t e8 = b1_0 * (kFan / 8) + lane;
+            if (lane < kEpiBlocks * kFan / 8 && e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
         }
         int64_t mine = LLONG_MIN;
 #pragma unroll
@@ -3722,45 +3728,43 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             }
             if (lane == q) mine = x;
         }
-        if (lane < kEpiBlocks) {
-            if (b1l < n1) {
-                m.lvl[1][b1l] = mine;
-                m.skey[0][b1l] = sk;
-                // search-tree levels above: block b1l is entry b1l / A^L of level L when divisible
-                // (arithmetic level offsets: a dynamic index into skey[] would spill the argument)
-                int64_t d = b1l, off = 0;
-                for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
-                    off += idx_level_cap(m.idx_cap, L - 1);
-                    d /= kArity;
-                    m.skey[0][off + d] = sk;
-                }
-                if (m.edir_epoch) {
-                    // delta directory: slots (top16(previous sample), top16(this sample)] hold this
-                    // sample's index (the first sample not below them); the last sample also fills
-                    // the slots above it with n1.  At most kDirRun slots per run: slots left over keep
-                    // an older epoch and send their lookups down the tree.
-                    const uint64_t tag = (uint64_t)m.edir_epoch << 32;
-                    const int64_t a = b1l > 0 ? (int64_t)(prev_hi >> 48) : -1, c = (int64_t)(sk.x >> 48);
-                    for (int64_t v = a + 1; v <= c && v <= a + kDirRun; v++) m.edir[v] = tag | (uint64_t)b1l;
-                    if (b1l == n1 - 1)
-                        for (int64_t v = c + 1; v <= kDirSlots && v <= c + kDirRun; v++) m.edir[v] = tag | (uint64_t)n1;
-                }
+        if (lane < kEpiBlocks && b1l < n1) {
+            m.lvl[1][b1l] = mine;
+            m.skey[0][b1l] = sk;
+            // search-tree levels above: block b1l is entry b1l / A^L of level L when divisible
+            // (arithmetic level offsets: a dynamic index into skey[] would spill the argument)
+            int64_t d = b1l, off = 0;
+            for (int L = 1; L < kIdxLevels && d % kArity == 0; L++) {
+                off += idx_level_cap(m.idx_cap, L - 1);
+                d /= kArity;
+                m.skey[0][off + d] = sk;
             }
-            l1[wid * kEpiBlocks + lane] = mine;
-        }
-        __syncthreads();
-        if (wid == 0) {
-            int64_t v = l1[lane];
-            for (int o = 32; o > 0; o >>= 1) {
-                const int64_t y = __shfl_xor(v, o, 64);
-                v = y > v ? y : v;
-            }
-            if (lane == 0) {
-                m.lvl[2][b2] = v;
-                atomicMax((long long*)&m.lvl[3][b2 / kFan], (long long)v);
+            if (m.edir_epoch) {
+                // delta directory: slots (top16(previous sample), top16(this sample)] hold this
+                // sample's index (the first sample not below them); the last sample also fills
+                // the slots above it with n1.  At most kDirRun slots per run: slots left over keep
+                // an older epoch and send their lookups down the tree.
+                const uint64_t tag = (uint64_t)m.edir_epoch << 32;
+                const int64_t a = b1l > 0 ? (int64_t)(prev_hi >> 48) : -1, c = (int64_t)(sk.x >> 48);
+                for (int64_t v = a + 1; v <= c && v <= a + kDirRun; v++) m.edir[v] = tag | (uint64_t)b1l;
+                if (b1l == n1 - 1)
+                    for (int64_t v = c + 1; v <= kDirSlots && v <= c + kDirRun; v++) m.edir[v] = tag | (uint64_t)n1;
             }
         }
-        __syncthreads();
+        // the wave's maximum into levels 2 and 3; level 3 only when above what it already holds
+        // (up to 1024 waves share a level-3 word, and one word takes ~90 atomics per us)
+        int64_t x = lane < kEpiBlocks ? mine : LLONG_MIN;
+#pragma unroll
+        for (int o = 1; o < kEpiBlocks; o <<= 1) {
+            const int64_t y = __shfl_xor(x, o, 64);
+            x = y > x ? y : x;
+        }
+        if (lane == 0 && b1_0 < n1) {
+            atomicMax((long long*)&m.lvl[2][b1_0 / kFan], (long long)x);
+            int64_t* l3 = &m.lvl[3][b1_0 / ((int64_t)kFan * kFan)];
+            if (x > __hip_atomic_load(l3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                atomicMax((long long*)l3, (long long)x);
+        }
     }
     if (!ep.verdict_out) return;
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiLevels);
@@ -3786,17 +3790,48 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
     if (blockIdx.x != 0) return;
     // Workgroup 0 writes the scalars the host reads next to the verdicts (which k_resolve already
     // wrote to the host-mapped buffer), then publishes the batch's sequence number; everything
-    // else this launch writes is read only by later kernels on the same stream.
-    if (threadIdx.x == 0) {
-        if (ep.compacted) {
-            sc->n = ep.gc_ran ? sc->n_gc : sc->n_next;
-            sc->nd = 0;
-        } else {
-            sc->nd = sc->nd_next;
+    // else this launch writes is read only by later kernels on the same stream.  Wave 0 holds the
+    // prefetched words (lane i: Scalars word i, lane 32 + i: BatchScalars word i) and writes the
+    // host copy one word per lane, with the roll-over applied.
+    if (wid == 0) {
+        auto scw = [&](size_t off) -> int64_t { return (int64_t)__shfl(pre, sc_word(off), 64); };
+        auto bsw = [&](size_t off) -> uint64_t { return __shfl(pre, 32 + sc_word(off), 64); };
+        auto bs32 = [&](size_t off) -> uint32_t { return (uint32_t)(bsw(off) >> (8 * (off % 8))); };
+        const int64_t n_new = !ep.compacted ? scw(offsetof(Scalars, n))
+                                            : (ep.gc_ran ? scw(offsetof(Scalars, n_gc)) : scw(offsetof(Scalars, n_next)));
+        const int64_t nd_new = ep.compacted ? 0 : scw(offsetof(Scalars, nd_next));
+        const int64_t tail_new = ep.gc_ran ? scw(offsetof(Scalars, tail_gc)) : scw(offsetof(Scalars, tail_next));
+        const int64_t edges = bs32(offsetof(BatchScalars, edge_overflow)) ? -1 : (int64_t)bsw(offsetof(BatchScalars, n_edges));
+        const uint32_t dbg = bs32(offsetof(BatchScalars, debug_error)), rounds = bs32(offsetof(BatchScalars, rounds));
+        const uint32_t big = bs32(offsetof(BatchScalars, sort_big));
+        const int64_t nseg = (int64_t)bsw(offsetof(BatchScalars, n_segments));
+        // the delta buffer the batch leaves current: one of Scalars::ndb
+        const int64_t nd_slot = ep.nd_out ? ep.nd_out - sc->ndb : -1;
+        static_assert(offsetof(Scalars, debug_error) % 8 == 0 &&
+                          offsetof(Scalars, intra_rounds) == offsetof(Scalars, debug_error) + 4 &&
+                          offsetof(Scalars, sort_big) % 8 == 0 && offsetof(Scalars, intra_edges) % 8 == 0,
+                      "Scalars word packing the host copy assumes");
+        if (lane < kScWords) {
+            uint64_t x = pre;
+            if (lane == sc_word(offsetof(Scalars, n))) x = (uint64_t)n_new;
+            if (lane == sc_word(offsetof(Scalars, nd))) x = (uint64_t)nd_new;
+            if (lane == sc_word(offsetof(Scalars, tail_used))) x = (uint64_t)tail_new;
+            if (nd_slot >= 0 && nd_slot < 2 && lane == sc_word(offsetof(Scalars, ndb)) + nd_slot) x = (uint64_t)nd_new;
+            if (lane == sc_word(offsetof(Scalars, debug_error))) x = (uint64_t)dbg | (uint64_t)rounds << 32;
+            if (lane == sc_word(offsetof(Scalars, intra_edges))) x = (uint64_t)edges;
+            if (lane == sc_word(offsetof(Scalars, sort_big))) x = (x & ~0xffffffffull) | big;
+            if (lane == sc_word(offsetof(Scalars, n_segments))) x = (uint64_t)nseg;
+            reinterpret_cast<uint64_t*>(ep.verdict_out + verdict_scalars_offset(ep.T))[lane] = x;
         }
-        if (ep.nd_out) *ep.nd_out = sc->nd;
-        sc->tail_used = ep.gc_ran ? sc->tail_gc : sc->tail_next;
-        publish_scalars(sc, ep);
+        if (lane == 0) {
+            sc->n = n_new;
+            sc->nd = nd_new;
+            if (ep.nd_out) *ep.nd_out = nd_new;
+            sc->tail_used = tail_new;
+            ep.bsc->debug_error = 0;
+            ep.bsc->ovf_n = 0;  // the sort's overflow list and big-bucket count (this batch's sort is done)
+            ep.bsc->sort_big = 0;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiHost);
@@ -3859,12 +3894,13 @@ void launch_hold(hipStream_t s, const uint32_t* release) {
     fdb_launch(k_hold, dim3(1), dim3(64), 0, s, (const volatile uint32_t*)release);
 }
 
-__global__ void k_lvl3_reset(int64_t* lvl3, int64_t n) {
+__global__ void k_lvl3_reset(int64_t* lvl3, int64_t n, int64_t* lvl2, int64_t n2) {
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) lvl2[i] = LLONG_MIN;
 }
 
 static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
-    int64_t g = (hint_n + (int64_t)kFan * kFan - 1) / ((int64_t)kFan * kFan);
+    int64_t g = (hint_n + kEpiSpan - 1) / kEpiSpan;
     const int64_t ge = (extra + kEpiThreads - 1) / kEpiThreads;
     g = g > ge ? g : ge;
     g = g < 1 ? 1 : g;
@@ -3899,9 +3935,9 @@ static void launch_directory(hipStream_t s, const MaxLevels& m, const int64_t* n
 }
 
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
-                     int64_t grid_hint_n) {
+                     int64_t lvl2_n, int64_t grid_hint_n) {
     launch_directory(s, m, n);
-    fdb_launch(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n);
+    fdb_launch(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n, m.lvl[2], lvl2_n);
     Epilogue ep{};
     ep.trace = nullptr;
     fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kEpiThreads), 0, s, m, sc, n, ep);
