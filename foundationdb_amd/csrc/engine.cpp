@@ -247,12 +247,17 @@ struct fdbcs_conflict_set {
     // cross-stream waits and records included as event wait / record nodes, so the stream
     // layout and every dependency stay those of direct mode at three graph launches per batch.
     int stage_graphs = 0;  // 1: runs between sync points (FDBCS_GRAPH=2); 2: whole lists (=3)
+    int graph_ring = 16;   // FDBCS_GRAPH_RING: executable copies per stage shape
     struct StageGraph {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
         std::vector<hipGraphNode_t> nodes;
     };
     std::vector<std::pair<uint64_t, StageGraph>> stage_cache;
+    // Each stage shape has kGraphRing executable copies used in turn, so a copy is updated only
+    // after the batches in flight have moved past its last launch (an exec updated while its
+    // previous launch is still queued is what the runtime has to wait out).
+    std::vector<std::pair<uint64_t, uint32_t>> stage_turn;
     // FDBCS_SUBMIT_THREAD=1: two submitting threads.  A helper thread issues stage A of batch i
     // (and its base-tier check) while the calling thread issues stage B of batch i-1, which waited
     // (as in graph mode) for this call: kernel launches on two streams from two threads take about
@@ -891,6 +896,16 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
         key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u + r.kind)) *
               1099511628211ull;
     }
+    {  // this launch's copy of the shape
+        uint32_t* turn = nullptr;
+        for (auto& kv : cs->stage_turn)
+            if (kv.first == key) turn = &kv.second;
+        if (!turn) {
+            cs->stage_turn.push_back({key, 0u});
+            turn = &cs->stage_turn.back().second;
+        }
+        key = key * 1099511628211ull + (*turn)++ % (uint32_t)cs->graph_ring;
+    }
     fdbcs_conflict_set::StageGraph* sg = nullptr;
     for (auto& kv : cs->stage_cache)
         if (kv.first == key) sg = &kv.second;
@@ -1084,6 +1099,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
     if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2' ? 1 : (v[0] == '3' ? 2 : 0);
+    if (const char* v = getenv("FDBCS_GRAPH_RING")) cs->graph_ring = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
@@ -2583,7 +2599,7 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
 }
 
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch) {
-    if (!b || !us_per_launch || reps <= 0 || which < 0 || which > 2) return FDBCS_E_INVALID;
+    if (!b || !us_per_launch || reps <= 0 || which < 0 || which > 4) return FDBCS_E_INVALID;
     if (!b->cs) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
     HIPOK(hipSetDevice(cs->device));
@@ -2598,7 +2614,7 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     Scalars* sc = (Scalars*)cs->scal.p;
     const Tier base{hist_of(cs, cs->cur), levels_of(cs, cs->cur), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->ndb[cs->dcur], kHole};
-    if (which >= 1) {  // the sort kernels
+    if (which == 1 || which == 2) {  // the sort kernels
         if (!cs->quant_valid) return FDBCS_E_STATE;  // warm splitters only: detect a batch first
         HIPOK(debug_time_sort(cs->stream, b->bd, w, (SplitKey*)cs->quant.p + cs->qcur * kQuant, cs->bucket_target,
                               b->max_len > (int32_t)kSortNxLen, which, reps, us_per_launch));
@@ -2608,10 +2624,19 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));
     const int cv = cs->check_version == 7 && b->max_len > 24 ? 6 : cs->check_version;
-    launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cv);
+    // 0: the whole check; 3 / 4: the split check's base / delta tier launch alone
+    auto one = [&]() {
+        uint8_t* ht = (uint8_t*)cs->htail[cs->tcur].p;
+        if (which == 0)
+            launch_check(cs->stream, b->bd, w, base, delta, ht, cv);
+        else
+            launch_check_tier(cs->stream, b->bd, w, which == 3 ? base : delta, which == 3, ht,
+                              cs->long_probe && b->max_len > 24, !cs->group_rmax, PrevSegs{},
+                              cs->check_version == 7 && b->max_len <= 24);
+    };
+    one();
     HIPOK(hipEventRecord(e0, cs->stream));
-    for (int i = 0; i < reps; i++)
-        launch_check(cs->stream, b->bd, w, base, delta, (uint8_t*)cs->htail[cs->tcur].p, cv);
+    for (int i = 0; i < reps; i++) one();
     HIPOK(hipEventRecord(e1, cs->stream));
     HIPOK(hipEventSynchronize(e1));
     *us_per_launch = ev_ms(e0, e1) * 1000.0 / reps;

@@ -256,7 +256,8 @@ int fdbcs_batch_routed_info(fdbcs_batch* b, int32_t* n_txn, int32_t* n_reads, in
 /* Diagnostics (tuning, not part of the ConflictSet contract): average device time of one launch
  * of a pipeline kernel over `reps` back-to-back launches on the uploaded batch `b` against the
  * current history, with no batch in flight.  which: 0 = the read check (D.CheckRead); 1-2 = the
- * endpoint sort's kernels (partition, per-bucket sort; splitters of the last batch detected). */
+ * endpoint sort's kernels (partition, per-bucket sort; splitters of the last batch detected); 3-4 =
+ * the split check's base / delta tier launch alone. */
 int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_launch);
 /* Per-kernel device time accumulated since fdbcs_reset_stats: timing level 3 brackets every kernel
  * of every batch with events, level 1 the kernel named by fdbcs_set_timed_kernel on the sampled
