@@ -215,9 +215,11 @@ struct fdbcs_conflict_set {
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
-    int check_version = 7;    // FDBCS_CHECK: read-check kernel (7: one lane per lookup, for batches of keys
-                              // up to 24 bytes; 6: kArity lanes per lookup, the base and delta lookups in
-                              // separate waves, 1: kArity lanes per lookup, the four of a read in one wave)
+    int check_version = 7;    // FDBCS_CHECK: read-check kernel (7: one lane per lookup; 6: kArity lanes per
+                              // lookup, the base and delta lookups in separate waves, 1: kArity lanes per
+                              // lookup, the four of a read in one wave)
+    int long_lanes = 1;       // FDBCS_LONG_LANES=0: batches of keys over 24 bytes take the kArity-lane
+                              // lookups (6) under FDBCS_CHECK=7 (round 3's layout, for A/B)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
     bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
@@ -1107,6 +1109,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
+    if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));
@@ -2098,8 +2101,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ties on the prefix with k only, and the length decides)
     const bool long_keys = cs->long_probe && b->max_len > 24;
     // one lane per lookup unless tails run past a word (then the cooperative long-key probes)
-    const bool lanes = cs->check_version == 7 && b->max_len <= 24;
-    const int check_version = cs->check_version == 7 && !lanes ? 6 : cs->check_version;
+    const bool lanes = cs->check_version == 7 && (b->max_len <= 24 || cs->long_lanes);
+    const int check_version = cs->check_version == 7 && !lanes ? 6 : (lanes && long_keys ? 8 : cs->check_version);
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     // Stage B in two halves (fdbcs_conflict_set::ystream): X = check, resolution, D.Combine on
@@ -2623,7 +2626,9 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     hipEvent_t e0, e1;
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));
-    const int cv = cs->check_version == 7 && b->max_len > 24 ? 6 : cs->check_version;
+    const bool dl = cs->check_version == 7 && (b->max_len <= 24 || cs->long_lanes);
+    const bool dlong = cs->long_probe && b->max_len > 24;
+    const int cv = cs->check_version == 7 && !dl ? 6 : (dl && dlong ? 8 : cs->check_version);
     // 0: the whole check; 3 / 4: the split check's base / delta tier launch alone
     auto one = [&]() {
         uint8_t* ht = (uint8_t*)cs->htail[cs->tcur].p;
@@ -2631,8 +2636,7 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
             launch_check(cs->stream, b->bd, w, base, delta, ht, cv);
         else
             launch_check_tier(cs->stream, b->bd, w, which == 3 ? base : delta, which == 3, ht,
-                              cs->long_probe && b->max_len > 24, !cs->group_rmax, PrevSegs{},
-                              cs->check_version == 7 && b->max_len <= 24);
+                              dlong, !cs->group_rmax, PrevSegs{}, dl);
     };
     one();
     HIPOK(hipEventRecord(e0, cs->stream));

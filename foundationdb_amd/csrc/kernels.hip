@@ -840,16 +840,12 @@ __device__ __forceinline__ int lane_count(const ulonglong2* a, int64_t base, int
     return c;
 }
 
-// std::lower_bound of q over the n boundaries of a tier by one lane (the result and eq as
-// group_lower_bound's): the radix directory slot (at most kLaneProbe level-0 samples) or the
-// kArity-ary sample tree down to one 64-boundary block, then the block's eight group starts
-// (skey8) and the seven boundaries after the last start below q; prefix ties compare lengths and
-// tails against the boundary itself (probe_cmp_lean).  A run of boundaries sharing q's 16-byte
-// prefix over more than one block (tuple subspaces) falls back to a binary search.
-__device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
-                                                    const uint8_t* htail, const uint8_t* qtail, bool& eq) {
-    eq = false;
-    if (n <= 0) return 0;
+// The level-0 samples of a tier below q's 16-byte prefix (c) and the end of the run of samples
+// sharing that prefix (b >= c), by one lane: the radix directory slot (at most kLaneProbe level-0
+// samples) or the kArity-ary sample tree, each node's entries loaded by the lane as independent
+// 16-byte loads.  Boundary 64(c-1) lies below q and boundary 64b (if any) above it.
+__device__ __forceinline__ void lane_sample_range(const MaxLevels& m, int64_t n, const DKey& q, int64_t& c_out,
+                                                  int64_t& b_out) {
     int64_t sz[kIdxLevels];
     sz[0] = (n + kFan - 1) / kFan;
 #pragma unroll
@@ -909,6 +905,21 @@ __device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLeve
         if (k.x != q.hi || k.y != q.lo) break;
         b++;
     }
+    c_out = c;
+    b_out = b;
+}
+
+// std::lower_bound of q over the n boundaries of a tier by one lane (the result and eq as
+// group_lower_bound's): lane_sample_range down to one 64-boundary block, then the block's eight
+// group starts (skey8) and the seven boundaries after the last start below q; prefix ties compare
+// lengths and tails against the boundary itself (probe_cmp_lean).  A run of boundaries sharing q's
+// 16-byte prefix over more than one block (tuple subspaces) falls back to a binary search.
+__device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
+                                                    const uint8_t* htail, const uint8_t* qtail, bool& eq) {
+    eq = false;
+    if (n <= 0) return 0;
+    int64_t c, b;
+    lane_sample_range(m, n, q, c, b);
     const int64_t hi = min(n, kFan * b);
     if (b == c) {
         // boundary 64(c-1) < q < boundary 64c: one 64-boundary block; its group starts, then the
@@ -979,6 +990,187 @@ __device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLeve
     return lo;
 }
 
+// ---- per-lane lookups of long keys (batches with keys over 24 bytes: C4 tuple keys)
+//
+// Keys of one tuple subspace / user share their 16-byte prefix, so a lookup that reaches their run
+// compares tails.  One lane per lookup, in three steps: lane_sample_range; the run [s, e) of
+// boundaries sharing q's prefix, by prefix-only counts (the group starts of skey8, then the seven
+// boundaries after a start: no tails); inside the run a (kRunProbes + 1)-ary search by full
+// compares, whose probes' (len, tail offset) and then tails are loaded together against the query
+// tail held in registers (QTail): two dependent loads per round.  Keys between two probes share
+// with q at least the tail words both probes share with it, so later rounds load and compare only
+// the words from there on (C4: the item bytes after a user's ~20-85 shared bytes).
+[[maybe_unused]] constexpr int kRunProbes = 3;
+
+// Boundaries of [lo1, hi) whose prefix is below q's, counted among the n <= N from `base` (sorted).
+template <int N>
+__device__ __forceinline__ int lane_count_below(const ulonglong2* a, int64_t base, int n, const DKey& q, bool not_above) {
+    ulonglong2 k[N];
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (i < n) k[i] = a[base + i];
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (i < n) c += (not_above ? !(q.hi < k[i].x || (q.hi == k[i].x && q.lo < k[i].y)) : prefix_less(k[i], q)) ? 1 : 0;
+    return c;
+}
+
+// The run of boundaries of [lo1, hi) sharing q's 16-byte prefix: s = the first whose prefix is not
+// below q's, e = the first whose prefix is above it (hi if none).  Boundaries before lo1 lie below
+// q's prefix, hi and after it above.
+__device__ __forceinline__ void lane_prefix_run(const Hist& h, const MaxLevels& m, int64_t lo1, int64_t hi,
+                                                const DKey& q, int64_t& s, int64_t& e) {
+    const int64_t G0 = (lo1 + 7) / 8;                           // group starts 8g in [lo1, hi)
+    const int64_t NG = hi > 8 * G0 ? (hi - 1) / 8 - G0 + 1 : 0;
+    if (NG > kLaneProbe) {  // a run over several blocks (a hot subspace): binary searches on prefixes
+        int64_t lo = lo1, hh = hi;
+        while (lo < hh) {
+            const int64_t mid = (lo + hh) >> 1;
+            if (prefix_less(h.key[mid], q)) lo = mid + 1; else hh = mid;
+        }
+        s = lo;
+        hh = hi;
+        while (lo < hh) {
+            const int64_t mid = (lo + hh) >> 1;
+            const ulonglong2 k = h.key[mid];
+            if (!(q.hi < k.x || (q.hi == k.x && q.lo < k.y))) lo = mid + 1; else hh = mid;
+        }
+        e = lo;
+        return;
+    }
+    ulonglong2 g[kLaneProbe];
+#pragma unroll
+    for (int i = 0; i < kLaneProbe; i++)
+        if (i < NG) g[i] = m.skey8[G0 + i];
+    int kl = 0, kle = 0;
+#pragma unroll
+    for (int i = 0; i < kLaneProbe; i++) {
+        if (i < NG) {
+            kl += prefix_less(g[i], q) ? 1 : 0;
+            kle += (q.hi < g[i].x || (q.hi == g[i].x && q.lo < g[i].y)) ? 0 : 1;
+        }
+    }
+    // s lies in [as, bs], e in [ae, be]: at most seven boundaries after a group start each
+    const int64_t as = kl > 0 ? 8 * (G0 + kl - 1) + 1 : lo1, bs = kl < NG ? 8 * (G0 + kl) : hi;
+    const int64_t ae = kle > 0 ? 8 * (G0 + kle - 1) + 1 : lo1, be = kle < NG ? 8 * (G0 + kle) : hi;
+    ulonglong2 ks[7], ke[7];
+    const int ns = (int)(bs - as), ne = (int)(be - ae);
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        if (i < ns) ks[i] = h.key[as + i];
+        if (i < ne) ke[i] = h.key[ae + i];
+    }
+    int cs = 0, ce = 0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        if (i < ns) cs += prefix_less(ks[i], q) ? 1 : 0;
+        if (i < ne) ce += (q.hi < ke[i].x || (q.hi == ke[i].x && q.lo < ke[i].y)) ? 0 : 1;
+    }
+    s = as + cs;
+    e = ae + ce;
+}
+
+// lane_lower_bound for long keys (same result and eq); qt: q's tail words (load_qtail).
+__device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
+                                                         const QTail& qt, const uint8_t* htail, const uint8_t* qtail,
+                                                         bool& eq) {
+    eq = false;
+    if (n <= 0) return 0;
+    int64_t c, b;
+    lane_sample_range(m, n, q, c, b);
+    int64_t lo, hh;
+    lane_prefix_run(h, m, c > 0 ? kFan * (c - 1) + 1 : 0, min(n, kFan * b), q, lo, hh);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // [lo, hh): boundaries sharing q's prefix, lower_bound among them by full compares.  dlo / dhi:
+    // tail words known equal to q's in the boundaries just below lo and at hh (none at first: their
+    // prefixes differ from q's).
+    int dlo = 0, dhi = 0;
+    bool eq_hh = false;  // the boundary at hh equals q (hh was set by a probe)
+    const bool qlong = q.len > 16u;
+    while (lo < hh) {
+        const int64_t span = hh - lo;
+        const int w0 = dlo < dhi ? dlo : dhi;  // tail words every boundary in [lo, hh) shares with q
+        int64_t p[kRunProbes];
+        bool v[kRunProbes];
+        uint2 lt[kRunProbes];
+#pragma unroll
+        for (int j = 0; j < kRunProbes; j++) {
+            p[j] = lo + (span * (j + 1)) / (kRunProbes + 1);
+            v[j] = p[j] < hh && (j == 0 || p[j] != p[j - 1]);
+            if (v[j]) lt[j] = h.lt[p[j]];
+        }
+        uint64_t x[kRunProbes][kQW];
+        uint32_t nb[kRunProbes];
+#pragma unroll
+        for (int j = 0; j < kRunProbes; j++) {
+            nb[j] = v[j] && qlong && lt[j].x > 16u ? (lt[j].x < q.len ? lt[j].x : q.len) - 16u : 0u;
+            const uint64_t* ha = (const uint64_t*)hist_tail(htail, v[j] ? lt[j].y : 0u);
+            const int nw = (int)((nb[j] + 7u) / 8u);
+#pragma unroll
+            for (int u = 0; u < kQW; u++)
+                if (u >= w0 && u < nw) x[j][u] = ha[u];
+        }
+        int r[kRunProbes], d[kRunProbes];
+#pragma unroll
+        for (int j = 0; j < kRunProbes; j++) {
+            r[j] = 1;
+            d[j] = 0;
+            if (!v[j]) continue;
+            const int nw = (int)((nb[j] + 7u) / 8u);
+            bool found = false;
+#pragma unroll
+            for (int u = 0; u < kQW; u++) {
+                if (!found && u >= w0 && u < nw) {
+                    const int vb = (int)nb[j] - 8 * u;
+                    const uint64_t msk = vb >= 8 ? ~0ull : ~0ull << (64 - 8 * vb);
+                    const uint64_t hx = __builtin_bswap64(x[j][u]) & msk, qy = qt.w[u] & msk;
+                    if (hx != qy) {
+                        r[j] = hx < qy ? -1 : 1;
+                        d[j] = u;
+                        found = true;
+                    }
+                }
+            }
+            if (!found) {
+                if (nw > kQW) {  // both tails run past the registers: the rest from memory
+                    r[j] = tail_cmp(hist_tail(htail, lt[j].y) + 8 * kQW, lt[j].x - 8 * kQW, qtail + q.tail + 8 * kQW,
+                                    q.len - 8 * kQW);
+                    d[j] = kQW;
+                } else {
+                    r[j] = (lt[j].x > q.len) - (lt[j].x < q.len);
+                    d[j] = (int)(nb[j] / 8u);
+                }
+            }
+        }
+        // the probes below q form a prefix of the valid ones
+        int64_t nlo = lo, nhh = hh;
+        int ndlo = dlo, ndhi = dhi;
+        bool neq = eq_hh, hit = false;
+#pragma unroll
+        for (int j = 0; j < kRunProbes; j++) {
+            if (!v[j] || hit) continue;
+            if (r[j] < 0) {
+                nlo = p[j] + 1;
+                ndlo = d[j];
+            } else {
+                nhh = p[j];
+                ndhi = d[j];
+                neq = r[j] == 0;
+                hit = true;
+            }
+        }
+        lo = nlo;
+        hh = nhh;
+        dlo = ndlo;
+        dhi = ndhi;
+        eq_hh = neq;
+    }
+    eq = eq_hh;
+#endif
+    return lo;
+}
+
 // The previous batch's union segments (prev_seg_hit) searched by the four lanes of one read
 // (lanes 4i..4i+3 call with the same read): 16 probes per round, four per lane.
 __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U, const DKey& kb, const DKey& ke,
@@ -1020,6 +1212,7 @@ __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U,
 // in the base tier, 4i + 2 / 3 in the delta tier; the begin lanes take the end's position by a
 // shuffle and decide their tier (tier_conflict); the previous batch's segments by the quad; the
 // quad's verdict goes to the read's flags from lane 4i.
+template <bool LONG>
 __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& base, const Tier& delta,
                                                  const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
                                                  const PrevSegs& ps) {
@@ -1037,8 +1230,16 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
     const bool active = live && (!is_delta || n > 0);
     int64_t lb = 0;
     bool eq = false;
-    if (active && !((k & 1) && degenerate))
-        lb = lane_lower_bound(tier.h, tier.m, n, (k & 1) ? ke : kb, htail, b.tail, eq);
+    if (active && !((k & 1) && degenerate)) {
+        const DKey& q = (k & 1) ? ke : kb;
+        if constexpr (LONG) {
+            QTail qt;
+            load_qtail(qt, q, b.tail);
+            lb = lane_lower_bound_long(tier.h, tier.m, n, q, qt, htail, b.tail, eq);
+        } else {
+            lb = lane_lower_bound(tier.h, tier.m, n, q, htail, b.tail, eq);
+        }
+    }
     const int64_t j = __shfl_xor(lb, 1, 64);  // the begin lane takes the end key's position
     bool conf = false;
     if (active && !(k & 1)) conf = tier_conflict(tier.h, tier.m, is_delta ? kHole : tier.hdr, lb, eq, j, degenerate, snap);
@@ -1059,6 +1260,7 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
 
 // One tier only (the split check) by two lanes per read: begin / end; conflicts OR into the
 // pre-zeroed flags like check_read_tier.
+template <bool LONG>
 __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const Tier& tier, bool is_base,
                                                       const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
                                                       const PrevSegs& ps) {
@@ -1074,7 +1276,16 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
     const bool active = live && (is_base || n > 0);
     int64_t lb = 0;
     bool eq = false;
-    if (active && !(k && degenerate)) lb = lane_lower_bound(tier.h, tier.m, n, k ? ke : kb, htail, b.tail, eq);
+    if (active && !(k && degenerate)) {
+        const DKey& q = k ? ke : kb;
+        if constexpr (LONG) {
+            QTail qt;
+            load_qtail(qt, q, b.tail);
+            lb = lane_lower_bound_long(tier.h, tier.m, n, q, qt, htail, b.tail, eq);
+        } else {
+            lb = lane_lower_bound(tier.h, tier.m, n, q, htail, b.tail, eq);
+        }
+    }
     const int64_t j = __shfl_xor(lb, 1, 64);
     bool conf = false;
     if (active && !k) conf = tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
@@ -1273,13 +1484,15 @@ __global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const
 }
 
 // Per-lane checks (FDBCS_CHECK=7): both tiers, four lanes per read; one tier, two lanes per read.
+// LONG: the batch has keys over 24 bytes (lane_lower_bound_long).
+template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes(BatchDev b, CheckReads c) {
-    check_read_lanes(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
+    check_read_lanes<LONG>(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
 }
-template <bool BASE>
+template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t, const uint8_t* htail,
                                                              uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps) {
-    check_read_lanes_tier(b, t, BASE, htail, hist_conf, rconf, ps);
+    check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, ps);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
@@ -1287,8 +1500,9 @@ void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Ti
     if (b.R == 0) return;
     if (lanes) {
         const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
-        fdb_launch(is_base ? k_check_lanes_tier<true> : k_check_lanes_tier<false>, dim3(grid), dim3(kBlock), 0, s, b,
-                   t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
+        auto k = is_base ? (long_keys ? k_check_lanes_tier<true, true> : k_check_lanes_tier<true, false>)
+                         : (long_keys ? k_check_lanes_tier<false, true> : k_check_lanes_tier<false, false>);
+        fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
         return;
     }
     const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
@@ -1316,9 +1530,10 @@ void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& b
     // four lookups per read: 7 = one lane each, 6 = kArity lanes each with the base and delta lookups
     // in separate waves, 1 = kArity lanes each in one wave
     CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps};
-    if (check_version == 7) {
+    if (check_version == 7 || check_version == 8) {  // 8: the long-key lanes
         const int grid = (int)(((int64_t)b.R * 4 + kBlock - 1) / kBlock);
-        fdb_launch(k_check_lanes, dim3(grid), dim3(kBlock), 0, s, b, c);
+        fdb_launch(check_version == 8 ? k_check_lanes<true> : k_check_lanes<false>, dim3(grid), dim3(kBlock), 0, s, b,
+                   c);
         return;
     }
     const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);

@@ -255,14 +255,17 @@ def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
+@pytest.mark.parametrize("lanes", ["1", "0"])
 @pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("plen", [30, 60, 104, 150])
-def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split):
+def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split, lanes):
     """Keys sharing prefixes of 30-150 bytes, so that tail comparisons end inside the long-key
     probe's first word round (48 bytes), its second (96), and past the query words it holds in
     registers (the rest compared from memory); history and batch keys of every length around them.
-    split "1": the split read check (long-key probes in both check launches); "2": the default."""
+    split "1": the split read check (long-key probes in both check launches); "2": the default.
+    lanes "1": one lane per lookup (lane_lower_bound_long, the default); "0": kArity lanes per lookup."""
     monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
+    monkeypatch.setenv("FDBCS_LONG_LANES", lanes)
     rng = np.random.default_rng(plen)
     prefixes = [bytes([0x15, 0x2a + i]) + b"x" * (plen - 2) for i in range(2)]
 
@@ -585,7 +588,8 @@ def test_empty_batches(engine, oracle_mod):
                                    {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
                                    {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"},
-                                   {"FDBCS_SPLIT_B": "0"}, {"FDBCS_SPLIT_B": "0", "FDBCS_SPLIT_CHECK": "1"}])
+                                   {"FDBCS_SPLIT_B": "0"}, {"FDBCS_SPLIT_B": "0", "FDBCS_SPLIT_CHECK": "1"},
+                                   {"FDBCS_LONG_LANES": "0"}, {"FDBCS_LONG_LANES": "0", "FDBCS_SPLIT_CHECK": "1"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the unsplit and
     split read checks, the one-wave check, long-key sorting without LDS windows, stage graphs, the
@@ -604,8 +608,9 @@ def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     rng = np.random.default_rng(71)
     now = 10
     for i in range(20):
-        pb = W.random_small_batch(rng, 250, alphabet=6 if i % 2 else 200, max_len=24 if i % 3 == 0 else 3, now=now,
-                                  staleness=12)
+        # keys up to 24 bytes (short-key lookups) and up to 40 (long-key lookups) in some batches
+        pb = W.random_small_batch(rng, 250, alphabet=6 if i % 2 else 200,
+                                  max_len=24 if i % 3 == 0 else (40 if i % 5 == 1 else 3), now=now, staleness=12)
         ve, ce = eng.detect(pb, now, now - 9)
         vo, co = ora.detect(pb, now, now - 9)
         assert (ve == vo).all()
