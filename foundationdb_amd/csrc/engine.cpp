@@ -442,15 +442,24 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     if (const char* env = getenv("FDBCS_EDGE_CAP")) edge_cap = std::max<int64_t>(1, atoll(env));  // testing knob
     for (int k = 0; k < kNumWork; k++) {
     Work& w = cs->work[k];
-    int i = 0;
+    // One arena per workspace (slot 0), its size a multiple of 2 MiB: the ~50 scratch arrays of a
+    // batch share a few large pages instead of one small allocation each (every kernel touches a
+    // dozen of them; a single-workgroup kernel's first loads otherwise wait on address
+    // translation misses).  Two passes: sizes, then the carve.
+    size_t off = 0;
+    char* arena = nullptr;
     auto take = [&](size_t bytes, void** ptr) -> int {
-        if (i >= kWsTileSlot) return FDBCS_E_INVALID;  // more TAKE slots than ws[] reserves
-        int rc = cs->ws[k][i].ensure(bytes + 64);
-        if (rc) return rc;
-        *ptr = cs->ws[k][i].p;
-        i++;
+        off = align_up(off, 256);
+        if (arena) *ptr = arena + off;
+        off += bytes + 64;
         return FDBCS_OK;
     };
+    for (int pass = 0; pass < 2; pass++) {
+    if (pass == 1) {
+        if (int rc = cs->ws[k][0].ensure(align_up(off, (size_t)2 << 20))) return rc;
+        arena = (char*)cs->ws[k][0].p;
+        off = 0;
+    }
 #define TAKE(field, bytes) \
     if (int rc = take((bytes), (void**)&w.field)) return rc
     TAKE(hist_conf, T);
@@ -482,7 +491,6 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(wbpos, 4 * W);
     TAKE(wlead, 4 * (W + 1));
     TAKE(wtxn, 4 * (W + 1));
-    TAKE(members, 8 * (W + 1));
     TAKE(gminc, 4 * (W + 1));
     TAKE(rbpos, 4 * R);
     TAKE(eoff, 4 * (R + 1));
@@ -495,6 +503,8 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(pre_st, T);
     TAKE(pre_ep, 4 * T);
     TAKE(pre_end, 4 * T);
+    TAKE(ulist, 32 * T);
+    TAKE(wpk, 4 * (W + 1));
     TAKE(tedges, 4 * edge_cap);
     TAKE(mcs_bits, 8 * (E / 64 + 2));
     TAKE(seg_b, 4 * (W + 1));
@@ -508,6 +518,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(seg_vend, 8 * (W + 1));
     TAKE(verdict, T);
     TAKE(bsc, sizeof(BatchScalars));
+    }
 #undef TAKE
     w.edge_cap = edge_cap;
     w.cap_T = T;
@@ -2131,7 +2142,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         HIPOK(hipStreamSynchronize(s));
         unsigned long long init[kTrSlots];
         for (int i = 0; i < kTrSlots; i++)
-            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin || i == kTrResBegin ||
+            init[i] = (i == kTrSampleBegin || i == kTrCheckBegin || i == kTrEpiBegin || i == kTrResBegin || i == kTrResW0min ||
                        i == kTrPartBegin || i == kTrBktBegin)
                           ? ~0ull
                           : 0ull;
@@ -2413,9 +2424,12 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                         tr[kTrPartWaves], tr[kTrPartSumFill] / np / 100.0, tr[kTrPartSumCopy] / np / 100.0,
                         tr[kTrPartSumSearch] / np / 100.0, tr[kTrPartSumPlace] / np / 100.0);
             }
-            fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us, finish %.2f us\n",
+            fprintf(stderr, "fdbcs trace: resolve pre-pass %.2f us, wait %.2f us, rounds %.2f us (setup %.2f, first round "
+                    "%.2f of which minima %.2f, %d rounds), finish %.2f us; waves start %.2f..%.2f us before the first kernarg use\n",
                     us(kTrResBegin, kTrResPre), us(kTrResPre, kTrResWait), us(kTrResWait, kTrResRounds),
-                    us(kTrResRounds, kTrResEnd));
+                    us(kTrResWait, kTrResSetup), us(kTrResSetup, kTrResRound1), us(kTrResSetup, kTrResMin1),
+                    (int)b->h_scal->intra_rounds,
+                    us(kTrResRounds, kTrResEnd), us(kTrResW0min, kTrResWait), us(kTrResW0max, kTrResWait));
             fprintf(stderr, "fdbcs trace: combine chunk 0: loads %.2f, scan1 %.2f, scan2 %.2f, stores %.2f us\n",
                     us(kTrResRounds, kTrCmbLoad), us(kTrCmbLoad, kTrCmbScan1), us(kTrCmbScan1, kTrCmbScan2),
                     us(kTrCmbScan2, kTrCmbStore));

@@ -96,6 +96,8 @@ struct BatchScalars {
     int32_t sort_big;      // sort: buckets past the slab, sorted by the workgroup path (reset by the epilogue)
     int64_t n_segments;    // union segments of committed writes (D.Combine, k_resolve)
     int64_t n_pranges;     // ranges with candidate pairs (k_scan<EdgePairScan>)
+    int32_t n_undec;       // transactions the resolution pre-pass left undecided (Work::ulist; reset by the epilogue)
+    int32_t pad2;
 };
 
 // Delta-tier version meaning "not written in this window: the base tier's version applies".
@@ -198,16 +200,19 @@ struct Work {
     // group's first write-begin index) instead of one per writer (C3: a hot key's writers)
     int32_t* wlead;        // [W] per write-begin index: 2 first of a group, 1 member, 0 none
     int32_t* wtxn;         // [W] transaction of the write with that write-begin
-    int2* members;         // [W] (transaction, group) of each group member, compacted (k_resolve)
     int32_t* gminc;        // [W] per group: least committed member transaction (k_resolve)
     int32_t groups = 0;    // set per batch
-    int32_t member_lds = 0;  // group members the resolver keeps in LDS (set at its launch)
     int32_t* edges;        // [edge_cap] writer transaction of each candidate edge
     int64_t edge_cap;
     int32_t* eptr;         // [T] resume pointer per transaction
     uint8_t* pre_st;       // [T] k_resolve pre-pass: status before the batch-order rounds
     int32_t* pre_ep;       // [T] k_resolve pre-pass: start of t's packed live writers in tedges
     int32_t* pre_end;      // [T] k_resolve pre-pass: end of t's packed live writers
+    int4* ulist;           // [2T] k_resolve pre-pass: per undecided transaction {t, first live writer slot,
+                           // end slot, 0} and its first four live writers (-1 past the end)
+    uint32_t* wpk;         // [W] per write-begin index: group lead (bits 30-31: 2 first, 1 member, 0 none)
+                           // | its transaction + 1 unless the pre-pass knows it aborted (k_resolve_pre)
+    int32_t report = 0;    // the batch reports conflicting keys (k_resolve keeps gminc)
     int32_t* tedges;       // [edge_cap] per transaction, its writers not known aborted (packed)
     uint64_t* mcs_bits;    // [E/64+1] sequential-fallback MiniConflictSet
     // union segments (<= W)
@@ -245,6 +250,9 @@ enum TraceSlot {
     kTrBktWaves, kTrBktSumLoad, kTrBktSumSort, kTrBktSumTies, kTrBktSumPut,  // per-wave sums (ticks)
     kTrPartWaves, kTrPartSumFill, kTrPartSumCopy, kTrPartSumSearch, kTrPartSumPlace,
     kTrCmbLoad, kTrCmbScan1, kTrCmbScan2, kTrCmbStore,
+    kTrResSetup, kTrResRound1,  // k_resolve: statuses and members staged; first round done
+    kTrResMin1,  // k_resolve: the first round's group minima done
+    kTrResW0min, kTrResW0max,  // k_resolve: first instruction of its first / last wave (before kernargs)
     kTrSlots
 };
 __device__ __forceinline__ void trace_min(unsigned long long* tr, int slot) {

@@ -1000,7 +1000,10 @@ __device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLeve
 // tail held in registers (QTail): two dependent loads per round.  Keys between two probes share
 // with q at least the tail words both probes share with it, so later rounds load and compare only
 // the words from there on (C4: the item bytes after a user's ~20-85 shared bytes).
-[[maybe_unused]] constexpr int kRunProbes = 3;
+#ifndef FDBCS_RUN_PROBES
+#define FDBCS_RUN_PROBES 3
+#endif
+[[maybe_unused]] constexpr int kRunProbes = FDBCS_RUN_PROBES;
 
 // Boundaries of [lo1, hi) whose prefix is below q's, counted among the n <= N from `base` (sorted).
 template <int N>
@@ -2599,6 +2602,17 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
         return;
     }
     if (sc->edge_overflow || w.no_prepass) return;
+    // The write groups' members packed for k_resolve (one word per write-begin index): members
+    // the pre-pass knows aborted (history conflict or TooOld) never count in a group's minima and
+    // carry only their lead bits.
+    if (w.groups) {
+        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < b.W; j += gridDim.x * blockDim.x) {
+            const uint32_t lead = (uint32_t)w.wlead[j];
+            const int tx = w.wtxn[j];
+            const bool dead = lead == 0 || w.hist_conf[tx] || (b.flags[tx] & kFlagTooOld);
+            w.wpk[j] = lead << 30 | (dead ? 0u : (uint32_t)tx + 1u);
+        }
+    }
     // Skip the candidate writers already known aborted (history conflict or TooOld), 64 edges per
     // step with one ballot, and commit the transactions left with none; the rest keep a resume
     // pointer at their first writer not known aborted.  These are exactly the decisions round one
@@ -2613,6 +2627,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
         // t's slots are contiguous over its reads: its live writers are packed at their start
         const int tbase = r0 < r1 ? w.eoff[r0] : 0;
         int cnt = 0;
+        int first[4] = {-1, -1, -1, -1};  // t's first four live writers (uniform over the wave)
         if (s0 == kUndecided) {
             // t's reads 64 at a time, their edge runs flattened into one index space so the loads
             // of every read's edges go out together (per-read chains no longer add up); 256 edges
@@ -2657,9 +2672,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
                     }
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const uint64_t m = __ballot(live[u]);
+                        uint64_t m = __ballot(live[u]);
                         if (live[u]) w.tedges[tbase + cnt + __popcll(m & ((1ull << lane) - 1))] = e[u];
-                        cnt += __popcll(m);
+                        for (int j = cnt; j < 4 && m; j++) {  // the first ones, by shuffles
+                            first[j] = __shfl(e[u], __ffsll((unsigned long long)m) - 1, 64);
+                            m &= m - 1;
+                        }
+                        cnt += __popcll(__ballot(live[u]));
                     }
                 }
             }
@@ -2669,99 +2688,165 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
             w.pre_st[t] = s0;
             w.pre_ep[t] = tbase;
             w.pre_end[t] = tbase + cnt;
+            w.first_conf[t] = INT_MAX;  // (k_resolve's reports)
+            if (s0 != kUndecided) {  // final: k_resolve's register rounds see only the undecided
+                w.status[t] = s0;
+                vout[t] = verdict_byte(b, t, s0);
+            } else {
+                const int u = atomicAdd(&w.bsc->n_undec, 1);
+                w.ulist[2 * u] = make_int4(t, tbase, tbase + cnt, 0);
+                w.ulist[2 * u + 1] = make_int4(first[0], first[1], first[2], first[3]);
+            }
         }
     }
     if (threadIdx.x == 0) trace_max(w.trace, kTrResPre);
 }
 
+// TPER: transactions per thread held in registers on the register path (T <= TPER * kWG); two
+// instantiations so the common batch sizes keep every register-resident value without spills.
+template <int TPER>
 __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vout, Scalars* hs) {
+    const unsigned long long t_start = wall_clock64();
+    if ((threadIdx.x & 63) == 0 && w.trace) {
+        atomicMin(&w.trace[kTrResW0min], t_start);
+        atomicMax(&w.trace[kTrResW0max], t_start);
+    }
     BatchScalars* sc = w.bsc;
     extern __shared__ __attribute__((aligned(16))) uint8_t st[];
     __shared__ int s_more;
     const int T = b.T;
     if (threadIdx.x == 0) trace_max(w.trace, kTrResWait);
-    if (sc->n_edges == 0 && !sc->edge_overflow) {  // k_resolve_pre decided everything and combined
+    constexpr int kTPer = TPER;
+    // One workgroup pays ~2 us per dependent round trip to data another XCD's kernel wrote, and its
+    // loads are bounded by one CU's outstanding misses: the rounds load as little as possible, in
+    // two round trips.  First: the edge counters, the number of transactions the pre-pass left
+    // undecided, every status byte (four per load) and this thread's packed group members.
+    const int64_t n_edges = sc->n_edges;
+    const int32_t overflow = sc->edge_overflow;
+    const int U = w.no_prepass ? 0 : sc->n_undec;
+    const int NW = w.groups ? b.W : 0;
+    constexpr int kPer = (kMaxGroupWrites + kWG - 1) / kWG;
+    const int per = (NW + blockDim.x - 1) / blockDim.x, x0 = threadIdx.x * per;
+    uint32_t pk[kPer];  // lead << 30 | transaction + 1 (0: none, or known aborted)
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const bool in = k < per && x0 + k < NW;
+        pk[k] = !in ? 0u
+                : !w.no_prepass ? w.wpk[x0 + k]
+                                : (uint32_t)w.wlead[x0 + k] << 30 | ((uint32_t)w.wtxn[x0 + k] + 1u);
+    }
+    const int nsw = (T + 3) / 4;  // status words
+    const uint32_t* pre_w = (const uint32_t*)w.pre_st;
+    uint32_t sw[4];
+    if (!w.no_prepass) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = threadIdx.x + u * blockDim.x;
+            sw[u] = i < nsw ? pre_w[i] : 0u;
+        }
+    }
+    if (n_edges == 0 && !overflow) {  // k_resolve_pre decided everything and combined
         if (threadIdx.x == 0) {
             sc->rounds = 0;
             trace_max(w.trace, kTrResEnd);
         }
         return;
     }
-    const bool use_pre = !sc->edge_overflow && !w.no_prepass;
-    constexpr int kTPer = 8;  // transactions per thread held in registers (T <= 8 * kWG)
-    const bool in_regs = use_pre && T <= kTPer * (int)blockDim.x;
-    // Register rounds: each thread's transactions' resume pointers and the writer at each pointer,
-    // loaded here so that their two dependent loads overlap the status and member loads below
-    // (only a transaction the pre-pass left undecided has writers: ep < en)
-    int ep[kTPer], en[kTPer], cur[kTPer];
+    const bool use_pre = !overflow && !w.no_prepass;
+    const bool in_regs = use_pre && U <= kTPer * (int)blockDim.x;
+    // Second: this thread's undecided transactions (the pre-pass's list): transaction, resume
+    // pointer, end and its first four live writers.  The rounds see only them; every other
+    // transaction's verdict is final and already written by the pre-pass.
+    int tt[kTPer], ep[kTPer], en[kTPer], cur[kTPer];
+    int4 f4[kTPer];
     if (in_regs) {
 #pragma unroll
         for (int k = 0; k < kTPer; k++) {
-            const int t = threadIdx.x + k * blockDim.x;
-            ep[k] = t < T ? w.pre_ep[t] : 0;
-            en[k] = t < T ? w.pre_end[t] : 0;
+            const int i = threadIdx.x + k * blockDim.x;
+            int4 r = make_int4(-1, 0, 0, 0);
+            f4[k] = make_int4(-1, -1, -1, -1);
+            if (i < U) {
+                r = w.ulist[2 * i];
+                f4[k] = w.ulist[2 * i + 1];
+            }
+            tt[k] = r.x;
+            ep[k] = r.y;
+            en[k] = r.z;
         }
-#pragma unroll
-        for (int k = 0; k < kTPer; k++) cur[k] = ep[k] < en[k] ? w.tedges[ep[k]] : -1;
     }
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        st[t] = use_pre ? w.pre_st[t] : ((w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided);
-        w.first_conf[t] = INT_MAX;
+    // the status bytes into LDS: the pre-pass's (in words), or from the flags without a pre-pass
+    if (use_pre) {
+        uint32_t* stw = (uint32_t*)st;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int i = threadIdx.x + u * blockDim.x;
+            if (i < nsw) stw[i] = sw[u];
+        }
+        for (int i = threadIdx.x + 4 * blockDim.x; i < nsw; i += blockDim.x) stw[i] = pre_w[i];  // T > 16K
+    } else {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+            st[t] = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kUndecided;
+            w.first_conf[t] = INT_MAX;
+        }
+    }
+    int ep0[kTPer];
+#pragma unroll
+    for (int k = 0; k < kTPer; k++) {
+        ep0[k] = ep[k];
+        cur[k] = in_regs && ep[k] < en[k] ? f4[k].x : -1;
     }
     __syncthreads();
     int rounds = 0;
     // write groups: per group j (its first write-begin index), the least transaction among its
     // members not aborted (minLive) and among its committed members (minComm), recomputed from the
     // statuses at the start of every round, in LDS after the status bytes
-    const int NW = w.groups ? b.W : 0;
     int32_t* minLive = (int32_t*)(st + ((T + 15) & ~15));
     int32_t* minComm = minLive + NW;
-    int2* smembers = (int2*)(minComm + NW);  // the members, when they fit (w.member_lds)
-    __shared__ int s_nmem;
-    __shared__ int s_mlds;
     __shared__ int s_wred[kWG / 64];
+    // The group members stay in registers for the whole launch: each thread holds the members
+    // among its contiguous run of <= kPer write-begin indices (W <= kMaxGroupWrites), as
+    // (transaction, group = nearest group start at or before it); members the pre-pass knows
+    // aborted never count and are left out.
+    static_assert(kMaxTxnLds <= 65536 && kMaxGroupWrites < 65535, "member packing");
+    uint32_t mem[kPer];  // transaction | group << 16; group 0xffff: none
+#pragma unroll
+    for (int k = 0; k < kPer; k++) mem[k] = 0xffff0000u;
+    // A thread's members of one group are consecutive: each run is min-reduced in registers and
+    // takes one pair of LDS atomics (a hot key's writers fill whole runs of one group).
     auto group_minima = [&](const volatile uint8_t* sv) {
         for (int j = threadIdx.x; j < NW; j += blockDim.x) minLive[j] = minComm[j] = INT_MAX;
+        uint8_t sx[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) sx[k] = (mem[k] >> 16) != 0xffffu ? sv[mem[k] & 0xffffu] : kAborted;
         __syncthreads();
-        const int M = s_nmem;
-        const int2* mem = s_mlds ? smembers : w.members;
-        for (int m0 = threadIdx.x; m0 < M; m0 += 4 * blockDim.x) {
-            int2 e[4];
+        int g = -1, lv = INT_MAX, cm = INT_MAX;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int m = m0 + u * blockDim.x;
-                e[u] = m < M ? mem[m] : make_int2(-1, 0);
+        for (int k = 0; k < kPer; k++) {
+            const int mg = (int)(mem[k] >> 16), mt = (int)(mem[k] & 0xffffu);
+            if (mg == 0xffff) continue;
+            if (mg != g) {
+                if (g >= 0) {
+                    if (lv != INT_MAX) atomicMin(&minLive[g], lv);
+                    if (cm != INT_MAX) atomicMin(&minComm[g], cm);
+                }
+                g = mg;
+                lv = cm = INT_MAX;
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (e[u].x < 0) continue;
-                const uint8_t sx = sv[e[u].x];
-                if (sx != kAborted) atomicMin(&minLive[e[u].y], e[u].x);
-                if (sx == kCommitted) atomicMin(&minComm[e[u].y], e[u].x);
-            }
+            if (sx[k] != kAborted) lv = mt < lv ? mt : lv;
+            if (sx[k] == kCommitted) cm = mt < cm ? mt : cm;
+        }
+        if (g >= 0) {
+            if (lv != INT_MAX) atomicMin(&minLive[g], lv);
+            if (cm != INT_MAX) atomicMin(&minComm[g], cm);
         }
         __syncthreads();
     };
-    if (NW && !sc->edge_overflow) {
-        // compact the group members once: (transaction, group = nearest group start at or before
-        // it).  Each thread takes a contiguous run of <= 12 write-begin indices (W <=
-        // kMaxGroupWrites), all its loads in flight; a block max-scan carries the group start in,
-        // a block sum places the thread's members.
-        constexpr int kPer = (kMaxGroupWrites + kWG - 1) / kWG;
-        const int per = (NW + blockDim.x - 1) / blockDim.x, x0 = threadIdx.x * per;
-        int lw[kPer], tx[kPer];
+    if (NW && !overflow) {
+        // a block max-scan carries the group start into each thread's run
+        int last = -1;
 #pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const bool in = k < per && x0 + k < NW;
-            lw[k] = in ? w.wlead[x0 + k] : 0;
-            tx[k] = in ? w.wtxn[x0 + k] : 0;
-        }
-        int last = -1, nm = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            if (lw[k] == 2) last = x0 + k;
-            nm += lw[k] != 0 ? 1 : 0;
-        }
+        for (int k = 0; k < kPer; k++)
+            if ((pk[k] >> 30) == 2u) last = x0 + k;
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         int v = last;
 #pragma unroll
@@ -2775,22 +2860,12 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         for (int q = 0; q < wid; q++) carry = s_wred[q] > carry ? s_wred[q] : carry;
         const int prev_in_wave = __shfl_up(v, 1, 64);
         if (lane > 0) carry = prev_in_wave > carry ? prev_in_wave : carry;
-        __syncthreads();
-        int total;
-        int off = block_excl_sum<int>(nm, s_wred, &total);
-        const bool in_lds = total <= w.member_lds;  // uniform: every round reads them from LDS
-        int2* mdst = in_lds ? smembers : w.members;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
-            if (lw[k] == 2) carry = x0 + k;
-            if (lw[k] != 0) mdst[off++] = make_int2(tx[k], carry);
+            const uint32_t lead = pk[k] >> 30, txp = pk[k] & 0x3fffffffu;
+            if (lead == 2u) carry = x0 + k;
+            if (lead != 0u && txp != 0u) mem[k] = (txp - 1u) | (uint32_t)carry << 16;
         }
-        if (threadIdx.x == 0) {
-            s_nmem = total;
-            s_mlds = in_lds ? 1 : 0;
-        }
-        __threadfence_block();
-        __syncthreads();
     }
     // the group rule for reader t and group edge e = T + j: a committed member before t aborts t,
     // an undecided one before t makes it wait, otherwise the group is no obstacle
@@ -2800,6 +2875,8 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         if (minLive[j] < t) return kUndecided;
         return kAborted;
     };
+    __syncthreads();
+    if (threadIdx.x == 0) trace_max(w.trace, kTrResSetup);
     if (in_regs) {
         // Rounds with each thread's transactions' resume pointers and current writers in
         // registers: a round reads only LDS unless a walk steps past writers aborted since (the
@@ -2814,24 +2891,49 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         for (;;) {
             if (NW) group_minima(vst);
             __syncthreads();
+            if (rounds == 0 && threadIdx.x == 0) trace_max(w.trace, kTrResMin1);
             if (threadIdx.x == 0) s_more2[(rounds + 1) & 1] = 0;
             int more = 0;
 #pragma unroll
             for (int k = 0; k < kTPer; k++) {
-                const int t = threadIdx.x + k * blockDim.x;
-                if (t >= T || vst[t] != kUndecided) continue;
+                const int t = tt[k];
+                if (t < 0 || vst[t] != kUndecided) continue;
                 int p = ep[k];
                 const int end = en[k];
                 uint8_t res = kUndecided;
                 int e = cur[k];
                 while (p < end) {
                     const uint8_t sp = e >= T ? group_status(e, t) : vst[e];
-                    if (sp == kAborted) {
-                        if (++p < end) e = w.tedges[p];
-                        continue;
+                    if (sp != kAborted) {
+                        if (sp == kCommitted) res = kAborted;
+                        break;
                     }
-                    if (sp == kCommitted) res = kAborted;
-                    break;
+                    // e aborted since: the next four writers, their loads issued together (one
+                    // global round trip per four writers aborted in earlier rounds, not per writer)
+                    int nx[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int q = p + 1 + u, d = q - ep0[k];  // d < 4: held in f4
+                        nx[u] = q >= end ? 0
+                                : d < 4  ? (d == 0 ? f4[k].x : d == 1 ? f4[k].y : d == 2 ? f4[k].z : f4[k].w)
+                                         : w.tedges[q];
+                    }
+                    int adv = 0, ne = 0;
+                    bool stop = false;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (!stop && p + 1 + u < end) {
+                            const int x = nx[u];
+                            if ((x >= T ? group_status(x, t) : vst[x]) != kAborted) {
+                                stop = true;
+                                ne = x;
+                            } else {
+                                adv++;
+                            }
+                        }
+                    }
+                    p += 1 + adv;
+                    if (p < end) e = stop ? ne : (p - ep0[k] < 4 ? f4[k].w : w.tedges[p]);
                 }
                 if (p == end) res = kCommitted;
                 ep[k] = p;
@@ -2843,11 +2945,12 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
             }
             if (more) s_more2[rounds & 1] = 1;
             __syncthreads();
+            if (rounds == 0 && threadIdx.x == 0) trace_max(w.trace, kTrResRound1);
             const int again = s_more2[rounds & 1];
             rounds++;
             if (!again) break;
         }
-    } else if (!sc->edge_overflow) {
+    } else if (!overflow) {
         for (int t = threadIdx.x; t < T; t += blockDim.x)
             w.eptr[t] = use_pre ? w.pre_ep[t] : (b.roff[t] < b.roff[t + 1] ? w.eoff[b.roff[t]] : 0);
         volatile uint8_t* vst = st;
@@ -2971,13 +3074,25 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
     }
     __syncthreads();
     if (threadIdx.x == 0) trace_max(w.trace, kTrResRounds);
-    if (NW && !sc->edge_overflow) {  // final committed minima per group (conflicting-key reports)
+    if (NW && !overflow && w.report) {  // final committed minima per group (conflicting-key reports)
         group_minima(st);
         for (int j = threadIdx.x; j < NW; j += blockDim.x) w.gminc[j] = minComm[j];
     }
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        w.status[t] = st[t];
-        vout[t] = verdict_byte(b, t, st[t]);
+    if (in_regs) {  // the undecided ones (never TooOld: the pre-pass aborted those)
+#pragma unroll
+        for (int k = 0; k < kTPer; k++) {
+            const int t = tt[k];
+            if (t >= 0) {
+                const uint8_t x = st[t];
+                w.status[t] = x;
+                vout[t] = x == kCommitted ? 2 : 0;  // verdict_byte
+            }
+        }
+    } else {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+            w.status[t] = st[t];
+            vout[t] = verdict_byte(b, t, st[t]);
+        }
     }
     if (threadIdx.x == 0) sc->rounds = rounds;
     (void)hs;  // D.Combine: k_combine, across workgroups, after this launch
@@ -3024,7 +3139,8 @@ constexpr size_t kResolveLdsMax = 160 * 1024 - 1024;  // dynamic LDS of k_resolv
 void init_kernel_attributes() {
     // status bytes (<= kMaxTxnLds) + write-group minima (<= 8 kMaxGroupWrites) + the members that
     // fit, within kResolveLdsMax (the rest of the 160 KiB is the kernel's static LDS)
-    (void)hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLdsMax);
+    (void)hipFuncSetAttribute((const void*)k_resolve<5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLdsMax);
+    (void)hipFuncSetAttribute((const void*)k_resolve<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResolveLdsMax);
 }
 
 void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report, uint8_t* verdict_out, Scalars* sc) {
@@ -3037,15 +3153,12 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
     const int64_t pre_grid = std::max<int64_t>(((int64_t)b.T * 64 + kBlock - 1) / kBlock,
                                                (2 * (int64_t)b.W + kCombineTile - 1) / kCombineTile);
     fdb_launch(k_resolve_pre, dim3((unsigned)pre_grid), dim3(kBlock), 0, s, b, w, verdict_out);
-    size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
-    Work wl = w;
-    wl.member_lds = 0;
-    if (w.groups) {  // the group members too, in what the dynamic LDS limit leaves
-        const size_t room = kResolveLdsMax > lds ? (kResolveLdsMax - lds) / 8 : 0;
-        wl.member_lds = (int32_t)std::min<size_t>(room, (size_t)b.W);
-        lds += 8 * (size_t)wl.member_lds;
-    }
-    fdb_launch(k_resolve, dim3(1), dim3(kWG), (uint32_t)lds, s, b, wl, verdict_out, sc);
+    // LDS: the status bytes and the write groups' minima (the members stay in registers)
+    const size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
+    Work wr = w;
+    wr.report = report ? 1 : 0;
+    fdb_launch(b.T <= 5 * kWG ? k_resolve<5> : k_resolve<8>, dim3(1), dim3(kWG), (uint32_t)lds, s, b, wr, verdict_out,
+               sc);
     fdb_launch(k_combine, dim3((unsigned)std::max<int64_t>(1, (2 * (int64_t)b.W + kCombineTile - 1) / kCombineTile)),
                dim3(kScanThreads), 0, s, b, w);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
@@ -4045,6 +4158,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             sc->tail_used = tail_new;
             ep.bsc->debug_error = 0;
             ep.bsc->ovf_n = 0;  // the sort's overflow list and big-bucket count (this batch's sort is done)
+            ep.bsc->n_undec = 0;  // the resolution's undecided list
             ep.bsc->sort_big = 0;
         }
     }

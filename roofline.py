@@ -110,7 +110,7 @@ def kernel_bytes(name: str, s: dict):
         return (T * (1 + 1 + 1 + 4 + 1) + 2 * W * (8 + 1 + 1 + 1) + U * (2 * D + 8),
                 "statuses (hist flag, tooOld flag, status, first conflict, verdict); D.Combine: per write endpoint its "
                 "record, owner's flags, segment flag; per segment 2 keys and 2 positions")
-    if name == "k_resolve":
+    if name.startswith("k_resolve<") or name == "k_resolve":
         if X == 0:
             return 8, "no candidate edges: the pre-pass decided and combined; one scalar"
         return (T * (1 + 1 + 8 + 4 + 1) + X * (4 + 1) + W * 16,
