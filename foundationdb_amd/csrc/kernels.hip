@@ -1668,12 +1668,15 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     __syncthreads();
     if (threadIdx.x == 0) trace_max(a.trace, kTrPartFill);
     const unsigned long long tp1 = a.trace ? wall_clock64() : 0ull;
-    if (a.btail) {  // the batch tail region into the workspace copy, 8-byte words, strided over
-        // EVERY thread of the grid (the tail region can hold many more words than endpoints)
-        const int64_t nw = (a.btail_n + 7) / 8;
+    if (a.btail && p < E && (p >> 1) >= b.R && it.len > 16u) {
+        // the tails of the write endpoints' keys into the workspace copy at the same offsets (the
+        // union segments the next batch's check reads are made of write keys only): the aligned
+        // words holding the tail; neighbouring keys' threads may write a shared word, always with
+        // the same bytes
         const uint64_t* src = (const uint64_t*)b.tail;
         uint64_t* dst = (uint64_t*)a.btail;
-        for (int64_t q = p; q < nw; q += (int64_t)gridDim.x * blockDim.x) dst[q] = src[q];
+        const int64_t w0 = it.tail / 8, w1 = ((int64_t)it.tail + (it.len - 16u) + 7) / 8;
+        for (int64_t q = w0; q < w1; q++) dst[q] = src[q];
     }
     if (p >= E) {
         if (a.trace) trace_max(a.trace, kTrPartEnd);
@@ -2889,8 +2892,12 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
         if (threadIdx.x == 0) s_more2[0] = s_more2[1] = 0;
         __syncthreads();
         for (;;) {
-            if (NW) group_minima(vst);
-            __syncthreads();
+            // a barrier between the last round's reads of its "more" flag and the reset below:
+            // group_minima ends with one
+            if (NW)
+                group_minima(vst);
+            else
+                __syncthreads();
             if (rounds == 0 && threadIdx.x == 0) trace_max(w.trace, kTrResMin1);
             if (threadIdx.x == 0) s_more2[(rounds + 1) & 1] = 0;
             int more = 0;
@@ -3234,8 +3241,9 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 constexpr int kSegPer = kWG / (2 * kArity) - 1;  // 63
 
 inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / kSegPer + 1; }
-// lanes per lookup and workgroup size of k_seg_prep
-constexpr int seg_lanes(bool long_keys) { return (void)long_keys, kArity; }
+// lanes per lookup and workgroup size of k_seg_prep: long keys one lane per lookup
+// (lane_lower_bound_long: C4's segment lookups 64 -> ? us in the pipeline), short keys kArity
+constexpr int seg_lanes(bool long_keys) { return long_keys ? 1 : kArity; }
 constexpr int seg_threads(bool long_keys) { return 2 * seg_lanes(long_keys) * (kSegPer + 1); }
 
 template <bool LONG>
@@ -3269,7 +3277,14 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
     if (live) {
         kb = seg_key(b, w, w.seg_b[sg], 0);
         ke = seg_key(b, w, w.seg_e[sg], 1);
-        pos = group_lower_bound<LONG>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        if constexpr (LONG) {
+            const DKey& key = role ? ke : kb;
+            QTail qt;
+            load_qtail(qt, key, b.tail);
+            pos = lane_lower_bound_long(h, hm, n, key, qt, htail, b.tail, eq);
+        } else {
+            pos = group_lower_bound<false>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        }
     }
     const int lane = threadIdx.x & 63;
     const int64_t hi = __shfl(pos, (lane + LL) & 63, 64);
