@@ -36,6 +36,10 @@ struct __attribute__((aligned(16))) SortItem {
     uint32_t meta, nx;
 };
 constexpr uint32_t kSortNxLen = 19;
+// nx bit 31 (slab items of k_sort_partition only): the endpoint is the end of a non-empty range
+// (its key differs from its begin's), which orders the two ends of one range inside the bucket
+// sort without their tails; the 24 key bits below it are what every comparison reads.
+constexpr uint32_t kNxEndFlag = 1u << 31;
 constexpr uint32_t kPadMeta = 0xffffffffu;
 static_assert(sizeof(SortItem) == 32, "SortItem is 32 bytes");
 

@@ -1373,11 +1373,11 @@ __device__ __forceinline__ bool item_less_tail(uint32_t alen, uint32_t atail, ui
 // keys both longer than kSortNxLen with equal words (see item_tie).
 __device__ __forceinline__ uint64_t item_aux(const SortItem& a) {
     const uint64_t l = a.len > kSortNxLen ? kSortNxLen + 1 : a.len;
-    return ((uint64_t)a.nx << 37) | (l << 32) | ((uint64_t)item_class(a.meta) << 30) | (a.meta >> 2);
+    return ((uint64_t)(a.nx & 0xffffffu) << 37) | (l << 32) | ((uint64_t)item_class(a.meta) << 30) | (a.meta >> 2);
 }
 // Equal prefixes: does the order need the tail bytes?
 __device__ __forceinline__ bool item_tie(const SortItem& a, const SortItem& b) {
-    return a.len > kSortNxLen && b.len > kSortNxLen && a.nx == b.nx;
+    return a.len > kSortNxLen && b.len > kSortNxLen && (a.nx & 0xffffffu) == (b.nx & 0xffffffu);
 }
 __device__ __forceinline__ bool is_pad(const SortItem& a) { return a.meta == kPadMeta; }
 
@@ -1597,9 +1597,16 @@ __device__ __forceinline__ uint64_t key_word(uint64_t hi, uint64_t lo, const uin
 // Tie-break word of an endpoint whose key bytes [0, c) are already known equal among the keys it
 // is sorted with: key bytes [c + 16, c + kSortNxLen), length past c capped at kSortNxLen + 1,
 // class, endpoint id (item_aux of the key with its first c bytes removed).
-__device__ __forceinline__ uint64_t aux_at(uint64_t w2, uint32_t len_c, uint32_t meta) {
+// Layout of the bucket sort's tie-break word: window bytes at bits 38-61, the capped length at
+// 33-37, the range-end flag at 32 (kNxEndFlag, only for keys longer than the window: tied keys,
+// whose run the tie ranking would otherwise order), class at 30-31, endpoint id at 0-29.
+__device__ __forceinline__ uint64_t sort_aux(uint64_t nx24, uint32_t len_c, uint32_t meta, uint32_t nxf) {
     const uint64_t l = len_c > kSortNxLen ? kSortNxLen + 1 : len_c;
-    return ((w2 >> 40) << 37) | (l << 32) | ((uint64_t)item_class(meta) << 30) | (meta >> 2);
+    const uint64_t f = len_c > kSortNxLen && (nxf & kNxEndFlag) ? 1ull : 0ull;
+    return (nx24 << 38) | (l << 33) | (f << 32) | ((uint64_t)item_class(meta) << 30) | (meta >> 2);
+}
+__device__ __forceinline__ uint64_t aux_at(uint64_t w2, uint32_t len_c, uint32_t meta, uint32_t nxf) {
+    return sort_aux(w2 >> 40, len_c, meta, nxf);
 }
 __device__ __forceinline__ bool key3_less(uint64_t ah, uint64_t al, uint64_t aa, uint64_t bh, uint64_t bl,
                                           uint64_t ba) {
@@ -1650,6 +1657,8 @@ struct SortArgs {
     BatchScalars* bsc;
     int nb;
     unsigned long long* trace;
+    int exp = 0;  // fdbcs_debug_kernel_time (FDBCS_SORT_EXP): 1 skips the tie ranking, 2 the position writes
+    int long_keys = 0;  // keys over kSortNxLen bytes: the partition marks the ends of non-empty ranges
 };
 
 __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs a) {
@@ -1660,6 +1669,10 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     const unsigned long long tp0 = a.trace ? wall_clock64() : 0ull;
     SortItem it{};
     if (p < E) it = make_item(b, p);  // in flight during the splitter fill
+    // the end of a range also loads its begin's key: is the range non-empty? (kNxEndFlag)
+    const bool mark = a.long_keys && p < E && (p & 1);
+    DKey pk{};
+    if (mark) pk = b.keys[p ^ 1];
     for (int k = threadIdx.x; k < ns; k += blockDim.x) {
         const SplitKey* sk = &a.quant[split_index(k, nb)];
         s_spl[2 * k] = sk->w[0];
@@ -1722,6 +1735,15 @@ __global__ __launch_bounds__(kBlock) void k_sort_partition(BatchDev b, SortArgs 
     }
     if (a.trace) trace_max(a.trace, kTrPartSearch);
     const unsigned long long tp3 = a.trace ? wall_clock64() : 0ull;
+    if (mark && it.len > kSortNxLen) {  // (the flag matters only to keys the sort window cannot decide)
+        bool ne = pk.hi != it.hi || pk.lo != it.lo || pk.len != it.len;
+        if (!ne) {  // equal prefixes and lengths (> 19 bytes): last tail words first, then the tails
+            const uint32_t tl = it.len - 16u;
+            ne = tail_last(b.tail + it.tail, tl) != tail_last(b.tail + pk.tail, tl) ||
+                 tail_cmp(b.tail + it.tail, it.len, b.tail + pk.tail, pk.len) != 0;
+        }
+        if (ne) it.nx |= kNxEndFlag;
+    }
     const uint32_t cls = item_class(it.meta);
     const unsigned long long old =
         atomicAdd((unsigned long long*)&a.cnt[(size_t)kCntStride * bk], 1ull | (cls == kWriteBegin ? 1ull << 32 : 0ull));
@@ -1954,12 +1976,12 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                 if (c == 0) {
                     kh[s] = it.hi;
                     kl[s] = it.lo;
-                    ka[s] = item_aux(it);
+                    ka[s] = sort_aux(it.nx & 0xffffffu, it.len, it.meta, it.nx);
                 } else {  // the key with its first c bytes removed
                     const uint8_t* t = b.tail + it.tail;
                     kh[s] = key_word(it.hi, it.lo, t, it.len, c);
                     kl[s] = key_word(it.hi, it.lo, t, it.len, c + 8);
-                    ka[s] = aux_at(key_word(it.hi, it.lo, t, it.len, c + 16), it.len - c, it.meta);
+                    ka[s] = aux_at(key_word(it.hi, it.lo, t, it.len, c + 16), it.len - c, it.meta, it.nx);
                 }
             }
         }
@@ -1972,7 +1994,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
         int ps[4];  // endpoint at each position (id bits of the tie-break word)
 #pragma unroll
         for (int s = 0; s < 4; s++) ps[s] = (int)(ka[s] & 0x3fffffffull);
-        if (LONG || c > 0) {
+        if ((LONG || c > 0) && !(a.exp & 1)) {  // exp: fdbcs_debug_kernel_time's cost breakdown only
             // positions k, k+1 tied: same two words, both keys longer than kSortNxLen past c with
             // equal bytes up to there: their order needs the tails
             bool any = false;
@@ -1989,8 +2011,8 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                     na = a2;
                 }
                 const int k = s * 64 + lane;
-                const bool tie = k + 1 < n && nh == kh[s] && nl == kl[s] && (na >> 32) == (ka[s] >> 32) &&
-                                 ((ka[s] >> 32) & 31u) == kSortNxLen + 1;
+                const bool tie = k + 1 < n && nh == kh[s] && nl == kl[s] && (na >> 33) == (ka[s] >> 33) &&
+                                 ((ka[s] >> 33) & 31u) == kSortNxLen + 1;
                 s_tie[wave][k] = tie ? 1 : 0;
                 s_p[wave][k] = ps[s];
                 any |= tie;
@@ -2003,22 +2025,83 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                 for (int s = 0; s < 4; s++) {
                     const int k = s * 64 + lane;
                     fin[s] = k;
-                    if (s >= S || k >= n) continue;
-                    const bool in_run = s_tie[wave][k] || (k > 0 && s_tie[wave][k - 1]);
-                    if (!in_run) continue;
+                    if (s >= S) break;  // uniform
+                    const bool in_run = k < n && (s_tie[wave][k] || (k > 0 && s_tie[wave][k - 1]));
                     int st = k, en = k;
-                    while (st > 0 && s_tie[wave][st - 1]) st--;
-                    while (s_tie[wave][en]) en++;
+                    if (in_run) {
+                        while (st > 0 && s_tie[wave][st - 1]) st--;
+                        while (s_tie[wave][en]) en++;
+                    }
+                    // a run of just the two ends of one range is in order already: the sort word
+                    // holds the range-end flag (begin first when the keys differ, else class order)
+                    const bool pair = in_run && en == st + 1 && (s_p[wave][k == st ? en : st] >> 1) == (ps[s] >> 1);
+                    bool todo = in_run && !pair;
+                    // Runs inside this slot's 64 positions: every member loads its own key's tail
+                    // words once (two dependent loads) and takes the others' by shuffles, so a
+                    // member's rank costs no load per other member.  Tied keys share their first
+                    // c + 19 > 16 bytes: the order is the tails, then the length, class and id.
+                    const bool simple = todo && st >= s * 64 && en < s * 64 + 64 && en - st < 16;
+                    DKey kme{};
+                    QTail tw;
+                    if (simple) {
+                        kme = b.keys[ps[s]];
+                        load_qtail(tw, kme, b.tail);
+                    }
+                    bool fallback = simple && kme.len > 16u + 8u * kQW;  // past the words held
+                    int mr = simple ? en - st + 1 : 0;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int y = __shfl_xor(mr, o, 64);
+                        mr = y > mr ? y : mr;
+                    }
+                    int rank = 0;
+                    const uint32_t mcls = item_class(endpoint_meta(b, ps[s]));
+                    for (int r = 0; r < mr; r++) {  // uniform: every lane shuffles
+                        const int j = simple ? st + r : k;
+                        const int pl = (j - s * 64) & 63;
+                        const uint32_t plen = (uint32_t)__shfl((int)kme.len, pl, 64);
+                        const int pid = __shfl(ps[s], pl, 64);
+                        const int pfall = __shfl((int)fallback, pl, 64);
+                        const uint32_t nbytes = (plen < kme.len ? plen : kme.len) - 16u;
+                        int cmpv = 0;  // partner against me
+#pragma unroll
+                        for (int u = 0; u < kQW; u++) {
+                            const uint64_t pw = (uint64_t)__shfl((long long)tw.w[u], pl, 64);
+                            const int vb = (int)nbytes - 8 * u;
+                            if (cmpv == 0 && vb > 0) {
+                                const uint64_t msk = vb >= 8 ? ~0ull : ~0ull << (64 - 8 * vb);
+                                const uint64_t x = pw & msk, y = tw.w[u] & msk;
+                                if (x != y) cmpv = x < y ? -1 : 1;
+                            }
+                        }
+                        if (simple && j <= en && j != k) {
+                            if (pfall) {
+                                fallback = true;
+                            } else {
+                                if (cmpv == 0) cmpv = plen < kme.len ? -1 : (plen > kme.len ? 1 : 0);
+                                if (cmpv == 0) {
+                                    const uint32_t pc = item_class(endpoint_meta(b, pid));
+                                    cmpv = pc < mcls ? -1 : (pc > mcls ? 1 : (pid < ps[s] ? -1 : 1));
+                                }
+                                rank += cmpv < 0 ? 1 : 0;
+                            }
+                        }
+                    }
+                    if (simple && !fallback) {
+                        fin[s] = st + rank;
+                        todo = false;
+                    }
+                    if (!todo) continue;
                     // The two endpoints of one range (a point range [k, k\0], a prefix range
                     // [p\0, p\xff]): begin <= end holds for every admitted range, so keys that
                     // differ at all order begin first — different lengths, or (equality needs no
                     // order) different last tail words, one load each instead of the whole
                     // tails.  Other pairs compare whole keys.
                     const int pm = ps[s];
-                    const DKey kme = b.keys[pm];
-                    int rank = 0;
+                    kme = b.keys[pm];
                     bool need_me = false;
                     int differ = -1;  // position of the same range's other endpoint when its key differs
+                    rank = 0;
                     for (int j = st; j <= en; j++) {
                         if (j == k) continue;
                         const int po = s_p[wave][j];
@@ -2083,9 +2166,11 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                 ex[q] = carry[q] + x - f[q];
                 carry[q] += __shfl(x, 63, 64);
             }
-            if (live) {
+            if (live && !(a.exp & 2)) {
                 put_position(b, o, ps[s], base + k, (int32_t)ex[0], (int32_t)ex[1], (int32_t)ex[2]);
                 if (o.quant) put_quantiles(b, o.quant, base + k, E, ps[s]);
+            } else if (live && ex[0] == 0x7fffffff) {
+                o.pos[0] = 0;
             }
         }
         if (a.trace && lane == 0) {
@@ -2181,8 +2266,10 @@ int sort_bucket_count(int64_t E, int target, int slab_buckets) {
     return (int)std::max<int64_t>(1, std::min(nb, cap));
 }
 
-static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb, int64_t btail_n) {
-    return SortArgs{w.btail, btail_n, quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
+static SortArgs sort_args(const Work& w, const SplitKey* quant, int nb, int64_t btail_n, bool long_keys) {
+    SortArgs a{w.btail, btail_n, quant, w.scnt, w.slab, w.ovf, w.ovf_b, w.bsc, nb, w.trace};
+    a.long_keys = long_keys ? 1 : 0;
+    return a;
 }
 
 void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, SplitKey* quant_out, bool cold,
@@ -2202,7 +2289,7 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
         fdb_launch(k_quant_cold, dim3(1), dim3(kWG), 0, s, b, (const SortItem*)w.samples, (const int32_t*)w.srank,
                    c.S, quant);
     }
-    const SortArgs a = sort_args(w, quant, nb, b.tail_n);
+    const SortArgs a = sort_args(w, quant, nb, b.tail_n, long_keys);
     fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
     SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, validate ? w.items : nullptr,
               quant_out, w.big, w.big_p};
@@ -2225,7 +2312,8 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
     hipEvent_t e0, e1;
     hipError_t err;
     if ((err = hipEventCreate(&e0)) || (err = hipEventCreate(&e1))) return err;
-    const SortArgs a = sort_args(w, quant, nb, b.tail_n);
+    SortArgs a = sort_args(w, quant, nb, b.tail_n, long_keys);
+    if (const char* v = getenv("FDBCS_SORT_EXP")) a.exp = atoi(v);  // cost breakdown (results unused)
     SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, nullptr, nullptr, w.big, w.big_p};
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     double total = 0;
