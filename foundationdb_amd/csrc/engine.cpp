@@ -218,6 +218,7 @@ struct fdbcs_conflict_set {
     int check_version = 7;    // FDBCS_CHECK: read-check kernel (7: one lane per lookup; 6: kArity lanes per
                               // lookup, the base and delta lookups in separate waves, 1: kArity lanes per
                               // lookup, the four of a read in one wave)
+    int upload_kernel = 0;    // FDBCS_UPLOAD=kernel: batches go up by a copy kernel over PCIe, not the DMA engine
     int long_lanes = 1;       // FDBCS_LONG_LANES=0: batches of keys over 24 bytes take the kArity-lane
                               // lookups (6) under FDBCS_CHECK=7 (round 3's layout, for A/B)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
@@ -877,7 +878,12 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
     (void)cs;
     if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
-    HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us));
+    if (cs->upload_kernel) {
+        launch_upload(us, sl->dev.p, sl->pin_in.dp, (int64_t)L.total);
+        HIPOK(take_launch_error());
+    } else {
+        HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us));
+    }
     HIPOK(hipEventRecord(sl->ev_up, us));
     char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
@@ -909,6 +915,7 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
         key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u + r.kind)) *
               1099511628211ull;
     }
+    const uint64_t shape = key;
     {  // this launch's copy of the shape
         uint32_t* turn = nullptr;
         for (auto& kv : cs->stage_turn)
@@ -922,6 +929,7 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
     fdbcs_conflict_set::StageGraph* sg = nullptr;
     for (auto& kv : cs->stage_cache)
         if (kv.first == key) sg = &kv.second;
+    const bool fresh = sg == nullptr;  // a new shape: every copy is instantiated now (first batch)
     auto params = [&](const LaunchList::Rec& r) {
         hipKernelNodeParams p{};
         p.func = const_cast<void*>(r.func);
@@ -931,7 +939,11 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
         p.kernelParams = L.argp.data() + r.arg0;
         return p;
     };
-    if (!sg) {
+    for (int c = 0; fresh && c < cs->graph_ring; c++) {
+        const uint64_t kc = shape * 1099511628211ull + (uint32_t)c;
+        bool have = false;
+        for (auto& kv : cs->stage_cache) have |= kv.first == kc;
+        if (have) continue;
         fdbcs_conflict_set::StageGraph g;
         HIPOK(hipGraphCreate(&g.graph, 0));
         hipGraphNode_t prev = nullptr;
@@ -950,8 +962,11 @@ int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1
             prev = nd;
         }
         HIPOK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
-        cs->stage_cache.push_back({key, g});
-        sg = &cs->stage_cache.back().second;
+        cs->stage_cache.push_back({kc, g});
+    }
+    if (fresh) {
+        for (auto& kv : cs->stage_cache)
+            if (kv.first == key) sg = &kv.second;
     } else {
         size_t k = 0;
         for (size_t i = i0; i < i1; i++) {
@@ -1121,6 +1136,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
+    if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
     if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));

@@ -402,6 +402,8 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, c
 void launch_hold(hipStream_t s, const uint32_t* release);
 // Kernel attributes set once per process (the resolver's dynamic LDS above 64 KiB).
 void init_kernel_attributes();
+// H2D copy of a packed batch by a kernel reading the host-mapped staging buffer (FDBCS_UPLOAD=kernel).
+void launch_upload(hipStream_t s, void* dst, const void* src_mapped, int64_t n);
 // Byte copy (device -> host-mapped result buffer), as a kernel.
 void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n);
 // Multi-resolver conflict bytes out[g] = 2 - verdict of batch transaction inv[g] (0 if inv[g] < 0).

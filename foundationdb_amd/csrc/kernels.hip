@@ -4283,6 +4283,33 @@ __global__ __launch_bounds__(kBlock) void k_copy_bytes(uint8_t* __restrict__ dst
         dst[i] = src[i];
 }
 
+// H2D of a packed batch by the CUs (FDBCS_UPLOAD=kernel): 16-byte loads from the host-mapped
+// pinned staging buffer over PCIe, many in flight per thread, instead of one DMA-engine copy.
+__global__ __launch_bounds__(kBlock) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16,
+                                                   const uint8_t* __restrict__ src_b, uint8_t* __restrict__ dst_b,
+                                                   int64_t n) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = tid;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; u++) dst[i + u * stride] = v[u];
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+    for (int64_t j = 16 * n16 + tid; j < n; j += stride) dst_b[j] = src_b[j];
+}
+
+void launch_upload(hipStream_t s, void* dst, const void* src, int64_t n) {
+    if (n <= 0) return;
+    const int64_t n16 = n / 16;
+    int64_t blocks = (n16 + 4 * kBlock - 1) / (4 * kBlock);
+    blocks = blocks < 1 ? 1 : (blocks > 512 ? 512 : blocks);
+    fdb_launch(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)src, (uint4*)dst, n16,
+               (const uint8_t*)src, (uint8_t*)dst, n);
+}
+
 void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n) {
     if (n <= 0) return;
     int64_t blocks = (n + kBlock - 1) / kBlock;
