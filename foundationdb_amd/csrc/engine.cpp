@@ -149,6 +149,12 @@ struct fdbcs_conflict_set {
     int64_t prev_now = 0;
     int last_wp = -1, prev2_wp = -1;    // workspaces of the last two batches submitted (their Y events)
     bool xfree_rec[kNumWork] = {};      // xfree_ev[k] set since workspace k's last use
+    // The batches behind ws ev_b[k] (workspace k's last user) and xfree_ev[k] (the batch whose check
+    // reads workspace k's segments), or null once destroyed: while a batch lives its completion
+    // flag tells whether its stages are done, one load from host-mapped memory instead of an event
+    // query (a runtime call) per dependency per batch.
+    fdbcs_batch* ws_user[kNumWork] = {};
+    fdbcs_batch* xfree_user[kNumWork] = {};
     bool y_async[kNumWork] = {};        // Y of workspace k's last batch ran on ystream (not in `stream` order)
     bool wused[kNumWork] = {};
     int wpar = 0;                   // workspace of the next batch
@@ -218,6 +224,7 @@ struct fdbcs_conflict_set {
     int check_version = 7;    // FDBCS_CHECK: read-check kernel (7: one lane per lookup; 6: kArity lanes per
                               // lookup, the base and delta lookups in separate waves, 1: kArity lanes per
                               // lookup, the four of a read in one wave)
+    int lag = 0;              // FDBCS_LAG=1: a batch's stage B is issued with the next batch's detect
     int upload_kernel = 0;    // FDBCS_UPLOAD=kernel: batches go up by a copy kernel over PCIe, not the DMA engine
     int long_lanes = 1;       // FDBCS_LONG_LANES=0: batches of keys over 24 bytes take the kArity-lane
                               // lookups (6) under FDBCS_CHECK=7 (round 3's layout, for A/B)
@@ -287,8 +294,9 @@ struct fdbcs_conflict_set {
 
 // Host/device staging of one batch.  Batches are short-lived (one per commit batch, as the
 // reference's ConflictBatch), so their pinned and device buffers come from a per-set pool instead
-// of fresh hipHostMalloc / hipMalloc calls.  `ev_free` (stage B, after the epilogue) guards the
-// device copy: a slot's next upload waits for it.
+// of fresh hipHostMalloc / hipMalloc calls.  A slot goes back to the pool only when its batch is
+// destroyed, after its completion flag was seen (the epilogue's last store) or, for a batch still
+// in flight, after its streams were synchronized: the next user's upload needs no event.
 struct BatchSlot {
     DBuf dev;
     HBuf pin_in;
@@ -297,8 +305,6 @@ struct BatchSlot {
     hipEvent_t ev[kPhCount] = {};
     bool events_made = false;
     hipEvent_t ev_up = nullptr;    // upload done (recorded on stage A's stream)
-    hipEvent_t ev_free = nullptr;  // the last batch using this slot finished on the device
-    bool free_recorded = false;
     HBuf pin_inv;  // fdbcs_batch_set_conflict_output: global -> batch transaction map (host-mapped)
     // device routing (fdbcs_batch_add_routed): scan state, global -> batch map, read ids, totals
     DBuf rt_scan, rt_inv, rt_rids, rt_dres, rt_info, rt_txpre;
@@ -341,6 +347,7 @@ struct fdbcs_batch {
     bool compacted = false;
     uint32_t seq = 0;
     volatile uint32_t* h_flag = nullptr;
+    int64_t n_report = 0;  // transactions added with report_conflicting_keys (and reports enabled)
     uint32_t recorded = 0;  // phases whose events were recorded (bit per Phase)
     bool any_report = false;
     int64_t check_hist = 0;  // boundaries (both tiers, upper bound) the read check searched
@@ -736,7 +743,6 @@ void release_slot(BatchSlot* sl) {
     if (sl->events_made)
         for (int i = 0; i < kPhCount; i++) (void)hipEventDestroy(sl->ev[i]);
     if (sl->ev_up) (void)hipEventDestroy(sl->ev_up);
-    if (sl->ev_free) (void)hipEventDestroy(sl->ev_free);
     if (sl->ev_rt0) (void)hipEventDestroy(sl->ev_rt0);
     if (sl->ev_rt1) (void)hipEventDestroy(sl->ev_rt1);
     sl->rt_scan.release();
@@ -830,7 +836,6 @@ int make_slot_events(BatchSlot* sl) {
         sl->events_made = true;
     }
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
-    if (!sl->ev_free) HIPOK(hipEventCreateWithFlags(&sl->ev_free, hipEventDisableTiming));
     return FDBCS_OK;
 }
 
@@ -850,6 +855,9 @@ void materialize(fdbcs_batch* b) {
     b->tail.assign(t, t + b->d_tail_bytes);
     b->direct = false;
 }
+
+// Has batch x's epilogue published its completion flag (null: destroyed, so done)?
+inline bool batch_done(const fdbcs_batch* x) { return !x || (x->h_flag && *x->h_flag == x->seq && x->seq != 0); }
 
 // H2D of the packed batch by the DMA engine, issued now on `us` (the upload stream, or stage A's
 // stream when the phases are timed one after another); ev_up marks its completion.
@@ -877,7 +885,6 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     // of the batch that used it last.
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
     (void)cs;
-    if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
     if (cs->upload_kernel) {
         launch_upload(us, sl->dev.p, sl->pin_in.dp, (int64_t)L.total);
         HIPOK(take_launch_error());
@@ -1137,6 +1144,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
+    if (const char* v = getenv("FDBCS_LAG")) cs->lag = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));
@@ -1491,6 +1499,11 @@ void fdbcs_batch_destroy(fdbcs_batch* b) {
         (void)hipStreamSynchronize(b->cs->ustream);
         (void)hipStreamSynchronize(b->cs->astream);
     }
+    // done (waited or synchronized): dependencies on it need no wait any more
+    for (int k = 0; k < kNumWork; k++) {
+        if (b->cs->ws_user[k] == b) b->cs->ws_user[k] = nullptr;
+        if (b->cs->xfree_user[k] == b) b->cs->xfree_user[k] = nullptr;
+    }
     // the slot goes back to the set's pool (its buffers and events are reused by the next batch)
     if (b->slot) b->cs->pool.push_back(b->slot);
     b->cs->live.erase(b);
@@ -1519,6 +1532,7 @@ int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int repor
     materialize(b);
     const int32_t t = b->T();
     uint8_t fl = (report_conflicting_keys && b->report_enabled) ? kFlagReport : 0;
+    b->n_report += fl ? 1 : 0;
     const bool too_old = read_snapshot < b->cs->oldest && n_reads > 0;  // SkipList.cpp:770
     if (too_old) fl |= kFlagTooOld;
     b->snap.push_back(read_snapshot);
@@ -1557,6 +1571,7 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
         uint8_t fl = (pb->report_conflicting_keys && pb->report_conflicting_keys[t] && b->report_enabled)
                          ? kFlagReport
                          : 0;
+        b->n_report += fl ? 1 : 0;
         const bool too_old = pb->read_snapshot[t] < oldest && nr > 0;  // SkipList.cpp:770
         if (too_old) fl |= kFlagTooOld;
         b->flags[t] = fl;
@@ -1650,6 +1665,7 @@ int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
         uint8_t fl = (pb->report_conflicting_keys && pb->report_conflicting_keys[t] && b->report_enabled)
                          ? kFlagReport
                          : 0;
+        b->n_report += fl ? 1 : 0;
         const bool too_old = pb->read_snapshot[t] < oldest && r1 > r0;
         if (too_old) fl |= kFlagTooOld;
         b->snap.push_back(pb->read_snapshot[t]);
@@ -1884,7 +1900,6 @@ int fdbcs_batch_add_routed(fdbcs_batch* b, const void* shares, int64_t stride, i
     a.ready_value = ready_value;
     a.wait_ticks = (uint64_t)cs->route_timeout_ms * 100000ull;  // 100 MHz wall clock
     a.wait_err = (uint32_t*)((uint64_t*)sl->rt_scan.p + 2);
-    if (sl->free_recorded && hipEventQuery(sl->ev_free) != hipSuccess) HIPOK(hipStreamWaitEvent(us, sl->ev_free, 0));
     HIPOK(hipMemsetAsync(sl->rt_scan.p, 0, 8 * (size_t)route_scan_words(n_elems), us));
     // global indices past the shares' transactions stay "not routed here"
     HIPOK(hipMemsetAsync(sl->rt_inv.p, 0xFF, 4 * (size_t)a.inv_n, us));
@@ -2033,8 +2048,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         for (int32_t t = 0; t < (int32_t)T; t++) inv[b->out_ids[t]] = t;
     }
     if (!b->routed) {  // (a routed batch's count came with its sizes)
-        b->any_report = false;
-        for (int64_t t = 0; t < T && !b->any_report; t++) b->any_report = (b->flags[t] & kFlagReport) != 0;
+        b->any_report = b->n_report > 0;  // (counted as the transactions were added)
     }
     b->seq = ++cs->seq;
     if (b->seq == 0) b->seq = ++cs->seq;  // 0 means "not done"
@@ -2095,6 +2109,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it
     // records cannot be queried here: waits on its events are kept unconditionally.
     const bool threaded = cs->submit_thread && !(cs->stage_graphs && timing < 2) && timing < 2 && !cs->trace && sa != s;
+    const bool lag = cs->lag && !threaded && !(cs->stage_graphs && timing < 2) && timing < 2 && !cs->trace && sa != s;
     cs->stats.host_ms_prepare += host_ms_since(t_begin);
     const auto t_rec = std::chrono::steady_clock::now();
     // ---- upload (issued now) and record stage A: D.Sort and the candidate edges of D.CheckIntraBatch
@@ -2109,13 +2124,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ev_b[wp] is recorded by every batch's stage B, whatever its stream layout, so the query is
     // never answered by a stale or never-recorded event (a timing-level change with batches in
     // flight included).
-    const bool ws_busy = cs->wused[wp] && (threaded || hipEventQuery(cs->ev_b[wp]) != hipSuccess);
+    const bool ws_busy = cs->wused[wp] && (threaded || !batch_done(cs->ws_user[wp]));
     if (ws_busy && (sa != s || cs->y_async[wp])) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     // and the check after that batch may still read its union segments and their tails
-    if (cs->xfree_rec[wp] && sa != s && (threaded || hipEventQuery(cs->xfree_ev[wp]) != hipSuccess))
+    if (cs->xfree_rec[wp] && sa != s && (threaded || !batch_done(cs->xfree_user[wp])))
         fdb_event(LaunchList::kSyncWait, cs->xfree_ev[wp], sa);
     cs->xfree_rec[wp] = false;
     cs->wused[wp] = true;
+    cs->ws_user[wp] = b;
     // stage A reads the batch: wait for the upload stream
     if (own_upload || (was_uploaded && hipEventQuery(sl->ev_up) != hipSuccess))
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sa);
@@ -2217,7 +2233,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // previous batch's segments), or of the previous batch (it compacted, or nothing pending).
         // Only a Y on ystream needs the event (a timing-level change may switch layouts mid-flight).
         const int wy = use_prev ? cs->prev2_wp : cs->last_wp;
-        if (wy >= 0 && cs->y_async[wy] && (threaded || hipEventQuery(cs->ev_b[wy]) != hipSuccess))
+        if (wy >= 0 && cs->y_async[wy] && (threaded || !batch_done(cs->ws_user[wy])))
             fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
     }
     const bool graphs = cs->stage_graphs && timing != 2;
@@ -2232,6 +2248,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
         cs->xfree_ev[cs->prev_wp] = cs->ev_res[wp];  // recorded at the end of this half X
+        cs->xfree_user[cs->prev_wp] = b;
         cs->xfree_rec[cs->prev_wp] = true;
     }
     mark(kPhCheck);
@@ -2309,12 +2326,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
                     gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1, &sc->ndb[dnew], sort_nb, sort_samples);
     fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], ys);
-    fdb_event(LaunchList::kSyncRecord, sl->ev_free, ys);
+    // (no event marks the slot free: a slot returns to the pool only from fdbcs_batch_destroy,
+    // after the batch's completion flag was seen or its streams were synchronized)
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
         fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, ys);
         cs->cmp_recorded = true;
     }
-    sl->free_recorded = true;
     mark(kPhEpilogue);
     mark(kPhEnd);
     t_record = nullptr;
@@ -2342,6 +2359,23 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         std::swap(cs->pending_y, ly);
         cs->pending_ys = ys;
         cs->b_recorded++;
+        cs->pending_batch = b;
+    } else if (lag) {
+        // Lagged submission (FDBCS_LAG, one thread): this batch's upload (issued) and stage A now,
+        // then the previous batch's stage B, and this batch's stage B at the next call (or a flush).
+        // By then its waits on its stage A and upload mostly find them complete, which the runtime
+        // passes at ~0.1 us against ~6 us for a wait on a pending event (tools/launchbench.hip).
+        // Stage B of the previous batch records no event this batch's A waits for, except the
+        // base rewrite its compaction / GC signals, which the base-tier check waits for.
+        HIPOK(la.replay(sa));
+        if (split && cs->pending_batch && (cs->pending_batch->compacted || cs->pending_batch->gc_ran)) {
+            if ((rc = flush_pending(cs))) return rc;
+        }
+        if (split) HIPOK(lc.replay(cs->cstream));
+        if ((rc = flush_pending(cs))) return rc;
+        std::swap(cs->pending_b, lb);
+        std::swap(cs->pending_y, ly);
+        cs->pending_ys = ys;
         cs->pending_batch = b;
     } else if (flush_pending(cs)) {
         return FDBCS_E_DEVICE;

@@ -57,12 +57,14 @@ def check_against_restatement(oracle_mod, kb, ko, vers, seq, got, gc="bounded"):
     return sl
 
 
-@pytest.mark.parametrize("submit_thread", ["0", "1"])
+@pytest.mark.parametrize("submit_thread", ["0", "1", "lag"])
 def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
     """C2 at full size (5M-boundary history, 5000 txns x 5R+2W) through the async pipeline for 72
     batches: crosses several size-triggered compactions and a removeBefore pass; with one and with
-    two submitting threads (FDBCS_SUBMIT_THREAD)."""
-    monkeypatch.setenv("FDBCS_SUBMIT_THREAD", submit_thread)
+    two submitting threads (FDBCS_SUBMIT_THREAD), and with each batch's stage B issued at the next
+    detect (FDBCS_LAG)."""
+    monkeypatch.setenv("FDBCS_SUBMIT_THREAD", "0" if submit_thread == "lag" else submit_thread)
+    monkeypatch.setenv("FDBCS_LAG", "1" if submit_thread == "lag" else "0")
     p = W.C2Params()
     start = 10_000_000
     kb, ko, vers = W.c2_history(p, seed=1, start_version=start)
@@ -82,9 +84,16 @@ def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
     cs.close()
 
 
-def test_async_pipeline_full_c3(engine, oracle_mod):
+@pytest.mark.parametrize("mode", ["default", "lag_split"])
+def test_async_pipeline_full_c3(engine, oracle_mod, monkeypatch, mode):
     """C3 at full size: Zipf(0.99) hot keys, 5000 txns per batch over the 5M-boundary history,
-    heavy intra-batch conflicts resolved in batch order on the device."""
+    heavy intra-batch conflicts resolved in batch order on the device.  lag_split: each batch's
+    stage B issued at the next detect (FDBCS_LAG) with the base-tier check on its own stream
+    (FDBCS_SPLIT_CHECK=1) and compactions every few batches, so a stage A is issued before the
+    previous batch's compaction (the base-tier check must wait for it)."""
+    if mode == "lag_split":
+        monkeypatch.setenv("FDBCS_LAG", "1")
+        monkeypatch.setenv("FDBCS_SPLIT_CHECK", "1")
     p = W.C2Params()
     start = 10_000_000
     kb, ko, vers = W.c2_history(p, seed=2, start_version=start)
@@ -96,10 +105,14 @@ def test_async_pipeline_full_c3(engine, oracle_mod):
         seq.append((W.c3_batch(p, rng, now, z), now, now - p.window))
     cs = engine.ConflictSet(0)
     cs.load_history(kb, ko, vers, 0)
+    if mode == "lag_split":
+        cs.set_delta_limit(60_000)  # a compaction every few batches
     got = {}
     pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
     st = cs.stats()
     assert st["intra_edges"] > 0
+    if mode == "lag_split":
+        assert st["compactions"] >= 3, st["compactions"]
     check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
     assert any((got[i] == 0).sum() > 500 for i in got)  # heavy contention really happened
     cs.close()

@@ -60,6 +60,27 @@ int main() {
                    (void)hipStreamWaitEvent(s, ev, 0);
                }, s));
     }
+    // cross-stream ordering alternatives: a wait on an event already complete, stream memory
+    // operations (write a value on one stream, wait for it on another)
+    {
+        CK(hipEventRecord(ev, s2));
+        CK(hipStreamSynchronize(s2));
+        printf("wait on a completed event:        %6.2f us\n", us_per(n, [&] { (void)hipStreamWaitEvent(s, ev, 0); }, s));
+        uint32_t* flag;
+        CK(hipMalloc(&flag, 64));
+        CK(hipMemset(flag, 0, 64));
+        uint32_t v = 0;
+        printf("write value + cross-stream wait:  %6.2f us\n", us_per(n, [&] {
+                   v++;
+                   (void)hipStreamWriteValue32(s2, flag, v, 0);
+                   (void)hipStreamWaitValue32(s, flag, v, hipStreamWaitValueGte, 0xffffffffu);
+               }, s));
+        CK(hipStreamSynchronize(s2));
+        printf("write value alone:                %6.2f us\n", us_per(n, [&] {
+                   v++;
+                   (void)hipStreamWriteValue32(s2, flag, v, 0);
+               }, s2));
+    }
     // a 15-kernel graph vs 15 launches
     hipGraph_t g;
     hipGraphExec_t ge;
