@@ -268,13 +268,14 @@ struct fdbcs_conflict_set {
     // after the batches in flight have moved past its last launch (an exec updated while its
     // previous launch is still queued is what the runtime has to wait out).
     std::vector<std::pair<uint64_t, uint32_t>> stage_turn;
-    // FDBCS_SUBMIT_THREAD=1: two submitting threads.  A helper thread issues stage A of batch i
+    // Two submitting threads (the default since round 4: C2 +3-10 % over five same-box A/Bs, C3 and
+    // C4 unchanged; FDBCS_SUBMIT_THREAD=0 keeps one).  A helper thread issues stage A of batch i
     // (and its base-tier check) while the calling thread issues stage B of batch i-1, which waited
     // (as in graph mode) for this call: kernel launches on two streams from two threads take about
     // half the wall time of one thread's (tools/threadbench.hip: 3.4 -> 1.85 us per launch).  The
     // check of batch i waits (host side) until stage B of batch i-1 is issued, because it may wait
     // on that stage's compaction event; stage B of batch i waits for the helper to go idle.
-    bool submit_thread = false;
+    bool submit_thread = true;
     std::thread worker;
     std::mutex wmu;
     std::condition_variable wcv;
@@ -1150,11 +1151,19 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));
     static std::once_flag attr_once;
     std::call_once(attr_once, init_kernel_attributes);
-    bool ok = hipStreamCreateWithFlags(&cs->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&cs->ystream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&cs->astream, hipStreamNonBlocking) == hipSuccess &&
+    // FDBCS_PRIO names the streams created at the device's greatest priority (A/B of which chain
+    // the hardware should favour when the stages compete for CUs): letters a (stage A), x (check /
+    // resolution), y (merge / epilogue), c (base-tier check)
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const char* prio = getenv("FDBCS_PRIO");
+    auto mk = [&](hipStream_t* st, char tag) {
+        if (prio && strchr(prio, tag)) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio_hi) == hipSuccess;
+        return hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess;
+    };
+    bool ok = mk(&cs->stream, 'x') && mk(&cs->ystream, 'y') && mk(&cs->astream, 'a') &&
               hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&cs->cstream, hipStreamNonBlocking) == hipSuccess &&
+              mk(&cs->cstream, 'c') &&
               hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&cs->ev_quant, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < kNumWork && ok; k++)
@@ -2218,7 +2227,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         hipStream_t sc_ = cs->cstream;
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sc_);
         if (ws_busy) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sc_);
-        if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
+        if (cs->cmp_recorded && (threaded || lag || hipEventQuery(cs->ev_cmp) != hipSuccess))
             fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
         launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, PrevSegs{}, lanes);

@@ -93,6 +93,7 @@ def test_async_pipeline_full_c3(engine, oracle_mod, monkeypatch, mode):
     previous batch's compaction (the base-tier check must wait for it)."""
     if mode == "lag_split":
         monkeypatch.setenv("FDBCS_LAG", "1")
+        monkeypatch.setenv("FDBCS_SUBMIT_THREAD", "0")
         monkeypatch.setenv("FDBCS_SPLIT_CHECK", "1")
     p = W.C2Params()
     start = 10_000_000

@@ -585,12 +585,13 @@ def test_empty_batches(engine, oracle_mod):
                                    {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
                                    {"FDBCS_GRAPH": "3"}, {"FDBCS_GRAPH": "3", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_SUBMIT_THREAD": "1", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "1"},
+                                   {"FDBCS_SUBMIT_THREAD": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "0"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
                                    {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"},
                                    {"FDBCS_SPLIT_B": "0"}, {"FDBCS_SPLIT_B": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_LONG_LANES": "0"}, {"FDBCS_LONG_LANES": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_LAG": "1"}, {"FDBCS_LAG": "1", "FDBCS_SPLIT_CHECK": "1"},
+                                   {"FDBCS_LAG": "1", "FDBCS_SUBMIT_THREAD": "0"},
+                                   {"FDBCS_LAG": "1", "FDBCS_SUBMIT_THREAD": "0", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_UPLOAD": "kernel"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
     """Non-default pipeline variants kept for measurement stay exact: the unsplit and
