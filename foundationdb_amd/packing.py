@@ -101,6 +101,16 @@ class PackedBatch:
     def n_writes(self) -> int:
         return int(self.write_offsets[-1])
 
+    @property
+    def tail_bytes(self) -> int:
+        """Key bytes past the 16-byte prefix over every endpoint (the batch's tail region)."""
+        return int(np.maximum(np.diff(self.key_offsets) - 16, 0).sum())
+
+    @property
+    def long_endpoints(self) -> int:
+        """Endpoints whose key runs past 16 bytes."""
+        return int((np.diff(self.key_offsets) > 16).sum())
+
     def key(self, k: int) -> bytes:
         return self.key_bytes[self.key_offsets[k] : self.key_offsets[k + 1]].tobytes()
 

@@ -61,6 +61,9 @@ def shape_of(batches, st: dict, history: int, dir_share: float = 1.0) -> dict:
         "compact_bytes": st.get("compact_bytes_all", 0) / max(1, st.get("compactions", 0)),
         "fc": st.get("compactions", 0) / b,  # share of batches that compact (their epilogue rebuilds the base)
         "dir_share": dir_share,
+        # tail bytes per batch and the share of endpoints whose keys run past 16 bytes
+        "tail_bytes": sum(x.tail_bytes for x in batches) / nb,
+        "long_share": sum(x.long_endpoints for x in batches) / max(1.0, sum(2 * (x.n_reads + x.n_writes) for x in batches)),
     }
 
 
@@ -70,7 +73,7 @@ def kernel_bytes(name: str, s: dict):
     S = min(E, max(1024.0, min(8192.0, 4 * math.ceil(E / 128))))
     nb = min(2048.0, math.ceil(E / 128))
     look_b, look_d = lookup_bytes(N, s["dir_share"]), lookup_bytes(Nd, 0.5)
-    if name == "k_check_lanes" or name.startswith("k_check_reads"):  # both tiers
+    if name == "k_check_lanes" or name.startswith("k_check_lanes<") or name.startswith("k_check_reads"):  # both tiers
         return (2 * R * (D + look_b + look_d) + R * (4 + V) + 2 * R * V + T,
                 "2R(D + base lookup + delta lookup) + R(owner + snapshot) + range-max ends 2RV + T")
     if name.startswith("k_check_tier<true") or name.startswith("k_check_lanes_tier<true"):
@@ -87,19 +90,29 @@ def kernel_bytes(name: str, s: dict):
         return 2 * I * E, "one read and one write of every 32-byte item"
     if name == "k_sort_partition":
         # the slot and class-count atomics execute at the memory side (1 + 1/2 per endpoint): PMC
-        # counts ~32 bytes each beyond the item traffic (profiles/pmc_c2_*: 4.1 MB for 105k atomics)
-        return (E * (D + I) + 1.5 * E * 32 + nb * 16,
+        # counts ~32 bytes each beyond the item traffic (profiles/pmc_c2_*: 4.1 MB for 105k atomics);
+        # keys over 16 bytes: the first tail word of every endpoint (a 64-byte sector) and the write
+        # keys' tails copied for the next batch's check
+        tl = s.get("tail_bytes", 0.0)
+        lk = s.get("long_share", 0.0)
+        return (E * (D + I) + 1.5 * E * 32 + nb * 16 + lk * E * 64 + 2 * tl * W / max(1.0, R + W),
                 "E keys read, E 32-byte items written to their bucket slabs; 1.5 memory-side atomics per endpoint "
-                "(~32 bytes each)")
+                "(~32 bytes each); long keys: a tail sector per endpoint, the write keys' tails copied")
     if name.startswith("k_sort_bucket"):
-        # pos[p] is a scattered 4-byte store: one 64-byte line written per endpoint
-        return (E * (I + 64 + 4 + 12) + G * 4 + nb * 16,
+        # pos[p] is a scattered 4-byte store: one 64-byte line written per endpoint; keys over 16 bytes
+        # read their sort window past the bucket's common prefix from the tail (a 64-byte sector)
+        lk = s.get("long_share", 0.0)
+        return (E * (I + 64 + 4 + 12) + G * 4 + nb * 16 + lk * E * 64,
                 "E slab items read; meta and 3 class prefixes written by position, pos[] by endpoint (a scattered "
-                "store: a 64-byte line each); R+W begin lists")
+                "store: a 64-byte line each); R+W begin lists; long keys: a tail sector per endpoint")
     if name.startswith("k_scan<3, fdbcs::PosScan"):
         return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
     if name.startswith("k_scan<3, fdbcs::EdgePairScan"):
-        return G * (8 + 24 + 8) + W * 8, "per range: 2 positions, class prefixes at both, slot/pair offsets (+ index of ranges with pairs)"
+        # the class prefixes at a range's two sorted positions are six scattered 4-byte gathers: a
+        # 32-byte sector each; writes also place their sorted endpoint records and keys for D.Combine
+        return (G * (8 + 6 * 32 + 8) + W * (2 * 8 + 2 * D + 8),
+                "per range: 2 positions, 3 class prefixes at both (scattered gathers, 32-byte sectors), slot/pair "
+                "offsets; per write its two sorted endpoint records and keys, group lead and owner")
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
     if name == "k_resolve_pre":
@@ -138,12 +151,13 @@ def kernel_bytes(name: str, s: dict):
     if name == "k_epilogue":
         # the levels and sample index of the tier that changed: the delta after a merge, the whole
         # base after a compaction (a share fc of the launches); per boundary its version, and per 8
-        # boundaries the 64-byte line holding the sampled key plus the skey8 entry written
+        # boundaries the 128-byte line (gfx950) holding the sampled key plus the skey8 entry written
         fc = s.get("fc", 0.0)
         n = (1 - fc) * Nd + fc * N if (Nd > 0 or fc > 0) else N
-        return (n * (V + 64 / 8 + P / 8) + T * 2 + R * 6,
+        return (n * (V + 128 / 8 + P / 8) + T * 2 + R * 6,
                 "levels and sample index of the changed tier (the base on the compacting share of the launches): "
-                "versions, one key line and one skey8 entry per 8 boundaries; verdicts; re-zeroed flags and edge counts")
+                "versions, one 128-byte key line and one skey8 entry per 8 boundaries; verdicts; re-zeroed flags "
+                "and edge counts")
     if name == "k_directory":
         return 65537 * (4 + 17 * P), "65537 slots: binary search over level-0 samples"
     if name == "k_conflict_output":

@@ -53,4 +53,19 @@ for k in sorted(set(per["FETCH_SIZE"]) & set(per["WRITE_SIZE"])):
     out["bytes_per_launch"][k] = (2 * f + w) * 1024
     out["bytes_per_launch_raw"][k] = (f + w) * 1024
     out["launches"][k] = len(per["FETCH_SIZE"][k])
+# The model of the same run (the FETCH_SIZE pass's bench line prices every kernel at that run's own
+# shape: its delta sizes and its share of compacting batches, which set what an average launch of
+# the merge copy or the epilogue moves), beside the measured bytes.
+try:
+    line = [l for l in open(os.path.join(root, "FETCH_SIZE.json")).read().splitlines() if l.startswith("{")][-1]
+    kern = json.loads(line).get("kernels", {})
+    out["model_bytes_per_launch"] = {}
+    out["ratio_to_model"] = {}
+    for k, v in out["bytes_per_launch"].items():
+        m = (kern.get(k) or {}).get("algorithmic_bytes_per_launch")
+        if m:
+            out["model_bytes_per_launch"][k] = m
+            out["ratio_to_model"][k] = round(v / m, 3)
+except (OSError, IndexError, ValueError):
+    pass
 print(json.dumps(out, indent=1))
