@@ -4105,6 +4105,10 @@ static_assert(sizeof(Scalars) % 8 == 0 && sizeof(BatchScalars) % 8 == 0, "scalar
 static_assert(kScWords <= 32 && kBscWords <= 32, "one lane per word, Scalars in lanes 0-31, BatchScalars in 32-63");
 constexpr int sc_word(size_t off) { return (int)(off / 8); }
 
+// BASE: the launch rebuilds a whole tier (after a compaction, or a history load), not the delta a
+// merge left: the same code, named apart so per-kernel times separate the per-batch work from the
+// occasional full rebuild.
+template <bool BASE>
 __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* sc, const int64_t* n_levels, Epilogue ep) {
     if (threadIdx.x == 0) trace_min(ep.trace, kTrEpiBegin);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -4399,7 +4403,7 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
     fdb_launch(k_lvl3_reset, dim3(1), dim3(kBlock), 0, s, m.lvl[3], lvl3_n, m.lvl[2], lvl2_n);
     Epilogue ep{};
     ep.trace = nullptr;
-    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kEpiThreads), 0, s, m, sc, n, ep);
+    fdb_launch(k_epilogue<true>, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kEpiThreads), 0, s, m, sc, n, ep);
 }
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
@@ -4410,8 +4414,12 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
     int64_t extra = std::max<int64_t>(b.R, b.T);
     for (int k = 0; k <= kNumScans; k++) extra = std::max(extra, ep.zero64_n[k]);
-    fdb_launch(k_epilogue, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kEpiThreads), 0, s, m, sc,
-                       (const int64_t*)nullptr, ep);
+    if (compacted)
+        fdb_launch(k_epilogue<true>, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kEpiThreads), 0, s, m, sc,
+                   (const int64_t*)nullptr, ep);
+    else
+        fdb_launch(k_epilogue<false>, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kEpiThreads), 0, s, m, sc,
+                   (const int64_t*)nullptr, ep);
 }
 
 }  // namespace fdbcs

@@ -59,7 +59,6 @@ def shape_of(batches, st: dict, history: int, dir_share: float = 1.0) -> dict:
         "X": st.get("intra_edges", 0) / max(1, b - st.get("intra_fallbacks", 0)),
         "merge_bytes": st.get("merge_bytes_all", 0) / b,
         "compact_bytes": st.get("compact_bytes_all", 0) / max(1, st.get("compactions", 0)),
-        "fc": st.get("compactions", 0) / b,  # share of batches that compact (their epilogue rebuilds the base)
         "dir_share": dir_share,
         # tail bytes per batch and the share of endpoints whose keys run past 16 bytes
         "tail_bytes": sum(x.tail_bytes for x in batches) / nb,
@@ -148,16 +147,16 @@ def kernel_bytes(name: str, s: dict):
         return Nd * (8 + 8 + 1 + 24), "per delta boundary: lo, version, exact flag; 3 words written"
     if name.startswith("k_scan<2, fdbcs::GcScan"):
         return N * (2 * V + 8) + N * 32, "versions (own + predecessor) and lengths read, kept boundaries rewritten"
-    if name == "k_epilogue":
-        # the levels and sample index of the tier that changed: the delta after a merge, the whole
-        # base after a compaction (a share fc of the launches); per boundary its version, and per 8
-        # boundaries the 128-byte line (gfx950) holding the sampled key plus the skey8 entry written
-        fc = s.get("fc", 0.0)
-        n = (1 - fc) * Nd + fc * N if (Nd > 0 or fc > 0) else N
+    if name.startswith("k_epilogue"):
+        # the levels and sample index of the tier that changed: the delta after a merge
+        # (k_epilogue<false>), the whole base after a compaction (k_epilogue<true>); per boundary its
+        # version, and per 8 boundaries the 128-byte line (gfx950) holding the sampled key plus the
+        # skey8 entry written
+        n = N if name.startswith("k_epilogue<true") or Nd <= 0 else Nd
         return (n * (V + 128 / 8 + P / 8) + T * 2 + R * 6,
-                "levels and sample index of the changed tier (the base on the compacting share of the launches): "
-                "versions, one 128-byte key line and one skey8 entry per 8 boundaries; verdicts; re-zeroed flags "
-                "and edge counts")
+                "levels and sample index of the changed tier (the delta after a merge; the base after a compaction, "
+                "k_epilogue<true>): versions, one 128-byte key line and one skey8 entry per 8 boundaries; verdicts; "
+                "re-zeroed flags and edge counts")
     if name == "k_directory":
         return 65537 * (4 + 17 * P), "65537 slots: binary search over level-0 samples"
     if name == "k_conflict_output":

@@ -31,7 +31,7 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"], short(r["Kernel_Name"])))
     rows.sort()
-    ep = [i for i, r in enumerate(rows) if r[3] == "k_epilogue"]
+    ep = [i for i, r in enumerate(rows) if r[3].startswith("k_epilogue")]
     ep = ep[-(a.last + 1):]
     t0, t1 = rows[ep[0]][1], rows[ep[-1]][1]
     win = [r for r in rows if r[0] >= t0 and r[1] <= t1]
@@ -62,7 +62,7 @@ def main():
                 cur = ("B", s, e, 0)
             elif cur is not None:
                 cur = (cur[0], cur[1], e, cur[3])
-            if cur is not None and ((cur[0] == "A" and k == "k_edge_fill") or (cur[0] == "B" and k == "k_epilogue")):
+            if cur is not None and ((cur[0] == "A" and k == "k_edge_fill") or (cur[0] == "B" and k.startswith("k_epilogue"))):
                 spans[cur[0]].append((cur[1], cur[2]))
                 cur = None
     for st, v in sorted(spans.items()):
