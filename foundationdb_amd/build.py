@@ -11,7 +11,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libfdbcs.so")
 SOURCES = ["engine.cpp", "kernels.hip"]
-HEADERS = ["dkey.h", "engine.h", "scan.h", "launch.h"]
+HEADERS = ["dkey.h", "engine.h", "scan.h", "launch.h", "lane_xor.h"]
 ARCH = os.environ.get("FDBCS_OFFLOAD_ARCH", "gfx950")
 
 

@@ -26,6 +26,7 @@
 #include <limits.h>
 
 #include "engine.h"
+#include "lane_xor.h"
 
 namespace fdbcs {
 
@@ -1657,7 +1658,7 @@ struct SortArgs {
     BatchScalars* bsc;
     int nb;
     unsigned long long* trace;
-    int exp = 0;  // fdbcs_debug_kernel_time (FDBCS_SORT_EXP): 1 skips the tie ranking, 2 the position writes
+    int exp = 0;  // fdbcs_debug_kernel_time (FDBCS_SORT_EXP): 1 skips the tie ranking, 2 the position writes, 4 the network, 8 the count prologue
     int long_keys = 0;  // keys over kSortNxLen bytes: the partition marks the ends of non-empty ranges
 };
 
@@ -1784,7 +1785,8 @@ struct SortOut {
 };
 
 // Bitonic network over 64 S (hi, lo, aux) triples of one wave: element s * 64 + lane in slot s of
-// the lane; partners closer than 64 by shuffles, farther ones inside the lane's registers.
+// the lane; partners closer than 64 by lane exchanges (lane_xor64), farther ones inside the lane's
+// registers.
 template <int S>
 __device__ __forceinline__ void wave_bitonic(uint64_t (&kh)[4], uint64_t (&kl)[4], uint64_t (&ka)[4]) {
     const int lane = threadIdx.x & 63;
@@ -1808,8 +1810,8 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&kh)[4], uint64_t (&kl)[4
             } else {
 #pragma unroll
                 for (int s = 0; s < S; s++) {
-                    const uint64_t yh = __shfl_xor(kh[s], j, 64), yl = __shfl_xor(kl[s], j, 64),
-                                   ya = __shfl_xor(ka[s], j, 64);
+                    const uint64_t yh = lane_xor64_rt(kh[s], j), yl = lane_xor64_rt(kl[s], j),
+                                   ya = lane_xor64_rt(ka[s], j);
                     const bool up = ((s * 64 + lane) & k) == 0, lower = (lane & j) == 0;
                     const bool y_less = key3_less(yh, yl, ya, kh[s], kl[s], ka[s]);
                     if (lower == up ? y_less : !y_less) {
@@ -1889,7 +1891,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
     // ---- bucket offsets: counts of every bucket before B0 and of all buckets, reduced by the
     // workgroup (nb <= kSortMaxBuckets: 16 per thread at most, loads issued together)
     uint32_t pre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
-    for (int k0 = threadIdx.x; k0 < nb; k0 += 4 * kBlock) {
+    for (int k0 = threadIdx.x; k0 < ((a.exp & 8) ? 0 : nb); k0 += 4 * kBlock) {  // (exp 8: cost breakdown only)
         uint64_t c0[4], c1[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1928,6 +1930,10 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
     if (threadIdx.x < kWaves && B0 + (int)threadIdx.x >= nb)
 #pragma unroll
         for (int c = 0; c < 4; c++) s_cnt[threadIdx.x][c] = 0;
+    if ((a.exp & 8) && threadIdx.x < kWaves && B0 + (int)threadIdx.x < nb) {  // cost breakdown: 64 per bucket
+        s_cnt[threadIdx.x][0] = 64;
+        s_cnt[threadIdx.x][1] = s_cnt[threadIdx.x][2] = s_cnt[threadIdx.x][3] = 16;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t run[4] = {0, 0, 0, 0};
@@ -1986,7 +1992,8 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             }
         }
         if (a.trace) tw1 = wall_clock64();
-        if (S == 1) wave_bitonic<1>(kh, kl, ka);
+        if (a.exp & 4) {  // cost breakdown only: no network
+        } else if (S == 1) wave_bitonic<1>(kh, kl, ka);
         else if (S == 2) wave_bitonic<2>(kh, kl, ka);
         else wave_bitonic<4>(kh, kl, ka);
         if (lane == 0) trace_max(a.trace, kTrBktSorted);

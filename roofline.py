@@ -205,7 +205,8 @@ def sort_phase(table: dict) -> dict | None:
 # from the running tree's describes other code and is not used.
 BUILD_SOURCES = ("foundationdb_amd/csrc/kernels.hip", "foundationdb_amd/csrc/engine.cpp",
                  "foundationdb_amd/csrc/engine.h", "foundationdb_amd/csrc/scan.h", "foundationdb_amd/csrc/launch.h",
-                 "foundationdb_amd/csrc/dkey.h", "include/fdb_conflict_set.h")
+                 "foundationdb_amd/csrc/dkey.h", "foundationdb_amd/csrc/lane_xor.h",
+                 "include/fdb_conflict_set.h")
 
 
 def build_id(root: str) -> str:

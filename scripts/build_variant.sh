@@ -9,8 +9,8 @@ REV=$1; NAME=$2
 TMP=$(mktemp -d)
 mkdir -p $TMP/foundationdb_amd/csrc $TMP/include foundationdb_amd/variants
 for f in foundationdb_amd/csrc/engine.cpp foundationdb_amd/csrc/kernels.hip foundationdb_amd/csrc/engine.h \
-         foundationdb_amd/csrc/scan.h foundationdb_amd/csrc/launch.h foundationdb_amd/csrc/dkey.h include/fdb_conflict_set.h; do
-  if [ "$REV" = "WT" ]; then cp $f $TMP/$f; else git show $REV:$f > $TMP/$f; fi
+         foundationdb_amd/csrc/scan.h foundationdb_amd/csrc/launch.h foundationdb_amd/csrc/dkey.h foundationdb_amd/csrc/lane_xor.h include/fdb_conflict_set.h; do
+  if [ "$REV" = "WT" ]; then cp $f $TMP/$f; else git show $REV:$f > $TMP/$f 2>/dev/null || : > $TMP/$f; fi
 done
 H=/opt/rocm/bin/hipcc
 $H -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -disable-promote-alloca-to-lds ${EXTRA:-} \
