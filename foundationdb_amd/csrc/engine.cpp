@@ -270,9 +270,10 @@ struct fdbcs_conflict_set {
     std::vector<std::pair<uint64_t, uint32_t>> stage_turn;
     // Two submitting threads (the default since round 4: C2 +3-10 % over five same-box A/Bs, C3 and
     // C4 unchanged; FDBCS_SUBMIT_THREAD=0 keeps one).  A helper thread issues stage A of batch i
-    // (and its base-tier check) while the calling thread issues stage B of batch i-1, which waited
-    // (as in graph mode) for this call: kernel launches on two streams from two threads take about
-    // half the wall time of one thread's (tools/threadbench.hip: 3.4 -> 1.85 us per launch).  The
+    // (and its base-tier check) while the calling thread issues stage B's X half of batch i-1,
+    // which waited (as in graph mode) for this call; the helper then issues that batch's Y half
+    // once X is out (helper_y): kernel launches on two streams from two threads take about half
+    // the wall time of one thread's (tools/threadbench.hip: 3.4 -> 1.85 us per launch).  The
     // check of batch i waits (host side) until stage B of batch i-1 is issued, because it may wait
     // on that stage's compaction event; stage B of batch i waits for the helper to go idle.
     bool submit_thread = true;
@@ -286,6 +287,16 @@ struct fdbcs_conflict_set {
     LaunchList work_a, work_c;          // the helper's lists
     hipStream_t work_sa = nullptr;
     uint32_t work_need_b = 0;           // the check goes out once b_issued >= this
+    // Stage B's Y half of the previous batch, issued by the helper once the calling thread has
+    // issued its X half (FDBCS_HELPER_Y=0: both halves from the calling thread).  The calling
+    // thread issues record + X, the helper stage A + Y + base check: their runtime calls split
+    // about evenly instead of ~2:1.
+    bool helper_y = true;
+    LaunchList work_y;
+    hipStream_t work_ys = nullptr;
+    uint32_t work_need_x = 0;            // Y goes out once x_issued >= this
+    std::atomic<uint32_t> x_issued{0};   // stage-B X lists issued (calling thread)
+    fdbcs_batch* work_y_batch = nullptr; // whose Y the helper holds (calling thread's view)
     LaunchList rec_a, rec_b, rec_c, rec_y, pending_b, pending_y;
     hipStream_t pending_ys = nullptr;  // the stream of pending_y
     fdbcs_batch* pending_batch = nullptr;
@@ -1040,6 +1051,13 @@ void worker_main(fdbcs_conflict_set* cs) {
         }
         if (j == 2) return;
         hipError_t e = cs->work_a.replay(cs->work_sa);
+        if (!cs->work_y.recs.empty()) {
+            while (cs->x_issued.load(std::memory_order_acquire) < cs->work_need_x) std::this_thread::yield();
+            const hipError_t e3 = cs->work_y.replay(cs->work_ys);
+            if (e == hipSuccess) e = e3;
+            cs->work_y.clear();
+            cs->b_issued.fetch_add(1, std::memory_order_release);
+        }
         if (!cs->work_c.recs.empty()) {
             while (cs->b_issued.load(std::memory_order_acquire) < cs->work_need_b) std::this_thread::yield();
             const hipError_t e2 = cs->work_c.replay(cs->cstream);
@@ -1057,6 +1075,7 @@ void worker_main(fdbcs_conflict_set* cs) {
 int worker_wait(fdbcs_conflict_set* cs) {
     if (!cs->worker.joinable()) return FDBCS_OK;
     while (cs->wjob.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    cs->work_y_batch = nullptr;  // any Y it held is issued
     return cs->werr.exchange(0) ? FDBCS_E_DEVICE : FDBCS_OK;
 }
 
@@ -1086,6 +1105,7 @@ int flush_pending(fdbcs_conflict_set* cs) {
     cs->pending_batch = nullptr;
     int rc = FDBCS_OK;
     if (cs->pending_b.replay(cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
+    cs->x_issued.fetch_add(1, std::memory_order_release);
     if (cs->pending_y.replay(cs->pending_ys) != hipSuccess) rc = FDBCS_E_DEVICE;
     cs->b_issued.fetch_add(1, std::memory_order_release);
     cs->pending_b.clear();
@@ -1140,6 +1160,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
+    if (const char* v = getenv("FDBCS_HELPER_Y")) cs->helper_y = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
@@ -2355,13 +2376,24 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         std::swap(cs->work_c, lc);  // empty unless split
         cs->work_sa = sa;
         const bool prev = cs->pending_batch != nullptr;
+        const bool hy = prev && cs->helper_y;
+        if (hy) {  // the previous batch's Y to the helper, after the X this thread issues below
+            std::swap(cs->work_y, cs->pending_y);
+            cs->work_ys = cs->pending_ys;
+            cs->work_need_x = cs->x_issued.load(std::memory_order_relaxed) + 1;
+            cs->work_y_batch = cs->pending_batch;
+        }
         cs->work_need_b = cs->b_recorded;  // every stage B recorded so far, batch i-1's included
         worker_start_job(cs);
         if (prev) {
             cs->pending_batch = nullptr;
             hipError_t e = cs->pending_b.replay(s);
-            const hipError_t e2 = cs->pending_y.replay(cs->pending_ys);
-            cs->b_issued.fetch_add(1, std::memory_order_release);
+            cs->x_issued.fetch_add(1, std::memory_order_release);
+            hipError_t e2 = hipSuccess;
+            if (!hy) {
+                e2 = cs->pending_y.replay(cs->pending_ys);
+                cs->b_issued.fetch_add(1, std::memory_order_release);
+            }
             if (e != hipSuccess || e2 != hipSuccess) return FDBCS_E_DEVICE;
         }
         std::swap(cs->pending_b, lb);
@@ -2433,6 +2465,8 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
         HIPOK(hipSetDevice(cs->device));
         if (cs->pending_batch == b)  // its stage B still waits for the next detect: launch it now
             if (int rc = flush_pending(cs)) return rc;
+        if (cs->work_y_batch == b)  // its Y is with the helper: issued (events and all) before reading them
+            if (int rc = worker_wait(cs)) return rc;
         // the epilogue's last workgroup publishes b->seq; poll it (checking the stream for errors)
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
             if ((spin & 1023) == 1023) {
