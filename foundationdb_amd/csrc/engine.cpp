@@ -234,6 +234,12 @@ struct fdbcs_conflict_set {
                               // even for batches with keys over 16 bytes (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
     bool directory = true;  // FDBCS_DIRECTORY=0: base-tier lookups descend the whole sample tree (A/B)
+    // Bytes every loaded key shares ahead of the directory's 16 bits (MaxLevels::dir_p; 0 with
+    // FDBCS_DIR_PREFIX=0): the load's common prefix, capped at 14.  Keys written later outside it
+    // take the directories' end slots (dir_slot), so the mapping stays monotone.
+    bool dir_prefix = true;
+    uint32_t dir_p = 0;
+    uint64_t dir_phi = 0, dir_plo = 0;
     DBuf trace_buf;
     // Per-kernel device time (fdbcs_kernel_profile): launches and milliseconds by kernel, from the
     // events of timing level 3 (every kernel) or of the timed kernel at level 1.
@@ -604,6 +610,9 @@ MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     m.keys = (const ulonglong2*)cs->hkey[k].p;
     carve_index(m, (ulonglong2*)cs->lvl[0].p, cs->hist_cap);
     m.dir = cs->directory ? (const int32_t*)cs->dir.p : nullptr;
+    m.dir_p = cs->dir_p;
+    m.dir_phi = cs->dir_phi;
+    m.dir_plo = cs->dir_plo;
     return m;
 }
 
@@ -623,6 +632,9 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     carve_index(m, (ulonglong2*)cs->dlvl[k][0].p, cs->delta_cap);
     m.edir = (uint64_t*)cs->edir[k].p;
     m.edir_epoch = cs->edir[k].p ? cs->ddir_epoch[k] : 0;
+    m.dir_p = cs->dir_p;  // the delta's directory slots too (the epilogue's fill)
+    m.dir_phi = cs->dir_phi;
+    m.dir_plo = cs->dir_plo;
     return m;
 }
 
@@ -1163,6 +1175,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_HELPER_Y")) cs->helper_y = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
+    if (const char* v = getenv("FDBCS_DIR_PREFIX")) cs->dir_prefix = v[0] != '0';
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
@@ -1288,6 +1301,8 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     cs->header_version = version;
     cs->max_written = version;
     cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;
+    cs->dir_p = 0;
+    cs->dir_phi = cs->dir_plo = 0;
     cs->prev_segs = false;
     cs->n_ub = 0;
     cs->nd_ub = 0;
@@ -1391,12 +1406,26 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     s.n = n;
     s.tail_used = (int64_t)tail.size();
     HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
+    // the directory skips the bytes the first and last keys' (zero-padded) prefixes share
+    cs->dir_p = 0;
+    cs->dir_phi = cs->dir_plo = 0;
+    if (cs->dir_prefix && n >= 2) {
+        const uint64_t xh = k[0].x ^ k[n - 1].x, xl = k[0].y ^ k[n - 1].y;
+        const uint32_t lcp = xh ? (uint32_t)__builtin_clzll(xh) / 8 : (xl ? 8 + (uint32_t)__builtin_clzll(xl) / 8 : 16);
+        cs->dir_p = std::min<uint32_t>(lcp, 14);
+        const uint32_t p = cs->dir_p;
+        const uint64_t mh = p >= 8 ? ~0ull : (p ? ~0ull << (64 - 8 * p) : 0ull);
+        const uint64_t ml = p <= 8 ? 0ull : ~0ull << (128 - 8 * p);
+        cs->dir_phi = k[0].x & mh;
+        cs->dir_plo = k[0].y & ml;
+    }
     launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n, cs->lvl3_n,
                     cs->lvl2_n, std::max<int64_t>(n, 1));
     HIPOK(take_launch_error());
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
     cs->max_written = maxv;
+    cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;  // no delta directory entry of the old slot mapping is trusted
     cs->prev_segs = false;
     cs->n_ub = n;
     cs->nd_ub = 0;

@@ -49,6 +49,12 @@ struct MaxLevels {
     int64_t idx_cap;                // capacity the levels were carved for: skey[L] = skey[0] + sum of
                                     // idx_level_cap(idx_cap, l < L), computable without indexing skey[]
     const int32_t* dir = nullptr;   // [65537] radix directory over skey[0] (base tier; k_directory)
+    // Directory slots (kernels.hip dir_slot): the 16 bits after the first dir_p bytes the loaded
+    // keys share (dir_phi, dir_plo: those bytes, the rest zero), so keys under one long common
+    // prefix (C4: 9 bytes) still spread over the slots; 0 = the first two bytes.  Fixed when the
+    // history is loaded; used by both tiers.
+    uint32_t dir_p = 0;
+    uint64_t dir_phi = 0, dir_plo = 0;
     uint64_t* edir = nullptr;       // [65537] delta tier's directory, entries (epoch << 32 | count),
     uint32_t edir_epoch = 0;        // filled by k_epilogue; lookups trust entries of this epoch (0: off)
 };

@@ -331,6 +331,29 @@ __device__ __forceinline__ uint32_t gmask(bool pred) {
     return (uint32_t)(m >> (threadIdx.x & 63 & ~(kArity - 1))) & ((1u << kArity) - 1u);
 }
 
+// Radix directory of the base tier (k_directory): its slot is the 16 bits after the first
+// m.dir_p bytes of a 16-byte prefix, bytes every base key shares (MaxLevels::dir_p).
+__host__ __device__ __forceinline__ uint32_t dir_bits(uint64_t hi, uint64_t lo, uint32_t p) {
+    if (p == 0) return (uint32_t)(hi >> 48);
+    if (p < 8) return (uint32_t)(((hi << (8 * p)) | (lo >> (64 - 8 * p))) >> 48);
+    return (uint32_t)((lo << (8 * (p - 8))) >> 48);
+}
+// Directory slot of a 16-byte prefix, monotone over all keys: with a shared prefix (dir_p > 0),
+// keys below it take slot 0, keys above it slot 0xffff, and keys under it their bits clamped to
+// [1, 0xfffe]; without one, the first two bytes.  Both tiers' directories (k_directory, the
+// epilogue's delta fill) and every lookup use it.
+__device__ __forceinline__ uint32_t dir_slot(const MaxLevels& m, uint64_t hi, uint64_t lo) {
+    const uint32_t p = m.dir_p;
+    if (p == 0) return (uint32_t)(hi >> 48);
+    const uint64_t mh = p >= 8 ? ~0ull : ~0ull << (64 - 8 * p);
+    const uint64_t ml = p <= 8 ? 0ull : ~0ull << (128 - 8 * p);
+    const uint64_t xh = hi & mh, xl = lo & ml;
+    if (xh != m.dir_phi || xl != m.dir_plo)
+        return (xh < m.dir_phi || (xh == m.dir_phi && xl < m.dir_plo)) ? 0u : 0xffffu;
+    const uint32_t v = dir_bits(hi, lo, p);
+    return v < 1u ? 1u : (v > 0xfffeu ? 0xfffeu : v);
+}
+
 // LONG: the long-key probes above (the batch has keys over 16 bytes); same result.
 template <bool LONG = false>
 __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
@@ -368,10 +391,10 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     const ulonglong2 e_top = m.skey[top][v_top ? gl : 0];
     bool direct = false;
     if (m.dir || m.edir_epoch) {
-        // radix directory: the level-0 samples sharing q's first two bytes are [dir[v], dir[v+1])
+        // radix directory: the level-0 samples sharing q's directory bits are [dir[v], dir[v+1])
         // (base: k_directory, exact; delta: k_epilogue's fill, entries of the current epoch only);
         // a slot of at most two groups is counted directly at level 0
-        const uint32_t dv = (uint32_t)(q.hi >> 48);
+        const uint32_t dv = dir_slot(m, q.hi, q.lo);
         int64_t d0, d1;
         bool have = true;
         if (m.dir) {
@@ -856,8 +879,9 @@ __device__ __forceinline__ void lane_sample_range(const MaxLevels& m, int64_t n,
     int64_t c = 0;      // level-0 samples whose prefix is below q
     bool bknown = false;  // the sample at c (if any) is known not to share q's prefix
     bool direct = false;
+    int64_t w0 = -1, w1 = -1;  // a directory slot too wide to count at level 0
     if (m.dir || m.edir_epoch) {
-        const uint32_t dv = (uint32_t)(q.hi >> 48);
+        const uint32_t dv = dir_slot(m, q.hi, q.lo);
         int64_t d0, d1;
         bool have = true;
         if (m.dir) {
@@ -877,10 +901,33 @@ __device__ __forceinline__ void lane_sample_range(const MaxLevels& m, int64_t n,
             c = d0 + k;
             // all of the slot below q: the next sample's first two bytes are greater
             bknown = k < cnt ? !eqn : true;
+        } else if (have && d1 <= sz[0]) {
+            w0 = d0;
+            w1 = d1;
         }
     }
     if (!direct) {
-        for (int64_t j0 = 0; j0 < sz[top]; j0 += kArity) {
+        // A wide slot (keys whose directory bits take few values: C4's decimal digits after the
+        // shared prefix) still bounds q: samples before w0 lie below it and from w1 on above it, so
+        // the descent starts at the lowest level whose entries over [w0, w1) fit one probe round
+        // (entry j of level L is sample j A^L) instead of at the top.
+        int lv = top;
+        bool started = false;
+        if (w0 >= 0) {
+            int64_t span = 1;
+            for (int L = 1; L < top; L++) {
+                span *= kArity;
+                const int64_t a = w0 / span, z = (w1 - 1) / span;
+                if (z - a + 1 <= kLaneProbe) {
+                    bool eqn;
+                    c = a + lane_count<kLaneProbe>(m.skey[L], a, (int)(z - a + 1), q, eqn);
+                    lv = L;
+                    started = true;
+                    break;
+                }
+            }
+        }
+        for (int64_t j0 = 0; !started && j0 < sz[top]; j0 += kArity) {
             const int cnt = (int)min((int64_t)kArity, sz[top] - j0);
             bool eqn;
             const int k = lane_count<kArity>(m.skey[top], j0, cnt, q, eqn);
@@ -888,7 +935,7 @@ __device__ __forceinline__ void lane_sample_range(const MaxLevels& m, int64_t n,
             c += k;
             if (k < cnt) break;
         }
-        for (int L = top; L > 0; L--) {
+        for (int L = lv; L > 0; L--) {
             if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
             const int64_t base = (int64_t)kArity * (c - 1) + 1;
             const int64_t end = min((int64_t)kArity * c, sz[L - 1]);
@@ -4148,10 +4195,10 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         }
         const int64_t b1l = b1_0 + lane;  // lane q < kEpiBlocks owns block b1_0 + q
         ulonglong2 sk = make_ulonglong2(0, 0);
-        uint64_t prev_hi = 0;  // the previous block's sampled key (delta directory fill)
+        ulonglong2 prev_k = make_ulonglong2(0, 0);  // the previous block's sampled key (delta directory fill)
         if (lane < kEpiBlocks && b1l < n1) {
             sk = m.keys[b1l * kFan];  // sampled key of the block
-            if (m.edir_epoch && b1l > 0) prev_hi = m.keys[(b1l - 1) * kFan].x;
+            if (m.edir_epoch && b1l > 0) prev_k = m.keys[(b1l - 1) * kFan];
         }
         // every 8th boundary of the wave's blocks (8 entries of skey8 per block)
         static_assert(kEpiBlocks * kFan / 8 <= 64, "one skey8 entry per lane");
@@ -4182,12 +4229,13 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
                 m.skey[0][off + d] = sk;
             }
             if (m.edir_epoch) {
-                // delta directory: slots (top16(previous sample), top16(this sample)] hold this
+                // delta directory: slots (dir_slot(previous sample), dir_slot(this sample)] hold this
                 // sample's index (the first sample not below them); the last sample also fills
                 // the slots above it with n1.  At most kDirRun slots per run: slots left over keep
                 // an older epoch and send their lookups down the tree.
                 const uint64_t tag = (uint64_t)m.edir_epoch << 32;
-                const int64_t a = b1l > 0 ? (int64_t)(prev_hi >> 48) : -1, c = (int64_t)(sk.x >> 48);
+                const int64_t a = b1l > 0 ? (int64_t)dir_slot(m, prev_k.x, prev_k.y) : -1,
+                              c = (int64_t)dir_slot(m, sk.x, sk.y);
                 for (int64_t v = a + 1; v <= c && v <= a + kDirRun; v++) m.edir[v] = tag | (uint64_t)b1l;
                 if (b1l == n1 - 1)
                     for (int64_t v = c + 1; v <= kDirSlots && v <= c + kDirRun; v++) m.edir[v] = tag | (uint64_t)n1;
@@ -4383,14 +4431,18 @@ static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
 // instead of descending the ~6 levels above it; slots crowded by shared key prefixes (subspaces,
 // hot ranges) take the tree.  Rebuilt with the base tier's index (compaction, GC, load), one
 // binary search per slot.
-__global__ __launch_bounds__(kBlock) void k_directory(const ulonglong2* keys, const int64_t* np, int32_t* dir) {
+// (slots by dir_slot: the bits after the loaded keys' shared prefix, when there is one)
+__global__ __launch_bounds__(kBlock) void k_directory(MaxLevels m, const int64_t* np) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v > kDirSlots) return;
+    const ulonglong2* keys = m.keys;
+    int32_t* dir = const_cast<int32_t*>(m.dir);
     const int64_t S = (*np + kFan - 1) / kFan;
     int64_t lo = 0, hi = S;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)(keys[mid * kFan].x >> 48) < v)
+        const ulonglong2 k = keys[mid * kFan];
+        if ((int64_t)dir_slot(m, k.x, k.y) < v)
             lo = mid + 1;
         else
             hi = mid;
@@ -4400,8 +4452,7 @@ __global__ __launch_bounds__(kBlock) void k_directory(const ulonglong2* keys, co
 
 static void launch_directory(hipStream_t s, const MaxLevels& m, const int64_t* n) {
     if (!m.dir) return;
-    fdb_launch(k_directory, dim3((kDirSlots + kBlock) / kBlock), dim3(kBlock), 0, s, m.keys, n,
-               const_cast<int32_t*>(m.dir));
+    fdb_launch(k_directory, dim3((kDirSlots + kBlock) / kBlock), dim3(kBlock), 0, s, m, n);
 }
 
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,

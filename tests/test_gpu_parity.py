@@ -301,6 +301,74 @@ def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split,
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
+@pytest.mark.parametrize("lanes", ["1", "0"])
+@pytest.mark.parametrize("dir_prefix,alphabet", [("1", "bytes"), ("1", "digits"), ("0", "digits")])
+def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_prefix, alphabet, lanes):
+    """The base tier's radix directory keyed on the 16 bits after the bytes every loaded key shares
+    (MaxLevels::dir_p; C4's 9-byte prefix): 120k boundaries under one 10-byte prefix, queries inside
+    it, below and above it at every depth, keys shorter than it and the empty key; writes outside
+    the prefix, which both tiers' directories file under their end slots (dir_slot), before and
+    after the compactions that bring them into the base.  alphabet "digits": the bytes after the prefix are
+    decimal digits (C4's user ids), so the directory bits take 100 values and its slots are too
+    wide to count directly: the per-lane descent starts below the top of the tree, bounded by the
+    slot.  dir_prefix "0": the first two bytes (FDBCS_DIR_PREFIX)."""
+    monkeypatch.setenv("FDBCS_DIR_PREFIX", dir_prefix)
+    monkeypatch.setenv("FDBCS_LONG_LANES", lanes)
+    rng = np.random.default_rng(77)
+    P = bytes([0x41, 0x42, 0x43, 0x44, 0x00, 0xff, 0x45, 0x46, 0x47, 0x48])
+    lo_b, hi_b = (0, 256) if alphabet == "bytes" else (0x30, 0x3a)
+
+    long_keys = [False]  # batches alternate: keys up to 21 bytes (short-key lookups), up to 30
+
+    def suffix(n):
+        return bytes(rng.integers(lo_b, hi_b, size=n).astype(np.uint8))
+
+    def inside():
+        top = 21 if long_keys[0] else 12
+        return P + suffix(int(rng.integers(0, top)))
+
+    def any_key(outside_share):
+        r = rng.random()
+        if r >= outside_share:
+            return inside()
+        d = int(rng.integers(0, len(P)))  # diverge at byte d, below or above, or stop short of P
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            return P[:d]
+        x = P[d] - 1 if kind == 1 else P[d] + 1
+        if not 0 <= x <= 255:
+            return P[:d]
+        return P[:d] + bytes([x]) + bytes(rng.integers(0, 256, size=int(rng.integers(0, 8))).astype(np.uint8))
+
+    hist = sorted({P + suffix(6) for _ in range(120000)})
+    kb = np.frombuffer(b"".join(hist), np.uint8)
+    ko = np.zeros(len(hist) + 1, np.int64)
+    np.cumsum([len(k) for k in hist], out=ko[1:])
+    vers = rng.integers(0, 1000, size=len(hist)).astype(np.int64)
+    e = EngineDriver(engine, gc_interval=0, delta_limit=1200)
+    o = oracle_mod.SkipListBaseline()
+    e.load_history(kb, ko, vers)
+    o.load_history(kb, ko, vers)
+    now = 1000
+    for i in range(8):
+        now += 10
+        long_keys[0] = i % 2 == 1
+        txns = []
+        for _ in range(400):
+            def rr(share):
+                a, b = any_key(share), any_key(share)
+                return KeyRange(min(a, b), max(a, b))
+
+            txns.append(CommitTransaction([rr(0.3) for _ in range(int(rng.integers(1, 4)))],
+                                          [rr(0.05 if i < 3 else 0.3) for _ in range(int(rng.integers(0, 3)))],
+                                          now - int(rng.integers(0, 600)), False))
+        pb = PackedBatch.from_transactions(txns)
+        ve, _ = e.detect(pb, now, 0)
+        vo, _ = o.detect(pb, now, 0)
+        assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
+    assert e.cs.stats()["compactions"] >= 2
+
+
 def test_c1_skiplisttest(engine, oracle_mod):
     seq = list(W.c1_batches(25, seed=7))
     e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
