@@ -234,10 +234,13 @@ struct fdbcs_conflict_set {
                               // even for batches with keys over 16 bytes (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
     bool directory = true;  // FDBCS_DIRECTORY=0: base-tier lookups descend the whole sample tree (A/B)
-    // Bytes every loaded key shares ahead of the directory's 16 bits (MaxLevels::dir_p; 0 with
-    // FDBCS_DIR_PREFIX=0): the load's common prefix, capped at 14.  Keys written later outside it
-    // take the directories' end slots (dir_slot), so the mapping stays monotone.
-    bool dir_prefix = true;
+    // Bytes every loaded key shares ahead of the directory's 16 bits (MaxLevels::dir_p, with
+    // FDBCS_DIR_PREFIX=1): the load's common prefix, capped at 14.  Keys written later outside it
+    // take the directories' end slots (dir_slot), so the mapping stays monotone.  Off by default:
+    // at C4 the bytes after the 9-byte prefix are decimal digits (100 slots of ~7.8k samples), and
+    // the tree levels the wide-slot start skips are cache hits: the base check isolated 57.5 ->
+    // 59.5 us with it, the pipeline within noise (scripts/gpu_r04_final2.sh).
+    bool dir_prefix = false;
     uint32_t dir_p = 0;
     uint64_t dir_phi = 0, dir_plo = 0;
     DBuf trace_buf;
@@ -1175,7 +1178,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_HELPER_Y")) cs->helper_y = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
-    if (const char* v = getenv("FDBCS_DIR_PREFIX")) cs->dir_prefix = v[0] != '0';
+    if (const char* v = getenv("FDBCS_DIR_PREFIX")) cs->dir_prefix = v[0] == '1';
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;

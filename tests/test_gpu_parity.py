@@ -311,7 +311,7 @@ def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_prefi
     after the compactions that bring them into the base.  alphabet "digits": the bytes after the prefix are
     decimal digits (C4's user ids), so the directory bits take 100 values and its slots are too
     wide to count directly: the per-lane descent starts below the top of the tree, bounded by the
-    slot.  dir_prefix "0": the first two bytes (FDBCS_DIR_PREFIX)."""
+    slot.  dir_prefix "0": the first two bytes (the default; FDBCS_DIR_PREFIX)."""
     monkeypatch.setenv("FDBCS_DIR_PREFIX", dir_prefix)
     monkeypatch.setenv("FDBCS_LONG_LANES", lanes)
     rng = np.random.default_rng(77)
