@@ -4,7 +4,7 @@ set -eu
 cd "$(dirname "$0")/.."
 T=${TAG:-r04g}
 O=gpurun_out/$T
-for w in c1 c2 c3 c4; do cp $O/prof_$w/rocprof_*.json profiles/; done  # (the 32768 profile keeps its summary only)
+for w in c1 c2 c3 c4 c2_32768; do cp $O/prof_$w/rocprof_*.json profiles/; done
 cp gpurun_out/pmc/pmc_*.json profiles/
 for w in c1 c2 c3 c4 c2_32768; do
   cp $O/prof_$w/summary.txt profiles/${T}_kernel_stats_$w.txt

@@ -8,6 +8,8 @@ cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 W=${WORKLOAD:-c2}
 case $W in c1) TX=2500; HI=0 ;; c4) TX=5000; HI=50000000 ;; *) TX=5000; HI=5000000 ;; esac
+# a --txns in BENCH_ARGS names the profile (rocprof_c2_32768_5000000.json for the 32768-txn batches)
+T2=$(echo " ${BENCH_ARGS:-} " | sed -n 's/.* --txns \([0-9]*\) .*/\1/p'); [ -n "$T2" ] && TX=$T2
 OUT=${OUT:-gpurun_out/prof_$W}
 mkdir -p "$OUT"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- \
