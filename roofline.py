@@ -81,6 +81,12 @@ def kernel_bytes(name: str, s: dict):
         return (2 * R * (D + look_d) + R * (4 + V) + R * V + T, "delta tier: 2R(D + lookup) + R(4+V) + RV + T")
     if name == "k_sample":
         return S * (D + I + 4), "S samples: key read, item written, rank"
+    if name == "k_quant_cold":
+        # kQuant (4096) quantiles: rank inverse of the S samples, each quantile's item read and its
+        # SplitKey (8 words, length, meta: 72 B) written
+        return S * 8 + 4096 * (I + 72), "cold start: sample ranks inverted, 4096 quantile items read and splitters written"
+    if name == "k_lvl3_reset":
+        return 8 * (N / (64.0 ** 3) + N / (64.0 ** 2) + 2), "range-max levels 2 and 3 of a tier reset before a rebuild"
     if name == "k_bucket_count":
         return E * (D + 2) + nb * (I + 4), "E keys read, E bucket ids written, splitters"
     if name == "k_bucket_scatter":
