@@ -1,0 +1,18 @@
+#!/bin/bash
+# k_sort_bucket at 16 waves per workgroup (the working tree) against 4 (libfdbcs_b256.so): the GPU
+# suite, isolated bucket-sort times at C2/C3/C4, and pipelined kernel tables and lines at C2 and C4.
+set -u
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out/bkt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/bkt/tests.log 2>&1 || { tail -30 gpurun_out/bkt/tests.log; exit 1; }
+tail -1 gpurun_out/bkt/tests.log
+for W in c2 c3; do
+  for L in b256 cur; do
+    lib=foundationdb_amd/variants/libfdbcs_$L.so; [ $L = cur ] && lib=foundationdb_amd/libfdbcs.so
+    FDBCS_LIB=$PWD/$lib WORKLOAD=$W WHICH=1,2 timeout -k 10 300 python3 scripts/kernel_sweep.py "$L" || exit 1
+  done
+done
+for W in c2 c4; do
+  WORKLOAD=$W ROUNDS=2 LIBS="b256:b256 b1024:cur" timeout -k 10 900 bash scripts/gpu_ab_lib.sh 2>&1 | grep -E "value|sort_bucket|sort_partition|check_lanes|seg_prep|epilogue<false>" || exit 1
+done
