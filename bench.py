@@ -96,6 +96,12 @@ def parse():
                     help="global batches routed (not resolved) to train the balancer before the run")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the verdict all-reduce (nccl = RCCL over xGMI)")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the multi-resolver path (process group, device routing of gathered shares, "
+                    "conflict-byte MAX all-reduce) even at world size 1: the RCCL leg on one GPU")
+    ap.add_argument("--too-old-frac", type=float, default=0.0,
+                    help="share of transactions whose snapshot sits at the MVCC window's edge (about half of "
+                    "them TooOld, SkipList.cpp:770)")
     return ap.parse_args()
 
 
@@ -107,18 +113,18 @@ def workload_params(args):
     from foundationdb_amd import workloads as W
 
     if args.workload == "c4":
-        return W.C4Params(txns=args.txns or 5000, history=args.history or 50_000_000)
+        return W.C4Params(txns=args.txns or 5000, history=args.history or 50_000_000, too_old_frac=args.too_old_frac)
     if args.workload == "c1":
         return W.C2Params(txns=args.txns or 2500, reads=1, writes=1, history=args.history or 0)
-    return W.C2Params(txns=args.txns or 5000, history=args.history or 5_000_000)
+    return W.C2Params(txns=args.txns or 5000, history=args.history or 5_000_000, too_old_frac=args.too_old_frac)
 
 
 def sharding_for(args, p, world):
     from foundationdb_amd import workloads as W
     from foundationdb_amd.sharding import KeyRangeSharding
 
-    if world == 1:
-        return None
+    if world == 1:  # one resolver (the --dist rehearsal of the multi-resolver path: it owns every key)
+        return KeyRangeSharding([]) if args.dist else None
     if args.workload == "c4":  # every key shares the subspace: split by user
         return KeyRangeSharding([W.c4_user_split(p, g * p.users // world) for g in range(1, world)])
     if args.workload == "c1":  # setK keys share 12 bytes of '.': split on the integer
@@ -241,9 +247,11 @@ def cpu_model():
     return cpu
 
 
-def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank, n_batches=None):
+def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank, n_batches=None, add_oldest=None):
     """Replay every batch in order on the CPU restatement (oracle/skiplist_baseline.cpp): compare
-    each GPU verdict vector and time the batches in `timed` (single thread, pinned to one core)."""
+    each GPU verdict vector and time the batches in `timed` (single thread, pinned to one core).
+    add_oldest[i]: the oldest version the engine's addTransaction saw for batch i (its TooOld test,
+    SkipList.cpp:770): a batch packed ahead of its predecessor's detect is replayed as added then."""
     from oracle import oracle
 
     oracle.build()
@@ -270,7 +278,7 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank, n_
         t = time.perf_counter()
         # the reference's removeBefore: bounded to 3|combined|+10 nodes, resumed at removalKey
         # (SkipList.cpp:880-889); verdict-neutral, so parity holds against the GPU's full GC
-        v, _ = sl.detect(b, now, no, gc="bounded")
+        v, _ = sl.detect(b, now, no, gc="bounded", add_oldest=(add_oldest or {}).get(i))
         dt = time.perf_counter() - t
         if i in timed:
             spent += dt
@@ -334,7 +342,7 @@ def main():
     dist = None
     ndev = max(1, torch.cuda.device_count())
     device = local % ndev  # one rank per GPU; more ranks than GPUs only for rehearsals (gloo)
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
 
         torch.cuda.set_device(device)
@@ -369,9 +377,10 @@ def main():
     # the shares are all-gathered over xGMI, and every resolver keeps its key range's part on the
     # device (fdbcs_batch_add_routed).  --reshard keeps the host routing of balancing.py (its
     # ownership history is not on the device): that path is a feature check, routed before timing.
-    droute = world > 1 and not args.reshard and cdev != "cpu"
+    multi = world > 1 or args.dist  # the multi-resolver path (one resolver of G, G >= 1)
+    droute = multi and not args.reshard and cdev != "cpu"
     sh = sharding_for(args, p, world)
-    all_routed, reshard = route_all(args, p, world, gbatches) if (world > 1 and not droute) else (None, None)
+    all_routed, reshard = route_all(args, p, world, gbatches) if (multi and not droute) else (None, None)
     route_cache = {}
 
     def routed_at(i):
@@ -383,7 +392,7 @@ def main():
         return route_cache[i]
 
     def mine_at(i):
-        return routed_at(i).batch if world > 1 else gbatches[i][0]
+        return routed_at(i).batch if multi else gbatches[i][0]
 
     log(f"[rank {rank}] generated history {len(vers)} + {n_all} batches in {time.time() - t0:.1f}s")
 
@@ -398,7 +407,7 @@ def main():
         return int(((t[t > 0] + 7) // 8 * 8).sum())
 
     # capacity: a resolver's batch is at most the global batch (device routing) or its host-routed part
-    sized = [pb for pb, _, _ in gbatches] if (world == 1 or droute) else [mine_at(i) for i in range(n_all)]
+    sized = [pb for pb, _, _ in gbatches] if (not multi or droute) else [mine_at(i) for i in range(n_all)]
     maxT = max(b.n_txn for b in sized)
     maxR = max(b.n_reads for b in sized)
     maxW = max(b.n_writes for b in sized)
@@ -472,6 +481,16 @@ def main():
         combined[i] = c
 
     host = {"add": 0.0, "submit": 0.0, "wait": 0.0}
+    # the oldest version the engine held when each batch was added (its TooOld test is made then,
+    # SkipList.cpp:770): batches packed ahead of their predecessors' detects are replayed that way
+    add_oldest = {}
+
+    def add_batch(i):
+        o = C.ConflictBatch(cs)
+        add_oldest[i] = cs.oldest_version
+        o.add_packed(mine_at(i))
+        attach(i, o)
+        return o
 
     def run(lo, hi, objs, window=WINDOW, lat=None):
         """Submit batches lo..hi-1 (objs: packed ConflictBatch objects — or, with device routing,
@@ -518,10 +537,8 @@ def main():
                     detect(*pending)
                     pending = None
                 continue
-            if objs is None:
-                o = C.ConflictBatch(cs)
-                o.add_packed(mine_at(i))
-                attach(i, o)
+            if objs is None:  # the Resolver's order: added after the previous batch's detect
+                o = add_batch(i)
             else:
                 o = objs[i]
             t1 = pc()
@@ -543,10 +560,7 @@ def main():
             if droute:  # the proxy's addTransaction: its share in the wire layout
                 objs[i] = pack_share(i)
                 continue
-            o = C.ConflictBatch(cs)
-            o.add_packed(mine_at(i))  # addTransaction: normalized into pinned staging, not uploaded
-            attach(i, o)
-            objs[i] = o
+            objs[i] = add_batch(i)  # addTransaction: normalized into pinned staging, not uploaded
         return objs
 
     def barrier():
@@ -624,12 +638,23 @@ def main():
         resident_elapsed = max_over_ranks(time.perf_counter() - t_start)
 
     total_elapsed = None
+    total_host = None
     if n_total > 0:  # the reference's "total": addTransaction inside the loop as well
+        for k in host:
+            host[k] = 0.0
+        cs.reset_stats()
         barrier()
         t_start = time.perf_counter()
         run(*spans["total"], None)
         barrier()
         total_elapsed = max_over_ranks(time.perf_counter() - t_start)
+        stt = cs.stats()
+        # where a batch's host time goes when addTransaction is in the loop (the calling thread):
+        # add = ConflictBatch + addTransaction of the packed batch (engine_add: inside
+        # fdbcs_batch_add_packed alone), submit = detect_async, wait = waiting for verdicts
+        total_host = {k: v / n_total * 1e3 for k, v in host.items()}
+        total_host["engine_add"] = stt["host_ms_add"] / max(1, stt["added_txns"]) * p.txns
+        total_host["elapsed"] = total_elapsed / n_total * 1e3
 
     sync = None
     if args.sync_steps > 0:
@@ -771,7 +796,8 @@ def main():
     parity = cpu_base = None
     if not args.no_cpu_baseline:
         timed = set(range(timed_lo, timed_hi))
-        parity, cpu_base = cpu_replay(args, kb, ko, vers, mine_at, gbatches, verdicts, timed, rank)
+        parity, cpu_base = cpu_replay(args, kb, ko, vers, mine_at, gbatches, verdicts, timed, rank,
+                                      add_oldest=add_oldest)
         if dist is not None:
             t = torch.tensor([parity["batches_checked"], parity["mismatched_batches"], parity["mismatched_txns"]],
                              dtype=torch.int64, device=cdev)
@@ -841,6 +867,7 @@ def main():
         },
         "conflict_ranges_per_s": granges / elapsed,
         "total_txns_per_s": ttxn / total_elapsed if total_elapsed else None,
+        "total_host_ms_per_batch": total_host,
         "device_resident_txns_per_s": pass_txns("resident") / resident_elapsed if resident_elapsed else None,
         "sync": sync,
         "sync_txns_per_s": sync["txns_per_s"] if sync else None,

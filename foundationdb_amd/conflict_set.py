@@ -94,6 +94,8 @@ class Stats(ctypes.Structure):
         ("routed_batches", ctypes.c_int64),
         ("ms_route_kernels", ctypes.c_double),
         ("host_ms_route", ctypes.c_double),
+        ("host_ms_add", ctypes.c_double),
+        ("added_txns", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -387,16 +389,18 @@ class ConflictBatch:
         )
         _check(rc, "addTransaction")
         self.transaction_count += 1
-        self._report.append(bool(tr.report_conflicting_keys))
-        self._has_reads.append(len(tr.read_conflict_ranges) > 0)
+        if self.conflicting_key_range_map is not None:
+            self._report.append(bool(tr.report_conflicting_keys))
+            self._has_reads.append(len(tr.read_conflict_ranges) > 0)
 
     def add_packed(self, pb: PackedBatch) -> None:
         """addTransaction for every transaction of a packed batch, in order."""
         cs = pb.c_struct()
         _check(load_library().fdbcs_batch_add_packed(self._h, ctypes.byref(cs)), "addTransaction(packed)")
         self.transaction_count += pb.n_txn
-        self._report.extend(bool(x) for x in pb.report)
-        self._has_reads.extend((np.diff(pb.read_offsets) > 0).tolist())
+        if self.conflicting_key_range_map is not None:  # per-transaction bookkeeping only for reports
+            self._report.extend(bool(x) for x in pb.report)
+            self._has_reads.extend((np.diff(pb.read_offsets) > 0).tolist())
 
     def upload(self) -> None:
         _check(load_library().fdbcs_batch_upload(self._h), "upload")

@@ -883,8 +883,18 @@ void materialize(fdbcs_batch* b) {
     b->direct = false;
 }
 
-// Has batch x's epilogue published its completion flag (null: destroyed, so done)?
+// Has batch x's epilogue published its completion flag (null: destroyed, so done)?  The flag
+// says the batch's results are final; workgroups of the epilogue other than the publishing one may
+// still be writing the delta index and zeroing workspace scratch, so it never stands alone for
+// "the launch is over" (stage_b_done).
 inline bool batch_done(const fdbcs_batch* x) { return !x || (x->h_flag && *x->h_flag == x->seq && x->seq != 0); }
+
+// May a dependency on workspace k's last stage B be skipped?  Only once that batch's flag was seen
+// (so its stage B was issued: ev_b[k]'s last record is its own) AND ev_b[k] has completed, i.e. the
+// whole epilogue launch is over.
+inline bool stage_b_done(fdbcs_conflict_set* cs, int k) {
+    return batch_done(cs->ws_user[k]) && hipEventQuery(cs->ev_b[k]) == hipSuccess;
+}
 
 // H2D of the packed batch by the DMA engine, issued now on `us` (the upload stream, or stage A's
 // stream when the phases are timed one after another); ev_up marks its completion.
@@ -1697,7 +1707,23 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     return FDBCS_OK;
 }
 
+static inline double host_ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+static int add_packed_impl(fdbcs_batch* b, const fdbcs_packed_batch* pb);
+
 int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = add_packed_impl(b, pb);
+    if (rc == FDBCS_OK && b->cs) {
+        b->cs->stats.host_ms_add += host_ms_since(t0);
+        b->cs->stats.added_txns += pb->n_txn;
+    }
+    return rc;
+}
+
+static int add_packed_impl(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     if (!b || !pb || pb->n_txn < 0) return FDBCS_E_INVALID;
     if (b->state != 0 || !b->cs) return FDBCS_E_STATE;
     const int32_t T = pb->n_txn;
@@ -2002,15 +2028,17 @@ static int finish_route(fdbcs_batch* b) {
     RouteResult r;
     memcpy(&r, (const void*)sl->rt_res.p, sizeof(r));
     if (r.error != 0) {
-        if (r.error == 2) {  // the shares never arrived: nothing was placed, the batch can be routed again
-            fprintf(stderr, "fdbcs: routed batch: the shares' ready flag was never set\n");
-            b->routed = b->route_pending = false;
-            b->out_dev = nullptr;
-            b->out_n = 0;
-            b->state = 0;
-            return FDBCS_E_TIMEOUT;
-        }
-        return r.error == 1 ? FDBCS_E_NOMEM : r.error == 3 ? FDBCS_E_INVALID : FDBCS_E_DEVICE;
+        // 2: the shares never arrived; 1: the routed part exceeds the capacities given; 3: n_global
+        // differs from the shares' transaction count.  Whatever the routing kernels placed is
+        // unusable either way: the batch goes back to the empty state, so it can be routed again
+        // (with corrected arguments) or destroyed, never detected half-routed.
+        if (r.error == 2) fprintf(stderr, "fdbcs: routed batch: the shares' ready flag was never set\n");
+        b->routed = b->route_pending = false;
+        b->out_dev = nullptr;
+        b->out_n = 0;
+        b->state = 0;
+        return r.error == 2 ? FDBCS_E_TIMEOUT
+                            : r.error == 1 ? FDBCS_E_NOMEM : r.error == 3 ? FDBCS_E_INVALID : FDBCS_E_DEVICE;
     }
     b->rT = r.T;
     b->rR = r.R;
@@ -2050,9 +2078,6 @@ int fdbcs_batch_upload(fdbcs_batch* b) {
     return do_upload(b, b->cs->ustream);
 }
 
-static inline double host_ms_since(std::chrono::steady_clock::time_point t0) {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-}
 
 int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_version) {
     if (!b) return FDBCS_E_INVALID;
@@ -2186,7 +2211,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // ev_b[wp] is recorded by every batch's stage B, whatever its stream layout, so the query is
     // never answered by a stale or never-recorded event (a timing-level change with batches in
     // flight included).
-    const bool ws_busy = cs->wused[wp] && (threaded || !batch_done(cs->ws_user[wp]));
+    const bool ws_busy = cs->wused[wp] && (threaded || !stage_b_done(cs, wp));
     if (ws_busy && (sa != s || cs->y_async[wp])) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sa);
     // and the check after that batch may still read its union segments and their tails
     if (cs->xfree_rec[wp] && sa != s && (threaded || !batch_done(cs->xfree_user[wp])))
@@ -2295,7 +2320,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // previous batch's segments), or of the previous batch (it compacted, or nothing pending).
         // Only a Y on ystream needs the event (a timing-level change may switch layouts mid-flight).
         const int wy = use_prev ? cs->prev2_wp : cs->last_wp;
-        if (wy >= 0 && cs->y_async[wy] && (threaded || !batch_done(cs->ws_user[wy])))
+        if (wy >= 0 && cs->y_async[wy] && (threaded || !stage_b_done(cs, wy)))
             fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
     }
     const bool graphs = cs->stage_graphs && timing != 2;
@@ -2389,7 +2414,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
                     compact ? base_hint : nd_after + 1, &sc->ndb[dnew], sort_nb, sort_samples);
     fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], ys);
     // (no event marks the slot free: a slot returns to the pool only from fdbcs_batch_destroy,
-    // after the batch's completion flag was seen or its streams were synchronized)
+    // after the batch's completion flag was seen or its streams were synchronized; every kernel
+    // of the batch that reads the slot precedes the epilogue's publishing workgroup, which reads
+    // the slot's flags before it publishes)
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
         fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, ys);
         cs->cmp_recorded = true;

@@ -4263,7 +4263,11 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         if (ep.flags[t] & kFlagTooOld) return 1;  // TransactionTooOld (ConflictSet.h:42)
         return ep.status[t] == kCommitted ? 2 : 0;
     };
-    for (int64_t t = tid; t < ep.T; t += stride) ep.verdict_dev[t] = verdict(t);
+    // The device verdicts read the batch's flags from its slot: workgroup 0 writes them before it
+    // publishes the flag, so once the host has seen the flag no workgroup still reads the slot (a
+    // destroyed batch's slot returns to the pool on the flag alone).
+    if (blockIdx.x == 0)
+        for (int64_t t = threadIdx.x; t < ep.T; t += blockDim.x) ep.verdict_dev[t] = verdict(t);
     for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
     for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
     for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
@@ -4279,8 +4283,10 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiZero);
     if (blockIdx.x != 0) return;
     // Workgroup 0 writes the scalars the host reads next to the verdicts (which k_resolve already
-    // wrote to the host-mapped buffer), then publishes the batch's sequence number; everything
-    // else this launch writes is read only by later kernels on the same stream.  Wave 0 holds the
+    // wrote to the host-mapped buffer), then publishes the batch's sequence number.  Other
+    // workgroups may still be writing levels, index and zeroed scratch when the flag lands: the
+    // flag tells the host the batch's results are final, never that this launch is over (the
+    // engine's cross-stream dependency checks query the ev_b event for that).  Wave 0 holds the
     // prefetched words (lane i: Scalars word i, lane 32 + i: BatchScalars word i) and writes the
     // host copy one word per lane, with the roll-over applied.
     if (wid == 0) {

@@ -111,6 +111,10 @@ class C2Params:
     version_step: int = 1000  # versions between batches
     window: int = 5_000_000  # MAX_WRITE_TRANSACTION_LIFE_VERSIONS (fdbserver/Knobs.cpp:41)
     staleness: int = 100_000  # snapshot = now - U[0, staleness)
+    # share of transactions whose snapshot sits at the MVCC window's edge, now - window +
+    # U[-2 step, 2 step): about half of them are TooOld (SkipList.cpp:770) once the oldest version
+    # follows now - window (Resolver.actor.cpp:194)
+    too_old_frac: float = 0.0
     range_write_frac: float = 0.5  # fraction of writes that are short ranges (rest single-key)
 
 
@@ -133,6 +137,18 @@ def c2_history(p: C2Params, seed: int, start_version: int):
     return kb, ko, vers
 
 
+def window_edge_snapshots(p, rng: np.random.Generator, now: int, snap: np.ndarray) -> np.ndarray:
+    """p.too_old_frac of the snapshots moved to the window's edge (no draws when it is 0, so the
+    default workloads' streams are unchanged)."""
+    if p.too_old_frac <= 0:
+        return snap
+    T = len(snap)
+    edge = rng.random(T) < p.too_old_frac
+    snap = snap.copy()
+    snap[edge] = now - p.window + rng.integers(-2 * p.version_step, 2 * p.version_step, size=int(edge.sum()))
+    return snap
+
+
 def c2_batch(p: C2Params, rng: np.random.Generator, now: int) -> PackedBatch:
     T, nr, nw = p.txns, p.reads, p.writes
     R, W = T * nr, T * nw
@@ -152,7 +168,7 @@ def c2_batch(p: C2Params, rng: np.random.Generator, now: int) -> PackedBatch:
     mat[2 * R + 1 :: 2] = we
     lens = np.full(2 * (R + W), 16, np.int64)
     lens[2 * R + 1 :: 2] = wlen
-    snap = now - rng.integers(0, p.staleness, size=T)
+    snap = window_edge_snapshots(p, rng, now, now - rng.integers(0, p.staleness, size=T))
     return PackedBatch.from_key_matrix(
         snap, np.arange(T + 1, dtype=np.int32) * nr, np.arange(T + 1, dtype=np.int32) * nw, mat, lens
     )
@@ -203,7 +219,7 @@ def c3_batch(p: C2Params, rng: np.random.Generator, now: int, zipf: ZipfGenerato
     mat[2 * R + 1 :: 2, :16] = wk
     lens = np.full(2 * (R + W), 16, np.int64)
     lens[1::2] = 17  # every range is singleKeyRange(k) = [k, k\0)
-    snap = now - rng.integers(0, p.staleness, size=T)
+    snap = window_edge_snapshots(p, rng, now, now - rng.integers(0, p.staleness, size=T))
     return PackedBatch.from_key_matrix(
         snap, np.arange(T + 1, dtype=np.int32) * nr, np.arange(T + 1, dtype=np.int32) * nw, mat, lens
     )
@@ -262,6 +278,7 @@ class C4Params:
     version_step: int = 1000
     window: int = 5_000_000
     staleness: int = 100_000
+    too_old_frac: float = 0.0  # as C2Params.too_old_frac
     subspace: bytes = b"\x15\x2a"  # tuple-encoded int 42
 
     @property
@@ -406,7 +423,7 @@ def c4_batch(p: C4Params, rng: np.random.Generator, now: int) -> PackedBatch:
     wide[0:R:nr] = True  # each transaction's first read covers the whole user
     kind = np.tile(np.array([0, 1], np.int64), R + W) + 2 * np.repeat(wide, 2)
     mat, lens = c4_keys(p, np.repeat(user, 2), np.repeat(item, 2), kind)
-    snap = now - rng.integers(0, p.staleness, size=T)
+    snap = window_edge_snapshots(p, rng, now, now - rng.integers(0, p.staleness, size=T))
     return PackedBatch.from_key_matrix(
         snap, np.arange(T + 1, dtype=np.int32) * nr, np.arange(T + 1, dtype=np.int32) * nw, mat, lens
     )

@@ -131,6 +131,10 @@ typedef struct fdbcs_stats {
     int64_t routed_batches;
     double ms_route_kernels;
     double host_ms_route;
+    /* addTransaction of whole batches (fdbcs_batch_add_packed): host time inside the
+     * calls (validation, normalization into pinned staging) and the calls' transactions. */
+    double host_ms_add;
+    int64_t added_txns;
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */
@@ -239,7 +243,8 @@ int fdbcs_batch_set_conflict_output(fdbcs_batch* b, const int32_t* txn_ids, int3
  *     reports are not collected for routed batches.  Detect and wait as for any batch; detect
  *     blocks until the routing kernels have run (issue the next batch's routing first).  The wait
  *     for the ready flag is bounded by FDBCS_ROUTE_TIMEOUT_MS (default 60000): past it detect
- *     returns FDBCS_E_TIMEOUT and the batch is empty again, to be routed anew.
+ *     returns FDBCS_E_TIMEOUT and the batch is empty again, to be routed anew.  The capacity
+ *     (FDBCS_E_NOMEM) and n_global (FDBCS_E_INVALID) errors leave it empty the same way.
  *   fdbcs_batch_routed_info: the routed batch's sizes and device views of its global -> batch
  *     transaction map (int32[n_shares * max_share_txns], -1 where not routed) and of each kept
  *     read's index in its transaction (txReadConflictRangeIndexMap, :144-165). */

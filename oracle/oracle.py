@@ -111,12 +111,20 @@ class _CSBase:
         vv = np.ascontiguousarray(versions, np.int64)
         self._fn["load_history"](self._h, len(vv), _p(kb), _p(ko), _p(vv), header_version)
 
-    def detect(self, pb, now: int, new_oldest: int, gc=True):
+    def detect(self, pb, now: int, new_oldest: int, gc=True, add_oldest=None):
         """Returns (verdicts uint8[T], conflicting: dict txn -> sorted list of read indices).
 
         gc: False = no removeBefore; True = a full removeBefore pass (history size comparable with
         the GPU engine after its full GC); "bounded" = the reference's bounded, resumable
-        removeBefore (SkipList.cpp:880-889; the skip-list restatement only)."""
+        removeBefore (SkipList.cpp:880-889; the skip-list restatement only).
+        add_oldest: the oldestVersion the batch's addTransaction saw when the caller added it
+        before the previous batch's detect (SkipList.cpp:770 reads it at add); None = added right
+        before this detect, as the Resolver does (Resolver.actor.cpp:179-194)."""
+        if add_oldest is not None:
+            f = getattr(self._L, self._prefix + "set_add_oldest")
+            f.restype = None
+            f.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+            f(self._h, int(add_oldest))
         T = pb.n_txn
         verdicts = np.zeros(T, np.uint8)
         cap = max(1, pb.n_reads)

@@ -51,6 +51,7 @@ struct OracleSet {
     std::map<Key, int64_t, KeyLess> history;  // boundary -> version of its segment
     int64_t headerVersion = 0;                // SkipList(Version) header, SkipList.cpp:398-404
     int64_t oldestVersion = 0;                // ConflictSet::oldestVersion, SkipList.cpp:731-736
+    int64_t addOldest = INT64_MIN;            // oldestVersion the next batch's add saw (one-shot; see slb)
     // The last batch's TransactionInfo::tooOld flags and transactionConflictStatus, from which
     // oracle_last_lists restates the verdict-list loop (SkipList.cpp:869-876).
     std::vector<char> lastTooOld, lastStatus;
@@ -122,6 +123,7 @@ void oracle_set_oldest(void* p, int64_t v) {
     if (v > cs->oldestVersion) cs->oldestVersion = v;
 }
 int64_t oracle_oldest(void* p) { return static_cast<OracleSet*>(p)->oldestVersion; }
+void oracle_set_add_oldest(void* p, int64_t v) { static_cast<OracleSet*>(p)->addOldest = v; }
 int64_t oracle_history_size(void* p) { return (int64_t) static_cast<OracleSet*>(p)->history.size(); }
 
 void oracle_load_history(void* p, int64_t n, const uint8_t* bytes, const int64_t* offs, const int64_t* vers,
@@ -161,6 +163,9 @@ int64_t oracle_dump_history(void* p, uint8_t* bytes, int64_t bytes_cap, int64_t*
 // GC is verdict-neutral).
 int64_t oracle_detect(void* p, const fdbcs_packed_batch* pb, int64_t now, int64_t newOldest, uint8_t* verdicts,
                       int32_t* conf_off, int32_t* conf_idx, int64_t cap, int gc) {
+    const int64_t addOldest = static_cast<OracleSet*>(p)->addOldest != INT64_MIN ? static_cast<OracleSet*>(p)->addOldest
+                                                                                 : static_cast<OracleSet*>(p)->oldestVersion;
+    static_cast<OracleSet*>(p)->addOldest = INT64_MIN;
     OracleSet* cs = static_cast<OracleSet*>(p);
     const int T = pb->n_txn;
     const int R = pb->read_offsets[T];
@@ -179,7 +184,7 @@ int64_t oracle_detect(void* p, const fdbcs_packed_batch* pb, int64_t now, int64_
         int r0 = pb->read_offsets[t], r1 = pb->read_offsets[t + 1];
         int w0 = pb->write_offsets[t], w1 = pb->write_offsets[t + 1];
         ti.report = pb->report_conflicting_keys ? pb->report_conflicting_keys[t] != 0 : false;
-        if (pb->read_snapshot[t] < cs->oldestVersion && r1 > r0) {  // SkipList.cpp:770
+        if (pb->read_snapshot[t] < addOldest && r1 > r0) {  // SkipList.cpp:770
             ti.tooOld = true;
             continue;
         }

@@ -497,6 +497,10 @@ struct ConflictSet {
     SkipSet list;
     std::string removal_key;  // ConflictSet::removalKey (:735)
     int64_t oldest = 0;
+    // The oldest version the next batch's addTransaction saw, when the caller added it before the
+    // previous batch's detect (a ConflictBatch reads cs->oldestVersion at add, SkipList.cpp:770);
+    // INT64_MIN: added right before its detect, as the Resolver does.  One-shot.
+    int64_t add_oldest = INT64_MIN;
     double last[8] = {};  // seconds of the last detect: add, sort, check, intra, combine, merge, gc, total
 };
 
@@ -528,6 +532,7 @@ void slb_set_oldest(void* p, int64_t v) {
     if (v > cs->oldest) cs->oldest = v;
 }
 int64_t slb_oldest(void* p) { return ((ConflictSet*)p)->oldest; }
+void slb_set_add_oldest(void* p, int64_t v) { ((ConflictSet*)p)->add_oldest = v; }
 int64_t slb_history_size(void* p) { return ((ConflictSet*)p)->list.count; }
 void slb_last_times(void* p, double* out) { memcpy(out, ((ConflictSet*)p)->last, sizeof(double) * 8); }
 
@@ -558,6 +563,9 @@ void slb_load_history(void* p, int64_t n, const uint8_t* bytes, const int64_t* o
 // ConflictBatch: addTransaction for every transaction (:763-794), then detectConflicts (:844-890).
 int64_t slb_detect(void* p, const fdbcs_packed_batch* pb, int64_t now, int64_t newOldest, uint8_t* verdicts,
                    int32_t* conf_off, int32_t* conf_idx, int64_t cap, int gc) {
+    const int64_t add_oldest = ((ConflictSet*)p)->add_oldest != INT64_MIN ? ((ConflictSet*)p)->add_oldest
+                                                                           : ((ConflictSet*)p)->oldest;
+    ((ConflictSet*)p)->add_oldest = INT64_MIN;
     ConflictSet* cs = (ConflictSet*)p;
     SkipSet& sl = cs->list;
     const double t0 = now_s();
@@ -579,7 +587,7 @@ int64_t slb_detect(void* p, const fdbcs_packed_batch* pb, int64_t now, int64_t n
         const int r0 = pb->read_offsets[t], r1 = pb->read_offsets[t + 1];
         const int w0 = pb->write_offsets[t], w1 = pb->write_offsets[t + 1];
         report[t] = pb->report_conflicting_keys ? pb->report_conflicting_keys[t] : 0;
-        if (pb->read_snapshot[t] < cs->oldest && r1 > r0) {  // :770
+        if (pb->read_snapshot[t] < add_oldest && r1 > r0) {  // :770
             too_old[t] = 1;
             continue;
         }

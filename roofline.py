@@ -1,6 +1,8 @@
 """Algorithmic bytes per launch of every pipeline kernel, for the bench roofline.
 
-The model prices the work the kernel must do, not this implementation's traffic: `achieved` GB/s
+The model prices the work the kernel must do, at element granularity (no sector, line or
+memory-side-atomic rounding: those are this implementation's traffic, which PMC measures), not
+this implementation's traffic: `achieved` GB/s
 is these bytes divided by the kernel's measured average launch time (HIP events around the
 kernel on the stream it runs on), and `frac` = achieved / 8 TB/s (MI355X HBM3E,
 /opt/skills/guides/MI355X_MICROARCH.md).  PMC counters (scripts/gpu_pmc.sh) give the bytes a
@@ -94,30 +96,29 @@ def kernel_bytes(name: str, s: dict):
     if name.startswith("k_bucket_sort"):
         return 2 * I * E, "one read and one write of every 32-byte item"
     if name == "k_sort_partition":
-        # the slot and class-count atomics execute at the memory side (1 + 1/2 per endpoint): PMC
-        # counts ~32 bytes each beyond the item traffic (profiles/pmc_c2_*: 4.1 MB for 105k atomics);
-        # keys over 16 bytes: the first tail word of every endpoint (a 64-byte sector) and the write
-        # keys' tails copied for the next batch's check
+        # E·(D + I) -- every endpoint's key record read once and its sort item
+        # written once.  Keys over 16 bytes add their tail bytes (read once).  The slot atomics and
+        # the write keys' tail copy are this implementation's traffic (PMC `traffic`), not the model.
         tl = s.get("tail_bytes", 0.0)
-        lk = s.get("long_share", 0.0)
-        return (E * (D + I) + 1.5 * E * 32 + nb * 16 + lk * E * 64 + 2 * tl * W / max(1.0, R + W),
-                "E keys read, E 32-byte items written to their bucket slabs; 1.5 memory-side atomics per endpoint "
-                "(~32 bytes each); long keys: a tail sector per endpoint, the write keys' tails copied")
+        return (E * (D + I) + tl,
+                "SURVEY 8(d): E(D + I), every endpoint's key record read and its item written once; + tail bytes of "
+                "keys over 16 B")
     if name.startswith("k_sort_bucket"):
-        # pos[p] is a scattered 4-byte store: one 64-byte line written per endpoint; keys over 16 bytes
-        # read their sort window past the bucket's common prefix from the tail (a 64-byte sector)
-        lk = s.get("long_share", 0.0)
-        return (E * (I + 64 + 4 + 12) + G * 4 + nb * 16 + lk * E * 64,
-                "E slab items read; meta and 3 class prefixes written by position, pos[] by endpoint (a scattered "
-                "store: a 64-byte line each); R+W begin lists; long keys: a tail sector per endpoint")
+        # SURVEY §8(d) intra term: one sort pass = 2·E·(P + 8) (every endpoint's prefix and its
+        # 8-byte length/class/owner word read and written once).  Scattered stores, sectors and
+        # lines are `traffic`, not algorithmic bytes.
+        tl = s.get("tail_bytes", 0.0)
+        return (2 * E * (P + 8) + tl,
+                "SURVEY 8(d): one sort pass 2E(P + 8), every endpoint's prefix and 8-byte word read and written once; "
+                "+ tail bytes of keys over 16 B")
     if name.startswith("k_scan<3, fdbcs::PosScan"):
         return E * (4 + 4 + 4 + 12) + G * 4, "E metas read; pos, pmeta, 3 class prefixes written; R+W begin lists"
     if name.startswith("k_scan<3, fdbcs::EdgePairScan"):
-        # the class prefixes at a range's two sorted positions are six scattered 4-byte gathers: a
-        # 32-byte sector each; writes also place their sorted endpoint records and keys for D.Combine
-        return (G * (8 + 6 * 32 + 8) + W * (2 * 8 + 2 * D + 8),
-                "per range: 2 positions, 3 class prefixes at both (scattered gathers, 32-byte sectors), slot/pair "
-                "offsets; per write its two sorted endpoint records and keys, group lead and owner")
+        # per range its two sorted positions, the three 4-byte class prefixes at both, its slot / pair
+        # offsets; writes also place their sorted endpoint records and keys for D.Combine
+        return (G * (8 + 6 * 4 + 8) + W * (2 * 8 + 2 * D + 8),
+                "per range: 2 positions, 3 class prefixes at both (6 x 4 B), slot/pair offsets; per write its two "
+                "sorted endpoint records and keys, group lead and owner")
     if name == "k_edge_fill":
         return X * (4 + 4 + 4 + 4) + G * 8, "per edge: partner, owner, slot atomic, edge; range offsets"
     if name == "k_resolve_pre":
@@ -156,13 +157,13 @@ def kernel_bytes(name: str, s: dict):
     if name.startswith("k_epilogue"):
         # the levels and sample index of the tier that changed: the delta after a merge
         # (k_epilogue<false>), the whole base after a compaction (k_epilogue<true>); per boundary its
-        # version, and per 8 boundaries the 128-byte line (gfx950) holding the sampled key plus the
-        # skey8 entry written
+        # version read, per 8 boundaries the sampled key read and its skey8 entry written, per 64 the
+        # level-1 maximum and the level-0 sample key written
         n = N if name.startswith("k_epilogue<true") or Nd <= 0 else Nd
-        return (n * (V + 128 / 8 + P / 8) + T * 2 + R * 6,
+        return (n * (V + 2 * P / 8 + (V + P) / 64) + T * 2 + R * 6,
                 "levels and sample index of the changed tier (the delta after a merge; the base after a compaction, "
-                "k_epilogue<true>): versions, one 128-byte key line and one skey8 entry per 8 boundaries; verdicts; "
-                "re-zeroed flags and edge counts")
+                "k_epilogue<true>): versions, per 8 boundaries a sampled key read and its skey8 entry written, per 64 "
+                "the level-1 max and sample key; verdicts; re-zeroed flags and edge counts")
     if name == "k_directory":
         return 65537 * (4 + 17 * P), "65537 slots: binary search over level-0 samples"
     if name == "k_conflict_output":

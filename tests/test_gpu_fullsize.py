@@ -84,6 +84,85 @@ def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
     cs.close()
 
 
+@pytest.mark.parametrize("order", ["resolver", "ahead"])
+def test_full_c2_too_old_at_window_edge(engine, oracle_mod, order):
+    """TooOld at full size: C2 over the 5M-boundary history with 2 % of the
+    snapshots at the MVCC window's edge (now - 5e6 +- 2 batches), the oldest version following
+    now - 5e6 every batch (Resolver.actor.cpp:194).  resolver: each batch added after the previous
+    batch's detect_async returned (Resolver.actor.cpp:179-194), so its TooOld test sees the oldest
+    that detect left (SkipList.cpp:770, 880-882); ahead: all batches added before the first detect
+    (bench.py's timed pass), replayed with the oldest each add saw.  Exact either way, with many
+    TooOld verdicts; the TooOld transactions' writes never reach the history (:779-790)."""
+    p = W.C2Params(too_old_frac=0.02)
+    start = 10_000_000
+    kb, ko, vers = W.c2_history(p, seed=3, start_version=start)
+    rng = np.random.default_rng(103)
+    seq, now = [], start
+    for _ in range(24):
+        now += p.version_step
+        seq.append((W.c2_batch(p, rng, now), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    got, add_oldest = {}, {}
+    if order == "resolver":
+        pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
+    else:
+        objs = []
+        for i, (pb, _, _) in enumerate(seq):
+            b = engine.ConflictBatch(cs)
+            add_oldest[i] = cs.oldest_version
+            b.add_packed(pb)
+            objs.append(b)
+        inflight = []
+        for i, (b, (_, now_, no_)) in enumerate(zip(objs, seq)):
+            b.detect_async(now_, no_)
+            inflight.append((i, b))
+            if len(inflight) > WINDOW:
+                j, bj = inflight.pop(0)
+                got[j] = bj.wait()
+                bj.close()
+        for j, bj in inflight:
+            got[j] = bj.wait()
+            bj.close()
+    sl = oracle_mod.SkipListBaseline()
+    sl.load_history(kb, ko, vers)
+    too_old = 0
+    for i, (pb, now_, no_) in enumerate(seq):
+        v, _ = sl.detect(pb, now_, no_, gc="bounded", add_oldest=add_oldest.get(i))
+        bad = np.nonzero(got[i] != v)[0]
+        assert len(bad) == 0, (i, bad[:10], got[i][bad[:10]], v[bad[:10]])
+        too_old += int((v == 1).sum())
+    # ~2 % of 120k transactions sit at the edge, about half of them below it
+    assert too_old > (300 if order == "resolver" else 50), too_old
+    cs.close()
+
+
+def test_flag_before_epilogue_end_without_submit_thread(engine, oracle_mod, monkeypatch):
+    """the completion flag is published by the epilogue's first workgroup while
+    the others may still build levels and zero workspace scratch.  Without the helper thread the
+    host's dependency checks may skip an event wait once the flag is seen; they must also find the
+    epilogue's event complete.  Window 3 with three workspaces: each wait is followed at once by the
+    detect that reuses the waited batch's workspace, and every second batch compacts and runs
+    removeBefore over a 2M-boundary base (a whole-base epilogue of thousands of workgroups)."""
+    monkeypatch.setenv("FDBCS_SUBMIT_THREAD", "0")
+    p = W.C2Params(history=2_000_000, txns=2000, too_old_frac=0.01)
+    start = 10_000_000
+    kb, ko, vers = W.c2_history(p, seed=4, start_version=start)
+    rng = np.random.default_rng(104)
+    seq, now = [], start
+    for _ in range(30):
+        now += p.version_step
+        seq.append((W.c2_batch(p, rng, now), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    cs.set_gc_interval(2)
+    got = {}
+    pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v), window=2)
+    assert cs.stats()["compactions"] >= 10
+    check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
+    cs.close()
+
+
 @pytest.mark.parametrize("mode", ["default", "lag_split"])
 def test_async_pipeline_full_c3(engine, oracle_mod, monkeypatch, mode):
     """C3 at full size: Zipf(0.99) hot keys, 5000 txns per batch over the 5M-boundary history,

@@ -212,3 +212,81 @@ def test_pipelined_device_routing_eight_resolvers(engine, G, workload):
     assert saw_too_old > 0 and too_old_window > 0
     for cs in sets:
         cs.close()
+
+
+def test_routed_batch_errors_leave_it_empty_and_reroutable(engine, monkeypatch):
+    """fdbcs_batch_add_routed's error paths: a ready flag that is never set times out
+    (FDBCS_E_TIMEOUT after FDBCS_ROUTE_TIMEOUT_MS), and n_global differing from the shares'
+    transaction count fails (FDBCS_E_INVALID); either way the batch is empty again, and routing it
+    anew with correct arguments detects exactly like the host routing's restatement."""
+    import numpy as np
+    import torch
+
+    from foundationdb_amd import workloads as W
+    from foundationdb_amd.sharding import KeyRangeSharding
+    from oracle import oracle as O
+
+    O.build()
+    monkeypatch.setenv("FDBCS_ROUTE_TIMEOUT_MS", "50")
+    cs = engine.ConflictSet(0)
+    ora = O.OracleConflictSet()
+    rng = np.random.default_rng(77)
+    Tshare = 100
+    pb = W.random_small_batch(rng, Tshare, alphabet=6, max_len=3, now=10, staleness=12)
+    dev, stride = _route_and_gather(engine, torch, np, pb, 1, Tshare)
+    tail = int(np.maximum(np.diff(pb.key_offsets) - 16, 0).sum())
+    caps = (pb.n_txn, pb.n_reads, pb.n_writes, tail)
+    out = torch.zeros(pb.n_txn, dtype=torch.uint8, device="cuda")
+    never = torch.zeros(1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    b = engine.ConflictBatch(cs)
+    # 1. the shares' ready flag is never set: bounded wait, then FDBCS_E_TIMEOUT
+    b.add_routed(dev.data_ptr(), stride, 1, Tshare, None, None, caps, out.data_ptr(), pb.n_txn, never.data_ptr(), 5)
+    with pytest.raises(engine.FdbcsError) as e:
+        b.routed_info()
+    assert e.value.status == engine.FDBCS_E_TIMEOUT
+    # 2. n_global differs from the shares' transaction count: FDBCS_E_INVALID, batch empty again
+    b.add_routed(dev.data_ptr(), stride, 1, Tshare, None, None, caps, out.data_ptr(), pb.n_txn + 3)
+    with pytest.raises(engine.FdbcsError) as e:
+        b.routed_info()
+    assert e.value.status == engine.FDBCS_E_INVALID
+    # 3. routed anew, correctly: the same verdicts as the restatement
+    b.add_routed(dev.data_ptr(), stride, 1, Tshare, None, None, caps, out.data_ptr(), pb.n_txn)
+    b.detect_async(10, 1)
+    got = b.wait()
+    b.close()
+    route = KeyRangeSharding([]).route(pb)[0]  # one resolver: transactions with at least one range
+    want, _ = ora.detect(route.batch, 10, 1)
+    np.testing.assert_array_equal(got, want)
+    ref = np.zeros(pb.n_txn, np.uint8)
+    ref[route.txn_ids] = 2 - want.astype(np.uint8)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    cs.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("workload", ["c2", "c3"])
+def test_rccl_leg_one_rank(engine, workload):
+    """C5's RCCL leg executed on one MI355X: torchrun with one rank and the
+    nccl backend (RCCL), --dist forcing the multi-resolver path at world size 1 -- the proxy's
+    share packed, H2D, all_gather_into_tensor over RCCL, the ready-flag hand-off from torch's HIP
+    runtime to the engine's, fdbcs_batch_add_routed on the device, the device conflict bytes and
+    their uint8 all_reduce(MAX) over RCCL (CommitProxyServer.actor.cpp:764-780).  Parity against
+    the restatement fed the same routing, the device combine against host-built bytes."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--dist", "--backend", "nccl", "--workload", workload, "--steps", "12", "--warmup", "2",
+           "--txns", "2000", "--history", "300000", "--resident-steps", "0", "--total-steps", "4",
+           "--breakdown-steps", "0", "--profile-steps", "4", "--sync-steps", "4", "--hold-steps", "0",
+           "--too-old-frac", "0.05", "--cpu-seconds", "30"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    d = out["distributed"]
+    assert d["world_size"] == 1 and d["backend"] == "nccl" and d["rccl_version"]
+    assert d["routing"].startswith("device")
+    assert "RCCL" in out["combine_check"]["path"] and out["combine_check"]["mismatched"] == 0
+    assert out["combine_check"]["batches"] >= 12
+    # warmup 2 + profile 4 + timed 12 + total 4 + sync 4, every batch routed on the device
+    assert out["parity"]["batches_checked"] >= 26 and out["parity"]["mismatched_batches"] == 0
+    assert out["verdict_mix"]["too_old"] > 0

@@ -260,3 +260,22 @@ def test_verdict_lists_follow_reference_loop(oracle_built):
             assert sorted(nc2 + to + np.flatnonzero(v == 0).tolist()) == list(range(len(v)))
             saw_too_old += len(to)
     assert saw_too_old > 10
+
+
+@pytest.mark.parametrize("impl", ["OracleConflictSet", "SkipListBaseline"])
+def test_add_before_previous_detect(oracle_built, impl):
+    """A batch added before the previous batch's detect sees the oldest version from before that
+    detect (ConflictBatch::addTransaction reads cs->oldestVersion, SkipList.cpp:770, 880-882): the
+    `add_oldest` replay of bench.py's pre-packed batches.  Both restatements agree."""
+    tr = lambda snap: CommitTransaction([KeyRange(b"a", b"b")], [KeyRange(b"c", b"d")], snap)  # noqa: E731
+    pb = PackedBatch.from_transactions([tr(5), tr(15), tr(25)])
+    cs = getattr(oracle_built, impl)()
+    cs.detect(PackedBatch.from_transactions([]), 30, 20)  # oldest 0 -> 20
+    v, _ = cs.detect(pb, 40, 20)  # added after: snapshots 5 and 15 are TooOld
+    assert v.tolist() == [1, 1, 2]
+    cs2 = getattr(oracle_built, impl)()
+    cs2.detect(PackedBatch.from_transactions([]), 30, 20)
+    v, _ = cs2.detect(pb, 40, 20, add_oldest=10)  # added while the oldest was 10: only snapshot 5
+    assert v.tolist() == [1, 2, 2]
+    v, _ = cs2.detect(pb, 50, 20)  # one-shot: the next batch sees the current oldest (20) again
+    assert v.tolist()[:2] == [1, 1]

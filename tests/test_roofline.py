@@ -27,8 +27,9 @@ def test_every_ranked_kernel_has_a_model():
 def test_epilogue_priced_on_the_tier_it_rebuilds():
     per_batch, _ = roofline.kernel_bytes("k_epilogue<false>", SHAPE)
     whole, _ = roofline.kernel_bytes("k_epilogue<true>", SHAPE)
-    # versions (8 B), a 128-byte key line and a 16-byte skey8 entry per 8 boundaries of the tier
-    per_boundary = 8 + 128 / 8 + 16 / 8
+    # versions (8 B), a sampled key read and its skey8 entry written per 8 boundaries, the level-1
+    # max and level-0 sample per 64 (element bytes: no line rounding)
+    per_boundary = 8 + 2 * 16 / 8 + (8 + 16) / 64
     fixed = SHAPE["T"] * 2 + SHAPE["R"] * 6
     assert abs(per_batch - (SHAPE["Nd"] * per_boundary + fixed)) < 1e-6
     assert abs(whole - (SHAPE["N"] * per_boundary + fixed)) < 1e-6
@@ -46,3 +47,11 @@ def test_profiles_of_another_build_are_refused(tmp_path):
     assert kern is None and "measured build" in note
     traffic, note = roofline.pmc_traffic(str(tmp_path), "c2", "k_sort_bucket<false>", 5000, 5000000, measured)
     assert traffic is None and note.startswith("no pmc_")
+
+
+def test_sort_priced_by_survey_8d():
+    """one sort pass is 2E(P + 8); the partition E(D + I) -- no sector or atomic terms."""
+    b, model = roofline.kernel_bytes("k_sort_bucket<false>", SHAPE)
+    assert b == 2 * SHAPE["E"] * (16 + 8) and "8(d)" in model
+    b, model = roofline.kernel_bytes("k_sort_partition", SHAPE)
+    assert b == SHAPE["E"] * (24 + 32) and "8(d)" in model
