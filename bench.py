@@ -883,6 +883,9 @@ def main():
         "amortized_ms_per_batch": amortized,
         "verdict_mix": mix,
         "compactions": st["compactions"],
+        # batch-order launches (k_resolve, k_combine, k_intra_report) left out of the timed batches'
+        # X halves: the host had seen their stage A find no candidate edge
+        "x_launches_skipped": st["x_launches_skipped"],
         "kernels": table,
         "sort_phase": roofline.sort_phase(table),
         "roofline": roof,

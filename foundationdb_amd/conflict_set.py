@@ -96,6 +96,7 @@ class Stats(ctypes.Structure):
         ("host_ms_route", ctypes.c_double),
         ("host_ms_add", ctypes.c_double),
         ("added_txns", ctypes.c_int64),
+        ("x_launches_skipped", ctypes.c_int64),
     ]
 
     def as_dict(self):

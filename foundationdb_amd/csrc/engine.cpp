@@ -17,6 +17,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <string>
@@ -79,13 +80,15 @@ struct HBuf {
     void* p = nullptr;
     void* dp = nullptr;  // device view (mapped buffers)
     size_t cap = 0;
-    int ensure(size_t bytes, bool mapped = false) {
+    int ensure(size_t bytes, bool mapped = false, bool noncoherent = false) {
         if (bytes <= cap) return FDBCS_OK;
         size_t want = align_up(std::max(bytes, cap + cap / 2), 4096);
         if (p) HIPOK(hipHostFree(p));
         p = dp = nullptr;
         cap = 0;
-        HIPOK(hipHostMalloc(&p, want, mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault));
+        const unsigned fl = !mapped ? hipHostMallocDefault
+                                    : (hipHostMallocMapped | (noncoherent ? hipHostMallocNonCoherent : hipHostMallocCoherent));
+        HIPOK(hipHostMalloc(&p, want, fl));
         if (mapped) HIPOK(hipHostGetDevicePointer(&dp, p, 0));
         cap = want;
         return FDBCS_OK;
@@ -114,6 +117,93 @@ constexpr int kWsTileSlot = 54, kWsArenaSlot = 55;
 // workspace is reused every third batch.
 constexpr int kNumWork = 3;
 constexpr int kGcEveryCompactions = 4;  // removeBefore cadence of size-triggered compactions
+
+// Host threads for addTransaction of whole batches (fdbcs_batch_add_packed): the endpoint keys'
+// validation and normalization into pinned staging split over chunks of transactions.  The
+// calling thread works too.  A ticket carries the job's generation, so a worker that wakes late
+// never takes a ticket of a later job with the earlier job's function.  Between jobs a worker
+// spins for ~kSpinUs before sleeping on the condition variable: a resolver adds a batch every
+// ~0.1 ms, and a wake-up through the condition variable costs ~10-20 us (scripts/add_sweep.py).
+struct AddPool {
+    static constexpr int kSpinUs = 300;
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::atomic<uint64_t> ticket{0};  // generation << 32 | next ticket
+    std::atomic<int> done{0};         // tickets finished in the current generation
+    std::atomic<uint32_t> gen{0};
+    std::atomic<int> sleepers{0};
+    int n = 0;
+    const std::function<void(int)>* job = nullptr;
+    bool stop = false;
+
+    explicit AddPool(int workers) {
+        for (int i = 0; i < workers; i++) th.emplace_back([this] { worker(); });
+    }
+    ~AddPool() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+            gen.fetch_add(1);
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+    void run(uint32_t g, int nn, const std::function<void(int)>* fn) {
+        uint64_t cur = ticket.load(std::memory_order_acquire);
+        for (;;) {
+            if ((uint32_t)(cur >> 32) != g || (int)(cur & 0xffffffffu) >= nn) return;
+            if (ticket.compare_exchange_weak(cur, cur + 1, std::memory_order_acq_rel)) {
+                (*fn)((int)(cur & 0xffffffffu));
+                done.fetch_add(1, std::memory_order_acq_rel);
+                cur = ticket.load(std::memory_order_acquire);
+            }
+        }
+    }
+    void worker() {
+        uint32_t seen = 0;
+        for (;;) {
+            // spin a while for the next job, then sleep
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen.load(std::memory_order_acquire) == seen &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs))
+                __builtin_ia32_pause();
+            uint32_t g;
+            int nn;
+            const std::function<void(int)>* fn;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                if (gen.load(std::memory_order_relaxed) == seen && !stop) {
+                    sleepers.fetch_add(1);
+                    cv.wait(lk, [&] { return stop || gen.load(std::memory_order_relaxed) != seen; });
+                    sleepers.fetch_sub(1);
+                }
+                if (stop) return;
+                seen = g = gen.load(std::memory_order_relaxed);
+                nn = n;
+                fn = job;
+            }
+            run(g, nn, fn);
+        }
+    }
+    // fn(c) for c in [0, tickets), in ticket order across the workers and the calling thread;
+    // returns when all are done.
+    void parallel_for(int tickets, const std::function<void(int)>& fn) {
+        uint32_t g;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            g = gen.load(std::memory_order_relaxed) + 1;
+            n = tickets;
+            job = &fn;
+            done.store(0, std::memory_order_relaxed);
+            ticket.store((uint64_t)g << 32, std::memory_order_release);
+            gen.store(g, std::memory_order_release);
+        }
+        if (sleepers.load(std::memory_order_acquire) > 0) cv.notify_all();
+        run(g, tickets, &fn);
+        while (done.load(std::memory_order_acquire) < tickets) __builtin_ia32_pause();
+    }
+};
 
 struct fdbcs_conflict_set {
     int device = 0;
@@ -254,6 +344,8 @@ struct fdbcs_conflict_set {
     std::vector<KProf> kprof;
     const void* timed_func = nullptr;  // fdbcs_set_timed_kernel
     HBuf hold;                         // fdbcs_debug_hold: host-mapped release word of the hold kernels
+    HBuf hedge;                        // per workspace {batch seq, any candidate edge} (Work::hedge)
+    bool skip_edges = true;            // FDBCS_SKIP_EDGES=0: always issue the kGroupEdges launches
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
     // FDBCS_GRAPH=2: stage graphs.  The launches of each stage (A on its stream, B on the batch-order
@@ -286,6 +378,11 @@ struct fdbcs_conflict_set {
     // check of batch i waits (host side) until stage B of batch i-1 is issued, because it may wait
     // on that stage's compaction event; stage B of batch i waits for the helper to go idle.
     bool submit_thread = true;
+    // addTransaction threads (FDBCS_ADD_THREADS, workers besides the calling thread; 0 = serial)
+    int add_threads = 5;
+    AddPool* add_pool = nullptr;
+    double add_prof[4] = {0, 0, 0, 0};  // FDBCS_ADD_PROFILE: ms in add's serial pass, slot, count, fill
+    int64_t add_prof_n = 0;
     std::thread worker;
     std::mutex wmu;
     std::condition_variable wcv;
@@ -787,6 +884,16 @@ void release_slot(BatchSlot* sl) {
     delete sl;
 }
 
+// Pinned staging of batches (pin_in): host-coherent mapped memory by default; FDBCS_PIN_IN=nc maps
+// it non-coherent (A/B of the addTransaction write rate into it).
+static bool pin_in_noncoherent() {
+    static const bool nc = [] {
+        const char* v = getenv("FDBCS_PIN_IN");
+        return v && v[0] == 'n';
+    }();
+    return nc;
+}
+
 // Layout of a batch in pin_in / dev: [keys | rowner | wowner | snap | roff | woff | flags | tail].
 // add_packed normalizes keys, owners and tails in place; the tail region is last so a capacity
 // sized for an upper bound of the tail bytes costs no upload.
@@ -904,7 +1011,7 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     const size_t T = b->T(), R = b->R(), W = b->W();
     const UploadLayout L = upload_layout(T, R, W, b->tail_size());
     int rc;
-    if (!b->direct && (rc = sl->pin_in.ensure(L.total, true))) return rc;
+    if (!b->direct && (rc = sl->pin_in.ensure(L.total, true, pin_in_noncoherent()))) return rc;
     if ((rc = ensure_slot(sl, L.total, T, R))) return rc;
     char* h = (char*)sl->pin_in.p;
     if (!b->direct) {  // add_transaction path: normalized keys are in the pageable vectors
@@ -1124,12 +1231,25 @@ void worker_stop(fdbcs_conflict_set* cs) {
     cs->worker.join();
 }
 
+// The skip groups of batch b's X half at its replay: the kGroupEdges launches are left out once
+// b's stage A has completed (ev_a) and its edge scan told the host (Work::hedge) that b has no
+// candidate edge; otherwise (stage A still running, or not tracked) everything is issued.
+uint8_t x_skip(fdbcs_conflict_set* cs, const fdbcs_batch* b) {
+    if (!b || !cs->skip_edges || !cs->hedge.p) return 0;
+    const volatile uint32_t* h = (const volatile uint32_t*)((char*)cs->hedge.p + 64 * b->wp);
+    if (h[0] != b->seq) return 0;  // (cheap test first: no runtime call when the scan is not done)
+    if (hipEventQuery(cs->ev_a[b->wp]) != hipSuccess) return 0;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return h[1] == 0u ? kGroupEdges : 0;
+}
+
 int flush_pending(fdbcs_conflict_set* cs) {
     if (int rc = worker_wait(cs)) return rc;  // stage A / check of the pending batch issued
     if (!cs->pending_batch) return FDBCS_OK;
+    const uint8_t skip = x_skip(cs, cs->pending_batch);
     cs->pending_batch = nullptr;
     int rc = FDBCS_OK;
-    if (cs->pending_b.replay(cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
+    if (cs->pending_b.replay(cs->stream, skip, &cs->stats.x_launches_skipped) != hipSuccess) rc = FDBCS_E_DEVICE;
     cs->x_issued.fetch_add(1, std::memory_order_release);
     if (cs->pending_y.replay(cs->pending_ys) != hipSuccess) rc = FDBCS_E_DEVICE;
     cs->b_issued.fetch_add(1, std::memory_order_release);
@@ -1179,6 +1299,8 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
+    if (const char* v = getenv("FDBCS_ADD_THREADS")) cs->add_threads = std::max(0, std::min(64, atoi(v)));
+    if (const char* v = getenv("FDBCS_SKIP_EDGES")) cs->skip_edges = v[0] != '0';
     if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2' ? 1 : (v[0] == '3' ? 2 : 0);
     if (const char* v = getenv("FDBCS_GRAPH_RING")) cs->graph_ring = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
@@ -1236,6 +1358,11 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
     if (!rc) rc = ensure_btail(cs, 0);
     if (!rc && cs->trace) rc = cs->trace_buf.ensure(8 * kTrSlots);
+    if (!rc && cs->skip_edges) rc = cs->hedge.ensure(64 * kNumWork, true);
+    if (!rc && cs->skip_edges) {
+        memset(cs->hedge.p, 0, 64 * kNumWork);
+        for (int k = 0; k < kNumWork; k++) cs->work[k].hedge = (uint32_t*)((char*)cs->hedge.dp + 64 * k);
+    }
     if (rc) {
         fdbcs_destroy_conflict_set(cs);
         return rc;
@@ -1249,6 +1376,12 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     (void)hipSetDevice(cs->device);
     (void)flush_pending(cs);
     worker_stop(cs);
+    if (getenv("FDBCS_ADD_PROFILE") && cs->add_prof_n)
+        fprintf(stderr, "fdbcs add profile (%d threads, ms per batch over %lld): serial %.4f slot %.4f count %.4f fill %.4f\n",
+                cs->add_threads, (long long)cs->add_prof_n, cs->add_prof[0] / cs->add_prof_n,
+                cs->add_prof[1] / cs->add_prof_n, cs->add_prof[2] / cs->add_prof_n, cs->add_prof[3] / cs->add_prof_n);
+    delete cs->add_pool;
+    cs->add_pool = nullptr;
     if (cs->ustream) (void)hipStreamSynchronize(cs->ustream);
     if (cs->cstream) (void)hipStreamSynchronize(cs->cstream);
     if (cs->astream) (void)hipStreamSynchronize(cs->astream);
@@ -1277,6 +1410,7 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->quant.release();
     cs->trace_buf.release();
     cs->hold.release();
+    cs->hedge.release();
     for (BatchSlot* sl : cs->pool) release_slot(sl);
     cs->pool.clear();
     for (auto& kv : cs->stage_cache) {
@@ -1627,23 +1761,43 @@ int fdbcs_batch_add_transaction(fdbcs_batch* b, int64_t read_snapshot, int repor
     return FDBCS_OK;
 }
 
-// addTransaction of a whole (validated) packed batch into an empty batch: the endpoint keys are
-// normalized straight into the batch's pinned staging (no per-range vectors, no copy at upload).
+// begin <= end of one range (KeyRangeRef, FDBTypes.h:288-291) from the normalized prefixes, the
+// tails only when both prefixes tie and both keys run past 16 bytes (SkipList.cpp:53-60 order).
+static inline bool range_inverted(const DKey& a, const DKey& b, const uint8_t* ka, const uint8_t* kb) {
+    if (a.hi != b.hi) return a.hi > b.hi;
+    if (a.lo != b.lo) return a.lo > b.lo;
+    if (a.len <= 16 || b.len <= 16) return a.len > b.len;  // the shorter is a prefix of the longer
+    return cmp_bytes(ka + 16, (int32_t)a.len - 16, kb + 16, (int32_t)b.len - 16) > 0;
+}
+
+static inline void normalize_key(const uint8_t* p, uint32_t len, DKey* out) {
+    fast_prefix(p, len, &out->hi, &out->lo);
+    out->len = len;
+    out->tail = 0;
+}
+
+// addTransaction of a whole packed batch into an empty batch (offsets already checked monotone):
+// the endpoint keys are validated and normalized straight into the batch's pinned staging, in
+// chunks of transactions over the conflict set's add threads (AddPool), with no per-range
+// vectors and no copy at upload.  All-or-nothing: an inverted range leaves the batch empty.
 static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
+    fdbcs_conflict_set* cs = b->cs;
     const int32_t T = pb->n_txn;
-    const int64_t oldest = b->cs->oldest;
+    const int64_t oldest = cs->oldest;
+    using clk = std::chrono::steady_clock;
+    const auto tp0 = clk::now();
     b->snap.assign(pb->read_snapshot, pb->read_snapshot + T);
     b->flags.resize(T);
     b->roff.resize(T + 1);
     b->woff.resize(T + 1);
-    int32_t Ra = 0, Wa = 0;
+    int32_t Ra = 0, Wa = 0, n_report = 0;
     for (int32_t t = 0; t < T; t++) {
         const int32_t nr = pb->read_offsets[t + 1] - pb->read_offsets[t];
         const int32_t nw = pb->write_offsets[t + 1] - pb->write_offsets[t];
         uint8_t fl = (pb->report_conflicting_keys && pb->report_conflicting_keys[t] && b->report_enabled)
                          ? kFlagReport
                          : 0;
-        b->n_report += fl ? 1 : 0;
+        n_report += fl ? 1 : 0;
         const bool too_old = pb->read_snapshot[t] < oldest && nr > 0;  // SkipList.cpp:770
         if (too_old) fl |= kFlagTooOld;
         b->flags[t] = fl;
@@ -1656,54 +1810,150 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     }
     b->roff[T] = Ra;
     b->woff[T] = Wa;
-    const int64_t nk = 2 * ((int64_t)pb->read_offsets[T] + pb->write_offsets[T]);
+    const int32_t R = pb->read_offsets[T];
+    const int64_t nk = 2 * ((int64_t)R + pb->write_offsets[T]);
     const size_t tail_bound = nk ? (size_t)(pb->key_offsets[nk] - pb->key_offsets[0]) : 0;
     const UploadLayout L = upload_layout(T, Ra, Wa, tail_bound);
-    if (int rc = b->slot->pin_in.ensure(L.total, true)) return rc;
+    auto fail = [&](int rc) {
+        b->snap.clear();
+        b->flags.clear();
+        b->roff.assign(1, 0);
+        b->woff.assign(1, 0);
+        return rc;
+    };
+    const auto tp1 = clk::now();
+    if (int rc = b->slot->pin_in.ensure(L.total, true, pin_in_noncoherent())) return fail(rc);
+    if (int rc = ensure_slot(b->slot, L.total, T, Ra)) return fail(rc);
+    const auto tp2 = clk::now();
     char* h = (char*)b->slot->pin_in.p;
     DKey* keys = (DKey*)(h + L.keys);
+    DKey* wk = keys + 2 * (size_t)Ra;
     int32_t* rown = (int32_t*)(h + L.rown);
     int32_t* wown = (int32_t*)(h + L.wown);
     uint8_t* tail = (uint8_t*)(h + L.tail);
-    size_t tb = 0;
-    auto put = [&](DKey* out, int64_t k) {
-        const uint8_t* p = pb->key_bytes + pb->key_offsets[k];
-        const uint32_t len = (uint32_t)(pb->key_offsets[k + 1] - pb->key_offsets[k]);
-        fast_prefix(p, len, &out->hi, &out->lo);
-        out->len = len;
-        out->tail = 0;
-        if ((int32_t)len > b->max_len) b->max_len = (int32_t)len;
-        if (len > 16) {
-            out->tail = (uint32_t)tb;
-            memcpy(tail + tb, p + 16, len - 16);
-            tb += len - 16;
-        }
+    const uint8_t* kb = pb->key_bytes;
+    const int64_t* ko = pb->key_offsets;
+    // chunks of ~512 ranges; one chunk (no pool) for small batches
+    const int64_t G = (int64_t)R + pb->write_offsets[T];
+    const int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>(256, G / 512));
+    struct Chunk {
+        int32_t t0, t1;
+        int64_t tails, wtail;
+        int32_t max_len;
+        bool bad;
     };
-    if (int rc = ensure_slot(b->slot, L.total, T, Ra)) return rc;
-    const int32_t R = pb->read_offsets[T];
-    DKey* wk = keys + 2 * (size_t)Ra;
-    for (int32_t t = 0; t < T; t++) {
-        if (b->flags[t] & kFlagTooOld) continue;
-        const int32_t ra = b->roff[t], wa = b->woff[t];
-        for (int32_t r = pb->read_offsets[t], i = 0; r < pb->read_offsets[t + 1]; r++, i++) {
-            put(keys + 2 * (size_t)(ra + i), 2 * (int64_t)r);
-            put(keys + 2 * (size_t)(ra + i) + 1, 2 * (int64_t)r + 1);
-            rown[ra + i] = t;
-        }
-        for (int32_t w = pb->write_offsets[t], i = 0; w < pb->write_offsets[t + 1]; w++, i++) {
-            put(wk + 2 * (size_t)(wa + i), 2 * ((int64_t)R + w));
-            put(wk + 2 * (size_t)(wa + i) + 1, 2 * ((int64_t)R + w) + 1);
-            b->wtail += padded_tail((int32_t)wk[2 * (size_t)(wa + i)].len) +
-                        padded_tail((int32_t)wk[2 * (size_t)(wa + i) + 1].len);
-            wown[wa + i] = t;
-        }
+    std::vector<Chunk> ch(nchunk);
+    for (int c = 0; c < nchunk; c++) {
+        ch[c] = Chunk{(int32_t)((int64_t)T * c / nchunk), (int32_t)((int64_t)T * (c + 1) / nchunk), 0, 0, 0, false};
     }
+    const bool pooled = nchunk > 1 && cs->add_threads > 0;
+    if (pooled && !cs->add_pool) cs->add_pool = new (std::nothrow) AddPool(cs->add_threads);
+    // pass 1 (tickets [0, nchunk)): tail bytes of each chunk's admitted keys (key offsets only), so
+    // the tails pack exactly in transaction order; pass 2 (tickets [nchunk, 2 nchunk)) waits for
+    // every count (tickets go out in order, so every count is held by a running thread)
+    std::atomic<int> counted{0};
+    const std::function<void(int)> count = [&](int c) {
+        Chunk& k = ch[c];
+        int64_t tb = 0;
+        for (int32_t t = k.t0; t < k.t1; t++) {
+            if (b->flags[t] & kFlagTooOld) continue;
+            const int64_t r0 = 2 * (int64_t)pb->read_offsets[t], r1 = 2 * (int64_t)pb->read_offsets[t + 1];
+            const int64_t w0 = 2 * ((int64_t)R + pb->write_offsets[t]), w1 = 2 * ((int64_t)R + pb->write_offsets[t + 1]);
+            for (int64_t q = r0; q < r1; q++) tb += std::max<int64_t>(0, ko[q + 1] - ko[q] - 16);
+            for (int64_t q = w0; q < w1; q++) tb += std::max<int64_t>(0, ko[q + 1] - ko[q] - 16);
+        }
+        k.tails = tb;
+        counted.fetch_add(1, std::memory_order_release);
+    };
+    const auto tp3 = clk::now();
+    // pass 2: every range validated (TooOld transactions' too: KeyRangeRef asserts begin <= end
+    // whatever the batch does with it), admitted ones normalized with their owners and tails
+    const std::function<void(int)> fill = [&](int c) {
+        Chunk& k = ch[c];
+        while (counted.load(std::memory_order_acquire) < nchunk) __builtin_ia32_pause();
+        int64_t tb = 0, wt = 0;
+        for (int q = 0; q < c; q++) tb += ch[q].tails;
+        int32_t ml = 0;
+        bool bad = false;
+        auto put = [&](DKey* out, int64_t q) {
+            const uint8_t* p = kb + ko[q];
+            const uint32_t len = (uint32_t)(ko[q + 1] - ko[q]);
+            normalize_key(p, len, out);
+            if ((int32_t)len > ml) ml = (int32_t)len;
+            if (len > 16) {
+                out->tail = (uint32_t)tb;
+                memcpy(tail + tb, p + 16, len - 16);
+                tb += len - 16;
+            }
+        };
+        for (int32_t t = k.t0; t < k.t1 && !bad; t++) {
+            const int32_t r0 = pb->read_offsets[t], r1 = pb->read_offsets[t + 1];
+            const int32_t w0 = pb->write_offsets[t], w1 = pb->write_offsets[t + 1];
+            if (b->flags[t] & kFlagTooOld) {
+                auto check = [&](int64_t q) {
+                    DKey x, y;
+                    normalize_key(kb + ko[q], (uint32_t)(ko[q + 1] - ko[q]), &x);
+                    normalize_key(kb + ko[q + 1], (uint32_t)(ko[q + 2] - ko[q + 1]), &y);
+                    bad |= range_inverted(x, y, kb + ko[q], kb + ko[q + 1]);
+                };
+                for (int32_t r = r0; r < r1; r++) check(2 * (int64_t)r);
+                for (int32_t w = w0; w < w1; w++) check(2 * ((int64_t)R + w));
+                continue;
+            }
+            const int32_t ra = b->roff[t], wa = b->woff[t];
+            for (int32_t r = r0, i = 0; r < r1; r++, i++) {
+                DKey* o = keys + 2 * (size_t)(ra + i);
+                put(o, 2 * (int64_t)r);
+                put(o + 1, 2 * (int64_t)r + 1);
+                bad |= range_inverted(o[0], o[1], kb + ko[2 * (int64_t)r], kb + ko[2 * (int64_t)r + 1]);
+                rown[ra + i] = t;
+            }
+            for (int32_t w = w0, i = 0; w < w1; w++, i++) {
+                DKey* o = wk + 2 * (size_t)(wa + i);
+                const int64_t q = 2 * ((int64_t)R + w);
+                put(o, q);
+                put(o + 1, q + 1);
+                bad |= range_inverted(o[0], o[1], kb + ko[q], kb + ko[q + 1]);
+                wt += padded_tail((int32_t)(ko[q + 1] - ko[q])) + padded_tail((int32_t)(ko[q + 2] - ko[q + 1]));
+                wown[wa + i] = t;
+            }
+        }
+        k.wtail = wt;
+        k.max_len = ml;
+        k.bad = bad;
+    };
+    const std::function<void(int)> both = [&](int q) { q < nchunk ? count(q) : fill(q - nchunk); };
+    if (pooled && cs->add_pool)
+        cs->add_pool->parallel_for(2 * nchunk, both);
+    else
+        for (int q = 0; q < 2 * nchunk; q++) both(q);
+    int64_t tb_total = 0;
+    for (int c = 0; c < nchunk; c++) tb_total += ch[c].tails;
+    const auto tp4 = clk::now();
+    {
+        auto ms = [](clk::time_point a, clk::time_point b_) { return std::chrono::duration<double, std::milli>(b_ - a).count(); };
+        cs->add_prof[0] += ms(tp0, tp1);
+        cs->add_prof[1] += ms(tp1, tp2);
+        cs->add_prof[2] += ms(tp2, tp3);  // (nothing: count and fill run as one job)
+        cs->add_prof[3] += ms(tp3, tp4);
+        cs->add_prof_n++;
+    }
+    int64_t wtail = 0;
+    int32_t max_len = b->max_len;
+    for (const Chunk& k : ch) {
+        if (k.bad) return fail(FDBCS_E_INVALID);
+        wtail += k.wtail;
+        max_len = std::max(max_len, k.max_len);
+    }
+    b->wtail += wtail;
+    b->max_len = max_len;
+    b->n_report += n_report;
     b->direct = true;
     b->d_keys = L.keys;
     b->d_rown = L.rown;
     b->d_wown = L.wown;
     b->d_tail = L.tail;
-    b->d_tail_bytes = tb;
+    b->d_tail_bytes = (size_t)tb_total;
     return FDBCS_OK;
 }
 
@@ -1732,18 +1982,20 @@ static int add_packed_impl(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
     const int32_t R = pb->read_offsets[T];
     const int64_t nk = 2 * ((int64_t)R + pb->write_offsets[T]);
     if (nk && !pb->key_bytes) return FDBCS_E_INVALID;
-    // validate everything first (all-or-nothing)
+    // validate everything first (all-or-nothing): offsets here, ranges below (fused with the
+    // normalization on the direct path)
     for (int32_t t = 0; t < T; t++)
         if (pb->read_offsets[t + 1] < pb->read_offsets[t] || pb->write_offsets[t + 1] < pb->write_offsets[t])
             return FDBCS_E_INVALID;
+    for (int64_t k = 0; k < nk; k++)
+        if (pb->key_offsets[k + 1] < pb->key_offsets[k]) return FDBCS_E_INVALID;
+    if (b->T() == 0 && !b->direct) return add_packed_direct(b, pb);
     for (int64_t k = 0; k < nk; k += 2) {
         const int64_t a0 = pb->key_offsets[k], a1 = pb->key_offsets[k + 1], a2 = pb->key_offsets[k + 2];
-        if (a1 < a0 || a2 < a1) return FDBCS_E_INVALID;
         if (cmp_bytes(pb->key_bytes + a0, (int32_t)(a1 - a0), pb->key_bytes + a1, (int32_t)(a2 - a1)) > 0)
             return FDBCS_E_INVALID;
     }
     const int64_t oldest = b->cs->oldest;
-    if (b->T() == 0 && !b->direct) return add_packed_direct(b, pb);
     materialize(b);
     b->snap.reserve(b->snap.size() + T);
     for (int32_t t = 0; t < T; t++) {
@@ -2297,6 +2549,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     mark(kPhSort);
     if (cs->validate) launch_validate_sort(sa, bd, w);
+    w.hseq = b->seq;  // (Work is passed by value: the edge scan's finish tags its host word)
     launch_edges(sa, bd, w);
     if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_a[wp], sa);
     mark(kPhEdges);
@@ -2446,7 +2699,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         worker_start_job(cs);
         if (prev) {
             cs->pending_batch = nullptr;
-            hipError_t e = cs->pending_b.replay(s);
+            hipError_t e = cs->pending_b.replay(s, x_skip(cs, cs->pending_batch), &cs->stats.x_launches_skipped);
             cs->x_issued.fetch_add(1, std::memory_order_release);
             hipError_t e2 = hipSuccess;
             if (!hy) {

@@ -244,6 +244,10 @@ struct Work {
     uint8_t* c_exact;
     unsigned long long* trace;  // [kTrSlots] or null
     int32_t no_prepass;         // FDBCS_RESOLVE_PREPASS=0: resolution rounds without the pre-pass (tests)
+    // host-mapped {batch seq, any candidate edge} of the batch on this workspace, written by the
+    // edge scan's finish (kGroupEdges launches left out when 0; null: not tracked)
+    uint32_t* hedge;
+    uint32_t hseq;
 };
 
 // FDBCS_TRACE: device timestamps (wall_clock64 ticks) of kernel sections, for tuning.

@@ -31,6 +31,7 @@
 namespace fdbcs {
 
 thread_local LaunchList* t_record = nullptr;
+thread_local uint8_t t_group = 0;
 thread_local hipError_t t_launch_error = hipSuccess;
 
 // ------------------------------------------------------------------ helpers
@@ -2525,6 +2526,13 @@ struct EdgePairScan {
         w.bsc->n_pranges = tot[2];
         w.bsc->n_edges = tot[0];
         w.bsc->edge_overflow = (int64_t)tot[0] > w.edge_cap || tot[0] > 0x7fffffffu || tot[1] > 0x7fffffffu ? 1 : 0;
+        // to the host (mapped memory): does this batch have candidate edges?  Read once the
+        // batch's stage A event completed, tagged with the batch's sequence number
+        if (w.hedge) {
+            w.hedge[1] = tot[0] != 0 ? 1u : 0u;
+            __threadfence_system();
+            w.hedge[0] = w.hseq;
+        }
     }
 };
 
@@ -2715,7 +2723,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
     if (blockIdx.x == 0 && threadIdx.x == 0) trace_min(w.trace, kTrResBegin);
     if (sc->n_edges == 0 && !sc->edge_overflow) {
         // no candidate writer anywhere: every admitted transaction without a history conflict
-        // commits (SkipList.cpp:817-833 with an empty MiniConflictSet)
+        // commits (SkipList.cpp:817-833 with an empty MiniConflictSet).  No rounds (k_resolve, which
+        // a replay may leave out, would set the same).
+        if (blockIdx.x == 0 && threadIdx.x == 0) w.bsc->rounds = 0;
         for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < T; t += gridDim.x * blockDim.x) {
             const uint8_t st = (w.hist_conf[t] || (b.flags[t] & kFlagTooOld)) ? kAborted : kCommitted;
             w.status[t] = st;
@@ -3306,11 +3316,15 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
     const size_t lds = ((size_t)b.T + 15) / 16 * 16 + (w.groups ? 8 * (size_t)b.W : 0);
     Work wr = w;
     wr.report = report ? 1 : 0;
+    // Without candidate edges (k_resolve_pre decided, combined and set the rounds to 0) these
+    // three have nothing to do: a replay leaves them out once stage A's edge count reached the host
+    t_group = kGroupEdges;
     fdb_launch(b.T <= 5 * kWG ? k_resolve<5> : k_resolve<8>, dim3(1), dim3(kWG), (uint32_t)lds, s, b, wr, verdict_out,
                sc);
     fdb_launch(k_combine, dim3((unsigned)std::max<int64_t>(1, (2 * (int64_t)b.W + kCombineTile - 1) / kCombineTile)),
                dim3(kScanThreads), 0, s, b, w);
     if (b.R && report) fdb_launch(k_intra_report, dim3((b.R + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b, w);
+    t_group = 0;
 }
 
 // Epilogue work of a batch (k_epilogue, or fused into the merge copy when the batch does not

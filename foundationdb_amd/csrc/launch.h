@@ -32,6 +32,8 @@ struct LaunchList {
         dim3 grid, block;
         uint32_t shmem;
         uint32_t arg0, nargs;  // argument slots [arg0, arg0 + nargs) of argoff / argp
+        uint8_t group = 0;     // skip group (t_group when recorded): replay(s, mask) leaves out
+                               // kernels whose group is in mask (never a kernel with timing events)
     };
     std::vector<Rec> recs;
     std::vector<uint32_t> argoff;  // byte offset of each argument value in `arena`
@@ -99,17 +101,28 @@ struct LaunchList {
         }
         return hipSuccess;
     }
-    // Direct mode: submit in order (waits and records on `s`).
-    hipError_t replay(hipStream_t s) {
+    // Direct mode: submit in order (waits and records on `s`), leaving out the kernels of the
+    // skip groups in `skip` (whose results the caller knows are not needed).  *skipped counts them.
+    hipError_t replay(hipStream_t s, uint8_t skip = 0, int64_t* skipped = nullptr) {
         finalize();
-        for (const Rec& r : recs)
+        for (const Rec& r : recs) {
+            if (r.kind == kKernel && (r.group & skip)) {
+                if (skipped) ++*skipped;
+                continue;
+            }
             if (hipError_t e = issue(r, s)) return e;
+        }
         return hipSuccess;
     }
 };
 
 // Non-null while the engine records a stage: fdb_launch / fdb_event append to it.
 extern thread_local LaunchList* t_record;
+// Skip group of the kernels recorded now (LaunchList::Rec::group).  kGroupEdges: the launches that
+// have work only when stage A found candidate intra-batch edges (k_resolve, k_combine,
+// k_intra_report); a replay leaves them out once the host has seen that batch's edge count be 0.
+constexpr uint8_t kGroupEdges = 1;
+extern thread_local uint8_t t_group;
 // First failed direct launch since the last take_launch_error().  The engine checks its own
 // launches this way rather than with hipGetLastError(), whose per-thread "last error" also holds
 // failures of other HIP users in the process (torch shares the runtime) that they never cleared.
@@ -129,6 +142,7 @@ inline void fdb_launch(void (*k)(P...), dim3 grid, dim3 block, uint32_t shmem, h
         (L->push_arg(static_cast<std::decay_t<P>>(a)), ...);
         const bool timed = L->prof && (!L->timed_func || L->timed_func == (const void*)k);
         hipEvent_t e0 = timed ? L->prof->take() : nullptr, e1 = timed ? L->prof->take() : nullptr;
+        r.group = (e0 && e1) ? 0 : t_group;  // a kernel between timing events is always issued
         if (e0 && e1) L->recs.push_back({LaunchList::kTimingRecord, nullptr, e0, dim3(), dim3(), 0, 0, 0});
         L->recs.push_back(r);
         if (e0 && e1) {

@@ -135,6 +135,9 @@ typedef struct fdbcs_stats {
      * calls (validation, normalization into pinned staging) and the calls' transactions. */
     double host_ms_add;
     int64_t added_txns;
+    /* Launches of batch-order resolution left out of a batch's X half because the host had seen
+     * its stage A find no candidate intra-batch edge (k_resolve, k_combine, k_intra_report). */
+    int64_t x_launches_skipped;
 } fdbcs_stats;
 
 /* newConflictSet() — SkipList.cpp:739-741.  `device` = HIP ordinal. */

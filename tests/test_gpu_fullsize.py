@@ -106,24 +106,19 @@ def test_full_c2_too_old_at_window_edge(engine, oracle_mod, order):
     got, add_oldest = {}, {}
     if order == "resolver":
         pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
-    else:
-        objs = []
-        for i, (pb, _, _) in enumerate(seq):
-            b = engine.ConflictBatch(cs)
-            add_oldest[i] = cs.oldest_version
-            b.add_packed(pb)
-            objs.append(b)
-        inflight = []
-        for i, (b, (_, now_, no_)) in enumerate(zip(objs, seq)):
-            b.detect_async(now_, no_)
-            inflight.append((i, b))
-            if len(inflight) > WINDOW:
-                j, bj = inflight.pop(0)
-                got[j] = bj.wait()
-                bj.close()
-        for j, bj in inflight:
-            got[j] = bj.wait()
-            bj.close()
+    else:  # bench.py's passes: each group of 8 batches added before the group's first detect
+        for g0 in range(0, len(seq), 8):
+            objs = []
+            for i in range(g0, min(g0 + 8, len(seq))):
+                b = engine.ConflictBatch(cs)
+                add_oldest[i] = cs.oldest_version
+                b.add_packed(seq[i][0])
+                objs.append((i, b))
+            for i, b in objs:
+                b.detect_async(seq[i][1], seq[i][2])
+            for i, b in objs:
+                got[i] = b.wait()
+                b.close()
     sl = oracle_mod.SkipListBaseline()
     sl.load_history(kb, ko, vers)
     too_old = 0
@@ -133,7 +128,7 @@ def test_full_c2_too_old_at_window_edge(engine, oracle_mod, order):
         assert len(bad) == 0, (i, bad[:10], got[i][bad[:10]], v[bad[:10]])
         too_old += int((v == 1).sum())
     # ~2 % of 120k transactions sit at the edge, about half of them below it
-    assert too_old > (300 if order == "resolver" else 50), too_old
+    assert too_old > (300 if order == "resolver" else 25), too_old
     cs.close()
 
 

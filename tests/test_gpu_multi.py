@@ -246,7 +246,10 @@ def test_routed_batch_errors_leave_it_empty_and_reroutable(engine, monkeypatch):
         b.routed_info()
     assert e.value.status == engine.FDBCS_E_TIMEOUT
     # 2. n_global differs from the shares' transaction count: FDBCS_E_INVALID, batch empty again
-    b.add_routed(dev.data_ptr(), stride, 1, Tshare, None, None, caps, out.data_ptr(), pb.n_txn + 3)
+    # (more than the shares can hold is refused on the host at once; fewer is found on the device)
+    with pytest.raises(engine.InvertedRange):
+        b.add_routed(dev.data_ptr(), stride, 1, Tshare, None, None, caps, out.data_ptr(), pb.n_txn + 3)
+    b.add_routed(dev.data_ptr(), stride, 1, Tshare, None, None, caps, out.data_ptr(), pb.n_txn - 3)
     with pytest.raises(engine.FdbcsError) as e:
         b.routed_info()
     assert e.value.status == engine.FDBCS_E_INVALID

@@ -486,6 +486,78 @@ def test_edge_cases(engine):
     assert ex.value.status == engine.FDBCS_E_VERSION
 
 
+def _packed(txns, inverted=None):
+    """A PackedBatch of (snapshot, reads, writes) with [(begin, end)] byte ranges, built directly so
+    that `inverted` = (txn, 'r'|'w', i) can swap one range's ends (KeyRange itself refuses that)."""
+    keys, roff, woff, snap = [], [0], [0], []
+    for t, (sn, reads, writes) in enumerate(txns):
+        snap.append(sn)
+        roff.append(roff[-1] + len(reads))
+        woff.append(woff[-1] + len(writes))
+    rk, wk = [], []
+    for t, (_, reads, writes) in enumerate(txns):
+        for i, (a, b) in enumerate(reads):
+            rk += [b, a] if inverted == (t, "r", i) else [a, b]
+        for i, (a, b) in enumerate(writes):
+            wk += [b, a] if inverted == (t, "w", i) else [a, b]
+    keys = rk + wk
+    ko = np.zeros(len(keys) + 1, np.int64)
+    ko[1:] = np.cumsum([len(k) for k in keys])
+    kb = np.frombuffer(b"".join(keys), np.uint8).copy() if keys else np.zeros(0, np.uint8)
+    return PackedBatch(np.array(snap, np.int64), np.zeros(len(txns), np.uint8), np.array(roff, np.int32),
+                       np.array(woff, np.int32), kb, ko)
+
+
+@pytest.mark.parametrize("n_txn", [40, 3000])
+def test_add_packed_rejects_inverted_ranges(engine, oracle_mod, n_txn):
+    """addTransaction refuses a range with begin > end (KeyRangeRef, FDBTypes.h:288-291) wherever it
+    sits -- a read, a write, a TooOld transaction's range, keys tied on the 16-byte prefix and
+    ordered by their tails -- all or nothing: the batch stays empty and takes a valid batch
+    afterwards.  3000 transactions: the validation runs fused with the normalization over the
+    add threads' chunks (FDBCS_ADD_THREADS)."""
+    rng = np.random.default_rng(n_txn)
+    long = b"p" * 16
+
+    def key():
+        return (long if rng.random() < 0.3 else b"") + bytes(rng.integers(0, 4, size=int(rng.integers(1, 6))).tolist())
+
+    def rng_range():
+        a, b = sorted([key(), key()])
+        return a, b
+
+    txns = [(int(rng.integers(0, 20)), [rng_range() for _ in range(2)], [rng_range() for _ in range(2)])
+            for _ in range(n_txn)]
+    # a pair tied on the 16-byte prefix, ordered by the tails only
+    txns[n_txn // 2] = (15, [(long + b"\x01", long + b"\x02")], [(long + b"\x00\x05", long + b"\x00\x06")])
+    cs = engine.ConflictSet(0)
+    ora = oracle_mod.OracleConflictSet()
+    b0 = engine.ConflictBatch(cs)  # oldest -> 10: snapshots below it are TooOld
+    b0.add_packed(_packed([]))
+    b0.detect_conflicts(20, 10)
+    b0.close()
+    ora.detect(_packed([]), 20, 10)
+    spots = [(1, "r", 0), (n_txn - 1, "w", 1), (n_txn // 2, "r", 0), (n_txn // 2, "w", 0)]
+    old_t = next(t for t, (sn, _, _) in enumerate(txns) if sn < 10)
+    spots.append((old_t, "w", 0))  # a TooOld transaction's range is validated too
+    now = 30
+    for spot in spots:
+        t, kind, i = spot
+        a, bb = (txns[t][1] if kind == "r" else txns[t][2])[i]
+        if a == bb:
+            continue
+        b = engine.ConflictBatch(cs)
+        with pytest.raises(engine.InvertedRange):
+            b.add_packed(_packed(txns, inverted=spot))
+        assert b.transaction_count == 0
+        b.add_packed(_packed(txns))  # the same batch object, now valid
+        got = b.detect_conflicts(now, 10)
+        b.close()
+        want, _ = ora.detect(_packed(txns), now, 10)
+        np.testing.assert_array_equal(got, want)
+        now += 5
+    cs.close()
+
+
 @pytest.mark.parametrize("bucket,cold", [("3000", "0"), ("600", "0"), ("40", "0"), ("160", "1"), ("64", "1"),
                                          ("8", "0")])
 def test_sort_bucket_sizes_match(engine, oracle_mod, monkeypatch, bucket, cold):
