@@ -2594,7 +2594,9 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhCheck);
     if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
     if (split) fdb_event(LaunchList::kSyncWait, cs->ev_c[wp], s);
+    w.vdev = (uint8_t*)sl->dverdict.p;  // (Work by value: the resolution's launches carry it)
     launch_resolve(s, bd, w, b->any_report, (uint8_t*)sl->pin_out.dp, sc);
+    w.vdev = nullptr;
     if (b->out_dev && b->out_n > 0)  // multi-resolver combine input, final before the completion flag
         launch_conflict_output(s, bd, w, b->routed ? (const int32_t*)sl->rt_inv.p : (const int32_t*)sl->pin_inv.dp,
                                b->out_n, b->out_dev);
@@ -2663,13 +2665,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->ddir_epoch[dnew] = ++cs->ddir_counter;
     }
     launch_epilogue(ys, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
-                    gc ? 1 : 0, (uint8_t*)hd, (uint8_t*)sl->dverdict.p, (uint32_t*)(hd + o_fl), b->seq,
+                    gc ? 1 : 0, (uint8_t*)hd, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1, &sc->ndb[dnew], sort_nb, sort_samples);
     fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], ys);
     // (no event marks the slot free: a slot returns to the pool only from fdbcs_batch_destroy,
     // after the batch's completion flag was seen or its streams were synchronized; every kernel
-    // of the batch that reads the slot precedes the epilogue's publishing workgroup, which reads
-    // the slot's flags before it publishes)
+    // of the batch that reads or writes the slot precedes the epilogue, which touches none of it)
     if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
         fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, ys);
         cs->cmp_recorded = true;

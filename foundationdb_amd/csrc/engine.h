@@ -248,6 +248,9 @@ struct Work {
     // edge scan's finish (kGroupEdges launches left out when 0; null: not tracked)
     uint32_t* hedge;
     uint32_t hseq;
+    // [T] device copy of the batch's verdicts (its slot's dverdict), written by the resolution next
+    // to the host-mapped verdict bytes (fdbcs_batch_device_verdicts); set per batch, null: none
+    uint8_t* vdev;
 };
 
 // FDBCS_TRACE: device timestamps (wall_clock64 ticks) of kernel sections, for tuning.
@@ -432,7 +435,7 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 // sort_nb / sort_samples: the batch's sort buckets and cold-start samples (their counters and
 // ranks are re-zeroed; 0 samples on a warm start).
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
-                     int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
+                     int compacted, int gc_ran, uint8_t* verdict_out, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n, int64_t* nd_out, int sort_nb, int sort_samples);
 // Cold-start samples of a sort over E endpoints in nb buckets (k_sample; ranks re-zeroed by the epilogue).
 int sort_cold_samples(int64_t E, int nb);

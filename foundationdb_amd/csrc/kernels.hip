@@ -1936,82 +1936,31 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int B0 = blockIdx.x * kWaves;
     if (threadIdx.x == 0) trace_min(a.trace, kTrBktBegin);
-    // ---- bucket offsets: counts of every bucket before B0 and of all buckets, reduced by the
-    // workgroup (nb <= kSortMaxBuckets: 16 per thread at most, loads issued together)
-    uint32_t pre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
-    for (int k0 = threadIdx.x; k0 < ((a.exp & 8) ? 0 : nb); k0 += 4 * kBlock) {  // (exp 8: cost breakdown only)
-        uint64_t c0[4], c1[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * kBlock;
-            c0[u] = k < nb ? a.cnt[(size_t)kCntStride * k] : 0;
-            c1[u] = k < nb ? a.cnt[(size_t)kCntStride * k + 1] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + u * kBlock;
-            const uint32_t v[4] = {(uint32_t)c0[u], (uint32_t)(c0[u] >> 32), (uint32_t)c1[u], (uint32_t)(c1[u] >> 32)};
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                tot[c] += v[c];
-                pre[c] += k < B0 ? v[c] : 0u;
-            }
-            if (k >= B0 && k < B0 + kWaves)
-#pragma unroll
-                for (int c = 0; c < 4; c++) s_cnt[k - B0][c] = v[c];
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            pre[c] += __shfl_xor(pre[c], off, 64);
-            tot[c] += __shfl_xor(tot[c], off, 64);
-        }
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            s_red[c][wave] = pre[c];
-            s_red[4 + c][wave] = tot[c];
-        }
-    if (threadIdx.x < kWaves && B0 + (int)threadIdx.x >= nb)
-#pragma unroll
-        for (int c = 0; c < 4; c++) s_cnt[threadIdx.x][c] = 0;
-    if ((a.exp & 8) && threadIdx.x < kWaves && B0 + (int)threadIdx.x < nb) {  // cost breakdown: 64 per bucket
-        s_cnt[threadIdx.x][0] = 64;
-        s_cnt[threadIdx.x][1] = s_cnt[threadIdx.x][2] = s_cnt[threadIdx.x][3] = 16;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run[4] = {0, 0, 0, 0};
-        for (int q = 0; q < kWaves; q++)
-#pragma unroll
-            for (int c = 0; c < 4; c++) run[c] += s_red[c][q];
-        for (int q = 0; q < kWaves; q++)
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                s_base[q][c] = run[c];
-                run[c] += s_cnt[q][c];
-            }
-        if (blockIdx.x == 0) {  // class totals after the last position
-            uint32_t t4[4] = {0, 0, 0, 0};
-            for (int q = 0; q < kWaves; q++)
-#pragma unroll
-                for (int c = 0; c < 4; c++) t4[c] += s_red[4 + c][q];
-            o.cwb[E] = (int32_t)t4[1];
-            o.crb[E] = (int32_t)t4[2];
-            o.cwe[E] = (int32_t)t4[3];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) trace_max(a.trace, kTrBktPrologue);
-    // ---- one bucket per wave
+    // ---- this wave's bucket: its own counts first (one line), then every thread's share of the
+    // counters the bucket offsets sum (all buckets before B0, and all), issued now and summed only
+    // after the network so their latency hides behind the slab loads and the sort
     const int bk = B0 + wave;
-    const int n = (int)s_cnt[wave][0];
-    const int64_t base = s_base[wave][0];
-    if (lane == 0) s_big[wave] = n > kSlab ? 1 : 0;
-    if (bk < nb && n > 0 && n <= kSlab) {
+    uint64_t own0 = 0, own1 = 0;
+    if (bk < nb && !(a.exp & 8)) {
+        own0 = a.cnt[(size_t)kCntStride * bk];
+        own1 = a.cnt[(size_t)kCntStride * bk + 1];
+    }
+    if (a.exp & 8) own0 = bk < nb ? (64ull | 16ull << 32) : 0ull, own1 = bk < nb ? (16ull | 16ull << 32) : 0ull;
+    constexpr int kPreLoads = kSortMaxBuckets / kBlock;
+    uint64_t c0[kPreLoads], c1[kPreLoads];
+#pragma unroll
+    for (int u = 0; u < kPreLoads; u++) {
+        const int k = threadIdx.x + u * kBlock;
+        const bool in = k < nb && !(a.exp & 8);  // (exp 8: cost breakdown only)
+        c0[u] = in ? a.cnt[(size_t)kCntStride * k] : 0;
+        c1[u] = in ? a.cnt[(size_t)kCntStride * k + 1] : 0;
+    }
+    const int n = (int)(uint32_t)own0;
+    const bool small = bk < nb && n > 0 && n <= kSlab;
+    int ps[4] = {0, 0, 0, 0};  // endpoint at each position of the wave's bucket (after the sort)
+    int S = 1;
+    unsigned long long tt[3] = {0, 0, 0};  // FDBCS_TRACE section stamps
+    if (small) {
         const unsigned long long tw0 = a.trace ? wall_clock64() : 0ull;
         unsigned long long tw1 = 0, tw2 = 0;
         // bytes every key of the bucket shares: those its bounding splitters share (none at the ends)
@@ -2020,7 +1969,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
         if (LONG && bk > 0 && bk < nb - 1)
             c = split_lcp(a.quant[split_index(bk - 1, nb)], a.quant[split_index(bk, nb)]);
         uint64_t kh[4], kl[4], ka[4];
-        const int S = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
+        S = n <= 64 ? 1 : (n <= 128 ? 2 : 4);
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             const int k = s * 64 + lane;
@@ -2046,7 +1995,6 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
         else wave_bitonic<4>(kh, kl, ka);
         if (lane == 0) trace_max(a.trace, kTrBktSorted);
         if (a.trace) tw2 = wall_clock64();
-        int ps[4];  // endpoint at each position (id bits of the tie-break word)
 #pragma unroll
         for (int s = 0; s < 4; s++) ps[s] = (int)(ka[s] & 0x3fffffffull);
         if ((LONG || c > 0) && !(a.exp & 1)) {  // exp: fdbcs_debug_kernel_time's cost breakdown only
@@ -2199,6 +2147,77 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             }
         }
         if (lane == 0) trace_max(a.trace, kTrBktTies);
+        tt[0] = tw0;
+        tt[1] = tw1;
+        tt[2] = tw2;
+    }
+    // ---- bucket offsets: the counts of every bucket before B0 and of all buckets (loaded above)
+    {
+        uint32_t pre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < kPreLoads; u++) {
+            const int k = threadIdx.x + u * kBlock;
+            const uint32_t v[4] = {(uint32_t)c0[u], (uint32_t)(c0[u] >> 32), (uint32_t)c1[u], (uint32_t)(c1[u] >> 32)};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                tot[c] += v[c];
+                pre[c] += k < B0 ? v[c] : 0u;
+            }
+        }
+        if (a.exp & 8) {  // cost breakdown: 64 endpoints per bucket
+            const uint32_t per[4] = {64, 16, 16, 16};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                pre[c] = threadIdx.x == 0 ? per[c] * (uint32_t)B0 : 0u;
+                tot[c] = threadIdx.x == 0 ? per[c] * (uint32_t)nb : 0u;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                pre[c] += __shfl_xor(pre[c], off, 64);
+                tot[c] += __shfl_xor(tot[c], off, 64);
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                s_red[c][wave] = pre[c];
+                s_red[4 + c][wave] = tot[c];
+            }
+            const uint32_t v[4] = {(uint32_t)own0, (uint32_t)(own0 >> 32), (uint32_t)own1, (uint32_t)(own1 >> 32)};
+#pragma unroll
+            for (int c = 0; c < 4; c++) s_cnt[wave][c] = v[c];
+            s_big[wave] = n > kSlab ? 1 : 0;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run[4] = {0, 0, 0, 0};
+            for (int q = 0; q < kWaves; q++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) run[c] += s_red[c][q];
+            for (int q = 0; q < kWaves; q++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    s_base[q][c] = run[c];
+                    run[c] += s_cnt[q][c];
+                }
+            if (blockIdx.x == 0) {  // class totals after the last position
+                uint32_t t4[4] = {0, 0, 0, 0};
+                for (int q = 0; q < kWaves; q++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++) t4[c] += s_red[4 + c][q];
+                o.cwb[E] = (int32_t)t4[1];
+                o.crb[E] = (int32_t)t4[2];
+                o.cwe[E] = (int32_t)t4[3];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) trace_max(a.trace, kTrBktPrologue);
+    }
+    if (small) {
+        const int64_t base = s_base[wave][0];
         const unsigned long long tw3 = a.trace ? wall_clock64() : 0ull;
         // positions, class counts before them, begin lists; quantiles for the next batch
         uint32_t carry[3] = {s_base[wave][1], s_base[wave][2], s_base[wave][3]};
@@ -2232,9 +2251,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const unsigned long long tw4 = wall_clock64();
             atomicAdd(&a.trace[kTrBktWaves], 1ull);
-            atomicAdd(&a.trace[kTrBktSumLoad], tw1 - tw0);
-            atomicAdd(&a.trace[kTrBktSumSort], tw2 - tw1);
-            atomicAdd(&a.trace[kTrBktSumTies], tw3 - tw2);
+            atomicAdd(&a.trace[kTrBktSumLoad], tt[1] - tt[0]);
+            atomicAdd(&a.trace[kTrBktSumSort], tt[2] - tt[1]);
+            atomicAdd(&a.trace[kTrBktSumTies], tw3 - tt[2]);
             atomicAdd(&a.trace[kTrBktSumPut], tw4 - tw3);
         }
     }
@@ -2731,6 +2750,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
             w.status[t] = st;
             w.first_conf[t] = INT_MAX;
             vout[t] = verdict_byte(b, t, st);
+            if (w.vdev) w.vdev[t] = vout[t];
         }
         // D.Combine: tiles of kCombineTile write endpoints, ids in launch order.  Only the first
         // ntiles workgroups take an id: the grid is sized for the waves of the edge case, and
@@ -2847,6 +2867,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_pre(BatchDev b, Work w, uint
             if (s0 != kUndecided) {  // final: k_resolve's register rounds see only the undecided
                 w.status[t] = s0;
                 vout[t] = verdict_byte(b, t, s0);
+                if (w.vdev) w.vdev[t] = verdict_byte(b, t, s0);
             } else {
                 const int u = atomicAdd(&w.bsc->n_undec, 1);
                 w.ulist[2 * u] = make_int4(t, tbase, tbase + cnt, 0);
@@ -3245,12 +3266,14 @@ __global__ __launch_bounds__(kWG) void k_resolve(BatchDev b, Work w, uint8_t* vo
                 const uint8_t x = st[t];
                 w.status[t] = x;
                 vout[t] = x == kCommitted ? 2 : 0;  // verdict_byte
+                if (w.vdev) w.vdev[t] = x == kCommitted ? 2 : 0;
             }
         }
     } else {
         for (int t = threadIdx.x; t < T; t += blockDim.x) {
             w.status[t] = st[t];
             vout[t] = verdict_byte(b, t, st[t]);
+            if (w.vdev) w.vdev[t] = verdict_byte(b, t, st[t]);
         }
     }
     if (threadIdx.x == 0) sc->rounds = rounds;
@@ -3330,10 +3353,7 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
 // Epilogue work of a batch (k_epilogue, or fused into the merge copy when the batch does not
 // compact): device verdict copy, scratch zeroing, scalars and the completion flag.
 struct Epilogue {
-    const uint8_t* flags;
-    const uint8_t* status;
     uint8_t* verdict_out;  // [T] verdicts, then Scalars at kVerdictScalarsOffset(T) (host-mapped)
-    uint8_t* verdict_dev;  // [T] device copy of the verdicts (on-device combine)
     uint32_t* flag;        // host-mapped completion word, set to `seq` last
     uint32_t seq;
     unsigned long long* trace;
@@ -3662,14 +3682,11 @@ static unsigned copy_tiles(int64_t grid_hint_n, int tile, int64_t max_inserts = 
 }
 
 static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, int gc_ran, uint8_t* verdict_out,
-                              uint8_t* verdict_dev, uint32_t* flag, uint32_t seq, int sort_nb, int sort_samples) {
+                              uint32_t* flag, uint32_t seq, int sort_nb, int sort_samples) {
     Epilogue ep{};
-    ep.verdict_dev = verdict_dev;
     ep.flag = flag;
     ep.seq = seq;
     ep.trace = w.trace;
-    ep.flags = b.flags;
-    ep.status = w.status;
     ep.verdict_out = verdict_out;
     ep.T = b.T;
     ep.compacted = compacted;
@@ -4273,15 +4290,9 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
     if (!ep.verdict_out) return;
     if (threadIdx.x == 0) trace_max(ep.trace, kTrEpiLevels);
     const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
-    auto verdict = [&](int64_t t) -> uint8_t {
-        if (ep.flags[t] & kFlagTooOld) return 1;  // TransactionTooOld (ConflictSet.h:42)
-        return ep.status[t] == kCommitted ? 2 : 0;
-    };
-    // The device verdicts read the batch's flags from its slot: workgroup 0 writes them before it
-    // publishes the flag, so once the host has seen the flag no workgroup still reads the slot (a
-    // destroyed batch's slot returns to the pool on the flag alone).
-    if (blockIdx.x == 0)
-        for (int64_t t = threadIdx.x; t < ep.T; t += blockDim.x) ep.verdict_dev[t] = verdict(t);
+    // (the device verdicts are written by the resolution next to the host-mapped ones: this launch
+    // reads nothing of the batch's slot, so a destroyed batch's slot may return to the pool once
+    // the flag was seen)
     for (int64_t i = tid; i < ep.zero8_n; i += stride) ep.zero8[i] = 0;
     for (int64_t i = tid; i < ep.zero8r_n; i += stride) ep.zero8r[i] = 0;
     for (int64_t i = tid; i < ep.zero32_n; i += stride) ep.zero32b[i] = 0;
@@ -4485,9 +4496,9 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 }
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
-                     int compacted, int gc_ran, uint8_t* verdict_out, uint8_t* verdict_dev, uint32_t* flag,
+                     int compacted, int gc_ran, uint8_t* verdict_out, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n, int64_t* nd_out, int sort_nb, int sort_samples) {
-    Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, verdict_dev, flag, seq, sort_nb, sort_samples);
+    Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, flag, seq, sort_nb, sort_samples);
     ep.nd_out = nd_out;
     if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
     int64_t extra = std::max<int64_t>(b.R, b.T);
