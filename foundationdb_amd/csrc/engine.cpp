@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <cxxabi.h>
 
@@ -117,6 +118,21 @@ constexpr int kWsTileSlot = 54, kWsArenaSlot = 55;
 // workspace is reused every third batch.
 constexpr int kNumWork = 3;
 constexpr int kGcEveryCompactions = 4;  // removeBefore cadence of size-triggered compactions
+
+// FDBCS_HOST_TRACE=<path>: host-side spans of the pipeline (steady_clock ns, the clock rocprofv3
+// timestamps use), written as CSV when the set is destroyed: per batch sequence number the detect
+// call (D), the helper's issue of stage A (A) and of a Y half (Y), the calling thread's issue of an
+// X half (X) and the wait for the completion flag (W).  scripts/host_trace.py joins them with a
+// rocprofv3 kernel trace: when each chain's launches were issued against when they ran.
+struct HSpan {
+    uint32_t seq;
+    char kind;
+    int64_t t0, t1;
+};
+inline int64_t mono_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 // Host threads for addTransaction of whole batches (fdbcs_batch_add_packed): the endpoint keys'
 // validation and normalization into pinned staging split over chunks of transactions.  The
@@ -381,6 +397,11 @@ struct fdbcs_conflict_set {
     // addTransaction threads (FDBCS_ADD_THREADS, workers besides the calling thread; 0 = serial)
     int add_threads = 5;
     AddPool* add_pool = nullptr;
+    int wait_query_ms = 2;  // FDBCS_WAIT_QUERY_MS: stream error checks while a wait spins (0: every 4096 spins)
+    // FDBCS_HOST_TRACE: spans of the calling thread [0] and of the helper [1]
+    bool htrace = false;
+    std::vector<HSpan> htr[2];
+    uint32_t work_a_seq = 0, work_y_seq = 0;
     double add_prof[4] = {0, 0, 0, 0};  // FDBCS_ADD_PROFILE: ms in add's serial pass, slot, count, fill
     int64_t add_prof_n = 0;
     std::thread worker;
@@ -759,7 +780,7 @@ int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n, int64_t* l2_n) {
     for (int L = 1; L < kMaxLevels; L++) {
         m = (m + kFan - 1) / kFan + 1;
         lv[L].release();
-        if (int rc = lv[L].ensure(8 * m)) return rc;
+        if (int rc = lv[L].ensure(8 * (L == kMaxLevels - 1 ? l3_words(m) : m))) return rc;
         if (L == 2) *l2_n = m;
     }
     *top_n = m;
@@ -1182,10 +1203,14 @@ void worker_main(fdbcs_conflict_set* cs) {
             cs->wcv.wait(lk, [&] { return (j = cs->wjob.load(std::memory_order_acquire)) != 0; });
         }
         if (j == 2) return;
+        const int64_t ta = cs->htrace ? mono_ns() : 0;
         hipError_t e = cs->work_a.replay(cs->work_sa);
+        if (cs->htrace) cs->htr[1].push_back({cs->work_a_seq, 'A', ta, mono_ns()});
         if (!cs->work_y.recs.empty()) {
             while (cs->x_issued.load(std::memory_order_acquire) < cs->work_need_x) std::this_thread::yield();
+            const int64_t ty = cs->htrace ? mono_ns() : 0;
             const hipError_t e3 = cs->work_y.replay(cs->work_ys);
+            if (cs->htrace) cs->htr[1].push_back({cs->work_y_seq, 'Y', ty, mono_ns()});
             if (e == hipSuccess) e = e3;
             cs->work_y.clear();
             cs->b_issued.fetch_add(1, std::memory_order_release);
@@ -1247,11 +1272,18 @@ int flush_pending(fdbcs_conflict_set* cs) {
     if (int rc = worker_wait(cs)) return rc;  // stage A / check of the pending batch issued
     if (!cs->pending_batch) return FDBCS_OK;
     const uint8_t skip = x_skip(cs, cs->pending_batch);
+    const uint32_t pseq = cs->pending_batch->seq;
     cs->pending_batch = nullptr;
     int rc = FDBCS_OK;
+    const int64_t tx = cs->htrace ? mono_ns() : 0;
     if (cs->pending_b.replay(cs->stream, skip, &cs->stats.x_launches_skipped) != hipSuccess) rc = FDBCS_E_DEVICE;
+    const int64_t ty = cs->htrace ? mono_ns() : 0;
     cs->x_issued.fetch_add(1, std::memory_order_release);
     if (cs->pending_y.replay(cs->pending_ys) != hipSuccess) rc = FDBCS_E_DEVICE;
+    if (cs->htrace) {
+        cs->htr[0].push_back({pseq, 'X', tx, ty});
+        cs->htr[0].push_back({pseq, 'Y', ty, mono_ns()});
+    }
     cs->b_issued.fetch_add(1, std::memory_order_release);
     cs->pending_b.clear();
     cs->pending_y.clear();
@@ -1301,6 +1333,12 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
     if (const char* v = getenv("FDBCS_ADD_THREADS")) cs->add_threads = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("FDBCS_SKIP_EDGES")) cs->skip_edges = v[0] != '0';
+    if (const char* v = getenv("FDBCS_WAIT_QUERY_MS")) cs->wait_query_ms = std::max(0, atoi(v));
+    if (getenv("FDBCS_HOST_TRACE")) {
+        cs->htrace = true;
+        cs->htr[0].reserve(1 << 16);
+        cs->htr[1].reserve(1 << 16);
+    }
     if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2' ? 1 : (v[0] == '3' ? 2 : 0);
     if (const char* v = getenv("FDBCS_GRAPH_RING")) cs->graph_ring = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
@@ -1376,6 +1414,17 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     (void)hipSetDevice(cs->device);
     (void)flush_pending(cs);
     worker_stop(cs);
+    if (cs->htrace) {
+        char path[512];
+        snprintf(path, sizeof(path), "%s.%d.csv", getenv("FDBCS_HOST_TRACE"), (int)getpid());
+        if (FILE* f = fopen(path, "w")) {
+            fprintf(f, "thread,seq,kind,t0,t1\n");
+            for (int k = 0; k < 2; k++)
+                for (const HSpan& h : cs->htr[k])
+                    fprintf(f, "%d,%u,%c,%lld,%lld\n", k, h.seq, h.kind, (long long)h.t0, (long long)h.t1);
+            fclose(f);
+        }
+    }
     if (getenv("FDBCS_ADD_PROFILE") && cs->add_prof_n)
         fprintf(stderr, "fdbcs add profile (%d threads, ms per batch over %lld): serial %.4f slot %.4f count %.4f fill %.4f\n",
                 cs->add_threads, (long long)cs->add_prof_n, cs->add_prof[0] / cs->add_prof_n,
@@ -2688,9 +2737,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         std::swap(cs->work_a, la);
         std::swap(cs->work_c, lc);  // empty unless split
         cs->work_sa = sa;
+        cs->work_a_seq = b->seq;
         const bool prev = cs->pending_batch != nullptr;
         const bool hy = prev && cs->helper_y;
         if (hy) {  // the previous batch's Y to the helper, after the X this thread issues below
+            cs->work_y_seq = cs->pending_batch->seq;
             std::swap(cs->work_y, cs->pending_y);
             cs->work_ys = cs->pending_ys;
             cs->work_need_x = cs->x_issued.load(std::memory_order_relaxed) + 1;
@@ -2699,8 +2750,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->work_need_b = cs->b_recorded;  // every stage B recorded so far, batch i-1's included
         worker_start_job(cs);
         if (prev) {
+            fdbcs_batch* pb_ = cs->pending_batch;
             cs->pending_batch = nullptr;
-            hipError_t e = cs->pending_b.replay(s, x_skip(cs, cs->pending_batch), &cs->stats.x_launches_skipped);
+            const int64_t tx = cs->htrace ? mono_ns() : 0;
+            const uint32_t pseq = pb_->seq;
+            hipError_t e = cs->pending_b.replay(s, x_skip(cs, pb_), &cs->stats.x_launches_skipped);
+            if (cs->htrace) cs->htr[0].push_back({pseq, 'X', tx, mono_ns()});
             cs->x_issued.fetch_add(1, std::memory_order_release);
             hipError_t e2 = hipSuccess;
             if (!hy) {
@@ -2767,6 +2822,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->tail_ub += tail_add;
     cs->inflight++;
     b->state = 2;
+    if (cs->htrace)
+        cs->htr[0].push_back({b->seq, 'D',
+                              (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_begin.time_since_epoch()).count(),
+                              mono_ns()});
     return FDBCS_OK;
 }
 
@@ -2775,14 +2834,22 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
     if (b->state == 2 && !b->cs) return FDBCS_E_STATE;
     fdbcs_conflict_set* cs = b->cs;
     if (b->state == 2) {
+        const int64_t tw0 = cs->htrace ? mono_ns() : 0;
         HIPOK(hipSetDevice(cs->device));
         if (cs->pending_batch == b)  // its stage B still waits for the next detect: launch it now
             if (int rc = flush_pending(cs)) return rc;
         if (cs->work_y_batch == b)  // its Y is with the helper: issued (events and all) before reading them
             if (int rc = worker_wait(cs)) return rc;
-        // the epilogue's last workgroup publishes b->seq; poll it (checking the stream for errors)
+        // the epilogue publishes b->seq; poll it, checking the streams for errors only every ~2 ms:
+        // hipStreamQuery takes runtime locks the helper thread's launches need, so querying at
+        // the spin rate slows the submission of the batches behind this one
+        auto t_q = std::chrono::steady_clock::now();
         for (uint64_t spin = 0; *b->h_flag != b->seq; spin++) {
-            if ((spin & 1023) == 1023) {
+            __builtin_ia32_pause();
+            if ((spin & 4095) != 4095) continue;
+            if (std::chrono::steady_clock::now() - t_q < std::chrono::milliseconds(cs->wait_query_ms)) continue;
+            t_q = std::chrono::steady_clock::now();
+            {
                 // the flag comes from the epilogue (stage B's Y half): done or failing once both
                 // halves are idle
                 hipError_t e = hipStreamQuery(cs->astream);
@@ -2799,6 +2866,7 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        if (cs->htrace) cs->htr[0].push_back({b->seq, 'W', tw0, mono_ns()});
         if (cs->trace && cs->inflight == 1) {
             if (int rc = sync_all(cs)) return rc;
             unsigned long long tr[kTrSlots];

@@ -15,6 +15,13 @@ constexpr int kWG = 1024;          // single-workgroup kernels (scans, resolutio
 constexpr int kSortTile = 4096;    // endpoints per LDS sort tile (128 KiB of LDS)
 constexpr int kFan = 64;           // range-max fan-out per level (one wave per block)
 constexpr int kMaxLevels = 4;      // hv, max1 (/64), max2 (/4096), max3 (/262144)
+// Level 3 (the top, a few entries per tier) is built by atomicMax from every wave of the epilogue:
+// each entry is kept as kL3Rep replicas, one 128-byte line apart, written by different workgroups
+// and max-ed by the readers (one line took ~1000 atomics per entry: 89 of the 106 us of a 5M-base
+// rebuild, scripts/gpu_r05_k.sh).
+constexpr int kL3Rep = 8;
+constexpr int kL3Pad = 16;  // 8-byte words per replica line
+__host__ __device__ constexpr int64_t l3_words(int64_t n) { return n * kL3Rep * kL3Pad; }
 constexpr int kGcTile = 4096;      // history elements per GC / merge tile
 constexpr int kMaxGroupWrites = 12288;  // write groups: 8 bytes of resolver LDS per write
 constexpr int kMaxTxnLds = 49152;  // transactions whose status bytes fit the resolver's LDS (> the
@@ -151,7 +158,10 @@ constexpr int kSortMaxBuckets = 4096;
 constexpr int kQuant = 4096;
 constexpr int kQuantMinE = 2048;  // batches with fewer endpoints leave the quantiles as they are
 constexpr int kMaxSample = 8192;
-constexpr int kCntStride = 16;  // u64 words per sort bucket counter line
+#ifndef FDBCS_CNT_STRIDE
+#define FDBCS_CNT_STRIDE 16
+#endif
+constexpr int kCntStride = FDBCS_CNT_STRIDE;  // u64 words per sort bucket counter line
 // A splitter: the projection of an endpoint onto its first kSplitBytes key bytes (big-endian
 // words, zero past the key), min(len, kSplitBytes + 1), and for keys no longer than kSplitBytes
 // the class and id (meta).  Projections are monotone in the full order (keys tied on their first

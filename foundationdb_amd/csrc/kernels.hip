@@ -512,6 +512,17 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     return lo;
 }
 
+// Entry i of the top level (the max over its kL3Rep replicas).
+__device__ __forceinline__ int64_t l3_at(const int64_t* a, int64_t i) {
+    int64_t v[kL3Rep];
+#pragma unroll
+    for (int r = 0; r < kL3Rep; r++) v[r] = a[(i * kL3Rep + r) * kL3Pad];
+    int64_t best = v[0];
+#pragma unroll
+    for (int r = 1; r < kL3Rep; r++) best = v[r] > best ? v[r] : best;
+    return best;
+}
+
 // Max of lvl[0][lo, hi) through the 64-ary hierarchy; stops early once above `snap`.
 __device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
     int64_t best = LLONG_MIN;
@@ -519,7 +530,7 @@ __device__ __forceinline__ int64_t range_max(const MaxLevels& m, int64_t lo, int
         const int64_t* a = m.lvl[L];
         if (hi - lo <= 2 * kFan || L == kMaxLevels - 1) {
             for (int64_t i = lo; i < hi; i++) {
-                int64_t v = a[i];
+                int64_t v = L == kMaxLevels - 1 ? l3_at(a, i) : a[i];
                 best = v > best ? v : best;
                 if (best > snap) return best;
             }
@@ -754,7 +765,8 @@ __device__ __forceinline__ int64_t group_range_max(const MaxLevels& m, int64_t l
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int64_t k = base + u * kTierLanes + sl;
-                v[u] = k < cnt ? a[k < nl ? lo + k : rs + (k - nl)] : LLONG_MIN;
+                const int64_t ix = k < nl ? lo + k : rs + (k - nl);
+                v[u] = k >= cnt ? LLONG_MIN : (L == kMaxLevels - 1 ? l3_at(a, ix) : a[ix]);
             }
 #pragma unroll
             for (int u = 0; u < 8; u++) best = v[u] > best ? v[u] : best;
@@ -1946,6 +1958,12 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
         own1 = a.cnt[(size_t)kCntStride * bk + 1];
     }
     if (a.exp & 8) own0 = bk < nb ? (64ull | 16ull << 32) : 0ull, own1 = bk < nb ? (16ull | 16ull << 32) : 0ull;
+    // the bucket's first 128 slab slots, before its count arrives (slots past the count hold stale
+    // items of earlier batches and are masked once it has): one round trip instead of two
+    SortItem sp[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++)
+        if (bk < nb) sp[s] = a.slab[(size_t)bk * kSlab + s * 64 + lane];
     constexpr int kPreLoads = kSortMaxBuckets / kBlock;
     uint64_t c0[kPreLoads], c1[kPreLoads];
 #pragma unroll
@@ -1975,7 +1993,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             const int k = s * 64 + lane;
             kh[s] = kl[s] = ka[s] = ~0ull;  // padding sorts after every endpoint
             if (s < S && k < n) {
-                const SortItem it = a.slab[(size_t)bk * kSlab + k];
+                const SortItem it = s < 2 ? sp[s] : a.slab[(size_t)bk * kSlab + k];
                 if (c == 0) {
                     kh[s] = it.hi;
                     kl[s] = it.lo;
@@ -3435,7 +3453,7 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // the destination tier's top two levels, reset for the epilogue's atomicMax build (their
     // previous contents belonged to the history two batches back, which no check reads any more)
-    for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = gt; i < lvl3_n * kL3Rep; i += (int64_t)gridDim.x * blockDim.x) lvl3[i * kL3Pad] = LLONG_MIN;
     for (int64_t i = gt; i < lvl2_n; i += (int64_t)gridDim.x * blockDim.x) lvl2[i] = LLONG_MIN;
     if (threadIdx.x == 0) s_tile = atomicAdd(w.scan[kScanSegSum].counter, 1);
     __syncthreads();
@@ -3756,7 +3774,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
                                                            const int64_t* nd_ptr, int64_t hdr, Work w, int64_t* lvl3,
                                                            int64_t lvl3_n, int64_t* lvl2, int64_t lvl2_n) {
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (int64_t i = gt; i < lvl3_n; i += (int64_t)gridDim.x * blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = gt; i < lvl3_n * kL3Rep; i += (int64_t)gridDim.x * blockDim.x) lvl3[i * kL3Pad] = LLONG_MIN;
     for (int64_t i = gt; i < lvl2_n; i += (int64_t)gridDim.x * blockDim.x) lvl2[i] = LLONG_MIN;
     const int64_t j = gt / kArity;  // kArity lanes per delta boundary (cooperative search)
     const int64_t nd = *nd_ptr;
@@ -4280,10 +4298,13 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             const int64_t y = __shfl_xor(x, o, 64);
             x = y > x ? y : x;
         }
+#ifndef FDBCS_EPI_EXP
+#define FDBCS_EPI_EXP 0
+#endif
         if (lane == 0 && b1_0 < n1) {
-            atomicMax((long long*)&m.lvl[2][b1_0 / kFan], (long long)x);
-            int64_t* l3 = &m.lvl[3][b1_0 / ((int64_t)kFan * kFan)];
-            if (x > __hip_atomic_load(l3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            if (!(FDBCS_EPI_EXP & 1)) atomicMax((long long*)&m.lvl[2][b1_0 / kFan], (long long)x);
+            int64_t* l3 = &m.lvl[3][((b1_0 / ((int64_t)kFan * kFan)) * kL3Rep + (int64_t)(blockIdx.x % kL3Rep)) * kL3Pad];
+            if (!(FDBCS_EPI_EXP & 2) && x > __hip_atomic_load(l3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                 atomicMax((long long*)l3, (long long)x);
         }
     }
@@ -4444,7 +4465,7 @@ void launch_hold(hipStream_t s, const uint32_t* release) {
 }
 
 __global__ void k_lvl3_reset(int64_t* lvl3, int64_t n, int64_t* lvl2, int64_t n2) {
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) lvl3[i] = LLONG_MIN;
+    for (int64_t i = threadIdx.x; i < n * kL3Rep; i += blockDim.x) lvl3[i * kL3Pad] = LLONG_MIN;
     for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) lvl2[i] = LLONG_MIN;
 }
 
