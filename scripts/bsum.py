@@ -9,7 +9,7 @@ for f in sys.argv[1:]:
         print(f, "unreadable", e)
         continue
     g = lambda k: (d.get(k) or 0) / 1e6  # noqa: E731
-    print(f"{f}: value {d['value']/1e6:.2f}M total {g('total_txns_per_s'):.2f}M resident {g('device_resident_txns_per_s'):.2f}M "
+    print(f"{f}: value {d['value']/1e6:.2f}M total {g('total_txns_per_s'):.2f}M h2d {g('h2d_inclusive_txns_per_s'):.2f}M "
           f"sync {g('sync_txns_per_s'):.2f}M devbound {(d.get('device_bound') or {}).get('txns_per_s', 0)/1e6:.2f}M")
     p = d.get("parity") or {}
     print(f"  parity {p.get('batches_checked')}/{p.get('batches_total')} bad {p.get('mismatched_batches')} mix {d.get('verdict_mix')}")
