@@ -138,10 +138,10 @@ inline int64_t mono_ns() {
 // validation and normalization into pinned staging split over chunks of transactions.  The
 // calling thread works too.  A ticket carries the job's generation, so a worker that wakes late
 // never takes a ticket of a later job with the earlier job's function.  Between jobs a worker
-// spins for ~kSpinUs before sleeping on the condition variable: a resolver adds a batch every
+// spins for ~spin_us before sleeping on the condition variable: a resolver adds a batch every
 // ~0.1 ms, and a wake-up through the condition variable costs ~10-20 us (scripts/add_sweep.py).
 struct AddPool {
-    static constexpr int kSpinUs = 300;
+    int spin_us = 0;  // FDBCS_ADD_SPIN_US (0: sleep at once; scripts/gpu_r05_o.sh: 300 us of spinning measured no better)
     std::vector<std::thread> th;
     std::mutex m;
     std::condition_variable cv;
@@ -154,6 +154,7 @@ struct AddPool {
     bool stop = false;
 
     explicit AddPool(int workers) {
+        if (const char* v = getenv("FDBCS_ADD_SPIN_US")) spin_us = std::max(0, atoi(v));
         for (int i = 0; i < workers; i++) th.emplace_back([this] { worker(); });
     }
     ~AddPool() {
@@ -182,7 +183,7 @@ struct AddPool {
             // spin a while for the next job, then sleep
             const auto t0 = std::chrono::steady_clock::now();
             while (gen.load(std::memory_order_acquire) == seen &&
-                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs))
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us))
                 __builtin_ia32_pause();
             uint32_t g;
             int nn;
