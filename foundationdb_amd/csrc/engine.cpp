@@ -2888,6 +2888,8 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
                     us(kTrPartBegin, kTrBktBegin));
             {
                 const double nw = tr[kTrBktWaves] ? (double)tr[kTrBktWaves] : 1.0;
+                fprintf(stderr, "fdbcs trace: bucket tie runs: %llu lanes in runs, %llu ranked in registers, %llu serially, "
+                        "longest run %llu\n", tr[kTrBktRuns], tr[kTrBktSimple], tr[kTrBktSlow], tr[kTrBktMaxRun]);
                 fprintf(stderr,
                         "fdbcs trace: bucket per wave (%llu waves): load %.2f, sort %.2f, ties %.2f, put %.2f us\n",
                         tr[kTrBktWaves], tr[kTrBktSumLoad] / nw / 100.0, tr[kTrBktSumSort] / nw / 100.0,

@@ -276,6 +276,8 @@ enum TraceSlot {
     kTrResSetup, kTrResRound1,  // k_resolve: statuses and members staged; first round done
     kTrResMin1,  // k_resolve: the first round's group minima done
     kTrResW0min, kTrResW0max,  // k_resolve: first instruction of its first / last wave (before kernargs)
+    kTrBktRuns, kTrBktSimple, kTrBktSlow, kTrBktMaxRun,  // k_sort_bucket tie runs: lanes in a run, ranked
+                                                         // in registers, by the serial path; longest run
     kTrSlots
 };
 __device__ __forceinline__ void trace_min(unsigned long long* tr, int slot) {

@@ -1964,10 +1964,12 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
 #pragma unroll
     for (int s = 0; s < 2; s++)
         if (bk < nb) sp[s] = a.slab[(size_t)bk * kSlab + s * 64 + lane];
-    constexpr int kPreLoads = kSortMaxBuckets / kBlock;
-    uint64_t c0[kPreLoads], c1[kPreLoads];
+    // (the first kPreHeld chunks stay in registers across the sort, enough for nb <= 1536 buckets,
+    // ~98k endpoints; larger batches load the rest after it)
+    constexpr int kPreLoads = kSortMaxBuckets / kBlock, kPreHeld = 6;
+    uint64_t c0[kPreHeld], c1[kPreHeld];
 #pragma unroll
-    for (int u = 0; u < kPreLoads; u++) {
+    for (int u = 0; u < kPreHeld; u++) {
         const int k = threadIdx.x + u * kBlock;
         const bool in = k < nb && !(a.exp & 8);  // (exp 8: cost breakdown only)
         c0[u] = in ? a.cnt[(size_t)kCntStride * k] : 0;
@@ -2112,38 +2114,63 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
                         fin[s] = st + rank;
                         todo = false;
                     }
+                    if (a.trace && in_run) {
+                        atomicAdd(&a.trace[kTrBktRuns], 1ull);
+                        if (simple && !fallback) atomicAdd(&a.trace[kTrBktSimple], 1ull);
+                        if (todo) atomicAdd(&a.trace[kTrBktSlow], 1ull);
+                        atomicMax(&a.trace[kTrBktMaxRun], (unsigned long long)(en - st + 1));
+                    }
                     if (!todo) continue;
-                    // The two endpoints of one range (a point range [k, k\0], a prefix range
-                    // [p\0, p\xff]): begin <= end holds for every admitted range, so keys that
-                    // differ at all order begin first — different lengths, or (equality needs no
-                    // order) different last tail words, one load each instead of the whole
-                    // tails.  Other pairs compare whole keys.
+                    // Runs the register ranking above cannot take (crossing a 64-position slot, longer
+                    // than 16, or keys past the tail words held): every partner's key and tail words
+                    // are loaded, two partners at a time with all their loads in flight, and compared
+                    // against this lane's in registers (C4: ~50 lanes a batch, whose serial loads of
+                    // one partner after another set the launch's length).  Keys past the held words
+                    // compare whole (item_less_total).
                     const int pm = ps[s];
                     kme = b.keys[pm];
-                    bool need_me = false;
-                    int differ = -1;  // position of the same range's other endpoint when its key differs
+                    QTail tme;
+                    load_qtail(tme, kme, b.tail);
+                    const bool mlong = kme.len > 16u + 8u * kQW;
                     rank = 0;
-                    for (int j = st; j <= en; j++) {
-                        if (j == k) continue;
-                        const int po = s_p[wave][j];
-                        if ((po >> 1) == (pm >> 1)) {
-                            const DKey ko = b.keys[po];
-                            const uint32_t tl = kme.len - 16u;  // tied keys are longer than 19 bytes
-                            if (ko.len != kme.len ||
-                                tail_last(b.tail + ko.tail, tl) != tail_last(b.tail + kme.tail, tl)) {
-                                rank += (po & 1) ? 0 : 1;
-                                differ = j;  // (a range has one other endpoint)
+                    for (int j0 = st; j0 <= en; j0 += 2) {
+                        int po[2];
+                        DKey ko[2];
+                        QTail tq[2];
+#pragma unroll
+                        for (int u = 0; u < 2; u++) po[u] = (j0 + u <= en && j0 + u != k) ? s_p[wave][j0 + u] : -1;
+#pragma unroll
+                        for (int u = 0; u < 2; u++)
+                            if (po[u] >= 0) ko[u] = b.keys[po[u]];
+#pragma unroll
+                        for (int u = 0; u < 2; u++)
+                            if (po[u] >= 0) load_qtail(tq[u], ko[u], b.tail);
+#pragma unroll
+                        for (int u = 0; u < 2; u++) {
+                            if (po[u] < 0) continue;
+                            if (mlong || ko[u].len > 16u + 8u * kQW) {
+                                rank += item_less_total(make_item(b, po[u]), make_item(b, pm), b.tail) ? 1 : 0;
                                 continue;
                             }
-                        }
-                        need_me = true;
-                    }
-                    if (need_me) {
-                        const SortItem me = make_item(b, pm);
-                        for (int j = st; j <= en; j++) {
-                            if (j == k || j == differ) continue;
-                            const int po = s_p[wave][j];
-                            rank += item_less_total(make_item(b, po), me, b.tail) ? 1 : 0;
+                            // tied keys share bytes [0, c + 19 > 16): tails from byte 16, then
+                            // length, class, endpoint id (item_less_total's order)
+                            const uint32_t nbytes = (ko[u].len < kme.len ? ko[u].len : kme.len) - 16u;
+                            int cmpv = 0;
+#pragma unroll
+                            for (int w = 0; w < kQW; w++) {
+                                const int vb = (int)nbytes - 8 * w;
+                                if (cmpv == 0 && vb > 0) {
+                                    const uint64_t msk = vb >= 8 ? ~0ull : ~0ull << (64 - 8 * vb);
+                                    const uint64_t x = tq[u].w[w] & msk, y = tme.w[w] & msk;
+                                    if (x != y) cmpv = x < y ? -1 : 1;
+                                }
+                            }
+                            if (cmpv == 0) cmpv = ko[u].len < kme.len ? -1 : (ko[u].len > kme.len ? 1 : 0);
+                            if (cmpv == 0) {
+                                const uint32_t pc = item_class(endpoint_meta(b, po[u]));
+                                cmpv = pc < mcls ? -1 : (pc > mcls ? 1 : (po[u] < pm ? -1 : 1));
+                            }
+                            rank += cmpv < 0 ? 1 : 0;
                         }
                     }
                     fin[s] = st + rank;
@@ -2175,7 +2202,10 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
 #pragma unroll
         for (int u = 0; u < kPreLoads; u++) {
             const int k = threadIdx.x + u * kBlock;
-            const uint32_t v[4] = {(uint32_t)c0[u], (uint32_t)(c0[u] >> 32), (uint32_t)c1[u], (uint32_t)(c1[u] >> 32)};
+            if (u >= kPreHeld && (k >= nb || (a.exp & 8))) continue;
+            const uint64_t x0 = u < kPreHeld ? c0[u < kPreHeld ? u : 0] : a.cnt[(size_t)kCntStride * k];
+            const uint64_t x1 = u < kPreHeld ? c1[u < kPreHeld ? u : 0] : a.cnt[(size_t)kCntStride * k + 1];
+            const uint32_t v[4] = {(uint32_t)x0, (uint32_t)(x0 >> 32), (uint32_t)x1, (uint32_t)(x1 >> 32)};
 #pragma unroll
             for (int c = 0; c < 4; c++) {
                 tot[c] += v[c];
