@@ -15,6 +15,7 @@
 #include <cxxabi.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -341,15 +342,24 @@ struct fdbcs_conflict_set {
                               // even for batches with keys over 16 bytes (A/B)
     int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
     bool directory = true;  // FDBCS_DIRECTORY=0: base-tier lookups descend the whole sample tree (A/B)
-    // Bytes every loaded key shares ahead of the directory's 16 bits (MaxLevels::dir_p, with
-    // FDBCS_DIR_PREFIX=1): the load's common prefix, capped at 14.  Keys written later outside it
-    // take the directories' end slots (dir_slot), so the mapping stays monotone.  Off by default:
-    // at C4 the bytes after the 9-byte prefix are decimal digits (100 slots of ~7.8k samples), and
-    // the tree levels the wide-slot start skips are cache hits: the base check isolated 57.5 ->
-    // 59.5 us with it, the pipeline within noise (scripts/gpu_r04_final2.sh).
-    bool dir_prefix = false;
+    // Directory code (MaxLevels::dir_p .. dir_w; set_dir_map): with FDBCS_DIR_RANK=1 (default)
+    // the loaded keys' common prefix (capped at 15) and the value range of each byte position
+    // after it, as many positions as fit the slot budget (dir_bits); FDBCS_DIR_RANK=0: the first
+    // two key bytes (the round-4 directory, A/B).  Keys
+    // written later outside the loaded values take neighbouring codes, so the mapping stays
+    // monotone.  Round 4's prefix-only variant (16 bits after the prefix: C4's decimal digits gave
+    // 100 slots of ~7.8k samples) is the special case the rank tables replace.
+    bool dir_rank = true;
     uint32_t dir_p = 0;
     uint64_t dir_phi = 0, dir_plo = 0;
+    uint32_t dir_e = 0, dir_top = 0;
+    uint32_t dir_pos[kDirPos] = {}, dir_w[kDirPos] = {};
+    // FDBCS_DIR_BITS: slot budget 2^bits.  0 (default): 2^16, doubled while the base has over
+    // eight level-0 samples per slot (C4: 2^17; a slot of up to 16 samples is counted directly).
+    // A directory is read cold by every batch's check, so a larger one costs cache misses: C2's
+    // isolated check 11.0 us at 2^16, 16.4 at 2^18; C4's 57.3 at 2^17, 62 at 2^19 and 2^20, 64 on
+    // the first two bytes.
+    int dir_bits = 0;
     DBuf trace_buf;
     // Per-kernel device time (fdbcs_kernel_profile): launches and milliseconds by kernel, from the
     // events of timing level 3 (every kernel) or of the timed kernel at level 1.
@@ -725,6 +735,97 @@ int64_t index_bytes(int64_t cap) {
     return 16 * (n + cap / 8 + 2);
 }
 
+static void set_dir_fields(const fdbcs_conflict_set* cs, MaxLevels& m) {
+    m.dir_p = cs->dir_p;
+    m.dir_phi = cs->dir_phi;
+    m.dir_plo = cs->dir_plo;
+    m.dir_e = cs->dir_e;
+    m.dir_top = cs->dir_top;
+    for (int i = 0; i < kDirPos; i++) m.dir_pos[i] = cs->dir_pos[i], m.dir_w[i] = cs->dir_w[i];
+}
+
+// The directory code of the keys k[0..n) (sorted): their common prefix and, after it, the range
+// of byte values at each position while the product of the ranges fits the slot budget (the last
+// position coarsened by a shift).  See MaxLevels::dir_p.  Large loads are sampled (at most ~2M
+// keys); values outside a position's range get the range's end codes.
+static int set_dir_map(fdbcs_conflict_set* cs, const ulonglong2* k, int64_t n) {
+    auto byte_at = [](const ulonglong2& x, int i) -> uint32_t {
+        return i < 8 ? (uint32_t)(x.x >> (56 - 8 * i)) & 255u : (uint32_t)(x.y >> (56 - 8 * (i - 8))) & 255u;
+    };
+    const bool rank = cs->dir_rank && n >= 2;
+    uint32_t p = 0;
+    if (rank) {
+        const uint64_t xh = k[0].x ^ k[n - 1].x, xl = k[0].y ^ k[n - 1].y;
+        const uint32_t lcp = xh ? (uint32_t)__builtin_clzll(xh) / 8 : (xl ? 8 + (uint32_t)__builtin_clzll(xl) / 8 : 16);
+        p = std::min<uint32_t>(lcp, 15);
+    }
+    const uint64_t mh = p >= 8 ? ~0ull : (p ? ~0ull << (64 - 8 * p) : 0ull);
+    const uint64_t ml = p <= 8 ? 0ull : ~0ull << (128 - 8 * p);
+    cs->dir_p = p;
+    cs->dir_phi = n ? k[0].x & mh : 0;
+    cs->dir_plo = n ? k[0].y & ml : 0;
+    const int npos = std::min<int>(kDirPos, 16 - (int)p);
+    uint32_t lo[kDirPos], hi[kDirPos];
+    for (int i = 0; i < kDirPos; i++) lo[i] = rank ? 255 : 0, hi[i] = 255;
+    if (rank) {
+        for (int i = 0; i < kDirPos; i++) hi[i] = 0;
+        const int64_t stride = std::max<int64_t>(1, n / (1 << 21));
+        auto mark = [&](const ulonglong2& x) {
+            for (int i = 0; i < npos; i++) {
+                const uint32_t b = byte_at(x, (int)p + i);
+                lo[i] = std::min(lo[i], b);
+                hi[i] = std::max(hi[i], b);
+            }
+        };
+        for (int64_t j = 0; j < n; j += stride) mark(k[j]);
+        mark(k[n - 1]);
+    }
+    const int64_t samples = (n + kFan - 1) / kFan;
+    uint64_t budget = 1ull << 16;
+    if (cs->dir_bits)
+        budget = 1ull << cs->dir_bits;
+    else if (cs->dir_rank)
+        while (budget < (1ull << kDirMaxBits) && 8 * budget < (uint64_t)samples) budget <<= 1;
+    uint32_t radix[kDirPos], shift[kDirPos];
+    uint64_t prod = 1;
+    int e = 0;
+    for (int i = 0; i < npos; i++) {
+        const uint32_t d = hi[i] - lo[i] + 1;
+        shift[i] = 0;
+        if (prod * d <= budget) {
+            radix[i] = d;
+            prod *= d;
+            if (d > 1) e = i + 1;  // trailing single-value positions add nothing
+            continue;
+        }
+        uint32_t s = 0;  // coarsen: digit >> s, radix ((d - 1) >> s) + 1
+        while (prod * (((d - 1) >> s) + 1) > budget) s++;
+        if (((d - 1) >> s) + 1 > 1) {
+            radix[i] = ((d - 1) >> s) + 1;
+            shift[i] = s;
+            e = i + 1;
+        }
+        break;
+    }
+    prod = 1;
+    for (int i = 0; i < e; i++) prod *= radix[i];
+    uint64_t w = 1;
+    for (int i = kDirPos - 1; i >= 0; i--) {
+        if (i >= e) {
+            cs->dir_pos[i] = cs->dir_w[i] = 0;
+            continue;
+        }
+        cs->dir_pos[i] = lo[i] | (hi[i] - lo[i] + 1) << 8 | shift[i] << 17;
+        cs->dir_w[i] = (uint32_t)w;
+        w *= radix[i];
+    }
+    cs->dir_e = (uint32_t)e;
+    // codes run over [0, prod] (prod: above the range at the first position), slots are code + 1,
+    // 0 below the common prefix and prod + 2 above it
+    cs->dir_top = (uint32_t)prod + 2;
+    return FDBCS_OK;
+}
+
 MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     MaxLevels m;
     m.lvl[0] = (int64_t*)cs->hver[k].p;
@@ -732,9 +833,7 @@ MaxLevels levels_of(fdbcs_conflict_set* cs, int k) {
     m.keys = (const ulonglong2*)cs->hkey[k].p;
     carve_index(m, (ulonglong2*)cs->lvl[0].p, cs->hist_cap);
     m.dir = cs->directory ? (const int32_t*)cs->dir.p : nullptr;
-    m.dir_p = cs->dir_p;
-    m.dir_phi = cs->dir_phi;
-    m.dir_plo = cs->dir_plo;
+    set_dir_fields(cs, m);
     return m;
 }
 
@@ -754,9 +853,7 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     carve_index(m, (ulonglong2*)cs->dlvl[k][0].p, cs->delta_cap);
     m.edir = (uint64_t*)cs->edir[k].p;
     m.edir_epoch = cs->edir[k].p ? cs->ddir_epoch[k] : 0;
-    m.dir_p = cs->dir_p;  // the delta's directory slots too (the epilogue's fill)
-    m.dir_phi = cs->dir_phi;
-    m.dir_plo = cs->dir_plo;
+    set_dir_fields(cs, m);  // the delta's directory slots too (the epilogue's fill)
     return m;
 }
 
@@ -852,7 +949,7 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
         cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
         if ((rc = grow_sets(cs, cs->hkey, cs->hlt, cs->hver, cs->cur, cs->n_ub, cap))) return rc;
         if ((rc = alloc_levels(cs->lvl, cap, &cs->lvl3_n, &cs->lvl2_n))) return rc;
-        if (cs->directory && (rc = cs->dir.ensure(4 * ((size_t)kDirSlots + 1)))) return rc;
+        if (cs->directory && (rc = cs->dir.ensure(4 * (size_t)kDirAlloc))) return rc;
         cs->hist_cap = cap;
         launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n,
                         cs->lvl3_n, cs->lvl2_n, std::max<int64_t>(cs->n_ub, 1));
@@ -1349,7 +1446,8 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_HELPER_Y")) cs->helper_y = v[0] != '0';
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
-    if (const char* v = getenv("FDBCS_DIR_PREFIX")) cs->dir_prefix = v[0] == '1';
+    if (const char* v = getenv("FDBCS_DIR_RANK")) cs->dir_rank = v[0] != '0';
+    if (const char* v = getenv("FDBCS_DIR_BITS")) cs->dir_bits = std::max(0, std::min(kDirMaxBits, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
@@ -1388,10 +1486,11 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (!rc) rc = cs->quant.ensure(2 * sizeof(SplitKey) * kQuant);
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
     for (int k = 0; k < 2 && !rc && cs->directory; k++) {  // zeroed: epoch 0 entries are never trusted
-        rc = cs->edir[k].ensure(8 * ((size_t)kDirSlots + 1));
-        if (!rc && hipMemsetAsync(cs->edir[k].p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream) != hipSuccess)
+        rc = cs->edir[k].ensure(8 * (size_t)kDirAlloc);
+        if (!rc && hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream) != hipSuccess)
             rc = FDBCS_E_DEVICE;
     }
+    if (!rc) rc = set_dir_map(cs, nullptr, 0);
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
     if (!rc) rc = ensure_delta(cs, 1 << 14);
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
@@ -1498,8 +1597,7 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     cs->header_version = version;
     cs->max_written = version;
     cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;
-    cs->dir_p = 0;
-    cs->dir_phi = cs->dir_plo = 0;
+    if (int rc = set_dir_map(cs, nullptr, 0)) return rc;
     cs->prev_segs = false;
     cs->n_ub = 0;
     cs->nd_ub = 0;
@@ -1603,19 +1701,8 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     s.n = n;
     s.tail_used = (int64_t)tail.size();
     HIPOK(hipMemcpyAsync(cs->scal.p, &s, sizeof(s), hipMemcpyHostToDevice, cs->stream));
-    // the directory skips the bytes the first and last keys' (zero-padded) prefixes share
-    cs->dir_p = 0;
-    cs->dir_phi = cs->dir_plo = 0;
-    if (cs->dir_prefix && n >= 2) {
-        const uint64_t xh = k[0].x ^ k[n - 1].x, xl = k[0].y ^ k[n - 1].y;
-        const uint32_t lcp = xh ? (uint32_t)__builtin_clzll(xh) / 8 : (xl ? 8 + (uint32_t)__builtin_clzll(xl) / 8 : 16);
-        cs->dir_p = std::min<uint32_t>(lcp, 14);
-        const uint32_t p = cs->dir_p;
-        const uint64_t mh = p >= 8 ? ~0ull : (p ? ~0ull << (64 - 8 * p) : 0ull);
-        const uint64_t ml = p <= 8 ? 0ull : ~0ull << (128 - 8 * p);
-        cs->dir_phi = k[0].x & mh;
-        cs->dir_plo = k[0].y & ml;
-    }
+    // the directory code of the loaded keys (k_directory below builds on it)
+    if (int rc = set_dir_map(cs, k.data(), n)) return rc;
     launch_rangemax(cs->stream, levels_of(cs, cs->cur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->n, cs->lvl3_n,
                     cs->lvl2_n, std::max<int64_t>(n, 1));
     HIPOK(take_launch_error());
@@ -2408,7 +2495,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // the delta directory's 32-bit epoch tag is about to wrap: clear every entry (once per 2^32
         // batches) so that no entry left by an old fill can carry the reused epoch value
         if ((rc = sync_all(cs))) return rc;
-        for (int k = 0; k < 2; k++) HIPOK(hipMemsetAsync(cs->edir[k].p, 0, 8 * ((size_t)kDirSlots + 1), cs->stream));
+        for (int k = 0; k < 2; k++) HIPOK(hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream));
         HIPOK(hipStreamSynchronize(cs->stream));
         cs->ddir_counter = 0;
     }

@@ -45,8 +45,10 @@ struct Hist {
 // lookup descends the tree with kArity cooperating lanes, one node (one 128-byte line at A = 8) per
 // level, and lands in one 64-boundary block.
 constexpr int kArity = 8;
-constexpr int kDirSlots = 1 << 16;  // radix directory slots (first two key bytes) of a tier
-constexpr int kDirRun = 64;         // delta directory: slots one sample fills at most (the rest stay stale)
+constexpr int kDirMaxBits = 20;     // radix directory: at most 2^20 code values (+3 end slots) per tier
+constexpr int kDirAlloc = (1 << kDirMaxBits) + 4;  // directory entries allocated (dir, edir)
+constexpr int kDirPos = 8;          // byte positions after the common prefix a directory code reads
+constexpr int kDirRun = 128;        // delta directory: slots one sample fills at most (the rest stay stale)
 constexpr int kIdxLevels = 12;  // A^11 * 64 * A boundaries under an A-entry top level
 struct MaxLevels {
     int64_t* lvl[kMaxLevels];       // lvl[0] == current Hist::ver
@@ -55,14 +57,24 @@ struct MaxLevels {
     ulonglong2* skey8;              // [ceil(n / 8)] prefix of every 8th boundary: the level below skey[0]
     int64_t idx_cap;                // capacity the levels were carved for: skey[L] = skey[0] + sum of
                                     // idx_level_cap(idx_cap, l < L), computable without indexing skey[]
-    const int32_t* dir = nullptr;   // [65537] radix directory over skey[0] (base tier; k_directory)
-    // Directory slots (kernels.hip dir_slot): the 16 bits after the first dir_p bytes the loaded
-    // keys share (dir_phi, dir_plo: those bytes, the rest zero), so keys under one long common
-    // prefix (C4: 9 bytes) still spread over the slots; 0 = the first two bytes.  Fixed when the
-    // history is loaded; used by both tiers.
+    const int32_t* dir = nullptr;   // [dir_top + 2] radix directory over skey[0] (base tier; k_directory)
+    // Directory slots (kernels.hip dir_slot), an order-preserving code of the 16-byte prefix fixed
+    // when the history is loaded (engine.cpp set_dir_map) and used by both tiers: keys outside the
+    // dir_p bytes every loaded key shares (dir_phi, dir_plo: those bytes, the rest zero) take slot
+    // 0 (below) or dir_top (above); inside, the next dir_e byte positions are read as a mixed-radix
+    // number whose digit at position i is the byte's offset in the range [lo, lo + d) of values
+    // the loaded keys hold there (dir_pos[i] = lo | d << 8 | s << 17, weight dir_w[i]; a byte
+    // below the range counts 0 and one above it d, and either ends the code; the last position
+    // may be coarsened by >> s to fit the slot budget), so C4's decimal user digits after a 9-byte
+    // common prefix spread over 10^6 slots instead of 100.  Arithmetic only: no table loads on the
+    // lookup's chain.
     uint32_t dir_p = 0;
     uint64_t dir_phi = 0, dir_plo = 0;
-    uint64_t* edir = nullptr;       // [65537] delta tier's directory, entries (epoch << 32 | count),
+    uint32_t dir_e = 0;
+    uint32_t dir_top = 0;
+    uint32_t dir_pos[kDirPos] = {};
+    uint32_t dir_w[kDirPos] = {};
+    uint64_t* edir = nullptr;       // [dir_top + 2] delta tier's directory, entries (epoch << 32 | count),
     uint32_t edir_epoch = 0;        // filled by k_epilogue; lookups trust entries of this epoch (0: off)
 };
 __host__ __device__ inline int64_t idx_level_cap(int64_t cap, int L) {

@@ -332,27 +332,34 @@ __device__ __forceinline__ uint32_t gmask(bool pred) {
     return (uint32_t)(m >> (threadIdx.x & 63 & ~(kArity - 1))) & ((1u << kArity) - 1u);
 }
 
-// Radix directory of the base tier (k_directory): its slot is the 16 bits after the first
-// m.dir_p bytes of a 16-byte prefix, bytes every base key shares (MaxLevels::dir_p).
-__host__ __device__ __forceinline__ uint32_t dir_bits(uint64_t hi, uint64_t lo, uint32_t p) {
-    if (p == 0) return (uint32_t)(hi >> 48);
-    if (p < 8) return (uint32_t)(((hi << (8 * p)) | (lo >> (64 - 8 * p))) >> 48);
-    return (uint32_t)((lo << (8 * (p - 8))) >> 48);
-}
-// Directory slot of a 16-byte prefix, monotone over all keys: with a shared prefix (dir_p > 0),
-// keys below it take slot 0, keys above it slot 0xffff, and keys under it their bits clamped to
-// [1, 0xfffe]; without one, the first two bytes.  Both tiers' directories (k_directory, the
-// epilogue's delta fill) and every lookup use it.
+// Directory slot of a 16-byte prefix (MaxLevels::dir_p .. dir_w), monotone over all keys: keys
+// below the loaded keys' common prefix take slot 0, keys above it dir_top, keys under it 1 + the
+// mixed-radix code of the next dir_e bytes (each byte's offset in its position's value range; the
+// code ends at the first byte outside its range).  ALU only.  Both tiers' directories
+// (k_directory, the epilogue's delta fill) and every lookup use it.
 __device__ __forceinline__ uint32_t dir_slot(const MaxLevels& m, uint64_t hi, uint64_t lo) {
     const uint32_t p = m.dir_p;
-    if (p == 0) return (uint32_t)(hi >> 48);
-    const uint64_t mh = p >= 8 ? ~0ull : ~0ull << (64 - 8 * p);
-    const uint64_t ml = p <= 8 ? 0ull : ~0ull << (128 - 8 * p);
-    const uint64_t xh = hi & mh, xl = lo & ml;
-    if (xh != m.dir_phi || xl != m.dir_plo)
-        return (xh < m.dir_phi || (xh == m.dir_phi && xl < m.dir_plo)) ? 0u : 0xffffu;
-    const uint32_t v = dir_bits(hi, lo, p);
-    return v < 1u ? 1u : (v > 0xfffeu ? 0xfffeu : v);
+    if (p) {
+        const uint64_t mh = p >= 8 ? ~0ull : ~0ull << (64 - 8 * p);
+        const uint64_t ml = p <= 8 ? 0ull : ~0ull << (128 - 8 * p);
+        const uint64_t xh = hi & mh, xl = lo & ml;
+        if (xh != m.dir_phi || xl != m.dir_plo)
+            return (xh < m.dir_phi || (xh == m.dir_phi && xl < m.dir_plo)) ? 0u : m.dir_top;
+    }
+    // the bytes after the prefix, left-aligned: position p + i is byte i of h
+    const uint64_t h = p == 0 ? hi : (p < 8 ? (hi << (8 * p)) | (lo >> (64 - 8 * p)) : lo << (8 * (p - 8)));
+    uint32_t code = 1;
+    bool live = true;
+#pragma unroll
+    for (int i = 0; i < kDirPos; i++) {
+        const uint32_t b = (uint32_t)(h >> (56 - 8 * i)) & 255u;
+        const uint32_t pos = m.dir_pos[i];
+        const uint32_t l = pos & 255u, d = (pos >> 8) & 511u, s = pos >> 17;
+        const uint32_t r = b < l ? 0u : (b - l < d ? b - l : d);
+        if (live && (uint32_t)i < m.dir_e) code += (r >> s) * m.dir_w[i];
+        live = live && b >= l && b - l < d;
+    }
+    return code;
 }
 
 // LONG: the long-key probes above (the batch has keys over 16 bytes); same result.
@@ -4317,7 +4324,8 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
                               c = (int64_t)dir_slot(m, sk.x, sk.y);
                 for (int64_t v = a + 1; v <= c && v <= a + kDirRun; v++) m.edir[v] = tag | (uint64_t)b1l;
                 if (b1l == n1 - 1)
-                    for (int64_t v = c + 1; v <= kDirSlots && v <= c + kDirRun; v++) m.edir[v] = tag | (uint64_t)n1;
+                    for (int64_t v = c + 1; v <= (int64_t)m.dir_top + 1 && v <= c + kDirRun; v++)
+                        m.edir[v] = tag | (uint64_t)n1;
             }
         }
         // the wave's maximum into levels 2 and 3; level 3 only when above what it already holds
@@ -4508,15 +4516,14 @@ static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
 }
 
 // Radix directory of the base tier (D.CheckRead): dir[v] = number of level-0 samples (keys[64 j],
-// j < ceil(n / 64)) whose first two key bytes are below v, v in [0, 65536].  A lookup whose slot
+// j < ceil(n / 64)) whose directory slot (dir_slot) is below v, v in [0, dir_top + 1].  A lookup whose slot
 // holds at most two sample groups starts at level 0 (one directory load, one or two group loads)
 // instead of descending the ~6 levels above it; slots crowded by shared key prefixes (subspaces,
 // hot ranges) take the tree.  Rebuilt with the base tier's index (compaction, GC, load), one
 // binary search per slot.
-// (slots by dir_slot: the bits after the loaded keys' shared prefix, when there is one)
 __global__ __launch_bounds__(kBlock) void k_directory(MaxLevels m, const int64_t* np) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v > kDirSlots) return;
+    if (v > (int)m.dir_top + 1) return;
     const ulonglong2* keys = m.keys;
     int32_t* dir = const_cast<int32_t*>(m.dir);
     const int64_t S = (*np + kFan - 1) / kFan;
@@ -4534,7 +4541,7 @@ __global__ __launch_bounds__(kBlock) void k_directory(MaxLevels m, const int64_t
 
 static void launch_directory(hipStream_t s, const MaxLevels& m, const int64_t* n) {
     if (!m.dir) return;
-    fdb_launch(k_directory, dim3((kDirSlots + kBlock) / kBlock), dim3(kBlock), 0, s, m, n);
+    fdb_launch(k_directory, dim3((m.dir_top + 1 + kBlock) / kBlock), dim3(kBlock), 0, s, m, n);
 }
 
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,

@@ -302,25 +302,28 @@ def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split,
 
 
 @pytest.mark.parametrize("lanes", ["1", "0"])
-@pytest.mark.parametrize("dir_prefix,alphabet", [("1", "bytes"), ("1", "digits"), ("0", "digits")])
-def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_prefix, alphabet, lanes):
-    """The base tier's radix directory keyed on the 16 bits after the bytes every loaded key shares
-    (MaxLevels::dir_p; C4's 9-byte prefix): 120k boundaries under one 10-byte prefix, queries inside
-    it, below and above it at every depth, keys shorter than it and the empty key; writes outside
-    the prefix, which both tiers' directories file under their end slots (dir_slot), before and
-    after the compactions that bring them into the base.  alphabet "digits": the bytes after the prefix are
-    decimal digits (C4's user ids), so the directory bits take 100 values and its slots are too
-    wide to count directly: the per-lane descent starts below the top of the tree, bounded by the
-    slot.  dir_prefix "0": the first two bytes (the default; FDBCS_DIR_PREFIX)."""
-    monkeypatch.setenv("FDBCS_DIR_PREFIX", dir_prefix)
+@pytest.mark.parametrize("dir_rank,alphabet", [("1", "bytes"), ("1", "digits"), ("1", "sparse"), ("0", "digits")])
+def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_rank, alphabet, lanes):
+    """The radix directories' rank code after the bytes every loaded key shares (MaxLevels::dir_p;
+    C4's 9-byte prefix): 120k boundaries under one 10-byte prefix, queries inside it, below and
+    above it at every depth, keys shorter than it and the empty key; writes outside the prefix,
+    which both tiers' directories file under their end slots (dir_slot), before and after the
+    compactions that bring them into the base.  alphabet "digits": the bytes after the prefix are
+    decimal digits (C4's user ids), ten ranks per position; "sparse": the history holds only even
+    byte values in [0x20, 0x7e] while queries and writes take any value in [0x10, 0x90], so codes
+    end at unseen values (the next seen value's rank) and values above every seen one carry into
+    the position before.  dir_rank "0": the first two bytes (FDBCS_DIR_RANK=0)."""
+    monkeypatch.setenv("FDBCS_DIR_RANK", dir_rank)
     monkeypatch.setenv("FDBCS_LONG_LANES", lanes)
     rng = np.random.default_rng(77)
     P = bytes([0x41, 0x42, 0x43, 0x44, 0x00, 0xff, 0x45, 0x46, 0x47, 0x48])
-    lo_b, hi_b = (0, 256) if alphabet == "bytes" else (0x30, 0x3a)
+    lo_b, hi_b = {"bytes": (0, 256), "digits": (0x30, 0x3a), "sparse": (0x10, 0x91)}[alphabet]
 
     long_keys = [False]  # batches alternate: keys up to 21 bytes (short-key lookups), up to 30
 
-    def suffix(n):
+    def suffix(n, hist=False):
+        if hist and alphabet == "sparse":
+            return bytes((2 * rng.integers(0x10, 0x40, size=n)).astype(np.uint8))
         return bytes(rng.integers(lo_b, hi_b, size=n).astype(np.uint8))
 
     def inside():
@@ -340,7 +343,7 @@ def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_prefi
             return P[:d]
         return P[:d] + bytes([x]) + bytes(rng.integers(0, 256, size=int(rng.integers(0, 8))).astype(np.uint8))
 
-    hist = sorted({P + suffix(6) for _ in range(120000)})
+    hist = sorted({P + suffix(6, hist=True) for _ in range(120000)})
     kb = np.frombuffer(b"".join(hist), np.uint8)
     ko = np.zeros(len(hist) + 1, np.int64)
     np.cumsum([len(k) for k in hist], out=ko[1:])
