@@ -2630,13 +2630,17 @@ __device__ __forceinline__ int wave_last_le(const int32_t* a, int lo, int hi, in
 }
 
 __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
-    __shared__ int32_t s_off[kFillPairs + 2], s_g[kFillPairs + 1];
+    // per compacted range of the step: first pair, range id, the base of its partner list
+    // (cwb / crb at its begin) and its side of the edge test (the read's owner, or the write's
+    // edge target), staged once so each pair's chain starts at the partner list
+    __shared__ int32_t s_off[kFillPairs + 2], s_g[kFillPairs + 1], s_b[kFillPairs + 1], s_a[kFillPairs + 1];
     __shared__ int s_c[2];
     if (w.bsc->edge_overflow) return;
     const int R = b.R;
     const int M = (int)w.bsc->n_pranges;  // ranges with pairs: pcg / pcoff[0, M), pcoff[M] = P
     const int P = w.pcoff[M];
     const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     for (int Q0 = blockIdx.x * kFillPairs; Q0 < P; Q0 += gridDim.x * kFillPairs) {
         // the compacted ranges holding this step's first and last pair (each range there has at
         // least one pair, so at most kFillPairs of them), found by waves 0 and 1 side by side,
@@ -2644,39 +2648,47 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
         const int Q1 = min(P, Q0 + kFillPairs) - 1;
         if (wave < 2) {
             const int c = wave_last_le(w.pcoff, 0, M, wave == 0 ? Q0 : Q1);
-            if ((threadIdx.x & 63) == 0) s_c[wave] = c;
+            if (lane == 0) s_c[wave] = c;
         }
         __syncthreads();
         const int c0 = s_c[0], nc = s_c[1] - s_c[0] + 1;
         for (int i = threadIdx.x; i <= nc; i += blockDim.x) {
             s_off[i] = w.pcoff[c0 + i];
-            if (i < nc) s_g[i] = w.pcg[c0 + i];
+            if (i < nc) {
+                const int gg = w.pcg[c0 + i];
+                s_g[i] = gg;
+                const int p0 = w.pos[2 * gg];
+                if (gg < R) {
+                    s_b[i] = w.cwb[p0];  // read gg: its k-th write-begin is wbpos[cwb[begin] + k]
+                    s_a[i] = b.rowner[gg];
+                } else {
+                    s_b[i] = w.crb[p0];  // write gg: its k-th read-begin is rbpos[crb[begin] + k]
+                    // write group led by this write: one edge T + j for the group (its members'
+                    // transactions are compared with the reader's in the resolution rounds)
+                    s_a[i] = w.groups ? b.T + w.cwb[p0] : b.wowner[gg - R];
+                }
+            }
         }
         __syncthreads();
         // each dependent step of the pair filter for the thread's four pairs at once: four chains
         // of gathers in flight per thread instead of one after another (C3: 1.85M pairs per batch)
-        int gq[kPairsPerThread], kq[kPairsPerThread];
+        int gq[kPairsPerThread], part[kPairsPerThread], aq[kPairsPerThread];
 #pragma unroll
         for (int u = 0; u < kPairsPerThread; u++) {
             const int q = Q0 + threadIdx.x * kPairsPerThread + u;
             gq[u] = -1;
+            part[u] = aq[u] = 0;
             if (q >= P) continue;
             int lo = 0, hi = nc;  // s_off[lo] <= q < s_off[hi]
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
                 if (s_off[mid] <= q) lo = mid; else hi = mid;
             }
-            gq[u] = s_g[lo];
-            kq[u] = q - s_off[lo];
-        }
-        // partner endpoint: read g's k-th write-begin inside it, or write g's k-th read-begin
-        int part[kPairsPerThread];
-#pragma unroll
-        for (int u = 0; u < kPairsPerThread; u++) {
-            const int gg = gq[u];
-            part[u] = 0;
-            if (gg < 0) continue;
-            part[u] = gg < R ? w.wbpos[w.cwb[w.pos[2 * gg]] + kq[u]] : w.rbpos[w.crb[w.pos[2 * gg]] + kq[u]];
+            const int gg = s_g[lo];
+            gq[u] = gg;
+            aq[u] = s_a[lo];
+            // partner endpoint: read g's k-th write-begin inside it, or write g's k-th read-begin
+            part[u] = (gg < R ? w.wbpos : w.rbpos)[s_b[lo] + q - s_off[lo]];
         }
         int rd[kPairsPerThread], tw[kPairsPerThread];
         bool ok[kPairsPerThread];
@@ -2687,26 +2699,34 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
             rd[u] = tw[u] = 0;
             if (gg < 0) continue;
             const int other = (int)item_range(w.pmeta[part[u]]);
-            const int r = gg < R ? gg : other;            // the read
-            const int wr = (gg < R ? other : gg) - R;     // the write
-            rd[u] = r;
-            if (gg >= R && w.groups) {
-                // write group led by this write: one edge T + j for the group (its members'
-                // transactions are compared with the reader's in the resolution rounds)
-                tw[u] = b.T + w.cwb[w.pos[2 * gg]];
-                ok[u] = range_nonempty(w, r);
-                continue;
+            const bool ne = range_nonempty(w, other);  // the pair's own range is: it has pairs
+            if (gg < R) {  // read gg, write other: an earlier writer
+                rd[u] = gg;
+                tw[u] = b.wowner[other - R];
+                ok[u] = tw[u] < aq[u] && ne;
+            } else {       // write gg, read other
+                rd[u] = other;
+                tw[u] = aq[u];
+                ok[u] = ne && (w.groups || aq[u] < b.rowner[other]);
             }
-            tw[u] = b.wowner[wr];
-            // earlier writer, both ranges non-empty (the pair's own range is: it has pairs)
-            ok[u] = tw[u] < b.rowner[r] && range_nonempty(w, gg < R ? R + wr : r);
         }
+        // edge slots: one atomic per run of lanes filing under the same read (a read's own pairs
+        // are consecutive, so its lanes form one run per wave instead of one atomic each)
 #pragma unroll
         for (int u = 0; u < kPairsPerThread; u++) {
-            if (!ok[u]) continue;
-            const int r = rd[u];
-            const int slot = w.eoff[r] + atomicAdd(&w.ecur[r], 1);
-            if (slot < w.eoff[r + 1]) w.edges[slot] = tw[u];
+            const int key = ok[u] ? rd[u] : -1;
+            const int prev = __shfl_up(key, 1, 64);
+            const bool head = ok[u] && (lane == 0 || prev != key);
+            const uint64_t hm = __ballot(head), om = __ballot(ok[u]);
+            const uint64_t brk = (hm | ~om) & ~((2ull << lane) - 1);  // run breaks above this lane
+            const int start = ok[u] ? 63 - __builtin_clzll(hm & ((2ull << lane) - 1)) : lane;
+            int base = 0;
+            if (head) base = atomicAdd(&w.ecur[key], (brk ? __builtin_ctzll(brk) : 64) - lane);
+            base = __shfl(base, start, 64);
+            if (ok[u]) {
+                const int slot = w.eoff[key] + base + lane - start;
+                if (slot < w.eoff[key + 1]) w.edges[slot] = tw[u];
+            }
         }
         __syncthreads();  // the next step restages s_c / s_off / s_g
     }
