@@ -135,6 +135,7 @@ SIGNATURES = {
     "fdbcs_batch_detect_async": (ctypes.c_int, [_VP, _I64, _I64]),
     "fdbcs_batch_wait": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "fdbcs_batch_conflicting_reads": (ctypes.c_int, [_VP, _I32, _VP, _I32, ctypes.POINTER(_I32)]),
+    "fdbcs_batch_too_old": (ctypes.c_int, [_VP, _VP, _I32, ctypes.POINTER(_I32)]),
     "fdbcs_batch_device_verdicts": (ctypes.c_int, [_VP, ctypes.POINTER(_VP)]),
     "fdbcs_batch_set_conflict_output": (ctypes.c_int, [_VP, _VP, ctypes.c_int32, _VP]),
     "fdbcs_share_bytes": (ctypes.c_int, [ctypes.POINTER(_CPackedBatch), ctypes.POINTER(_I64)]),
@@ -483,6 +484,16 @@ class ConflictBatch:
         ids = np.ascontiguousarray(txn_ids, dtype=np.int32)
         _check(load_library().fdbcs_batch_set_conflict_output(self._h, _VP(ids.ctypes.data if ids.size else 0),
                                                               int(n_global), _VP(dev_out)), "setConflictOutput")
+
+    def get_too_old_transactions(self, too_old_transactions: List[int]) -> None:
+        """GetTooOldTransactions (SkipList.cpp:836-842): appends the transactions whose add-time
+        TooOld test held (SkipList.cpp:770); valid right after addTransaction, before detect."""
+        L = load_library()
+        n = _I32(0)
+        _check(L.fdbcs_batch_too_old(self._h, None, 0, ctypes.byref(n)), "GetTooOldTransactions")
+        out = np.zeros(max(n.value, 1), np.int32)
+        _check(L.fdbcs_batch_too_old(self._h, _p(out), n.value, ctypes.byref(n)), "GetTooOldTransactions")
+        too_old_transactions.extend(out[: n.value].tolist())
 
     def conflicting_reads(self, t: int) -> List[int]:
         L = load_library()

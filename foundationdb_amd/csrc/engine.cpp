@@ -3156,6 +3156,19 @@ int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out,
     return FDBCS_OK;
 }
 
+int fdbcs_batch_too_old(fdbcs_batch* b, int32_t* idx_out, int32_t cap, int32_t* n_out) {
+    if (!b || !n_out || cap < 0) return FDBCS_E_INVALID;
+    if (b->routed) return FDBCS_E_STATE;  // decided at detect (k_route_too_old)
+    int32_t n = 0;
+    for (int32_t t = 0; t < (int32_t)b->flags.size(); t++) {
+        if (!(b->flags[t] & kFlagTooOld)) continue;
+        if (idx_out && n < cap) idx_out[n] = t;
+        n++;
+    }
+    *n_out = n;
+    return FDBCS_OK;
+}
+
 int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr) {
     if (!b || !dptr) return FDBCS_E_INVALID;
     if (b->state < 2) return FDBCS_E_STATE;

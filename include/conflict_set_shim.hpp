@@ -136,9 +136,14 @@ struct ConflictBatchT {
         }
     }
 
-    void GetTooOldTransactions(std::vector<int>& tooOldTransactions) {  // SkipList.cpp:836-842
-        for (int i = 0; i < (int)verdicts.size(); i++)
-            if (verdicts[i] == TransactionTooOld) tooOldTransactions.push_back(i);
+    // SkipList.cpp:836-842: the add-time TooOld decisions (SkipList.cpp:770), valid right after
+    // addTransaction, before detectConflicts, as in the reference.
+    void GetTooOldTransactions(std::vector<int>& tooOldTransactions) {
+        int32_t n = 0;
+        fdbcs_shim::check(fdbcs_batch_too_old(b, nullptr, 0, &n), "GetTooOldTransactions");
+        std::vector<int32_t> idx(n > 0 ? n : 1);
+        fdbcs_shim::check(fdbcs_batch_too_old(b, idx.data(), n, &n), "GetTooOldTransactions");
+        for (int32_t i = 0; i < n; i++) tooOldTransactions.push_back(idx[i]);
     }
 
 private:

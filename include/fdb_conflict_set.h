@@ -210,6 +210,13 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
  * indices (indexInTx) that conflicted, ascending.  Valid after detect. */
 int fdbcs_batch_conflicting_reads(fdbcs_batch* b, int32_t txn, int32_t* idx_out, int32_t cap,
                                   int32_t* n_out);
+/* ConflictBatch::GetTooOldTransactions (SkipList.cpp:836-842): indices of the transactions added
+ * so far whose add-time TooOld test held (read_snapshot < oldestVersion with at least one read,
+ * SkipList.cpp:770), ascending; valid right after the adds, before detect, as in the reference.
+ * Writes at most cap indices (idx_out may be NULL to count).  A routed batch
+ * (fdbcs_batch_add_routed) is judged at detect on the device: FDBCS_E_STATE (read its verdict
+ * bytes instead). */
+int fdbcs_batch_too_old(fdbcs_batch* b, int32_t* idx_out, int32_t cap, int32_t* n_out);
 /* Device pointer to the batch's per-transaction verdict bytes (valid after
  * detect until the batch is destroyed) for on-device combine (RCCL). */
 int fdbcs_batch_device_verdicts(fdbcs_batch* b, void** dptr);

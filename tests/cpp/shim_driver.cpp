@@ -94,8 +94,10 @@ static int run_lists(const char* path) {
             }
             ConflictBatch a(with), b(without);
             for (auto& t : txns) a.addTransaction(t), b.addTransaction(t);
-            std::vector<int> nc, to, nc2;
+            std::vector<int> nc, to, nc2, early;
+            a.GetTooOldTransactions(early);  // before detect, as SkipList.cpp:836-842 allows
             a.detectConflicts(now, oldest, nc, &to);
+            if (early != to) return 4;
             b.detectConflicts(now, oldest, nc2);
             printf("L %d with", batch);
             print_list("nc", nc);
@@ -184,7 +186,9 @@ int main(int argc, char** argv) {
         batch.addTransaction(a);
         batch.addTransaction(w);
         batch.addTransaction(r);
-        std::vector<int> ok, tooOld, late;
+        std::vector<int> ok, tooOld, late, early;
+        batch.GetTooOldTransactions(early);  // right after the adds
+        if (early.size() != 1 || early[0] != 0) return 5;
         batch.detectConflicts(50, 35, ok, &tooOld);
         batch.GetTooOldTransactions(late);  // SkipList.cpp:836-842
         printf("b5 commit=%zu tooold=%zu late=%zu late0=%d entries=%zu\n", ok.size(), tooOld.size(), late.size(),

@@ -811,7 +811,8 @@ def test_verdict_lists_match_oracle_lists(engine, oracle_mod, tmp_path):
     """Both host adapters over the HIP engine fill nonConflicting / tooOld exactly as the oracle's
     restatement of SkipList.cpp:869-876, with a tooOld list (Resolver.actor.cpp:194) and without one
     (skipListTest's call shape, SkipList.cpp:1077): the Python ConflictBatch and the C++ shim
-    (tests/cpp/shim_driver.cpp --lists) on the KAT scenarios and random TooOld-heavy sequences."""
+    (tests/cpp/shim_driver.cpp --lists) on the KAT scenarios and random TooOld-heavy sequences.
+    GetTooOldTransactions right after the adds (SkipList.cpp:836-842) equals the tooOld list."""
     import subprocess
 
     from tests.helpers import list_scenarios, oracle_scenario_lists, write_list_file
@@ -833,8 +834,11 @@ def test_verdict_lists_match_oracle_lists(engine, oracle_mod, tmp_path):
             got_nc, got_to, got_nc2 = [], [], []
             b = engine.ConflictBatch(with_cs)
             b.add_packed(pb)
+            early = []
+            b.get_too_old_transactions(early)  # GetTooOldTransactions before detect (SkipList.cpp:836-842)
             b.detect_conflicts(now, no, got_nc, got_to)
             b.close()
+            assert early == to
             b = engine.ConflictBatch(without_cs)
             b.add_packed(pb)
             b.detect_conflicts(now, no, got_nc2)
