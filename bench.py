@@ -276,6 +276,10 @@ def cpu_replay(args, kb, ko, vers, mine, gbatches, gpu_verdicts, timed, rank, n_
     t_begin = time.time()
     n_batches = len(gbatches) if n_batches is None else n_batches
     for i in range(n_batches):
+        if gpu_verdicts[i] is None and i not in timed:
+            # a batch the GPU never resolved (the hold pass is skipped on the multi-resolver path):
+            # the device history never held it, so neither may the restatement's
+            continue
         b = mine(i)  # this resolver's sub-batch (host routing, CommitProxyServer.actor.cpp:118-187)
         _, now, no = gbatches[i]
         t = time.perf_counter()

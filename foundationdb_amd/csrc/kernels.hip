@@ -3485,26 +3485,41 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 // boundary of its own (no exact match, not glued to the next segment's B) and the version it
 // inherits, then the exclusive prefixes of removed boundaries, inserted boundaries and tail units
 // with one decoupled look-back across tiles, and tile_first for the copy.  One workgroup per tile
-// of kSegPer segments: 2 lookups each (B and E) plus one for the B of the segment before the tile,
-// whose lo bounds the tile's first copy tiles, kArity cooperating lanes per lookup.  (One lane per
-// lookup in 128-thread workgroups, as the read check does, measured slower here: 19.7 vs 18.0 us
-// per launch at C2 on one box; the tiles' look-back chain, not the lookups, sets the pace.)
-constexpr int kSegPer = kWG / (2 * kArity) - 1;  // 63
+// of seg_per segments: 2 lookups each (B and E) plus one for the B of the segment before the tile,
+// whose lo bounds the tile's first copy tiles.  Three layouts:
+//   short keys, W < kSegWideMinW: 1024-thread workgroups, 63 segments per tile, kArity cooperating
+//     lanes per lookup (group_lower_bound): many waves in flight for a small batch;
+//   short keys, larger batches (WIDE): 512 threads, 255 segments, one lane per lookup
+//     (lane_lower_bound).  The tiles' look-back chain sets the pace once tiles number in the
+//     hundreds: at 32768-txn C2 batches 1040 narrow tiles took 116 us per launch, 257 wide ones 50;
+//     at 5000 txns the wide layout is slower (17.7 -> 19.9 us: 40 tiles leave too few lookups in
+//     flight);
+//   long keys: 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long holds the
+//     query's tail words in registers).
+constexpr int kSegWideMinW = 24576;
+constexpr int seg_per(bool long_keys, bool wide) { return long_keys || !wide ? 63 : 255; }
+constexpr int seg_lanes(bool long_keys, bool wide) { return long_keys || wide ? 1 : kArity; }
+constexpr int seg_threads(bool long_keys, bool wide) {
+    return 2 * seg_lanes(long_keys, wide) * (seg_per(long_keys, wide) + 1);
+}
+inline bool seg_wide(int64_t W, bool long_keys) { return !long_keys && W >= kSegWideMinW; }
+inline int64_t seg_tiles(int64_t W, bool long_keys) {
+    return (W > 0 ? W : 1) / seg_per(long_keys, seg_wide(W, long_keys)) + 1;
+}
+// an upper bound over the layouts (workspace look-back granules)
+inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / 63 + 1; }
 
-inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / kSegPer + 1; }
-// lanes per lookup and workgroup size of k_seg_prep: long keys one lane per lookup
-// (lane_lower_bound_long: C4's segment lookups 64 -> ? us in the pipeline), short keys kArity
-constexpr int seg_lanes(bool long_keys) { return long_keys ? 1 : kArity; }
-constexpr int seg_threads(bool long_keys) { return 2 * seg_lanes(long_keys) * (kSegPer + 1); }
-
-template <bool LONG>
-__global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
-                                                                const uint8_t* htail, Scalars* sc, TierIO io,
-                                                                int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
-                                                                int64_t lvl2_n) {
-    constexpr int LL = seg_lanes(LONG);
-    __shared__ int64_t s_lo[kSegPer + 1];       // lo of the segment before the tile, then the tile's
-    __shared__ uint32_t s_val[3][kSegPer + 1];  // removed, inserted, tail units per segment
+template <bool LONG, bool WIDE>
+__global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
+                                                                      const uint8_t* htail, Scalars* sc, TierIO io,
+                                                                      int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
+                                                                      int64_t lvl2_n) {
+    constexpr int SP = seg_per(LONG, WIDE);
+    constexpr int LL = seg_lanes(LONG, WIDE);
+    constexpr int NSW = (SP + 1 + 63) / 64;     // waves over the tile's SP + 1 scan entries
+    __shared__ int64_t s_lo[SP + 1];            // lo of the segment before the tile, then the tile's
+    __shared__ uint32_t s_val[3][SP + 1];       // removed, inserted, tail units per segment
+    __shared__ uint32_t s_wsum[3][NSW];
     __shared__ uint32_t s_base[3];
     __shared__ int s_tile;
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3516,32 +3531,35 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
     __syncthreads();
     const int tile = s_tile;
     const int U = (int)w.bsc->n_segments;
-    const int ntiles = U > 0 ? (U + kSegPer - 1) / kSegPer : 1;
+    const int ntiles = U > 0 ? (U + SP - 1) / SP : 1;
     if (tile >= ntiles) return;  // spare workgroup: nobody waits on it
     const int64_t n = *io.n_in;
     const int q = threadIdx.x / (2 * LL), role = (threadIdx.x / LL) & 1;
-    const int sg = tile * kSegPer + (q < kSegPer ? q : -1);  // slot kSegPer: the segment before
-    const bool live = sg >= 0 && sg < U && (q < kSegPer || role == 0);
+    const int sg = tile * SP + (q < SP ? q : -1);  // slot SP: the segment before
+    const bool live = sg >= 0 && sg < U && (q < SP || role == 0);
     int64_t pos = 0;
     bool eq = false;
     DKey kb{}, ke{};
     if (live) {
         kb = seg_key(b, w, w.seg_b[sg], 0);
         ke = seg_key(b, w, w.seg_e[sg], 1);
+        const DKey& key = role ? ke : kb;
         if constexpr (LONG) {
-            const DKey& key = role ? ke : kb;
             QTail qt;
             load_qtail(qt, key, b.tail);
             pos = lane_lower_bound_long(h, hm, n, key, qt, htail, b.tail, eq);
-        } else {
-            pos = group_lower_bound<false>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+        } else if constexpr (WIDE) {
+            pos = lane_lower_bound(h, hm, n, key, htail, b.tail, eq);
         }
     }
-    const int lane = threadIdx.x & 63;
+    if constexpr (!LONG && !WIDE) {  // the group's kArity lanes search together (uniform per group)
+        if (live) pos = group_lower_bound<false>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t hi = __shfl(pos, (lane + LL) & 63, 64);
     const int exact = __shfl((int)eq, (lane + LL) & 63, 64);
     if (threadIdx.x % (2 * LL) == 0) {
-        if (q == kSegPer) {
+        if (q == SP) {
             s_lo[0] = live ? pos : 0;
         } else if (live) {
             const int64_t lo = pos;
@@ -3560,12 +3578,12 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
         }
     }
     __syncthreads();
+    // exclusive prefixes inside the tile (entry k: segment tile * SP + k, entry SP: past the tile)
     uint32_t ex[3] = {0, 0, 0};
-    if (threadIdx.x < 64) {
-        uint32_t btot[3];
+    if (wid < NSW) {
 #pragma unroll
         for (int c = 0; c < 3; c++) {
-            const uint32_t v = lane < kSegPer ? s_val[c][lane] : 0u;
+            const uint32_t v = threadIdx.x < SP ? s_val[c][threadIdx.x] : 0u;
             uint32_t x = v;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -3573,29 +3591,47 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
                 if (lane >= o) x += y;
             }
             ex[c] = x - v;
-            btot[c] = __shfl(x, 63, 64);
+            if (lane == 63) s_wsum[c][wid] = x;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t btot[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            uint32_t t = 0;
+#pragma unroll
+            for (int k = 0; k < NSW; k++) t += s_wsum[c][k];
+            btot[c] = t;
         }
         tile_lookback<3>(w.scan[kScanSegSum], tile, btot, s_base);
     }
     __syncthreads();
-    if (threadIdx.x < 64) {  // lanes 0..kSegPer: the tile's segments, then the one after it
-        const int j = tile * kSegPer + lane;
-        if (lane < kSegPer && j < U) {
-            w.seg_rem[j] = s_base[0] + ex[0];
-            w.seg_ins[j] = s_base[1] + ex[1];
-            w.seg_tlen[j] = s_base[2] + ex[2];
-            // tile_first[t] = j for the copy tiles t in (lo[j-1] / tile, lo[j] / tile]
-            const int64_t t0 = j > 0 ? s_lo[lane] / kDeltaTile + 1 : 0;
-            for (int64_t t = t0; t <= s_lo[lane + 1] / kDeltaTile; t++) w.tile_first[t] = j;
+    if (wid < NSW) {  // entries 0..SP: the tile's segments, then the one after it
+        const int k = threadIdx.x;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            uint32_t before = s_base[c];
+            for (int v = 0; v < wid; v++) before += s_wsum[c][v];
+            ex[c] += before;
         }
-        if (tile == ntiles - 1 && j == U) {
+        const int j = tile * SP + k;
+        if (k < SP && j < U) {
+            w.seg_rem[j] = ex[0];
+            w.seg_ins[j] = ex[1];
+            w.seg_tlen[j] = ex[2];
+            // tile_first[t] = j for the copy tiles t in (lo[j-1] / tile, lo[j] / tile]
+            const int64_t t0 = j > 0 ? s_lo[k] / kDeltaTile + 1 : 0;
+            for (int64_t t = t0; t <= s_lo[k + 1] / kDeltaTile; t++) w.tile_first[t] = j;
+        }
+        if (tile == ntiles - 1 && j == U && k <= SP) {
             // sentinel entries at U (totals, for elements after every segment), the remaining copy
             // tiles and the tier's new size
-            const uint32_t r = s_base[0] + ex[0], in = s_base[1] + ex[1], tl = s_base[2] + ex[2];
+            const uint32_t r = ex[0], in = ex[1], tl = ex[2];
             w.seg_rem[U] = r;
             w.seg_ins[U] = in;
             w.seg_tlen[U] = tl;
-            const int64_t t0 = U > 0 ? s_lo[lane] / kDeltaTile + 1 : 0;
+            const int64_t t0 = U > 0 ? s_lo[k] / kDeltaTile + 1 : 0;
             for (int64_t t = t0; t <= n / kDeltaTile + 1; t++) w.tile_first[t] = U;
             *io.before = n;
             *io.removed = r;
@@ -3799,8 +3835,9 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
-    fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_prep_tiles(b.W)),
-               dim3(seg_threads(long_keys)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
+    const bool wide = seg_wide(b.W, long_keys);
+    fdb_launch(long_keys ? k_seg_prep<true, false> : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
+               dim3((unsigned)seg_tiles(b.W, long_keys)), dim3(seg_threads(long_keys, wide)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
                dstm.lvl[2], lvl2_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
