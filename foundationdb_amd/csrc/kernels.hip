@@ -3486,36 +3486,24 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 // inherits, then the exclusive prefixes of removed boundaries, inserted boundaries and tail units
 // with one decoupled look-back across tiles, and tile_first for the copy.  One workgroup per tile
 // of seg_per segments: 2 lookups each (B and E) plus one for the B of the segment before the tile,
-// whose lo bounds the tile's first copy tiles.  Three layouts:
-//   short keys, W < kSegWideMinW: 1024-thread workgroups, 63 segments per tile, kArity cooperating
-//     lanes per lookup (group_lower_bound): many waves in flight for a small batch;
-//   short keys, larger batches (WIDE): 512 threads, 255 segments, one lane per lookup
-//     (lane_lower_bound).  The tiles' look-back chain sets the pace once tiles number in the
-//     hundreds: at 32768-txn C2 batches 1040 narrow tiles took 116 us per launch, 257 wide ones 50;
-//     at 5000 txns the wide layout is slower (17.7 -> 19.9 us: 40 tiles leave too few lookups in
-//     flight);
-//   long keys: 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long holds the
-//     query's tail words in registers).
-constexpr int kSegWideMinW = 24576;
-constexpr int seg_per(bool long_keys, bool wide) { return long_keys || !wide ? 63 : 255; }
-constexpr int seg_lanes(bool long_keys, bool wide) { return long_keys || wide ? 1 : kArity; }
-constexpr int seg_threads(bool long_keys, bool wide) {
-    return 2 * seg_lanes(long_keys, wide) * (seg_per(long_keys, wide) + 1);
-}
-inline bool seg_wide(int64_t W, bool long_keys) { return !long_keys && W >= kSegWideMinW; }
-inline int64_t seg_tiles(int64_t W, bool long_keys) {
-    return (W > 0 ? W : 1) / seg_per(long_keys, seg_wide(W, long_keys)) + 1;
-}
-// an upper bound over the layouts (workspace look-back granules)
-inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / 63 + 1; }
+// whose lo bounds the tile's first copy tiles, one lane per lookup: short keys 127 segments per
+// 256-thread workgroup (lane_lower_bound), long keys 63 per 128 threads (lane_lower_bound_long holds
+// the query's tail words in registers).  Round 4's short-key layout (kArity cooperating lanes per
+// lookup, 63 segments per 1024-thread tile) matched it at 5000-txn C2 batches (18.5 vs 18.6 us) but
+// at 32768-txn batches its 1040 tiles chained their prefixes for 116 us per launch, against 46 us
+// for 516 tiles of 127 (53 at 255 segments per tile, 67 at 511: too few lookups in flight).
+constexpr int seg_per(bool long_keys) { return long_keys ? 63 : 127; }
+constexpr int seg_threads(bool long_keys) { return 2 * (seg_per(long_keys) + 1); }
+inline int64_t seg_tiles(int64_t W, bool long_keys) { return (W > 0 ? W : 1) / seg_per(long_keys) + 1; }
+// an upper bound over both layouts (workspace look-back granules)
+inline int64_t seg_prep_tiles(int64_t W) { return seg_tiles(W, true); }
 
-template <bool LONG, bool WIDE>
-__global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
-                                                                      const uint8_t* htail, Scalars* sc, TierIO io,
-                                                                      int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
-                                                                      int64_t lvl2_n) {
-    constexpr int SP = seg_per(LONG, WIDE);
-    constexpr int LL = seg_lanes(LONG, WIDE);
+template <bool LONG>
+__global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
+                                                                const uint8_t* htail, Scalars* sc, TierIO io,
+                                                                int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
+                                                                int64_t lvl2_n) {
+    constexpr int SP = seg_per(LONG);
     constexpr int NSW = (SP + 1 + 63) / 64;     // waves over the tile's SP + 1 scan entries
     __shared__ int64_t s_lo[SP + 1];            // lo of the segment before the tile, then the tile's
     __shared__ uint32_t s_val[3][SP + 1];       // removed, inserted, tail units per segment
@@ -3534,7 +3522,7 @@ __global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b
     const int ntiles = U > 0 ? (U + SP - 1) / SP : 1;
     if (tile >= ntiles) return;  // spare workgroup: nobody waits on it
     const int64_t n = *io.n_in;
-    const int q = threadIdx.x / (2 * LL), role = (threadIdx.x / LL) & 1;
+    const int q = threadIdx.x >> 1, role = threadIdx.x & 1;
     const int sg = tile * SP + (q < SP ? q : -1);  // slot SP: the segment before
     const bool live = sg >= 0 && sg < U && (q < SP || role == 0);
     int64_t pos = 0;
@@ -3548,17 +3536,14 @@ __global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b
             QTail qt;
             load_qtail(qt, key, b.tail);
             pos = lane_lower_bound_long(h, hm, n, key, qt, htail, b.tail, eq);
-        } else if constexpr (WIDE) {
+        } else {
             pos = lane_lower_bound(h, hm, n, key, htail, b.tail, eq);
         }
     }
-    if constexpr (!LONG && !WIDE) {  // the group's kArity lanes search together (uniform per group)
-        if (live) pos = group_lower_bound<false>(h, hm, n, role ? ke : kb, htail, b.tail, eq);
-    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t hi = __shfl(pos, (lane + LL) & 63, 64);
-    const int exact = __shfl((int)eq, (lane + LL) & 63, 64);
-    if (threadIdx.x % (2 * LL) == 0) {
+    const int64_t hi = __shfl(pos, (lane + 1) & 63, 64);
+    const int exact = __shfl((int)eq, (lane + 1) & 63, 64);
+    if (role == 0) {
         if (q == SP) {
             s_lo[0] = live ? pos : 0;
         } else if (live) {
@@ -3835,9 +3820,8 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
-    const bool wide = seg_wide(b.W, long_keys);
-    fdb_launch(long_keys ? k_seg_prep<true, false> : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
-               dim3((unsigned)seg_tiles(b.W, long_keys)), dim3(seg_threads(long_keys, wide)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
+    fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_tiles(b.W, long_keys)),
+               dim3(seg_threads(long_keys)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
                dstm.lvl[2], lvl2_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
