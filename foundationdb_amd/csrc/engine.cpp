@@ -1463,7 +1463,36 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     const char* prio = getenv("FDBCS_PRIO");
+    // FDBCS_CU_MASK (A/B of CU partitions between the chains): "a:0-127,x:128-255" gives stream a
+    // (stage A), x (check / resolution), y (merge / epilogue) or c (base-tier check) the CUs whose
+    // index lies in the range; "x:%0-3" the CUs whose index mod 8 lies in it (the hardware's
+    // enumeration decides which XCD that is).  Unlisted streams use every CU.
+    const char* cumask = getenv("FDBCS_CU_MASK");
+    int n_cu = 0;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cs->device);
+    auto cu_mask_of = [&](char tag, std::vector<uint32_t>& m) -> bool {
+        if (!cumask || n_cu <= 0) return false;
+        for (const char* p = cumask; *p;) {
+            const char t = *p;
+            const char* e = strchr(p, ',');
+            const std::string item(p, e ? (size_t)(e - p) : strlen(p));
+            p = e ? e + 1 : p + item.size();
+            if (item.size() < 3 || t != tag || item[1] != ':') continue;
+            const bool mod = item[2] == '%';
+            int lo = 0, hi = 0;
+            if (sscanf(item.c_str() + (mod ? 3 : 2), "%d-%d", &lo, &hi) != 2) return false;
+            m.assign((size_t)(n_cu + 31) / 32, 0u);
+            for (int c = 0; c < n_cu; c++) {
+                const int k = mod ? c % 8 : c;
+                if (k >= lo && k <= hi) m[(size_t)c / 32] |= 1u << (c % 32);
+            }
+            return true;
+        }
+        return false;
+    };
     auto mk = [&](hipStream_t* st, char tag) {
+        std::vector<uint32_t> m;
+        if (cu_mask_of(tag, m)) return hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data()) == hipSuccess;
         if (prio && strchr(prio, tag)) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio_hi) == hipSuccess;
         return hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess;
     };
