@@ -4325,7 +4325,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         ulonglong2 prev_k = make_ulonglong2(0, 0);  // the previous block's sampled key (delta directory fill)
         if (lane < kEpiBlocks && b1l < n1) {
             sk = m.keys[b1l * kFan];  // sampled key of the block
-            if (m.edir_epoch && b1l > 0) prev_k = m.keys[(b1l - 1) * kFan];
+            if (m.edir_epoch && b1l > 0 && lane == 0) prev_k = m.keys[(b1l - 1) * kFan];
         }
         // every 8th boundary of the wave's blocks (8 entries of skey8 per block)
         static_assert(kEpiBlocks * kFan / 8 <= 64, "one skey8 entry per lane");
@@ -4355,18 +4355,30 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
                 d /= kArity;
                 m.skey[0][off + d] = sk;
             }
-            if (m.edir_epoch) {
-                // delta directory: slots (dir_slot(previous sample), dir_slot(this sample)] hold this
-                // sample's index (the first sample not below them); the last sample also fills
-                // the slots above it with n1.  At most kDirRun slots per run: slots left over keep
-                // an older epoch and send their lookups down the tree.
-                const uint64_t tag = (uint64_t)m.edir_epoch << 32;
-                const int64_t a = b1l > 0 ? (int64_t)dir_slot(m, prev_k.x, prev_k.y) : -1,
-                              c = (int64_t)dir_slot(m, sk.x, sk.y);
-                for (int64_t v = a + 1; v <= c && v <= a + kDirRun; v++) m.edir[v] = tag | (uint64_t)b1l;
-                if (b1l == n1 - 1)
-                    for (int64_t v = c + 1; v <= (int64_t)m.dir_top + 1 && v <= c + kDirRun; v++)
-                        m.edir[v] = tag | (uint64_t)n1;
+        }
+        if (m.edir_epoch) {
+            // delta directory: slots (dir_slot(previous sample), dir_slot(this sample)] hold this
+            // sample's index (the first sample not below them); the last sample also fills the
+            // slots above it with n1.  At most kDirRun slots per run: slots left over keep an older
+            // epoch and send their lookups down the tree.  The whole wave writes each run, 64
+            // consecutive slots per store, instead of one lane per sample looping over its run.
+            int64_t c_l = -1, a0 = -1;
+            if (lane < kEpiBlocks && b1l < n1) c_l = (int64_t)dir_slot(m, sk.x, sk.y);
+            if (lane == 0 && b1l > 0 && b1l < n1) a0 = (int64_t)dir_slot(m, prev_k.x, prev_k.y);
+            const uint64_t tag = (uint64_t)m.edir_epoch << 32;
+            int64_t aq = __shfl(a0, 0, 64);
+#pragma unroll
+            for (int q = 0; q < kEpiBlocks; q++) {
+                const int64_t bq = b1_0 + q, cq = __shfl(c_l, q, 64);
+                if (bq < n1) {  // (uniform)
+                    const int64_t e = cq < aq + kDirRun ? cq : aq + kDirRun;
+                    for (int64_t v = aq + 1 + lane; v <= e; v += 64) m.edir[v] = tag | (uint64_t)bq;
+                    if (bq == n1 - 1) {
+                        const int64_t top = (int64_t)m.dir_top + 1, e2 = cq + kDirRun < top ? cq + kDirRun : top;
+                        for (int64_t v = cq + 1 + lane; v <= e2; v += 64) m.edir[v] = tag | (uint64_t)n1;
+                    }
+                }
+                aq = cq;
             }
         }
         // the wave's maximum into levels 2 and 3; level 3 only when above what it already holds
