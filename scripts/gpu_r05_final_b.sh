@@ -26,4 +26,8 @@ step bench_c2_32768 500 python bench.py --workload c2 --txns 32768 > $O/bench_c2
 summ $O/bench_c2_32768.json
 step bench_c2_tooold 500 python bench.py --workload c2 --too-old-frac 0.05 > $O/bench_c2_tooold.json 2> $O/bench_c2_tooold.err
 summ $O/bench_c2_tooold.json
-echo done >&2
+
+step rccl_world1 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29517 bench.py --gpus 1 --dist --backend nccl --workload c2 --steps 20 --warmup 3 \
+  --too-old-frac 0.05 > $O/rccl_world1_c2.json 2> $O/rccl_world1_c2.err
+echo rccl done >&2
