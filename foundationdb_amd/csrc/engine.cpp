@@ -646,15 +646,17 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     TAKE(wkeys, sizeof(DKey) * (2 * W + 1));
     TAKE(segk, sizeof(DKey) * (2 * W + 2));
     TAKE(cflag, 2 * W + 2);
-    TAKE(wbpos, 4 * W);
+    TAKE(wbrange, 4 * W);
     TAKE(wlead, 4 * (W + 1));
     TAKE(wtxn, 4 * (W + 1));
     TAKE(gminc, 4 * (W + 1));
-    TAKE(rbpos, 4 * R);
+    TAKE(rbrange, 4 * R);
     TAKE(eoff, 4 * (R + 1));
     TAKE(poff, 4 * (R + W + 1));
     TAKE(pcg, 4 * (R + W + 1));
     TAKE(pcoff, 4 * (R + W + 1));
+    TAKE(pcbase, 4 * (R + W + 1));
+    TAKE(pca, 4 * (R + W + 1));
     TAKE(ecur, 4 * R);
     TAKE(edges, 4 * edge_cap);
     TAKE(eptr, 4 * T);

@@ -216,12 +216,14 @@ struct Work {
     uint8_t* cflag;        // [2W] D.Combine across workgroups: write endpoint opens (1) / closes (2) a segment
     uint8_t* btail;        // [btail_cap] copy of the batch's tail region (k_sort_partition): the next
                            // batch's read check reads segk's tails here, after the batch is waited
-    int32_t* wbpos;        // [W] positions of write-begins in order
-    int32_t* rbpos;        // [R] positions of read-begins in order
+    int32_t* wbrange;      // [W] range of each write-begin, in sorted order
+    int32_t* rbrange;      // [R] range of each read-begin, in sorted order
     int32_t* eoff;         // [R+1] first edge slot of each read
     int32_t* poff;         // [R+W+1] first candidate pair of each range
     int32_t* pcg;          // [R+W+1] the ranges with candidate pairs, in order (then G)
     int32_t* pcoff;        // [R+W+1] their first pairs (then the pair count): k_edge_fill's index
+    int32_t* pcbase;       // [R+W] their partner lists' bases (cwb / crb at the range's begin)
+    int32_t* pca;          // [R+W] their side of the edge test (EdgePairScan::store)
     int32_t* ecur;         // [R] edges of each read (slots taken; zeroed by the epilogue)
     // write groups (groups != 0): consecutive write-begins (in sorted order) whose writes contain
     // exactly the same read-begins are one group; a read gets one edge T + j per group j (j = the

@@ -1844,7 +1844,7 @@ struct SortOut {
     int32_t* pos;      // [E] position of endpoint p
     uint32_t* pmeta;   // [E] meta at position P
     int32_t *cwb, *crb, *cwe;  // [E + 1] write-begins / read-begins / write-ends before position P
-    int32_t *wbpos, *rbpos;    // positions of the write-begins / read-begins in order
+    int32_t *wbrange, *rbrange;  // ranges of the write-begins / read-begins in sorted order
     SortItem* items;   // [E] sorted items (FDBCS_VALIDATE) or null
     SplitKey* quant;   // quantiles of this batch for the next one, or null
     SortItem* big;     // [E] workgroup path: gathered endpoints of a big bucket
@@ -1919,8 +1919,8 @@ __device__ __forceinline__ void put_position(const BatchDev& b, const SortOut& o
     o.cwb[P] = wb;
     o.crb[P] = rb;
     o.cwe[P] = we;
-    if (cls == kWriteBegin) o.wbpos[wb] = (int32_t)P;
-    if (cls == kReadBegin) o.rbpos[rb] = (int32_t)P;
+    if (cls == kWriteBegin) o.wbrange[wb] = p >> 1;  // (the edge scans want the range, not P)
+    if (cls == kReadBegin) o.rbrange[rb] = p >> 1;
     if (o.items) o.items[P] = make_item(b, p);
 }
 
@@ -2420,7 +2420,7 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
     }
     const SortArgs a = sort_args(w, quant, nb, b.tail_n, long_keys);
     fdb_launch(k_sort_partition, dim3((E + kBlock - 1) / kBlock), dim3(kBlock), (uint32_t)(16 * (nb - 1)), s, b, a);
-    SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, validate ? w.items : nullptr,
+    SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbrange, w.rbrange, validate ? w.items : nullptr,
               quant_out, w.big, w.big_p};
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     if (long_keys)
@@ -2443,7 +2443,7 @@ hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, Spli
     if ((err = hipEventCreate(&e0)) || (err = hipEventCreate(&e1))) return err;
     SortArgs a = sort_args(w, quant, nb, b.tail_n, long_keys);
     if (const char* v = getenv("FDBCS_SORT_EXP")) a.exp = atoi(v);  // cost breakdown (results unused)
-    SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbpos, w.rbpos, nullptr, nullptr, w.big, w.big_p};
+    SortOut o{w.pos, w.pmeta, w.cwb, w.crb, w.cwe, w.wbrange, w.rbrange, nullptr, nullptr, w.big, w.big_p};
     const int grid = (nb + kBlock / 64 - 1) / (kBlock / 64);
     double total = 0;
     for (int r = 0; r < reps && err == hipSuccess; r++) {
@@ -2502,8 +2502,8 @@ void launch_validate_sort(hipStream_t s, const BatchDev& b, const Work& w) {
 //
 // Every (range, candidate) pair is enumerated in parallel, so a hot key written by hundreds of
 // transactions and read by thousands (Zipf, C3) costs no serial per-range loop:
-//   * read r owns the write-begins inside (rb, re): wbpos[cwb[rb] .. cwb[re]) ("a" pairs);
-//   * write w owns the read-begins inside (wb, we): rbpos[crb[wb] .. crb[we]) ("b" pairs).
+//   * read r owns the write-begins inside (rb, re): wbrange[cwb[rb] .. cwb[re]) ("a" pairs);
+//   * write w owns the read-begins inside (wb, we): rbrange[crb[wb] .. crb[we]) ("b" pairs).
 // Read r owns eoff[r+1] - eoff[r] slots: its a pairs plus one per write covering rb, a count that
 // is #(write-begins before rb) - #(write-ends before rb), known without enumerating (an empty write
 // has its end before its begin and no read-begin between them, so it counts 0).  Only pairs that
@@ -2534,6 +2534,8 @@ struct EdgePairScan {
     int32_t R, G;
     const int32_t* wowner;
     const DKey* keys;
+    const int32_t* rowner;
+    int32_t T;
     __device__ void counts(int64_t g, uint32_t& slots, uint32_t& pairs, uint32_t& a) const {
         slots = pairs = a = 0;
         if (g >= R) {
@@ -2556,7 +2558,7 @@ struct EdgePairScan {
             if (iv.y > iv.x) {
                 lead = 2;
                 if (j > 0) {
-                    const int gp = (int)item_range(w.pmeta[w.wbpos[j - 1]]);
+                    const int gp = w.wbrange[j - 1];
                     const uint2 ip = write_rb_interval(w, gp);
                     if (ip.x == iv.x && ip.y == iv.y) lead = 1;
                 }
@@ -2590,6 +2592,17 @@ struct EdgePairScan {
         if (own[2]) {
             w.pcg[ex[2]] = (int32_t)g;
             w.pcoff[ex[2]] = (int32_t)ex[1];
+            // k_edge_fill's per-range operands (its staging then takes one load, not three): the
+            // base of the partner list (cwb / crb at the range's begin) and the range's side of the
+            // edge test (the read's owner; the write's owner, or its group's edge T + j)
+            const int p0 = w.pos[2 * g];
+            if (g < R) {
+                w.pcbase[ex[2]] = w.cwb[p0];
+                w.pca[ex[2]] = rowner[g];
+            } else {
+                w.pcbase[ex[2]] = w.crb[p0];
+                w.pca[ex[2]] = w.groups ? T + w.cwb[p0] : wowner[g - R];
+            }
         }
     }
     __device__ void finish(const uint32_t (&tot)[3]) const {
@@ -2655,18 +2668,13 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
         for (int i = threadIdx.x; i <= nc; i += blockDim.x) {
             s_off[i] = w.pcoff[c0 + i];
             if (i < nc) {
-                const int gg = w.pcg[c0 + i];
-                s_g[i] = gg;
-                const int p0 = w.pos[2 * gg];
-                if (gg < R) {
-                    s_b[i] = w.cwb[p0];  // read gg: its k-th write-begin is wbpos[cwb[begin] + k]
-                    s_a[i] = b.rowner[gg];
-                } else {
-                    s_b[i] = w.crb[p0];  // write gg: its k-th read-begin is rbpos[crb[begin] + k]
-                    // write group led by this write: one edge T + j for the group (its members'
-                    // transactions are compared with the reader's in the resolution rounds)
-                    s_a[i] = w.groups ? b.T + w.cwb[p0] : b.wowner[gg - R];
-                }
+                // read gg: its k-th write-begin's range is wbrange[base + k]; write gg: its k-th
+                // read-begin's range is rbrange[base + k].  A write leading a group gets one edge
+                // T + j for the group (its members' transactions are compared with the reader's
+                // in the resolution rounds).  (EdgePairScan::store)
+                s_g[i] = w.pcg[c0 + i];
+                s_b[i] = w.pcbase[c0 + i];
+                s_a[i] = w.pca[c0 + i];
             }
         }
         __syncthreads();
@@ -2687,8 +2695,8 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
             const int gg = s_g[lo];
             gq[u] = gg;
             aq[u] = s_a[lo];
-            // partner endpoint: read g's k-th write-begin inside it, or write g's k-th read-begin
-            part[u] = (gg < R ? w.wbpos : w.rbpos)[s_b[lo] + q - s_off[lo]];
+            // partner range: read g's k-th write-begin inside it, or write g's k-th read-begin
+            part[u] = (gg < R ? w.wbrange : w.rbrange)[s_b[lo] + q - s_off[lo]];
         }
         int rd[kPairsPerThread], tw[kPairsPerThread];
         bool ok[kPairsPerThread];
@@ -2698,7 +2706,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
             ok[u] = false;
             rd[u] = tw[u] = 0;
             if (gg < 0) continue;
-            const int other = (int)item_range(w.pmeta[part[u]]);
+            const int other = part[u];
             const bool ne = range_nonempty(w, other);  // the pair's own range is: it has pairs
             if (gg < R) {  // read gg, write other: an earlier writer
                 rd[u] = gg;
@@ -2734,7 +2742,7 @@ __global__ __launch_bounds__(kBlock) void k_edge_fill(BatchDev b, Work w) {
 
 void launch_edges(hipStream_t s, const BatchDev& b, const Work& w) {
     const int G = b.R + b.W;
-    launch_scan<3, kEdgeScanP>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys}, nullptr, G, w.scan[kScanEdges]);
+    launch_scan<3, kEdgeScanP>(s, EdgePairScan{w, b.R, G, b.wowner, b.keys, b.rowner, b.T}, nullptr, G, w.scan[kScanEdges]);
     if (G) {
         const int blocks = G / 16 < 64 ? 64 : (G / 16 > 4096 ? 4096 : G / 16);
         fdb_launch(k_edge_fill, dim3(blocks), dim3(kBlock), 0, s, b, w);
@@ -3486,24 +3494,36 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 // inherits, then the exclusive prefixes of removed boundaries, inserted boundaries and tail units
 // with one decoupled look-back across tiles, and tile_first for the copy.  One workgroup per tile
 // of seg_per segments: 2 lookups each (B and E) plus one for the B of the segment before the tile,
-// whose lo bounds the tile's first copy tiles, one lane per lookup: short keys 127 segments per
-// 256-thread workgroup (lane_lower_bound), long keys 63 per 128 threads (lane_lower_bound_long holds
-// the query's tail words in registers).  Round 4's short-key layout (kArity cooperating lanes per
-// lookup, 63 segments per 1024-thread tile) matched it at 5000-txn C2 batches (18.5 vs 18.6 us) but
-// at 32768-txn batches its 1040 tiles chained their prefixes for 116 us per launch, against 46 us
-// for 516 tiles of 127 (53 at 255 segments per tile, 67 at 511: too few lookups in flight).
-constexpr int seg_per(bool long_keys) { return long_keys ? 63 : 127; }
-constexpr int seg_threads(bool long_keys) { return 2 * (seg_per(long_keys) + 1); }
-inline int64_t seg_tiles(int64_t W, bool long_keys) { return (W > 0 ? W : 1) / seg_per(long_keys) + 1; }
-// an upper bound over both layouts (workspace look-back granules)
-inline int64_t seg_prep_tiles(int64_t W) { return seg_tiles(W, true); }
+// whose lo bounds the tile's first copy tiles.  Three layouts:
+//   short keys, W < kSegWideMinW: 1024-thread workgroups, 63 segments per tile, kArity cooperating
+//     lanes per lookup (group_lower_bound): many waves in flight for a small batch (C3 17.2 us per
+//     launch against 24.6 with the wide layout, C2 17.7 against 19.2);
+//   short keys, larger batches (WIDE): 256 threads, 127 segments, one lane per lookup
+//     (lane_lower_bound).  The tiles' look-back chain sets the pace once tiles number in the
+//     hundreds: at 32768-txn C2 batches 1040 narrow tiles took 116 us per launch, 516 wide ones 46
+//     (255 segments per tile: 53, 511: 67, too few lookups in flight);
+//   long keys: 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long holds the
+//     query's tail words in registers).
+constexpr int kSegWideMinW = 24576;
+constexpr int seg_per(bool long_keys, bool wide) { return long_keys || !wide ? 63 : 127; }
+constexpr int seg_lanes(bool long_keys, bool wide) { return long_keys || wide ? 1 : kArity; }
+constexpr int seg_threads(bool long_keys, bool wide) {
+    return 2 * seg_lanes(long_keys, wide) * (seg_per(long_keys, wide) + 1);
+}
+inline bool seg_wide(int64_t W, bool long_keys) { return !long_keys && W >= kSegWideMinW; }
+inline int64_t seg_tiles(int64_t W, bool long_keys) {
+    return (W > 0 ? W : 1) / seg_per(long_keys, seg_wide(W, long_keys)) + 1;
+}
+// an upper bound over the layouts (workspace look-back granules)
+inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / 63 + 1; }
 
-template <bool LONG>
-__global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
-                                                                const uint8_t* htail, Scalars* sc, TierIO io,
-                                                                int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
-                                                                int64_t lvl2_n) {
-    constexpr int SP = seg_per(LONG);
+template <bool LONG, bool WIDE>
+__global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b, Work w, Hist h, MaxLevels hm,
+                                                                      const uint8_t* htail, Scalars* sc, TierIO io,
+                                                                      int64_t* lvl3, int64_t lvl3_n, int64_t* lvl2,
+                                                                      int64_t lvl2_n) {
+    constexpr int SP = seg_per(LONG, WIDE);
+    constexpr int LL = seg_lanes(LONG, WIDE);
     constexpr int NSW = (SP + 1 + 63) / 64;     // waves over the tile's SP + 1 scan entries
     __shared__ int64_t s_lo[SP + 1];            // lo of the segment before the tile, then the tile's
     __shared__ uint32_t s_val[3][SP + 1];       // removed, inserted, tail units per segment
@@ -3522,7 +3542,7 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
     const int ntiles = U > 0 ? (U + SP - 1) / SP : 1;
     if (tile >= ntiles) return;  // spare workgroup: nobody waits on it
     const int64_t n = *io.n_in;
-    const int q = threadIdx.x >> 1, role = threadIdx.x & 1;
+    const int q = threadIdx.x / (2 * LL), role = (threadIdx.x / LL) & 1;
     const int sg = tile * SP + (q < SP ? q : -1);  // slot SP: the segment before
     const bool live = sg >= 0 && sg < U && (q < SP || role == 0);
     int64_t pos = 0;
@@ -3536,14 +3556,16 @@ __global__ __launch_bounds__(seg_threads(LONG)) void k_seg_prep(BatchDev b, Work
             QTail qt;
             load_qtail(qt, key, b.tail);
             pos = lane_lower_bound_long(h, hm, n, key, qt, htail, b.tail, eq);
-        } else {
+        } else if constexpr (WIDE) {
             pos = lane_lower_bound(h, hm, n, key, htail, b.tail, eq);
+        } else {  // the group's kArity lanes search together (live is uniform per group)
+            pos = group_lower_bound<false>(h, hm, n, key, htail, b.tail, eq);
         }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t hi = __shfl(pos, (lane + 1) & 63, 64);
-    const int exact = __shfl((int)eq, (lane + 1) & 63, 64);
-    if (role == 0) {
+    const int64_t hi = __shfl(pos, (lane + LL) & 63, 64);
+    const int exact = __shfl((int)eq, (lane + LL) & 63, 64);
+    if (threadIdx.x % (2 * LL) == 0) {
         if (q == SP) {
             s_lo[0] = live ? pos : 0;
         } else if (live) {
@@ -3820,8 +3842,9 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
-    fdb_launch(long_keys ? k_seg_prep<true> : k_seg_prep<false>, dim3((unsigned)seg_tiles(b.W, long_keys)),
-               dim3(seg_threads(long_keys)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
+    const bool wide = seg_wide(b.W, long_keys);
+    fdb_launch(long_keys ? k_seg_prep<true, false> : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
+               dim3((unsigned)seg_tiles(b.W, long_keys)), dim3(seg_threads(long_keys, wide)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
                dstm.lvl[2], lvl2_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};
