@@ -1,5 +1,5 @@
 #!/bin/bash
-# Edge fill with the begin lists holding ranges and EdgePairScan-staged operands; k_seg_prep's
+# Edge fill step table from EdgePairScan (plus the staged operands and range lists):
 # cooperative layout back for small batches: GPU suite, rocprof C3 / C2, bench C3 / C2.
 set -u
 cd "$(dirname "$0")/.." || exit 1
