@@ -1,0 +1,12 @@
+#!/bin/bash
+# Workspaces in rotation (FDBCS_NUM_WORK 3 vs 4): pipeline tests with 4, then same-box A/B C2 / C4.
+set -u
+cd "$(dirname "$0")/.." || exit 1
+O=gpurun_out/${TAG:-r05nw}
+mkdir -p $O
+FDBCS_NUM_WORK=4 timeout -k 10 600 python -u -m pytest -x -v --timeout 280 --timeout-method thread -p no:cacheprovider tests/test_gpu_fullsize.py -m gpu -k "async_pipeline or flag_before or c4" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for w in c2 c4; do
+  BENCH_ARGS="--workload $w --steps 60 --no-cpu-baseline --breakdown-steps 0 --sync-steps 0 --h2d-steps 0 --total-steps 0" \
+  VARIANTS="w3:FDBCS_NUM_WORK=3 w4:FDBCS_NUM_WORK=4" ROUNDS=3 timeout -k 10 900 bash scripts/gpu_ab_env.sh 2>&1 | sed "s/^/$w /" || exit 1
+done
