@@ -238,6 +238,7 @@ struct fdbcs_conflict_set {
     // chain; over a 5M base (C2) the single launch measured faster (device-resident 34.0M vs
     // 32.1M txns/s: one launch and two cross-stream events fewer, no third stream competing)
     int split_check = 2;
+    int64_t delta_floor = 1250000;  // FDBCS_DELTA_FLOOR: delta bound floor (delta_limit_for); 0 = N/16
     hipStream_t ustream = nullptr;  // batch uploads (k_upload over PCIe), so batch i+1's upload overlaps
                                     // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
@@ -707,9 +708,14 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
 
 // Automatic delta bound: about 1/16 of the base, so a batch's merge touches a small tier and a
 // compaction (a full rewrite of the base) is amortised over many batches.
+// The delta tier's bound: N/16, raised towards N/4 up to delta_floor boundaries.  A compaction
+// rewrites the whole base on Y and the next check waits for it, so on a 5M-boundary base fewer,
+// larger deltas pay although every merge copies more: C2 54.6 -> 56.7M, C3 45.9 -> 50.4M, C2 at
+// 32768-txn batches 91.1 -> 92.9M over 150-400-batch windows with a 1.25M bound
+// (scripts/gpu_r05_dl*.sh); a 50M base (C4) keeps N/16 = 3.1M.
 int64_t delta_limit_for(const fdbcs_conflict_set* cs, int64_t n_base) {
     if (cs->delta_limit > 0) return cs->delta_limit;
-    return std::max<int64_t>(1 << 16, n_base / 16);
+    return std::max<int64_t>({(int64_t)1 << 16, n_base / 16, std::min<int64_t>(n_base / 4, cs->delta_floor)});
 }
 
 
@@ -1446,6 +1452,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_HELPER_Y")) cs->helper_y = v[0] != '0';
+    if (const char* v = getenv("FDBCS_DELTA_FLOOR")) cs->delta_floor = std::max<long long>(0, atoll(v));
     if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_DIR_RANK")) cs->dir_rank = v[0] != '0';

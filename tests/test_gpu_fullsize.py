@@ -65,6 +65,7 @@ def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
     detect (FDBCS_LAG)."""
     monkeypatch.setenv("FDBCS_SUBMIT_THREAD", "0" if submit_thread == "lag" else submit_thread)
     monkeypatch.setenv("FDBCS_LAG", "1" if submit_thread == "lag" else "0")
+    monkeypatch.setenv("FDBCS_DELTA_FLOOR", "0")  # the N/16 bound: a compaction every ~16 batches
     p = W.C2Params()
     start = 10_000_000
     kb, ko, vers = W.c2_history(p, seed=1, start_version=start)
