@@ -63,7 +63,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--window", type=int, default=8, help="batches in flight in the timed loops")
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200,
+                    help="timed batches; the default spans several delta compactions (one every ~60 C2 "
+                    "batches), so the rate carries their cost")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--txns", type=int, default=0, help="transactions per batch per GPU; 0 = the workload's")
     ap.add_argument("--history", type=int, default=0,
