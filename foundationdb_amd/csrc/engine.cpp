@@ -337,6 +337,10 @@ struct fdbcs_conflict_set {
     int upload_kernel = 0;    // FDBCS_UPLOAD=kernel: batches go up by a copy kernel over PCIe, not the DMA engine
     int long_lanes = 1;       // FDBCS_LONG_LANES=0: batches of keys over 24 bytes take the kArity-lane
                               // lookups (6) under FDBCS_CHECK=7 (round 3's layout, for A/B)
+    int compact_lanes = 2;    // FDBCS_COMPACT_LANES: k_compact_search mode (0: kArity lanes per delta
+                              // boundary; 1: one lane; 2: one lane, the long-key form after long batches)
+    int base_tile = 0;        // FDBCS_BASE_TILE: base boundaries per copy tile of a compaction (1024/2048/4096;
+                              // 0: 1024 up to 16M boundaries, C2 185 vs 223 us per copy, else 4096)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
     bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
     bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
@@ -1459,6 +1463,8 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_DIR_BITS")) cs->dir_bits = std::max(0, std::min(kDirMaxBits, atoi(v)));
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
+    if (const char* v = getenv("FDBCS_BASE_TILE")) cs->base_tile = atoi(v);
+    if (const char* v = getenv("FDBCS_COMPACT_LANES")) cs->compact_lanes = std::max(0, std::min(2, atoi(v)));
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
     if (const char* v = getenv("FDBCS_LAG")) cs->lag = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
@@ -2806,7 +2812,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (compact) {
         launch_compact(ys, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
                        cs->header_version, cs->lvl3_n, cs->lvl2_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
-                       rec(kPhCompEnd, 1));
+                       rec(kPhCompEnd, 1), cs->compact_lanes == 2 && !long_keys ? 1 : cs->compact_lanes,
+                       cs->base_tile ? cs->base_tile : (cs->n_ub <= (16 << 20) ? 1024 : 4096));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
         // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th

@@ -3677,6 +3677,9 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
         }
         __syncthreads();
         const int ja = s_j0, cnt = s_cnt;
+        int top = 0;  // the largest power of two <= cnt (0 for none): the lifting's first step
+        if (cnt > 0 && cnt <= kSegLds)
+            for (top = 1; 2 * top <= cnt;) top *= 2;
         if (cnt <= kSegLds) {
             // slot k <-> segment ja-1+k for k in [0, cnt]; slot holds lo/hi of that segment and the
             // shift applying to elements after it (= shift of segment index ja+k as prefix)
@@ -3701,6 +3704,7 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                     int sl = 0;  // last slot with s_lo <= i (slot 0 always qualifies)
 #pragma unroll
                     for (int step = kSegLds; step > 0; step >>= 1) {
+                        if (step > top) continue;
                         const int mid = sl + step;
                         if (mid <= cnt && s_lo[mid] <= i) sl = mid;
                     }
@@ -3870,6 +3874,10 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
 // of an earlier merge and becomes a real boundary carrying the base version at d_j, unless the
 // base already has a boundary at d_j.  The result is the boundary set the reference would hold.
 
+// MODE 0: kArity lanes per delta boundary (group_lower_bound); 1: one lane per boundary
+// (lane_lower_bound); 2: one lane, the long-key form (lane_lower_bound_long: tuple keys sharing
+// 16-byte prefixes).  Same result for every mode (FDBCS_COMPACT_LANES picks it).
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels basem, Hist delta,
                                                            const uint8_t* htail, const int64_t* nb_ptr,
                                                            const int64_t* nd_ptr, int64_t hdr, Work w, int64_t* lvl3,
@@ -3877,7 +3885,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = gt; i < lvl3_n * kL3Rep; i += (int64_t)gridDim.x * blockDim.x) lvl3[i * kL3Pad] = LLONG_MIN;
     for (int64_t i = gt; i < lvl2_n; i += (int64_t)gridDim.x * blockDim.x) lvl2[i] = LLONG_MIN;
-    const int64_t j = gt / kArity;  // kArity lanes per delta boundary (cooperative search)
+    const int64_t j = MODE == 0 ? gt / kArity : gt;  // MODE 0: kArity lanes per delta boundary
     const int64_t nd = *nd_ptr;
     if (j >= nd) return;  // whole groups leave together
     const int64_t nb = *nb_ptr;
@@ -3889,8 +3897,18 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     q.len = lt.x;
     q.tail = 0;  // the query's tail arena below starts at its own tail
     bool exact;
-    const int64_t lo = group_lower_bound(base, basem, nb, q, htail, hist_tail(htail, lt.y), exact);
-    if ((gt % kArity) != 0) return;
+    const uint8_t* qtail = hist_tail(htail, lt.y);
+    int64_t lo;
+    if constexpr (MODE == 0) {
+        lo = group_lower_bound(base, basem, nb, q, htail, qtail, exact);
+        if ((gt % kArity) != 0) return;
+    } else if constexpr (MODE == 1) {
+        lo = lane_lower_bound(base, basem, nb, q, htail, qtail, exact);
+    } else {
+        QTail qt;
+        load_qtail(qt, q, qtail);
+        lo = lane_lower_bound_long(base, basem, nb, q, qt, htail, qtail, exact);
+    }
     const int64_t dv = delta.ver[j];
     w.c_lo[j] = lo;
     w.c_exact[j] = exact ? 1 : 0;
@@ -3905,6 +3923,7 @@ struct CompactSumScan {
     const uint8_t* exact;
     TierIO io;
     const int64_t* nd_ptr;
+    int tile;  // the copy tile of k_merge_copy<CompactIns, tile>
     __device__ int64_t hi_of(int64_t j) const {
         if (dver[j] == kHole) return g.lo[j];
         return j + 1 < *nd_ptr ? g.lo[j + 1] : *io.n_in;
@@ -3917,13 +3936,13 @@ struct CompactSumScan {
         g.hi[j] = hi_of(j);
         g.rem[j] = ex[0];
         g.ins[j] = ex[1];
-        fill_tile_first(g.tile_first, g.lo, j, kBaseTile);
+        fill_tile_first(g.tile_first, g.lo, j, tile);
     }
     __device__ void finish(const uint32_t (&tot)[2]) const {
         const int64_t U = *nd_ptr, n = *io.n_in;
         g.rem[U] = tot[0];
         g.ins[U] = tot[1];
-        fill_tile_first_tail(g.tile_first, g.lo, U, n, kBaseTile);
+        fill_tile_first_tail(g.tile_first, g.lo, U, n, tile);
         *io.before = n;
         *io.removed = tot[0];
         *io.n_out = n - (int64_t)tot[0] + (int64_t)tot[1];
@@ -3944,20 +3963,33 @@ struct CompactIns {
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                    hipEvent_t copy_end) {
-    int64_t blocks = (kArity * delta_hint_n + kBlock - 1) / kBlock;
+                    hipEvent_t copy_end, int mode, int base_tile) {
+    int64_t blocks = ((mode == 0 ? kArity : 1) * delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
-    fdb_launch(k_compact_search, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
-                       &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
+    if (mode == 0)
+        fdb_launch(k_compact_search<0>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
+                   &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
+    else if (mode == 1)
+        fdb_launch(k_compact_search<1>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
+                   &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
+    else
+        fdb_launch(k_compact_search<2>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
+                   &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
     const Segs g{w.c_lo, w.c_hi, w.c_rem, w.c_ins, w.tile_first};
     const TierIO io{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem};
-    launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next}, &sc->nd_next, delta_hint_n + 1,
-                   w.scan[kScanCompact]);
+    const int tile = base_tile == 1024 || base_tile == 2048 ? base_tile : kBaseTile;
+    launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next, tile}, &sc->nd_next,
+                   delta_hint_n + 1, w.scan[kScanCompact]);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
-    fdb_launch((k_merge_copy<CompactIns, kBaseTile>), dim3(copy_tiles(grid_hint_n, kBaseTile, delta_hint_n + 1)),
-                       dim3(kBlock), 0,
-                       s, g, base, dst,
-                       &sc->n, &sc->nd_next, CompactIns{delta, w.c_val, w.c_ins});
+    const dim3 grid(copy_tiles(grid_hint_n, tile, delta_hint_n + 1));
+    const CompactIns ins{delta, w.c_val, w.c_ins};
+    if (tile == 1024)
+        fdb_launch((k_merge_copy<CompactIns, 1024>), grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next, ins);
+    else if (tile == 2048)
+        fdb_launch((k_merge_copy<CompactIns, 2048>), grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next, ins);
+    else
+        fdb_launch((k_merge_copy<CompactIns, kBaseTile>), grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next,
+                   ins);
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 

@@ -29,6 +29,8 @@ KNOBS = {
     "FDBCS_SPLIT_CHECK": ["2", "1"],
     "FDBCS_LONG_LANES": ["1", "0"],
     "FDBCS_SKIP_EDGES": ["1", "0"],
+    "FDBCS_COMPACT_LANES": ["2", "1", "0"],
+    "FDBCS_BASE_TILE": ["4096", "2048", "1024"],
 }
 
 

@@ -441,6 +441,19 @@ def test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, gc_interval, d
         assert e.cs.history_size() == o.history_size()
 
 
+@pytest.mark.parametrize("mode,tile", [("0", "4096"), ("1", "2048"), ("2", "1024"), ("2", "4096")])
+def test_compaction_search_modes(engine, oracle_mod, monkeypatch, mode, tile):
+    """Every k_compact_search mode (FDBCS_COMPACT_LANES: kArity lanes per delta boundary, one lane,
+    one lane in the long-key form) places the delta boundaries alike, and every copy tile of the
+    compaction's merge copy (FDBCS_BASE_TILE) moves them alike: compactions over tails behind a
+    60-byte shared prefix, over a tiny alphabet, and over C4 tuple keys stay verdict-exact."""
+    monkeypatch.setenv("FDBCS_COMPACT_LANES", mode)
+    monkeypatch.setenv("FDBCS_BASE_TILE", tile)
+    test_long_shared_prefix_tails(engine, oracle_mod, 0, 40)
+    test_delta_tier_configurations(engine, oracle_mod, 0, 25)
+    test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, 0, 3000, "2")
+
+
 def test_async_pipelined_batches_match_sync(engine):
     rng = np.random.default_rng(4)
     batches = []
