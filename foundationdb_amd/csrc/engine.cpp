@@ -339,6 +339,8 @@ struct fdbcs_conflict_set {
                               // lookups (6) under FDBCS_CHECK=7 (round 3's layout, for A/B)
     int compact_lanes = 2;    // FDBCS_COMPACT_LANES: k_compact_search mode (0: kArity lanes per delta
                               // boundary; 1: one lane; 2: one lane, the long-key form after long batches)
+    bool seg_long_coop = false;  // FDBCS_SEG_LONG_COOP=1: the segment search of long-key batches by kArity
+                                 // lanes per lookup (group_lower_bound<true>), not one lane
     int base_tile = 0;        // FDBCS_BASE_TILE: base boundaries per copy tile of a compaction (1024/2048/4096;
                               // 0: 1024 up to 16M boundaries, C2 185 vs 223 us per copy, else 4096)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
@@ -1464,6 +1466,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_BASE_TILE")) cs->base_tile = atoi(v);
+    if (const char* v = getenv("FDBCS_SEG_LONG_COOP")) cs->seg_long_coop = v[0] != '0';
     if (const char* v = getenv("FDBCS_COMPACT_LANES")) cs->compact_lanes = std::max(0, std::min(2, atoi(v)));
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
     if (const char* v = getenv("FDBCS_LAG")) cs->lag = atoi(v) != 0;
@@ -2804,7 +2807,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // D.MergeWrite into the delta tier
     char* hd = (char*)sl->pin_out.dp;
     launch_merge(ys, bd, w, delta.h, delta.m, delta_of(cs, dnew), dlevels_of(cs, dnew), &sc->ndb[dsrc], htail, sc, now,
-                 cs->dlvl3_n, cs->dlvl2_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
+                 cs->dlvl3_n, cs->dlvl2_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys,
+                 cs->seg_long_coop);
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;

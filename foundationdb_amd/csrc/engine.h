@@ -427,7 +427,7 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
                   int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end, bool long_keys = false);
+                  hipEvent_t copy_end, bool long_keys = false, bool long_coop = false);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,

@@ -1142,7 +1142,10 @@ __device__ __forceinline__ void lane_prefix_run(const Hist& h, const MaxLevels& 
     e = ae + ce;
 }
 
-// lane_lower_bound for long keys (same result and eq); qt: q's tail words (load_qtail).
+// lane_lower_bound for long keys (same result and eq); qt: q's tail words (load_qtail).  RP: probes
+// per round inside a prefix run (more per round made k_seg_prep's few, latency-bound lookups slower
+// at C4: 37.7 / 41.4 / 42.9 us at 3 / 5 / 7).
+template <int RP = kRunProbes>
 __device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
                                                          const QTail& qt, const uint8_t* htail, const uint8_t* qtail,
                                                          bool& eq) {
@@ -1162,19 +1165,19 @@ __device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const Ma
     while (lo < hh) {
         const int64_t span = hh - lo;
         const int w0 = dlo < dhi ? dlo : dhi;  // tail words every boundary in [lo, hh) shares with q
-        int64_t p[kRunProbes];
-        bool v[kRunProbes];
-        uint2 lt[kRunProbes];
+        int64_t p[RP];
+        bool v[RP];
+        uint2 lt[RP];
 #pragma unroll
-        for (int j = 0; j < kRunProbes; j++) {
-            p[j] = lo + (span * (j + 1)) / (kRunProbes + 1);
+        for (int j = 0; j < RP; j++) {
+            p[j] = lo + (span * (j + 1)) / (RP + 1);
             v[j] = p[j] < hh && (j == 0 || p[j] != p[j - 1]);
             if (v[j]) lt[j] = h.lt[p[j]];
         }
-        uint64_t x[kRunProbes][kQW];
-        uint32_t nb[kRunProbes];
+        uint64_t x[RP][kQW];
+        uint32_t nb[RP];
 #pragma unroll
-        for (int j = 0; j < kRunProbes; j++) {
+        for (int j = 0; j < RP; j++) {
             nb[j] = v[j] && qlong && lt[j].x > 16u ? (lt[j].x < q.len ? lt[j].x : q.len) - 16u : 0u;
             const uint64_t* ha = (const uint64_t*)hist_tail(htail, v[j] ? lt[j].y : 0u);
             const int nw = (int)((nb[j] + 7u) / 8u);
@@ -1182,9 +1185,9 @@ __device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const Ma
             for (int u = 0; u < kQW; u++)
                 if (u >= w0 && u < nw) x[j][u] = ha[u];
         }
-        int r[kRunProbes], d[kRunProbes];
+        int r[RP], d[RP];
 #pragma unroll
-        for (int j = 0; j < kRunProbes; j++) {
+        for (int j = 0; j < RP; j++) {
             r[j] = 1;
             d[j] = 0;
             if (!v[j]) continue;
@@ -1219,7 +1222,7 @@ __device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const Ma
         int ndlo = dlo, ndhi = dhi;
         bool neq = eq_hh, hit = false;
 #pragma unroll
-        for (int j = 0; j < kRunProbes; j++) {
+        for (int j = 0; j < RP; j++) {
             if (!v[j] || hit) continue;
             if (r[j] < 0) {
                 nlo = p[j] + 1;
@@ -3502,18 +3505,20 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 //     (lane_lower_bound).  The tiles' look-back chain sets the pace once tiles number in the
 //     hundreds: at 32768-txn C2 batches 1040 narrow tiles took 116 us per launch, 516 wide ones 46
 //     (255 segments per tile: 53, 511: 67, too few lookups in flight);
-//   long keys: 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long holds the
-//     query's tail words in registers).
+//   long keys (WIDE): 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long holds
+//     the query's tail words in registers);
+//   long keys, coop (FDBCS_SEG_LONG_COOP=1): 1024 threads, 63 segments, kArity lanes per lookup
+//     (group_lower_bound<true>).
 constexpr int kSegWideMinW = 24576;
 constexpr int seg_per(bool long_keys, bool wide) { return long_keys || !wide ? 63 : 127; }
-constexpr int seg_lanes(bool long_keys, bool wide) { return long_keys || wide ? 1 : kArity; }
+constexpr int seg_lanes(bool, bool wide) { return wide ? 1 : kArity; }
 constexpr int seg_threads(bool long_keys, bool wide) {
     return 2 * seg_lanes(long_keys, wide) * (seg_per(long_keys, wide) + 1);
 }
-inline bool seg_wide(int64_t W, bool long_keys) { return !long_keys && W >= kSegWideMinW; }
-inline int64_t seg_tiles(int64_t W, bool long_keys) {
-    return (W > 0 ? W : 1) / seg_per(long_keys, seg_wide(W, long_keys)) + 1;
+inline bool seg_wide(int64_t W, bool long_keys, bool long_coop) {
+    return long_keys ? !long_coop : W >= kSegWideMinW;
 }
+inline int64_t seg_tiles(int64_t W, bool long_keys, bool wide) { return (W > 0 ? W : 1) / seg_per(long_keys, wide) + 1; }
 // an upper bound over the layouts (workspace look-back granules)
 inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / 63 + 1; }
 
@@ -3552,10 +3557,12 @@ __global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b
         kb = seg_key(b, w, w.seg_b[sg], 0);
         ke = seg_key(b, w, w.seg_e[sg], 1);
         const DKey& key = role ? ke : kb;
-        if constexpr (LONG) {
+        if constexpr (LONG && WIDE) {
             QTail qt;
             load_qtail(qt, key, b.tail);
             pos = lane_lower_bound_long(h, hm, n, key, qt, htail, b.tail, eq);
+        } else if constexpr (LONG) {  // kArity lanes per lookup, long-key probes
+            pos = group_lower_bound<true>(h, hm, n, key, htail, b.tail, eq);
         } else if constexpr (WIDE) {
             pos = lane_lower_bound(h, hm, n, key, htail, b.tail, eq);
         } else {  // the group's kArity lanes search together (live is uniform per group)
@@ -3842,13 +3849,14 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
                   int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end, bool long_keys) {
+                  hipEvent_t copy_end, bool long_keys, bool long_coop) {
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
-    const bool wide = seg_wide(b.W, long_keys);
-    fdb_launch(long_keys ? k_seg_prep<true, false> : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
-               dim3((unsigned)seg_tiles(b.W, long_keys)), dim3(seg_threads(long_keys, wide)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
+    const bool wide = seg_wide(b.W, long_keys, long_coop);
+    fdb_launch(long_keys ? (wide ? k_seg_prep<true, true> : k_seg_prep<true, false>)
+                         : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
+               dim3((unsigned)seg_tiles(b.W, long_keys, wide)), dim3(seg_threads(long_keys, wide)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
                dstm.lvl[2], lvl2_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     BatchIns ins{};

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Probes per round of the long-key segment search (FDBCS_SEG_PROBES 3/5/7): parity, rocprof of C4
+# per setting, then same-box bench A/B.
+set -u
+cd "$(dirname "$0")/.." || exit 1
+O=gpurun_out/${TAG:-r05sp}
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread -m gpu \
+  -k "compaction_search_modes or long_shared or c4_tuple" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for c in 3 5 7; do
+  FDBCS_SEG_PROBES=$c WORKLOAD=c4 OUT=$O/p_c4_$c STEPS=100 timeout -k 10 400 bash scripts/gpu_profile.sh || exit 1
+  echo "probes $c: $(grep -h 'seg_prep' $O/p_c4_$c/summary.txt | sed 's/  */ /g' | cut -c1-90)"
+done
+for r in 1 2; do
+  for c in 3 5 7; do
+    FDBCS_SEG_PROBES=$c timeout -k 10 300 python bench.py --workload c4 --steps 200 --warmup 20 --no-cpu-baseline \
+      --breakdown-steps 0 --sync-steps 0 --h2d-steps 0 --total-steps 0 > $O/b_${c}_${r}.json 2> $O/b_${c}_$r.err || exit 1
+    python3 -c "
+import json;d=json.load(open('$O/b_${c}_${r}.json'))
+print('c4 probes $c r$r value %.2fM'%(d['value']/1e6), 'ms/step %.4f'%d['ms_per_step'])"
+  done
+done

@@ -31,6 +31,7 @@ KNOBS = {
     "FDBCS_SKIP_EDGES": ["1", "0"],
     "FDBCS_COMPACT_LANES": ["2", "1", "0"],
     "FDBCS_BASE_TILE": ["4096", "2048", "1024"],
+    "FDBCS_SEG_LONG_COOP": ["0", "1"],
 }
 
 
