@@ -341,6 +341,9 @@ struct fdbcs_conflict_set {
                               // boundary; 1: one lane; 2: one lane, the long-key form after long batches)
     bool seg_long_coop = false;  // FDBCS_SEG_LONG_COOP=1: the segment search of long-key batches by kArity
                                  // lanes per lookup (group_lower_bound<true>), not one lane
+    int copy_nt = -1;         // FDBCS_COPY_NT: the compaction copy by non-temporal loads/stores (1), not (0);
+                              // -1: above 16M base boundaries (C4: 1022 -> 919 us per 50M-boundary copy;
+                              // C2: 185 -> 180 us, but the bench line no better)
     int base_tile = 0;        // FDBCS_BASE_TILE: base boundaries per copy tile of a compaction (1024/2048/4096;
                               // 0: 1024 up to 16M boundaries, C2 185 vs 223 us per copy, else 4096)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
@@ -1466,6 +1469,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
     if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
     if (const char* v = getenv("FDBCS_BASE_TILE")) cs->base_tile = atoi(v);
+    if (const char* v = getenv("FDBCS_COPY_NT")) cs->copy_nt = v[0] != '0';
     if (const char* v = getenv("FDBCS_SEG_LONG_COOP")) cs->seg_long_coop = v[0] != '0';
     if (const char* v = getenv("FDBCS_COMPACT_LANES")) cs->compact_lanes = std::max(0, std::min(2, atoi(v)));
     if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
@@ -2817,7 +2821,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         launch_compact(ys, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
                        cs->header_version, cs->lvl3_n, cs->lvl2_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
                        rec(kPhCompEnd, 1), cs->compact_lanes == 2 && !long_keys ? 1 : cs->compact_lanes,
-                       cs->base_tile ? cs->base_tile : (cs->n_ub <= (16 << 20) ? 1024 : 4096));
+                       cs->base_tile ? cs->base_tile : (cs->n_ub <= (16 << 20) ? 1024 : 4096),
+                       cs->copy_nt >= 0 ? cs->copy_nt != 0 : cs->n_ub > (16 << 20));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
         // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th

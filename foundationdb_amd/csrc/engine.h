@@ -432,7 +432,7 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                    hipEvent_t copy_end, int mode, int base_tile);
+                    hipEvent_t copy_end, int mode, int base_tile, bool nt);
 // removeBefore over the whole base (src -> dst); the live tails are repacked from arena tsrc into
 // the empty arena tdst (reclaiming the bytes of removed and overwritten boundaries).
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,

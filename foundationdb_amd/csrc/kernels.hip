@@ -3657,6 +3657,20 @@ __global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b
 
 constexpr int kSegLds = 1024;
 
+// Streaming (non-temporal) moves for the compaction's whole-base copy: gigabytes read once and
+// written once, kept out of the caches the concurrent read checks use (FDBCS_COPY_NT A/B).
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+template <bool NT, class T>
+__device__ __forceinline__ T stream_load(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, class T>
+__device__ __forceinline__ void stream_store(T* p, const T& v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Copy surviving old boundaries to their new positions and write each segment's inserts.  Per
 // tile, the segments that can affect it are staged in LDS; element i is removed iff
 // lo_j <= i < hi_j for the last segment j with lo_j <= i, else it moves to i - rem_before +
@@ -3664,7 +3678,7 @@ constexpr int kSegLds = 1024;
 // are spread over the whole grid (grid-stride over the segments), not over the copy tiles that own
 // their positions: right after a compaction the delta is nearly empty and one copy tile owns every
 // segment of the batch (at the reference's 32768-transaction cap, ~60k inserts by one workgroup).
-template <class Ins, int TILE>
+template <class Ins, int TILE, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist dst, const int64_t* n_in,
                                                        const int64_t* U_ptr, Ins ins) {
     __shared__ int64_t s_lo[kSegLds + 1], s_hi[kSegLds + 1], s_shift[kSegLds + 1];
@@ -3718,23 +3732,22 @@ __global__ __launch_bounds__(kBlock) void k_merge_copy(Segs g, Hist src, Hist ds
                     const bool keep = i < i1 && !(i >= s_lo[sl] && i < s_hi[sl]);  // else inside a written span
                     dsto[k] = keep ? i + s_shift[sl] : -1;
                 }
-                uint64_t khi[kPer], klo[kPer], lt[kPer], vv[kPer];
+                u64x2 kk[kPer];
+                uint64_t lt[kPer], vv[kPer];
 #pragma unroll
                 for (int k = 0; k < kPer; k++) {
                     const int64_t i = c0 + k * kBlock + threadIdx.x;
                     const int64_t j = dsto[k] >= 0 ? i : i0;  // always-valid address, loads stay unconditional
-                    const ulonglong2 kv = src.key[j];
-                    khi[k] = kv.x;
-                    klo[k] = kv.y;
-                    lt[k] = reinterpret_cast<const uint64_t*>(src.lt)[j];
-                    vv[k] = (uint64_t)src.ver[j];
+                    kk[k] = stream_load<NT>(reinterpret_cast<const u64x2*>(src.key) + j);
+                    lt[k] = stream_load<NT>(reinterpret_cast<const uint64_t*>(src.lt) + j);
+                    vv[k] = stream_load<NT>(reinterpret_cast<const uint64_t*>(src.ver) + j);
                 }
 #pragma unroll
                 for (int k = 0; k < kPer; k++) {
                     if (dsto[k] >= 0) {
-                        dst.key[dsto[k]] = make_ulonglong2(khi[k], klo[k]);
-                        reinterpret_cast<uint64_t*>(dst.lt)[dsto[k]] = lt[k];
-                        dst.ver[dsto[k]] = (int64_t)vv[k];
+                        stream_store<NT>(reinterpret_cast<u64x2*>(dst.key) + dsto[k], kk[k]);
+                        stream_store<NT>(reinterpret_cast<uint64_t*>(dst.lt) + dsto[k], lt[k]);
+                        stream_store<NT>(reinterpret_cast<uint64_t*>(dst.ver) + dsto[k], vv[k]);
                     }
                 }
             }
@@ -3971,7 +3984,7 @@ struct CompactIns {
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                    hipEvent_t copy_end, int mode, int base_tile) {
+                    hipEvent_t copy_end, int mode, int base_tile, bool nt) {
     int64_t blocks = ((mode == 0 ? kArity : 1) * delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     if (mode == 0)
@@ -3991,13 +4004,10 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     const dim3 grid(copy_tiles(grid_hint_n, tile, delta_hint_n + 1));
     const CompactIns ins{delta, w.c_val, w.c_ins};
-    if (tile == 1024)
-        fdb_launch((k_merge_copy<CompactIns, 1024>), grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next, ins);
-    else if (tile == 2048)
-        fdb_launch((k_merge_copy<CompactIns, 2048>), grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next, ins);
-    else
-        fdb_launch((k_merge_copy<CompactIns, kBaseTile>), grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next,
-                   ins);
+    auto k = tile == 1024 ? (nt ? k_merge_copy<CompactIns, 1024, true> : k_merge_copy<CompactIns, 1024>)
+             : tile == 2048 ? (nt ? k_merge_copy<CompactIns, 2048, true> : k_merge_copy<CompactIns, 2048>)
+                            : (nt ? k_merge_copy<CompactIns, kBaseTile, true> : k_merge_copy<CompactIns, kBaseTile>);
+    fdb_launch(k, grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next, ins);
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 

@@ -32,6 +32,7 @@ KNOBS = {
     "FDBCS_COMPACT_LANES": ["2", "1", "0"],
     "FDBCS_BASE_TILE": ["4096", "2048", "1024"],
     "FDBCS_SEG_LONG_COOP": ["0", "1"],
+    "FDBCS_COPY_NT": ["0", "1"],
 }
 
 

@@ -441,16 +441,18 @@ def test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, gc_interval, d
         assert e.cs.history_size() == o.history_size()
 
 
-@pytest.mark.parametrize("mode,tile,coop", [("0", "4096", "0"), ("1", "2048", "1"), ("2", "1024", "0"), ("2", "4096", "1")])
-def test_compaction_search_modes(engine, oracle_mod, monkeypatch, mode, tile, coop):
+@pytest.mark.parametrize("mode,tile,coop,nt", [("0", "4096", "0", "1"), ("1", "2048", "1", "0"), ("2", "1024", "0", "0"),
+                                               ("2", "4096", "1", "0")])
+def test_compaction_search_modes(engine, oracle_mod, monkeypatch, mode, tile, coop, nt):
     """Every k_compact_search mode (FDBCS_COMPACT_LANES: kArity lanes per delta boundary, one lane,
     one lane in the long-key form) places the delta boundaries alike, and every copy tile of the
-    compaction's merge copy (FDBCS_BASE_TILE) moves them alike, as does either segment search of
+    compaction's merge copy (FDBCS_BASE_TILE, non-temporal or not: FDBCS_COPY_NT) moves them alike, as does either segment search of
     long-key batches (FDBCS_SEG_LONG_COOP): compactions over tails behind a 60-byte shared prefix,
     over a tiny alphabet, and over C4 tuple keys stay verdict-exact."""
     monkeypatch.setenv("FDBCS_COMPACT_LANES", mode)
     monkeypatch.setenv("FDBCS_BASE_TILE", tile)
     monkeypatch.setenv("FDBCS_SEG_LONG_COOP", coop)
+    monkeypatch.setenv("FDBCS_COPY_NT", nt)
     test_long_shared_prefix_tails(engine, oracle_mod, 0, 40)
     test_delta_tier_configurations(engine, oracle_mod, 0, 25)
     test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, 0, 3000, "2")
