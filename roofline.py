@@ -148,7 +148,7 @@ def kernel_bytes(name: str, s: dict):
         return s["merge_bytes"], "32 B per kept and inserted boundary read and per result boundary written (device scalars)"
     if name.startswith("k_merge_copy<fdbcs::CompactIns"):
         return s["compact_bytes"], "32 B per kept base / inserted delta boundary read and per result boundary written"
-    if name == "k_compact_search":
+    if name.startswith("k_compact_search"):
         return Nd * (P + 8 + lookup_bytes(N, s["dir_share"]) + 17), "per delta boundary: key + lookup in the base, 2 words"
     if name.startswith("k_scan<2, fdbcs::CompactSumScan"):
         return Nd * (8 + 8 + 1 + 24), "per delta boundary: lo, version, exact flag; 3 words written"
