@@ -63,9 +63,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--window", type=int, default=8, help="batches in flight in the timed loops")
-    ap.add_argument("--steps", type=int, default=200,
-                    help="timed batches; the default spans several delta compactions (one every ~60 C2 "
-                    "batches), so the rate carries their cost")
+    ap.add_argument("--steps", type=int, default=20,
+                    help="timed batches (the driver's count); --steps 200 spans several delta compactions")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--txns", type=int, default=0, help="transactions per batch per GPU; 0 = the workload's")
     ap.add_argument("--history", type=int, default=0,
@@ -74,8 +73,9 @@ def parse():
     ap.add_argument("--gc-interval", type=int, default=0,
                     help="force a compaction (+GC) at least every N batches; 0 = when the delta tier is full")
     ap.add_argument("--delta-limit", type=int, default=0, help="delta-tier bound; 0 = automatic (~base/16)")
-    ap.add_argument("--timing", type=int, default=1, choices=[0, 1],
-                    help="events in the timed region: 0 none, 1 around the hot kernels (roofline)")
+    ap.add_argument("--roof-steps", type=int, default=32,
+                    help="batches of the roofline pass (events around the dominant kernel, 1 batch in 4), run "
+                    "after the timed region so that no event record sits inside it; 0 = no roofline")
     ap.add_argument("--total-steps", type=int, default=-1,
                     help="batches of the add+detect ('total') pass; -1 = --steps, 0 = skip")
     ap.add_argument("--h2d-steps", type=int, default=20,
@@ -374,7 +374,7 @@ def main():
     spans = {}
     at = 0
     for name, n in (("warmup", args.warmup), ("profile", args.profile_steps), ("timed", args.steps),
-                    ("h2d", args.h2d_steps), ("total", n_total), ("sync", args.sync_steps),
+                    ("roof", args.roof_steps), ("h2d", args.h2d_steps), ("total", n_total), ("sync", args.sync_steps),
                     ("hold", args.hold_steps), ("breakdown", args.breakdown_steps)):
         spans[name] = (at, at + n)
         at += n
@@ -577,6 +577,9 @@ def main():
         return objs
 
     def barrier():
+        # the engine's streams live in its own HIP runtime: torch.cuda.synchronize()
+        # does not wait for them, so every upload and stage already issued is drained here
+        cs.sync()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -618,19 +621,25 @@ def main():
         if ranked:
             dominant = ranked[0]
             dominant_source = "rocprofv3 kernel trace: " + rp_note
-    cs.set_timing(args.timing)
-    if dominant and args.timing >= 1:
-        cs.set_timed_kernel(dominant)
+    cs.set_timing(0)
+    # resolved now, while the profile pass's kernel list still names it; recorded only at timing 1
+    cs.set_timed_kernel(dominant)
+
+    def resident(lo, hi):
+        """Batches lo..hi-1 packed and their H2D issued (a rank's proxy share likewise); the caller's
+        barrier() then waits for the copies on the engine's upload stream."""
+        objs = packed(lo, hi)
+        for i, o in objs.items():
+            if droute:
+                objs[i] = o.to(cdev)
+            else:
+                o.upload()
+        return objs
 
     # `value`: the batches' inputs resident in HBM when the timed region starts (each batch's packed
-    # H2D issued and finished before it; a rank's proxy share likewise) -- the PCIe-inclusive rate
-    # is the h2d pass below
-    objs = packed(timed_lo, timed_hi)
-    for i, o in objs.items():
-        if droute:
-            objs[i] = o.to(cdev)
-        else:
-            o.upload()
+    # H2D issued and drained by barrier() before it; a rank's proxy share likewise) -- the
+    # PCIe-inclusive rate is the h2d pass below.  No event is recorded inside the region.
+    objs = resident(timed_lo, timed_hi)
     cs.reset_stats()
     barrier()
     for k in host:
@@ -640,12 +649,28 @@ def main():
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t_start)
     st = cs.stats()
-    kprof_timed = cs.kernel_profile()
     host_timed = {k: v / args.steps * 1e3 for k, v in host.items()}
     for k in ("host_ms_prepare", "host_ms_record", "host_ms_submit"):  # inside detect_async (engine's clock)
         host_timed["engine_" + k[8:]] = st[k] / max(1, st["batches"])
-    cs.set_timed_kernel(None)
-    cs.set_timing(0)
+
+    # roofline pass: the same pipeline on its own resident batches, with events around the dominant
+    # kernel on 1 batch in 4 (on the stream it runs on)
+    kprof_timed = {}
+    st_roof = st
+    roof_elapsed = None
+    if dominant and args.roof_steps > 0:
+        objs = resident(*spans["roof"])
+        cs.set_timing(1)
+        cs.reset_stats()
+        barrier()
+        t_start = time.perf_counter()
+        run(*spans["roof"], objs)
+        barrier()
+        roof_elapsed = max_over_ranks(time.perf_counter() - t_start)
+        kprof_timed = cs.kernel_profile()
+        st_roof = cs.stats()
+        cs.set_timed_kernel(None)
+        cs.set_timing(0)
 
     h2d_elapsed = None
     if args.h2d_steps > 0:  # PCIe-inclusive: each batch's H2D (the proxy share's, with routing) inside the loop
@@ -744,17 +769,26 @@ def main():
                      "timed_region_compactions": st["compactions"], "timed_region_gc_runs": st["gc_runs"]}
     # The Resolver's verdict counters over the timed batches (Resolver.actor.cpp:206-208:
     # TransactionsAccepted / TooOld / Conflicted), combined over resolvers at N > 1
-    mix = {"committed": 0, "conflict": 0, "too_old": 0}
-    for i in range(timed_lo, timed_hi):
-        v = combined[i].cpu().numpy() if (dist is not None and i in combined) else verdicts[i]
-        if v is None:
-            continue
-        v = np.asarray(v)
-        if dist is not None and i in combined:  # conflict bytes: 2 - min verdict, 0 = not routed anywhere
-            v = np.where(v == 0, 2, 2 - v.astype(np.int64))
-        mix["committed"] += int((v == 2).sum())
-        mix["conflict"] += int((v == 0).sum())
-        mix["too_old"] += int((v == 1).sum())
+    def verdict_mix(lo, hi):
+        mix = {"committed": 0, "conflict": 0, "too_old": 0}
+        for i in range(lo, hi):
+            v = combined[i].cpu().numpy() if (dist is not None and i in combined) else verdicts[i]
+            if v is None:
+                continue
+            v = np.asarray(v)
+            if dist is not None and i in combined:  # conflict bytes: 2 - min verdict, 0 = not routed anywhere
+                v = np.where(v == 0, 2, 2 - v.astype(np.int64))
+            mix["committed"] += int((v == 2).sum())
+            mix["conflict"] += int((v == 0).sum())
+            mix["too_old"] += int((v == 1).sum())
+        return mix
+
+    mix = verdict_mix(timed_lo, timed_hi)
+    # the "total" pass adds every batch after the previous batch's detect was issued: the Resolver's
+    # order (Resolver.actor.cpp:179-194), so its TooOld tests (SkipList.cpp:770) see the oldest
+    # version the previous detect left; the timed pass packs its batches ahead of the region, so
+    # its TooOld tests use the oldest version at pack time
+    mix_total = verdict_mix(*spans["total"]) if n_total > 0 else None
     gtxn = pass_txns("timed")
     granges = sum(gbatches[i][0].n_reads + gbatches[i][0].n_writes for i in range(timed_lo, timed_hi))
     ttxn = pass_txns("total")
@@ -772,7 +806,7 @@ def main():
     roof = None
     if dominant and dominant in kprof_timed:
         k = kprof_timed[dominant]
-        ent = roofline.entry(dominant, k["ms"], k["launches"], shape, st)
+        ent = roofline.entry(dominant, k["ms"], k["launches"], shape, st_roof)
         traffic, traffic_note = roofline.pmc_traffic(ROOT, args.workload, dominant, p.txns, p.history, build)
         rp = (rp_kernels or {}).get(dominant)
         rp_frac = None
@@ -902,6 +936,10 @@ def main():
         "phase_ms_per_batch": phase,
         "amortized_ms_per_batch": amortized,
         "verdict_mix": mix,
+        "verdict_mix_total": mix_total,
+        "verdict_mix_note": "verdict_mix: timed batches, packed (addTransaction, TooOld test) before the region; "
+        "verdict_mix_total: the total pass, each batch added after the previous detect (the Resolver's order)",
+        "roofline_pass_txns_per_s": pass_txns("roof") / roof_elapsed if roof_elapsed else None,
         "compactions": st["compactions"],
         # batch-order launches (k_resolve, k_combine, k_intra_report) left out of the timed batches'
         # X halves: the host had seen their stage A find no candidate edge

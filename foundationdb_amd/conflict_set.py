@@ -149,6 +149,7 @@ SIGNATURES = {
                                             ctypes.POINTER(ctypes.c_double)]),
     "fdbcs_set_timed_kernel": (ctypes.c_int, [_VP, ctypes.c_char_p]),
     "fdbcs_debug_hold": (ctypes.c_int, [_VP, _I32]),
+    "fdbcs_sync": (ctypes.c_int, [_VP]),
     "fdbcs_strerror": (ctypes.c_char_p, [ctypes.c_int]),
 }
 
@@ -278,6 +279,11 @@ class ConflictSet:
     def set_timed_kernel(self, name: Optional[str]) -> None:
         """The kernel timed on sampled batches at timing level 1 (a name kernel_profile() reported)."""
         _check(load_library().fdbcs_set_timed_kernel(self._h, (name or "").encode()), "setTimedKernel")
+
+    def sync(self) -> None:
+        """Block until every engine stream is idle (uploads and every submitted stage): the engine's
+        HIP runtime is not torch's, so torch.cuda.synchronize() does not wait for it."""
+        _check(load_library().fdbcs_sync(self._h), "sync")
 
     def debug_hold(self, on: bool) -> None:
         """Diagnostics: hold every stream (on) so batches submitted next queue up; release (off)."""

@@ -2510,6 +2510,12 @@ int fdbcs_batch_routed_info(fdbcs_batch* b, int32_t* T, int32_t* R, int32_t* W, 
     return FDBCS_OK;
 }
 
+int fdbcs_sync(fdbcs_conflict_set* cs) {
+    if (!cs) return FDBCS_E_INVALID;
+    HIPOK(hipSetDevice(cs->device));
+    return sync_all(cs);
+}
+
 int fdbcs_batch_upload(fdbcs_batch* b) {
     if (!b) return FDBCS_E_INVALID;
     if (!b->cs) return FDBCS_E_STATE;

@@ -196,6 +196,11 @@ int fdbcs_batch_add_packed(fdbcs_batch* b, const fdbcs_packed_batch* pb);
 /* Stage the batch in HBM now (async H2D on the engine stream).  Optional:
  * detect uploads implicitly.  Lets callers keep PCIe out of a timed region. */
 int fdbcs_batch_upload(fdbcs_batch* b);
+/* Block until every stream of the conflict set is idle: uploads issued by fdbcs_batch_upload,
+ * and every stage of every batch already submitted.  The engine's HIP runtime is not torch's
+ * (INTEGRATION.md), so a caller timing HBM-resident batches calls this before starting its
+ * clock.  No reference counterpart (the reference is synchronous, Resolver.actor.cpp:179-194). */
+int fdbcs_sync(fdbcs_conflict_set* cs);
 /* ConflictBatch::detectConflicts(now, newOldestVersion, nonConflicting, tooOld)
  * — SkipList.cpp:844-890.  verdicts[t] receives 0/1/2 per transaction
  * (Resolver.actor.cpp:196-204 encoding); counts are optional (NULL). */
