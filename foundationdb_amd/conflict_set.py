@@ -83,7 +83,6 @@ class Stats(ctypes.Structure):
         ("host_ms_prepare", ctypes.c_double),
         ("host_ms_record", ctypes.c_double),
         ("host_ms_submit", ctypes.c_double),
-        ("graph_launches", ctypes.c_int64),
         ("compact_launches", ctypes.c_int64),
         ("merge_bytes_all", ctypes.c_int64),
         ("compact_bytes_all", ctypes.c_int64),

@@ -139,10 +139,9 @@ inline int64_t mono_ns() {
 // validation and normalization into pinned staging split over chunks of transactions.  The
 // calling thread works too.  A ticket carries the job's generation, so a worker that wakes late
 // never takes a ticket of a later job with the earlier job's function.  Between jobs a worker
-// spins for ~spin_us before sleeping on the condition variable: a resolver adds a batch every
-// ~0.1 ms, and a wake-up through the condition variable costs ~10-20 us (scripts/add_sweep.py).
+// sleeps on the condition variable (spinning ~300 us for the next job measured no better:
+// DESIGN.md §5).
 struct AddPool {
-    int spin_us = 0;  // FDBCS_ADD_SPIN_US (0: sleep at once; scripts/gpu_r05_o.sh: 300 us of spinning measured no better)
     std::vector<std::thread> th;
     std::mutex m;
     std::condition_variable cv;
@@ -155,7 +154,6 @@ struct AddPool {
     bool stop = false;
 
     explicit AddPool(int workers) {
-        if (const char* v = getenv("FDBCS_ADD_SPIN_US")) spin_us = std::max(0, atoi(v));
         for (int i = 0; i < workers; i++) th.emplace_back([this] { worker(); });
     }
     ~AddPool() {
@@ -181,11 +179,6 @@ struct AddPool {
     void worker() {
         uint32_t seen = 0;
         for (;;) {
-            // spin a while for the next job, then sleep
-            const auto t0 = std::chrono::steady_clock::now();
-            while (gen.load(std::memory_order_acquire) == seen &&
-                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us))
-                __builtin_ia32_pause();
             uint32_t g;
             int nn;
             const std::function<void(int)>* fn;
@@ -238,7 +231,6 @@ struct fdbcs_conflict_set {
     // chain; over a 5M base (C2) the single launch measured faster (device-resident 34.0M vs
     // 32.1M txns/s: one launch and two cross-stream events fewer, no third stream competing)
     int split_check = 2;
-    int64_t delta_floor = 1250000;  // FDBCS_DELTA_FLOOR: delta bound floor (delta_limit_for); 0 = N/16
     hipStream_t ustream = nullptr;  // batch uploads (k_upload over PCIe), so batch i+1's upload overlaps
                                     // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
@@ -248,7 +240,6 @@ struct fdbcs_conflict_set {
     // against the delta before batch i's merge plus batch i's union segments (PrevSegs), so it does
     // not wait for that merge: Y(i) overlaps X(i + 1).
     hipStream_t ystream = nullptr;
-    bool split_stage_b = true;          // FDBCS_SPLIT_B=0: both halves on `stream`, checks after the merge
     hipEvent_t ev_res[kNumWork] = {};   // X of the batch using workspace k is done (Y waits for it)
     // the next batch's check is done with workspace k's segments: that batch's ev_res (the end of
     // its half X, recorded anyway, and not re-recorded before workspace k's next user records)
@@ -330,36 +321,13 @@ struct fdbcs_conflict_set {
     bool serial = false;    // FDBCS_SERIAL=1: both stages on one stream (no cross-batch overlap)
     bool no_prepass = false;  // FDBCS_RESOLVE_PREPASS=0: k_resolve without its pre-pass (tests)
     int64_t tail_reclaim = kTailReclaimDefault;  // FDBCS_TAIL_RECLAIM: tail bytes that force the GC repack
-    int check_version = 7;    // FDBCS_CHECK: read-check kernel (7: one lane per lookup; 6: kArity lanes per
-                              // lookup, the base and delta lookups in separate waves, 1: kArity lanes per
-                              // lookup, the four of a read in one wave)
-    int lag = 0;              // FDBCS_LAG=1: a batch's stage B is issued with the next batch's detect
-    int upload_kernel = 0;    // FDBCS_UPLOAD=kernel: batches go up by a copy kernel over PCIe, not the DMA engine
-    int long_lanes = 1;       // FDBCS_LONG_LANES=0: batches of keys over 24 bytes take the kArity-lane
-                              // lookups (6) under FDBCS_CHECK=7 (round 3's layout, for A/B)
-    int compact_lanes = 2;    // FDBCS_COMPACT_LANES: k_compact_search mode (0: kArity lanes per delta
-                              // boundary; 1: one lane; 2: one lane, the long-key form after long batches)
-    bool seg_long_coop = false;  // FDBCS_SEG_LONG_COOP=1: the segment search of long-key batches by kArity
-                                 // lanes per lookup (group_lower_bound<true>), not one lane
-    int copy_nt = -1;         // FDBCS_COPY_NT: the compaction copy by non-temporal loads/stores (1), not (0);
-                              // -1: above 16M base boundaries (C4: 1022 -> 919 us per 50M-boundary copy;
-                              // C2: 185 -> 180 us, but the bench line no better)
-    int base_tile = 0;        // FDBCS_BASE_TILE: base boundaries per copy tile of a compaction (1024/2048/4096;
-                              // 0: 1024 up to 16M boundaries, C2 185 vs 223 us per copy, else 4096)
     bool write_groups = true;  // FDBCS_WRITE_GROUPS=0: one candidate edge per (read, writer) pair (A/B)
-    bool group_rmax = true;   // FDBCS_GROUP_RMAX=0: the split check's range max by one lane (A/B)
-    bool long_probe = true;   // FDBCS_LONG_PROBE=0: generic probes in the read check / segment search
-                              // even for batches with keys over 16 bytes (A/B)
-    int timing_every = 4;     // FDBCS_TIMING_EVERY: timing level 1 times the hot kernels of 1 batch in N
     bool directory = true;  // FDBCS_DIRECTORY=0: base-tier lookups descend the whole sample tree (A/B)
-    // Directory code (MaxLevels::dir_p .. dir_w; set_dir_map): with FDBCS_DIR_RANK=1 (default)
-    // the loaded keys' common prefix (capped at 15) and the value range of each byte position
-    // after it, as many positions as fit the slot budget (dir_bits); FDBCS_DIR_RANK=0: the first
-    // two key bytes (the round-4 directory, A/B).  Keys
-    // written later outside the loaded values take neighbouring codes, so the mapping stays
-    // monotone.  Round 4's prefix-only variant (16 bits after the prefix: C4's decimal digits gave
-    // 100 slots of ~7.8k samples) is the special case the rank tables replace.
-    bool dir_rank = true;
+    // Directory code (MaxLevels::dir_p .. dir_w; set_dir_map): the loaded keys' common prefix
+    // (capped at 15) and the value range of each byte position after it, as many positions as fit
+    // the slot budget (dir_bits).  Keys written later outside the loaded values take neighbouring
+    // codes, so the mapping stays monotone.  (Round 4's directory on the first two key bytes, and
+    // its prefix-only variant, are the special cases this code replaced: DESIGN.md §5.)
     uint32_t dir_p = 0;
     uint64_t dir_phi = 0, dir_plo = 0;
     uint32_t dir_e = 0, dir_top = 0;
@@ -385,27 +353,6 @@ struct fdbcs_conflict_set {
     bool skip_edges = true;            // FDBCS_SKIP_EDGES=0: always issue the kGroupEdges launches
     fdbcs_stats stats{};
     std::vector<BatchSlot*> pool;  // staging slots of destroyed batches, reused by new ones
-    // FDBCS_GRAPH=2: stage graphs.  The launches of each stage (A on its stream, B on the batch-order
-    // stream) go out as one cached hipGraph per stage shape on the stage's own stream, with the
-    // cross-stream event waits and records around it issued directly, so the stages still overlap
-    // across streams as in direct mode while the submitting thread makes ~3 graph launches instead
-    // of ~20 kernel launches per batch.
-    // FDBCS_GRAPH=3: whole-stage graphs.  Each stage list of a batch (A, the check / resolution
-    // half X, the merge / epilogue half Y) goes out as ONE cached graph on its stream, its
-    // cross-stream waits and records included as event wait / record nodes, so the stream
-    // layout and every dependency stay those of direct mode at three graph launches per batch.
-    int stage_graphs = 0;  // 1: runs between sync points (FDBCS_GRAPH=2); 2: whole lists (=3)
-    int graph_ring = 16;   // FDBCS_GRAPH_RING: executable copies per stage shape
-    struct StageGraph {
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t exec = nullptr;
-        std::vector<hipGraphNode_t> nodes;
-    };
-    std::vector<std::pair<uint64_t, StageGraph>> stage_cache;
-    // Each stage shape has kGraphRing executable copies used in turn, so a copy is updated only
-    // after the batches in flight have moved past its last launch (an exec updated while its
-    // previous launch is still queued is what the runtime has to wait out).
-    std::vector<std::pair<uint64_t, uint32_t>> stage_turn;
     // Two submitting threads (the default since round 4: C2 +3-10 % over five same-box A/Bs, C3 and
     // C4 unchanged; FDBCS_SUBMIT_THREAD=0 keeps one).  A helper thread issues stage A of batch i
     // (and its base-tier check) while the calling thread issues stage B's X half of batch i-1,
@@ -439,7 +386,6 @@ struct fdbcs_conflict_set {
     // issued its X half (FDBCS_HELPER_Y=0: both halves from the calling thread).  The calling
     // thread issues record + X, the helper stage A + Y + base check: their runtime calls split
     // about evenly instead of ~2:1.
-    bool helper_y = true;
     LaunchList work_y;
     hipStream_t work_ys = nullptr;
     uint32_t work_need_x = 0;            // Y goes out once x_issued >= this
@@ -448,7 +394,6 @@ struct fdbcs_conflict_set {
     LaunchList rec_a, rec_b, rec_c, rec_y, pending_b, pending_y;
     hipStream_t pending_ys = nullptr;  // the stream of pending_y
     fdbcs_batch* pending_batch = nullptr;
-    int64_t graph_launches = 0;
     std::unordered_set<fdbcs_batch*> live;  // batches not yet destroyed (detached if the set goes first)
 };
 
@@ -717,14 +662,16 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
 
 // Automatic delta bound: about 1/16 of the base, so a batch's merge touches a small tier and a
 // compaction (a full rewrite of the base) is amortised over many batches.
-// The delta tier's bound: N/16, raised towards N/4 up to delta_floor boundaries.  A compaction
+// The delta tier's bound: N/16, raised towards N/4 up to kDeltaFloor boundaries.  A compaction
 // rewrites the whole base on Y and the next check waits for it, so on a 5M-boundary base fewer,
 // larger deltas pay although every merge copies more: C2 54.6 -> 56.7M, C3 45.9 -> 50.4M, C2 at
 // 32768-txn batches 91.1 -> 92.9M over 150-400-batch windows with a 1.25M bound
 // (scripts/gpu_r05_dl*.sh); a 50M base (C4) keeps N/16 = 3.1M.
+constexpr int64_t kDeltaFloor = 1250000;
+constexpr int kTimingEvery = 4;  // timing level 1 times the hot kernels of 1 batch in kTimingEvery
 int64_t delta_limit_for(const fdbcs_conflict_set* cs, int64_t n_base) {
     if (cs->delta_limit > 0) return cs->delta_limit;
-    return std::max<int64_t>({(int64_t)1 << 16, n_base / 16, std::min<int64_t>(n_base / 4, cs->delta_floor)});
+    return std::max<int64_t>({(int64_t)1 << 16, n_base / 16, std::min<int64_t>(n_base / 4, kDeltaFloor)});
 }
 
 
@@ -769,7 +716,7 @@ static int set_dir_map(fdbcs_conflict_set* cs, const ulonglong2* k, int64_t n) {
     auto byte_at = [](const ulonglong2& x, int i) -> uint32_t {
         return i < 8 ? (uint32_t)(x.x >> (56 - 8 * i)) & 255u : (uint32_t)(x.y >> (56 - 8 * (i - 8))) & 255u;
     };
-    const bool rank = cs->dir_rank && n >= 2;
+    const bool rank = n >= 2;
     uint32_t p = 0;
     if (rank) {
         const uint64_t xh = k[0].x ^ k[n - 1].x, xl = k[0].y ^ k[n - 1].y;
@@ -801,7 +748,7 @@ static int set_dir_map(fdbcs_conflict_set* cs, const ulonglong2* k, int64_t n) {
     uint64_t budget = 1ull << 16;
     if (cs->dir_bits)
         budget = 1ull << cs->dir_bits;
-    else if (cs->dir_rank)
+    else
         while (budget < (1ull << kDirMaxBits) && 8 * budget < (uint64_t)samples) budget <<= 1;
     uint32_t radix[kDirPos], shift[kDirPos];
     uint64_t prod = 1;
@@ -1020,16 +967,6 @@ void release_slot(BatchSlot* sl) {
     delete sl;
 }
 
-// Pinned staging of batches (pin_in): host-coherent mapped memory by default; FDBCS_PIN_IN=nc maps
-// it non-coherent (A/B of the addTransaction write rate into it).
-static bool pin_in_noncoherent() {
-    static const bool nc = [] {
-        const char* v = getenv("FDBCS_PIN_IN");
-        return v && v[0] == 'n';
-    }();
-    return nc;
-}
-
 // Layout of a batch in pin_in / dev: [keys | rowner | wowner | snap | roff | woff | flags | tail].
 // add_packed normalizes keys, owners and tails in place; the tail region is last so a capacity
 // sized for an upper bound of the tail bytes costs no upload.
@@ -1147,7 +1084,7 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     const size_t T = b->T(), R = b->R(), W = b->W();
     const UploadLayout L = upload_layout(T, R, W, b->tail_size());
     int rc;
-    if (!b->direct && (rc = sl->pin_in.ensure(L.total, true, pin_in_noncoherent()))) return rc;
+    if (!b->direct && (rc = sl->pin_in.ensure(L.total, true))) return rc;
     if ((rc = ensure_slot(sl, L.total, T, R))) return rc;
     char* h = (char*)sl->pin_in.p;
     if (!b->direct) {  // add_transaction path: normalized keys are in the pageable vectors
@@ -1165,12 +1102,7 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     // of the batch that used it last.
     if (!sl->ev_up) HIPOK(hipEventCreateWithFlags(&sl->ev_up, hipEventDisableTiming));
     (void)cs;
-    if (cs->upload_kernel) {
-        launch_upload(us, sl->dev.p, sl->pin_in.dp, (int64_t)L.total);
-        HIPOK(take_launch_error());
-    } else {
-        HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us));
-    }
+    HIPOK(hipMemcpyAsync(sl->dev.p, h, L.total, hipMemcpyHostToDevice, us));
     HIPOK(hipEventRecord(sl->ev_up, us));
     char* d = (char*)sl->dev.p;
     b->bd.T = (int32_t)T;
@@ -1187,122 +1119,6 @@ int do_upload(fdbcs_batch* b, hipStream_t us) {
     b->tail_bytes = b->tail_size();
     b->bd.tail_n = (int64_t)b->tail_bytes;
     b->state = 1;
-    return FDBCS_OK;
-}
-
-// Stage graphs (FDBCS_GRAPH=2): a stage list is cut at its cross-stream waits and records,
-// which are issued directly on `st`; every run of two or more kernels (with the timing events
-// between them) goes out as one cached graph, keyed by its kernels and updated with this batch's
-// node parameters (tools/submitbench.hip: a 5-kernel graph with updates costs ~9 us of host time
-// against ~24 us for its direct launches; a single kernel is launched directly).
-int launch_graph_run(fdbcs_conflict_set* cs, LaunchList& L, size_t i0, size_t i1, hipStream_t st) {
-    uint64_t key = 1469598103934665603ull;
-    for (size_t i = i0; i < i1; i++) {
-        const LaunchList::Rec& r = L.recs[i];
-        key = (key ^ (r.kind == LaunchList::kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u + r.kind)) *
-              1099511628211ull;
-    }
-    const uint64_t shape = key;
-    {  // this launch's copy of the shape
-        uint32_t* turn = nullptr;
-        for (auto& kv : cs->stage_turn)
-            if (kv.first == key) turn = &kv.second;
-        if (!turn) {
-            cs->stage_turn.push_back({key, 0u});
-            turn = &cs->stage_turn.back().second;
-        }
-        key = key * 1099511628211ull + (*turn)++ % (uint32_t)cs->graph_ring;
-    }
-    fdbcs_conflict_set::StageGraph* sg = nullptr;
-    for (auto& kv : cs->stage_cache)
-        if (kv.first == key) sg = &kv.second;
-    const bool fresh = sg == nullptr;  // a new shape: every copy is instantiated now (first batch)
-    auto params = [&](const LaunchList::Rec& r) {
-        hipKernelNodeParams p{};
-        p.func = const_cast<void*>(r.func);
-        p.gridDim = r.grid;
-        p.blockDim = r.block;
-        p.sharedMemBytes = r.shmem;
-        p.kernelParams = L.argp.data() + r.arg0;
-        return p;
-    };
-    for (int c = 0; fresh && c < cs->graph_ring; c++) {
-        const uint64_t kc = shape * 1099511628211ull + (uint32_t)c;
-        bool have = false;
-        for (auto& kv : cs->stage_cache) have |= kv.first == kc;
-        if (have) continue;
-        fdbcs_conflict_set::StageGraph g;
-        HIPOK(hipGraphCreate(&g.graph, 0));
-        hipGraphNode_t prev = nullptr;
-        for (size_t i = i0; i < i1; i++) {
-            const LaunchList::Rec& r = L.recs[i];
-            hipGraphNode_t nd = nullptr;
-            if (r.kind == LaunchList::kKernel) {
-                const hipKernelNodeParams p = params(r);
-                HIPOK(hipGraphAddKernelNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, &p));
-            } else if (r.kind == LaunchList::kSyncWait) {
-                HIPOK(hipGraphAddEventWaitNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
-            } else {
-                HIPOK(hipGraphAddEventRecordNode(&nd, g.graph, prev ? &prev : nullptr, prev ? 1 : 0, r.event));
-            }
-            g.nodes.push_back(nd);
-            prev = nd;
-        }
-        HIPOK(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0));
-        cs->stage_cache.push_back({kc, g});
-    }
-    if (fresh) {
-        for (auto& kv : cs->stage_cache)
-            if (kv.first == key) sg = &kv.second;
-    } else {
-        size_t k = 0;
-        for (size_t i = i0; i < i1; i++) {
-            const LaunchList::Rec& r = L.recs[i];
-            if (r.kind == LaunchList::kKernel) {
-                const hipKernelNodeParams p = params(r);
-                HIPOK(hipGraphExecKernelNodeSetParams(sg->exec, sg->nodes[k++], &p));
-            } else if (r.kind == LaunchList::kSyncWait) {
-                HIPOK(hipGraphExecEventWaitNodeSetEvent(sg->exec, sg->nodes[k++], r.event));
-            } else {
-                HIPOK(hipGraphExecEventRecordNodeSetEvent(sg->exec, sg->nodes[k++], r.event));
-            }
-        }
-    }
-    HIPOK(hipGraphLaunch(sg->exec, st));
-    cs->graph_launches++;
-    return FDBCS_OK;
-}
-
-int launch_stage(fdbcs_conflict_set* cs, LaunchList& L, hipStream_t st) {
-    auto is_sync = [](const LaunchList::Rec& r) {
-        return r.kind == LaunchList::kSyncWait || r.kind == LaunchList::kSyncRecord;
-    };
-    L.finalize();
-    const size_t n = L.recs.size();
-    if (cs->stage_graphs == 2) {  // the whole list, its waits and records included, as one graph
-        size_t kernels = 0;
-        for (const LaunchList::Rec& r : L.recs) kernels += r.kind == LaunchList::kKernel ? 1 : 0;
-        if (kernels >= 1 && n >= 2) return launch_graph_run(cs, L, 0, n, st);
-        for (const LaunchList::Rec& r : L.recs) HIPOK(L.issue(r, st));
-        return FDBCS_OK;
-    }
-    size_t i = 0;
-    while (i < n) {
-        if (is_sync(L.recs[i])) {
-            HIPOK(L.issue(L.recs[i], st));
-            i++;
-            continue;
-        }
-        size_t j = i;
-        int kernels = 0;
-        while (j < n && !is_sync(L.recs[j])) kernels += L.recs[j++].kind == LaunchList::kKernel ? 1 : 0;
-        if (kernels >= 2) {
-            if (int rc = launch_graph_run(cs, L, i, j, st)) return rc;
-        } else {
-            for (size_t k = i; k < j; k++) HIPOK(L.issue(L.recs[k], st));
-        }
-        i = j;
-    }
     return FDBCS_OK;
 }
 
@@ -1454,73 +1270,19 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
         cs->htr[0].reserve(1 << 16);
         cs->htr[1].reserve(1 << 16);
     }
-    if (const char* v = getenv("FDBCS_GRAPH")) cs->stage_graphs = v[0] == '2' ? 1 : (v[0] == '3' ? 2 : 0);
-    if (const char* v = getenv("FDBCS_GRAPH_RING")) cs->graph_ring = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
-    if (const char* v = getenv("FDBCS_LONG_PROBE")) cs->long_probe = v[0] != '0';
-    if (const char* v = getenv("FDBCS_GROUP_RMAX")) cs->group_rmax = v[0] != '0';
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
-    if (const char* v = getenv("FDBCS_HELPER_Y")) cs->helper_y = v[0] != '0';
-    if (const char* v = getenv("FDBCS_DELTA_FLOOR")) cs->delta_floor = std::max<long long>(0, atoll(v));
-    if (const char* v = getenv("FDBCS_TIMING_EVERY")) cs->timing_every = std::max(1, atoi(v));
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
-    if (const char* v = getenv("FDBCS_DIR_RANK")) cs->dir_rank = v[0] != '0';
     if (const char* v = getenv("FDBCS_DIR_BITS")) cs->dir_bits = std::max(0, std::min(kDirMaxBits, atoi(v)));
-    if (const char* v = getenv("FDBCS_CHECK")) cs->check_version = atoi(v) == 1 ? 1 : (atoi(v) == 6 ? 6 : 7);
-    if (const char* v = getenv("FDBCS_LONG_LANES")) cs->long_lanes = atoi(v) != 0;
-    if (const char* v = getenv("FDBCS_BASE_TILE")) cs->base_tile = atoi(v);
-    if (const char* v = getenv("FDBCS_COPY_NT")) cs->copy_nt = v[0] != '0';
-    if (const char* v = getenv("FDBCS_SEG_LONG_COOP")) cs->seg_long_coop = v[0] != '0';
-    if (const char* v = getenv("FDBCS_COMPACT_LANES")) cs->compact_lanes = std::max(0, std::min(2, atoi(v)));
-    if (const char* v = getenv("FDBCS_UPLOAD")) cs->upload_kernel = strcmp(v, "kernel") == 0;
-    if (const char* v = getenv("FDBCS_LAG")) cs->lag = atoi(v) != 0;
-    if (const char* v = getenv("FDBCS_SPLIT_B")) cs->split_stage_b = v[0] != '0';
     if (const char* v = getenv("FDBCS_TAIL_RECLAIM")) cs->tail_reclaim = std::max<long long>(1, atoll(v));
     if (const char* v = getenv("FDBCS_ROUTE_TIMEOUT_MS")) cs->route_timeout_ms = std::max<long long>(1, atoll(v));
     static std::once_flag attr_once;
     std::call_once(attr_once, init_kernel_attributes);
-    // FDBCS_PRIO names the streams created at the device's greatest priority (A/B of which chain
-    // the hardware should favour when the stages compete for CUs): letters a (stage A), x (check /
-    // resolution), y (merge / epilogue), c (base-tier check)
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const char* prio = getenv("FDBCS_PRIO");
-    // FDBCS_CU_MASK (A/B of CU partitions between the chains): "a:0-127,x:128-255" gives stream a
-    // (stage A), x (check / resolution), y (merge / epilogue) or c (base-tier check) the CUs whose
-    // index lies in the range; "x:%0-3" the CUs whose index mod 8 lies in it (the hardware's
-    // enumeration decides which XCD that is).  Unlisted streams use every CU.
-    const char* cumask = getenv("FDBCS_CU_MASK");
-    int n_cu = 0;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, cs->device);
-    auto cu_mask_of = [&](char tag, std::vector<uint32_t>& m) -> bool {
-        if (!cumask || n_cu <= 0) return false;
-        for (const char* p = cumask; *p;) {
-            const char t = *p;
-            const char* e = strchr(p, ',');
-            const std::string item(p, e ? (size_t)(e - p) : strlen(p));
-            p = e ? e + 1 : p + item.size();
-            if (item.size() < 3 || t != tag || item[1] != ':') continue;
-            const bool mod = item[2] == '%';
-            int lo = 0, hi = 0;
-            if (sscanf(item.c_str() + (mod ? 3 : 2), "%d-%d", &lo, &hi) != 2) return false;
-            m.assign((size_t)(n_cu + 31) / 32, 0u);
-            for (int c = 0; c < n_cu; c++) {
-                const int k = mod ? c % 8 : c;
-                if (k >= lo && k <= hi) m[(size_t)c / 32] |= 1u << (c % 32);
-            }
-            return true;
-        }
-        return false;
-    };
-    auto mk = [&](hipStream_t* st, char tag) {
-        std::vector<uint32_t> m;
-        if (cu_mask_of(tag, m)) return hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data()) == hipSuccess;
-        if (prio && strchr(prio, tag)) return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio_hi) == hipSuccess;
-        return hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess;
-    };
-    bool ok = mk(&cs->stream, 'x') && mk(&cs->ystream, 'y') && mk(&cs->astream, 'a') &&
-              hipStreamCreateWithFlags(&cs->ustream, hipStreamNonBlocking) == hipSuccess &&
-              mk(&cs->cstream, 'c') &&
+    // Five streams at the default priority, every CU: stream priorities and CU partitions between
+    // the chains measured slower (extra hardware queues; the chains slow each other
+    // through the memory system, not by competing for CU slots).
+    auto mk = [](hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking) == hipSuccess; };
+    bool ok = mk(&cs->stream) && mk(&cs->ystream) && mk(&cs->astream) && mk(&cs->ustream) && mk(&cs->cstream) &&
               hipEventCreateWithFlags(&cs->ev_cmp, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&cs->ev_quant, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < kNumWork && ok; k++)
@@ -1613,11 +1375,6 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
     cs->hedge.release();
     for (BatchSlot* sl : cs->pool) release_slot(sl);
     cs->pool.clear();
-    for (auto& kv : cs->stage_cache) {
-        if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
-        if (kv.second.graph) (void)hipGraphDestroy(kv.second.graph);
-    }
-    cs->stage_cache.clear();
     // batches that outlive their set (e.g. garbage-collection order in a binding) keep their own
     // slot and refuse every further call
     for (fdbcs_batch* b : cs->live) b->cs = nullptr;
@@ -2010,7 +1767,7 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
         return rc;
     };
     const auto tp1 = clk::now();
-    if (int rc = b->slot->pin_in.ensure(L.total, true, pin_in_noncoherent())) return fail(rc);
+    if (int rc = b->slot->pin_in.ensure(L.total, true)) return fail(rc);
     if (int rc = ensure_slot(b->slot, L.total, T, Ra)) return fail(rc);
     const auto tp2 = clk::now();
     char* h = (char*)b->slot->pin_in.p;
@@ -2603,7 +2360,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // phase events: level 2 records every phase, level 1 only the hot kernels (roofline)
     // level-1 (roofline) events on one batch in timing_every: each event record is a runtime call
     // on the submitting thread, and the per-launch averages need only a sample of the batches
-    const bool sampled = timing >= 2 || cs->timing_every <= 1 || b->seq % (uint32_t)cs->timing_every == 0;
+    const bool sampled = timing >= 2 || b->seq % (uint32_t)kTimingEvery == 0;
     // level 3 (per-kernel profile) records only the events around every kernel
     // level 1 with a timed kernel (fdbcs_set_timed_kernel) records only that kernel's events
     auto rec = [&](int ph, int level) -> hipEvent_t {
@@ -2641,8 +2398,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // two submitting threads: this batch's stage A and check go out from the helper, stage B on the
     // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it
     // records cannot be queried here: waits on its events are kept unconditionally.
-    const bool threaded = cs->submit_thread && !(cs->stage_graphs && timing < 2) && timing < 2 && !cs->trace && sa != s;
-    const bool lag = cs->lag && !threaded && !(cs->stage_graphs && timing < 2) && timing < 2 && !cs->trace && sa != s;
+    const bool threaded = cs->submit_thread && timing < 2 && !cs->trace && sa != s;
     cs->stats.host_ms_prepare += host_ms_since(t_begin);
     const auto t_rec = std::chrono::steady_clock::now();
     // ---- upload (issued now) and record stage A: D.Sort and the candidate edges of D.CheckIntraBatch
@@ -2675,10 +2431,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (b->routed) launch_route_too_old(sa, bd, cs->oldest);
     // long-key probes pay off once tails run past a word (a 17-byte end key k\0 of a 16-byte key
     // ties on the prefix with k only, and the length decides)
-    const bool long_keys = cs->long_probe && b->max_len > 24;
-    // one lane per lookup unless tails run past a word (then the cooperative long-key probes)
-    const bool lanes = cs->check_version == 7 && (b->max_len <= 24 || cs->long_lanes);
-    const int check_version = cs->check_version == 7 && !lanes ? 6 : (lanes && long_keys ? 8 : cs->check_version);
+    const bool long_keys = b->max_len > 24;
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     // Stage B in two halves (fdbcs_conflict_set::ystream): X = check, resolution, D.Combine on
@@ -2686,7 +2439,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // compacted, this batch's check reads the delta before the previous batch's merge (buffer
     // dsrc ^ 1, complete once the batch before it finished Y) plus the previous batch's union
     // segments at its `now` (PrevSegs): the same history, so the check need not wait for that merge.
-    const bool pipe = cs->split_stage_b && !(timing == 2 || cs->serial || cs->check_version == 1);
+    const bool pipe = !(timing == 2 || cs->serial);
     hipStream_t ys = pipe ? cs->ystream : s;
     const bool use_prev = pipe && cs->prev_segs;
     const int dchk = use_prev ? dsrc ^ 1 : dsrc;
@@ -2752,10 +2505,10 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         hipStream_t sc_ = cs->cstream;
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sc_);
         if (ws_busy) fdb_event(LaunchList::kSyncWait, cs->ev_b[wp], sc_);
-        if (cs->cmp_recorded && (threaded || lag || hipEventQuery(cs->ev_cmp) != hipSuccess))
+        if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
             fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
-        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, !cs->group_rmax, PrevSegs{}, lanes);
+        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, PrevSegs{});
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
@@ -2770,14 +2523,13 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (wy >= 0 && cs->y_async[wy] && (threaded || !stage_b_done(cs, wy)))
             fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
     }
-    const bool graphs = cs->stage_graphs && timing != 2;
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, !cs->group_rmax, ps, lanes);
+        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, ps);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-        launch_check(s, bd, w, base, cdelta, htail, check_version, ps);
+        launch_check(s, bd, w, base, cdelta, htail, long_keys, ps);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
@@ -2817,8 +2569,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     // D.MergeWrite into the delta tier
     char* hd = (char*)sl->pin_out.dp;
     launch_merge(ys, bd, w, delta.h, delta.m, delta_of(cs, dnew), dlevels_of(cs, dnew), &sc->ndb[dsrc], htail, sc, now,
-                 cs->dlvl3_n, cs->dlvl2_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys,
-                 cs->seg_long_coop);
+                 cs->dlvl3_n, cs->dlvl2_n, cs->nd_ub + 1, rec(kPhCopyBegin, 1), rec(kPhCopyEnd, 1), long_keys);
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;
@@ -2826,9 +2577,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if (compact) {
         launch_compact(ys, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
                        cs->header_version, cs->lvl3_n, cs->lvl2_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
-                       rec(kPhCompEnd, 1), cs->compact_lanes == 2 && !long_keys ? 1 : cs->compact_lanes,
-                       cs->base_tile ? cs->base_tile : (cs->n_ub <= (16 << 20) ? 1024 : 4096),
-                       cs->copy_nt >= 0 ? cs->copy_nt != 0 : cs->n_ub > (16 << 20));
+                       rec(kPhCompEnd, 1), long_keys ? 2 : 1, cs->n_ub <= (16 << 20) ? 1024 : 4096,
+                       cs->n_ub > (16 << 20));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
         // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th
@@ -2887,7 +2637,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->work_sa = sa;
         cs->work_a_seq = b->seq;
         const bool prev = cs->pending_batch != nullptr;
-        const bool hy = prev && cs->helper_y;
+        const bool hy = prev;
         if (hy) {  // the previous batch's Y to the helper, after the X this thread issues below
             cs->work_y_seq = cs->pending_batch->seq;
             std::swap(cs->work_y, cs->pending_y);
@@ -2917,30 +2667,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->pending_ys = ys;
         cs->b_recorded++;
         cs->pending_batch = b;
-    } else if (lag) {
-        // Lagged submission (FDBCS_LAG, one thread): this batch's upload (issued) and stage A now,
-        // then the previous batch's stage B, and this batch's stage B at the next call (or a flush).
-        // By then its waits on its stage A and upload mostly find them complete, which the runtime
-        // passes at ~0.1 us against ~6 us for a wait on a pending event (tools/launchbench.hip).
-        // Stage B of the previous batch records no event this batch's A waits for, except the
-        // base rewrite its compaction / GC signals, which the base-tier check waits for.
-        HIPOK(la.replay(sa));
-        if (split && cs->pending_batch && (cs->pending_batch->compacted || cs->pending_batch->gc_ran)) {
-            if ((rc = flush_pending(cs))) return rc;
-        }
-        if (split) HIPOK(lc.replay(cs->cstream));
-        if ((rc = flush_pending(cs))) return rc;
-        std::swap(cs->pending_b, lb);
-        std::swap(cs->pending_y, ly);
-        cs->pending_ys = ys;
-        cs->pending_batch = b;
     } else if (flush_pending(cs)) {
         return FDBCS_E_DEVICE;
-    } else if (graphs) {
-        if ((rc = launch_stage(cs, la, sa))) return rc;
-        if (split && (rc = launch_stage(cs, lc, cs->cstream))) return rc;
-        if ((rc = launch_stage(cs, lb, s))) return rc;
-        if ((rc = launch_stage(cs, ly, ys))) return rc;
     } else {
         HIPOK(la.replay(sa));
         if (split) HIPOK(lc.replay(cs->cstream));
@@ -2949,7 +2677,6 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     }
     HIPOK(take_launch_error());
     cs->stats.host_ms_submit += host_ms_since(t_sub);
-    cs->stats.graph_launches = cs->graph_launches;
     cs->cur = final_base;
     cs->dcur = dnew;
     // the next batch's check: this batch's segments stand in for its merge unless it compacted
@@ -3277,17 +3004,14 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     hipEvent_t e0, e1;
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));
-    const bool dl = cs->check_version == 7 && (b->max_len <= 24 || cs->long_lanes);
-    const bool dlong = cs->long_probe && b->max_len > 24;
-    const int cv = cs->check_version == 7 && !dl ? 6 : (dl && dlong ? 8 : cs->check_version);
+    const bool dlong = b->max_len > 24;
     // 0: the whole check; 3 / 4: the split check's base / delta tier launch alone
     auto one = [&]() {
         uint8_t* ht = (uint8_t*)cs->htail[cs->tcur].p;
         if (which == 0)
-            launch_check(cs->stream, b->bd, w, base, delta, ht, cv);
+            launch_check(cs->stream, b->bd, w, base, delta, ht, dlong);
         else
-            launch_check_tier(cs->stream, b->bd, w, which == 3 ? base : delta, which == 3, ht,
-                              dlong, !cs->group_rmax, PrevSegs{}, dl);
+            launch_check_tier(cs->stream, b->bd, w, which == 3 ? base : delta, which == 3, ht, dlong, PrevSegs{});
     };
     one();
     HIPOK(hipEventRecord(e0, cs->stream));

@@ -164,7 +164,10 @@ struct BatchDev {
 // D.Sort geometry (kernels.hip): a bucket holds kSortTarget endpoints on average and is sorted in
 // registers by one wave up to kSlab endpoints; splitters are projections of the quantiles of the
 // last sorted batch (kQuant of them), or of this batch's ranked samples at a cold start.
-constexpr int kSortTarget = 64;
+#ifndef FDBCS_SORT_TARGET
+#define FDBCS_SORT_TARGET 64
+#endif
+constexpr int kSortTarget = FDBCS_SORT_TARGET;
 constexpr int kSlab = 256;
 constexpr int kSortMaxBuckets = 4096;
 constexpr int kQuant = 4096;
@@ -399,18 +402,15 @@ void launch_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quan
                  int bucket_target, bool long_keys, bool validate, hipEvent_t sort_begin, hipEvent_t sort_end);
 // Buckets of a batch of E endpoints (target 0 = kSortTarget), within the workspace slab.
 int sort_bucket_count(int64_t E, int target, int slab_buckets);
-// D.CheckRead against the history the previous batch left.
-// check_version: 7 = one lane per lookup (default for keys up to 24 bytes), 6 = kArity lanes per
-// lookup with the base and delta lookups in separate waves, 1 = kArity lanes per lookup in one wave.
+// D.CheckRead against the history the previous batch left: one lane per lookup, four lanes per
+// read (begin and end in both tiers).  long_keys: the batch has keys over 24 bytes (the long-key
+// lookup, lane_lower_bound_long).
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, int check_version = 6, const PrevSegs& ps = PrevSegs{});
+                  const uint8_t* htail, bool long_keys = false, const PrevSegs& ps = PrevSegs{});
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
-// delta tier in stage B); both OR into the workspace's pre-zeroed conflict flags.
-// long_keys: the batch has keys over 16 bytes (long-key probe instantiation).
-// lanes: one lane per lookup (FDBCS_CHECK=7 on keys up to 24 bytes).
+// delta tier in stage B), two lanes per read; both OR into the workspace's pre-zeroed conflict flags.
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys = false, bool lead_rmax = false,
-                       const PrevSegs& ps = PrevSegs{}, bool lanes = false);
+                       const uint8_t* htail, bool long_keys = false, const PrevSegs& ps = PrevSegs{});
 // Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
 // k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,
@@ -427,7 +427,7 @@ void launch_resolve(hipStream_t s, const BatchDev& b, const Work& w, bool report
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
                   int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end, bool long_keys = false, bool long_coop = false);
+                  hipEvent_t copy_end, bool long_keys = false);
 // Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
@@ -441,8 +441,6 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, c
 void launch_hold(hipStream_t s, const uint32_t* release);
 // Kernel attributes set once per process (the resolver's dynamic LDS above 64 KiB).
 void init_kernel_attributes();
-// H2D copy of a packed batch by a kernel reading the host-mapped staging buffer (FDBCS_UPLOAD=kernel).
-void launch_upload(hipStream_t s, void* dst, const void* src_mapped, int64_t n);
 // Byte copy (device -> host-mapped result buffer), as a kernel.
 void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n);
 // Multi-resolver conflict bytes out[g] = 2 - verdict of batch transaction inv[g] (0 if inv[g] < 0).

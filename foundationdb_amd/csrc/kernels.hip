@@ -63,77 +63,8 @@ __device__ __forceinline__ int hist_cmp(const Hist& h, int64_t i, const uint8_t*
     return (lt.x > q.len) - (lt.x < q.len);
 }
 
-// First index in [lo, hi) whose boundary key is >= q (std::lower_bound).
-__device__ __forceinline__ int64_t hist_lower_bound(const Hist& h, int64_t lo, int64_t hi, const uint8_t* htail,
-                                                    const DKey& q, const uint8_t* qtail) {
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (hist_cmp(h, mid, htail, q, qtail) < 0)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
-// Q independent std::lower_bound searches advanced in lockstep: each round issues every active
-// probe load before comparing, so a thread keeps Q requests in flight and the critical path is one
-// search deep.  eq[i]: key[lo[i]] == q[i] (the last probe that lowered hi hit the key itself).
-template <int Q>
-__device__ __forceinline__ void multi_lower_bound(const Hist (&h)[Q], int64_t (&lo)[Q], int64_t (&hi)[Q],
-                                                  bool (&eq)[Q], const uint8_t* htail, const DKey (&q)[Q],
-                                                  const uint8_t* qtail) {
-#pragma unroll
-    for (int i = 0; i < Q; i++) eq[i] = false;
-    for (;;) {
-        bool any = false;
-        int64_t mid[Q];
-        ulonglong2 k[Q];
-#pragma unroll
-        for (int i = 0; i < Q; i++) {
-            mid[i] = (lo[i] + hi[i]) >> 1;
-            if (lo[i] < hi[i]) {
-                k[i] = h[i].key[mid[i]];
-                any = true;
-            }
-        }
-        if (!any) break;
-#pragma unroll
-        for (int i = 0; i < Q; i++) {
-            if (lo[i] < hi[i]) {
-                int c;
-                if (k[i].x != q[i].hi)
-                    c = k[i].x < q[i].hi ? -1 : 1;
-                else if (k[i].y != q[i].lo)
-                    c = k[i].y < q[i].lo ? -1 : 1;
-                else
-                    c = hist_cmp(h[i], mid[i], htail, q[i], qtail);  // equal prefixes: length / tail
-                if (c < 0) {
-                    lo[i] = mid[i] + 1;
-                } else {
-                    hi[i] = mid[i];
-                    eq[i] = c == 0;
-                }
-            }
-        }
-    }
-}
-
 __device__ __forceinline__ bool prefix_less(const ulonglong2& k, const DKey& q) {
     return k.x < q.hi || (k.x == q.hi && k.y < q.lo);
-}
-
-// Number of leading entries of a[base, base+cnt) (cnt <= 16, sorted) whose prefix is < q's: the
-// 16 loads are issued together.
-__device__ __forceinline__ int count16(const ulonglong2* a, int64_t base, int cnt, const DKey& q) {
-    ulonglong2 k[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-        if (i < cnt) k[i] = a[base + i];
-    int c = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) c += (i < cnt && prefix_less(k[i], q)) ? 1 : 0;
-    return c;
 }
 
 // Full key comparison of boundary i with q, given its prefix already loaded.
@@ -164,98 +95,6 @@ __device__ __forceinline__ int probe_cmp_lean(const Hist& h, int64_t i, const ul
     }
 #endif
     return (lt.x > q.len) - (lt.x < q.len);
-}
-
-// std::lower_bound of q over the n boundaries of a tier, through its search tree: one 16-wide
-// probe per tree level down to a 64-boundary block, then two probes inside the block (about 6
-// dependent rounds instead of ~23 for a plain binary search over millions of boundaries).
-// eq: the boundary at the result equals q.
-__device__ __forceinline__ int64_t tree_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
-                                                    const uint8_t* htail, const uint8_t* qtail, bool& eq) {
-    eq = false;
-    if (n <= 0) return 0;
-    int64_t sz[kIdxLevels];
-    sz[0] = (n + kFan - 1) / kFan;
-#pragma unroll
-    for (int L = 1; L < kIdxLevels; L++) sz[L] = (sz[L - 1] + 15) / 16;
-    int top = 0;
-    while (top + 1 < kIdxLevels && sz[top] > 16) top++;
-    // c = number of entries of level `top` whose prefix is < q
-    int64_t c = 0;
-    for (int64_t j0 = 0; j0 < sz[top]; j0 += 16) {
-        const int cnt = (int)min((int64_t)16, sz[top] - j0);
-        const int k = count16(m.skey[top], j0, cnt, q);
-        c += k;
-        if (k < cnt) break;
-    }
-    for (int L = top; L > 0; L--) {
-        if (c == 0) continue;  // nothing below q at this level: nothing below it underneath either
-        // entries of level L-1 below q: [0, c') with c' in [16(c-1)+1, 16c]
-        const int64_t base = 16 * (c - 1) + 1;
-        const int64_t end = min(16 * c, sz[L - 1]);
-        c = base + count16(m.skey[L - 1], base, (int)(end - base), q);
-    }
-    // c = #samples below q; samples equal to q's prefix (shared prefixes) widen the block
-    int64_t b = c;
-    while (b < sz[0] && m.skey[0][b].x == q.hi && m.skey[0][b].y == q.lo) b++;
-    int64_t lo = c > 0 ? kFan * (c - 1) + 1 : 0;
-    int64_t hi = min(n, kFan * b);
-    if (hi - lo > kFan) {  // long run of shared prefixes: plain binary search
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) >> 1;
-            const int r = hist_cmp(h, mid, htail, q, qtail);
-            if (r < 0) {
-                lo = mid + 1;
-            } else {
-                hi = mid;
-                eq = r == 0;
-            }
-        }
-        return lo;
-    }
-    // lower_bound in [lo, hi], hi - lo <= 64: probes at lo+4i+3, then the 3 left in one quad
-    ulonglong2 k1[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const int64_t p = lo + 4 * i + 3;
-        if (p < hi) k1[i] = h.key[p];
-    }
-    int c1 = 0;
-    bool eq1 = false;  // the probe that stopped the count hit q itself
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const int64_t p = lo + 4 * i + 3;
-        if (p < hi && c1 == i) {
-            const int r = probe_cmp(h, p, k1[i], htail, q, qtail);
-            if (r < 0)
-                c1++;
-            else
-                eq1 = r == 0;
-        }
-    }
-    const int64_t q0 = lo + 4 * c1;  // lower_bound in [q0, min(hi, q0 + 3)]
-    ulonglong2 k2[3];
-#pragma unroll
-    for (int i = 0; i < 3; i++)
-        if (q0 + i < hi) k2[i] = h.key[q0 + i];
-    int c2 = 0;
-    bool eq2 = false, stopped = false;
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        if (q0 + i < hi && !stopped) {
-            const int r = probe_cmp(h, q0 + i, k2[i], htail, q, qtail);
-            if (r < 0) {
-                c2++;
-            } else {
-                stopped = true;
-                eq2 = r == 0;
-            }
-        }
-    }
-    const int64_t lb = q0 + c2;
-    // the boundary at lb was probed in the quad (stopped) or is the round-1 probe lo+4c1+3
-    eq = stopped ? eq2 : (c2 == 3 && lb < hi ? eq1 : false);
-    return lb;
 }
 
 // ---- long-key probes (batches with keys over 16 bytes: C4 tuple keys)
@@ -628,232 +467,19 @@ __device__ __forceinline__ bool tier_conflict(const Hist& h, const MaxLevels& m,
     return range_max(m, ub - 1, j, snap) > snap;
 }
 
-// Does the read [kb, ke) (degenerate: [kb, kb)) meet a union segment of the previous batch, i.e.
-// would the merge of that batch (SkipList.cpp:899-924: [B, E) set to its `now`, E keeping its old
-// version) put a boundary the read counts at `now`?  Segments are disjoint and sorted, so the last
-// one whose begin lies below the read's end decides (below its begin for a degenerate read, which
-// looks at the greatest boundary < b): it meets the read iff its end lies past the read's begin (at
-// or past it for a degenerate read).  The kArity lanes of one group call this with the same read
-// (ballots and shuffles stay inside the group): a kArity-ary search over the U begin keys.
-__device__ __forceinline__ bool prev_seg_hit(const PrevSegs& ps, int64_t U, const DKey& kb, const DKey& ke,
-                                             bool degenerate, const uint8_t* qtail) {
-    const DKey& target = degenerate ? kb : ke;
-    const int lane = threadIdx.x & 63;
-    const int gl = lane & (kArity - 1), gbase = lane & ~(kArity - 1);
-    int64_t lo = 0, hi = U;  // begins below the target: all of [0, lo), none of [hi, U)
-    while (lo < hi) {
-        const int64_t idx = lo + ((hi - lo) * (gl + 1)) / (kArity + 1);
-        const bool below = dkey_cmp(ps.segk[2 * idx], ps.tail, target, qtail) < 0;
-        const uint32_t m = (uint32_t)(__ballot(below) >> gbase) & ((1u << kArity) - 1);
-        const int c = __popc(m);  // the probes below form a prefix (begins ascend with idx)
-        const int64_t nlo = c > 0 ? __shfl(idx, gbase + c - 1, 64) + 1 : lo;
-        const int64_t nhi = c < kArity ? __shfl(idx, gbase + c, 64) : hi;
-        lo = nlo;
-        hi = nhi;
-    }
-    if (lo == 0) return false;
-    const int cmp = dkey_cmp(ps.segk[2 * lo - 1], ps.tail, kb, qtail);  // end of segment lo - 1 vs b
-    return degenerate ? cmp >= 0 : cmp > 0;
-}
-
-// kArity lanes per lookup, four lookups per read range (SkipList.cpp:426-458 + CheckMax :619-706,
-// as the step-function rule of SURVEY A.2): lane groups 0/1 of a read locate its begin/end key in
-// the base tier, groups 2/3 in the delta tier, all concurrently.  The history is the base tier
-// overlaid by the delta tier; every delta version is >= the base versions it covers (versions only
-// grow), so the max over the overlay equals the max of the two tiers' maxima, and holes (kHole)
-// never conflict.  Every lane of the wave calls this (shuffles and ballots).
-constexpr int kReadLanes = 4 * kArity;
-
-__device__ __forceinline__ void check_read(const BatchDev& b, const Tier& base, const Tier& delta,
-                                           const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf, int64_t slot) {
-    const int lane = threadIdx.x & 63;
-    const int r = (int)(slot / kReadLanes);
-    const int grp = (lane / kArity) & 3;
-    const int lead = lane & ~(kReadLanes - 1);  // first lane of this read
-    const bool live = r < b.R;
-    const int rr = live ? r : 0;
-    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
-    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    const Tier& tier = grp < 2 ? base : delta;
-    const int64_t n = *tier.n;
-    const int64_t snap = b.snap[b.rowner[rr]];  // issued before the search
-    int64_t lb = 0;
-    bool eq = false;
-    if (live && !((grp & 1) && degenerate))
-        lb = group_lower_bound(tier.h, tier.m, n, (grp & 1) ? ke : kb, htail, b.tail, eq);
-    const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // groups 0 and 2 take the end key's position
-    const bool leader = lane == lead || lane == lead + 2 * kArity;
-    bool conf = false;
-    if (live && leader && (grp == 0 || n > 0)) {
-        conf = tier_conflict(tier.h, tier.m, grp == 0 ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
-    }
-    const int dconf = __shfl((int)conf, lead + 2 * kArity, 64);
-    if (live && lane == lead) {
-        conf = conf || dconf;
-        rconf[r] = conf ? 1 : 0;
-        if (conf) hist_conf[b.rowner[r]] = 1;
-    }
-}
-
-// check_read with the tiers in separate waves (FDBCS_CHECK=6): a block's first half of waves
-// searches the base tier for its kBlock / kReadLanes reads (16 lanes each: begin and end groups),
-// the second half the delta tier for the same reads, and the delta verdicts reach the base
-// leaders through LDS.  In check_read a wave holds both tiers' groups, so a base lookup taking the
-// radix directory and a delta lookup descending its tree run one after the other (divergent
-// branches of one wave); here each wave runs one of them.
-__device__ __forceinline__ void check_read_tier_waves(const BatchDev& b, const Tier& base, const Tier& delta,
-                                                      const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
-                                                      const PrevSegs& ps) {
-    constexpr int kPerWave = 64 / (2 * kArity);               // reads per wave (16 lanes each)
-    constexpr int kHalf = kBlock / 64 / 2;                    // waves per tier
-    constexpr int kReadsPerBlock = kHalf * kPerWave;          // == kBlock / kReadLanes
-    static_assert(kReadsPerBlock == kBlock / kReadLanes, "same reads per block as check_read");
-    __shared__ uint8_t sconf[kReadsPerBlock];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const bool is_delta = wave >= kHalf;
-    const int local = (wave % kHalf) * kPerWave + lane / (2 * kArity);
-    const int64_t r = (int64_t)blockIdx.x * kReadsPerBlock + local;
-    const int grp = (lane / kArity) & 1;  // 0 begin key, 1 end key
-    const bool live = r < b.R;
-    const int64_t rr = live ? r : 0;
-    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
-    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    const Tier& tier = is_delta ? delta : base;
-    const int64_t n = *tier.n;
-    const int64_t snap = b.snap[b.rowner[rr]];
-    int64_t lb = 0;
-    bool eq = false;
-    if (live && !(grp && degenerate)) lb = group_lower_bound(tier.h, tier.m, n, grp ? ke : kb, htail, b.tail, eq);
-    const int64_t j = __shfl(lb, (lane + kArity) & 63, 64);  // the begin group takes the end key's position
-    const bool leader = (lane & (2 * kArity - 1)) == 0;
-    bool conf = false;
-    if (live && leader && (!is_delta || n > 0))
-        conf = tier_conflict(tier.h, tier.m, is_delta ? kHole : tier.hdr, lb, eq, j, degenerate, snap);
-    if (is_delta && ps.n) {  // the previous batch's union segments, not merged into the delta yet
-        const int64_t U = *ps.n;
-        bool hit = false;
-        if (live && grp == 1 && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
-        conf = conf || __shfl((int)hit, (lane + kArity) & 63, 64);
-    }
-    if (leader && is_delta) sconf[local] = conf ? 1 : 0;
-    __syncthreads();
-    if (live && leader && !is_delta) {
-        conf = conf || sconf[local];
-        rconf[r] = conf ? 1 : 0;
-        if (conf) hist_conf[b.rowner[r]] = 1;
-    }
-}
-
-// One tier only (the split check): 2 lane groups per read locate its begin / end in `tier`; a
-// conflict sets the read's and its transaction's flags (zeroed beforehand by the epilogue that last
-// used the workspace), so the base-tier launch (stage A, on its own stream) and the delta-tier
-// launch (stage B) OR into the same flags.  is_base: the tier's header version applies below its
-// first boundary (the delta's header is kHole: the base shows through).
-constexpr int kTierLanes = 2 * kArity;
-
-// range_max by the kTierLanes lanes of one read (all call with the same lo / hi): at each level of
-// the 64-ary hierarchy the partial blocks at both ends (< 2 kFan entries, or the whole rest at the
-// last level) are read kTierLanes entries per coalesced access, 8 accesses per lane in flight, and
-// max-reduced across the lanes; stops after a level once above `snap`.  A wide read (C4's
-// Tuple.range() over a user's ~50 boundaries) costs one round of loads instead of a dependent scan
-// by one lane.
-__device__ __forceinline__ int64_t group_range_max(const MaxLevels& m, int64_t lo, int64_t hi, int64_t snap) {
-    const int sl = threadIdx.x & (kTierLanes - 1);
-    int64_t best = LLONG_MIN;
-    for (int L = 0; L < kMaxLevels; L++) {
-        const int64_t* a = m.lvl[L];
-        const bool last = hi - lo <= 2 * kFan || L == kMaxLevels - 1;
-        const int64_t lo2 = last ? 0 : (lo + kFan - 1) / kFan, hi2 = last ? 0 : hi / kFan;
-        const int64_t le = last ? hi : lo2 * kFan;  // left part [lo, le)
-        const int64_t rs = last ? hi : hi2 * kFan;  // right part [rs, hi)
-        const int64_t nl = le - lo, cnt = nl + (hi - rs);
-        for (int64_t base = 0; base < cnt; base += 8 * kTierLanes) {
-            int64_t v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int64_t k = base + u * kTierLanes + sl;
-                const int64_t ix = k < nl ? lo + k : rs + (k - nl);
-                v[u] = k >= cnt ? LLONG_MIN : (L == kMaxLevels - 1 ? l3_at(a, ix) : a[ix]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) best = v[u] > best ? v[u] : best;
-        }
-#pragma unroll
-        for (int o = 1; o < kTierLanes; o <<= 1) {
-            const int64_t y = __shfl_xor(best, o, 64);
-            best = y > best ? y : best;
-        }
-        if (last || best > snap) return best;
-        lo = lo2;
-        hi = hi2;
-    }
-    return best;
-}
-
-template <bool LONG = false>
-__device__ __forceinline__ void check_read_tier(const BatchDev& b, const Tier& tier, bool is_base, const uint8_t* htail,
-                                                uint8_t* hist_conf, uint8_t* rconf, int64_t slot, int lead_rmax,
-                                                const PrevSegs& ps) {
-    const int lane = threadIdx.x & 63;
-    const int k = (int)(slot / kTierLanes);
-    const int grp = (lane / kArity) & 1;
-    const int lead = lane & ~(kTierLanes - 1);
-    const bool live = k < b.R;
-    const int rr = live ? k : 0;
-    const int r = rr;
-    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
-    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
-    const int64_t n = *tier.n;
-    const int64_t snap = b.snap[b.rowner[rr]];
-    const bool active = live && (is_base || n > 0);  // uniform over the read's lanes
-    int64_t lb = 0;
-    bool eq = false;
-    if (active && !(grp && degenerate))
-        lb = group_lower_bound<LONG>(tier.h, tier.m, n, grp ? ke : kb, htail, b.tail, eq);
-    // every lane of the read: the begin key's position (group 0) and the end key's (group 1)
-    const int64_t lbb = __shfl(lb, lead, 64);
-    const int eqb = __shfl((int)eq, lead, 64);
-    const int64_t j = __shfl(lb, lead + kArity, 64);
-    bool conf = false;
-    if (!is_base && ps.n) {  // the previous batch's union segments, not merged into the delta yet
-        const int64_t U = *ps.n;
-        bool hit = false;
-        if (live && grp == 1 && U > 0 && ps.version > snap) hit = prev_seg_hit(ps, U, kb, ke, degenerate, b.tail);
-        if (__shfl((int)hit, lead + kArity, 64) && live && lane == lead) {
-            rconf[r] = 1;
-            hist_conf[b.rowner[r]] = 1;
-        }
-    }
-    if (lead_rmax) {  // FDBCS_GROUP_RMAX=0 (A/B): the range max by the read's first lane alone
-        if (active && lane == lead && tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap)) {
-            rconf[r] = 1;
-            hist_conf[b.rowner[r]] = 1;
-        }
-        return;
-    }
-    if (active) {  // tier_conflict with the range max shared by the read's lanes
-        const int64_t hdr = is_base ? tier.hdr : kHole;
-        if (degenerate) {
-            conf = (lbb > 0 ? tier.h.ver[lbb - 1] : hdr) > snap;
-        } else {
-            const int64_t ub = lbb + (eqb ? 1 : 0);
-            // segments [ub-1, j): the one containing b (header if ub == 0) and boundaries in (b, e)
-            conf = (ub == 0 && hdr > snap) || group_range_max(tier.m, ub > 0 ? ub - 1 : 0, j, snap) > snap;
-        }
-    }
-    if (active && lane == lead && conf) {
-        rconf[r] = 1;
-        hist_conf[b.rowner[r]] = 1;
-    }
-}
-
-// ---- per-lane lookups (FDBCS_CHECK=7, the default for batches of keys up to 24 bytes)
+// ---- per-lane lookups (SkipList.cpp:426-458 + CheckMax :619-706, as the step-function rule of
+// SURVEY A.2)
 //
-// One lane per lookup.  The cooperative lookups above give each lookup kArity lanes that load one
-// node entry each, so a wave serves kArity lookups and the wave's instruction stream (ballots,
-// shuffles, 64-bit compares) is paid per kArity lookups: at C2 12,500 waves of ~350 VALU + ~260
-// SALU instructions each, 77 % of their life waiting on loads (rocprofv3 SQ counters), the chip
-// never holding all of them at once.  Here a lane issues a whole node's (or directory slot's)
+// The history is the base tier overlaid by the delta tier; every delta version is >= the base
+// versions it covers (versions only grow), so the max over the overlay equals the max of the two
+// tiers' maxima, and holes (kHole) never conflict.
+//
+// One lane per lookup.  Round 3's cooperative lookups (group_lower_bound, still used by the
+// segment search of small batches) gave each lookup kArity lanes that load one node entry each,
+// so a wave served kArity lookups and the wave's instruction stream (ballots, shuffles, 64-bit
+// compares) was paid per kArity lookups: at C2 12,500 waves of ~350 VALU + ~260 SALU instructions
+// each, 77 % of their life waiting on loads (rocprofv3 SQ counters), the chip never holding all
+// of them at once.  Here a lane issues a whole node's (or directory slot's)
 // entries itself, up to kLaneProbe independent 16-byte loads in flight, and counts them in
 // registers: the same dependent rounds per lookup, 64 lookups per wave, every wave of a C2 batch
 // resident at once.
@@ -1245,8 +871,13 @@ __device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const Ma
     return lo;
 }
 
-// The previous batch's union segments (prev_seg_hit) searched by the four lanes of one read
-// (lanes 4i..4i+3 call with the same read): 16 probes per round, four per lane.
+// Does the read [kb, ke) (degenerate: [kb, kb)) meet a union segment of the previous batch, i.e.
+// would the merge of that batch (SkipList.cpp:899-924: [B, E) set to its `now`, E keeping its old
+// version) put a boundary the read counts at `now`?  Segments are disjoint and sorted, so the last
+// one whose begin lies below the read's end decides (below its begin for a degenerate read, which
+// looks at the greatest boundary < b): it meets the read iff its end lies past the read's begin (at
+// or past it for a degenerate read).  Searched by the four lanes of one read (lanes 4i..4i+3 call
+// with the same read): 16 probes per round, four per lane.
 __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U, const DKey& kb, const DKey& ke,
                                                   bool degenerate, const uint8_t* qtail, bool active) {
     const DKey& target = degenerate ? kb : ke;
@@ -1332,8 +963,11 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
     }
 }
 
-// One tier only (the split check) by two lanes per read: begin / end; conflicts OR into the
-// pre-zeroed flags like check_read_tier.
+// One tier only (the split check) by two lanes per read: begin / end; a conflict sets the read's and
+// its transaction's flags (zeroed beforehand by the epilogue that last used the workspace), so the
+// base-tier launch (stage A, on its own stream) and the delta-tier launch (stage B) OR into the
+// same flags.  is_base: the tier's header version applies below its first boundary (the delta's
+// header is kHole: the base shows through).
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const Tier& tier, bool is_base,
                                                       const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
@@ -1537,27 +1171,17 @@ __global__ __launch_bounds__(kBlock) void k_sample(BatchDev b, SampleRank c) {
     if (threadIdx.x == 0) trace_max(c.trace, kTrSampleEnd);
 }
 
-// D.CheckRead (stage B: reads the history as the previous batch left it), kReadLanes lanes per
-// read range.
+// D.CheckRead (stage B: reads the history as the previous batch left it).
 struct CheckReads {
     Tier base, delta;
     const uint8_t* htail;
     uint8_t *hist_conf, *rconf;
     unsigned long long* trace;
-    PrevSegs ps;  // FDBCS_CHECK=6 only (the one-wave variant runs after the previous batch's merge)
+    PrevSegs ps;  // the previous batch's union segments, not merged yet
 };
 
-// Split check: base tier (stage A, own stream) or delta tier (stage B); two instantiations so
-// profiles tell the launches apart.
-// LONG: the batch has keys over 16 bytes (long-key probes, group_lower_bound<true>).
-template <bool BASE, bool LONG>
-__global__ __launch_bounds__(kBlock) void k_check_tier(BatchDev b, Tier t, const uint8_t* htail, uint8_t* hist_conf,
-                                                       uint8_t* rconf, int lead_rmax, PrevSegs ps) {
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    check_read_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, slot, lead_rmax, ps);
-}
-
-// Per-lane checks (FDBCS_CHECK=7): both tiers, four lanes per read; one tier, two lanes per read.
+// Per-lane checks: both tiers, four lanes per read; one tier (the split check), two lanes per read;
+// two instantiations of the tier launch so profiles tell the base and delta launches apart.
 // LONG: the batch has keys over 24 bytes (lane_lower_bound_long).
 template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes(BatchDev b, CheckReads c) {
@@ -1570,51 +1194,20 @@ __global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t,
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys, bool lead_rmax, const PrevSegs& ps, bool lanes) {
+                       const uint8_t* htail, bool long_keys, const PrevSegs& ps) {
     if (b.R == 0) return;
-    if (lanes) {
-        const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
-        auto k = is_base ? (long_keys ? k_check_lanes_tier<true, true> : k_check_lanes_tier<true, false>)
-                         : (long_keys ? k_check_lanes_tier<false, true> : k_check_lanes_tier<false, false>);
-        fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
-        return;
-    }
-    const int grid = (int)(((int64_t)b.R * kTierLanes + kBlock - 1) / kBlock);
-    auto k = is_base ? (long_keys ? k_check_tier<true, true> : k_check_tier<true, false>)
-                     : (long_keys ? k_check_tier<false, true> : k_check_tier<false, false>);
-    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, lead_rmax ? 1 : 0,
-               is_base ? PrevSegs{} : ps);
-}
-
-template <bool TIER_WAVES>
-__global__ __launch_bounds__(kBlock) void k_check_reads(BatchDev b, CheckReads c) {
-    if (threadIdx.x == 0) trace_min(c.trace, kTrCheckBegin);
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if constexpr (TIER_WAVES)
-        check_read_tier_waves(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
-    else
-        check_read(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, slot);
-    __syncthreads();
-    if (threadIdx.x == 0) trace_max(c.trace, kTrCheckEnd);
+    const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
+    auto k = is_base ? (long_keys ? k_check_lanes_tier<true, true> : k_check_lanes_tier<true, false>)
+                     : (long_keys ? k_check_lanes_tier<false, true> : k_check_lanes_tier<false, false>);
+    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, int check_version, const PrevSegs& ps) {
+                  const uint8_t* htail, bool long_keys, const PrevSegs& ps) {
     if (b.R == 0) return;
-    // four lookups per read: 7 = one lane each, 6 = kArity lanes each with the base and delta lookups
-    // in separate waves, 1 = kArity lanes each in one wave
-    CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps};
-    if (check_version == 7 || check_version == 8) {  // 8: the long-key lanes
-        const int grid = (int)(((int64_t)b.R * 4 + kBlock - 1) / kBlock);
-        fdb_launch(check_version == 8 ? k_check_lanes<true> : k_check_lanes<false>, dim3(grid), dim3(kBlock), 0, s, b,
-                   c);
-        return;
-    }
-    const int grid = (int)(((int64_t)b.R * kReadLanes + kBlock - 1) / kBlock);
-    if (check_version == 6)
-        fdb_launch(k_check_reads<true>, dim3(grid), dim3(kBlock), 0, s, b, c);
-    else
-        fdb_launch(k_check_reads<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
+    const CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps};
+    const int grid = (int)(((int64_t)b.R * 4 + kBlock - 1) / kBlock);
+    fdb_launch(long_keys ? k_check_lanes<true> : k_check_lanes<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
 
 // ---- D.Sort (SkipList.cpp:161-208) and the sorted positions (KeyInfo::pIndex, SkipList.cpp:814)
@@ -1943,6 +1536,12 @@ __device__ __forceinline__ uint32_t split_lcp(const SplitKey& a, const SplitKey&
     return c < b.len ? c : b.len;
 }
 
+// Slab slots every bucket wave loads before its count arrives (the rest after it).
+#ifndef FDBCS_SPEC_SLOTS
+#define FDBCS_SPEC_SLOTS 128
+#endif
+constexpr int kSpecSlots = FDBCS_SPEC_SLOTS;
+
 template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, SortOut o) {
     constexpr int kWaves = kBlock / 64;
@@ -1973,7 +1572,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
     SortItem sp[2];
 #pragma unroll
     for (int s = 0; s < 2; s++)
-        if (bk < nb) sp[s] = a.slab[(size_t)bk * kSlab + s * 64 + lane];
+        if (bk < nb && s * 64 + lane < kSpecSlots) sp[s] = a.slab[(size_t)bk * kSlab + s * 64 + lane];
     // (the first kPreHeld chunks stay in registers across the sort, enough for nb <= 1536 buckets,
     // ~98k endpoints; larger batches load the rest after it)
     constexpr int kPreLoads = kSortMaxBuckets / kBlock, kPreHeld = 6;
@@ -2005,7 +1604,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             const int k = s * 64 + lane;
             kh[s] = kl[s] = ka[s] = ~0ull;  // padding sorts after every endpoint
             if (s < S && k < n) {
-                const SortItem it = s < 2 ? sp[s] : a.slab[(size_t)bk * kSlab + k];
+                const SortItem it = s < 2 && k < kSpecSlots ? sp[s] : a.slab[(size_t)bk * kSlab + k];
                 if (c == 0) {
                     kh[s] = it.hi;
                     kl[s] = it.lo;
@@ -3505,19 +3104,16 @@ __device__ __forceinline__ void fill_tile_first_tail(int32_t* tile_first, const 
 //     (lane_lower_bound).  The tiles' look-back chain sets the pace once tiles number in the
 //     hundreds: at 32768-txn C2 batches 1040 narrow tiles took 116 us per launch, 516 wide ones 46
 //     (255 segments per tile: 53, 511: 67, too few lookups in flight);
-//   long keys (WIDE): 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long holds
-//     the query's tail words in registers);
-//   long keys, coop (FDBCS_SEG_LONG_COOP=1): 1024 threads, 63 segments, kArity lanes per lookup
-//     (group_lower_bound<true>).
+//   long keys (always WIDE): 128 threads, 63 segments, one lane per lookup (lane_lower_bound_long
+//     holds the query's tail words in registers; kArity lanes per lookup measured 56 against 39 us
+//     at C4).
 constexpr int kSegWideMinW = 24576;
 constexpr int seg_per(bool long_keys, bool wide) { return long_keys || !wide ? 63 : 127; }
 constexpr int seg_lanes(bool, bool wide) { return wide ? 1 : kArity; }
 constexpr int seg_threads(bool long_keys, bool wide) {
     return 2 * seg_lanes(long_keys, wide) * (seg_per(long_keys, wide) + 1);
 }
-inline bool seg_wide(int64_t W, bool long_keys, bool long_coop) {
-    return long_keys ? !long_coop : W >= kSegWideMinW;
-}
+inline bool seg_wide(int64_t W, bool long_keys) { return long_keys || W >= kSegWideMinW; }
 inline int64_t seg_tiles(int64_t W, bool long_keys, bool wide) { return (W > 0 ? W : 1) / seg_per(long_keys, wide) + 1; }
 // an upper bound over the layouts (workspace look-back granules)
 inline int64_t seg_prep_tiles(int64_t W) { return (W > 0 ? W : 1) / 63 + 1; }
@@ -3557,12 +3153,11 @@ __global__ __launch_bounds__(seg_threads(LONG, WIDE)) void k_seg_prep(BatchDev b
         kb = seg_key(b, w, w.seg_b[sg], 0);
         ke = seg_key(b, w, w.seg_e[sg], 1);
         const DKey& key = role ? ke : kb;
-        if constexpr (LONG && WIDE) {
+        if constexpr (LONG) {
+            static_assert(WIDE, "long-key batches take the one-lane layout");
             QTail qt;
             load_qtail(qt, key, b.tail);
             pos = lane_lower_bound_long(h, hm, n, key, qt, htail, b.tail, eq);
-        } else if constexpr (LONG) {  // kArity lanes per lookup, long-key probes
-            pos = group_lower_bound<true>(h, hm, n, key, htail, b.tail, eq);
         } else if constexpr (WIDE) {
             pos = lane_lower_bound(h, hm, n, key, htail, b.tail, eq);
         } else {  // the group's kArity lanes search together (live is uniform per group)
@@ -3862,13 +3457,12 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
 void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& src, const MaxLevels& srcm,
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
                   int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
-                  hipEvent_t copy_end, bool long_keys, bool long_coop) {
+                  hipEvent_t copy_end, bool long_keys) {
     const TierIO io{nd_src, &sc->nd_next, &sc->d_before, &sc->d_rem};
     // the destination's top level is reset for the epilogue's atomicMax build (the source's levels
     // stay intact: the next batch's read check may still search them)
-    const bool wide = seg_wide(b.W, long_keys, long_coop);
-    fdb_launch(long_keys ? (wide ? k_seg_prep<true, true> : k_seg_prep<true, false>)
-                         : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
+    const bool wide = seg_wide(b.W, long_keys);
+    fdb_launch(long_keys ? k_seg_prep<true, true> : (wide ? k_seg_prep<false, true> : k_seg_prep<false, false>),
                dim3((unsigned)seg_tiles(b.W, long_keys, wide)), dim3(seg_threads(long_keys, wide)), 0, s, b, w, src, srcm, htail, sc, io, dstm.lvl[3], lvl3_n,
                dstm.lvl[2], lvl2_n);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
@@ -3895,9 +3489,9 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
 // of an earlier merge and becomes a real boundary carrying the base version at d_j, unless the
 // base already has a boundary at d_j.  The result is the boundary set the reference would hold.
 
-// MODE 0: kArity lanes per delta boundary (group_lower_bound); 1: one lane per boundary
-// (lane_lower_bound); 2: one lane, the long-key form (lane_lower_bound_long: tuple keys sharing
-// 16-byte prefixes).  Same result for every mode (FDBCS_COMPACT_LANES picks it).
+// One lane per delta boundary.  MODE 1: lane_lower_bound; 2: the long-key form
+// (lane_lower_bound_long: tuple keys sharing 16-byte prefixes), after long-key batches.  (kArity
+// lanes per boundary, round 4's search, measured 1321 against 535 us at C4.)
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels basem, Hist delta,
                                                            const uint8_t* htail, const int64_t* nb_ptr,
@@ -3906,9 +3500,9 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int64_t i = gt; i < lvl3_n * kL3Rep; i += (int64_t)gridDim.x * blockDim.x) lvl3[i * kL3Pad] = LLONG_MIN;
     for (int64_t i = gt; i < lvl2_n; i += (int64_t)gridDim.x * blockDim.x) lvl2[i] = LLONG_MIN;
-    const int64_t j = MODE == 0 ? gt / kArity : gt;  // MODE 0: kArity lanes per delta boundary
+    const int64_t j = gt;
     const int64_t nd = *nd_ptr;
-    if (j >= nd) return;  // whole groups leave together
+    if (j >= nd) return;
     const int64_t nb = *nb_ptr;
     const ulonglong2 k = delta.key[j];
     const uint2 lt = delta.lt[j];
@@ -3920,10 +3514,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_search(Hist base, MaxLevels 
     bool exact;
     const uint8_t* qtail = hist_tail(htail, lt.y);
     int64_t lo;
-    if constexpr (MODE == 0) {
-        lo = group_lower_bound(base, basem, nb, q, htail, qtail, exact);
-        if ((gt % kArity) != 0) return;
-    } else if constexpr (MODE == 1) {
+    if constexpr (MODE == 1) {
         lo = lane_lower_bound(base, basem, nb, q, htail, qtail, exact);
     } else {
         QTail qt;
@@ -3985,12 +3576,9 @@ void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLev
                     const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
                     hipEvent_t copy_end, int mode, int base_tile, bool nt) {
-    int64_t blocks = ((mode == 0 ? kArity : 1) * delta_hint_n + kBlock - 1) / kBlock;
+    int64_t blocks = (delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
-    if (mode == 0)
-        fdb_launch(k_compact_search<0>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
-                   &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
-    else if (mode == 1)
+    if (mode == 1)
         fdb_launch(k_compact_search<1>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
                    &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
     else
@@ -4556,33 +4144,6 @@ __global__ __launch_bounds__(kBlock) void k_copy_bytes(uint8_t* __restrict__ dst
                                                        int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
-}
-
-// H2D of a packed batch by the CUs (FDBCS_UPLOAD=kernel): 16-byte loads from the host-mapped
-// pinned staging buffer over PCIe, many in flight per thread, instead of one DMA-engine copy.
-__global__ __launch_bounds__(kBlock) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16,
-                                                   const uint8_t* __restrict__ src_b, uint8_t* __restrict__ dst_b,
-                                                   int64_t n) {
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = tid;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = src[i + u * stride];
-#pragma unroll
-        for (int u = 0; u < 4; u++) dst[i + u * stride] = v[u];
-    }
-    for (; i < n16; i += stride) dst[i] = src[i];
-    for (int64_t j = 16 * n16 + tid; j < n; j += stride) dst_b[j] = src_b[j];
-}
-
-void launch_upload(hipStream_t s, void* dst, const void* src, int64_t n) {
-    if (n <= 0) return;
-    const int64_t n16 = n / 16;
-    int64_t blocks = (n16 + 4 * kBlock - 1) / (4 * kBlock);
-    blocks = blocks < 1 ? 1 : (blocks > 512 ? 512 : blocks);
-    fdb_launch(k_upload, dim3((unsigned)blocks), dim3(kBlock), 0, s, (const uint4*)src, (uint4*)dst, n16,
-               (const uint8_t*)src, (uint8_t*)dst, n);
 }
 
 void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n) {

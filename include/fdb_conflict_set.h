@@ -117,7 +117,6 @@ typedef struct fdbcs_stats {
     double host_ms_prepare;
     double host_ms_record;
     double host_ms_submit;
-    int64_t graph_launches; /* stage lists submitted as one graph launch (FDBCS_GRAPH=2) */
     int64_t compact_launches; /* compactions whose copy kernel was timed (compact_bytes counts these only) */
     /* Shapes of every batch, whatever the timing level (the roofline's byte models, roofline.py). */
     int64_t merge_bytes_all;   /* algorithmic bytes of every delta-merge copy */

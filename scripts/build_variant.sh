@@ -15,7 +15,7 @@ done
 H=/opt/rocm/bin/hipcc
 $H -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -mllvm -disable-promote-alloca-to-lds ${EXTRA:-} \
   -c $TMP/foundationdb_amd/csrc/kernels.hip -o $TMP/kernels.o
-$H -O3 -std=c++17 -fPIC -Wall -c $TMP/foundationdb_amd/csrc/engine.cpp -o $TMP/engine.o
+$H -O3 -std=c++17 -fPIC -Wall ${EXTRA:-} -c $TMP/foundationdb_amd/csrc/engine.cpp -o $TMP/engine.o
 $H --offload-arch=gfx950 -shared -fPIC -o foundationdb_amd/variants/libfdbcs_$NAME.so $TMP/engine.o $TMP/kernels.o
 rm -rf $TMP
 echo foundationdb_amd/variants/libfdbcs_$NAME.so

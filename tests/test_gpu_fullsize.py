@@ -57,15 +57,12 @@ def check_against_restatement(oracle_mod, kb, ko, vers, seq, got, gc="bounded"):
     return sl
 
 
-@pytest.mark.parametrize("submit_thread", ["0", "1", "lag"])
+@pytest.mark.parametrize("submit_thread", ["0", "1"])
 def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
     """C2 at full size (5M-boundary history, 5000 txns x 5R+2W) through the async pipeline for 72
     batches: crosses several size-triggered compactions and a removeBefore pass; with one and with
-    two submitting threads (FDBCS_SUBMIT_THREAD), and with each batch's stage B issued at the next
-    detect (FDBCS_LAG)."""
-    monkeypatch.setenv("FDBCS_SUBMIT_THREAD", "0" if submit_thread == "lag" else submit_thread)
-    monkeypatch.setenv("FDBCS_LAG", "1" if submit_thread == "lag" else "0")
-    monkeypatch.setenv("FDBCS_DELTA_FLOOR", "0")  # the N/16 bound: a compaction every ~16 batches
+    two submitting threads (FDBCS_SUBMIT_THREAD)."""
+    monkeypatch.setenv("FDBCS_SUBMIT_THREAD", submit_thread)
     p = W.C2Params()
     start = 10_000_000
     kb, ko, vers = W.c2_history(p, seed=1, start_version=start)
@@ -76,6 +73,7 @@ def test_async_pipeline_full_c2(engine, oracle_mod, monkeypatch, submit_thread):
         seq.append((W.c2_batch(p, rng, now), now, now - p.window))
     cs = engine.ConflictSet(0)
     cs.load_history(kb, ko, vers, 0)
+    cs.set_delta_limit(len(vers) // 16)  # the N/16 bound: a compaction every ~16 batches
     got = {}
     pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
     st = cs.stats()
@@ -159,16 +157,13 @@ def test_flag_before_epilogue_end_without_submit_thread(engine, oracle_mod, monk
     cs.close()
 
 
-@pytest.mark.parametrize("mode", ["default", "lag_split"])
+@pytest.mark.parametrize("mode", ["default", "split"])
 def test_async_pipeline_full_c3(engine, oracle_mod, monkeypatch, mode):
     """C3 at full size: Zipf(0.99) hot keys, 5000 txns per batch over the 5M-boundary history,
-    heavy intra-batch conflicts resolved in batch order on the device.  lag_split: each batch's
-    stage B issued at the next detect (FDBCS_LAG) with the base-tier check on its own stream
-    (FDBCS_SPLIT_CHECK=1) and compactions every few batches, so a stage A is issued before the
-    previous batch's compaction (the base-tier check must wait for it)."""
-    if mode == "lag_split":
-        monkeypatch.setenv("FDBCS_LAG", "1")
-        monkeypatch.setenv("FDBCS_SUBMIT_THREAD", "0")
+    heavy intra-batch conflicts resolved in batch order on the device.  split: the base-tier check
+    on its own stream (FDBCS_SPLIT_CHECK=1) and compactions every few batches, so a base-tier check
+    is issued before the previous batch's compaction (and must wait for it)."""
+    if mode == "split":
         monkeypatch.setenv("FDBCS_SPLIT_CHECK", "1")
     p = W.C2Params()
     start = 10_000_000
@@ -181,29 +176,62 @@ def test_async_pipeline_full_c3(engine, oracle_mod, monkeypatch, mode):
         seq.append((W.c3_batch(p, rng, now, z), now, now - p.window))
     cs = engine.ConflictSet(0)
     cs.load_history(kb, ko, vers, 0)
-    if mode == "lag_split":
+    if mode == "split":
         cs.set_delta_limit(60_000)  # a compaction every few batches
     got = {}
     pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
     st = cs.stats()
     assert st["intra_edges"] > 0
-    if mode == "lag_split":
+    if mode == "split":
         assert st["compactions"] >= 3, st["compactions"]
     check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
     assert any((got[i] == 0).sum() > 500 for i in got)  # heavy contention really happened
     cs.close()
 
 
-def test_full_c4_window_gc_and_tail_reclaim(engine, oracle_mod, monkeypatch):
+@pytest.fixture(scope="module")
+def c4_history():
+    """The 50M-boundary C4 window (tuple keys), generated once for the module's C4 tests."""
+    p = W.C4Params()
+    start = 10_000_000
+    kb, ko, vers = W.c4_history(p, seed=1000, start_version=start)
+    return p, start, kb, ko, vers
+
+
+def test_async_pipeline_full_c4(engine, oracle_mod, c4_history):
+    """C4 in production mode: 50M boundaries of tuple keys, 8 batches in
+    flight, the default stream layout (the base-tier check on its own stream above 16M
+    boundaries, the submit thread's defaults), size-triggered compactions of the 50M base (the
+    long-key lane search, the non-temporal copy) with removeBefore on every fourth, the window
+    sliding every batch (SkipList.cpp:844-890).  A small delta bound makes the compactions come
+    every few batches.  Every verdict matches the restatement with the reference's bounded
+    removeBefore (verdict-neutral against the device's full GC)."""
+    p, start, kb, ko, vers = c4_history
+    rng = np.random.default_rng(104)
+    seq, now = [], start
+    for _ in range(20):
+        now += p.version_step
+        seq.append((W.c4_batch(p, rng, now), now, now - p.window))
+    cs = engine.ConflictSet(0)
+    cs.load_history(kb, ko, vers, 0)
+    cs.set_delta_limit(60_000)  # ~20k boundaries per batch: a compaction every three batches
+    got = {}
+    pipeline(engine, cs, seq, lambda i, v: got.__setitem__(i, v))
+    st = cs.stats()
+    assert st["compactions"] >= 4, st["compactions"]
+    assert st["gc_runs"] >= 1, st["gc_runs"]
+    check_against_restatement(oracle_mod, kb, ko, vers, seq, got)
+    cs.close()
+
+
+def test_full_c4_window_gc_and_tail_reclaim(engine, oracle_mod, monkeypatch, c4_history):
     """C4 at full size: 50M boundaries of tuple keys (~1.9 GB of tail bytes), the window sliding
     every batch.  The tail-reclaim threshold is lowered to just above the loaded arena so the
     size-triggered path compacts, runs removeBefore and repacks the tails within a few batches.
     Every verdict matches the restatement, and after each device removeBefore the boundary count
     equals the restatement's after a full removeBefore on the same batch."""
-    p = W.C4Params()
-    start = 10_000_000
     t0 = time.time()
-    kb, ko, vers = W.c4_history(p, seed=1000, start_version=start)
+    p, start, kb, ko, vers = c4_history
     tl = np.diff(ko) - 16
     tail0 = int(((tl[tl > 0] + 7) // 8 * 8).sum())  # the loaded arena: tails padded to 8 bytes
     monkeypatch.setenv("FDBCS_TAIL_RECLAIM", str(tail0 + 3_000_000))

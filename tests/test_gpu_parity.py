@@ -255,17 +255,14 @@ def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
-@pytest.mark.parametrize("lanes", ["1", "0"])
 @pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("plen", [30, 60, 104, 150])
-def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split, lanes):
+def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split):
     """Keys sharing prefixes of 30-150 bytes, so that tail comparisons end inside the long-key
     probe's first word round (48 bytes), its second (96), and past the query words it holds in
     registers (the rest compared from memory); history and batch keys of every length around them.
-    split "1": the split read check (long-key probes in both check launches); "2": the default.
-    lanes "1": one lane per lookup (lane_lower_bound_long, the default); "0": kArity lanes per lookup."""
+    split "1": the split read check (long-key probes in both check launches); "2": the default."""
     monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
-    monkeypatch.setenv("FDBCS_LONG_LANES", lanes)
     rng = np.random.default_rng(plen)
     prefixes = [bytes([0x15, 0x2a + i]) + b"x" * (plen - 2) for i in range(2)]
 
@@ -301,9 +298,8 @@ def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split,
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
-@pytest.mark.parametrize("lanes", ["1", "0"])
-@pytest.mark.parametrize("dir_rank,alphabet", [("1", "bytes"), ("1", "digits"), ("1", "sparse"), ("0", "digits")])
-def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_rank, alphabet, lanes):
+@pytest.mark.parametrize("alphabet", ["bytes", "digits", "sparse"])
+def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, alphabet):
     """The radix directories' rank code after the bytes every loaded key shares (MaxLevels::dir_p;
     C4's 9-byte prefix): 120k boundaries under one 10-byte prefix, queries inside it, below and
     above it at every depth, keys shorter than it and the empty key; writes outside the prefix,
@@ -312,9 +308,7 @@ def test_directory_past_shared_prefix(engine, oracle_mod, monkeypatch, dir_rank,
     decimal digits (C4's user ids), ten ranks per position; "sparse": the history holds only even
     byte values in [0x20, 0x7e] while queries and writes take any value in [0x10, 0x90], so codes
     end at unseen values (the next seen value's rank) and values above every seen one carry into
-    the position before.  dir_rank "0": the first two bytes (FDBCS_DIR_RANK=0)."""
-    monkeypatch.setenv("FDBCS_DIR_RANK", dir_rank)
-    monkeypatch.setenv("FDBCS_LONG_LANES", lanes)
+    the position before."""
     rng = np.random.default_rng(77)
     P = bytes([0x41, 0x42, 0x43, 0x44, 0x00, 0xff, 0x45, 0x46, 0x47, 0x48])
     lo_b, hi_b = {"bytes": (0, 256), "digits": (0x30, 0x3a), "sparse": (0x10, 0x91)}[alphabet]
@@ -441,18 +435,12 @@ def test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, gc_interval, d
         assert e.cs.history_size() == o.history_size()
 
 
-@pytest.mark.parametrize("mode,tile,coop,nt", [("0", "4096", "0", "1"), ("1", "2048", "1", "0"), ("2", "1024", "0", "0"),
-                                               ("2", "4096", "1", "0")])
-def test_compaction_search_modes(engine, oracle_mod, monkeypatch, mode, tile, coop, nt):
-    """Every k_compact_search mode (FDBCS_COMPACT_LANES: kArity lanes per delta boundary, one lane,
-    one lane in the long-key form) places the delta boundaries alike, and every copy tile of the
-    compaction's merge copy (FDBCS_BASE_TILE, non-temporal or not: FDBCS_COPY_NT) moves them alike, as does either segment search of
-    long-key batches (FDBCS_SEG_LONG_COOP): compactions over tails behind a 60-byte shared prefix,
-    over a tiny alphabet, and over C4 tuple keys stay verdict-exact."""
-    monkeypatch.setenv("FDBCS_COMPACT_LANES", mode)
-    monkeypatch.setenv("FDBCS_BASE_TILE", tile)
-    monkeypatch.setenv("FDBCS_SEG_LONG_COOP", coop)
-    monkeypatch.setenv("FDBCS_COPY_NT", nt)
+def test_compaction_search_modes(engine, oracle_mod, monkeypatch):
+    """Both k_compact_search modes (one lane per delta boundary: lane_lower_bound after short-key
+    batches, lane_lower_bound_long after long-key ones) place the delta boundaries alike:
+    compactions over tails behind a 60-byte shared prefix, over a tiny alphabet, and over C4 tuple
+    keys stay verdict-exact.  (The non-temporal copy of bases over 16M boundaries is covered by
+    test_async_pipeline_full_c4.)"""
     test_long_shared_prefix_tails(engine, oracle_mod, 0, 40)
     test_delta_tier_configurations(engine, oracle_mod, 0, 25)
     test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, 0, 3000, "2")
@@ -741,21 +729,14 @@ def test_empty_batches(engine, oracle_mod):
 # is parity-tested here; knobs measured slower and not kept were deleted with their code.
 @pytest.mark.parametrize("knobs", [{"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
                                    {"FDBCS_SORT_COLD": "1"},
-                                   {"FDBCS_LONG_PROBE": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_GROUP_RMAX": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_GRAPH": "2"},
-                                   {"FDBCS_GRAPH": "3"}, {"FDBCS_GRAPH": "3", "FDBCS_SPLIT_CHECK": "1"},
                                    {"FDBCS_SUBMIT_THREAD": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "0"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
-                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_CHECK": "1"}, {"FDBCS_CHECK": "6"},
-                                   {"FDBCS_SPLIT_B": "0"}, {"FDBCS_SPLIT_B": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_LONG_LANES": "0"}, {"FDBCS_LONG_LANES": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_LAG": "1", "FDBCS_SUBMIT_THREAD": "0"},
-                                   {"FDBCS_LAG": "1", "FDBCS_SUBMIT_THREAD": "0", "FDBCS_SPLIT_CHECK": "1"},
-                                   {"FDBCS_UPLOAD": "kernel"}])
+                                   {"FDBCS_DIRECTORY": "0"}, {"FDBCS_SKIP_EDGES": "0"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
-    """Non-default pipeline variants kept for measurement stay exact: the unsplit and
-    split read checks, the one-wave check, long-key sorting without LDS windows, stage graphs, the
-    helper submitting thread, one candidate edge per writer, the serial stream layout."""
+    """The engine's remaining path-selecting knobs stay exact: the unsplit and split read checks,
+    cold-start splitters on every batch, one submitting thread, one candidate edge per writer (the
+    production path past 12288 writes), the serial stream layout, base lookups without the radix
+    directory, the no-edge launches kept."""
     saved = {k: os.environ.get(k) for k in knobs}
     os.environ.update(knobs)
     try:
