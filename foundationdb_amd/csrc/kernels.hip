@@ -1538,7 +1538,7 @@ __device__ __forceinline__ uint32_t split_lcp(const SplitKey& a, const SplitKey&
 
 // Slab slots every bucket wave loads before its count arrives (the rest after it).
 #ifndef FDBCS_SPEC_SLOTS
-#define FDBCS_SPEC_SLOTS 128
+#define FDBCS_SPEC_SLOTS 80
 #endif
 constexpr int kSpecSlots = FDBCS_SPEC_SLOTS;
 
