@@ -34,7 +34,8 @@ def test_multi_rank_bench_parity(engine, world, workload, extra):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(world), "--workload", workload, "--steps", "8", "--warmup", "2", "--txns", txns,
            "--history", history, "--h2d-steps", "0", "--total-steps", "0", "--breakdown-steps", "0",
-           "--profile-steps", "4", "--sync-steps", "4", "--backend", "gloo", "--cpu-seconds", "20"] + extra
+           "--profile-steps", "4", "--sync-steps", "4", "--roof-steps", "0", "--backend", "gloo",
+           "--cpu-seconds", "20"] + extra
     env = dict(os.environ, OMP_NUM_THREADS="1" if world > 2 else "2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280 if world > 2 else 110)
     assert r.returncode == 0, "\n".join([l for l in r.stderr.splitlines() if "[rank1]" in l][-30:]) + r.stderr[-1500:]
@@ -281,7 +282,7 @@ def test_rccl_leg_one_rank(engine, workload):
            "--gpus", "1", "--dist", "--backend", "nccl", "--workload", workload, "--steps", "12", "--warmup", "2",
            "--txns", "2000", "--history", "300000", "--h2d-steps", "0", "--total-steps", "4",
            "--breakdown-steps", "2", "--profile-steps", "4", "--sync-steps", "4", "--hold-steps", "2",
-           "--too-old-frac", "0.05", "--cpu-seconds", "30"]
+           "--roof-steps", "8", "--too-old-frac", "0.05", "--cpu-seconds", "30"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
