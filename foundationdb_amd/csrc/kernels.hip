@@ -957,11 +957,9 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
     int c = conf ? 1 : 0;
     c |= __shfl_xor(c, 1, 64);
     c |= __shfl_xor(c, 2, 64);
-    // OR into the pre-zeroed flags (the epilogue that last used the workspace zeroed them): the
-    // delta tier's launch in stage B sets them too, beside this one
-    if (live && k == 0 && c) {
-        rconf[r] = 1;
-        hist_conf[b.rowner[r]] = 1;
+    if (live && k == 0) {
+        rconf[r] = (uint8_t)c;
+        if (c) hist_conf[b.rowner[r]] = 1;
     }
 }
 
