@@ -84,8 +84,6 @@ class Stats(ctypes.Structure):
         ("host_ms_record", ctypes.c_double),
         ("host_ms_submit", ctypes.c_double),
         ("compact_launches", ctypes.c_int64),
-        ("folds", ctypes.c_int64),
-        ("mid_sum", ctypes.c_int64),
         ("merge_bytes_all", ctypes.c_int64),
         ("compact_bytes_all", ctypes.c_int64),
         ("delta_sum", ctypes.c_int64),

@@ -42,6 +42,9 @@ using namespace fdbcs;
         }                                                                                             \
     } while (0)
 
+// Base-tier size from which the read check splits by default (FDBCS_SPLIT_CHECK=2).
+constexpr int64_t kSplitCheckMinBase = 16 << 20;
+
 namespace {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -222,6 +225,12 @@ struct fdbcs_conflict_set {
     hipEvent_t ev_c[kNumWork] = {}; // base-tier check of the batch using workspace k is done
     hipEvent_t ev_cmp = nullptr;    // stage B of the last batch that rewrote the base (compaction / GC)
     bool cmp_recorded = false;
+    // FDBCS_SPLIT_CHECK: 0 = one read check over both tiers in stage B, 1 = the base-tier half on
+    // its own stream beside stage A, 2 (default) = split only over a large base tier (>= 16M
+    // boundaries): there the base check is long (C4: ~150 us) and must leave the batch-order
+    // chain; over a 5M base (C2) the single launch measured faster (device-resident 34.0M vs
+    // 32.1M txns/s: one launch and two cross-stream events fewer, no third stream competing)
+    int split_check = 2;
     hipStream_t ustream = nullptr;  // batch uploads (k_upload over PCIe), so batch i+1's upload overlaps
                                     // batch i's stage A; stage A waits for the upload's event
     hipEvent_t ev_a[kNumWork] = {}; // stage A of the batch using workspace k is done
@@ -280,21 +289,7 @@ struct fdbcs_conflict_set {
     int64_t nd_ub = 0;
     int64_t dlvl3_n = 0;
     int64_t dlvl2_n = 0;
-    // mid tier (between the delta and the base): the delta is folded into it every few batches and
-    // it is compacted into the base when it outgrows delta_limit_for(); two buffer sets, one set of
-    // levels / index / epoch-tagged directory rebuilt at each fold (checks wait for the fold, as
-    // they wait for a compaction of the base)
-    DBuf mkey[2], mlt[2], mver[2];
-    DBuf mlvl[kMaxLevels];
-    DBuf medir;
-    uint32_t mdir_epoch = 0;
-    int mcur = 0;
-    int64_t mid_cap = 0;
-    int64_t nm_ub = 0;
-    int64_t mlvl3_n = 0;
-    int64_t mlvl2_n = 0;
-    DBuf cws[6];  // compaction arrays (per boundary of the overlaid tier: the delta at a fold, the mid
-                  // tier at a compaction)
+    DBuf cws[6];  // compaction arrays (per delta boundary)
     DBuf htail[2];  // tail arenas (bytes [16, len) of long keys): append-only between GCs; each GC
     int tcur = 0;   // repacks the live tails into the other one, reclaiming the rest
     int64_t tail_ub = 0;
@@ -455,7 +450,6 @@ struct fdbcs_batch {
     int32_t* h_first = nullptr;
     bool gc_ran = false;
     bool compacted = false;
-    bool folded = false;
     uint32_t seq = 0;
     volatile uint32_t* h_flag = nullptr;
     int64_t n_report = 0;  // transactions added with report_conflicting_keys (and reports enabled)
@@ -507,16 +501,15 @@ int cmp_bytes(const uint8_t* a, int32_t al, const uint8_t* b, int32_t bl) {
 int ensure_scan_arena(fdbcs_conflict_set* cs) {
     if (cs->ws_T < 0 || cs->hist_cap <= 0) return FDBCS_OK;
     if (cs->delta_cap <= 0) return FDBCS_OK;
-    const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap, cs->mid_cap);
+    const int64_t words = scan_arena_words(cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
     for (int k = 0; k < kNumWork; k++) {
         Work& w = cs->work[k];
         int rc = cs->ws[k][kWsArenaSlot].ensure(8 * words + 64);
         if (rc) return rc;
         w.scan_arena = (uint64_t*)cs->ws[k][kWsArenaSlot].p;
-        if ((rc = cs->ws[k][kWsTileSlot].ensure(4 * (std::max({cs->hist_cap, cs->delta_cap, cs->mid_cap}) / 256 + 8))))
-            return rc;
+        if ((rc = cs->ws[k][kWsTileSlot].ensure(4 * (std::max(cs->hist_cap, cs->delta_cap) / 256 + 8)))) return rc;
         w.tile_first = (int32_t*)cs->ws[k][kWsTileSlot].p;
-        carve_scans(w, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap, cs->mid_cap);
+        carve_scans(w, cs->ws_T, cs->ws_R, cs->ws_W, cs->hist_cap, cs->delta_cap);
         HIPOK(hipMemsetAsync(w.scan_arena, 0, 8 * w.scan_words, cs->stream));
         for (int q = 0; q < kNumScans; q++) w.scan[q].error = &w.bsc->debug_error;
     }
@@ -675,15 +668,6 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
 // 32768-txn batches 91.1 -> 92.9M over 150-400-batch windows with a 1.25M bound
 // (scripts/gpu_r05_dl*.sh); a 50M base (C4) keeps N/16 = 3.1M.
 constexpr int64_t kDeltaFloor = 1250000;
-int64_t delta_limit_for(const fdbcs_conflict_set* cs, int64_t n_base);
-// The delta's bound before it is folded into the mid tier: N/32 within [64K, 256K] boundaries
-// (C2: ~156K, a fold every ~8 batches; C4: 256K), at most a quarter of the mid tier's bound.  The
-// delta is what every batch's merge rewrites and every epilogue re-indexes, so it stays small;
-// the mid tier absorbs it every few batches and is compacted into the base rarely.
-int64_t fold_limit_for(const fdbcs_conflict_set* cs, int64_t n_base) {
-    const int64_t auto_l = std::max<int64_t>(1 << 16, std::min<int64_t>(n_base / 32, 1 << 18));
-    return std::max<int64_t>(1, std::min(auto_l, delta_limit_for(cs, n_base) / 4));
-}
 constexpr int kTimingEvery = 4;  // timing level 1 times the hot kernels of 1 batch in kTimingEvery
 int64_t delta_limit_for(const fdbcs_conflict_set* cs, int64_t n_base) {
     if (cs->delta_limit > 0) return cs->delta_limit;
@@ -837,26 +821,6 @@ MaxLevels dlevels_of(fdbcs_conflict_set* cs, int k) {
     return m;
 }
 
-Hist mid_of(fdbcs_conflict_set* cs, int k) {
-    Hist h;
-    h.key = (ulonglong2*)cs->mkey[k].p;
-    h.lt = (uint2*)cs->mlt[k].p;
-    h.ver = (int64_t*)cs->mver[k].p;
-    return h;
-}
-
-MaxLevels mlevels_of(fdbcs_conflict_set* cs, int k) {
-    MaxLevels m;
-    m.lvl[0] = (int64_t*)cs->mver[k].p;
-    for (int L = 1; L < kMaxLevels; L++) m.lvl[L] = (int64_t*)cs->mlvl[L].p;
-    m.keys = (const ulonglong2*)cs->mkey[k].p;
-    carve_index(m, (ulonglong2*)cs->mlvl[0].p, cs->mid_cap);
-    m.edir = (uint64_t*)cs->medir.p;
-    m.edir_epoch = cs->medir.p ? cs->mdir_epoch : 0;
-    set_dir_fields(cs, m);
-    return m;
-}
-
 // Read the exact history size/tail usage back (synchronizes the stream).
 int sync_sizes(fdbcs_conflict_set* cs) {
     if (int rc = sync_all(cs)) return rc;  // both halves of stage B
@@ -865,7 +829,6 @@ int sync_sizes(fdbcs_conflict_set* cs) {
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->n_ub = s.n;
     cs->nd_ub = s.nd;
-    cs->nm_ub = s.nm;
     cs->tail_ub = s.tail_used;
     return FDBCS_OK;
 }
@@ -908,45 +871,7 @@ int grow_sets(fdbcs_conflict_set* cs, DBuf* key, DBuf* lt, DBuf* ver, int live, 
     return FDBCS_OK;
 }
 
-// The overlay arrays (launch_compact) for an overlaid tier of up to `cap` boundaries.
-int ensure_cws(fdbcs_conflict_set* cs, int64_t cap) {
-    if (cs->cws[5].p && cs->cws[5].cap >= (size_t)(cap + 2)) return FDBCS_OK;
-    int rc;
-    for (int k = 0; k < 5; k++) {
-        cs->cws[k].release();
-        if ((rc = cs->cws[k].ensure(8 * (cap + 2)))) return rc;
-    }
-    cs->cws[5].release();
-    if ((rc = cs->cws[5].ensure(cap + 2))) return rc;
-    for (Work& w : cs->work) {  // overlays run on stage B only: every workspace shares the arrays
-        int64_t** c64[5] = {&w.c_lo, &w.c_hi, &w.c_rem, &w.c_ins, &w.c_val};
-        for (int k = 0; k < 5; k++) *c64[k] = (int64_t*)cs->cws[k].p;
-        w.c_exact = (uint8_t*)cs->cws[5].p;
-    }
-    return FDBCS_OK;
-}
-
-// Mid-tier capacity for `need` boundaries (sizes synchronized first: every stream drained).
-int ensure_mid(fdbcs_conflict_set* cs, int64_t need) {
-    if (need <= cs->mid_cap) return FDBCS_OK;
-    int rc = sync_sizes(cs);
-    if (rc) return rc;
-    int64_t cap = std::max<int64_t>(need, cs->mid_cap);
-    cap = std::max<int64_t>(cap + cap / 2, 1 << 14);
-    if ((rc = grow_sets(cs, cs->mkey, cs->mlt, cs->mver, cs->mcur, cs->nm_ub, cap))) return rc;
-    if ((rc = ensure_cws(cs, std::max(cap, cs->delta_cap)))) return rc;
-    if ((rc = alloc_levels(cs->mlvl, cap, &cs->mlvl3_n, &cs->mlvl2_n))) return rc;
-    cs->mid_cap = cap;
-    cs->mdir_epoch = 0;  // the levels are rebuilt below, the directory not
-    cs->prev_segs = false;
-    launch_rangemax(cs->stream, mlevels_of(cs, cs->mcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->nm,
-                    cs->mlvl3_n, cs->mlvl2_n, std::max<int64_t>(cs->nm_ub, 1));
-    HIPOK(take_launch_error());
-    HIPOK(hipStreamSynchronize(cs->stream));
-    return ensure_scan_arena(cs);
-}
-
-// Delta-tier capacity for `need` boundaries (plus the overlay arrays sized to match).
+// Delta-tier capacity for `need` boundaries (plus the compaction arrays sized to match).
 int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
     if (need <= cs->delta_cap) return FDBCS_OK;
     int rc = sync_sizes(cs);
@@ -954,7 +879,17 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
     int64_t cap = std::max<int64_t>(need, cs->delta_cap);
     cap = std::max<int64_t>(cap + cap / 2, 1 << 14);
     if ((rc = grow_sets(cs, cs->dkey, cs->dlt, cs->dver, cs->dcur, cs->nd_ub, cap))) return rc;
-    if ((rc = ensure_cws(cs, std::max(cap, cs->mid_cap)))) return rc;
+    for (int k = 0; k < 5; k++) {
+        cs->cws[k].release();
+        if ((rc = cs->cws[k].ensure(8 * (cap + 2)))) return rc;
+    }
+    cs->cws[5].release();
+    if ((rc = cs->cws[5].ensure(cap + 2))) return rc;
+    for (Work& w : cs->work) {  // compaction runs on stage B only: both workspaces share the arrays
+        int64_t** c64[5] = {&w.c_lo, &w.c_hi, &w.c_rem, &w.c_ins, &w.c_val};
+        for (int k = 0; k < 5; k++) *c64[k] = (int64_t*)cs->cws[k].p;
+        w.c_exact = (uint8_t*)cs->cws[5].p;
+    }
     for (int k = 0; k < 2; k++)
         if ((rc = alloc_levels(cs->dlvl[k], cap, &cs->dlvl3_n, &cs->dlvl2_n))) return rc;
     cs->delta_cap = cap;
@@ -1335,6 +1270,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
         cs->htr[0].reserve(1 << 16);
         cs->htr[1].reserve(1 << 16);
     }
+    if (const char* v = getenv("FDBCS_SPLIT_CHECK")) cs->split_check = atoi(v);
     if (const char* v = getenv("FDBCS_WRITE_GROUPS")) cs->write_groups = v[0] != '0';
     if (const char* v = getenv("FDBCS_DIRECTORY")) cs->directory = v[0] != '0';
     if (const char* v = getenv("FDBCS_DIR_BITS")) cs->dir_bits = std::max(0, std::min(kDirMaxBits, atoi(v)));
@@ -1362,15 +1298,14 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = cs->quant.ensure(2 * sizeof(SplitKey) * kQuant);
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
-    for (int k = 0; k < 3 && !rc && cs->directory; k++) {  // zeroed: epoch 0 entries are never trusted
-        DBuf& e = k < 2 ? cs->edir[k] : cs->medir;
-        rc = e.ensure(8 * (size_t)kDirAlloc);
-        if (!rc && hipMemsetAsync(e.p, 0, 8 * (size_t)kDirAlloc, cs->stream) != hipSuccess) rc = FDBCS_E_DEVICE;
+    for (int k = 0; k < 2 && !rc && cs->directory; k++) {  // zeroed: epoch 0 entries are never trusted
+        rc = cs->edir[k].ensure(8 * (size_t)kDirAlloc);
+        if (!rc && hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream) != hipSuccess)
+            rc = FDBCS_E_DEVICE;
     }
     if (!rc) rc = set_dir_map(cs, nullptr, 0);
     if (!rc) rc = ensure_history(cs, 1 << 16, 1 << 16);
     if (!rc) rc = ensure_delta(cs, 1 << 14);
-    if (!rc) rc = ensure_mid(cs, 1 << 14);
     if (!rc) rc = ensure_workspace(cs, 1024, 4096, 4096);
     if (!rc) rc = ensure_btail(cs, 0);
     if (!rc && cs->trace) rc = cs->trace_buf.ensure(8 * kTrSlots);
@@ -1421,17 +1356,12 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         cs->dkey[k].release();
         cs->dlt[k].release();
         cs->dver[k].release();
-        cs->mkey[k].release();
-        cs->mlt[k].release();
-        cs->mver[k].release();
     }
     cs->htail[0].release();
     cs->htail[1].release();
     for (auto& l : cs->lvl) l.release();
     cs->dir.release();
     for (auto& e : cs->edir) e.release();
-    cs->medir.release();
-    for (auto& l : cs->mlvl) l.release();
     for (auto& set : cs->dlvl)
         for (auto& l : set) l.release();
     for (auto& x : cs->cws) x.release();
@@ -1475,12 +1405,10 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     cs->header_version = version;
     cs->max_written = version;
     cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;
-    cs->mdir_epoch = 0;
     if (int rc = set_dir_map(cs, nullptr, 0)) return rc;
     cs->prev_segs = false;
     cs->n_ub = 0;
     cs->nd_ub = 0;
-    cs->nm_ub = 0;
     cs->tail_ub = 0;
     return FDBCS_OK;
 }
@@ -1505,8 +1433,7 @@ int fdbcs_reserve(fdbcs_conflict_set* cs, int64_t boundaries, int64_t tail_bytes
     int rc = ensure_workspace(cs, max_txns, max_reads, max_writes);
     if (rc) return rc;
     const int64_t dneed = delta_limit_for(cs, boundaries) + 2 * (int64_t)max_writes + 2;
-    if ((rc = ensure_delta(cs, fold_limit_for(cs, boundaries) + 2 * (int64_t)max_writes + 2))) return rc;
-    if ((rc = ensure_mid(cs, dneed))) return rc;
+    if ((rc = ensure_delta(cs, dneed))) return rc;
     return ensure_history(cs, std::max<int64_t>(boundaries + dneed, cs->hist_cap),
                           std::max<int64_t>(tail_bytes, cs->tail_cap));
 }
@@ -1534,7 +1461,7 @@ int fdbcs_history_size(fdbcs_conflict_set* cs, int64_t* out) {
     HIPOK(hipSetDevice(cs->device));
     int rc = sync_sizes(cs);
     if (rc) return rc;
-    *out = cs->n_ub + cs->nm_ub + cs->nd_ub;
+    *out = cs->n_ub + cs->nd_ub;
     return FDBCS_OK;
 }
 
@@ -1591,11 +1518,9 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     cs->header_version = header_version;
     cs->max_written = maxv;
     cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;  // no delta directory entry of the old slot mapping is trusted
-    cs->mdir_epoch = 0;
     cs->prev_segs = false;
     cs->n_ub = n;
     cs->nd_ub = 0;
-    cs->nm_ub = 0;
     cs->tail_ub = (int64_t)tail.size();
     return FDBCS_OK;
 }
@@ -2377,8 +2302,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     if ((rc = ensure_workspace(cs, T, R, W))) return rc;
     if ((rc = ensure_btail(cs, (int64_t)b->tail_size()))) return rc;
     if ((rc = ensure_delta(cs, cs->nd_ub + 2 * W + 1))) return rc;
-    if ((rc = ensure_mid(cs, cs->nm_ub + cs->nd_ub + 2 * W + 1))) return rc;
-    if ((rc = ensure_history(cs, cs->n_ub + cs->nm_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + tail_add + 1)))
+    if ((rc = ensure_history(cs, cs->n_ub + cs->nd_ub + 2 * W + 1, cs->tail_ub + tail_add + 1)))
         return rc;
     if ((rc = ensure_events(b))) return rc;
     if (cs->ddir_counter == UINT32_MAX && cs->edir[0].p) {
@@ -2386,8 +2310,6 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // batches) so that no entry left by an old fill can carry the reused epoch value
         if ((rc = sync_all(cs))) return rc;
         for (int k = 0; k < 2; k++) HIPOK(hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream));
-        HIPOK(hipMemsetAsync(cs->medir.p, 0, 8 * (size_t)kDirAlloc, cs->stream));
-        cs->mdir_epoch = 0;
         HIPOK(hipStreamSynchronize(cs->stream));
         cs->ddir_counter = 0;
     }
@@ -2468,11 +2390,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         L->prof = kprof ? &sl->prof : nullptr;
         L->timed_func = timing == 3 ? nullptr : cs->timed_func;
     }
-    // Split read check: the base and mid tiers change only at compactions and folds, so unless one
-    // is still pending on the stream their lookups run beside stage A on their own stream (one
-    // launch, four lanes per read); stage B's X half checks the small delta tier and the previous
-    // batch's union segments.  (One stream for everything when the phases are timed serially.)
-    const bool split = !cs->serial && timing != 2;
+    // Split read check: the base tier changes only at compactions, so unless one is still pending
+    // on the stream its half of D.CheckRead runs beside stage A on its own stream; stage B keeps the
+    // delta half.
+    const bool split = (cs->split_check == 1 || (cs->split_check == 2 && cs->n_ub >= kSplitCheckMinBase)) &&
+                       !cs->serial && timing != 2;
     // two submitting threads: this batch's stage A and check go out from the helper, stage B on the
     // next call.  The previous batch's stage B is recorded but maybe not issued yet, so an event it
     // records cannot be queried here: waits on its events are kept unconditionally.
@@ -2524,8 +2446,6 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->ndb[dsrc], kHole};
     const Tier cdelta{delta_of(cs, dchk), dlevels_of(cs, dchk), &sc->ndb[dchk], kHole};  // what the check reads
-    const int msrc = cs->mcur;
-    const Tier mid{mid_of(cs, msrc), mlevels_of(cs, msrc), &sc->nm, kHole};
     PrevSegs ps{};
     if (use_prev) {
         const Work& pw = cs->work[cs->prev_wp];
@@ -2580,8 +2500,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     launch_edges(sa, bd, w);
     if (sa != s) fdb_event(LaunchList::kSyncRecord, cs->ev_a[wp], sa);
     mark(kPhEdges);
-    b->check_hist = cs->n_ub + cs->nm_ub;  // the timed (base + mid) check
-    if (split) {  // ---- record the base + mid check (its own stream)
+    if (split) {  // ---- record the base-tier check (its own stream)
         t_record = &lc;
         hipStream_t sc_ = cs->cstream;
         fdb_event(LaunchList::kSyncWait, sl->ev_up, sc_);
@@ -2589,7 +2508,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (cs->cmp_recorded && (threaded || hipEventQuery(cs->ev_cmp) != hipSuccess))
             fdb_event(LaunchList::kSyncWait, cs->ev_cmp, sc_);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), sc_);
-        launch_check(sc_, bd, w, base, mid, htail, long_keys, PrevSegs{});
+        launch_check_tier(sc_, bd, w, base, true, htail, long_keys, PrevSegs{});
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), sc_);
         fdb_event(LaunchList::kSyncRecord, cs->ev_c[wp], sc_);
     }
@@ -2604,12 +2523,15 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         if (wy >= 0 && cs->y_async[wy] && (threaded || !stage_b_done(cs, wy)))
             fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
     }
-    if (!split) {
+    if (split) {
+        b->check_hist = cs->n_ub;  // the timed (base-tier) check
+        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, ps);
+    } else {
+        b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-        launch_check(s, bd, w, base, mid, htail, long_keys, PrevSegs{});
+        launch_check(s, bd, w, base, cdelta, htail, long_keys, ps);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
-    launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, ps);
     if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
         cs->xfree_ev[cs->prev_wp] = cs->ev_res[wp];  // recorded at the end of this half X
         cs->xfree_user[cs->prev_wp] = b;
@@ -2636,19 +2558,14 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     fdb_event(LaunchList::kSyncRecord, cs->ev_res[wp], s);
     t_record = &ly;
     if (ys != s) fdb_event(LaunchList::kSyncWait, cs->ev_res[wp], ys);
-    const int dnew = dsrc ^ 1, mnew = msrc ^ 1;
+    const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
-    const int64_t nm_after = cs->nm_ub + nd_after;  // the mid tier's bound after a fold
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
-    // Three tiers: every batch merges into the small delta; the delta is folded into
-    // the mid tier once it may outgrow fold_limit_for(); the mid tier is compacted into the base
-    // once it may outgrow delta_limit_for() (or on the forced cadence, or to reclaim tails), the
-    // delta folded first, so that removeBefore (SkipList.cpp:880-889), which runs with a compaction
-    // whenever the oldest version moved and repacks the tails, finds every boundary in the base.
-    bool compact = nm_after > delta_limit_for(cs, cs->n_ub);
+    // Compaction when the delta may outgrow its bound (or on the forced cadence); removeBefore
+    // (SkipList.cpp:880-889) runs with it whenever the oldest version moved.
+    bool compact = nd_after > delta_limit_for(cs, cs->n_ub);
     if (cs->gc_interval > 0 && ++cs->batches_since_compact >= cs->gc_interval) compact = true;
     if (cs->tail_ub > cs->tail_reclaim) compact = true;
-    const bool fold = compact || nd_after > fold_limit_for(cs, cs->n_ub);
     // D.MergeWrite into the delta tier
     char* hd = (char*)sl->pin_out.dp;
     launch_merge(ys, bd, w, delta.h, delta.m, delta_of(cs, dnew), dlevels_of(cs, dnew), &sc->ndb[dsrc], htail, sc, now,
@@ -2656,22 +2573,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhMerge);
     bool gc = false;
     int final_base = bsrc;
-    const int64_t base_hint = cs->n_ub + nm_after + 1;
-    if (fold) {  // the delta (after this batch's merge) overlaid onto the mid tier: mid[msrc] -> mid[mnew]
-        const CompactIO fio{&sc->nm, &sc->nm_next, &sc->m_before, &sc->m_rem, &sc->nd_next, kHole, kScanFold};
-        launch_compact(ys, w, mid.h, mid.m, delta_of(cs, dnew), mid_of(cs, mnew), htail, fio, cs->mlvl3_n, cs->mlvl2_n,
-                       nd_after + 1, cs->nm_ub + 1, nullptr, nullptr, long_keys ? 2 : 1, 1024, false);
-        if (!compact) {  // its levels, index and directory (a compaction below empties it instead)
-            cs->mdir_epoch = cs->medir.p ? ++cs->ddir_counter : 0;
-            launch_levels(ys, mlevels_of(cs, mnew), sc, &sc->nm_next, nm_after + 1);
-        }
-    }
-    if (compact) {  // the mid tier (every boundary above the base now) overlaid onto the base
-        const CompactIO cio{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem, &sc->nm_next, cs->header_version,
-                            kScanCompact};
-        launch_compact(ys, w, base.h, base.m, mid_of(cs, mnew), hist_of(cs, bsrc ^ 1), htail, cio, cs->lvl3_n,
-                       cs->lvl2_n, nm_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1), rec(kPhCompEnd, 1),
-                       long_keys ? 2 : 1, cs->n_ub <= (16 << 20) ? 1024 : 4096, cs->n_ub > (16 << 20));
+    const int64_t base_hint = cs->n_ub + nd_after + 1;
+    if (compact) {
+        launch_compact(ys, w, base.h, base.m, delta_of(cs, dnew), hist_of(cs, bsrc ^ 1), htail, sc,
+                       cs->header_version, cs->lvl3_n, cs->lvl2_n, nd_after + 1, cs->n_ub + 1, rec(kPhCompBegin, 1),
+                       rec(kPhCompEnd, 1), long_keys ? 2 : 1, cs->n_ub <= (16 << 20) ? 1024 : 4096,
+                       cs->n_ub > (16 << 20));
         final_base = bsrc ^ 1;
         cs->batches_since_compact = 0;
         // Size-triggered compactions (gc_interval 0) run removeBefore on every kGcEveryCompactions-th
@@ -2696,23 +2603,22 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     mark(kPhGc);
     b->gc_ran = gc;
     b->compacted = compact;
-    b->folded = fold;
     // the epilogue that rebuilds the delta tier's index also fills its directory under a new epoch
     // (a compaction leaves none).  The epoch tag is 32 bits: before it wraps, every entry is
     // cleared (ensure_delta_directory), so a slot an old fill left behind is never trusted.
-    if (fold || !cs->edir[dnew].p) {
+    if (compact || !cs->edir[dnew].p) {
         cs->ddir_epoch[dnew] = 0;
     } else {
         cs->ddir_epoch[dnew] = ++cs->ddir_counter;
     }
     launch_epilogue(ys, bd, w, compact ? levels_of(cs, final_base) : dlevels_of(cs, dnew), sc, compact ? 1 : 0,
-                    fold ? 1 : 0, gc ? 1 : 0, (uint8_t*)hd, (uint32_t*)(hd + o_fl), b->seq,
+                    gc ? 1 : 0, (uint8_t*)hd, (uint32_t*)(hd + o_fl), b->seq,
                     compact ? base_hint : nd_after + 1, &sc->ndb[dnew], sort_nb, sort_samples);
     fdb_event(LaunchList::kSyncRecord, cs->ev_b[wp], ys);
     // (no event marks the slot free: a slot returns to the pool only from fdbcs_batch_destroy,
     // after the batch's completion flag was seen or its streams were synchronized; every kernel
     // of the batch that reads or writes the slot precedes the epilogue, which touches none of it)
-    if (compact || gc || fold) {  // later base + mid checks wait for this rewrite of the base or mid tier
+    if (compact || gc) {  // later base-tier checks wait for this rewrite of the base
         fdb_event(LaunchList::kSyncRecord, cs->ev_cmp, ys);
         cs->cmp_recorded = true;
     }
@@ -2773,8 +2679,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->stats.host_ms_submit += host_ms_since(t_sub);
     cs->cur = final_base;
     cs->dcur = dnew;
-    // the next batch's check: this batch's segments stand in for its merge unless it folded
-    cs->prev_segs = pipe && !fold;
+    // the next batch's check: this batch's segments stand in for its merge unless it compacted
+    cs->prev_segs = pipe && !compact;
     cs->prev2_wp = cs->last_wp;
     cs->last_wp = wp;
     cs->y_async[wp] = ys != s;
@@ -2783,16 +2689,11 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
     if (W) cs->max_written = std::max(cs->max_written, now);
     if (compact) {
-        cs->n_ub += nm_after;
-        cs->nm_ub = 0;
-        cs->nd_ub = 0;
-    } else if (fold) {
-        cs->nm_ub = nm_after;
+        cs->n_ub += nd_after;
         cs->nd_ub = 0;
     } else {
         cs->nd_ub = nd_after;
     }
-    if (fold) cs->mcur = mnew;
     cs->tail_ub += tail_add;
     cs->inflight++;
     b->state = 2;
@@ -2971,7 +2872,6 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             st.merge_bytes_all += bytes;
             st.delta_sum += b->h_scal->d_before;
             st.base_sum += b->h_scal->n;
-            st.mid_sum += b->h_scal->nm;
             st.segments_sum += b->h_scal->n_segments;
             if ((b->recorded >> kPhCopyEnd) & 1u) {
                 st.ms_merge_kernel += ph(kPhCopyBegin, kPhCopyEnd);
@@ -3011,11 +2911,9 @@ int fdbcs_batch_wait(fdbcs_batch* b, uint8_t* verdicts, int32_t* n_committed, in
             }
         }
         cs->inflight--;
-        st.folds += b->folded ? 1 : 0;
         if (cs->inflight == 0) {
             cs->n_ub = b->h_scal->n;
             cs->nd_ub = b->h_scal->nd;
-            cs->nm_ub = b->h_scal->nm;
             cs->tail_ub = b->h_scal->tail_used;
         }
         b->state = 3;
@@ -3097,7 +2995,6 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     Scalars* sc = (Scalars*)cs->scal.p;
     const Tier base{hist_of(cs, cs->cur), levels_of(cs, cs->cur), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, cs->dcur), dlevels_of(cs, cs->dcur), &sc->ndb[cs->dcur], kHole};
-    const Tier mid{mid_of(cs, cs->mcur), mlevels_of(cs, cs->mcur), &sc->nm, kHole};
     if (which == 1 || which == 2) {  // the sort kernels
         if (!cs->quant_valid) return FDBCS_E_STATE;  // warm splitters only: detect a batch first
         HIPOK(debug_time_sort(cs->stream, b->bd, w, (SplitKey*)cs->quant.p + cs->qcur * kQuant, cs->bucket_target,
@@ -3108,11 +3005,13 @@ int fdbcs_debug_kernel_time(fdbcs_batch* b, int which, int reps, double* us_per_
     HIPOK(hipEventCreate(&e0));
     HIPOK(hipEventCreate(&e1));
     const bool dlong = b->max_len > 24;
-    // 0: the whole check (both launches); 3: the base + mid launch alone; 4: the delta launch alone
+    // 0: the whole check; 3 / 4: the split check's base / delta tier launch alone
     auto one = [&]() {
         uint8_t* ht = (uint8_t*)cs->htail[cs->tcur].p;
-        if (which != 4) launch_check(cs->stream, b->bd, w, base, mid, ht, dlong);
-        if (which != 3) launch_check_tier(cs->stream, b->bd, w, delta, false, ht, dlong, PrevSegs{});
+        if (which == 0)
+            launch_check(cs->stream, b->bd, w, base, delta, ht, dlong);
+        else
+            launch_check_tier(cs->stream, b->bd, w, which == 3 ? base : delta, which == 3, ht, dlong, PrevSegs{});
     };
     one();
     HIPOK(hipEventRecord(e0, cs->stream));

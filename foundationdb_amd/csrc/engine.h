@@ -432,27 +432,11 @@ void launch_merge(hipStream_t s, const BatchDev& b, const Work& w, const Hist& s
                   const Hist& dst, const MaxLevels& dstm, const int64_t* nd_src, uint8_t* htail, Scalars* sc,
                   int64_t now, int64_t lvl3_n, int64_t lvl2_n, int64_t grid_hint_n, hipEvent_t copy_begin,
                   hipEvent_t copy_end, bool long_keys = false);
-// Sizes of one overlay of a tier onto the tier below it (launch_compact): the delta folded into
-// the mid tier, or the mid tier compacted into the base.
-struct CompactIO {
-    const int64_t* n_base;  // the lower tier's size (base: Scalars::n; mid: Scalars::nm)
-    int64_t* n_out;         // its size after the overlay
-    int64_t* before;        // stats: the lower tier's size before, boundaries it lost
-    int64_t* removed;
-    const int64_t* nd;      // the overlaid tier's size
-    int64_t hdr;            // the lower tier's version below its first boundary (kHole for the mid tier)
-    int scan;               // ScanKind of the overlay's look-back scan
-};
-// Overlay the upper tier `delta` onto the lower tier `base` (src -> dst); the upper tier becomes
-// empty.  basem: the lower tier's levels (its key index is searched, its top two levels reset for
-// the epilogue that rebuilds them).
+// Overlay the delta tier onto the base tier (src -> dst); the delta becomes empty.
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
-                    const Hist& dst, const uint8_t* htail, const CompactIO& io, int64_t lvl3_n,
+                    const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
                     hipEvent_t copy_end, int mode, int base_tile, bool nt);
-// Range-max levels, key index and (epoch-tagged) directory of a tier of *n boundaries, without the
-// epilogue's scalars and flag (the mid tier after a fold).
-void launch_levels(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t grid_hint_n);
 // removeBefore over the whole base (src -> dst); the live tails are repacked from arena tsrc into
 // the empty arena tdst (reclaiming the bytes of removed and overwritten boundaries).
 void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, const uint8_t* tsrc, uint8_t* tdst,
@@ -466,8 +450,8 @@ void launch_copy_bytes(hipStream_t s, void* dst, const void* src, int64_t n);
 // Multi-resolver conflict bytes out[g] = 2 - verdict of batch transaction inv[g] (0 if inv[g] < 0).
 void launch_conflict_output(hipStream_t s, const BatchDev& b, const Work& w, const int32_t* inv, int64_t n,
                             uint8_t* out);
-int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap, int64_t mid_cap);
-void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap, int64_t mid_cap);
+int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
+void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap);
 // Range-max levels of a tier whose size is *n (lvl[2] and lvl[3] reset first).
 void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t lvl3_n,
                      int64_t lvl2_n, int64_t grid_hint_n);
@@ -479,7 +463,7 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 // sort_nb / sort_samples: the batch's sort buckets and cold-start samples (their counters and
 // ranks are re-zeroed; 0 samples on a warm start).
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
-                     int compacted, int folded, int gc_ran, uint8_t* verdict_out, uint32_t* flag,
+                     int compacted, int gc_ran, uint8_t* verdict_out, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n, int64_t* nd_out, int sort_nb, int sort_samples);
 // Cold-start samples of a sort over E endpoints in nb buckets (k_sample; ranks re-zeroed by the epilogue).
 int sort_cold_samples(int64_t E, int nb);

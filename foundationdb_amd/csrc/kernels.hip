@@ -3044,7 +3044,6 @@ struct Epilogue {
     unsigned long long* trace;
     int32_t T;
     int compacted, gc_ran;
-    int folded;  // the delta was folded into the mid tier (it leaves empty; compacted implies folded)
     // Scratch the next batch on this workspace expects zeroed: exactly what this batch dirtied
     // (everything else is still zero from the allocation or an earlier epilogue), not the
     // workspace's capacity.
@@ -3419,8 +3418,8 @@ static unsigned copy_tiles(int64_t grid_hint_n, int tile, int64_t max_inserts = 
     return (unsigned)tiles;
 }
 
-static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, int folded, int gc_ran,
-                              uint8_t* verdict_out, uint32_t* flag, uint32_t seq, int sort_nb, int sort_samples) {
+static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, int gc_ran, uint8_t* verdict_out,
+                              uint32_t* flag, uint32_t seq, int sort_nb, int sort_samples) {
     Epilogue ep{};
     ep.flag = flag;
     ep.seq = seq;
@@ -3428,7 +3427,6 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
     ep.verdict_out = verdict_out;
     ep.T = b.T;
     ep.compacted = compacted;
-    ep.folded = folded;
     ep.gc_ran = gc_ran;
     ep.zero8 = w.hist_conf;
     ep.zero8_n = b.T;
@@ -3441,8 +3439,7 @@ static Epilogue make_epilogue(const BatchDev& b, const Work& w, int compacted, i
     const int64_t used[kNumScans] = {scan_granules(G, 3, kEdgeScanP), 3 * seg_prep_tiles(b.W),
                                      compacted ? w.scan_gran[kScanCompact] : 0, gc_ran ? w.scan_gran[kScanGc] : 0,
                                      scan_granules(2 * (int64_t)b.W, 1, kCombineP),
-                                     scan_granules(2 * (int64_t)b.W, 1, kCombineP),
-                                     folded ? w.scan_gran[kScanFold] : 0};
+                                     scan_granules(2 * (int64_t)b.W, 1, kCombineP)};
     ep.zero64[0] = w.scan_arena;
     ep.zero64_n[0] = kNumScans;
     for (int k = 0; k < kNumScans; k++) {
@@ -3576,29 +3573,29 @@ struct CompactIns {
 };
 
 void launch_compact(hipStream_t s, const Work& w, const Hist& base, const MaxLevels& basem, const Hist& delta,
-                    const Hist& dst, const uint8_t* htail, const CompactIO& cio, int64_t lvl3_n,
+                    const Hist& dst, const uint8_t* htail, Scalars* sc, int64_t header_version, int64_t lvl3_n,
                     int64_t lvl2_n, int64_t delta_hint_n, int64_t grid_hint_n, hipEvent_t copy_begin,
                     hipEvent_t copy_end, int mode, int base_tile, bool nt) {
     int64_t blocks = (delta_hint_n + kBlock - 1) / kBlock;
     if (blocks < 1) blocks = 1;
     if (mode == 1)
         fdb_launch(k_compact_search<1>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
-                   cio.n_base, cio.nd, cio.hdr, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
+                   &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
     else
         fdb_launch(k_compact_search<2>, dim3((unsigned)blocks), dim3(kBlock), 0, s, base, basem, delta, htail,
-                   cio.n_base, cio.nd, cio.hdr, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
+                   &sc->n, &sc->nd_next, header_version, w, basem.lvl[3], lvl3_n, basem.lvl[2], lvl2_n);
     const Segs g{w.c_lo, w.c_hi, w.c_rem, w.c_ins, w.tile_first};
-    const TierIO io{cio.n_base, cio.n_out, cio.before, cio.removed};
+    const TierIO io{&sc->n, &sc->n_next, &sc->c_before, &sc->c_rem};
     const int tile = base_tile == 1024 || base_tile == 2048 ? base_tile : kBaseTile;
-    launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, cio.nd, tile}, cio.nd, delta_hint_n + 1,
-                   w.scan[cio.scan]);
+    launch_scan<2>(s, CompactSumScan{g, delta.ver, w.c_exact, io, &sc->nd_next, tile}, &sc->nd_next,
+                   delta_hint_n + 1, w.scan[kScanCompact]);
     fdb_event(LaunchList::kTimingRecord, copy_begin, s);
     const dim3 grid(copy_tiles(grid_hint_n, tile, delta_hint_n + 1));
     const CompactIns ins{delta, w.c_val, w.c_ins};
     auto k = tile == 1024 ? (nt ? k_merge_copy<CompactIns, 1024, true> : k_merge_copy<CompactIns, 1024>)
              : tile == 2048 ? (nt ? k_merge_copy<CompactIns, 2048, true> : k_merge_copy<CompactIns, 2048>)
                             : (nt ? k_merge_copy<CompactIns, kBaseTile, true> : k_merge_copy<CompactIns, kBaseTile>);
-    fdb_launch(k, grid, dim3(kBlock), 0, s, g, base, dst, cio.n_base, cio.nd, ins);
+    fdb_launch(k, grid, dim3(kBlock), 0, s, g, base, dst, &sc->n, &sc->nd_next, ins);
     fdb_event(LaunchList::kTimingRecord, copy_end, s);
 }
 
@@ -3650,21 +3647,22 @@ void launch_gc(hipStream_t s, const Work& w, const Hist& src, const Hist& dst, c
                    w.scan[kScanGc]);
 }
 
-int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap, int64_t mid_cap) {
+int64_t scan_arena_words(int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
-    return kNumScans + scan_granules(R + W, 3, kEdgeScanP) + 3 * seg_prep_tiles(W) +
-           scan_granules(std::max(delta_cap, mid_cap) + 1, 2) + scan_granules(hist_cap, 2) +
-           2 * scan_granules(2 * W, 1, kCombineP) + scan_granules(delta_cap + 1, 2);
+    const int64_t E = 2 * (R + W);
+    (void)E;
+    return kNumScans + scan_granules(R + W, 3, kEdgeScanP) + 3 * seg_prep_tiles(W) + scan_granules(delta_cap + 1, 2) +
+           scan_granules(hist_cap, 2) + 2 * scan_granules(2 * W, 1, kCombineP);
 }
 
-void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap, int64_t mid_cap) {
+void carve_scans(Work& w, int64_t T, int64_t R, int64_t W, int64_t hist_cap, int64_t delta_cap) {
     (void)T;
+    const int64_t E = 2 * (R + W);
     uint64_t* a = w.scan_arena;
-    // compaction: over the mid tier's boundaries; fold: over the delta's
+    (void)E;
     const int64_t gran[kNumScans] = {scan_granules(R + W, 3, kEdgeScanP), 3 * seg_prep_tiles(W),
-                                     scan_granules(std::max(delta_cap, mid_cap) + 1, 2), scan_granules(hist_cap, 2),
-                                     scan_granules(2 * W, 1, kCombineP), scan_granules(2 * W, 1, kCombineP),
-                                     scan_granules(delta_cap + 1, 2)};
+                                     scan_granules(delta_cap + 1, 2), scan_granules(hist_cap, 2),
+                                     scan_granules(2 * W, 1, kCombineP), scan_granules(2 * W, 1, kCombineP)};
     uint64_t* g = a + kNumScans;
     for (int k = 0; k < kNumScans; k++) {
         w.scan[k].counter = (int*)(a + k);
@@ -3972,7 +3970,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
     else if (ep.compacted)
         n0 = ep.gc_ran ? sc->n_gc : sc->n_next;
     else
-        n0 = ep.folded ? 0 : sc->nd_next;  // a folded delta leaves empty: no levels to build
+        n0 = sc->nd_next;
     const int64_t n1 = (n0 + kFan - 1) / kFan, nwv = (n1 + kEpiBlocks - 1) / kEpiBlocks;
     for (int64_t wv = (int64_t)blockIdx.x * kEpiWaves + wid; wv < nwv; wv += (int64_t)gridDim.x * kEpiWaves) {
         // the wave's kEpiBlocks blocks of 64 versions: all loads first, then the reductions
@@ -4095,8 +4093,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         auto bs32 = [&](size_t off) -> uint32_t { return (uint32_t)(bsw(off) >> (8 * (off % 8))); };
         const int64_t n_new = !ep.compacted ? scw(offsetof(Scalars, n))
                                             : (ep.gc_ran ? scw(offsetof(Scalars, n_gc)) : scw(offsetof(Scalars, n_next)));
-        const int64_t nd_new = ep.compacted || ep.folded ? 0 : scw(offsetof(Scalars, nd_next));
-        const int64_t nm_new = ep.compacted ? 0 : (ep.folded ? scw(offsetof(Scalars, nm_next)) : scw(offsetof(Scalars, nm)));
+        const int64_t nd_new = ep.compacted ? 0 : scw(offsetof(Scalars, nd_next));
         const int64_t tail_new = ep.gc_ran ? scw(offsetof(Scalars, tail_gc)) : scw(offsetof(Scalars, tail_next));
         const int64_t edges = bs32(offsetof(BatchScalars, edge_overflow)) ? -1 : (int64_t)bsw(offsetof(BatchScalars, n_edges));
         const uint32_t dbg = bs32(offsetof(BatchScalars, debug_error)), rounds = bs32(offsetof(BatchScalars, rounds));
@@ -4112,7 +4109,6 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             uint64_t x = pre;
             if (lane == sc_word(offsetof(Scalars, n))) x = (uint64_t)n_new;
             if (lane == sc_word(offsetof(Scalars, nd))) x = (uint64_t)nd_new;
-            if (lane == sc_word(offsetof(Scalars, nm))) x = (uint64_t)nm_new;
             if (lane == sc_word(offsetof(Scalars, tail_used))) x = (uint64_t)tail_new;
             if (nd_slot >= 0 && nd_slot < 2 && lane == sc_word(offsetof(Scalars, ndb)) + nd_slot) x = (uint64_t)nd_new;
             if (lane == sc_word(offsetof(Scalars, debug_error))) x = (uint64_t)dbg | (uint64_t)rounds << 32;
@@ -4124,7 +4120,6 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         if (lane == 0) {
             sc->n = n_new;
             sc->nd = nd_new;
-            sc->nm = nm_new;
             if (ep.nd_out) *ep.nd_out = nd_new;
             sc->tail_used = tail_new;
             ep.bsc->debug_error = 0;
@@ -4246,10 +4241,9 @@ void launch_rangemax(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64
 }
 
 void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxLevels& m, Scalars* sc,
-                     int compacted, int folded, int gc_ran, uint8_t* verdict_out, uint32_t* flag,
+                     int compacted, int gc_ran, uint8_t* verdict_out, uint32_t* flag,
                      uint32_t seq, int64_t grid_hint_n, int64_t* nd_out, int sort_nb, int sort_samples) {
-    Epilogue ep = make_epilogue(b, w, compacted, folded || compacted, gc_ran, verdict_out, flag, seq, sort_nb,
-                                sort_samples);
+    Epilogue ep = make_epilogue(b, w, compacted, gc_ran, verdict_out, flag, seq, sort_nb, sort_samples);
     ep.nd_out = nd_out;
     if (compacted) launch_directory(s, m, gc_ran ? &sc->n_gc : &sc->n_next);  // the k_epilogue's n0
     int64_t extra = std::max<int64_t>(b.R, b.T);
@@ -4260,12 +4254,6 @@ void launch_epilogue(hipStream_t s, const BatchDev& b, const Work& w, const MaxL
     else
         fdb_launch(k_epilogue<false>, dim3((unsigned)epilogue_grid(grid_hint_n, extra)), dim3(kEpiThreads), 0, s, m, sc,
                    (const int64_t*)nullptr, ep);
-}
-
-void launch_levels(hipStream_t s, const MaxLevels& m, Scalars* sc, const int64_t* n, int64_t grid_hint_n) {
-    Epilogue ep{};  // no verdicts: the launch returns once the levels, index and directory are built
-    fdb_launch(k_epilogue<true>, dim3((unsigned)epilogue_grid(grid_hint_n, 0)), dim3(kEpiThreads), 0, s, m, sc, n,
-               ep);
 }
 
 }  // namespace fdbcs

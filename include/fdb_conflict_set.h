@@ -118,8 +118,6 @@ typedef struct fdbcs_stats {
     double host_ms_record;
     double host_ms_submit;
     int64_t compact_launches; /* compactions whose copy kernel was timed (compact_bytes counts these only) */
-    int64_t folds;            /* delta tier folded into the mid tier (every compaction folds first) */
-    int64_t mid_sum;          /* mid-tier boundaries after each batch, summed */
     /* Shapes of every batch, whatever the timing level (the roofline's byte models, roofline.py). */
     int64_t merge_bytes_all;   /* algorithmic bytes of every delta-merge copy */
     int64_t compact_bytes_all; /* algorithmic bytes of every compaction copy */

@@ -10,7 +10,7 @@ kernel really moved (`traffic`); the two side by side show wasted re-reads.
 
 Notation (§8(d)): P = 16 (key prefix bytes), V = 8 (version bytes), D = 24 (a batch key record:
 prefix, length, tail offset), I = 32 (a sort item), N / Nd = base / delta history boundaries,
-Nm = mid-tier boundaries, R / W = read / write ranges, T = transactions, E = 2 (R + W) endpoints, G = R + W ranges,
+R / W = read / write ranges, T = transactions, E = 2 (R + W) endpoints, G = R + W ranges,
 U = union segments of committed writes, X = candidate intra-batch edges.
 
 A lookup in a tier is priced by the nodes it must read: a 128-byte node per search-tree level
@@ -57,9 +57,6 @@ def shape_of(batches, st: dict, history: int, dir_share: float = 1.0) -> dict:
         "T": T, "R": R, "W": W, "E": 2 * (R + W), "G": R + W,
         "N": st.get("base_sum", 0) / b if st.get("base_sum") else float(history),
         "Nd": st.get("delta_sum", 0) / b,
-        "Nm": st.get("mid_sum", 0) / b,
-        "folds": st.get("folds", 0) / b,
-        "compactions": st.get("compactions", 0) / b,
         "U": st.get("segments_sum", 0) / b,
         "X": st.get("intra_edges", 0) / max(1, b - st.get("intra_fallbacks", 0)),
         "merge_bytes": st.get("merge_bytes_all", 0) / b,
@@ -76,14 +73,13 @@ def kernel_bytes(name: str, s: dict):
     T, R, W, E, G, N, Nd, U, X = (s[k] for k in ("T", "R", "W", "E", "G", "N", "Nd", "U", "X"))
     S = min(E, max(1024.0, min(8192.0, 4 * math.ceil(E / 128))))
     nb = min(2048.0, math.ceil(E / 128))
-    Nm = s.get("Nm", 0.0)
-    look_b, look_d, look_m = lookup_bytes(N, s["dir_share"]), lookup_bytes(Nd, 0.5), lookup_bytes(Nm, 0.5)
-    if name == "k_check_lanes" or name.startswith("k_check_lanes<"):  # the base and mid tiers
-        return (2 * R * (D + look_b + look_m) + R * (4 + V) + 2 * R * V + T,
-                "2R(D + base lookup + mid lookup) + R(owner + snapshot) + range-max ends 2RV + T")
-    if name.startswith("k_check_lanes_tier<true"):  # one tier, the base (the two-tier builds' split check)
+    look_b, look_d = lookup_bytes(N, s["dir_share"]), lookup_bytes(Nd, 0.5)
+    if name == "k_check_lanes" or name.startswith("k_check_lanes<") or name.startswith("k_check_reads"):  # both tiers
+        return (2 * R * (D + look_b + look_d) + R * (4 + V) + 2 * R * V + T,
+                "2R(D + base lookup + delta lookup) + R(owner + snapshot) + range-max ends 2RV + T")
+    if name.startswith("k_check_tier<true") or name.startswith("k_check_lanes_tier<true"):
         return (2 * R * (D + look_b) + R * (4 + V) + R * V + T, "base tier: 2R(D + lookup) + R(4+V) + RV + T")
-    if name.startswith("k_check_lanes_tier<false"):
+    if name.startswith("k_check_tier<false") or name.startswith("k_check_lanes_tier<false"):
         return (2 * R * (D + look_d) + R * (4 + V) + R * V + T, "delta tier: 2R(D + lookup) + R(4+V) + RV + T")
     if name == "k_sample":
         return S * (D + I + 4), "S samples: key read, item written, rank"
@@ -152,18 +148,10 @@ def kernel_bytes(name: str, s: dict):
         return s["merge_bytes"], "32 B per kept and inserted boundary read and per result boundary written (device scalars)"
     if name.startswith("k_merge_copy<fdbcs::CompactIns"):
         return s["compact_bytes"], "32 B per kept base / inserted delta boundary read and per result boundary written"
-    if name.startswith("k_compact_search") or name.startswith("k_scan<2, fdbcs::CompactSumScan"):
-        # one launch per fold (the delta's boundaries searched in the mid tier) and one per
-        # compaction (the mid tier's searched in the base): the launch-weighted average
-        f, c = s.get("folds", 0.0), s.get("compactions", 0.0)
-        nf, nc = Nd, max(Nm, Nd)
-        if name.startswith("k_compact_search"):
-            per_f, per_c = nf * (P + 8 + look_m + 17), nc * (P + 8 + look_b + 17)
-            text = "per overlaid boundary: key + lookup in the tier below, 2 words (folds and compactions averaged)"
-        else:
-            per_f, per_c = nf * (8 + 8 + 1 + 24), nc * (8 + 8 + 1 + 24)
-            text = "per overlaid boundary: lo, version, exact flag; 3 words written (folds and compactions averaged)"
-        return ((f * per_f + c * per_c) / (f + c) if f + c > 0 else per_f), text
+    if name.startswith("k_compact_search"):
+        return Nd * (P + 8 + lookup_bytes(N, s["dir_share"]) + 17), "per delta boundary: key + lookup in the base, 2 words"
+    if name.startswith("k_scan<2, fdbcs::CompactSumScan"):
+        return Nd * (8 + 8 + 1 + 24), "per delta boundary: lo, version, exact flag; 3 words written"
     if name.startswith("k_scan<2, fdbcs::GcScan"):
         return N * (2 * V + 8) + N * 32, "versions (own + predecessor) and lengths read, kept boundaries rewritten"
     if name.startswith("k_epilogue"):
@@ -171,11 +159,7 @@ def kernel_bytes(name: str, s: dict):
         # (k_epilogue<false>), the whole base after a compaction (k_epilogue<true>); per boundary its
         # version read, per 8 boundaries the sampled key read and its skey8 entry written, per 64 the
         # level-1 maximum and the level-0 sample key written
-        if name.startswith("k_epilogue<true"):  # the mid tier after a fold, the base after a compaction
-            f, c = s.get("folds", 0.0) - s.get("compactions", 0.0), s.get("compactions", 0.0)
-            n = (f * Nm + c * N) / (f + c) if f + c > 0 else N
-        else:
-            n = Nd
+        n = N if name.startswith("k_epilogue<true") or Nd <= 0 else Nd
         return (n * (V + 2 * P / 8 + (V + P) / 64) + T * 2 + R * 6,
                 "levels and sample index of the changed tier (the delta after a merge; the base after a compaction, "
                 "k_epilogue<true>): versions, per 8 boundaries a sampled key read and its skey8 entry written, per 64 "

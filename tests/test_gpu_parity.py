@@ -162,15 +162,14 @@ def test_shared_long_prefixes(engine, oracle_mod):
     run_pair(engine, oracle_mod, seq, gc_interval=0, delta_limit=30)
 
 
-@pytest.mark.parametrize("layout", ["pipelined", "serial"])
+@pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("tail_max", [40, 8])
-def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, layout, tail_max):
+def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, split, tail_max):
     """Thousands of history boundaries behind one 16-byte prefix (a few huge tuple subspaces): the
     search must order them by their tail bytes over a run far longer than one 64-boundary block
     (the cooperative probe rounds start at a stride of 512 or more; with keys of at most 24 bytes
-    the per-lane lookups' binary search over the run).  layout "serial": every launch on one
-    stream (FDBCS_SERIAL), the base + mid check inside stage B."""
-    monkeypatch.setenv("FDBCS_SERIAL", "1" if layout == "serial" else "0")
+    the per-lane lookups' binary search over the run)."""
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(123 + tail_max)
     prefixes = [b"\x15\x2a\x02huge-subspa%d\x00" % i for i in range(3)]
     assert all(len(x) == 16 for x in prefixes)
@@ -206,9 +205,8 @@ def test_long_shared_prefix_runs(engine, oracle_mod, monkeypatch, layout, tail_m
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
-@pytest.mark.parametrize("directory,layout,gc", [("1", "pipelined", 2), ("1", "serial", 2), ("0", "pipelined", 2),
-                                                 ("1", "pipelined", 0)])
-def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, layout, gc):
+@pytest.mark.parametrize("directory,split,gc", [("1", "2", 2), ("1", "1", 2), ("0", "2", 2), ("1", "2", 0)])
+def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, split, gc):
     """The base tier's radix directory (first two key bytes -> level-0 samples): sparse slots
     counted directly, a crowded slot (one 2-byte prefix holding thousands of boundaries) taking
     the tree, keys at the slot edges (empty key, 0x0000.., 0xffff.., bare 2-byte keys), and
@@ -216,7 +214,7 @@ def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, layou
     tier, whose directory k_epilogue refills per batch under a new epoch (runs over kDirRun slots
     stay stale and take the tree)."""
     monkeypatch.setenv("FDBCS_DIRECTORY", directory)
-    monkeypatch.setenv("FDBCS_SERIAL", "1" if layout == "serial" else "0")
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(4242)
     edges = [b"", b"\x00", b"\x00\x00", b"\x00\x00\x00", b"\x12\x33\xff", b"\x12\x34", b"\x12\x34\x00",
              b"\x12\x35", b"\xff\xfe\xff", b"\xff\xff", b"\xff\xff\x00", b"\xff\xff\xff\xff"]
@@ -257,14 +255,14 @@ def test_radix_directory_slots(engine, oracle_mod, monkeypatch, directory, layou
         assert (ve == vo).all(), (i, np.nonzero(ve != vo)[0][:10])
 
 
-@pytest.mark.parametrize("layout", ["pipelined", "serial"])
+@pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("plen", [30, 60, 104, 150])
-def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, layout):
+def test_very_long_shared_prefixes(engine, oracle_mod, monkeypatch, plen, split):
     """Keys sharing prefixes of 30-150 bytes, so that tail comparisons end inside the long-key
     probe's first word round (48 bytes), its second (96), and past the query words it holds in
     registers (the rest compared from memory); history and batch keys of every length around them.
-    layout "serial": every launch on one stream (FDBCS_SERIAL)."""
-    monkeypatch.setenv("FDBCS_SERIAL", "1" if layout == "serial" else "0")
+    split "1": the split read check (long-key probes in both check launches); "2": the default."""
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     rng = np.random.default_rng(plen)
     prefixes = [bytes([0x15, 0x2a + i]) + b"x" * (plen - 2) for i in range(2)]
 
@@ -408,15 +406,14 @@ def test_c3_zipf_heavy_contention(engine, oracle_mod, monkeypatch, prepass):
     e, o = run_pair(engine, oracle_mod, seq, check_conf=False, ref="skiplist")
 
 
-@pytest.mark.parametrize("gc_interval,delta_limit,layout", [(1, 0, "pipelined"), (0, 3000, "pipelined"),
-                                                            (1, 0, "serial"), (0, 3000, "serial")])
-def test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, gc_interval, delta_limit, layout):
+@pytest.mark.parametrize("gc_interval,delta_limit,split", [(1, 0, "2"), (0, 3000, "2"), (1, 0, "1"), (0, 3000, "1")])
+def test_c4_tuple_keys_window_gc(engine, oracle_mod, monkeypatch, gc_interval, delta_limit, split):
     """BASELINE config C4, reduced: tuple-encoded keys up to ~100 B whose 16-byte prefixes are
     shared by every key of a user (comparisons go to the tail bytes), wide Tuple.range() reads, and
     the window sliding with newOldest = now - window every batch (GC), against the skip-list
-    restatement; after a compaction with GC both hold the same boundary count.  layout "serial":
-    every launch on one stream (FDBCS_SERIAL)."""
-    monkeypatch.setenv("FDBCS_SERIAL", "1" if layout == "serial" else "0")
+    restatement; after a compaction with GC both hold the same boundary count.  split "1": the
+    split check (the base tier's long-key lookups on their own launch)."""
+    monkeypatch.setenv("FDBCS_SPLIT_CHECK", split)
     p = W.C4Params(txns=1500, users=3000, items=400, history=80_000, window=12_000, staleness=4_000)
     kb, ko, vers = W.c4_history(p, seed=4, start_version=100_000)
     e = EngineDriver(engine, gc_interval=gc_interval, delta_limit=delta_limit)
@@ -730,11 +727,14 @@ def test_empty_batches(engine, oracle_mod):
 
 # Every engine knob that selects a different kernel or submission path (DESIGN.md §5 "Engine knobs")
 # is parity-tested here; knobs measured slower and not kept were deleted with their code.
-@pytest.mark.parametrize("knobs", [{"FDBCS_SORT_COLD": "1"}, {"FDBCS_SUBMIT_THREAD": "0"},
+@pytest.mark.parametrize("knobs", [{"FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SPLIT_CHECK": "0"},
+                                   {"FDBCS_SORT_COLD": "1"},
+                                   {"FDBCS_SUBMIT_THREAD": "0", "FDBCS_SPLIT_CHECK": "1"}, {"FDBCS_SUBMIT_THREAD": "0"},
                                    {"FDBCS_WRITE_GROUPS": "0"}, {"FDBCS_SERIAL": "1"},
                                    {"FDBCS_DIRECTORY": "0"}, {"FDBCS_SKIP_EDGES": "0"}])
 def test_pipeline_variants_match_oracle(engine, oracle_mod, knobs):
-    """The engine's remaining path-selecting knobs stay exact: cold-start splitters on every batch, one submitting thread, one candidate edge per writer (the
+    """The engine's remaining path-selecting knobs stay exact: the unsplit and split read checks,
+    cold-start splitters on every batch, one submitting thread, one candidate edge per writer (the
     production path past 12288 writes), the serial stream layout, base lookups without the radix
     directory, the no-edge launches kept."""
     saved = {k: os.environ.get(k) for k in knobs}
