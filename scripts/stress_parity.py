@@ -2,8 +2,8 @@
 
 Each round draws a key alphabet (arbitrary bytes, decimal digits, a sparse byte set, a tiny
 alphabet), a shared prefix, key lengths around 16 and 24 bytes, a loaded history, engine knobs
-read at set creation (directory code and slot budget, split check, lookup layouts, compaction and
-GC cadence), and a sequence of batches whose snapshots straddle the oldest version; verdicts and
+read at set creation (directory slot budget, split check, stream layout, submitting threads),
+compaction and GC cadence, and a sequence of batches whose snapshots straddle the oldest version; verdicts and
 conflicting-read reports must match oracle/skiplist_baseline.cpp batch by batch.
 
     python3 scripts/stress_parity.py [seconds] [first_seed]
@@ -24,15 +24,11 @@ from oracle import oracle  # noqa: E402
 from tests.helpers import EngineDriver  # noqa: E402
 
 KNOBS = {
-    "FDBCS_DIR_RANK": ["1", "1", "0"],
     "FDBCS_DIR_BITS": ["0", "0", "16", "18"],
     "FDBCS_SPLIT_CHECK": ["2", "1"],
-    "FDBCS_LONG_LANES": ["1", "0"],
+    "FDBCS_SERIAL": ["0", "0", "0", "1"],
     "FDBCS_SKIP_EDGES": ["1", "0"],
-    "FDBCS_COMPACT_LANES": ["2", "1", "0"],
-    "FDBCS_BASE_TILE": ["4096", "2048", "1024"],
-    "FDBCS_SEG_LONG_COOP": ["0", "1"],
-    "FDBCS_COPY_NT": ["0", "1"],
+    "FDBCS_SUBMIT_THREAD": ["1", "1", "0"],
 }
 
 
