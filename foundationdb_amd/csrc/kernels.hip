@@ -201,6 +201,25 @@ __device__ __forceinline__ uint32_t dir_slot(const MaxLevels& m, uint64_t hi, ui
     return code;
 }
 
+// The directory range of q's slot, in skey8 entries (every 8th boundary): entries [d8a, d8b) share
+// q's slot, every entry before d8a lies below q and every entry from d8b on above it (dir_slot is
+// monotone over the 16-byte prefix).  Both tiers' directories count skey8 entries (base:
+// k_directory, exact; delta: the epilogue's fill, entries of the current epoch only).  false: no
+// directory, or a delta slot of another epoch.
+__device__ __forceinline__ bool dir_range8(const MaxLevels& m, const DKey& q, int64_t& d8a, int64_t& d8b) {
+    if (!m.dir && !m.edir_epoch) return false;
+    const uint32_t dv = dir_slot(m, q.hi, q.lo);
+    if (m.dir) {
+        d8a = m.dir[dv];
+        d8b = m.dir[dv + 1];
+        return true;
+    }
+    const uint64_t x0 = m.edir[dv], x1 = m.edir[dv + 1];
+    d8a = (uint32_t)x0;
+    d8b = (uint32_t)x1;
+    return (uint32_t)(x0 >> 32) == m.edir_epoch && (uint32_t)(x1 >> 32) == m.edir_epoch;
+}
+
 // LONG: the long-key probes above (the batch has keys over 16 bytes); same result.
 template <bool LONG = false>
 __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLevels& m, int64_t n, const DKey& q,
@@ -237,23 +256,12 @@ __device__ __forceinline__ int64_t group_lower_bound(const Hist& h, const MaxLev
     const bool v_top = gl < sz[top];
     const ulonglong2 e_top = m.skey[top][v_top ? gl : 0];
     bool direct = false;
-    if (m.dir || m.edir_epoch) {
-        // radix directory: the level-0 samples sharing q's directory bits are [dir[v], dir[v+1])
-        // (base: k_directory, exact; delta: k_epilogue's fill, entries of the current epoch only);
-        // a slot of at most two groups is counted directly at level 0
-        const uint32_t dv = dir_slot(m, q.hi, q.lo);
-        int64_t d0, d1;
-        bool have = true;
-        if (m.dir) {
-            d0 = m.dir[dv];
-            d1 = m.dir[dv + 1];
-        } else {
-            const uint64_t x0 = m.edir[dv], x1 = m.edir[dv + 1];
-            have = (uint32_t)(x0 >> 32) == m.edir_epoch && (uint32_t)(x1 >> 32) == m.edir_epoch;
-            d0 = (uint32_t)x0;
-            d1 = (uint32_t)x1;
-        }
-        if (have && d1 - d0 <= 2 * kArity && d1 <= sz[0]) {
+    int64_t d8a, d8b;
+    if (dir_range8(m, q, d8a, d8b)) {
+        // radix directory: the level-0 samples (every 8th skey8 entry) sharing q's directory bits
+        // are [d0, d1); a slot of at most two groups is counted directly at level 0
+        const int64_t d0 = (d8a + 7) >> 3, d1 = (d8b + 7) >> 3;
+        if (d1 - d0 <= 2 * kArity && d1 <= sz[0]) {
             direct = true;
             c = d0;
             bknown = true;  // all of the slot below q: the next sample's first two bytes are greater
@@ -526,20 +534,11 @@ __device__ __forceinline__ void lane_sample_range(const MaxLevels& m, int64_t n,
     bool bknown = false;  // the sample at c (if any) is known not to share q's prefix
     bool direct = false;
     int64_t w0 = -1, w1 = -1;  // a directory slot too wide to count at level 0
-    if (m.dir || m.edir_epoch) {
-        const uint32_t dv = dir_slot(m, q.hi, q.lo);
-        int64_t d0, d1;
-        bool have = true;
-        if (m.dir) {
-            d0 = m.dir[dv];
-            d1 = m.dir[dv + 1];
-        } else {
-            const uint64_t x0 = m.edir[dv], x1 = m.edir[dv + 1];
-            have = (uint32_t)(x0 >> 32) == m.edir_epoch && (uint32_t)(x1 >> 32) == m.edir_epoch;
-            d0 = (uint32_t)x0;
-            d1 = (uint32_t)x1;
-        }
-        if (have && d1 - d0 <= kLaneProbe && d1 <= sz[0]) {
+    int64_t d8a, d8b;
+    if (dir_range8(m, q, d8a, d8b)) {
+        // the level-0 samples (every 8th skey8 entry) in q's slot: [d0, d1)
+        const int64_t d0 = (d8a + 7) >> 3, d1 = (d8b + 7) >> 3;
+        if (d1 - d0 <= kLaneProbe && d1 <= sz[0]) {
             direct = true;
             bool eqn;
             const int cnt = (int)(d1 - d0);
@@ -547,7 +546,7 @@ __device__ __forceinline__ void lane_sample_range(const MaxLevels& m, int64_t n,
             c = d0 + k;
             // all of the slot below q: the next sample's first two bytes are greater
             bknown = k < cnt ? !eqn : true;
-        } else if (have && d1 <= sz[0]) {
+        } else if (d1 <= sz[0]) {
             w0 = d0;
             w1 = d1;
         }
@@ -612,6 +611,62 @@ __device__ __forceinline__ int64_t lane_lower_bound(const Hist& h, const MaxLeve
                                                     const uint8_t* htail, const uint8_t* qtail, bool& eq) {
     eq = false;
     if (n <= 0) return 0;
+    // Directory slot of at most kLaneProbe skey8 entries (C2: ~10 per slot of the base, ~2 of the
+    // delta): the group starts of q's slot are probed at once, so the lookup takes three dependent
+    // rounds (directory, group starts, the seven boundaries after the last start below q) instead
+    // of four (the level-0 samples first).  Entries before the slot lie below q, entries past it
+    // above q (dir_range8); prefix ties compare against the boundary itself (probe_cmp_lean).
+    int64_t d8a, d8b;
+    const int64_t n8 = (n + 7) >> 3;
+    if (dir_range8(m, q, d8a, d8b) && d8b - d8a <= kLaneProbe && d8b <= n8) {
+        const int cnt = (int)(d8b - d8a);
+        ulonglong2 s8[kLaneProbe];
+#pragma unroll
+        for (int i = 0; i < kLaneProbe; i++)
+            if (i < cnt) s8[i] = m.skey8[d8a + i];
+        int r8[kLaneProbe];
+        int k8 = 0;
+        bool stop = false;
+#pragma unroll
+        for (int i = 0; i < kLaneProbe; i++) {
+            r8[i] = 1;
+            if (i < cnt && !stop) {
+                r8[i] = probe_cmp_lean(h, 8 * (d8a + i), s8[i], htail, q, qtail);
+                if (r8[i] < 0) k8++; else stop = true;
+            }
+        }
+        const int64_t g = d8a + k8 - 1;  // the last group start below q (-1: none)
+        if (g < 0) {                     // q <= boundary 0 (probed when the slot holds entry 0)
+            eq = cnt > 0 && r8[0] == 0;
+            return 0;
+        }
+        const int64_t B = 8 * g, gend = min(B + 8, n);
+        const int nk = (int)(gend - B - 1);
+        ulonglong2 kk[7];
+#pragma unroll
+        for (int i = 0; i < 7; i++)
+            if (i < nk) kk[i] = h.key[B + 1 + i];
+        int k1 = 0, r_stop = 1;
+        stop = false;
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            if (i < nk && !stop) {
+                const int r = probe_cmp_lean(h, B + 1 + i, kk[i], htail, q, qtail);
+                if (r < 0) {
+                    k1++;
+                } else {
+                    stop = true;
+                    r_stop = r;
+                }
+            }
+        }
+        const int64_t lb = B + 1 + k1;
+        if (lb < gend)
+            eq = r_stop == 0;
+        else if (lb < n)  // lb = 8(g + 1): the next group start, probed above unless past the slot
+            eq = k8 < cnt && r8[k8] == 0;
+        return lb;
+    }
     int64_t c, b;
     lane_sample_range(m, n, q, c, b);
     const int64_t hi = min(n, kFan * b);
@@ -3983,17 +4038,18 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
         }
         const int64_t b1l = b1_0 + lane;  // lane q < kEpiBlocks owns block b1_0 + q
         ulonglong2 sk = make_ulonglong2(0, 0);
-        ulonglong2 prev_k = make_ulonglong2(0, 0);  // the previous block's sampled key (delta directory fill)
-        if (lane < kEpiBlocks && b1l < n1) {
-            sk = m.keys[b1l * kFan];  // sampled key of the block
-            if (m.edir_epoch && b1l > 0 && lane == 0) prev_k = m.keys[(b1l - 1) * kFan];
+        if (lane < kEpiBlocks && b1l < n1) sk = m.keys[b1l * kFan];  // sampled key of the block
+        // every 8th boundary of the wave's blocks (8 entries of skey8 per block), one per lane
+        constexpr int kE8 = kEpiBlocks * kFan / 8;
+        static_assert(kE8 <= 64, "one skey8 entry per lane");
+        const int64_t n8 = (n0 + 7) / 8, e8_0 = b1_0 * (kFan / 8);
+        ulonglong2 k8 = make_ulonglong2(0, 0);
+        ulonglong2 prev_k = make_ulonglong2(0, 0);  // the previous wave's last group start (delta directory fill)
+        if (lane < kE8 && e8_0 + lane < n8) {
+            k8 = m.keys[(e8_0 + lane) * 8];
+            m.skey8[e8_0 + lane] = k8;
         }
-        // every 8th boundary of the wave's blocks (8 entries of skey8 per block)
-        static_assert(kEpiBlocks * kFan / 8 <= 64, "one skey8 entry per lane");
-        {
-            const int64_t e8 = b1_0 * (kFan / 8) + lane;
-            if (lane < kEpiBlocks * kFan / 8 && e8 * 8 < n0) m.skey8[e8] = m.keys[e8 * 8];
-        }
+        if (m.edir_epoch && lane == 0 && e8_0 > 0 && e8_0 < n8) prev_k = m.keys[(e8_0 - 1) * 8];
         int64_t mine = LLONG_MIN;
 #pragma unroll
         for (int q = 0; q < kEpiBlocks; q++) {
@@ -4018,26 +4074,24 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             }
         }
         if (m.edir_epoch) {
-            // delta directory: slots (dir_slot(previous sample), dir_slot(this sample)] hold this
-            // sample's index (the first sample not below them); the last sample also fills the
-            // slots above it with n1.  At most kDirRun slots per run: slots left over keep an older
-            // epoch and send their lookups down the tree.  The whole wave writes each run, 64
-            // consecutive slots per store, instead of one lane per sample looping over its run.
+            // delta directory (group starts, as the base's): slots (dir_slot(previous start),
+            // dir_slot(this start)] hold this start's skey8 index (the first start not below
+            // them); the last start also fills the slots above it with the entry count.  At most
+            // kDirRun slots per run: slots left over keep an older epoch and send their lookups
+            // down the tree.  The whole wave writes each run, 64 consecutive slots per store.
             int64_t c_l = -1, a0 = -1;
-            if (lane < kEpiBlocks && b1l < n1) c_l = (int64_t)dir_slot(m, sk.x, sk.y);
-            if (lane == 0 && b1l > 0 && b1l < n1) a0 = (int64_t)dir_slot(m, prev_k.x, prev_k.y);
+            if (lane < kE8 && e8_0 + lane < n8) c_l = (int64_t)dir_slot(m, k8.x, k8.y);
+            if (lane == 0 && e8_0 > 0 && e8_0 < n8) a0 = (int64_t)dir_slot(m, prev_k.x, prev_k.y);
             const uint64_t tag = (uint64_t)m.edir_epoch << 32;
             int64_t aq = __shfl(a0, 0, 64);
-#pragma unroll
-            for (int q = 0; q < kEpiBlocks; q++) {
-                const int64_t bq = b1_0 + q, cq = __shfl(c_l, q, 64);
-                if (bq < n1) {  // (uniform)
-                    const int64_t e = cq < aq + kDirRun ? cq : aq + kDirRun;
-                    for (int64_t v = aq + 1 + lane; v <= e; v += 64) m.edir[v] = tag | (uint64_t)bq;
-                    if (bq == n1 - 1) {
-                        const int64_t top = (int64_t)m.dir_top + 1, e2 = cq + kDirRun < top ? cq + kDirRun : top;
-                        for (int64_t v = cq + 1 + lane; v <= e2; v += 64) m.edir[v] = tag | (uint64_t)n1;
-                    }
+            for (int q = 0; q < kE8; q++) {
+                const int64_t bq = e8_0 + q, cq = __shfl(c_l, q, 64);
+                if (bq >= n8) break;  // (uniform)
+                const int64_t e = cq < aq + kDirRun ? cq : aq + kDirRun;
+                for (int64_t v = aq + 1 + lane; v <= e; v += 64) m.edir[v] = tag | (uint64_t)bq;
+                if (bq == n8 - 1) {
+                    const int64_t top = (int64_t)m.dir_top + 1, e2 = cq + kDirRun < top ? cq + kDirRun : top;
+                    for (int64_t v = cq + 1 + lane; v <= e2; v += 64) m.edir[v] = tag | (uint64_t)n8;
                 }
                 aq = cq;
             }
@@ -4202,22 +4256,23 @@ static int64_t epilogue_grid(int64_t hint_n, int64_t extra) {
     return g > 4096 ? 4096 : g;
 }
 
-// Radix directory of the base tier (D.CheckRead): dir[v] = number of level-0 samples (keys[64 j],
-// j < ceil(n / 64)) whose directory slot (dir_slot) is below v, v in [0, dir_top + 1].  A lookup whose slot
-// holds at most two sample groups starts at level 0 (one directory load, one or two group loads)
-// instead of descending the ~6 levels above it; slots crowded by shared key prefixes (subspaces,
-// hot ranges) take the tree.  Rebuilt with the base tier's index (compaction, GC, load), one
-// binary search per slot.
+// Radix directory of the base tier (D.CheckRead): dir[v] = number of group starts (keys[8 j], the
+// skey8 entries, j < ceil(n / 8)) whose directory slot (dir_slot) is below v, v in [0, dir_top + 1].
+// A lookup whose slot holds at most kLaneProbe group starts probes them at once (lane_lower_bound:
+// one directory load, one round over the slot's group starts, one over a group); a wider slot
+// starts at level 0 (its samples are every 8th entry) or, crowded by shared key prefixes
+// (subspaces, hot ranges), part-way down the tree.  Rebuilt with the base tier's index
+// (compaction, GC, load), one binary search per slot.
 __global__ __launch_bounds__(kBlock) void k_directory(MaxLevels m, const int64_t* np) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v > (int)m.dir_top + 1) return;
     const ulonglong2* keys = m.keys;
     int32_t* dir = const_cast<int32_t*>(m.dir);
-    const int64_t S = (*np + kFan - 1) / kFan;
+    const int64_t S = (*np + 7) / 8;
     int64_t lo = 0, hi = S;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        const ulonglong2 k = keys[mid * kFan];
+        const ulonglong2 k = keys[mid * 8];
         if ((int64_t)dir_slot(m, k.x, k.y) < v)
             lo = mid + 1;
         else
