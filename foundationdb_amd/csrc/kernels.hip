@@ -4078,22 +4078,30 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             // dir_slot(this start)] hold this start's skey8 index (the first start not below
             // them); the last start also fills the slots above it with the entry count.  At most
             // kDirRun slots per run: slots left over keep an older epoch and send their lookups
-            // down the tree.  The whole wave writes each run, 64 consecutive slots per store.
-            int64_t c_l = -1, a0 = -1;
-            if (lane < kE8 && e8_0 + lane < n8) c_l = (int64_t)dir_slot(m, k8.x, k8.y);
-            if (lane == 0 && e8_0 > 0 && e8_0 < n8) a0 = (int64_t)dir_slot(m, prev_k.x, prev_k.y);
+            // down the tree.  Most runs are short (C2's delta: ~0.4 slots per start) and each lane
+            // writes its own; runs over 4 slots (keys crowding a few slots, as C3's hot range, and
+            // the last start's run to the top) are written by the whole wave, 64 slots per store.
+            const int64_t e = e8_0 + lane;
+            const bool live = lane < kE8 && e < n8;
+            const int64_t c_l = live ? (int64_t)dir_slot(m, k8.x, k8.y) : -1;
+            int64_t a = __shfl_up(c_l, 1, 64);
+            if (lane == 0) a = e8_0 > 0 && live ? (int64_t)dir_slot(m, prev_k.x, prev_k.y) : -1;
             const uint64_t tag = (uint64_t)m.edir_epoch << 32;
-            int64_t aq = __shfl(a0, 0, 64);
-            for (int q = 0; q < kE8; q++) {
-                const int64_t bq = e8_0 + q, cq = __shfl(c_l, q, 64);
-                if (bq >= n8) break;  // (uniform)
-                const int64_t e = cq < aq + kDirRun ? cq : aq + kDirRun;
-                for (int64_t v = aq + 1 + lane; v <= e; v += 64) m.edir[v] = tag | (uint64_t)bq;
-                if (bq == n8 - 1) {
-                    const int64_t top = (int64_t)m.dir_top + 1, e2 = cq + kDirRun < top ? cq + kDirRun : top;
-                    for (int64_t v = cq + 1 + lane; v <= e2; v += 64) m.edir[v] = tag | (uint64_t)n8;
-                }
-                aq = cq;
+            const int64_t z = live ? (c_l < a + kDirRun ? c_l : a + kDirRun) : a;
+            const bool wide = live && z - a > 4;
+            if (live && !wide)
+                for (int64_t v = a + 1; v <= z; v++) m.edir[v] = tag | (uint64_t)e;
+            for (uint64_t wm = __ballot(wide); wm; wm &= wm - 1) {
+                const int q = __builtin_ctzll(wm);
+                const int64_t aq = __shfl(a, q, 64), zq = __shfl(z, q, 64);
+                for (int64_t v = aq + 1 + lane; v <= zq; v += 64) m.edir[v] = tag | (uint64_t)(e8_0 + q);
+            }
+            const uint64_t lm = __ballot(live && e == n8 - 1);  // the last start: slots above it
+            if (lm) {
+                const int q = __builtin_ctzll(lm);
+                const int64_t cq = __shfl(c_l, q, 64);
+                const int64_t top = (int64_t)m.dir_top + 1, z2 = cq + kDirRun < top ? cq + kDirRun : top;
+                for (int64_t v = cq + 1 + lane; v <= z2; v += 64) m.edir[v] = tag | (uint64_t)n8;
             }
         }
         // the wave's maximum into levels 2 and 3; level 3 only when above what it already holds
