@@ -933,38 +933,11 @@ __device__ __forceinline__ int64_t lane_lower_bound_long(const Hist& h, const Ma
 // looks at the greatest boundary < b): it meets the read iff its end lies past the read's begin (at
 // or past it for a degenerate read).  Searched by the four lanes of one read (lanes 4i..4i+3 call
 // with the same read): 16 probes per round, four per lane.
-//
-// The search's upper levels are staged in LDS (stage: prev_stage's layout, or null): round one
-// probes 16 fixed positions over [0, U), and round two the 16 positions inside whichever of the 17
-// intervals round one left, so every workgroup loads those 16 + 17 x 16 begin keys once, beside its
-// lookups, and its reads take their first two rounds from LDS; later rounds load from the segment
-// keys themselves (C2: ~10k segments, four rounds in all).
-constexpr int kPrevStage = 16 + 17 * 16;
-__device__ __forceinline__ int64_t prev_probe(int64_t lo, int64_t hi, int k) { return lo + ((hi - lo) * (k + 1)) / 17; }
-// Staged entry t's segment, or -1 (an interval round one cannot leave).
-__device__ __forceinline__ int64_t prev_stage_pos(int64_t U, int t) {
-    if (t < 16) return prev_probe(0, U, t);
-    const int i = (t - 16) >> 4, k = (t - 16) & 15;  // interval i of round one: below == i
-    const int64_t lo = i > 0 ? (U * i) / 17 + 1 : 0, hi = i < 16 ? (U * (i + 1)) / 17 : U;
-    return lo < hi ? prev_probe(lo, hi, k) : -1;
-}
-__device__ __forceinline__ void prev_stage_load(const PrevSegs& ps, DKey* stage) {
-    if (!ps.n) return;
-    const int64_t U = *ps.n;
-    if (U <= 0) return;
-    for (int t = threadIdx.x; t < kPrevStage; t += blockDim.x) {
-        const int64_t pos = prev_stage_pos(U, t);
-        if (pos >= 0) stage[t] = ps.segk[2 * pos];
-    }
-}
-
 __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U, const DKey& kb, const DKey& ke,
-                                                  bool degenerate, const uint8_t* qtail, bool active,
-                                                  const DKey* stage) {
+                                                  bool degenerate, const uint8_t* qtail, bool active) {
     const DKey& target = degenerate ? kb : ke;
     const int ql = threadIdx.x & 3;
     int64_t lo = 0, hi = active ? U : 0;  // begins below the target: all of [0, lo), none of [hi, U)
-    int round = 0, iv = 0;
     for (;;) {
         const bool more = lo < hi;
         // the quad's lanes share lo / hi: the loop runs while any read of the wave searches
@@ -973,16 +946,10 @@ __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U,
         if (more) {
             int64_t idx[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) idx[j] = prev_probe(lo, hi, 4 * ql + j);
+            for (int j = 0; j < 4; j++) idx[j] = lo + ((hi - lo) * (4 * ql + j + 1)) / 17;
             DKey d[4];
-            if (stage && round < 2) {
-                const DKey* sr = stage + (round == 0 ? 0 : 16 + 16 * iv) + 4 * ql;
 #pragma unroll
-                for (int j = 0; j < 4; j++) d[j] = sr[j];
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) d[j] = ps.segk[2 * idx[j]];
-            }
+            for (int j = 0; j < 4; j++) d[j] = ps.segk[2 * idx[j]];
 #pragma unroll
             for (int j = 0; j < 4; j++) below += dkey_cmp(d[j], ps.tail, target, qtail) < 0 ? 1 : 0;
         }
@@ -994,9 +961,7 @@ __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U,
             const int64_t nhi = below < 16 ? lo + ((hi - lo) * (below + 1)) / 17 : hi;
             lo = nlo;
             hi = nhi;
-            if (round == 0) iv = below;
         }
-        round++;
     }
     if (!active || lo == 0) return false;
     const int cmp = dkey_cmp(ps.segk[2 * lo - 1], ps.tail, kb, qtail);  // end of segment lo - 1 vs b
@@ -1010,7 +975,7 @@ __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U,
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& base, const Tier& delta,
                                                  const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
-                                                 const PrevSegs& ps, const DKey* stage) {
+                                                 const PrevSegs& ps) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r = t >> 2;
     const int k = (int)(t & 3);
@@ -1041,9 +1006,7 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
     if (ps.n) {  // the previous batch's union segments, not merged into the delta yet (every lane
                  // of the quad takes part in the search's shuffles)
         const int64_t U = *ps.n;
-        __syncthreads();  // the staged upper levels (prev_stage_load, at the launch's start)
-        const bool hit = prev_seg_hit_quad(ps, U, kb, ke, degenerate, b.tail, live && U > 0 && ps.version > snap,
-                                           stage);
+        const bool hit = prev_seg_hit_quad(ps, U, kb, ke, degenerate, b.tail, live && U > 0 && ps.version > snap);
         conf = conf || hit;
     }
     int c = conf ? 1 : 0;
@@ -1063,7 +1026,7 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const Tier& tier, bool is_base,
                                                       const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
-                                                      const PrevSegs& ps, const DKey* stage) {
+                                                      const PrevSegs& ps) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r = t >> 1;
     const int k = (int)(t & 1);
@@ -1094,7 +1057,6 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
         // every lane; each pair's read is its own, the quad shares no state but the shuffles)
         const int64_t U = *ps.n;
         const bool act = live && U > 0 && ps.version > snap;
-        __syncthreads();  // the staged upper levels (prev_stage_load, at the launch's start)
         // two reads per quad: search them one after the other so the quad's lanes agree on lo / hi
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -1105,7 +1067,7 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
                              (uint32_t)__shfl((int)ke.len, src, 64), (uint32_t)__shfl((int)ke.tail, src, 64)};
             const int sdeg = __shfl((int)degenerate, src, 64);
             const int sact = __shfl((int)act, src, 64);
-            const bool hit = prev_seg_hit_quad(ps, U, sb, se, sdeg != 0, b.tail, sact != 0, stage);
+            const bool hit = prev_seg_hit_quad(ps, U, sb, se, sdeg != 0, b.tail, sact != 0);
             if (((threadIdx.x >> 1) & 1) == s) conf = conf || hit;
         }
     }
@@ -1278,16 +1240,12 @@ struct CheckReads {
 // LONG: the batch has keys over 24 bytes (lane_lower_bound_long).
 template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes(BatchDev b, CheckReads c) {
-    __shared__ DKey s_prev[kPrevStage];
-    prev_stage_load(c.ps, s_prev);  // in flight beside the lookups
-    check_read_lanes<LONG>(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps, s_prev);
+    check_read_lanes<LONG>(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
 }
 template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t, const uint8_t* htail,
                                                              uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps) {
-    __shared__ DKey s_prev[BASE ? 1 : kPrevStage];
-    if (!BASE) prev_stage_load(ps, s_prev);
-    check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, ps, BASE ? nullptr : s_prev);
+    check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, ps);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
