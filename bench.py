@@ -373,7 +373,7 @@ def main():
     # batch index ranges of the passes, in order
     spans = {}
     at = 0
-    for name, n in (("warmup", args.warmup), ("profile", args.profile_steps), ("timed", args.steps),
+    for name, n in (("warmup", args.warmup), ("timed", args.steps), ("profile", args.profile_steps),
                     ("roof", args.roof_steps), ("h2d", args.h2d_steps), ("total", n_total), ("sync", args.sync_steps),
                     ("hold", args.hold_steps), ("breakdown", args.breakdown_steps)):
         spans[name] = (at, at + n)
@@ -598,33 +598,6 @@ def main():
 
     run(*spans["warmup"], packed(*spans["warmup"]))
 
-    # per-kernel profile: events around every kernel of every batch (timing level 3), pipelined as
-    # in the timed region; the dominant kernel (largest device time) is then timed in the timed
-    # region itself (level 1, 1 batch in 4, on the stream it runs on)
-    kprof = {}
-    dominant = None
-    if args.profile_steps > 0:
-        cs.reset_stats()
-        cs.set_timing(3)
-        run(*spans["profile"], packed(*spans["profile"]))
-        kprof = cs.kernel_profile()
-        st_prof = cs.stats()
-        dominant = max(kprof, key=lambda k: kprof[k]["ms"]) if kprof else None
-    # The dominant kernel by rocprofv3 kernel-trace time (dispatch to completion) when a summary of
-    # this configuration and build is committed: the profile pass's events also count the time a
-    # kernel waits for its stream's turn behind the other streams' kernels.
-    build = roofline.build_id(ROOT)
-    rp_kernels, rp_note = roofline.rocprof_kernels(ROOT, args.workload, p.txns, p.history, build)
-    dominant_source = "profile pass (events around every kernel)"
-    if rp_kernels:
-        ranked = [k for k in rp_kernels if k in kprof]
-        if ranked:
-            dominant = ranked[0]
-            dominant_source = "rocprofv3 kernel trace: " + rp_note
-    cs.set_timing(0)
-    # resolved now, while the profile pass's kernel list still names it; recorded only at timing 1
-    cs.set_timed_kernel(dominant)
-
     def resident(lo, hi):
         """Batches lo..hi-1 packed and their H2D issued (a rank's proxy share likewise); the caller's
         barrier() then waits for the copies on the engine's upload stream."""
@@ -652,6 +625,35 @@ def main():
     host_timed = {k: v / args.steps * 1e3 for k, v in host.items()}
     for k in ("host_ms_prepare", "host_ms_record", "host_ms_submit"):  # inside detect_async (engine's clock)
         host_timed["engine_" + k[8:]] = st[k] / max(1, st["batches"])
+
+    # per-kernel profile, after the timed region so that it sees the history the roofline pass runs
+    # on (the kernels can change with it: a base tier past kSplitCheckMinBase splits the read check):
+    # events around every kernel of every batch (timing level 3), pipelined as in the timed region;
+    # the dominant kernel (largest device time) is then timed by the roofline pass (level 1, 1 batch
+    # in 4, on the stream it runs on)
+    kprof = {}
+    dominant = None
+    if args.profile_steps > 0:
+        cs.reset_stats()
+        cs.set_timing(3)
+        run(*spans["profile"], packed(*spans["profile"]))
+        kprof = cs.kernel_profile()
+        st_prof = cs.stats()
+        dominant = max(kprof, key=lambda k: kprof[k]["ms"]) if kprof else None
+    # The dominant kernel by rocprofv3 kernel-trace time (dispatch to completion) when a summary of
+    # this configuration and build is committed: the profile pass's events also count the time a
+    # kernel waits for its stream's turn behind the other streams' kernels.
+    build = roofline.build_id(ROOT)
+    rp_kernels, rp_note = roofline.rocprof_kernels(ROOT, args.workload, p.txns, p.history, build)
+    dominant_source = "profile pass (events around every kernel)"
+    if rp_kernels:
+        ranked = [k for k in rp_kernels if k in kprof]  # (kernels this history state launches)
+        if ranked:
+            dominant = ranked[0]
+            dominant_source = "rocprofv3 kernel trace: " + rp_note
+    cs.set_timing(0)
+    # resolved now, while the profile pass's kernel list still names it; recorded only at timing 1
+    cs.set_timed_kernel(dominant)
 
     # roofline pass: the same pipeline on its own resident batches, with events around the dominant
     # kernel on 1 batch in 4 (on the stream it runs on)
@@ -804,6 +806,9 @@ def main():
                               dir_share=directory_share(kb, ko, sample))
     table = roofline.kernel_table(kprof, shape, st_prof if args.profile_steps > 0 else None)
     roof = None
+    if dominant and args.roof_steps > 0 and dominant not in kprof_timed:
+        print(f"[rank {rank}] roofline pass timed no launch of {dominant!r} (timed: {sorted(kprof_timed)}, "
+              f"batches {st_roof.get('batches')})", file=sys.stderr)
     if dominant and dominant in kprof_timed:
         k = kprof_timed[dominant]
         ent = roofline.entry(dominant, k["ms"], k["launches"], shape, st_roof)
