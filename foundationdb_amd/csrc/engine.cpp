@@ -153,17 +153,27 @@ struct AddPool {
     const std::function<void(int)>* job = nullptr;
     bool stop = false;
 
+    // std::thread's constructor throws (std::system_error) at the process's thread limit: the
+    // workers already started are stopped and joined before the exception leaves, so the caller
+    // can fall back to the serial loop
     explicit AddPool(int workers) {
-        for (int i = 0; i < workers; i++) th.emplace_back([this] { worker(); });
+        try {
+            for (int i = 0; i < workers; i++) th.emplace_back([this] { worker(); });
+        } catch (...) {
+            shutdown();
+            throw;
+        }
     }
-    ~AddPool() {
+    ~AddPool() { shutdown(); }
+    void shutdown() {
         {
             std::lock_guard<std::mutex> lk(m);
             stop = true;
             gen.fetch_add(1);
         }
         cv.notify_all();
-        for (auto& t : th) t.join();
+        for (auto& t : th)
+            if (t.joinable()) t.join();
     }
     void run(uint32_t g, int nn, const std::function<void(int)>* fn) {
         uint64_t cur = ticket.load(std::memory_order_acquire);
@@ -1792,7 +1802,14 @@ static int add_packed_direct(fdbcs_batch* b, const fdbcs_packed_batch* pb) {
         ch[c] = Chunk{(int32_t)((int64_t)T * c / nchunk), (int32_t)((int64_t)T * (c + 1) / nchunk), 0, 0, 0, false};
     }
     const bool pooled = nchunk > 1 && cs->add_threads > 0;
-    if (pooled && !cs->add_pool) cs->add_pool = new (std::nothrow) AddPool(cs->add_threads);
+    if (pooled && !cs->add_pool) {
+        try {
+            cs->add_pool = new AddPool(cs->add_threads);
+        } catch (...) {  // no memory or no threads left: this call and later ones run serially
+            cs->add_pool = nullptr;
+            cs->add_threads = 0;
+        }
+    }
     // pass 1 (tickets [0, nchunk)): tail bytes of each chunk's admitted keys (key offsets only), so
     // the tails pack exactly in transaction order; pass 2 (tickets [nchunk, 2 nchunk)) waits for
     // every count (tickets go out in order, so every count is held by a running thread)

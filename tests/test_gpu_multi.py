@@ -42,10 +42,10 @@ def test_multi_rank_bench_parity(engine, world, workload, extra):
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == world and out["value"] > 0
-    # warmup 2 + profile 4 + timed 8 + sync 4 batches, every one combined and replayed on each rank
+    # warmup 2 + timed 8 + profile 4 + sync 4 batches, every one combined and replayed on each rank
     assert out["parity"]["batches_checked"] >= world * 18 and out["parity"]["mismatched_batches"] == 0
-    # the combine check covers the timed and later batches (timed 8 + sync 4)
-    assert out["combine_check"]["mismatched"] == 0 and out["combine_check"]["batches"] == 12
+    # the combine check covers the timed and later batches (timed 8 + profile 4 + sync 4)
+    assert out["combine_check"]["mismatched"] == 0 and out["combine_check"]["batches"] == 16
     # G resolvers on G cores: every rank's restatement timed at once, over the slowest one
     assert out["cpu_baseline"]["cores"] == world and out["cpu_baseline"]["value"] > 0
     assert out["distributed"]["world_size"] == world and out["distributed"]["backend"] == "gloo"
