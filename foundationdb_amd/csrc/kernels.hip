@@ -1591,12 +1591,6 @@ __device__ __forceinline__ uint32_t split_lcp(const SplitKey& a, const SplitKey&
     return c < b.len ? c : b.len;
 }
 
-// Slab slots every bucket wave loads before its count arrives (the rest after it).
-#ifndef FDBCS_SPEC_SLOTS
-#define FDBCS_SPEC_SLOTS 80
-#endif
-constexpr int kSpecSlots = FDBCS_SPEC_SLOTS;
-
 template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, SortOut o) {
     constexpr int kWaves = kBlock / 64;
@@ -1622,12 +1616,6 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
         own1 = a.cnt[(size_t)kCntStride * bk + 1];
     }
     if (a.exp & 8) own0 = bk < nb ? (64ull | 16ull << 32) : 0ull, own1 = bk < nb ? (16ull | 16ull << 32) : 0ull;
-    // the bucket's first 128 slab slots, before its count arrives (slots past the count hold stale
-    // items of earlier batches and are masked once it has): one round trip instead of two
-    SortItem sp[2];
-#pragma unroll
-    for (int s = 0; s < 2; s++)
-        if (bk < nb && s * 64 + lane < kSpecSlots) sp[s] = a.slab[(size_t)bk * kSlab + s * 64 + lane];
     // (the first kPreHeld chunks stay in registers across the sort, enough for nb <= 1536 buckets,
     // ~98k endpoints; larger batches load the rest after it)
     constexpr int kPreLoads = kSortMaxBuckets / kBlock, kPreHeld = 6;
@@ -1659,7 +1647,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_bucket(BatchDev b, SortArgs a, 
             const int k = s * 64 + lane;
             kh[s] = kl[s] = ka[s] = ~0ull;  // padding sorts after every endpoint
             if (s < S && k < n) {
-                const SortItem it = s < 2 && k < kSpecSlots ? sp[s] : a.slab[(size_t)bk * kSlab + k];
+                const SortItem it = a.slab[(size_t)bk * kSlab + k];
                 if (c == 0) {
                     kh[s] = it.hi;
                     kl[s] = it.lo;

@@ -9,7 +9,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     name=${v%%:*}; envs=${v#*:}
     (
       IFS=','; for e in $envs; do [ -n "$e" ] && export "$e"; done; unset IFS
-      timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 60 --no-cpu-baseline --breakdown-steps 0 --sync-steps 0 --resident-steps 0 --total-steps 0} \
+      timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 60 --no-cpu-baseline --breakdown-steps 0 --sync-steps 0 --h2d-steps 0 --total-steps 0} \
         > gpurun_out/ab/${name}_$r.json 2> gpurun_out/ab/${name}_$r.err
     ) || { echo "$name failed"; tail -5 gpurun_out/ab/${name}_$r.err; exit 1; }
     python3 -c "

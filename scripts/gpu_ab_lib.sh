@@ -22,7 +22,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       IFS=','; for x in $envs; do [ -n "$x" ] && export "$x"; done; unset IFS
       FDBCS_LIB=$PWD/$lib timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
         python3 bench.py --workload $W --steps ${STEPS:-40} --warmup 3 --no-cpu-baseline --breakdown-steps 0 \
-        --sync-steps 0 --total-steps 0 --resident-steps 0 ${BENCH_ARGS:-} > $d.json 2> $d.err
+        --sync-steps 0 --total-steps 0 --h2d-steps 0 ${BENCH_ARGS:-} > $d.json 2> $d.err
     ) || { echo "$label failed"; tail -5 $d.err; exit 1; }
     find $d -name "*kernel_trace.csv" -delete
   done
