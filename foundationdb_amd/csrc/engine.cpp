@@ -366,9 +366,9 @@ struct fdbcs_conflict_set {
     // Two submitting threads (the default since round 4: C2 +3-10 % over five same-box A/Bs, C3 and
     // C4 unchanged; FDBCS_SUBMIT_THREAD=0 keeps one).  A helper thread issues stage A of batch i
     // (and its base-tier check) while the calling thread issues stage B's X half of batch i-1,
-    // which waited (as in graph mode) for this call; the helper then issues that batch's Y half
-    // once X is out (helper_y): kernel launches on two streams from two threads take about half
-    // the wall time of one thread's (tools/threadbench.hip: 3.4 -> 1.85 us per launch).  The
+    // which waited for this call; the helper then issues that batch's Y half once X is out:
+    // kernel launches on two streams from two threads take about half the wall time of one
+    // thread's (tools/threadbench.hip: 3.4 -> 1.85 us per launch).  The
     // check of batch i waits (host side) until stage B of batch i-1 is issued, because it may wait
     // on that stage's compaction event; stage B of batch i waits for the helper to go idle.
     bool submit_thread = true;
@@ -386,16 +386,15 @@ struct fdbcs_conflict_set {
     std::mutex wmu;
     std::condition_variable wcv;
     std::atomic<int> wjob{0};           // 0 idle, 1 job queued or running, 2 exit
-    std::atomic<uint32_t> b_issued{0};  // stage-B lists issued (by the calling thread)
+    std::atomic<uint32_t> b_issued{0};  // stage-B lists issued (their Y halves: helper or flush)
     uint32_t b_recorded = 0;            // stage-B lists recorded
     std::atomic<int> werr{0};           // first HIP error of the helper
     LaunchList work_a, work_c;          // the helper's lists
     hipStream_t work_sa = nullptr;
     uint32_t work_need_b = 0;           // the check goes out once b_issued >= this
     // Stage B's Y half of the previous batch, issued by the helper once the calling thread has
-    // issued its X half (FDBCS_HELPER_Y=0: both halves from the calling thread).  The calling
-    // thread issues record + X, the helper stage A + Y + base check: their runtime calls split
-    // about evenly instead of ~2:1.
+    // issued its X half.  The calling thread issues record + X, the helper stage A + Y + base
+    // check: their runtime calls split about evenly instead of ~2:1.
     LaunchList work_y;
     hipStream_t work_ys = nullptr;
     uint32_t work_need_x = 0;            // Y goes out once x_issued >= this
@@ -2654,8 +2653,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         cs->work_sa = sa;
         cs->work_a_seq = b->seq;
         const bool prev = cs->pending_batch != nullptr;
-        const bool hy = prev;
-        if (hy) {  // the previous batch's Y to the helper, after the X this thread issues below
+        if (prev) {  // the previous batch's Y to the helper, after the X this thread issues below
             cs->work_y_seq = cs->pending_batch->seq;
             std::swap(cs->work_y, cs->pending_y);
             cs->work_ys = cs->pending_ys;
@@ -2671,13 +2669,8 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
             const uint32_t pseq = pb_->seq;
             hipError_t e = cs->pending_b.replay(s, x_skip(cs, pb_), &cs->stats.x_launches_skipped);
             if (cs->htrace) cs->htr[0].push_back({pseq, 'X', tx, mono_ns()});
-            cs->x_issued.fetch_add(1, std::memory_order_release);
-            hipError_t e2 = hipSuccess;
-            if (!hy) {
-                e2 = cs->pending_y.replay(cs->pending_ys);
-                cs->b_issued.fetch_add(1, std::memory_order_release);
-            }
-            if (e != hipSuccess || e2 != hipSuccess) return FDBCS_E_DEVICE;
+            cs->x_issued.fetch_add(1, std::memory_order_release);  // (the helper issues its Y)
+            if (e != hipSuccess) return FDBCS_E_DEVICE;
         }
         std::swap(cs->pending_b, lb);
         std::swap(cs->pending_y, ly);

@@ -4189,7 +4189,8 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
 }
 
 // Report side outputs (rconf, hist_conf, first_conf) into the batch's host-mapped result buffer:
-// a kernel rather than a DMA copy so it can be a node of the batch's graph.
+// a kernel rather than a DMA copy, in stream order on the batch's X stream without a copy-engine
+// hand-off.
 __global__ __launch_bounds__(kBlock) void k_copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
                                                        int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

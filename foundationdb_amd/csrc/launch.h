@@ -1,11 +1,11 @@
 // launch.h — kernel submission for the engine: launch now, or record into a LaunchList.
 //
 // A LaunchList is one pipeline stage of one batch as data: kernel launches (host stub, grid,
-// block, dynamic LDS, argument values) and event records / waits.  The engine either replays it
-// onto streams (direct mode) or feeds it, as per-batch parameters, to the nodes of a cached
-// hipGraph of the same shape: one hipGraphLaunch per batch instead of ~20 runtime calls
-// (tools/launchbench.hip: 15 launches ~45 us of host time, their graph 6 us, a node parameter
-// update 0.12 us).  Every kernel launch of the pipeline goes through fdb_launch.
+// block, dynamic LDS, argument values) and event records / waits.  The engine records a batch's
+// stages on the calling thread and replays them onto their streams from whichever thread submits
+// them (the calling thread or the helper), leaving out launches the host knows to be no-ops.
+// Every kernel launch of the pipeline goes through fdb_launch.  (Replaying the lists as hipGraphs
+// measured slower than direct launches and was removed: DESIGN.md §5.)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,8 +21,8 @@ namespace fdbcs {
 struct LaunchList {
     enum Kind : uint8_t {
         kKernel = 0,
-        kTimingRecord = 1,  // event record kept in graph mode (phase / roofline timing)
-        kSyncRecord = 2,    // cross-stream ordering, direct mode only (a graph is ordered already)
+        kTimingRecord = 1,  // event record for phase / roofline timing
+        kSyncRecord = 2,    // cross-stream ordering
         kSyncWait = 3,
     };
     struct Rec {
@@ -77,16 +77,6 @@ struct LaunchList {
     void finalize() {
         argp.resize(argoff.size());
         for (size_t i = 0; i < argoff.size(); i++) argp[i] = arena.data() + argoff[i];
-    }
-    // Shape of the list as a graph sees it: the kernels and timing events in order.
-    uint64_t signature() const {
-        uint64_t h = 1469598103934665603ull;
-        for (const Rec& r : recs) {
-            if (r.kind == kSyncRecord || r.kind == kSyncWait) continue;
-            const uint64_t x = r.kind == kKernel ? (uint64_t)(uintptr_t)r.func : 0x5bd1e995u;
-            h = (h ^ x) * 1099511628211ull;
-        }
-        return h;
     }
     // One record, now, on `s` (after finalize()).
     hipError_t issue(const Rec& r, hipStream_t s) {
