@@ -117,8 +117,7 @@ struct BatchSlot;
 constexpr int kWsTileSlot = 54, kWsArenaSlot = 55;
 // Batch workspaces in rotation: stage A can run up to two batches ahead of stage B, so each
 // workspace is reused every third batch.
-constexpr int kNumWork = 4;   // batch workspaces in rotation (a check reads the two before its own)
-constexpr int kNumDelta = 3;  // delta buffers: the one a check reads and the two merges after it write
+constexpr int kNumWork = 3;
 constexpr int kGcEveryCompactions = 4;  // removeBefore cadence of size-triggered compactions
 
 // FDBCS_HOST_TRACE=<path>: host-side spans of the pipeline (steady_clock ns, the clock rocprofv3
@@ -255,13 +254,10 @@ struct fdbcs_conflict_set {
     // the next batch's check is done with workspace k's segments: that batch's ev_res (the end of
     // its half X, recorded anyway, and not re-recorded before workspace k's next user records)
     hipEvent_t xfree_ev[kNumWork] = {};
-    // The next check reads the delta from before the last prev_n merges (0-2) plus those batches'
-    // union segments: prev_wps / prev_nows [0] = the last batch, [1] = the one before it.
-    int prev_n = 0;
-    int prev_max = 2;                   // FDBCS_PREV_DEPTH
-    int prev_wps[2] = {0, 0};
-    int64_t prev_nows[2] = {0, 0};
-    int y_wps[3] = {-1, -1, -1};        // workspaces of the last three batches submitted (their Y events)
+    bool prev_segs = false;             // the last batch's segments are not merged when the next check runs
+    int prev_wp = 0;
+    int64_t prev_now = 0;
+    int last_wp = -1, prev2_wp = -1;    // workspaces of the last two batches submitted (their Y events)
     bool xfree_rec[kNumWork] = {};      // xfree_ev[k] set since workspace k's last use
     // The batches behind ws ev_b[k] (workspace k's last user) and xfree_ev[k] (the batch whose check
     // reads workspace k's segments), or null once destroyed: while a batch lives its completion
@@ -287,8 +283,8 @@ struct fdbcs_conflict_set {
     DBuf hkey[2], hlt[2], hver[2];
     DBuf lvl[kMaxLevels];  // lvl[0]: sampled key index (the level-0 versions are hver[cur])
     DBuf dir;              // radix directory over the base tier's level-0 samples (k_directory)
-    DBuf edir[kNumDelta];  // each delta buffer's directory (epoch-tagged entries, filled by k_epilogue)
-    uint32_t ddir_epoch[kNumDelta] = {};  // epoch of each delta buffer's directory (0: none)
+    DBuf edir[2];          // each delta buffer's directory (epoch-tagged entries, filled by k_epilogue)
+    uint32_t ddir_epoch[2] = {0, 0};  // epoch of each delta buffer's directory (0: none)
     uint32_t ddir_counter = 0;  // last epoch handed out
     int cur = 0;
     int64_t hist_cap = 0;  // elements per buffer set
@@ -296,8 +292,8 @@ struct fdbcs_conflict_set {
     int64_t lvl3_n = 0;
     int64_t lvl2_n = 0;
     // delta tier: the same layout, small
-    DBuf dkey[kNumDelta], dlt[kNumDelta], dver[kNumDelta];
-    DBuf dlvl[kNumDelta][kMaxLevels];  // per delta buffer: checks read one while epilogues build the others
+    DBuf dkey[2], dlt[2], dver[2];
+    DBuf dlvl[2][kMaxLevels];  // per delta buffer: the next batch's check reads one while the epilogue builds the other
     int dcur = 0;
     int64_t delta_cap = 0;
     int64_t nd_ub = 0;
@@ -540,7 +536,7 @@ int sync_all(fdbcs_conflict_set* cs) {
     HIPOK(hipStreamSynchronize(cs->astream));
     HIPOK(hipStreamSynchronize(cs->stream));
     HIPOK(hipStreamSynchronize(cs->ystream));
-    cs->prev_n = 0;  // everything submitted is merged: the next check reads the current delta
+    cs->prev_segs = false;  // everything submitted is merged: the next check reads the current delta
     return FDBCS_OK;
 }
 
@@ -666,7 +662,7 @@ int ensure_workspace(fdbcs_conflict_set* cs, int64_t T, int64_t R, int64_t W) {
     }
     }
     cs->edge_cap = edge_cap;
-    cs->prev_n = 0;  // the last batches' segments were in the old arrays (and are merged: synced)
+    cs->prev_segs = false;  // the last batch's segments were in the old arrays (and are merged: synced)
     cs->ws_T = T;
     cs->ws_R = R;
     cs->ws_W = W;
@@ -862,10 +858,10 @@ int alloc_levels(DBuf* lv, int64_t cap, int64_t* top_n, int64_t* l2_n) {
     return FDBCS_OK;
 }
 
-// Grow `sets` buffer sets to `cap` elements, keeping the live `n` of set `live`.
-int grow_sets(fdbcs_conflict_set* cs, DBuf* key, DBuf* lt, DBuf* ver, int sets, int live, int64_t n, int64_t cap) {
+// Grow one ping-pong buffer set pair to `cap` elements, keeping the live `n` of set `live`.
+int grow_sets(fdbcs_conflict_set* cs, DBuf* key, DBuf* lt, DBuf* ver, int live, int64_t n, int64_t cap) {
     int rc;
-    for (int k = 0; k < sets; k++) {
+    for (int k = 0; k < 2; k++) {
         DBuf nk, nl, nv;
         if ((rc = nk.ensure(16 * cap)) || (rc = nl.ensure(8 * cap)) || (rc = nv.ensure(8 * cap))) return rc;
         if (k == live && n) {
@@ -891,7 +887,7 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
     if (rc) return rc;
     int64_t cap = std::max<int64_t>(need, cs->delta_cap);
     cap = std::max<int64_t>(cap + cap / 2, 1 << 14);
-    if ((rc = grow_sets(cs, cs->dkey, cs->dlt, cs->dver, kNumDelta, cs->dcur, cs->nd_ub, cap))) return rc;
+    if ((rc = grow_sets(cs, cs->dkey, cs->dlt, cs->dver, cs->dcur, cs->nd_ub, cap))) return rc;
     for (int k = 0; k < 5; k++) {
         cs->cws[k].release();
         if ((rc = cs->cws[k].ensure(8 * (cap + 2)))) return rc;
@@ -903,11 +899,11 @@ int ensure_delta(fdbcs_conflict_set* cs, int64_t need) {
         for (int k = 0; k < 5; k++) *c64[k] = (int64_t*)cs->cws[k].p;
         w.c_exact = (uint8_t*)cs->cws[5].p;
     }
-    for (int k = 0; k < kNumDelta; k++)
+    for (int k = 0; k < 2; k++)
         if ((rc = alloc_levels(cs->dlvl[k], cap, &cs->dlvl3_n, &cs->dlvl2_n))) return rc;
     cs->delta_cap = cap;
-    for (auto& e : cs->ddir_epoch) e = 0;  // the current delta's levels are rebuilt, its directory not
-    cs->prev_n = 0;                        // (sync_sizes drained every stream)
+    cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;  // the current delta's levels are rebuilt, its directory not
+    cs->prev_segs = false;                      // (sync_sizes drained every stream)
     launch_rangemax(cs->stream, dlevels_of(cs, cs->dcur), (Scalars*)cs->scal.p, &((Scalars*)cs->scal.p)->ndb[cs->dcur],
                     cs->dlvl3_n, cs->dlvl2_n, std::max<int64_t>(cs->nd_ub, 1));
     HIPOK(take_launch_error());
@@ -924,7 +920,7 @@ int ensure_history(fdbcs_conflict_set* cs, int64_t need, int64_t tail_need) {
     if (need > cs->hist_cap) {
         int64_t cap = std::max<int64_t>(need, cs->hist_cap);
         cap = std::max<int64_t>(cap + cap / 4, 1 << 16);
-        if ((rc = grow_sets(cs, cs->hkey, cs->hlt, cs->hver, 2, cs->cur, cs->n_ub, cap))) return rc;
+        if ((rc = grow_sets(cs, cs->hkey, cs->hlt, cs->hver, cs->cur, cs->n_ub, cap))) return rc;
         if ((rc = alloc_levels(cs->lvl, cap, &cs->lvl3_n, &cs->lvl2_n))) return rc;
         if (cs->directory && (rc = cs->dir.ensure(4 * (size_t)kDirAlloc))) return rc;
         cs->hist_cap = cap;
@@ -1275,7 +1271,6 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     if (const char* v = getenv("FDBCS_SERIAL")) cs->serial = v[0] == '1';
     if (const char* v = getenv("FDBCS_RESOLVE_PREPASS")) cs->no_prepass = v[0] == '0';
     if (const char* v = getenv("FDBCS_SUBMIT_THREAD")) cs->submit_thread = v[0] != '0';
-    if (const char* v = getenv("FDBCS_PREV_DEPTH")) cs->prev_max = std::max(0, std::min(2, atoi(v)));
     if (const char* v = getenv("FDBCS_ADD_THREADS")) cs->add_threads = std::max(0, std::min(64, atoi(v)));
     if (const char* v = getenv("FDBCS_SKIP_EDGES")) cs->skip_edges = v[0] != '0';
     if (const char* v = getenv("FDBCS_WAIT_QUERY_MS")) cs->wait_query_ms = std::max(0, atoi(v));
@@ -1312,7 +1307,7 @@ int fdbcs_new_conflict_set(int device, fdbcs_conflict_set** out) {
     int rc = cs->scal.ensure(sizeof(Scalars));
     if (!rc) rc = cs->quant.ensure(2 * sizeof(SplitKey) * kQuant);
     if (!rc) rc = (hipMemsetAsync(cs->scal.p, 0, sizeof(Scalars), cs->stream) == hipSuccess) ? 0 : FDBCS_E_DEVICE;
-    for (int k = 0; k < kNumDelta && !rc && cs->directory; k++) {  // zeroed: epoch 0 entries are never trusted
+    for (int k = 0; k < 2 && !rc && cs->directory; k++) {  // zeroed: epoch 0 entries are never trusted
         rc = cs->edir[k].ensure(8 * (size_t)kDirAlloc);
         if (!rc && hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream) != hipSuccess)
             rc = FDBCS_E_DEVICE;
@@ -1367,8 +1362,6 @@ void fdbcs_destroy_conflict_set(fdbcs_conflict_set* cs) {
         cs->hkey[k].release();
         cs->hlt[k].release();
         cs->hver[k].release();
-    }
-    for (int k = 0; k < kNumDelta; k++) {
         cs->dkey[k].release();
         cs->dlt[k].release();
         cs->dver[k].release();
@@ -1420,9 +1413,9 @@ int fdbcs_clear_conflict_set(fdbcs_conflict_set* cs, int64_t version) {
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = version;
     cs->max_written = version;
-    for (auto& e : cs->ddir_epoch) e = 0;
+    cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;
     if (int rc = set_dir_map(cs, nullptr, 0)) return rc;
-    cs->prev_n = 0;
+    cs->prev_segs = false;
     cs->n_ub = 0;
     cs->nd_ub = 0;
     cs->tail_ub = 0;
@@ -1533,8 +1526,8 @@ int fdbcs_load_history(fdbcs_conflict_set* cs, int64_t n, const uint8_t* key_byt
     HIPOK(hipStreamSynchronize(cs->stream));
     cs->header_version = header_version;
     cs->max_written = maxv;
-    for (auto& e : cs->ddir_epoch) e = 0;  // no delta directory entry of the old slot mapping is trusted
-    cs->prev_n = 0;
+    cs->ddir_epoch[0] = cs->ddir_epoch[1] = 0;  // no delta directory entry of the old slot mapping is trusted
+    cs->prev_segs = false;
     cs->n_ub = n;
     cs->nd_ub = 0;
     cs->tail_ub = (int64_t)tail.size();
@@ -2332,7 +2325,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // the delta directory's 32-bit epoch tag is about to wrap: clear every entry (once per 2^32
         // batches) so that no entry left by an old fill can carry the reused epoch value
         if ((rc = sync_all(cs))) return rc;
-        for (int k = 0; k < kNumDelta; k++) HIPOK(hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream));
+        for (int k = 0; k < 2; k++) HIPOK(hipMemsetAsync(cs->edir[k].p, 0, 8 * (size_t)kDirAlloc, cs->stream));
         HIPOK(hipStreamSynchronize(cs->stream));
         cs->ddir_counter = 0;
     }
@@ -2458,27 +2451,21 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     Scalars* sc = (Scalars*)cs->scal.p;
     const int bsrc = cs->cur, dsrc = cs->dcur;
     // Stage B in two halves (fdbcs_conflict_set::ystream): X = check, resolution, D.Combine on
-    // `stream`; Y = merge, compaction / GC, epilogue on `ystream`.  Unless one of them compacted,
-    // this batch's check reads the delta from before the last np batches' merges (np = prev_n <= 2:
-    // buffer (dsrc - np) mod 3, complete once the batch before them finished Y) plus those batches'
-    // union segments at their `now` (PrevSegs): the same history, so the check waits for neither
-    // merge, and one X -> Y round trip of the batch-order chain covers np + 1 batches.
+    // `stream`; Y = merge, compaction / GC, epilogue on `ystream`.  Unless the previous batch
+    // compacted, this batch's check reads the delta before the previous batch's merge (buffer
+    // dsrc ^ 1, complete once the batch before it finished Y) plus the previous batch's union
+    // segments at its `now` (PrevSegs): the same history, so the check need not wait for that merge.
     const bool pipe = !(timing == 2 || cs->serial);
     hipStream_t ys = pipe ? cs->ystream : s;
-    const int np = pipe ? std::min(cs->prev_n, cs->prev_max) : 0;
-    const bool use_prev = np > 0;
-    const int dchk = (dsrc + kNumDelta - np) % kNumDelta;
+    const bool use_prev = pipe && cs->prev_segs;
+    const int dchk = use_prev ? dsrc ^ 1 : dsrc;
     const Tier base{hist_of(cs, bsrc), levels_of(cs, bsrc), &sc->n, cs->header_version};
     const Tier delta{delta_of(cs, dsrc), dlevels_of(cs, dsrc), &sc->ndb[dsrc], kHole};
     const Tier cdelta{delta_of(cs, dchk), dlevels_of(cs, dchk), &sc->ndb[dchk], kHole};  // what the check reads
-    PrevSegs ps{}, ps2{};
-    if (np >= 1) {
-        const Work& pw = cs->work[cs->prev_wps[0]];
-        ps = PrevSegs{pw.segk, pw.btail, &pw.bsc->n_segments, cs->prev_nows[0]};
-    }
-    if (np >= 2) {
-        const Work& pw = cs->work[cs->prev_wps[1]];
-        ps2 = PrevSegs{pw.segk, pw.btail, &pw.bsc->n_segments, cs->prev_nows[1]};
+    PrevSegs ps{};
+    if (use_prev) {
+        const Work& pw = cs->work[cs->prev_wp];
+        ps = PrevSegs{pw.segk, pw.btail, &pw.bsc->n_segments, cs->prev_now};
     }
     uint8_t* htail = (uint8_t*)cs->htail[cs->tcur].p;
 
@@ -2548,26 +2535,23 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
         // the delta the check reads is complete: Y of the batch before the previous one (with the
         // previous batch's segments), or of the previous batch (it compacted, or nothing pending).
         // Only a Y on ystream needs the event (a timing-level change may switch layouts mid-flight).
-        const int wy = cs->y_wps[np];
+        const int wy = use_prev ? cs->prev2_wp : cs->last_wp;
         if (wy >= 0 && cs->y_async[wy] && (threaded || !stage_b_done(cs, wy)))
             fdb_event(LaunchList::kSyncWait, cs->ev_b[wy], s);
     }
     if (split) {
         b->check_hist = cs->n_ub;  // the timed (base-tier) check
-        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, ps, ps2);
+        launch_check_tier(s, bd, w, cdelta, false, htail, long_keys, ps);
     } else {
         b->check_hist = cs->n_ub + cs->nd_ub;
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckBegin, 1), s);
-        launch_check(s, bd, w, base, cdelta, htail, long_keys, ps, ps2);
+        launch_check(s, bd, w, base, cdelta, htail, long_keys, ps);
         fdb_event(LaunchList::kTimingRecord, rec(kPhCheckEnd, 1), s);
     }
     if (use_prev) {  // the previous batch's workspace may be reused once this check is done with it
-        for (int q = 0; q < np; q++) {
-            const int pwp = cs->prev_wps[q];
-            cs->xfree_ev[pwp] = cs->ev_res[wp];  // recorded at the end of this half X
-            cs->xfree_user[pwp] = b;
-            cs->xfree_rec[pwp] = true;
-        }
+        cs->xfree_ev[cs->prev_wp] = cs->ev_res[wp];  // recorded at the end of this half X
+        cs->xfree_user[cs->prev_wp] = b;
+        cs->xfree_rec[cs->prev_wp] = true;
     }
     mark(kPhCheck);
     if (sa != s) fdb_event(LaunchList::kSyncWait, cs->ev_a[wp], s);
@@ -2590,7 +2574,7 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     fdb_event(LaunchList::kSyncRecord, cs->ev_res[wp], s);
     t_record = &ly;
     if (ys != s) fdb_event(LaunchList::kSyncWait, cs->ev_res[wp], ys);
-    const int dnew = (dsrc + 1) % kNumDelta;
+    const int dnew = dsrc ^ 1;
     const int64_t nd_after = cs->nd_ub + 2 * W;
     const int64_t new_oldest = std::max(cs->oldest, new_oldest_version);
     // Compaction when the delta may outgrow its bound (or on the forced cadence); removeBefore
@@ -2706,15 +2690,12 @@ int fdbcs_batch_detect_async(fdbcs_batch* b, int64_t now, int64_t new_oldest_ver
     cs->cur = final_base;
     cs->dcur = dnew;
     // the next batch's check: this batch's segments stand in for its merge unless it compacted
-    cs->prev_n = pipe && !compact ? std::min(cs->prev_n + 1, 2) : 0;
-    cs->y_wps[2] = cs->y_wps[1];
-    cs->y_wps[1] = cs->y_wps[0];
-    cs->y_wps[0] = wp;
+    cs->prev_segs = pipe && !compact;
+    cs->prev2_wp = cs->last_wp;
+    cs->last_wp = wp;
     cs->y_async[wp] = ys != s;
-    cs->prev_wps[1] = cs->prev_wps[0];
-    cs->prev_nows[1] = cs->prev_nows[0];
-    cs->prev_wps[0] = wp;
-    cs->prev_nows[0] = now;
+    cs->prev_wp = wp;
+    cs->prev_now = now;
     cs->oldest = new_oldest;  // SkipList.cpp:880-882
     if (W) cs->max_written = std::max(cs->max_written, now);
     if (compact) {

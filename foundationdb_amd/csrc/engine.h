@@ -105,9 +105,13 @@ struct Scalars {
     int64_t intra_edges;   // copied from BatchScalars::n_edges (host view only; overflow -> -1)
     int32_t sort_big;      // copied from BatchScalars::sort_big (host view only)
     int32_t sort_pad;
-    int64_t ndb[3];        // delta boundaries held by delta buffer k (read checks and merges address
-                           // the buffer they use: a check reads the buffer from before the last one
-                           // or two merges while those merges write the others)
+    int64_t ndb[2];        // delta boundaries held by delta buffer k (read checks and merges address
+                           // the buffer they use: the next batch's check reads the buffer before
+                           // this batch's merge while the merge writes the other one)
+    int64_t nm;            // mid-tier boundaries
+    int64_t nm_next;       // mid tier after this batch's fold of the delta into it
+    int64_t m_before;      // mid size at the start of a fold
+    int64_t m_rem;         // mid boundaries removed (overwritten) by the fold
 };
 
 // Device scalars of one batch workspace (two workspaces alternate, so batch i+1's history-
@@ -387,7 +391,7 @@ struct PrevSegs {
     const DKey* segk;     // begin / end keys of segment j at 2j / 2j + 1
     const uint8_t* tail;  // their tails (the previous batch's workspace copy)
     const int64_t* n;     // segments
-    int64_t version;      // that batch's `now`
+    int64_t version;      // the previous batch's `now`
 };
 // Per batch, two stages on two streams:
 //   A (history-independent): launch_sort (D.Sort + positions), launch_edges;
@@ -406,13 +410,11 @@ int sort_bucket_count(int64_t E, int target, int slab_buckets);
 // read (begin and end in both tiers).  long_keys: the batch has keys over 24 bytes (the long-key
 // lookup, lane_lower_bound_long).
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, bool long_keys = false, const PrevSegs& ps = PrevSegs{},
-                  const PrevSegs& ps2 = PrevSegs{});
+                  const uint8_t* htail, bool long_keys = false, const PrevSegs& ps = PrevSegs{});
 // D.CheckRead over one tier (the split check: base tier in stage A when no compaction is pending,
 // delta tier in stage B), two lanes per read; both OR into the workspace's pre-zeroed conflict flags.
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys = false, const PrevSegs& ps = PrevSegs{},
-                       const PrevSegs& ps2 = PrevSegs{});
+                       const uint8_t* htail, bool long_keys = false, const PrevSegs& ps = PrevSegs{});
 // Diagnostics (fdbcs_debug_kernel_time): isolated device time of the sort's launches (which 1 =
 // k_sort_partition, 2 = k_sort_bucket) over `reps` runs on an idle stream.
 hipError_t debug_time_sort(hipStream_t s, const BatchDev& b, const Work& w, SplitKey* quant, int bucket_target,

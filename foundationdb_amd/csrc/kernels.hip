@@ -975,7 +975,7 @@ __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U,
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& base, const Tier& delta,
                                                  const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
-                                                 const PrevSegs& ps, const PrevSegs& ps2) {
+                                                 const PrevSegs& ps) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r = t >> 2;
     const int k = (int)(t & 3);
@@ -1009,11 +1009,6 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
         const bool hit = prev_seg_hit_quad(ps, U, kb, ke, degenerate, b.tail, live && U > 0 && ps.version > snap);
         conf = conf || hit;
     }
-    if (ps2.n) {  // and the batch before it, when neither merge has reached the delta the check reads
-        const int64_t U = *ps2.n;
-        const bool hit = prev_seg_hit_quad(ps2, U, kb, ke, degenerate, b.tail, live && U > 0 && ps2.version > snap);
-        conf = conf || hit;
-    }
     int c = conf ? 1 : 0;
     c |= __shfl_xor(c, 1, 64);
     c |= __shfl_xor(c, 2, 64);
@@ -1031,7 +1026,7 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const Tier& tier, bool is_base,
                                                       const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
-                                                      const PrevSegs& ps0, const PrevSegs& ps1) {
+                                                      const PrevSegs& ps) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t r = t >> 1;
     const int k = (int)(t & 1);
@@ -1057,9 +1052,7 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
     const int64_t j = __shfl_xor(lb, 1, 64);
     bool conf = false;
     if (active && !k) conf = tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
-    for (int q = 0; q < 2; q++) {
-        const PrevSegs& ps = q ? ps1 : ps0;
-        if (is_base || !ps.n) continue;
+    if (!is_base && ps.n) {
         // the pair of lanes runs the quad search with its neighbour pair (the same code path for
         // every lane; each pair's read is its own, the quad shares no state but the shuffles)
         const int64_t U = *ps.n;
@@ -1239,7 +1232,7 @@ struct CheckReads {
     const uint8_t* htail;
     uint8_t *hist_conf, *rconf;
     unsigned long long* trace;
-    PrevSegs ps, ps2;  // the previous batch's union segments, and the batch's before it, not merged yet
+    PrevSegs ps;  // the previous batch's union segments, not merged yet
 };
 
 // Per-lane checks: both tiers, four lanes per read; one tier (the split check), two lanes per read;
@@ -1247,29 +1240,27 @@ struct CheckReads {
 // LONG: the batch has keys over 24 bytes (lane_lower_bound_long).
 template <bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes(BatchDev b, CheckReads c) {
-    check_read_lanes<LONG>(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps, c.ps2);
+    check_read_lanes<LONG>(b, c.base, c.delta, c.htail, c.hist_conf, c.rconf, c.ps);
 }
 template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t, const uint8_t* htail,
-                                                             uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps,
-                                                             PrevSegs ps2) {
-    check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, ps, ps2);
+                                                             uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps) {
+    check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, ps);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
-                       const uint8_t* htail, bool long_keys, const PrevSegs& ps, const PrevSegs& ps2) {
+                       const uint8_t* htail, bool long_keys, const PrevSegs& ps) {
     if (b.R == 0) return;
     const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
     auto k = is_base ? (long_keys ? k_check_lanes_tier<true, true> : k_check_lanes_tier<true, false>)
                      : (long_keys ? k_check_lanes_tier<false, true> : k_check_lanes_tier<false, false>);
-    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps,
-               is_base ? PrevSegs{} : ps2);
+    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
-                  const uint8_t* htail, bool long_keys, const PrevSegs& ps, const PrevSegs& ps2) {
+                  const uint8_t* htail, bool long_keys, const PrevSegs& ps) {
     if (b.R == 0) return;
-    const CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps, ps2};
+    const CheckReads c{base, delta, htail, w.hist_conf, w.rconf, w.trace, ps};
     const int grid = (int)(((int64_t)b.R * 4 + kBlock - 1) / kBlock);
     fdb_launch(long_keys ? k_check_lanes<true> : k_check_lanes<false>, dim3(grid), dim3(kBlock), 0, s, b, c);
 }
@@ -4169,7 +4160,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue(MaxLevels m, Scalars* 
             if (lane == sc_word(offsetof(Scalars, n))) x = (uint64_t)n_new;
             if (lane == sc_word(offsetof(Scalars, nd))) x = (uint64_t)nd_new;
             if (lane == sc_word(offsetof(Scalars, tail_used))) x = (uint64_t)tail_new;
-            if (nd_slot >= 0 && nd_slot < 3 && lane == sc_word(offsetof(Scalars, ndb)) + nd_slot) x = (uint64_t)nd_new;
+            if (nd_slot >= 0 && nd_slot < 2 && lane == sc_word(offsetof(Scalars, ndb)) + nd_slot) x = (uint64_t)nd_new;
             if (lane == sc_word(offsetof(Scalars, debug_error))) x = (uint64_t)dbg | (uint64_t)rounds << 32;
             if (lane == sc_word(offsetof(Scalars, intra_edges))) x = (uint64_t)edges;
             if (lane == sc_word(offsetof(Scalars, sort_big))) x = (x & ~0xffffffffull) | big;

@@ -29,7 +29,6 @@ KNOBS = {
     "FDBCS_SERIAL": ["0", "0", "0", "1"],
     "FDBCS_SKIP_EDGES": ["1", "0"],
     "FDBCS_SUBMIT_THREAD": ["1", "1", "0"],
-    "FDBCS_PREV_DEPTH": ["2", "2", "1"],
 }
 
 
