@@ -108,10 +108,6 @@ struct Scalars {
     int64_t ndb[2];        // delta boundaries held by delta buffer k (read checks and merges address
                            // the buffer they use: the next batch's check reads the buffer before
                            // this batch's merge while the merge writes the other one)
-    int64_t nm;            // mid-tier boundaries
-    int64_t nm_next;       // mid tier after this batch's fold of the delta into it
-    int64_t m_before;      // mid size at the start of a fold
-    int64_t m_rem;         // mid boundaries removed (overwritten) by the fold
 };
 
 // Device scalars of one batch workspace (two workspaces alternate, so batch i+1's history-
