@@ -8,8 +8,9 @@
 //
 //   stage A   D.Sort             k_sort_partition, k_sort_bucket (cold start: k_sample, k_quant_cold)
 //             D.CheckIntraBatch  k_scan<EdgePairScan>, k_edge_fill: candidate edges (one per write group)
-//   stage B X D.CheckRead        k_check_reads<tier waves> (both tiers, plus the previous batch's union
-//                                segments: prev_seg_hit) or k_check_tier<base / delta> (split check)
+//   stage B X D.CheckRead        k_check_lanes (both tiers and the previous batch's union segments)
+//                                or k_check_lanes_tier<base / delta> (split check; other workgroups
+//                                of the delta-tier launch search the segments)
 //             D.CheckIntraBatch  k_resolve_pre (statuses, or the pre-pass), k_resolve (batch-order rounds)
 //             D.Combine          in k_resolve_pre without candidate edges, else k_combine
 //   stage B Y D.MergeWrite       k_seg_prep, k_merge_copy<BatchIns>; compaction: k_compact_search,
@@ -971,7 +972,9 @@ __device__ __forceinline__ bool prev_seg_hit_quad(const PrevSegs& ps, int64_t U,
 // D.CheckRead of one read by four lanes (both tiers): lane 4i + 0 / 1 locates its begin / end key
 // in the base tier, 4i + 2 / 3 in the delta tier; the begin lanes take the end's position by a
 // shuffle and decide their tier (tier_conflict); the previous batch's segments by the quad; the
-// quad's verdict goes to the read's flags from lane 4i.
+// quad's verdict goes to the read's flags from lane 4i.  (Searching the segments in workgroups of
+// their own, as the delta-tier launch does, made this launch 31-34 -> 28-30 us in the C2 pipeline
+// but the line 1-2 % slower over three same-box A/Bs: the doubled grid crowds the kernels beside it.)
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& base, const Tier& delta,
                                                  const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
@@ -1018,6 +1021,31 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
     }
 }
 
+// The previous batch's union segments (not merged into the delta the check reads) against read r
+// by the four lanes of a quad, in workgroups of their own beside the delta-tier lookups'
+// (k_check_lanes_tier): the two dependent chains run side by side instead of one after the other
+// in the same lanes (C4: the delta-tier launch 72-78 -> 58-63 us in the pipeline, the line
+// +2-6 %).  ORs into the same pre-zeroed flags.
+__device__ __forceinline__ void check_read_segs(const BatchDev& b, const PrevSegs& ps, uint8_t* hist_conf,
+                                                uint8_t* rconf, int64_t blk) {
+    const int64_t t = blk * blockDim.x + threadIdx.x;
+    const int64_t r = t >> 2;
+    const bool live = r < b.R;
+    const int64_t rr = live ? r : 0;
+    const DKey kb = b.keys[2 * rr], ke = b.keys[2 * rr + 1];
+    const int64_t snap = b.snap[b.rowner[rr]];
+    const bool degenerate = dkey_cmp(kb, b.tail, ke, b.tail) == 0;
+    const int64_t U = *ps.n;
+    const bool hit = prev_seg_hit_quad(ps, U, kb, ke, degenerate, b.tail, live && U > 0 && ps.version > snap);
+    int c = hit ? 1 : 0;
+    c |= __shfl_xor(c, 1, 64);
+    c |= __shfl_xor(c, 2, 64);
+    if (live && (t & 3) == 0 && c) {
+        rconf[r] = 1;
+        hist_conf[b.rowner[r]] = 1;
+    }
+}
+
 // One tier only (the split check) by two lanes per read: begin / end; a conflict sets the read's and
 // its transaction's flags (zeroed beforehand by the epilogue that last used the workspace), so the
 // base-tier launch (stage A, on its own stream) and the delta-tier launch (stage B) OR into the
@@ -1026,8 +1054,8 @@ __device__ __forceinline__ void check_read_lanes(const BatchDev& b, const Tier& 
 template <bool LONG>
 __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const Tier& tier, bool is_base,
                                                       const uint8_t* htail, uint8_t* hist_conf, uint8_t* rconf,
-                                                      const PrevSegs& ps) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                      int64_t blk) {
+    const int64_t t = blk * blockDim.x + threadIdx.x;
     const int64_t r = t >> 1;
     const int k = (int)(t & 1);
     const bool live = r < b.R;
@@ -1052,25 +1080,6 @@ __device__ __forceinline__ void check_read_lanes_tier(const BatchDev& b, const T
     const int64_t j = __shfl_xor(lb, 1, 64);
     bool conf = false;
     if (active && !k) conf = tier_conflict(tier.h, tier.m, is_base ? tier.hdr : kHole, lb, eq, j, degenerate, snap);
-    if (!is_base && ps.n) {
-        // the pair of lanes runs the quad search with its neighbour pair (the same code path for
-        // every lane; each pair's read is its own, the quad shares no state but the shuffles)
-        const int64_t U = *ps.n;
-        const bool act = live && U > 0 && ps.version > snap;
-        // two reads per quad: search them one after the other so the quad's lanes agree on lo / hi
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const int src = (int)(threadIdx.x & ~3) + 2 * s;  // the first lane of read s of the quad
-            const DKey sb = {(uint64_t)__shfl((long long)kb.hi, src, 64), (uint64_t)__shfl((long long)kb.lo, src, 64),
-                             (uint32_t)__shfl((int)kb.len, src, 64), (uint32_t)__shfl((int)kb.tail, src, 64)};
-            const DKey se = {(uint64_t)__shfl((long long)ke.hi, src, 64), (uint64_t)__shfl((long long)ke.lo, src, 64),
-                             (uint32_t)__shfl((int)ke.len, src, 64), (uint32_t)__shfl((int)ke.tail, src, 64)};
-            const int sdeg = __shfl((int)degenerate, src, 64);
-            const int sact = __shfl((int)act, src, 64);
-            const bool hit = prev_seg_hit_quad(ps, U, sb, se, sdeg != 0, b.tail, sact != 0);
-            if (((threadIdx.x >> 1) & 1) == s) conf = conf || hit;
-        }
-    }
     int c = conf ? 1 : 0;
     c |= __shfl_xor(c, 1, 64);
     if (live && !k && c) {
@@ -1244,17 +1253,23 @@ __global__ __launch_bounds__(kBlock) void k_check_lanes(BatchDev b, CheckReads c
 }
 template <bool BASE, bool LONG>
 __global__ __launch_bounds__(kBlock) void k_check_lanes_tier(BatchDev b, Tier t, const uint8_t* htail,
-                                                             uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps) {
-    check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, ps);
+                                                             uint8_t* hist_conf, uint8_t* rconf, PrevSegs ps,
+                                                             int look_blocks) {
+    // workgroups past look_blocks search the previous batch's segments (check_read_segs)
+    if ((int)blockIdx.x < look_blocks)
+        check_read_lanes_tier<LONG>(b, t, BASE, htail, hist_conf, rconf, blockIdx.x);
+    else
+        check_read_segs(b, ps, hist_conf, rconf, blockIdx.x - look_blocks);
 }
 
 void launch_check_tier(hipStream_t s, const BatchDev& b, const Work& w, const Tier& t, bool is_base,
                        const uint8_t* htail, bool long_keys, const PrevSegs& ps) {
     if (b.R == 0) return;
     const int grid = (int)(((int64_t)b.R * 2 + kBlock - 1) / kBlock);
+    const int seg = !is_base && ps.n ? (int)(((int64_t)b.R * 4 + kBlock - 1) / kBlock) : 0;
     auto k = is_base ? (long_keys ? k_check_lanes_tier<true, true> : k_check_lanes_tier<true, false>)
                      : (long_keys ? k_check_lanes_tier<false, true> : k_check_lanes_tier<false, false>);
-    fdb_launch(k, dim3(grid), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, is_base ? PrevSegs{} : ps);
+    fdb_launch(k, dim3(grid + seg), dim3(kBlock), 0, s, b, t, htail, w.hist_conf, w.rconf, seg ? ps : PrevSegs{}, grid);
 }
 
 void launch_check(hipStream_t s, const BatchDev& b, const Work& w, const Tier& base, const Tier& delta,
